@@ -1,0 +1,97 @@
+"""ctypes binding of libclimsr_hip.so (the C ABI declared in include/climsr_hip.h).
+
+The product path has no CPU fallback: if the library is missing or a call fails, this module
+raises.  torch is imported first so the process has exactly one HIP runtime (torch's bundled
+libamdhip64 has the same SONAME, libamdhip64.so.7, that the library links against).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch  # noqa: F401  (must be loaded before the HIP library, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("CLIMSR_HIP_LIB", os.path.join(_HERE, "csrc", "libclimsr_hip.so"))
+
+c_int, c_float, c_double, c_void_p, c_int64, c_size_t = (ctypes.c_int, ctypes.c_float, ctypes.c_double, ctypes.c_void_p,
+                                                         ctypes.c_int64, ctypes.c_size_t)
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "n", "in_h", "in_w", "in_c", "in_cstride", "in_coff", "up", "ks", "stride", "pad", "out_h", "out_w", "out_c",
+        "out_cstride", "out_coff", "cc")]
+
+
+class Epilogue(ctypes.Structure):
+    _fields_ = [("act", ctypes.c_int32), ("slope", c_float), ("alpha1", c_float), ("res1", c_void_p),
+                ("res1_cstride", ctypes.c_int32), ("res1_coff", ctypes.c_int32), ("alpha2", c_float), ("res2", c_void_p),
+                ("res2_cstride", ctypes.c_int32), ("res2_coff", ctypes.c_int32), ("out_mode", ctypes.c_int32),
+                ("down2", ctypes.c_int32)]
+
+
+P = ctypes.POINTER
+# name -> (restype, argtypes); must match include/climsr_hip.h exactly (tests/test_abi.py checks the symbols)
+SIGNATURES = {
+    "climsr_last_error": (ctypes.c_char_p, []),
+    "climsr_version": (c_int, []),
+    "climsr_conv_chunk": (c_int, [c_int, c_int, c_int]),
+    "climsr_conv_packed_k": (c_int, [c_int, c_int, c_int]),
+    "climsr_conv_packed_rows": (c_int, [c_int]),
+    "climsr_pack_conv_weight": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "climsr_conv2d_fwd": (c_int, [P(ConvDesc), c_void_p, c_void_p, c_void_p, P(Epilogue), c_void_p, c_void_p]),
+    "climsr_conv2d_wgrad": (c_int, [P(ConvDesc), c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
+    "climsr_conv2d_wgrad_reduce": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
+                                           c_void_p]),
+    "climsr_conv2d_wgrad_splits": (c_int, [P(ConvDesc)]),
+    "climsr_conv2d_wgrad_workspace": (c_size_t, [P(ConvDesc), c_int]),
+    "climsr_act_grad": (c_int, [c_int64, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_float, c_float,
+                                c_void_p, c_int, c_void_p]),
+    "climsr_nchw_to_nhwc_bf16": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p]),
+    "climsr_nhwc_to_nchw_f32": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "climsr_axpby_f32": (c_int, [c_int64, c_int, c_float, c_void_p, c_int, c_int, c_float, c_void_p, c_int, c_int, c_void_p]),
+    "climsr_l1_loss": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
+    "climsr_l1_loss_grad": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
+    "climsr_adamw_hparams": (c_int, [c_void_p, c_int, c_double, c_double, c_double, c_double, c_double, c_double, c_double,
+                                     c_void_p, c_void_p]),
+    "climsr_adamw_step": (c_int, [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+}
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+class ClimsrError(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and type the HIP library.  Raises if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ClimsrError(f"libclimsr_hip.so not found at {LIB_PATH}: build it with `python -c 'import __graft_entry__ as g; "
+                          f"g.build()'` (the product path has no CPU fallback)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().climsr_last_error().decode(errors="replace")
+        raise ClimsrError(f"{what} failed (rc={rc}): {msg}")
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t) -> Optional[int]:
+    return None if t is None else t.data_ptr()

@@ -1,0 +1,38 @@
+// Shared device helpers for libclimsr_hip (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "climsr_hip.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace climsr {
+
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32: RNE, NaN-preserving
+  return __builtin_bit_cast(uint16_t, b);
+}
+__device__ __forceinline__ float bf2f(uint16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
+
+__device__ __forceinline__ float act_apply(float v, int act, float slope) {
+  if (act == 1) return v > 0.f ? v : v * slope;
+  if (act == 2) return v > 0.f ? v : 0.f;
+  return v;
+}
+
+// Transposed LDS read: within each 16-lane group, lane 4q+p supplies the address of row q, columns
+// 4p..4p+3 (16-bit elements); lane i receives column i of the 4 rows (row q -> element q).
+__device__ __forceinline__ s16x4 ds_read_tr16(const void* lds_ptr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)(lds_ptr));
+}
+
+static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
+static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
+
+}  // namespace climsr

@@ -1,0 +1,722 @@
+// Implicit-GEMM convolution for CDNA4 (gfx950): forward / data-gradient and weight-gradient.
+//
+// Replaces nn.Conv2d (+ fused F.interpolate(nearest), LeakyReLU/ReLU, residual adds) on the
+// ESRGAN hot path: climsr/models/esrgan.py:17-102, srcnn.py:6-18, rfb_esrgan.py:26-61.
+//
+// Layout: activations NHWC bf16; a conv reads channels [in_coff, in_coff+in_c) of a buffer with
+// in_cstride channels per pixel (the RDB dense concatenation is one 128-channel buffer, so
+// torch.cat is free).  GEMM view: M = output channels (MFMA A = packed weights), N = output pixels
+// (MFMA B = input pixels staged in LDS, im2col done by LDS addressing), K = taps x channels.
+// MFMA: v_mfma_f32_16x16x32_bf16.  Lane l: A[row l&15][k 8(l>>4)+j], B[k 8(l>>4)+j][col l&15],
+// C[row 4(l>>4)+i][col l&15].
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "common.h"
+
+namespace climsr {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s: %s", what, hipGetErrorString(e));
+    return CLIMSR_EHIP;
+  }
+  return CLIMSR_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// Tiling constants
+// ------------------------------------------------------------------------------------------
+constexpr int TW = 16;            // output tile width (one MFMA N-fragment of pixels)
+constexpr int XPAD = 8;           // channel padding of the LDS input tile (bank spread)
+constexpr int WPAD = 8;           // k padding of the LDS weight tile rows
+constexpr int FWD_LDS_BUDGET = 64 * 1024;
+
+struct FwdGeom {
+  int th, tph, tpw, ccp, kc, kcpad, nchunk, kpk, nt, mw;
+  size_t lds_tab, lds_x, lds_w, lds_total;
+};
+
+static int fwd_nt(int out_c) {
+  int nt = (out_c + 15) / 16;
+  return nt > 4 ? 4 : (nt == 3 ? 4 : nt);
+}
+
+static void fwd_geom(int in_c, int ks, int stride, int out_c, int cc, int mw, FwdGeom* g) {
+  g->mw = mw;
+  g->th = 4 * mw;
+  g->tph = (g->th - 1) * stride + ks;
+  g->tpw = (TW - 1) * stride + ks;
+  g->ccp = cc + XPAD;
+  g->kc = ks * ks * cc;
+  g->kcpad = round_up(g->kc, 32);
+  g->nchunk = ceil_div(in_c, cc);
+  g->kpk = g->nchunk * g->kcpad;
+  g->nt = fwd_nt(out_c);
+  g->lds_tab = (size_t)(g->kcpad / 8) * 4;
+  g->lds_tab = (g->lds_tab + 15) / 16 * 16;
+  g->lds_x = (size_t)g->tph * g->tpw * g->ccp * 2;
+  g->lds_w = (size_t)g->nt * 16 * (g->kcpad + WPAD) * 2;
+  g->lds_total = g->lds_tab + g->lds_x + g->lds_w;
+}
+
+}  // namespace climsr
+
+using namespace climsr;
+
+extern "C" const char* climsr_last_error(void) { return g_err; }
+extern "C" int climsr_version(void) { return 1; }
+
+extern "C" int climsr_conv_chunk(int in_c, int ks, int out_c) {
+  int cc = round_up(in_c, 8);
+  FwdGeom g;
+  while (cc > 8) {
+    fwd_geom(in_c, ks, 1, out_c, cc, 2, &g);
+    if (g.lds_total <= (size_t)FWD_LDS_BUDGET) break;
+    cc = round_up((cc + 1) / 2, 8);
+  }
+  return cc;
+}
+
+extern "C" int climsr_conv_packed_k(int in_c, int ks, int cc) {
+  return ceil_div(in_c, cc) * round_up(ks * ks * cc, 32);
+}
+
+extern "C" int climsr_conv_packed_rows(int out_c) {
+  int nt = fwd_nt(out_c);
+  return round_up(out_c, nt * 16);
+}
+
+// ------------------------------------------------------------------------------------------
+// Weight packing: fp32 OIHW -> bf16 [co_pad16][nchunk][kcpad], k' = tap*cc + c (zeros elsewhere)
+// ------------------------------------------------------------------------------------------
+__global__ void pack_kernel(const float* __restrict__ w, int rows, int kpk, int in_c_real, int out_c_real, int ks, int cc,
+                            int kcpad, int tflip, uint16_t* __restrict__ out) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long total = (long)rows * kpk;
+  if (idx >= total) return;
+  int co = (int)(idx / kpk);
+  int kk = (int)(idx % kpk);
+  int j = kk / kcpad;
+  int kr = kk % kcpad;
+  int tap = kr / cc;
+  int c = j * cc + kr % cc;
+  float v = 0.f;
+  int kk2 = ks * ks;
+  if (co < out_c_real && tap < kk2 && c < in_c_real) {
+    int ky = tap / ks, kx = tap % ks;
+    if (!tflip) {
+      v = w[(((long)co * in_c_real + c) * ks + ky) * ks + kx];
+    } else {  // src W[c][co][ks-1-ky][ks-1-kx] with src dims [in_c_real][out_c_real]
+      v = w[(((long)c * out_c_real + co) * ks + (ks - 1 - ky)) * ks + (ks - 1 - kx)];
+    }
+  }
+  out[idx] = f2bf(v);
+}
+
+extern "C" int climsr_pack_conv_weight(const float* w, int out_c, int in_c, int in_c_real, int out_c_real, int ks, int cc,
+                                       int transpose_flip, uint16_t* wpk, void* stream) {
+  if (!w || !wpk || in_c % 8 || cc % 8 || cc <= 0 || ks <= 0) {
+    set_error("pack_conv_weight: bad args (in_c=%d cc=%d ks=%d)", in_c, cc, ks);
+    return CLIMSR_EINVAL;
+  }
+  int rows = climsr_conv_packed_rows(out_c);
+  int kcpad = round_up(ks * ks * cc, 32);
+  int kpk = climsr_conv_packed_k(in_c, ks, cc);
+  long total = (long)rows * kpk;
+  hipLaunchKernelGGL(pack_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, w, rows, kpk, in_c_real,
+                     out_c_real, ks, cc, kcpad, transpose_flip, wpk);
+  return check_launch("pack_conv_weight");
+}
+
+// ------------------------------------------------------------------------------------------
+// Forward / data-gradient kernel
+// ------------------------------------------------------------------------------------------
+struct FwdArgs {
+  const uint16_t* x;
+  const uint16_t* w;
+  const float* bias;
+  void* y;
+  const uint16_t* res1;
+  const uint16_t* res2;
+  int n, in_h, in_w, in_c, in_cs, in_co, up, ks, stride, pad, out_h, out_w, out_c, out_cs, out_co, cc;
+  int tph, tpw, ccp, kcpad, nchunk, kpk, tiles_x, tiles_y;
+  int act, out_mode, down2;
+  float slope, alpha1, alpha2;
+  int r1_cs, r1_co, r2_cs, r2_co;
+  int lds_tab, lds_x;
+};
+
+template <int MW, int NT>
+__global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int* tab = (int*)smem;
+  uint16_t* xs = (uint16_t*)(smem + a.lds_tab);
+  uint16_t* ws = (uint16_t*)(smem + a.lds_tab + a.lds_x);
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int g = lane >> 4;
+  const int col = lane & 15;
+
+  int bid = blockIdx.x;
+  const int tx = bid % a.tiles_x;
+  bid /= a.tiles_x;
+  const int ty = bid % a.tiles_y;
+  const int nimg = bid / a.tiles_y;
+  const int ox0 = tx * TW;
+  const int oy0 = ty * (4 * MW);
+  const int co_blk0 = blockIdx.y * NT * 16;
+  const int wpitch = a.kcpad + WPAD;
+  const int ks2 = a.ks * a.ks;
+
+  // tap table: LDS element offset of k-group (8 channels) within a chunk
+  for (int i = tid; i < a.kcpad / 8; i += 256) {
+    int kr = i * 8;
+    int tap = kr / a.cc;
+    int c = kr - tap * a.cc;
+    if (tap >= ks2) { tap = 0; c = 0; }
+    int ky = tap / a.ks, kx = tap - (tap / a.ks) * a.ks;
+    tab[i] = (ky * a.tpw + kx) * a.ccp + c;
+  }
+
+  f32x4 acc[MW][NT];
+#pragma unroll
+  for (int m = 0; m < MW; ++m)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[m][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  int pixbase[MW];
+#pragma unroll
+  for (int m = 0; m < MW; ++m) pixbase[m] = ((wave * MW + m) * a.stride * a.tpw + col * a.stride) * a.ccp;
+
+  const int lh = a.in_h * a.up, lw = a.in_w * a.up;
+  const int iy0 = oy0 * a.stride - a.pad, ix0 = ox0 * a.stride - a.pad;
+  const int cvec = a.cc / 8;
+  const int nvec_x = a.tph * a.tpw * cvec;
+  const int wvec_row = a.kcpad / 8;
+  const int nvec_w = NT * 16 * wvec_row;
+  const int upsh = a.up == 2 ? 1 : 0;
+
+  for (int j = 0; j < a.nchunk; ++j) {
+    const int c0 = j * a.cc;
+    __syncthreads();
+    // stage input tile (logical, upsampled coordinates; zero padding)
+    for (int v = tid; v < nvec_x; v += 256) {
+      int pix = v / cvec;
+      int cg = v - pix * cvec;
+      int ty_ = pix / a.tpw;
+      int tx_ = pix - ty_ * a.tpw;
+      int iy = iy0 + ty_, ix = ix0 + tx_;
+      int c = c0 + cg * 8;
+      uint4 val = make_uint4(0, 0, 0, 0);
+      if (iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c) {
+        long src = (((long)nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + c;
+        val = *(const uint4*)(a.x + src);
+      }
+      *(uint4*)(xs + pix * a.ccp + cg * 8) = val;
+    }
+    // stage weight chunk
+    for (int v = tid; v < nvec_w; v += 256) {
+      int r = v / wvec_row;
+      int kv = v - r * wvec_row;
+      uint4 val = *(const uint4*)(a.w + (long)(co_blk0 + r) * a.kpk + (long)j * a.kcpad + kv * 8);
+      *(uint4*)(ws + r * wpitch + kv * 8) = val;
+    }
+    __syncthreads();
+    const int nks = a.kcpad / 32;
+    for (int kstep = 0; kstep < nks; ++kstep) {
+      const int off = tab[kstep * 4 + g];
+      bf16x8 af[NT];
+      bf16x8 bfr[MW];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) af[t] = *(const bf16x8*)(ws + (t * 16 + col) * wpitch + kstep * 32 + g * 8);
+#pragma unroll
+      for (int m = 0; m < MW; ++m) bfr[m] = *(const bf16x8*)(xs + pixbase[m] + off);
+#pragma unroll
+      for (int m = 0; m < MW; ++m)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bfr[m], acc[m][t], 0, 0, 0);
+    }
+  }
+
+  // ---------------- epilogue ----------------
+  const int ox = ox0 + col;
+  if (a.down2) {
+    // sum the 2x2 block: rows (m, m+1) are in this wave (MW even, oy0 even); columns pair via lane^1
+#pragma unroll
+    for (int m = 0; m < MW; m += 2) {
+      const int oy = oy0 + wave * MW + m;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float s = acc[m][t][i] + acc[m + 1][t][i];
+          s += __shfl_xor(s, 1);
+          v[i] = s;
+        }
+        const int co = co_blk0 + t * 16 + g * 4;
+        if ((col & 1) == 0 && oy < a.out_h && ox < a.out_w) {
+          const int dh = a.out_h >> 1, dw = a.out_w >> 1;
+          long pidx = ((long)nimg * dh + (oy >> 1)) * dw + (ox >> 1);
+          float* yp = (float*)a.y + pidx * a.out_cs + a.out_co + co;
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (co + i < a.out_c) {
+              if (a.out_mode == 2) yp[i] += v[i];
+              else yp[i] = v[i];
+            }
+        }
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int m = 0; m < MW; ++m) {
+    const int oy = oy0 + wave * MW + m;
+    const bool pv = oy < a.out_h && ox < a.out_w;
+    const long pidx = ((long)nimg * a.out_h + oy) * a.out_w + ox;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int co = co_blk0 + t * 16 + g * 4;
+      if (!pv || co >= a.out_c) continue;
+      const bool full = (co + 3 < a.out_c);
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float s = acc[m][t][i];
+        if (a.bias && co + i < a.out_c) s += a.bias[co + i];
+        v[i] = act_apply(s, a.act, a.slope);
+      }
+      if (a.res1) {
+        const uint16_t* rp = a.res1 + pidx * a.r1_cs + a.r1_co + co;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (co + i < a.out_c) v[i] = v[i] * a.alpha1 + bf2f(rp[i]);
+      }
+      if (a.res2) {
+        const uint16_t* rp = a.res2 + pidx * a.r2_cs + a.r2_co + co;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (co + i < a.out_c) v[i] = v[i] * a.alpha2 + bf2f(rp[i]);
+      }
+      const long ob = pidx * a.out_cs + a.out_co + co;
+      if (a.out_mode == 0) {
+        uint16_t* yp = (uint16_t*)a.y + ob;
+        if (full && (ob & 3) == 0) {
+          uint2 pk;
+          pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+          pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+          *(uint2*)yp = pk;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (co + i < a.out_c) yp[i] = f2bf(v[i]);
+        }
+      } else {
+        float* yp = (float*)a.y + ob;
+        if (a.out_mode == 2) {
+          if (full && (ob & 3) == 0) {
+            float4 o = *(float4*)yp;
+            o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
+            *(float4*)yp = o;
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              if (co + i < a.out_c) yp[i] += v[i];
+          }
+        } else {
+          if (full && (ob & 3) == 0) {
+            *(float4*)yp = make_float4(v[0], v[1], v[2], v[3]);
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              if (co + i < a.out_c) yp[i] = v[i];
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int MW, int NT>
+static int launch_fwd(const FwdArgs& a, int ncob, size_t lds, hipStream_t s) {
+  dim3 grid(a.tiles_x * a.tiles_y * a.n, ncob);
+  auto k = conv_fwd_kernel<MW, NT>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a);
+  return check_launch("conv2d_fwd");
+}
+
+extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, const uint16_t* wpk, const float* bias,
+                                 const ClimsrEpilogue* ep, void* y, void* stream) {
+  if (!d || !x || !wpk || !ep || !y) {
+    set_error("conv2d_fwd: null argument");
+    return CLIMSR_EINVAL;
+  }
+  if (d->in_c % 8 || d->in_cstride % 8 || d->in_coff % 8 || d->cc % 8 || d->cc <= 0 || (d->up != 1 && d->up != 2) ||
+      (d->stride != 1 && d->stride != 2) || d->ks < 1 || d->n <= 0 || d->out_c <= 0 || d->in_coff + d->in_c > d->in_cstride) {
+    set_error("conv2d_fwd: unsupported geometry (in_c=%d cs=%d coff=%d cc=%d up=%d stride=%d ks=%d)", d->in_c, d->in_cstride,
+              d->in_coff, d->cc, d->up, d->stride, d->ks);
+    return CLIMSR_EINVAL;
+  }
+  if (ep->down2 && (ep->out_mode == 0 || ep->res1 || ep->res2 || bias || ep->act || (d->out_h & 1) || (d->out_w & 1))) {
+    set_error("conv2d_fwd: down2 epilogue needs f32 output, no bias/act/residual, even output size");
+    return CLIMSR_EINVAL;
+  }
+  FwdGeom g;
+  fwd_geom(d->in_c, d->ks, d->stride, d->out_c, d->cc, 2, &g);
+  if (g.lds_total > 160 * 1024) {
+    set_error("conv2d_fwd: LDS %zu exceeds 160 KiB (cc=%d)", g.lds_total, d->cc);
+    return CLIMSR_EINVAL;
+  }
+  FwdArgs a;
+  a.x = x; a.w = wpk; a.bias = bias; a.y = y;
+  a.res1 = (const uint16_t*)ep->res1; a.res2 = (const uint16_t*)ep->res2;
+  a.n = d->n; a.in_h = d->in_h; a.in_w = d->in_w; a.in_c = d->in_c; a.in_cs = d->in_cstride; a.in_co = d->in_coff;
+  a.up = d->up; a.ks = d->ks; a.stride = d->stride; a.pad = d->pad; a.out_h = d->out_h; a.out_w = d->out_w;
+  a.out_c = d->out_c; a.out_cs = d->out_cstride; a.out_co = d->out_coff; a.cc = d->cc;
+  a.tph = g.tph; a.tpw = g.tpw; a.ccp = g.ccp; a.kcpad = g.kcpad; a.nchunk = g.nchunk; a.kpk = g.kpk;
+  a.tiles_x = ceil_div(d->out_w, TW); a.tiles_y = ceil_div(d->out_h, g.th);
+  a.act = ep->act; a.out_mode = ep->out_mode; a.down2 = ep->down2;
+  a.slope = ep->slope; a.alpha1 = ep->alpha1; a.alpha2 = ep->alpha2;
+  a.r1_cs = ep->res1_cstride; a.r1_co = ep->res1_coff; a.r2_cs = ep->res2_cstride; a.r2_co = ep->res2_coff;
+  a.lds_tab = (int)g.lds_tab; a.lds_x = (int)g.lds_x;
+  int rows = climsr_conv_packed_rows(d->out_c);
+  int ncob = rows / (g.nt * 16);
+  hipStream_t s = (hipStream_t)stream;
+  switch (g.nt) {
+    case 1: return launch_fwd<2, 1>(a, ncob, g.lds_total, s);
+    case 2: return launch_fwd<2, 2>(a, ncob, g.lds_total, s);
+    default: return launch_fwd<2, 4>(a, ncob, g.lds_total, s);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Weight gradient: dW[co][ci][tap] = sum_px dz[px][co] * x[px*stride + tap - pad][ci]
+// GEMM: M = co (A = dz^T), N = ci (B = x), K = pixels.  Both operands are pixel-major in NHWC, so
+// they are read from LDS with ds_read_b64_tr_b16 (row = pixel, any per-lane pixel address: the
+// tap shift of the im2col is free).  WG tile: 16*NTC co x 16 ci x TB taps; the 4 waves split the
+// pixels of each 16x16 output-pixel tile and are summed through LDS at the end; splits over
+// pixel tiles write disjoint fp32 partial slabs (deterministic, reduced by wgrad_reduce).
+// ------------------------------------------------------------------------------------------
+constexpr int WG_TH = 16;
+constexpr int WG_XP = 24;  // LDS pixel pitch (channels) of the x tile (16 + 8 pad)
+
+struct WgArgs {
+  const uint16_t* x;
+  const uint16_t* dz;
+  float* part;
+  float* bpart;
+  int n, in_h, in_w, in_c, in_cs, in_co, up, ks, stride, pad, out_h, out_w, out_c, dz_cs;
+  int tph, tpw, dzp, tiles_x, tiles_y, ntiles, nsplit, ntapb, ncib, co_rows, kw;
+  int lds_x;
+};
+
+template <int NTC, int TB>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* xs = (uint16_t*)smem;
+  uint16_t* zs = (uint16_t*)(smem + a.lds_x);
+  float* red = (float*)smem;  // reused for the cross-wave reduction at the end
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int g = lane >> 4;
+  const int q = (lane & 15) >> 2;
+  const int p = lane & 3;
+  const int col = lane & 15;
+
+  int bid = blockIdx.x;
+  const int tb = bid % a.ntapb;
+  bid /= a.ntapb;
+  const int cib = bid % a.ncib;
+  const int cob = bid / a.ncib;
+  const int split = blockIdx.y;
+  const int ci0 = cib * 16;
+  const int co0 = cob * NTC * 16;
+  const int tap0 = tb * TB;
+  const int ks2 = a.ks * a.ks;
+  const bool do_bias = (cib == 0 && tb == 0 && a.bpart != nullptr);
+
+  f32x4 acc[NTC][TB];
+  f32x4 accb[NTC];
+#pragma unroll
+  for (int t = 0; t < NTC; ++t) {
+    accb[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < TB; ++u) acc[t][u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+  bf16x8 ones;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ones[i] = (__bf16)1.0f;
+
+  int tapoff[TB];
+#pragma unroll
+  for (int u = 0; u < TB; ++u) {
+    int tap = tap0 + u;
+    if (tap >= ks2) tap = 0;  // weight rows past ks*ks are never written
+    tapoff[u] = ((tap / a.ks) * a.tpw + (tap % a.ks)) * WG_XP;
+  }
+
+  const int lh = a.in_h * a.up, lw = a.in_w * a.up;
+  const int upsh = a.up == 2 ? 1 : 0;
+  const int zvec = NTC * 2;  // 16B vectors of dz per pixel
+  const int nvec_x = a.tph * a.tpw * 2;
+  const int nvec_z = WG_TH * TW * zvec;
+
+  for (int tile = split; tile < a.ntiles; tile += a.nsplit) {
+    int tt = tile;
+    const int tx = tt % a.tiles_x;
+    tt /= a.tiles_x;
+    const int ty = tt % a.tiles_y;
+    const int nimg = tt / a.tiles_y;
+    const int ox0 = tx * TW, oy0 = ty * WG_TH;
+    const int iy0 = oy0 * a.stride - a.pad, ix0 = ox0 * a.stride - a.pad;
+    __syncthreads();
+    for (int v = tid; v < nvec_x; v += 256) {
+      int pix = v >> 1;
+      int h = v & 1;
+      int ty_ = pix / a.tpw, tx_ = pix - (pix / a.tpw) * a.tpw;
+      int iy = iy0 + ty_, ix = ix0 + tx_;
+      int c = ci0 + h * 8;
+      uint4 val = make_uint4(0, 0, 0, 0);
+      if (iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c) {
+        long src = (((long)nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + c;
+        val = *(const uint4*)(a.x + src);
+      }
+      *(uint4*)(xs + pix * WG_XP + h * 8) = val;
+    }
+    for (int v = tid; v < nvec_z; v += 256) {
+      int pix = v / zvec;
+      int cv = v - pix * zvec;
+      int oy = oy0 + pix / TW, ox = ox0 + (pix % TW);
+      int c = co0 + cv * 8;
+      uint4 val = make_uint4(0, 0, 0, 0);
+      if (oy < a.out_h && ox < a.out_w && c < a.dz_cs) {
+        val = *(const uint4*)(a.dz + (((long)nimg * a.out_h + oy) * a.out_w + ox) * a.dz_cs + c);
+      }
+      *(uint4*)(zs + pix * a.dzp + cv * 8) = val;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int kk = wave * 2 + s;  // k-step: output pixel rows 2kk, 2kk+1 of the tile
+      // pixel handled as row q (+4) of this lane's tr reads
+      const int k0 = kk * 32 + 8 * g + q;
+      const int k1 = k0 + 4;
+      const int r0 = k0 >> 4, c0_ = k0 & 15, r1 = k1 >> 4, c1_ = k1 & 15;
+      bf16x8 af[NTC];
+#pragma unroll
+      for (int t = 0; t < NTC; ++t) {
+        s16x4 lo = ds_read_tr16(zs + k0 * a.dzp + t * 16 + 4 * p);
+        s16x4 hi = ds_read_tr16(zs + k1 * a.dzp + t * 16 + 4 * p);
+        short v8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[t] = __builtin_bit_cast(bf16x8, v8);
+      }
+      const int xb0 = ((r0 * a.stride) * a.tpw + c0_ * a.stride) * WG_XP + 4 * p;
+      const int xb1 = ((r1 * a.stride) * a.tpw + c1_ * a.stride) * WG_XP + 4 * p;
+      if (do_bias) {
+#pragma unroll
+        for (int t = 0; t < NTC; ++t) accb[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], ones, accb[t], 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < TB; ++u) {
+        s16x4 lo = ds_read_tr16(xs + xb0 + tapoff[u]);
+        s16x4 hi = ds_read_tr16(xs + xb1 + tapoff[u]);
+        short v8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bf16x8 bfr = __builtin_bit_cast(bf16x8, v8);
+#pragma unroll
+        for (int t = 0; t < NTC; ++t) acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bfr, acc[t][u], 0, 0, 0);
+      }
+    }
+  }
+
+  // cross-wave reduction through LDS (waves 1..3 -> wave 0)
+  constexpr int NF = NTC * TB;
+  for (int r = 1; r < 4; ++r) {
+    __syncthreads();
+    if (wave == r) {
+#pragma unroll
+      for (int t = 0; t < NTC; ++t)
+#pragma unroll
+        for (int u = 0; u < TB; ++u) *(f32x4*)(red + ((t * TB + u) * 64 + lane) * 4) = acc[t][u];
+#pragma unroll
+      for (int t = 0; t < NTC; ++t) *(f32x4*)(red + ((NF + t) * 64 + lane) * 4) = accb[t];
+    }
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+      for (int t = 0; t < NTC; ++t) {
+#pragma unroll
+        for (int u = 0; u < TB; ++u) acc[t][u] += *(f32x4*)(red + ((t * TB + u) * 64 + lane) * 4);
+        accb[t] += *(f32x4*)(red + ((NF + t) * 64 + lane) * 4);
+      }
+    }
+  }
+  if (wave != 0) return;
+  const int ci = ci0 + col;
+  float* slab = a.part + (long)split * a.co_rows * a.kw;
+#pragma unroll
+  for (int t = 0; t < NTC; ++t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = co0 + t * 16 + g * 4 + i;
+      if (ci < a.in_c) {
+#pragma unroll
+        for (int u = 0; u < TB; ++u) {
+          const int tap = tap0 + u;
+          if (tap < ks2) slab[(long)co * a.kw + ci * ks2 + tap] = acc[t][u][i];
+        }
+      }
+      if (do_bias && col == 0) a.bpart[(long)split * a.co_rows + co] = accb[t][i];
+    }
+  }
+}
+
+struct WgPlan {
+  int ntc, tb, ntapb, ncib, ncob, co_rows, tiles_x, tiles_y, ntiles, tph, tpw, dzp, kw;
+  size_t lds_x, lds_z, lds_total;
+};
+
+static void wg_plan(const ClimsrConvDesc* d, WgPlan* w) {
+  int rows = round_up(d->out_c, 16);
+  w->ntc = rows >= 64 ? 4 : (rows >= 32 ? 2 : 1);
+  int ks2 = d->ks * d->ks;
+  w->tb = ks2 >= 9 ? 9 : (ks2 >= 5 ? 5 : 1);
+  if (ks2 == 25) w->tb = 5;
+  w->ntapb = ceil_div(ks2, w->tb);
+  w->ncib = ceil_div(d->in_c, 16);
+  w->ncob = ceil_div(rows, w->ntc * 16);
+  w->co_rows = w->ncob * w->ntc * 16;
+  w->tiles_x = ceil_div(d->out_w, TW);
+  w->tiles_y = ceil_div(d->out_h, WG_TH);
+  w->ntiles = d->n * w->tiles_x * w->tiles_y;
+  w->tph = (WG_TH - 1) * d->stride + d->ks;
+  w->tpw = (TW - 1) * d->stride + d->ks;
+  w->dzp = w->ntc * 16 + 8;
+  w->kw = d->in_c * ks2;
+  w->lds_x = (size_t)w->tph * w->tpw * WG_XP * 2;
+  w->lds_x = (w->lds_x + 15) / 16 * 16;
+  w->lds_z = (size_t)WG_TH * TW * w->dzp * 2;
+  size_t red = (size_t)(w->ntc * w->tb + w->ntc) * 64 * 16;
+  w->lds_total = w->lds_x + w->lds_z;
+  if (red > w->lds_total) w->lds_total = red;
+}
+
+extern "C" int climsr_conv2d_wgrad_splits(const ClimsrConvDesc* d) {
+  WgPlan w;
+  wg_plan(d, &w);
+  int base = w.ntapb * w.ncib * w.ncob;
+  int ns = ceil_div(1024, base);
+  if (ns > w.ntiles) ns = w.ntiles;
+  if (ns < 1) ns = 1;
+  return ns;
+}
+
+extern "C" size_t climsr_conv2d_wgrad_workspace(const ClimsrConvDesc* d, int nsplit) {
+  WgPlan w;
+  wg_plan(d, &w);
+  return (size_t)nsplit * w.co_rows * w.kw + (size_t)nsplit * w.co_rows;
+}
+
+template <int NTC, int TB>
+static int launch_wg(const WgArgs& a, int nblk, size_t lds, hipStream_t s) {
+  auto k = conv_wgrad_kernel<NTC, TB>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(k, dim3(nblk, a.nsplit), dim3(256), lds, s, a);
+  return check_launch("conv2d_wgrad");
+}
+
+extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, const uint16_t* dz, int dz_cstride, float* partial,
+                                   float* bias_partial, int nsplit, void* stream) {
+  if (!d || !x || !dz || !partial || nsplit <= 0 || d->in_c % 8 || d->in_cstride % 8 || d->in_coff % 8 || dz_cstride % 8 ||
+      (d->up != 1 && d->up != 2) || (d->stride != 1 && d->stride != 2)) {
+    set_error("conv2d_wgrad: bad args");
+    return CLIMSR_EINVAL;
+  }
+  WgPlan w;
+  wg_plan(d, &w);
+  if (w.lds_total > 160 * 1024) {
+    set_error("conv2d_wgrad: LDS %zu too large", w.lds_total);
+    return CLIMSR_EINVAL;
+  }
+  WgArgs a;
+  a.x = x; a.dz = dz; a.part = partial; a.bpart = bias_partial;
+  a.n = d->n; a.in_h = d->in_h; a.in_w = d->in_w; a.in_c = d->in_c; a.in_cs = d->in_cstride; a.in_co = d->in_coff;
+  a.up = d->up; a.ks = d->ks; a.stride = d->stride; a.pad = d->pad; a.out_h = d->out_h; a.out_w = d->out_w;
+  a.out_c = d->out_c; a.dz_cs = dz_cstride;
+  a.tph = w.tph; a.tpw = w.tpw; a.dzp = w.dzp; a.tiles_x = w.tiles_x; a.tiles_y = w.tiles_y; a.ntiles = w.ntiles;
+  a.nsplit = nsplit; a.ntapb = w.ntapb; a.ncib = w.ncib; a.co_rows = w.co_rows; a.kw = w.kw;
+  a.lds_x = (int)w.lds_x;
+  int nblk = w.ntapb * w.ncib * w.ncob;
+  hipStream_t s = (hipStream_t)stream;
+#define WG_CASE(NTC, TB) \
+  if (w.ntc == NTC && w.tb == TB) return launch_wg<NTC, TB>(a, nblk, w.lds_total, s);
+  WG_CASE(1, 1) WG_CASE(2, 1) WG_CASE(4, 1)
+  WG_CASE(1, 5) WG_CASE(2, 5) WG_CASE(4, 5)
+  WG_CASE(1, 9) WG_CASE(2, 9) WG_CASE(4, 9)
+#undef WG_CASE
+  set_error("conv2d_wgrad: no kernel for ntc=%d tb=%d", w.ntc, w.tb);
+  return CLIMSR_EINVAL;
+}
+
+__global__ void wgrad_reduce_kernel(const float* __restrict__ part, const float* __restrict__ bpart, int nsplit, int out_c,
+                                    int in_c_real, int in_c, int ks2, int co_rows, int kw, float* __restrict__ wg,
+                                    float* __restrict__ bg, int accumulate) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long nw = (long)out_c * in_c_real * ks2;
+  if (idx < nw) {
+    int co = (int)(idx / ((long)in_c_real * ks2));
+    int rem = (int)(idx % ((long)in_c_real * ks2));  // ci*ks2 + tap
+    const float* src = part + (long)co * kw + rem;
+    float s = 0.f;
+    for (int sp = 0; sp < nsplit; ++sp) s += src[(long)sp * co_rows * kw];
+    if (accumulate) wg[idx] += s;
+    else wg[idx] = s;
+  } else if (bg && idx < nw + out_c) {
+    int co = (int)(idx - nw);
+    float s = 0.f;
+    for (int sp = 0; sp < nsplit; ++sp) s += bpart[(long)sp * co_rows + co];
+    if (accumulate) bg[co] += s;
+    else bg[co] = s;
+  }
+}
+
+extern "C" int climsr_conv2d_wgrad_reduce(const float* partial, const float* bias_partial, int nsplit, int out_c, int in_c_real,
+                                          int in_c, int ks, float* wgrad, float* bias_grad, int accumulate, void* stream) {
+  if (!partial || !wgrad || nsplit <= 0) {
+    set_error("conv2d_wgrad_reduce: bad args");
+    return CLIMSR_EINVAL;
+  }
+  int rows = round_up(out_c, 16);
+  int ntc = rows >= 64 ? 4 : (rows >= 32 ? 2 : 1);
+  int co_rows = ceil_div(rows, ntc * 16) * ntc * 16;
+  int ks2 = ks * ks;
+  int kw = in_c * ks2;
+  long total = (long)out_c * in_c_real * ks2 + (bias_grad ? out_c : 0);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, partial, bias_partial,
+                     nsplit, out_c, in_c_real, in_c, ks2, co_rows, kw, wgrad, bias_grad, accumulate);
+  return check_launch("conv2d_wgrad_reduce");
+}

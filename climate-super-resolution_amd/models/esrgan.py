@@ -1,0 +1,369 @@
+"""ESRGAN RRDB generator (drop-in for ``climsr.models.esrgan.ESRGANGenerator``).
+
+Same constructor kwargs (``in_channels, out_channels, nf, nb, gc, scaling_factor, **kwargs`` —
+``scale_factor`` from conf/generator/default.yaml:3 is swallowed by **kwargs exactly as in the
+reference, esrgan.py:58-67), same submodule names and ``state_dict`` keys, same
+``forward(x, elev, mask)`` (esrgan.py:89-102).  The forward and backward run as one autograd
+node whose arithmetic is entirely HIP (libclimsr_hip.so):
+
+* one NHWC bf16 "dense" buffer of nf+4*gc channels per RDB holds x, x1..x4 (torch.cat of
+  esrgan.py:34-37 is free: conv k reads channels [0, nf+(k-1)gc) and writes its gc outputs after
+  them);
+* conv5 fuses ``x5*0.2 + x`` (esrgan.py:38) and, in the third RDB of an RRDB, ``out*0.2 + x``
+  (esrgan.py:54) into its epilogue; trunk_conv fuses the global skip (esrgan.py:91);
+* the nearest x2 upsample (esrgan.py:94,97) is done on load by the following conv, and its
+  backward (2x2 sum) in the dgrad epilogue;
+* parameter gradients land in one flat fp32 buffer (core/flat.py).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn as nn
+from torch import Tensor
+
+from ..core.flat import FlatParamsMixin
+from ..ops import (ACT_LRELU, ACT_NONE, ACT_RELU, OUT_F32, ConvPlan, Workspace, act_grad, axpby, nchw_to_nhwc)
+from .srcnn import SRCNN
+
+
+class ResidualDenseBlock(nn.Module):
+    """Parameter container with the reference's names (esrgan.py:17-27)."""
+
+    def __init__(self, nf=64, gc=32, bias=True):
+        super().__init__()
+        self.conv1 = nn.Conv2d(nf, gc, 3, 1, 1, bias=bias)
+        self.conv2 = nn.Conv2d(nf + gc, gc, 3, 1, 1, bias=bias)
+        self.conv3 = nn.Conv2d(nf + 2 * gc, gc, 3, 1, 1, bias=bias)
+        self.conv4 = nn.Conv2d(nf + 3 * gc, gc, 3, 1, 1, bias=bias)
+        self.conv5 = nn.Conv2d(nf + 4 * gc, nf, 3, 1, 1, bias=bias)
+        self.lrelu = nn.LeakyReLU(negative_slope=0.2, inplace=True)
+
+    def forward(self, x):  # pragma: no cover - the whole generator runs as one native node
+        raise RuntimeError("ResidualDenseBlock runs inside ESRGANGenerator's native forward")
+
+
+class ResidualInResidualDenseBlock(nn.Module):
+    """esrgan.py:41-54."""
+
+    def __init__(self, nf, gc=32):
+        super().__init__()
+        self.RDB1 = ResidualDenseBlock(nf, gc)
+        self.RDB2 = ResidualDenseBlock(nf, gc)
+        self.RDB3 = ResidualDenseBlock(nf, gc)
+
+    def forward(self, x):  # pragma: no cover
+        raise RuntimeError("ResidualInResidualDenseBlock runs inside ESRGANGenerator's native forward")
+
+
+def _bf16(shape, dev):
+    return torch.empty(shape, dtype=torch.bfloat16, device=dev)
+
+
+def _f32(shape, dev):
+    return torch.empty(shape, dtype=torch.float32, device=dev)
+
+
+class _Engine:
+    """Native forward/backward of one ESRGANGenerator (per device)."""
+
+    def __init__(self, gen: "ESRGANGenerator"):
+        self.gen = gen
+        nf, gc, nb = gen.nf, gen.gc, gen.nb
+        self.nf, self.gc, self.nb = nf, gc, nb
+        self.dc = nf + 4 * gc
+        assert nf % 8 == 0 and gc % 8 == 0, "nf and gc must be multiples of 8"
+        self.cin = gen.in_channels
+        self.cin_pad = (self.cin + 7) // 8 * 8
+        self.plans: Dict[str, ConvPlan] = {}
+        self.ws = Workspace()
+        self.version = -1
+        self.scratch: Dict[str, Tensor] = {}
+
+        def add(name, conv: nn.Conv2d):
+            p = ConvPlan(conv.in_channels, conv.out_channels, conv.kernel_size[0], conv.stride[0], conv.padding[0], name)
+            self.plans[name] = p
+
+        add("conv_first", gen.conv_first)
+        for i, rrdb in enumerate(gen.RRDB_trunk):
+            for r in (1, 2, 3):
+                rdb = getattr(rrdb, f"RDB{r}")
+                for c in range(1, 6):
+                    add(f"RRDB_trunk.{i}.RDB{r}.conv{c}", getattr(rdb, f"conv{c}"))
+        add("trunk_conv", gen.trunk_conv)
+        add("upconv1", gen.upconv1)
+        if gen.scale_factor == 4:
+            add("upconv2", gen.upconv2)
+        add("HRconv", gen.HRconv)
+        add("conv_last", gen.conv_last)
+        add("srcnn.conv1", gen.srcnn.conv1)
+        add("srcnn.conv2", gen.srcnn.conv2)
+        add("srcnn.conv3", gen.srcnn.conv3)
+        self.modules = dict(gen.named_modules())
+        self.bind()
+
+    # ------------------------------------------------------------------ weights
+    def bind(self):
+        gen = self.gen
+        for name, p in self.plans.items():
+            conv = self.modules[name]
+            p.bind(conv.weight, conv.bias, need_t=(name != "conv_first"))
+        self.version = -1
+
+    def bind_grads(self):
+        for name, p in self.plans.items():
+            conv = self.modules[name]
+            p.gw = conv.weight.grad
+            p.gb = conv.bias.grad if conv.bias is not None else None
+
+    def ensure_packed(self):
+        v = self.gen._flat._version
+        if v != self.version:
+            for p in self.plans.values():
+                p.pack()
+            self.version = v
+
+    def repack(self):
+        for p in self.plans.values():
+            p.pack()
+        self.version = self.gen._flat._version
+
+    def rdb_name(self, i, r, c):
+        return f"RRDB_trunk.{i}.RDB{r}.conv{c}"
+
+    def _scratch(self, key, shape, dtype, dev, zero=False):
+        t = self.scratch.get(key)
+        if t is None or tuple(t.shape) != tuple(shape) or t.device != dev:
+            t = torch.zeros(shape, dtype=dtype, device=dev) if zero else torch.empty(shape, dtype=dtype, device=dev)
+            self.scratch[key] = t
+        return t
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, x: Tensor, elev: Tensor, mask: Tensor, keep: bool):
+        n, cin, h, w = x.shape
+        dev = x.device
+        nf, gc, dc, nb = self.nf, self.gc, self.dc, self.nb
+        sf = self.gen.scale_factor
+        h2, w2 = 2 * h, 2 * w
+        hh, ww = (4 * h, 4 * w) if sf == 4 else (2 * h, 2 * w)
+        assert elev.shape == (n, 1, hh, ww) and mask.shape == (n, 1, hh, ww), "elev/mask must be [N,1,sH,sW]"
+        P = self.plans
+        self.ensure_packed()
+        x = x.contiguous().float()
+        lr = torch.zeros((n, h, w, self.cin_pad), dtype=torch.bfloat16, device=dev)
+        nchw_to_nhwc(x, lr, self.cin_pad, 0)
+        ndense = 3 * nb + 1 if keep else 2
+        dense = [_bf16((n, h, w, dc), dev) for _ in range(ndense)]
+        rrdb_in = _bf16((n, h, w, nf), dev) if not keep else None
+        P["conv_first"].fwd(lr, self.cin_pad, 0, h, w, dense[0], dc, 0, n)
+        fea = dense[0] if keep else _bf16((n, h, w, nf), dev)
+        if not keep:  # keep a copy of fea for the global skip (dense[0] is recycled)
+            P["conv_first"].fwd(lr, self.cin_pad, 0, h, w, fea, nf, 0, n)
+        for i in range(3 * nb):
+            blk, r = divmod(i, 3)
+            src = dense[i] if keep else dense[i % 2]
+            dst = dense[i + 1] if keep else dense[(i + 1) % 2]
+            if r == 0 and not keep:  # remember the RRDB input for its residual
+                axpby_bf16_copy(src, rrdb_in, n * h * w, nf, dc)
+            for c in range(1, 5):
+                P[self.rdb_name(blk, r + 1, c)].fwd(src, dc, 0, h, w, src, dc, nf + (c - 1) * gc, n, act=ACT_LRELU)
+            res2 = None
+            if r == 2:
+                res2 = dense[3 * blk] if keep else rrdb_in
+            P[self.rdb_name(blk, r + 1, 5)].fwd(src, dc, 0, h, w, dst, dc, 0, n, res1=src, alpha1=0.2, res1_cs=dc, res1_co=0,
+                                                 res2=res2, alpha2=0.2, res2_cs=(dc if keep else nf), res2_co=0)
+        last = dense[3 * nb] if keep else dense[(3 * nb) % 2]
+        fea2 = _bf16((n, h, w, nf), dev)
+        P["trunk_conv"].fwd(last, dc, 0, h, w, fea2, nf, 0, n, res1=fea, alpha1=1.0, res1_cs=(dc if keep else nf), res1_co=0)
+        u1 = _bf16((n, h2, w2, nf), dev)
+        P["upconv1"].fwd(fea2, nf, 0, h, w, u1, nf, 0, n, up=2, act=ACT_LRELU)
+        if sf == 4:
+            u2 = _bf16((n, hh, ww, nf), dev)
+            P["upconv2"].fwd(u1, nf, 0, h2, w2, u2, nf, 0, n, up=2, act=ACT_LRELU)
+        else:
+            u2 = u1
+        hr = _bf16((n, hh, ww, nf), dev)
+        P["HRconv"].fwd(u2, nf, 0, hh, ww, hr, nf, 0, n, act=ACT_LRELU)
+        tail = torch.zeros((n, hh, ww, 8), dtype=torch.bfloat16, device=dev)
+        oc = self.gen.out_channels
+        P["conv_last"].fwd(hr, nf, 0, hh, ww, tail, 8, 0, n)
+        nchw_to_nhwc(elev.contiguous().float(), tail, 8, oc)
+        nchw_to_nhwc(mask.contiguous().float(), tail, 8, oc + 1)
+        s1 = _bf16((n, hh, ww, 64), dev)
+        P["srcnn.conv1"].fwd(tail, 8, 0, hh, ww, s1, 64, 0, n, act=ACT_RELU)
+        s2 = _bf16((n, hh, ww, 32), dev)
+        P["srcnn.conv2"].fwd(s1, 64, 0, hh, ww, s2, 32, 0, n, act=ACT_RELU)
+        out = torch.empty((n, oc, hh, ww), dtype=torch.float32, device=dev)
+        if oc == 1:
+            P["srcnn.conv3"].fwd(s2, 32, 0, hh, ww, out, 1, 0, n, out_mode=OUT_F32)
+        else:
+            tmp = _f32((n, hh, ww, oc), dev)
+            P["srcnn.conv3"].fwd(s2, 32, 0, hh, ww, tmp, oc, 0, n, out_mode=OUT_F32)
+            out.copy_(tmp.permute(0, 3, 1, 2))
+        saved = None
+        if keep:
+            saved = dict(n=n, h=h, w=w, hh=hh, ww=ww, lr=lr, dense=dense, fea2=fea2, u1=u1, u2=u2, hr=hr, tail=tail, s1=s1, s2=s2)
+        return out, saved
+
+    # ------------------------------------------------------------------ backward
+    def backward(self, gout: Tensor, sv: dict, accumulate: bool) -> None:
+        P = self.plans
+        n, h, w, hh, ww = sv["n"], sv["h"], sv["w"], sv["hh"], sv["ww"]
+        dev = gout.device
+        nf, gc, dc, nb = self.nf, self.gc, self.dc, self.nb
+        sf = self.gen.scale_factor
+        h2, w2 = 2 * h, 2 * w
+        acc = accumulate
+        ws = self.ws
+        oc = self.gen.out_channels
+        assert oc == 1, "native backward implemented for out_channels=1 (the climate config)"
+        npx_hr = n * hh * ww
+        npx_lr = n * h * w
+        gout = gout.contiguous().float()
+        gbig = self._scratch("gbig", (n, hh, ww, nf), torch.float32, dev)
+        dzbig = self._scratch("dzbig", (n, hh, ww, nf), torch.bfloat16, dev)
+        dz8 = self._scratch("dz8", (n, hh, ww, 8), torch.bfloat16, dev)
+        # ---- SRCNN tail (srcnn.py:13-18)
+        act_grad(npx_hr, 1, gout, 1, 0, None, 0, 0, ACT_NONE, dz8, 8)
+        P["srcnn.conv3"].wgrad(sv["s2"], 32, 0, hh, ww, dz8, 8, n, ws, acc)
+        g32 = self._scratch("g32", (n, hh, ww, 32), torch.float32, dev)
+        P["srcnn.conv3"].dgrad(dz8, 8, hh, ww, g32, 32, 0, n)
+        dz32 = self._scratch("dz32", (n, hh, ww, 32), torch.bfloat16, dev)
+        act_grad(npx_hr, 32, g32, 32, 0, sv["s2"], 32, 0, ACT_RELU, dz32, 32)
+        P["srcnn.conv2"].wgrad(sv["s1"], 64, 0, hh, ww, dz32, 32, n, ws, acc)
+        P["srcnn.conv2"].dgrad(dz32, 32, hh, ww, gbig, nf, 0, n)
+        act_grad(npx_hr, 64, gbig, nf, 0, sv["s1"], 64, 0, ACT_RELU, dzbig, 64)
+        P["srcnn.conv1"].wgrad(sv["tail"], 8, 0, hh, ww, dzbig, 64, n, ws, acc)
+        gtail = self._scratch("gtail", (n, hh, ww, 8), torch.float32, dev)
+        P["srcnn.conv1"].dgrad(dzbig, 64, hh, ww, gtail, 8, 0, n, cout_t=1)  # only d(out) is needed
+        # ---- conv_last / HRconv (esrgan.py:99)
+        act_grad(npx_hr, 1, gtail, 8, 0, None, 0, 0, ACT_NONE, dz8, 8)
+        P["conv_last"].wgrad(sv["hr"], nf, 0, hh, ww, dz8, 8, n, ws, acc)
+        P["conv_last"].dgrad(dz8, 8, hh, ww, gbig, nf, 0, n)
+        act_grad(npx_hr, nf, gbig, nf, 0, sv["hr"], nf, 0, ACT_LRELU, dzbig, nf)
+        P["HRconv"].wgrad(sv["u2"], nf, 0, hh, ww, dzbig, nf, n, ws, acc)
+        P["HRconv"].dgrad(dzbig, nf, hh, ww, gbig, nf, 0, n)
+        # ---- upsampling (esrgan.py:94-97)
+        g_u1 = self._scratch("g_u1", (n, h2, w2, nf), torch.float32, dev)
+        dz_u1 = self._scratch("dz_u1", (n, h2, w2, nf), torch.bfloat16, dev)
+        if sf == 4:
+            act_grad(npx_hr, nf, gbig, nf, 0, sv["u2"], nf, 0, ACT_LRELU, dzbig, nf)
+            P["upconv2"].wgrad(sv["u1"], nf, 0, h2, w2, dzbig, nf, n, ws, acc, up=2)
+            P["upconv2"].dgrad(dzbig, nf, hh, ww, g_u1, nf, 0, n, down2=True)
+            act_grad(n * h2 * w2, nf, g_u1, nf, 0, sv["u1"], nf, 0, ACT_LRELU, dz_u1, nf)
+        else:
+            act_grad(npx_hr, nf, gbig, nf, 0, sv["u1"], nf, 0, ACT_LRELU, dz_u1, nf)
+        g_fea2 = self._scratch("g_fea2", (n, h, w, nf), torch.float32, dev)
+        P["upconv1"].wgrad(sv["fea2"], nf, 0, h, w, dz_u1, nf, n, ws, acc, up=2)
+        P["upconv1"].dgrad(dz_u1, nf, h2, w2, g_fea2, nf, 0, n, down2=True)
+        # ---- trunk_conv + global skip (esrgan.py:90-91)
+        dz64 = self._scratch("dz64", (n, h, w, nf), torch.bfloat16, dev)
+        dz16 = self._scratch("dz16", (n, h, w, gc), torch.bfloat16, dev)
+        act_grad(npx_lr, nf, g_fea2, nf, 0, None, 0, 0, ACT_NONE, dz64, nf)
+        dense = sv["dense"]
+        P["trunk_conv"].wgrad(dense[3 * nb], dc, 0, h, w, dz64, nf, n, ws, acc)
+        gX = self._scratch("gA", (n, h, w, dc), torch.float32, dev)
+        gY = self._scratch("gB", (n, h, w, dc), torch.float32, dev)
+        gskip = self._scratch("gskip", (n, h, w, nf), torch.float32, dev)
+        P["trunk_conv"].dgrad(dz64, nf, h, w, gX, dc, 0, n)
+        # ---- RRDB trunk, reverse (esrgan.py:32-54)
+        for i in reversed(range(3 * nb)):
+            blk, r = divmod(i, 3)
+            a_o = 1.0
+            if r == 2:  # output of RRDB blk: out*0.2 + x
+                axpby(npx_lr, nf, 1.0, gX, dc, 0, 0.0, gskip, nf, 0)
+                a_o = 0.2
+            axpby(npx_lr, nf, a_o, gX, dc, 0, 0.0, gY, dc, 0)
+            if r == 0:
+                axpby(npx_lr, nf, 1.0, gskip, nf, 0, 1.0, gY, dc, 0)
+            axpby(npx_lr, dc - nf, 0.0, None, 0, 0, 0.0, gY, dc, nf)
+            act_grad(npx_lr, nf, gX, dc, 0, None, 0, 0, ACT_NONE, dz64, nf, scale=0.2 * a_o)
+            src = dense[i]
+            c5 = P[self.rdb_name(blk, r + 1, 5)]
+            c5.wgrad(src, dc, 0, h, w, dz64, nf, n, ws, acc)
+            c5.dgrad(dz64, nf, h, w, gY, dc, 0, n, accumulate=True)
+            for c in (4, 3, 2, 1):
+                co = nf + (c - 1) * gc
+                act_grad(npx_lr, gc, gY, dc, co, src, dc, co, ACT_LRELU, dz16, gc)
+                pc = P[self.rdb_name(blk, r + 1, c)]
+                pc.wgrad(src, dc, 0, h, w, dz16, gc, n, ws, acc)
+                pc.dgrad(dz16, gc, h, w, gY, dc, 0, n, accumulate=True)
+            gX, gY = gY, gX
+        # ---- conv_first: grad wrt fea = trunk path + global skip
+        axpby(npx_lr, nf, 1.0, g_fea2, nf, 0, 1.0, gX, dc, 0)
+        act_grad(npx_lr, nf, gX, dc, 0, None, 0, 0, ACT_NONE, dz64, nf)
+        P["conv_first"].wgrad(sv["lr"], self.cin_pad, 0, h, w, dz64, nf, n, ws, acc)
+
+
+def axpby_bf16_copy(src, dst, npix, c, src_cs):
+    """Copy channels [0, c) of an NHWC bf16 buffer (inference path only)."""
+    dst.copy_(src.view(-1, src_cs)[:, :c].reshape(dst.shape))
+
+
+class _GeneratorFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, elev, mask, engine_box, *params):
+        engine, keep = engine_box  # grad mode is off inside Function.forward: decided by the caller
+        out, saved = engine.forward(x, elev, mask, keep=keep)
+        ctx.engine = engine
+        ctx.saved = saved
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        engine = ctx.engine
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            raise NotImplementedError("gradient w.r.t. the generator inputs is not implemented (never needed by the task)")
+        if ctx.saved is None:
+            raise RuntimeError("generator forward ran without saving activations")
+        gen = engine.gen
+        acc = gen.grads_as_views()
+        engine.bind_grads()
+        engine.backward(gout, ctx.saved, accumulate=acc)
+        ctx.saved = None
+        return (None, None, None, None) + tuple(None for _ in range(len(ctx.needs_input_grad) - 4))
+
+
+class ESRGANGenerator(FlatParamsMixin, nn.Module):
+    def __init__(self, in_channels: int = 3, out_channels: int = 3, nf: int = 64, nb: int = 23, gc: int = 32,
+                 scaling_factor: int = 4, **kwargs):
+        super().__init__()
+        self.scale_factor = scaling_factor
+        self.in_channels, self.out_channels, self.nf, self.nb, self.gc = in_channels, out_channels, nf, nb, gc
+        self.conv_first = nn.Conv2d(in_channels, nf, 3, 1, 1, bias=True)
+        self.RRDB_trunk = nn.Sequential(*[ResidualInResidualDenseBlock(nf=nf, gc=gc) for _ in range(nb)])
+        self.trunk_conv = nn.Conv2d(nf, nf, 3, 1, 1, bias=True)
+        self.upconv1 = nn.Conv2d(nf, nf, 3, 1, 1, bias=True)
+        if self.scale_factor == 4:
+            self.upconv2 = nn.Conv2d(nf, nf, 3, 1, 1, bias=True)
+        self.HRconv = nn.Conv2d(nf, nf, 3, 1, 1, bias=True)
+        self.conv_last = nn.Conv2d(nf, out_channels, 3, 1, 1, bias=True)
+        self.lrelu = nn.LeakyReLU(negative_slope=0.2, inplace=True)
+        self.srcnn = SRCNN(in_channels=3, out_channels=out_channels)
+        self._flatten()
+        object.__setattr__(self, "_engine", None)
+
+    def _on_flat_moved(self):
+        object.__setattr__(self, "_engine", None)
+
+    def engine(self) -> _Engine:
+        self._ensure_flat()
+        if self._engine is None or self._engine.gen is not self:
+            object.__setattr__(self, "_engine", _Engine(self))
+        return self._engine
+
+    def repack_weights(self) -> None:
+        """Refresh the bf16 MFMA weight layouts after an in-place update of the fp32 master weights."""
+        self.engine().repack()
+
+    def forward(self, x: Tensor, elev: Tensor, mask: Tensor) -> Tensor:
+        if not x.is_cuda:
+            raise RuntimeError("climsr_amd.ESRGANGenerator runs on the GPU only (no CPU fallback); move it with .cuda()")
+        eng = self.engine()
+        params = self._flat_params()
+        keep = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+        return _GeneratorFn.apply(x, elev, mask, (eng, keep), *params)
+
+    def _flat_params(self) -> List[nn.Parameter]:
+        return [p for p, _o, _n in self._flat_index]

@@ -1,0 +1,161 @@
+"""Host-side conv layer plans over the HIP C ABI (all arithmetic in libclimsr_hip.so).
+
+``ConvPlan`` holds one nn.Conv2d's geometry: the packed bf16 weight layouts for the forward
+(``wpk``) and for the data gradient (``wpk_t``, transposed + flipped taps), and issues the
+forward / dgrad / wgrad launches on torch's current stream.  Activation buffers are NHWC torch
+tensors (bf16 or fp32) addressed by (channel stride, channel offset).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+
+from . import _lib
+from ._lib import ConvDesc, Epilogue, check, ptr
+
+ACT_NONE, ACT_LRELU, ACT_RELU = 0, 1, 2
+OUT_BF16, OUT_F32, OUT_F32_ADD = 0, 1, 2
+
+
+def round_up(a: int, b: int) -> int:
+    return (a + b - 1) // b * b
+
+
+class ConvPlan:
+    """Geometry + packed weights for one square-kernel conv (``nn.Conv2d``)."""
+
+    def __init__(self, cin_real: int, cout: int, ks: int, stride: int = 1, pad: Optional[int] = None, name: str = ""):
+        lib = _lib.load()
+        self.name = name
+        self.cin_real, self.cout, self.ks, self.stride = cin_real, cout, ks, stride
+        self.pad = ks // 2 if pad is None else pad
+        self.cin = round_up(cin_real, 8)
+        self.cc = lib.climsr_conv_chunk(self.cin, ks, cout)
+        self.kpk = lib.climsr_conv_packed_k(self.cin, ks, self.cc)
+        self.rows = lib.climsr_conv_packed_rows(cout)
+        # transposed conv (data gradient): in = cout (padded to 8), out = cin_real
+        self.cin_t = round_up(cout, 8)
+        self.cout_t = cin_real
+        self.cc_t = lib.climsr_conv_chunk(self.cin_t, ks, self.cout_t)
+        self.kpk_t = lib.climsr_conv_packed_k(self.cin_t, ks, self.cc_t)
+        self.rows_t = lib.climsr_conv_packed_rows(self.cout_t)
+        self.wpk: Optional[torch.Tensor] = None
+        self.wpk_t: Optional[torch.Tensor] = None
+        self.weight: Optional[torch.Tensor] = None  # fp32 OIHW master (a view of the module's flat buffer)
+        self.bias: Optional[torch.Tensor] = None
+        self.gw: Optional[torch.Tensor] = None  # fp32 OIHW weight grad (view of the flat grad buffer)
+        self.gb: Optional[torch.Tensor] = None
+
+    def flops_per_px(self) -> int:
+        return 2 * self.cin_real * self.cout * self.ks * self.ks
+
+    # ---------------------------------------------------------------- packing
+    def bind(self, weight: torch.Tensor, bias: Optional[torch.Tensor], need_t: bool = True) -> None:
+        self.weight, self.bias = weight, bias
+        dev = weight.device
+        if self.wpk is None or self.wpk.device != dev:
+            self.wpk = torch.empty((self.rows, self.kpk), dtype=torch.bfloat16, device=dev)
+            self.wpk_t = torch.empty((self.rows_t, self.kpk_t), dtype=torch.bfloat16, device=dev) if need_t else None
+
+    def pack(self, stream: Optional[int] = None) -> None:
+        lib = _lib.load()
+        s = _lib.stream_ptr() if stream is None else stream
+        w = self.weight
+        assert w is not None and w.dtype == torch.float32 and w.is_contiguous()
+        check(lib.climsr_pack_conv_weight(ptr(w), self.cout, self.cin, self.cin_real, self.cout, self.ks, self.cc, 0,
+                                          ptr(self.wpk), s), f"pack {self.name}")
+        if self.wpk_t is not None:
+            check(lib.climsr_pack_conv_weight(ptr(w), self.cout_t, self.cin_t, self.cout, self.cout_t, self.ks, self.cc_t, 1,
+                                              ptr(self.wpk_t), s), f"pack_t {self.name}")
+
+    # ---------------------------------------------------------------- launches
+    def out_hw(self, in_h: int, in_w: int, up: int = 1):
+        h = (in_h * up + 2 * self.pad - self.ks) // self.stride + 1
+        w = (in_w * up + 2 * self.pad - self.ks) // self.stride + 1
+        return h, w
+
+    def fwd(self, x: torch.Tensor, x_cs: int, x_co: int, in_h: int, in_w: int, y: torch.Tensor, y_cs: int, y_co: int,
+            n: int, up: int = 1, act: int = ACT_NONE, slope: float = 0.2, use_bias: bool = True,
+            res1: Optional[torch.Tensor] = None, alpha1: float = 1.0, res1_cs: int = 0, res1_co: int = 0,
+            res2: Optional[torch.Tensor] = None, alpha2: float = 1.0, res2_cs: int = 0, res2_co: int = 0,
+            out_mode: int = OUT_BF16) -> None:
+        oh, ow = self.out_hw(in_h, in_w, up)
+        d = ConvDesc(n, in_h, in_w, self.cin, x_cs, x_co, up, self.ks, self.stride, self.pad, oh, ow, self.cout, y_cs, y_co,
+                     self.cc)
+        ep = Epilogue(act, slope, alpha1, ptr(res1), res1_cs, res1_co, alpha2, ptr(res2), res2_cs, res2_co, out_mode, 0)
+        b = ptr(self.bias) if (use_bias and self.bias is not None) else None
+        check(_lib.load().climsr_conv2d_fwd(ctypes.byref(d), ptr(x), ptr(self.wpk), b, ctypes.byref(ep), ptr(y),
+                                            _lib.stream_ptr()), f"conv fwd {self.name}")
+
+    def dgrad(self, dz: torch.Tensor, dz_cs: int, out_h: int, out_w: int, g: torch.Tensor, g_cs: int, g_co: int, n: int,
+              accumulate: bool = False, down2: bool = False, cout_t: Optional[int] = None) -> None:
+        """Data gradient of a stride-1 conv: g[:, :, :, g_co:g_co+cin_real] (+)= conv^T(dz) (fp32).  With down2 the
+        result is summed over 2x2 pixel blocks (backward of the nearest x2 upsample feeding this conv)."""
+        assert self.stride == 1, "dgrad kernel covers stride-1 convs"
+        ct = self.cout_t if cout_t is None else cout_t
+        pad_t = self.ks - 1 - self.pad
+        d = ConvDesc(n, out_h, out_w, self.cin_t, dz_cs, 0, 1, self.ks, 1, pad_t, out_h, out_w, ct, g_cs, g_co, self.cc_t)
+        ep = Epilogue(0, 0.0, 1.0, None, 0, 0, 1.0, None, 0, 0, OUT_F32_ADD if accumulate else OUT_F32, 1 if down2 else 0)
+        check(_lib.load().climsr_conv2d_fwd(ctypes.byref(d), ptr(dz), ptr(self.wpk_t), None, ctypes.byref(ep), ptr(g),
+                                            _lib.stream_ptr()), f"conv dgrad {self.name}")
+
+    def wgrad_desc(self, n, in_h, in_w, x_cs, x_co, up):
+        oh, ow = self.out_hw(in_h, in_w, up)
+        return ConvDesc(n, in_h, in_w, self.cin, x_cs, x_co, up, self.ks, self.stride, self.pad, oh, ow, self.cout, 0, 0,
+                        self.cc)
+
+    def wgrad(self, x: torch.Tensor, x_cs: int, x_co: int, in_h: int, in_w: int, dz: torch.Tensor, dz_cs: int, n: int,
+              workspace: "Workspace", accumulate: bool, up: int = 1) -> None:
+        """Weight/bias gradient into self.gw / self.gb (fp32 OIHW)."""
+        lib = _lib.load()
+        d = self.wgrad_desc(n, in_h, in_w, x_cs, x_co, up)
+        ns = lib.climsr_conv2d_wgrad_splits(ctypes.byref(d))
+        need = lib.climsr_conv2d_wgrad_workspace(ctypes.byref(d), ns)
+        ws = workspace.get(need, x.device)
+        rows_c = need // (ns * (self.cin * self.ks * self.ks + 1))  # co_rows
+        part = ws
+        bpart = ws[ns * rows_c * self.cin * self.ks * self.ks:]
+        s = _lib.stream_ptr()
+        has_b = self.bias is not None and self.gb is not None
+        check(lib.climsr_conv2d_wgrad(ctypes.byref(d), ptr(x), ptr(dz), dz_cs, ptr(part), ptr(bpart) if has_b else None, ns, s),
+              f"conv wgrad {self.name}")
+        check(lib.climsr_conv2d_wgrad_reduce(ptr(part), ptr(bpart) if has_b else None, ns, self.cout, self.cin_real, self.cin,
+                                             self.ks, ptr(self.gw), ptr(self.gb) if has_b else None,
+                                             1 if accumulate else 0, s), f"wgrad reduce {self.name}")
+
+
+class Workspace:
+    """Grow-only fp32 scratch buffer (wgrad split partials)."""
+
+    def __init__(self):
+        self.buf: Optional[torch.Tensor] = None
+
+    def get(self, nfloats: int, device) -> torch.Tensor:
+        if self.buf is None or self.buf.numel() < nfloats or self.buf.device != device:
+            self.buf = torch.empty(max(nfloats, 1 << 20), dtype=torch.float32, device=device)
+        return self.buf
+
+
+def act_grad(npix: int, c_real: int, g: torch.Tensor, g_cs: int, g_co: int, y: Optional[torch.Tensor], y_cs: int, y_co: int,
+             act: int, dz: torch.Tensor, dz_cs: int, scale: float = 1.0, slope: float = 0.2) -> None:
+    check(_lib.load().climsr_act_grad(npix, c_real, ptr(g), g_cs, g_co, ptr(y), y_cs, y_co, act, slope, scale, ptr(dz), dz_cs,
+                                      _lib.stream_ptr()), "act_grad")
+
+
+def axpby(npix: int, c: int, a: float, x: Optional[torch.Tensor], x_cs: int, x_co: int, b: float, y: torch.Tensor, y_cs: int,
+          y_co: int) -> None:
+    check(_lib.load().climsr_axpby_f32(npix, c, a, ptr(x), x_cs, x_co, b, ptr(y), y_cs, y_co, _lib.stream_ptr()), "axpby")
+
+
+def nchw_to_nhwc(src: torch.Tensor, dst: torch.Tensor, cs: int, co: int) -> None:
+    n, c, h, w = src.shape
+    assert src.dtype == torch.float32 and src.is_contiguous()
+    check(_lib.load().climsr_nchw_to_nhwc_bf16(ptr(src), n, c, h, w, ptr(dst), cs, co, _lib.stream_ptr()), "nchw_to_nhwc")
+
+
+def nhwc_to_nchw(src: torch.Tensor, n: int, c: int, h: int, w: int, cs: int, co: int, dst: torch.Tensor) -> None:
+    is_bf16 = 1 if src.dtype == torch.bfloat16 else 0
+    check(_lib.load().climsr_nhwc_to_nchw_f32(ptr(src), is_bf16, n, c, h, w, cs, co, ptr(dst), _lib.stream_ptr()),
+          "nhwc_to_nchw")

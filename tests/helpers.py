@@ -39,3 +39,29 @@ def psnr(a, b, data_range=None):
         data_range = float(b.max() - b.min())
     mse = float(((a - b) ** 2).mean())
     return float("inf") if mse == 0 else 10 * np.log10(data_range ** 2 / mse)
+
+
+def ssim(a, b, data_range=None, kernel=11, sigma=1.5):
+    """Gaussian-window SSIM (torchmetrics defaults: 11x11, sigma 1.5, k1 .01, k2 .03, valid region)."""
+    import torch.nn.functional as F
+
+    a = a.double()
+    b = b.double()
+    if data_range is None:
+        data_range = float(b.max() - b.min())
+    x = torch.arange(kernel, dtype=torch.float64) - (kernel - 1) / 2
+    g = torch.exp(-(x ** 2) / (2 * sigma ** 2))
+    g = g / g.sum()
+    w = (g[:, None] * g[None, :])[None, None].repeat(a.shape[1], 1, 1, 1)
+    c1 = (0.01 * data_range) ** 2
+    c2 = (0.03 * data_range) ** 2
+
+    def f(t):
+        return F.conv2d(t, w, groups=a.shape[1])
+
+    mu_a, mu_b = f(a), f(b)
+    saa = f(a * a) - mu_a ** 2
+    sbb = f(b * b) - mu_b ** 2
+    sab = f(a * b) - mu_a * mu_b
+    m = ((2 * mu_a * mu_b + c1) * (2 * sab + c2)) / ((mu_a ** 2 + mu_b ** 2 + c1) * (saa + sbb + c2))
+    return float(m.mean())

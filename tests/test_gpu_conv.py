@@ -1,0 +1,167 @@
+"""GPU op-level parity: the HIP implicit-GEMM conv (fwd / dgrad / wgrad) through the C ABI vs a
+plain PyTorch fp64 reference of the same op on the same bf16-rounded operands.  The only
+difference left is fp32 MFMA accumulation order, so the bound is tight (rel 1e-5 of the scale
+plus one bf16 ulp where the output is stored in bf16)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+if torch.cuda.is_available():
+    from climsr_amd.ops import (ACT_LRELU, ACT_NONE, ACT_RELU, OUT_BF16, OUT_F32, OUT_F32_ADD, ConvPlan, Workspace, act_grad)
+
+DEV = "cuda"
+
+
+def bf(t):
+    return t.to(torch.bfloat16).to(torch.float32)
+
+
+def to_nhwc(x, cs=None, co=0, dtype=torch.bfloat16):
+    n, c, h, w = x.shape
+    cs = cs or ((c + 7) // 8 * 8)
+    buf = torch.zeros((n, h, w, cs), dtype=dtype, device=DEV)
+    buf[..., co:co + c] = x.permute(0, 2, 3, 1).to(dtype)
+    return buf
+
+
+def from_nhwc(buf, c, co=0):
+    return buf[..., co:co + c].permute(0, 3, 1, 2).float()
+
+
+def make_plan(cin, cout, ks, stride=1, pad=None, seed=0, bias=True):
+    g = torch.Generator().manual_seed(seed)
+    w = (torch.rand((cout, cin, ks, ks), generator=g) * 2 - 1) / (cin * ks * ks) ** 0.5
+    b = (torch.rand((cout,), generator=g) * 2 - 1) * 0.1 if bias else None
+    p = ConvPlan(cin, cout, ks, stride, pad, "t")
+    w_d = w.to(DEV).contiguous()
+    b_d = b.to(DEV) if b is not None else None
+    p.bind(w_d, b_d)
+    p.pack()
+    return p, w, b
+
+
+def check_close(got, want, tol=1e-5, what=""):
+    scale = want.abs().max().item() + 1e-12
+    err = (got.double() - want.double()).abs().max().item()
+    assert err <= tol * scale + 1e-7, f"{what}: max err {err:.3e} vs scale {scale:.3e}"
+
+
+CASES = [
+    # cin, cout, ks, stride, up, n, h, w
+    (64, 16, 3, 1, 1, 2, 20, 24),    # RDB conv1
+    (80, 16, 3, 1, 1, 2, 16, 16),    # RDB conv2 (cin not a multiple of 32)
+    (112, 16, 3, 1, 1, 1, 17, 33),   # RDB conv4, ragged tiles
+    (128, 64, 3, 1, 1, 2, 16, 16),   # RDB conv5
+    (3, 64, 3, 1, 1, 2, 16, 16),     # conv_first (cin padded to 8)
+    (64, 64, 3, 1, 2, 2, 8, 12),     # upconv (nearest x2 on load)
+    (64, 1, 3, 1, 1, 2, 16, 16),     # conv_last (cout 1)
+    (3, 64, 9, 1, 1, 1, 20, 20),     # srcnn conv1
+    (64, 32, 1, 1, 1, 2, 16, 16),    # srcnn conv2
+    (32, 1, 5, 1, 1, 2, 16, 16),     # srcnn conv3
+    (64, 128, 3, 2, 1, 2, 32, 32),   # D stride-2
+    (256, 512, 3, 1, 1, 1, 8, 8),    # D / VGG wide
+]
+
+
+@pytest.mark.parametrize("cin,cout,ks,stride,up,n,h,w", CASES)
+def test_conv_fwd_matches_torch(cin, cout, ks, stride, up, n, h, w):
+    p, wt, b = make_plan(cin, cout, ks, stride)
+    g = torch.Generator().manual_seed(1)
+    x = torch.rand((n, cin, h, w), generator=g) * 2 - 1
+    xb = bf(x)
+    xin = to_nhwc(xb)
+    oh, ow = p.out_hw(h, w, up)
+    cs_out = (cout + 7) // 8 * 8
+    y = torch.zeros((n, oh, ow, cs_out), dtype=torch.float32, device=DEV)
+    p.fwd(xin, xin.shape[-1], 0, h, w, y, cs_out, 0, n, up=up, out_mode=OUT_F32)
+    torch.cuda.synchronize()
+    xr = xb.double()
+    if up == 2:
+        xr = F.interpolate(xr, scale_factor=2, mode="nearest")
+    want = F.conv2d(xr, bf(wt).double(), b.double(), stride=stride, padding=ks // 2)
+    check_close(from_nhwc(y, cout).cpu(), want, what=f"fwd {cin}->{cout} k{ks} s{stride} up{up}")
+
+
+def test_conv_fwd_epilogue_slices_and_residuals():
+    """Dense-buffer slices (read [0,80), write at channel 80) + lrelu, and the RRDB double residual."""
+    n, h, w = 2, 16, 16
+    p, wt, b = make_plan(80, 16, 3)
+    g = torch.Generator().manual_seed(2)
+    dense = torch.rand((n, h, w, 128), generator=g) * 2 - 1
+    dense_d = dense.to(torch.bfloat16).to(DEV)
+    before = dense_d.clone()
+    p.fwd(dense_d, 128, 0, h, w, dense_d, 128, 80, n, act=ACT_LRELU)
+    torch.cuda.synchronize()
+    xr = bf(dense[..., :80]).permute(0, 3, 1, 2).double()
+    want = F.leaky_relu(F.conv2d(xr, bf(wt).double(), b.double(), padding=1), 0.2)
+    got = dense_d[..., 80:96].permute(0, 3, 1, 2).float().cpu()
+    check_close(got, want, tol=1e-2, what="slice write")  # bf16 store
+    assert torch.equal(dense_d[..., :80], before[..., :80]) and torch.equal(dense_d[..., 96:], before[..., 96:])
+    # conv5-style: v = (acc+b)*0.2 + r1; v = v*0.2 + r2
+    p5, w5, b5 = make_plan(128, 64, 3, seed=3)
+    r2 = (torch.rand((n, h, w, 64), generator=g) * 2 - 1).to(torch.bfloat16).to(DEV)
+    out = torch.zeros((n, h, w, 64), dtype=torch.float32, device=DEV)
+    p5.fwd(dense_d, 128, 0, h, w, out, 64, 0, n, res1=dense_d, alpha1=0.2, res1_cs=128, res1_co=0, res2=r2, alpha2=0.2,
+           res2_cs=64, res2_co=0, out_mode=OUT_F32)
+    torch.cuda.synchronize()
+    d = dense_d.float().cpu().permute(0, 3, 1, 2).double()
+    x5 = F.conv2d(d, bf(w5).double(), b5.double(), padding=1)
+    want = (x5 * 0.2 + d[:, :64]) * 0.2 + r2.float().cpu().permute(0, 3, 1, 2).double()
+    check_close(from_nhwc(out, 64).cpu(), want, what="double residual")
+
+
+@pytest.mark.parametrize("cin,cout,ks,up,down", [(64, 16, 3, 1, False), (128, 64, 3, 1, False), (80, 16, 3, 1, False),
+                                                 (64, 64, 3, 2, True), (32, 1, 5, 1, False), (3, 64, 9, 1, False),
+                                                 (64, 32, 1, 1, False), (64, 1, 3, 1, False)])
+def test_conv_dgrad_matches_autograd(cin, cout, ks, up, down):
+    n, h, w = 2, 16, 16
+    p, wt, b = make_plan(cin, cout, ks)
+    g = torch.Generator().manual_seed(4)
+    oh, ow = h * up, w * up
+    dz = bf(torch.rand((n, cout, oh, ow), generator=g) * 2 - 1)
+    dzb = to_nhwc(dz)
+    gx = torch.full((n, h, w, p.cin), 0.5, dtype=torch.float32, device=DEV)
+    p.dgrad(dzb, dzb.shape[-1], oh, ow, gx, p.cin, 0, n, accumulate=True, down2=down)
+    torch.cuda.synchronize()
+    x = torch.zeros((n, cin, h, w), dtype=torch.float64, requires_grad=True)
+    xin = F.interpolate(x, scale_factor=2, mode="nearest") if up == 2 else x
+    y = F.conv2d(xin, bf(wt).double(), None, padding=ks // 2)
+    (gref,) = torch.autograd.grad(y, x, dz.double())
+    check_close(from_nhwc(gx, cin).cpu() - 0.5, gref, tol=2e-5, what="dgrad")
+
+
+@pytest.mark.parametrize("cin,cout,ks,stride,up", [(64, 16, 3, 1, 1), (128, 64, 3, 1, 1), (112, 16, 3, 1, 1), (8, 64, 3, 1, 1),
+                                                   (64, 64, 3, 1, 2), (32, 1, 5, 1, 1), (3, 64, 9, 1, 1), (64, 32, 1, 1, 1),
+                                                   (64, 128, 3, 2, 1), (64, 1, 3, 1, 1)])
+def test_conv_wgrad_matches_autograd(cin, cout, ks, stride, up):
+    n, h, w = 2, 24, 20
+    p, wt, b = make_plan(cin, cout, ks, stride)
+    g = torch.Generator().manual_seed(5)
+    x = bf(torch.rand((n, cin, h, w), generator=g) * 2 - 1)
+    oh, ow = p.out_hw(h, w, up)
+    dz = bf(torch.rand((n, cout, oh, ow), generator=g) * 2 - 1)
+    xb, dzb = to_nhwc(x), to_nhwc(dz)
+    p.gw = torch.zeros_like(p.weight)
+    p.gb = torch.zeros_like(p.bias)
+    p.wgrad(xb, xb.shape[-1], 0, h, w, dzb, dzb.shape[-1], n, Workspace(), accumulate=False, up=up)
+    torch.cuda.synchronize()
+    wr = bf(wt).double().requires_grad_(True)
+    br = b.double().requires_grad_(True)
+    xin = F.interpolate(x.double(), scale_factor=2, mode="nearest") if up == 2 else x.double()
+    y = F.conv2d(xin, wr, br, stride=stride, padding=ks // 2)
+    gw, gb = torch.autograd.grad(y, (wr, br), dz.double())
+    check_close(p.gw.cpu(), gw, tol=2e-5, what="wgrad")
+    check_close(p.gb.cpu(), gb, tol=2e-5, what="bgrad")
+
+
+def test_act_grad():
+    n, h, w = 2, 8, 8
+    g = torch.Generator().manual_seed(6)
+    gr = torch.randn((n, h, w, 128), generator=g)
+    y = (torch.randn((n, h, w, 128), generator=g)).to(torch.bfloat16)
+    dz = torch.zeros((n, h, w, 16), dtype=torch.bfloat16, device=DEV)
+    act_grad(n * h * w, 16, gr.to(DEV), 128, 96, y.to(DEV), 128, 96, ACT_LRELU, dz, 16, scale=0.5)
+    want = gr[..., 96:112] * 0.5 * torch.where(y[..., 96:112].float() > 0, 1.0, 0.2)
+    assert torch.allclose(dz.float().cpu(), bf(want), rtol=0, atol=0)
