@@ -112,11 +112,15 @@ def test_conv_fwd_epilogue_slices_and_residuals():
     check_close(from_nhwc(out, 64).cpu(), want, what="double residual")
 
 
-@pytest.mark.parametrize("cin,cout,ks,up,down", [(64, 16, 3, 1, False), (128, 64, 3, 1, False), (80, 16, 3, 1, False),
-                                                 (64, 64, 3, 2, True), (32, 1, 5, 1, False), (3, 64, 9, 1, False),
-                                                 (64, 32, 1, 1, False), (64, 1, 3, 1, False)])
-def test_conv_dgrad_matches_autograd(cin, cout, ks, up, down):
-    n, h, w = 2, 16, 16
+@pytest.mark.parametrize("cin,cout,ks,up,down,h,w", [(64, 16, 3, 1, False, 16, 16), (128, 64, 3, 1, False, 16, 16),
+                                                     (80, 16, 3, 1, False, 16, 16), (64, 64, 3, 2, True, 16, 16),
+                                                     (32, 1, 5, 1, False, 16, 16), (3, 64, 9, 1, False, 16, 16),
+                                                     (64, 32, 1, 1, False, 16, 16), (64, 1, 3, 1, False, 16, 16),
+                                                     (32, 1, 5, 1, False, 64, 48), (64, 32, 1, 1, False, 64, 64),
+                                                     (3, 64, 9, 1, False, 40, 56), (64, 16, 3, 1, False, 33, 40),
+                                                     (64, 64, 3, 2, True, 24, 40)])
+def test_conv_dgrad_matches_autograd(cin, cout, ks, up, down, h, w):
+    n = 2
     p, wt, b = make_plan(cin, cout, ks)
     g = torch.Generator().manual_seed(4)
     oh, ow = h * up, w * up
