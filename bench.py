@@ -1,0 +1,227 @@
+"""Benchmark: HR MPix/s per training step of 4x ESRGAN SR on synthetic 64->256 tiles (BASELINE.json).
+
+Default workload = BASELINE config 2: RRDB generator (nf 64, nb 11, gc 16; conf/generator/esrgan.yaml)
+L1 pre-training step (pl_generator_pre_training.py:18-33: forward, L1Loss, backward, AdamW,
+OneCycleLR), per-GPU batch 32, bf16 MFMA compute, fp32 master weights / optimiser state.  The whole
+step (forward + loss + backward + AdamW + weight repack) is captured once in a hipGraph and replayed.
+
+Multi-GPU: one process per GPU (torchrun), per-rank seeded tiles (seed 42 + rank), the flat fp32
+gradient buffer is averaged with one RCCL all-reduce per step (DDP semantics), every rank steps its
+own replica.  Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+G_FWD_FLOP_PER_PX = 721_880  # 23,654,563,840 MAC per 64^2 sample / 65,536 HR px * 2
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32, help="per-GPU batch")
+    ap.add_argument("--lr-size", type=int, default=64)
+    ap.add_argument("--nb", type=int, default=11)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    return ap.parse_args()
+
+
+class KernelTimer:
+    """HIP-event timer around individual launches (ops.PROFILER hook), grouped by kernel name."""
+
+    def __init__(self):
+        self.rec = []
+
+    def __call__(self, name, flops, fn):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        self.rec.append((name, flops, s, e))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        agg = {}
+        for name, flops, s, e in self.rec:
+            a = agg.setdefault(name, [0, 0.0, 0])
+            a[0] += 1
+            a[1] += s.elapsed_time(e)
+            a[2] += flops
+        return agg
+
+
+def cpu_baseline(args, hr):
+    """Oracle (PyTorch-CPU fp32 eager) L1-pretrain step on the host cores, bounded sample."""
+    from oracle import climsr_ref as ref
+    from tests.helpers import gen_params
+
+    threads = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(threads)
+    b = 2
+    p = {k: v.float() for k, v in gen_params(args.nb, torch.float32).items()}
+    opt = ref.AdamWState(p, list(p.keys()), lr=1e-4, total_steps=1000)
+    bt = ref.synthetic_batch(b, hr)
+    ref.pretrain_step(p, opt, bt, args.nb)  # warm-up
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        ref.pretrain_step(p, opt, bt, args.nb)
+        n += 1
+        if time.perf_counter() - t0 >= args.cpu_seconds or n >= 50:
+            break
+    dt = (time.perf_counter() - t0) / n
+    return {"value": round(b * hr * hr / 1e6 / dt, 5), "unit": "HR MPix/s", "cores": threads, "kind": "port",
+            "sample": f"oracle L1-pretrain step (fp32 PyTorch-CPU eager), batch {b}, {hr // 4}->{hr}, nb={args.nb}, "
+                      f"{n} steps ({dt * 1e3:.0f} ms/step)"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import climsr_amd  # noqa: F401
+    from climsr_amd import ops
+    from climsr_amd.core.init import init_state, spec_from_shapes
+    from climsr_amd.core.optim import GraphedAdamW
+    from climsr_amd.losses.l1 import l1_loss
+    from climsr_amd.models.esrgan import ESRGANGenerator
+
+    B, lr_size = args.batch, args.lr_size
+    hr = 4 * lr_size
+    g = ESRGANGenerator(in_channels=3, out_channels=1, nf=64, nb=args.nb, gc=16, scale_factor=4)
+    st = init_state(spec_from_shapes({k: tuple(v.shape) for k, v in g.state_dict().items()}))
+    g.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in st.items()})
+    g = g.to(dev)
+    total_steps = max(1000, args.warmup + args.steps + 10)
+    opt = GraphedAdamW(g, lr=1e-4, total_steps=total_steps, weight_decay=1e-4)
+
+    gen = torch.Generator(device="cpu").manual_seed(42 + rank)
+    t = torch.rand((B, 1, hr, hr), generator=gen) * 2 - 1
+    e = torch.rand((B, 1, hr, hr), generator=gen) * 2 - 1
+    m = (torch.rand((B, 1, hr, hr), generator=gen) < 0.7).float()
+    lr = torch.cat([t, e, m], 1)[:, :, ::4, ::4].contiguous()
+    batch = {k: v.to(dev) for k, v in {"lr": lr, "hr": t, "elevation": e, "mask": m}.items()}
+
+    loss_buf = torch.zeros((), device=dev)
+
+    def step():
+        for p in g.parameters():
+            p.grad = None  # zero_grad(set_to_none=True): backward overwrites the flat grad buffer
+        sr = g(batch["lr"], batch["elevation"], batch["mask"])
+        loss = l1_loss(sr, batch["hr"])
+        loss.backward()
+        if world > 1:
+            dist.all_reduce(g._flat_grad, op=dist.ReduceOp.AVG)
+        opt.step()
+        loss_buf.copy_(loss.detach())
+
+    use_graph = not args.no_graph and world == 1
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            step()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    graph = None
+    if use_graph:
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step()
+        run = graph.replay
+    else:
+        run = step
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    ms = elapsed / args.steps * 1e3
+    loss_val = float(loss_buf.item())
+    mpix = world * B * hr * hr / 1e6 / (elapsed / args.steps)
+
+    roof = None
+    step_frac = None
+    flop_step = 3 * G_FWD_FLOP_PER_PX * B * hr * hr  # fwd + dgrad + wgrad
+    step_tflops = flop_step / (ms / 1e3) / 1e12
+    step_frac = step_tflops / PEAK_BF16_TFLOPS
+    kern = {}
+    if not args.no_kernel_timing:
+        timer = KernelTimer()
+        ops.PROFILER = timer
+        step()
+        ops.PROFILER = None
+        agg = timer.summary()
+        name, (cnt, tot_ms, flops) = max(agg.items(), key=lambda kv: kv[1][1])
+        avg_ms = tot_ms / cnt
+        achieved = flops / cnt / (avg_ms / 1e3) / 1e12
+        roof = {"bound": "mfma", "kernel": name, "launches_per_step": cnt, "avg_launch_us": round(avg_ms * 1e3, 2),
+                "flop_per_launch": flops // cnt, "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None}
+        kern = {k: {"launches": v[0], "ms_total": round(v[1], 3), "tflops": round(v[2] / (v[1] / 1e3) / 1e12, 1)}
+                for k, v in sorted(agg.items(), key=lambda kv: -kv[1][1])}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, hr)
+
+    if rank == 0:
+        out = {
+            "metric": "HR MPix/s per training step (4x SR, 64->256 tiles)",
+            "value": round(mpix, 3), "unit": "HR MPix/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (seed 42+rank: U(-1,1) temp/elev, Bernoulli(0.7) mask, LR = HR[::4,::4]); deterministic init",
+            "config": {"workload": "config 2: RRDB generator L1 pre-training step (fwd+L1+bwd+AdamW+OneCycleLR)",
+                       "generator": f"ESRGAN nf64 nb{args.nb} gc16 x4", "global_batch": world * B, "per_gpu_batch": B,
+                       "lr_tile": lr_size, "hr_tile": hr, "parallelism": f"dp{world}", "hip_graph": use_graph},
+            "roofline": roof,
+            "step_mfma": {"algorithmic_tflop_per_step": round(flop_step / 1e12, 3), "achieved_tflops": round(step_tflops, 1),
+                          "frac": round(step_frac, 4)},
+            "cpu_baseline": cpu,
+            "loss_last": round(loss_val, 6),
+            "kernels": kern,
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

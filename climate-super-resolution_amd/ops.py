@@ -23,6 +23,37 @@ def round_up(a: int, b: int) -> int:
     return (a + b - 1) // b * b
 
 
+# Optional launch observer (bench.py's per-kernel HIP-event timer).  Called as
+# PROFILER(kernel_name, algorithmic_flops, launch_fn); must call launch_fn() exactly once.
+PROFILER = None
+
+
+def _fwd_nt(out_c: int) -> int:
+    nt = (out_c + 15) // 16
+    return 4 if nt >= 3 else nt
+
+
+def fwd_kernel_name(out_c: int) -> str:
+    return f"conv_fwd_kernel<2, {_fwd_nt(out_c)}>"
+
+
+def wgrad_kernel_name(out_c: int, ks: int) -> str:
+    rows = round_up(out_c, 16)
+    ntc = 4 if rows >= 64 else (2 if rows >= 32 else 1)
+    k2 = ks * ks
+    tb = 9 if k2 >= 9 else (5 if k2 >= 5 else 1)
+    if k2 == 25:
+        tb = 5
+    return f"conv_wgrad_kernel<{ntc}, {tb}>"
+
+
+def _run(name, flops, fn):
+    if PROFILER is None:
+        fn()
+    else:
+        PROFILER(name, flops, fn)
+
+
 class ConvPlan:
     """Geometry + packed weights for one square-kernel conv (``nn.Conv2d``)."""
 
@@ -86,8 +117,10 @@ class ConvPlan:
                      self.cc)
         ep = Epilogue(act, slope, alpha1, ptr(res1), res1_cs, res1_co, alpha2, ptr(res2), res2_cs, res2_co, out_mode, 0)
         b = ptr(self.bias) if (use_bias and self.bias is not None) else None
-        check(_lib.load().climsr_conv2d_fwd(ctypes.byref(d), ptr(x), ptr(self.wpk), b, ctypes.byref(ep), ptr(y),
-                                            _lib.stream_ptr()), f"conv fwd {self.name}")
+        flops = 2 * self.cin_real * self.cout * self.ks * self.ks * n * oh * ow
+        _run(fwd_kernel_name(self.cout), flops, lambda: check(
+            _lib.load().climsr_conv2d_fwd(ctypes.byref(d), ptr(x), ptr(self.wpk), b, ctypes.byref(ep), ptr(y), _lib.stream_ptr()),
+            f"conv fwd {self.name}"))
 
     def dgrad(self, dz: torch.Tensor, dz_cs: int, out_h: int, out_w: int, g: torch.Tensor, g_cs: int, g_co: int, n: int,
               accumulate: bool = False, down2: bool = False, cout_t: Optional[int] = None) -> None:
@@ -98,8 +131,10 @@ class ConvPlan:
         pad_t = self.ks - 1 - self.pad
         d = ConvDesc(n, out_h, out_w, self.cin_t, dz_cs, 0, 1, self.ks, 1, pad_t, out_h, out_w, ct, g_cs, g_co, self.cc_t)
         ep = Epilogue(0, 0.0, 1.0, None, 0, 0, 1.0, None, 0, 0, OUT_F32_ADD if accumulate else OUT_F32, 1 if down2 else 0)
-        check(_lib.load().climsr_conv2d_fwd(ctypes.byref(d), ptr(dz), ptr(self.wpk_t), None, ctypes.byref(ep), ptr(g),
-                                            _lib.stream_ptr()), f"conv dgrad {self.name}")
+        flops = 2 * self.cout * ct * self.ks * self.ks * n * out_h * out_w
+        _run(fwd_kernel_name(ct), flops, lambda: check(
+            _lib.load().climsr_conv2d_fwd(ctypes.byref(d), ptr(dz), ptr(self.wpk_t), None, ctypes.byref(ep), ptr(g),
+                                          _lib.stream_ptr()), f"conv dgrad {self.name}"))
 
     def wgrad_desc(self, n, in_h, in_w, x_cs, x_co, up):
         oh, ow = self.out_hw(in_h, in_w, up)
@@ -119,8 +154,10 @@ class ConvPlan:
         bpart = ws[ns * rows_c * self.cin * self.ks * self.ks:]
         s = _lib.stream_ptr()
         has_b = self.bias is not None and self.gb is not None
-        check(lib.climsr_conv2d_wgrad(ctypes.byref(d), ptr(x), ptr(dz), dz_cs, ptr(part), ptr(bpart) if has_b else None, ns, s),
-              f"conv wgrad {self.name}")
+        flops = 2 * self.cin_real * self.cout * self.ks * self.ks * n * d.out_h * d.out_w
+        _run(wgrad_kernel_name(self.cout, self.ks), flops, lambda: check(
+            lib.climsr_conv2d_wgrad(ctypes.byref(d), ptr(x), ptr(dz), dz_cs, ptr(part), ptr(bpart) if has_b else None, ns, s),
+            f"conv wgrad {self.name}"))
         check(lib.climsr_conv2d_wgrad_reduce(ptr(part), ptr(bpart) if has_b else None, ns, self.cout, self.cin_real, self.cin,
                                              self.ks, ptr(self.gw), ptr(self.gb) if has_b else None,
                                              1 if accumulate else 0, s), f"wgrad reduce {self.name}")
