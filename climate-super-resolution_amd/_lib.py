@@ -32,6 +32,11 @@ class Epilogue(ctypes.Structure):
                 ("down2", ctypes.c_int32)]
 
 
+class PackDesc(ctypes.Structure):
+    _fields_ = [("w", c_void_p), ("out", c_void_p)] + [(n, ctypes.c_int32) for n in (
+        "out_c", "in_c", "in_c_real", "out_c_real", "ks", "cc", "tflip", "reserved")]
+
+
 P = ctypes.POINTER
 # name -> (restype, argtypes); must match include/climsr_hip.h exactly (tests/test_abi.py checks the symbols)
 SIGNATURES = {
@@ -41,6 +46,7 @@ SIGNATURES = {
     "climsr_conv_packed_k": (c_int, [c_int, c_int, c_int]),
     "climsr_conv_packed_rows": (c_int, [c_int]),
     "climsr_pack_conv_weight": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "climsr_pack_conv_weights_batched": (c_int, [c_void_p, c_int, c_int64, c_void_p]),
     "climsr_conv2d_fwd": (c_int, [P(ConvDesc), c_void_p, c_void_p, c_void_p, P(Epilogue), c_void_p, c_void_p]),
     "climsr_conv2d_wgrad": (c_int, [P(ConvDesc), c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "climsr_conv2d_wgrad_reduce": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
@@ -52,6 +58,8 @@ SIGNATURES = {
     "climsr_nchw_to_nhwc_bf16": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p]),
     "climsr_nhwc_to_nchw_f32": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "climsr_axpby_f32": (c_int, [c_int64, c_int, c_float, c_void_p, c_int, c_int, c_float, c_void_p, c_int, c_int, c_void_p]),
+    "climsr_rdb_bwd_init": (c_int, [c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_int,
+                                    c_void_p]),
     "climsr_l1_loss": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "climsr_l1_loss_grad": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "climsr_adamw_hparams": (c_int, [c_void_p, c_int, c_double, c_double, c_double, c_double, c_double, c_double, c_double,

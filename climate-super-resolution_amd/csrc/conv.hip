@@ -52,6 +52,12 @@ static int fwd_nt(int out_c) {
   return nt > 4 ? 4 : (nt == 3 ? 4 : nt);
 }
 
+__device__ inline int climsr_rows_dev(int out_c) {
+  int nt = (out_c + 15) / 16;
+  nt = nt > 4 ? 4 : (nt == 3 ? 4 : nt);
+  return (out_c + nt * 16 - 1) / (nt * 16) * (nt * 16);
+}
+
 static void fwd_geom(int in_c, int ks, int stride, int out_c, int cc, int mw, FwdGeom* g) {
   g->mw = mw;
   g->th = 4 * mw;
@@ -137,6 +143,43 @@ extern "C" int climsr_pack_conv_weight(const float* w, int out_c, int in_c, int 
   hipLaunchKernelGGL(pack_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, w, rows, kpk, in_c_real,
                      out_c_real, ks, cc, kcpad, transpose_flip, wpk);
   return check_launch("pack_conv_weight");
+}
+
+// Batched form: one launch packs every conv of a network (blockIdx.y = descriptor).
+__global__ void pack_batched_kernel(const ClimsrPackDesc* __restrict__ descs) {
+  const ClimsrPackDesc d = descs[blockIdx.y];
+  const int rows = climsr_rows_dev(d.out_c);
+  const int kcpad = (d.ks * d.ks * d.cc + 31) / 32 * 32;
+  const int kpk = (d.in_c + d.cc - 1) / d.cc * kcpad;
+  const long total = (long)rows * kpk;
+  const int kk2 = d.ks * d.ks;
+  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    int co = (int)(idx / kpk);
+    int kk = (int)(idx % kpk);
+    int j = kk / kcpad;
+    int kr = kk % kcpad;
+    int tap = kr / d.cc;
+    int c = j * d.cc + kr % d.cc;
+    float v = 0.f;
+    if (co < d.out_c_real && tap < kk2 && c < d.in_c_real) {
+      int ky = tap / d.ks, kx = tap % d.ks;
+      if (!d.tflip) v = d.w[(((long)co * d.in_c_real + c) * d.ks + ky) * d.ks + kx];
+      else v = d.w[(((long)c * d.out_c_real + co) * d.ks + (d.ks - 1 - ky)) * d.ks + (d.ks - 1 - kx)];
+    }
+    d.out[idx] = f2bf(v);
+  }
+}
+
+extern "C" int climsr_pack_conv_weights_batched(const ClimsrPackDesc* descs, int ndesc, int64_t max_elems, void* stream) {
+  if (!descs || ndesc <= 0 || ndesc > 65535) {
+    set_error("pack_conv_weights_batched: bad args");
+    return CLIMSR_EINVAL;
+  }
+  int gx = ceil_div(max_elems, 256);
+  if (gx > 128) gx = 128;
+  if (gx < 1) gx = 1;
+  hipLaunchKernelGGL(pack_batched_kernel, dim3(gx, ndesc), dim3(256), 0, (hipStream_t)stream, descs);
+  return check_launch("pack_conv_weights_batched");
 }
 
 // ------------------------------------------------------------------------------------------
@@ -625,7 +668,7 @@ extern "C" int climsr_conv2d_wgrad_splits(const ClimsrConvDesc* d) {
   WgPlan w;
   wg_plan(d, &w);
   int base = w.ntapb * w.ncib * w.ncob;
-  int ns = ceil_div(1024, base);
+  int ns = ceil_div(512, base);
   if (ns > w.ntiles) ns = w.ntiles;
   if (ns < 1) ns = 1;
   return ns;
@@ -682,25 +725,41 @@ extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, c
   return CLIMSR_EINVAL;
 }
 
-__global__ void wgrad_reduce_kernel(const float* __restrict__ part, const float* __restrict__ bpart, int nsplit, int out_c,
-                                    int in_c_real, int in_c, int ks2, int co_rows, int kw, float* __restrict__ wg,
-                                    float* __restrict__ bg, int accumulate) {
-  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+// 256 threads = 32 consecutive outputs x 8 split groups (8 independent load chains per output,
+// coalesced 128 B rows), combined in a fixed order through LDS: deterministic.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, const float* __restrict__ bpart,
+                                                          int nsplit, int out_c, int in_c_real, int in_c, int ks2, int co_rows,
+                                                          int kw, float* __restrict__ wg, float* __restrict__ bg, int accumulate) {
+  __shared__ float red[8][33];
+  const int lane = threadIdx.x & 31;
+  const int sg = threadIdx.x >> 5;
+  long idx = (long)blockIdx.x * 32 + lane;
   long nw = (long)out_c * in_c_real * ks2;
+  long total = nw + (bg ? out_c : 0);
+  const float* src = nullptr;
+  long sstride = 0;
   if (idx < nw) {
     int co = (int)(idx / ((long)in_c_real * ks2));
     int rem = (int)(idx % ((long)in_c_real * ks2));  // ci*ks2 + tap
-    const float* src = part + (long)co * kw + rem;
-    float s = 0.f;
-    for (int sp = 0; sp < nsplit; ++sp) s += src[(long)sp * co_rows * kw];
-    if (accumulate) wg[idx] += s;
-    else wg[idx] = s;
-  } else if (bg && idx < nw + out_c) {
-    int co = (int)(idx - nw);
-    float s = 0.f;
-    for (int sp = 0; sp < nsplit; ++sp) s += bpart[(long)sp * co_rows + co];
-    if (accumulate) bg[co] += s;
-    else bg[co] = s;
+    src = part + (long)co * kw + rem;
+    sstride = (long)co_rows * kw;
+  } else if (idx < total) {
+    src = bpart + (idx - nw);
+    sstride = co_rows;
+  }
+  float acc = 0.f;
+  if (src) {
+    for (int sp = sg; sp < nsplit; sp += 8) acc += src[(long)sp * sstride];
+  }
+  red[sg][lane] = acc;
+  __syncthreads();
+  if (sg == 0 && idx < total) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t += red[i][lane];
+    float* dst = (idx < nw) ? (wg + idx) : (bg + (idx - nw));
+    if (accumulate) *dst += t;
+    else *dst = t;
   }
 }
 
@@ -716,7 +775,7 @@ extern "C" int climsr_conv2d_wgrad_reduce(const float* partial, const float* bia
   int ks2 = ks * ks;
   int kw = in_c * ks2;
   long total = (long)out_c * in_c_real * ks2 + (bias_grad ? out_c : 0);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, partial, bias_partial,
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ceil_div(total, 32)), dim3(256), 0, (hipStream_t)stream, partial, bias_partial,
                      nsplit, out_c, in_c_real, in_c, ks2, co_rows, kw, wgrad, bias_grad, accumulate);
   return check_launch("conv2d_wgrad_reduce");
 }

@@ -12,32 +12,52 @@ using namespace climsr;
 // ------------------------------------------------------------------------------------------
 __global__ void act_grad_kernel(long npix, int c_real, const float* __restrict__ g, int gcs, int gco,
                                 const uint16_t* __restrict__ y, int ycs, int yco, int act, float slope, float scale,
-                                uint16_t* __restrict__ dz, int dzcs) {
-  // one thread per (pixel, group of 8 dz channels)
+                                uint16_t* __restrict__ dz, int dzcs, int vec) {
+  // one thread per (pixel, group of 8 dz channels); vec: g/y slices are 16 B aligned and c_real % 8 == 0
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   int groups = dzcs / 8;
   if (idx >= npix * groups) return;
   long p = idx / groups;
   int c0 = (int)(idx % groups) * 8;
-  uint16_t o[8];
+  float v[8];
+  if (vec && c0 < c_real) {
+    const float4* gp = (const float4*)(g + p * gcs + gco + c0);
+    float4 a = gp[0], b = gp[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    if (act) {
+      uint4 yy = *(const uint4*)(y + p * ycs + yco + c0);
+      uint32_t w[4] = {yy.x, yy.y, yy.z, yy.w};
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    int c = c0 + i;
-    float v = 0.f;
-    if (c < c_real) {
-      v = g[p * gcs + gco + c] * scale;
-      if (act) {
-        float yy = bf2f(y[p * ycs + yco + c]);
-        if (!(yy > 0.f)) v = (act == 1) ? v * slope : 0.f;
+      for (int i = 0; i < 8; ++i) {
+        uint16_t u = (uint16_t)(w[i >> 1] >> ((i & 1) * 16));
+        float yf = bf2f(u);
+        v[i] *= scale;
+        if (!(yf > 0.f)) v[i] = (act == 1) ? v[i] * slope : 0.f;
       }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] *= scale;
     }
-    o[i] = f2bf(v);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      int c = c0 + i;
+      float t = 0.f;
+      if (c < c_real) {
+        t = g[p * gcs + gco + c] * scale;
+        if (act) {
+          float yy = bf2f(y[p * ycs + yco + c]);
+          if (!(yy > 0.f)) t = (act == 1) ? t * slope : 0.f;
+        }
+      }
+      v[i] = t;
+    }
   }
   uint4 pk;
-  pk.x = o[0] | ((uint32_t)o[1] << 16);
-  pk.y = o[2] | ((uint32_t)o[3] << 16);
-  pk.z = o[4] | ((uint32_t)o[5] << 16);
-  pk.w = o[6] | ((uint32_t)o[7] << 16);
+  pk.x = f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+  pk.y = f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+  pk.z = f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+  pk.w = f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
   *(uint4*)(dz + p * dzcs + c0) = pk;
 }
 
@@ -49,8 +69,10 @@ extern "C" int climsr_act_grad(int64_t npix, int c_real, const float* g, int g_c
     return CLIMSR_EINVAL;
   }
   long total = (long)npix * (dz_cstride / 8);
+  int vec = (c_real % 8 == 0) && (g_cstride % 4 == 0) && (g_coff % 4 == 0) && (!act || (y_cstride % 8 == 0 && y_coff % 8 == 0)) &&
+            ((uintptr_t)g % 16 == 0) && (!act || (uintptr_t)y % 16 == 0);
   hipLaunchKernelGGL(act_grad_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, (long)npix, c_real, g,
-                     g_cstride, g_coff, y, y_cstride, y_coff, act, slope, scale, dz, dz_cstride);
+                     g_cstride, g_coff, y, y_cstride, y_coff, act, slope, scale, dz, dz_cstride, vec);
   return check_launch("act_grad");
 }
 
@@ -105,10 +127,21 @@ extern "C" int climsr_nhwc_to_nchw_f32(const void* src, int src_is_bf16, int n, 
   return check_launch("nhwc_to_nchw_f32");
 }
 
-// y = a*x + b*y over channel slices (fp32); x may be NULL (then y = b*y)
+// y = a*x + b*y over channel slices (fp32); x may be NULL (then y = b*y).  4 channels per thread when aligned.
 __global__ void axpby_kernel(long npix, int c, float a, const float* __restrict__ x, int xcs, int xco, float b, float* y,
-                             int ycs, int yco) {
+                             int ycs, int yco, int vec) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (vec) {
+    int groups = c / 4;
+    if (idx >= npix * groups) return;
+    long p = idx / groups;
+    int ch = (int)(idx % groups) * 4;
+    float4* yp = (float4*)(y + p * ycs + yco + ch);
+    float4 xv = x ? *(const float4*)(x + p * xcs + xco + ch) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 yv = (b != 0.f) ? *yp : make_float4(0.f, 0.f, 0.f, 0.f);
+    *yp = make_float4(a * xv.x + b * yv.x, a * xv.y + b * yv.y, a * xv.z + b * yv.z, a * xv.w + b * yv.w);
+    return;
+  }
   if (idx >= npix * c) return;
   long p = idx / c;
   int ch = (int)(idx % c);
@@ -124,10 +157,58 @@ extern "C" int climsr_axpby_f32(int64_t npix, int c, float a, const float* x, in
     set_error("axpby_f32: null y");
     return CLIMSR_EINVAL;
   }
-  long total = (long)npix * c;
+  int vec = (c % 4 == 0) && (y_cstride % 4 == 0) && (y_coff % 4 == 0) && ((uintptr_t)y % 16 == 0) &&
+            (!x || (x_cstride % 4 == 0 && x_coff % 4 == 0 && (uintptr_t)x % 16 == 0));
+  long total = (long)npix * (vec ? c / 4 : c);
   hipLaunchKernelGGL(axpby_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, (long)npix, c, a, x, x_cstride,
-                     x_coff, b, y, y_cstride, y_coff);
+                     x_coff, b, y, y_cstride, y_coff, vec);
   return check_launch("axpby_f32");
+}
+
+// ------------------------------------------------------------------------------------------
+// Residual-dense-block backward prologue (esrgan.py:38,54), one pass over the block's pixels:
+//   g_o = a_o * gout (a_o = 0.2 for the 3rd RDB of an RRDB, whose output is out*0.2 + x)
+//   save_skip: gskip = gout (the RRDB skip gradient);   gy[:, :nf] = g_o (+ gskip if add_skip)
+//   gy[:, nf:dc] = 0;   dz5 = bf16(0.2 * g_o)  (conv5 output x5 enters as x5*0.2)
+// ------------------------------------------------------------------------------------------
+__global__ void rdb_bwd_init_kernel(long npix, int nf, int dc, const float* __restrict__ gx, float* __restrict__ gy,
+                                    float* __restrict__ gskip, uint16_t* __restrict__ dz, float a_o, int save_skip, int add_skip) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  int groups = dc / 4;
+  if (idx >= npix * groups) return;
+  long p = idx / groups;
+  int c = (int)(idx % groups) * 4;
+  float4* yp = (float4*)(gy + p * dc + c);
+  if (c >= nf) {
+    *yp = make_float4(0.f, 0.f, 0.f, 0.f);
+    return;
+  }
+  float4 g = *(const float4*)(gx + p * dc + c);
+  float4* sp = (float4*)(gskip + p * nf + c);
+  if (save_skip) *sp = g;
+  float4 o = make_float4(a_o * g.x, a_o * g.y, a_o * g.z, a_o * g.w);
+  float4 r = o;
+  if (add_skip) {
+    float4 s = *sp;
+    r.x += s.x; r.y += s.y; r.z += s.z; r.w += s.w;
+  }
+  *yp = r;
+  uint2 pk;
+  pk.x = f2bf(0.2f * o.x) | ((uint32_t)f2bf(0.2f * o.y) << 16);
+  pk.y = f2bf(0.2f * o.z) | ((uint32_t)f2bf(0.2f * o.w) << 16);
+  *(uint2*)(dz + p * nf + c) = pk;
+}
+
+extern "C" int climsr_rdb_bwd_init(int64_t npix, int nf, int dc, const float* gx, float* gy, float* gskip, uint16_t* dz, float a_o,
+                                   int save_skip, int add_skip, void* stream) {
+  if (!gx || !gy || !gskip || !dz || nf % 8 || dc % 4 || nf > dc) {
+    set_error("rdb_bwd_init: bad args");
+    return CLIMSR_EINVAL;
+  }
+  long total = (long)npix * (dc / 4);
+  hipLaunchKernelGGL(rdb_bwd_init_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, (long)npix, nf, dc, gx, gy,
+                     gskip, dz, a_o, save_skip, add_skip);
+  return check_launch("rdb_bwd_init");
 }
 
 // ------------------------------------------------------------------------------------------

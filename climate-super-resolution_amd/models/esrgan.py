@@ -24,7 +24,8 @@ import torch.nn as nn
 from torch import Tensor
 
 from ..core.flat import FlatParamsMixin
-from ..ops import (ACT_LRELU, ACT_NONE, ACT_RELU, OUT_F32, ConvPlan, Workspace, act_grad, axpby, nchw_to_nhwc)
+from ..ops import (ACT_LRELU, ACT_NONE, ACT_RELU, OUT_F32, BatchedPacker, ConvPlan, Workspace, act_grad, axpby, nchw_to_nhwc,
+                   rdb_bwd_init)
 from .srcnn import SRCNN
 
 
@@ -109,6 +110,7 @@ class _Engine:
         for name, p in self.plans.items():
             conv = self.modules[name]
             p.bind(conv.weight, conv.bias, need_t=(name != "conv_first"))
+        self.packer = BatchedPacker(list(self.plans.values()), gen.conv_first.weight.device)
         self.version = -1
 
     def bind_grads(self):
@@ -120,13 +122,11 @@ class _Engine:
     def ensure_packed(self):
         v = self.gen._flat._version
         if v != self.version:
-            for p in self.plans.values():
-                p.pack()
+            self.packer.run()
             self.version = v
 
     def repack(self):
-        for p in self.plans.values():
-            p.pack()
+        self.packer.run()
         self.version = self.gen._flat._version
 
     def rdb_name(self, i, r, c):
@@ -270,15 +270,9 @@ class _Engine:
         # ---- RRDB trunk, reverse (esrgan.py:32-54)
         for i in reversed(range(3 * nb)):
             blk, r = divmod(i, 3)
-            a_o = 1.0
-            if r == 2:  # output of RRDB blk: out*0.2 + x
-                axpby(npx_lr, nf, 1.0, gX, dc, 0, 0.0, gskip, nf, 0)
-                a_o = 0.2
-            axpby(npx_lr, nf, a_o, gX, dc, 0, 0.0, gY, dc, 0)
-            if r == 0:
-                axpby(npx_lr, nf, 1.0, gskip, nf, 0, 1.0, gY, dc, 0)
-            axpby(npx_lr, dc - nf, 0.0, None, 0, 0, 0.0, gY, dc, nf)
-            act_grad(npx_lr, nf, gX, dc, 0, None, 0, 0, ACT_NONE, dz64, nf, scale=0.2 * a_o)
+            # r == 2: this RDB's output is the RRDB's (out*0.2 + x): save the skip gradient, scale by 0.2
+            a_o = 0.2 if r == 2 else 1.0
+            rdb_bwd_init(npx_lr, nf, dc, gX, gY, gskip, dz64, a_o, save_skip=(r == 2), add_skip=(r == 0))
             src = dense[i]
             c5 = P[self.rdb_name(blk, r + 1, 5)]
             c5.wgrad(src, dc, 0, h, w, dz64, nf, n, ws, acc)

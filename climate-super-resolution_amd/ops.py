@@ -13,7 +13,7 @@ from typing import Optional
 import torch
 
 from . import _lib
-from ._lib import ConvDesc, Epilogue, check, ptr
+from ._lib import ConvDesc, Epilogue, PackDesc, check, ptr
 
 ACT_NONE, ACT_LRELU, ACT_RELU = 0, 1, 2
 OUT_BF16, OUT_F32, OUT_F32_ADD = 0, 1, 2
@@ -100,6 +100,13 @@ class ConvPlan:
         if self.wpk_t is not None:
             check(lib.climsr_pack_conv_weight(ptr(w), self.cout_t, self.cin_t, self.cout, self.cout_t, self.ks, self.cc_t, 1,
                                               ptr(self.wpk_t), s), f"pack_t {self.name}")
+
+    def pack_descs(self):
+        out = [PackDesc(ptr(self.weight), ptr(self.wpk), self.cout, self.cin, self.cin_real, self.cout, self.ks, self.cc, 0, 0)]
+        if self.wpk_t is not None:
+            out.append(PackDesc(ptr(self.weight), ptr(self.wpk_t), self.cout_t, self.cin_t, self.cout, self.cout_t, self.ks,
+                                self.cc_t, 1, 0))
+        return out
 
     # ---------------------------------------------------------------- launches
     def out_hw(self, in_h: int, in_w: int, up: int = 1):
@@ -196,3 +203,31 @@ def nhwc_to_nchw(src: torch.Tensor, n: int, c: int, h: int, w: int, cs: int, co:
     is_bf16 = 1 if src.dtype == torch.bfloat16 else 0
     check(_lib.load().climsr_nhwc_to_nchw_f32(ptr(src), is_bf16, n, c, h, w, cs, co, ptr(dst), _lib.stream_ptr()),
           "nhwc_to_nchw")
+
+
+def rdb_bwd_init(npix: int, nf: int, dc: int, gx: torch.Tensor, gy: torch.Tensor, gskip: torch.Tensor, dz: torch.Tensor, a_o: float,
+                 save_skip: bool, add_skip: bool) -> None:
+    check(_lib.load().climsr_rdb_bwd_init(npix, nf, dc, ptr(gx), ptr(gy), ptr(gskip), ptr(dz), a_o, int(save_skip), int(add_skip),
+                                          _lib.stream_ptr()), "rdb_bwd_init")
+
+
+class BatchedPacker:
+    """All weight packs of a network as ONE launch (descriptor table resident on the device)."""
+
+    def __init__(self, plans, device):
+        descs = []
+        for p in plans:
+            descs += p.pack_descs()
+        arr = (PackDesc * len(descs))(*descs)
+        raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+        self.table = raw.to(device)
+        self.n = len(descs)
+        self.max_elems = max(d.out_c for d in descs)  # placeholder, replaced below
+        self.max_elems = max(p.rows * p.kpk for p in plans)
+        for p in plans:
+            if p.wpk_t is not None:
+                self.max_elems = max(self.max_elems, p.rows_t * p.kpk_t)
+
+    def run(self):
+        check(_lib.load().climsr_pack_conv_weights_batched(ptr(self.table), self.n, self.max_elems, _lib.stream_ptr()),
+              "pack batched")

@@ -78,6 +78,16 @@ int climsr_conv_packed_rows(int out_c);
 int climsr_pack_conv_weight(const float* w, int out_c, int in_c, int in_c_real, int out_c_real, int ks, int cc,
                             int transpose_flip, uint16_t* wpk, void* stream);
 
+/* One pack job of climsr_pack_conv_weights_batched (fields as in climsr_pack_conv_weight). */
+typedef struct ClimsrPackDesc {
+  const float* w;
+  uint16_t* out;
+  int32_t out_c, in_c, in_c_real, out_c_real, ks, cc, tflip, reserved;
+} ClimsrPackDesc;
+/* Pack many convs in one launch; `descs` is a DEVICE array of ndesc descriptors, max_elems the
+ * largest packed size (rows*packed_k) among them.  Used after every optimiser step. */
+int climsr_pack_conv_weights_batched(const ClimsrPackDesc* descs, int ndesc, int64_t max_elems, void* stream);
+
 /* Implicit-GEMM convolution on MFMA (bf16 in, fp32 accumulate), fused epilogue.
  * Forward of nn.Conv2d (esrgan.py:22-26,72-83; srcnn.py:9-11; rfb_esrgan.py:28-52) and, with
  * transpose_flip weights, its data gradient (stride 1). */
@@ -111,6 +121,12 @@ int climsr_nhwc_to_nchw_f32(const void* src, int src_is_bf16, int n, int c, int 
 /* y[p][c] (+)= x[p][c] elementwise fp32 over channel slices (init / residual gradient routing). */
 int climsr_axpby_f32(int64_t npix, int c, float a, const float* x, int x_cstride, int x_coff, float b,
                      float* y, int y_cstride, int y_coff, void* stream);
+
+/* Residual-dense-block backward prologue (esrgan.py:38,54) over npix pixels of [npix][dc] fp32
+ * gradient buffers: save_skip: gskip = gx[:, :nf]; gy[:, :nf] = a_o*gx[:, :nf] (+ gskip if add_skip);
+ * gy[:, nf:] = 0; dz[:, :nf] = bf16(0.2*a_o*gx[:, :nf]) (conv5's output gradient). */
+int climsr_rdb_bwd_init(int64_t npix, int nf, int dc, const float* gx, float* gy, float* gskip, uint16_t* dz, float a_o,
+                        int save_skip, int add_skip, void* stream);
 
 /* L1Loss (mean) forward: out[0] = mean|a-b| (deterministic two-pass tree, fp64 partials).
  * workspace >= 1024 doubles.  torch.nn.L1Loss (task.py:141, pl_gan.py:20). */
