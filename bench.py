@@ -49,18 +49,30 @@ class KernelTimer:
     def __init__(self):
         self.rec = []
 
-    def __call__(self, name, flops, fn):
+    def __call__(self, name, flops, fn, tag=""):
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         s.record()
         fn()
         e.record()
-        self.rec.append((name, flops, s, e))
+        self.rec.append((name, flops, s, e, tag))
+
+    def by_tag(self, top=25):
+        torch.cuda.synchronize()
+        agg = {}
+        for name, flops, s, e, tag in self.rec:
+            key = name + " | " + ".".join(t for t in tag.split(".") if not t.isdigit() and not t.startswith("RDB"))
+            a = agg.setdefault(key, [0, 0.0, 0])
+            a[0] += 1
+            a[1] += s.elapsed_time(e)
+            a[2] += flops
+        rows = sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]
+        return {k: {"n": v[0], "ms": round(v[1], 3), "tflops": round(v[2] / (v[1] / 1e3) / 1e12, 1)} for k, v in rows}
 
     def summary(self):
         torch.cuda.synchronize()
         agg = {}
-        for name, flops, s, e in self.rec:
+        for name, flops, s, e, _tag in self.rec:
             a = agg.setdefault(name, [0, 0.0, 0])
             a[0] += 1
             a[1] += s.elapsed_time(e)
@@ -197,6 +209,8 @@ def main():
                 "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None}
         kern = {k: {"launches": v[0], "ms_total": round(v[1], 3), "tflops": round(v[2] / (v[1] / 1e3) / 1e12, 1)}
                 for k, v in sorted(agg.items(), key=lambda kv: -kv[1][1])}
+        if os.environ.get("CLIMSR_BENCH_DETAIL"):
+            print(json.dumps(timer.by_tag(), indent=0), file=sys.stderr)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -11,6 +11,7 @@
 // C[row 4(l>>4)+i][col l&15].
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include "common.h"
 
@@ -40,7 +41,8 @@ int check_launch(const char* what) {
 constexpr int TW = 16;            // output tile width (one MFMA N-fragment of pixels)
 constexpr int XPAD = 8;           // channel padding of the LDS input tile (bank spread)
 constexpr int WPAD = 8;           // k padding of the LDS weight tile rows
-constexpr int FWD_LDS_BUDGET = 64 * 1024;
+constexpr int FWD_LDS_BUDGET = 80 * 1024;  // two workgroups per CU
+constexpr int FWD_MAXV = 8;             // 16 B staging vectors per thread held in registers (prefetch)
 
 struct FwdGeom {
   int th, tph, tpw, ccp, kc, kcpad, nchunk, kpk, nt, mw;
@@ -87,8 +89,10 @@ extern "C" int climsr_conv_chunk(int in_c, int ks, int out_c) {
   int cc = round_up(in_c, 8);
   FwdGeom g;
   while (cc > 8) {
-    fwd_geom(in_c, ks, 1, out_c, cc, 2, &g);
+    fwd_geom(in_c, ks, 1, out_c, cc, 4, &g);
+    long nvec = (long)g.tph * g.tpw * (cc / 8) + (long)g.nt * 16 * (g.kcpad / 8);
     if (g.lds_total <= (size_t)FWD_LDS_BUDGET) break;
+    (void)nvec;
     cc = round_up((cc + 1) / 2, 8);
   }
   return cc;
@@ -198,6 +202,7 @@ struct FwdArgs {
   float slope, alpha1, alpha2;
   int r1_cs, r1_co, r2_cs, r2_co;
   int lds_tab, lds_x;
+  int ablate;  // diagnostics only (CLIMSR_ABLATE): 1 skip global loads, 2 skip MFMA, 4 skip stores
 };
 
 template <int MW, int NT>
@@ -250,34 +255,43 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
   const int nvec_x = a.tph * a.tpw * cvec;
   const int wvec_row = a.kcpad / 8;
   const int nvec_w = NT * 16 * wvec_row;
+  const int nvec = nvec_x + nvec_w;
   const int upsh = a.up == 2 ? 1 : 0;
 
-  for (int j = 0; j < a.nchunk; ++j) {
-    const int c0 = j * a.cc;
-    __syncthreads();
-    // stage input tile (logical, upsampled coordinates; zero padding)
-    for (int v = tid; v < nvec_x; v += 256) {
+  // staging = one flat space of 16 B vectors: [0, nvec_x) input tile, [nvec_x, nvec) weight chunk
+  auto gload = [&](int j, int v) -> uint4 {
+    if (v < nvec_x) {
       int pix = v / cvec;
       int cg = v - pix * cvec;
       int ty_ = pix / a.tpw;
       int tx_ = pix - ty_ * a.tpw;
       int iy = iy0 + ty_, ix = ix0 + tx_;
-      int c = c0 + cg * 8;
+      int c = j * a.cc + cg * 8;
       uint4 val = make_uint4(0, 0, 0, 0);
       if (iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c) {
         long src = (((long)nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + c;
         val = *(const uint4*)(a.x + src);
       }
-      *(uint4*)(xs + pix * a.ccp + cg * 8) = val;
+      return val;
     }
-    // stage weight chunk
-    for (int v = tid; v < nvec_w; v += 256) {
+    v -= nvec_x;
+    int r = v / wvec_row;
+    int kv = v - r * wvec_row;
+    return *(const uint4*)(a.w + (long)(co_blk0 + r) * a.kpk + (long)j * a.kcpad + kv * 8);
+  };
+  auto lstore = [&](int v, uint4 val) {
+    if (v < nvec_x) {
+      int pix = v / cvec;
+      int cg = v - pix * cvec;
+      *(uint4*)(xs + pix * a.ccp + cg * 8) = val;
+    } else {
+      v -= nvec_x;
       int r = v / wvec_row;
       int kv = v - r * wvec_row;
-      uint4 val = *(const uint4*)(a.w + (long)(co_blk0 + r) * a.kpk + (long)j * a.kcpad + kv * 8);
       *(uint4*)(ws + r * wpitch + kv * 8) = val;
     }
-    __syncthreads();
+  };
+  auto compute = [&]() {
     const int nks = a.kcpad / 32;
     for (int kstep = 0; kstep < nks; ++kstep) {
       const int off = tab[kstep * 4 + g];
@@ -292,101 +306,171 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bfr[m], acc[m][t], 0, 0, 0);
     }
+  };
+
+  // batched staging: every thread issues up to FWD_MAXV independent 16 B global loads before the
+  // first LDS store, so a chunk pays ~one memory latency instead of one per vector
+  for (int j = 0; j < a.nchunk; ++j) {
+    __syncthreads();
+    for (int base = 0; base < nvec; base += 256 * FWD_MAXV) {
+      uint4 buf[FWD_MAXV];
+#pragma unroll
+      for (int i = 0; i < FWD_MAXV; ++i) {
+        int v = base + tid + i * 256;
+        if (v < nvec) buf[i] = (a.ablate & 1) ? make_uint4(0, 0, 0, 0) : gload(j, v);
+      }
+#pragma unroll
+      for (int i = 0; i < FWD_MAXV; ++i) {
+        int v = base + tid + i * 256;
+        if (v < nvec) lstore(v, buf[i]);
+      }
+    }
+    __syncthreads();
+    if (!(a.ablate & 2)) compute();
+  }
+  if (a.ablate & 4) {
+    if (acc[0][0][0] == 123.f) ((float*)a.y)[0] = 0.f;  // keep the accumulators live
+    return;
   }
 
   // ---------------- epilogue ----------------
+  // All global reads of the epilogue (bias, residuals, accumulate targets) are issued for every
+  // fragment before the first store, so their latencies overlap instead of serialising.
   const int ox = ox0 + col;
   if (a.down2) {
     // sum the 2x2 block: rows (m, m+1) are in this wave (MW even, oy0 even); columns pair via lane^1
+    const int dh = a.out_h >> 1, dw = a.out_w >> 1;
+    float4 old[MW / 2][NT];
 #pragma unroll
     for (int m = 0; m < MW; m += 2) {
       const int oy = oy0 + wave * MW + m;
+      const long pidx = ((long)nimg * dh + (oy >> 1)) * dw + (ox >> 1);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int co = co_blk0 + t * 16 + g * 4;
+        old[m / 2][t] = make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool ok = (col & 1) == 0 && oy < a.out_h && ox < a.out_w && co + 3 < a.out_c && a.out_mode == 2;
+        if (ok) old[m / 2][t] = *(const float4*)((const float*)a.y + pidx * a.out_cs + a.out_co + co);
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < MW; m += 2) {
+      const int oy = oy0 + wave * MW + m;
+      const long pidx = ((long)nimg * dh + (oy >> 1)) * dw + (ox >> 1);
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         float v[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          float s = acc[m][t][i] + acc[m + 1][t][i];
-          s += __shfl_xor(s, 1);
-          v[i] = s;
+          float sm = acc[m][t][i] + acc[m + 1][t][i];
+          sm += __shfl_xor(sm, 1);
+          v[i] = sm;
         }
         const int co = co_blk0 + t * 16 + g * 4;
         if ((col & 1) == 0 && oy < a.out_h && ox < a.out_w) {
-          const int dh = a.out_h >> 1, dw = a.out_w >> 1;
-          long pidx = ((long)nimg * dh + (oy >> 1)) * dw + (ox >> 1);
           float* yp = (float*)a.y + pidx * a.out_cs + a.out_co + co;
+          if (co + 3 < a.out_c) {
+            float4 o = old[m / 2][t];
+            *(float4*)yp = make_float4(o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]);
+          } else {
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (co + i < a.out_c) {
-              if (a.out_mode == 2) yp[i] += v[i];
-              else yp[i] = v[i];
-            }
+            for (int i = 0; i < 4; ++i)
+              if (co + i < a.out_c) yp[i] = (a.out_mode == 2 ? yp[i] : 0.f) + v[i];
+          }
         }
       }
     }
     return;
   }
+  // vector path needs 4-channel-aligned rows (true for every layer of the generator)
+  const bool valign = ((a.out_cs | a.out_co) & 3) == 0 && (!a.res1 || ((a.r1_cs | a.r1_co) & 3) == 0) &&
+                      (!a.res2 || ((a.r2_cs | a.r2_co) & 3) == 0);
+  float4 bv[NT];
 #pragma unroll
-  for (int m = 0; m < MW; ++m) {
-    const int oy = oy0 + wave * MW + m;
-    const bool pv = oy < a.out_h && ox < a.out_w;
-    const long pidx = ((long)nimg * a.out_h + oy) * a.out_w + ox;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int co = co_blk0 + t * 16 + g * 4;
-      if (!pv || co >= a.out_c) continue;
-      const bool full = (co + 3 < a.out_c);
-      float v[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float s = acc[m][t][i];
-        if (a.bias && co + i < a.out_c) s += a.bias[co + i];
-        v[i] = act_apply(s, a.act, a.slope);
+  for (int t = 0; t < NT; ++t) {
+    const int co = co_blk0 + t * 16 + g * 4;
+    bv[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.bias) {
+      if (co + 3 < a.out_c) bv[t] = *(const float4*)(a.bias + co);
+      else {
+        if (co < a.out_c) bv[t].x = a.bias[co];
+        if (co + 1 < a.out_c) bv[t].y = a.bias[co + 1];
+        if (co + 2 < a.out_c) bv[t].z = a.bias[co + 2];
       }
-      if (a.res1) {
-        const uint16_t* rp = a.res1 + pidx * a.r1_cs + a.r1_co + co;
+    }
+  }
+  // two output rows (fragments) per round: operand loads for both rows are in flight together while
+  // the register footprint stays at 2*NT fragments
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (co + i < a.out_c) v[i] = v[i] * a.alpha1 + bf2f(rp[i]);
-      }
-      if (a.res2) {
-        const uint16_t* rp = a.res2 + pidx * a.r2_cs + a.r2_co + co;
+  for (int mm = 0; mm < MW; mm += 2) {
+    uint2 r1v[2][NT], r2v[2][NT];
+    float4 old[2][NT];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (co + i < a.out_c) v[i] = v[i] * a.alpha2 + bf2f(rp[i]);
-      }
-      const long ob = pidx * a.out_cs + a.out_co + co;
-      if (a.out_mode == 0) {
-        uint16_t* yp = (uint16_t*)a.y + ob;
-        if (full && (ob & 3) == 0) {
-          uint2 pk;
-          pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-          pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-          *(uint2*)yp = pk;
-        } else {
+    for (int h = 0; h < 2; ++h) {
+      const int m = mm + h;
+      const int oy = oy0 + wave * MW + m;
+      const bool pv = oy < a.out_h && ox < a.out_w;
+      const long pidx = ((long)nimg * a.out_h + oy) * a.out_w + ox;
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (co + i < a.out_c) yp[i] = f2bf(v[i]);
+      for (int t = 0; t < NT; ++t) {
+        const int co = co_blk0 + t * 16 + g * 4;
+        const bool vec = pv && valign && co + 3 < a.out_c;
+        r1v[h][t] = make_uint2(0, 0);
+        r2v[h][t] = make_uint2(0, 0);
+        old[h][t] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (vec) {
+          if (a.res1) r1v[h][t] = *(const uint2*)(a.res1 + pidx * a.r1_cs + a.r1_co + co);
+          if (a.res2) r2v[h][t] = *(const uint2*)(a.res2 + pidx * a.r2_cs + a.r2_co + co);
+          if (a.out_mode == 2) old[h][t] = *(const float4*)((const float*)a.y + pidx * a.out_cs + a.out_co + co);
         }
-      } else {
-        float* yp = (float*)a.y + ob;
-        if (a.out_mode == 2) {
-          if (full && (ob & 3) == 0) {
-            float4 o = *(float4*)yp;
-            o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
-            *(float4*)yp = o;
-          } else {
+      }
+    }
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-              if (co + i < a.out_c) yp[i] += v[i];
+    for (int h = 0; h < 2; ++h) {
+      const int m = mm + h;
+      const int oy = oy0 + wave * MW + m;
+      const bool pv = oy < a.out_h && ox < a.out_w;
+      const long pidx = ((long)nimg * a.out_h + oy) * a.out_w + ox;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int co = co_blk0 + t * 16 + g * 4;
+        if (!pv || co >= a.out_c) continue;
+        const bool vec = valign && co + 3 < a.out_c;
+        const float bb[4] = {bv[t].x, bv[t].y, bv[t].z, bv[t].w};
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = act_apply(acc[m][t][i] + bb[i], a.act, a.slope);
+        const long ob = pidx * a.out_cs + a.out_co + co;
+        if (vec) {
+          if (a.res1) {
+            const uint32_t w0 = r1v[h][t].x, w1 = r1v[h][t].y;
+            v[0] = v[0] * a.alpha1 + bf2f((uint16_t)w0); v[1] = v[1] * a.alpha1 + bf2f((uint16_t)(w0 >> 16));
+            v[2] = v[2] * a.alpha1 + bf2f((uint16_t)w1); v[3] = v[3] * a.alpha1 + bf2f((uint16_t)(w1 >> 16));
           }
-        } else {
-          if (full && (ob & 3) == 0) {
-            *(float4*)yp = make_float4(v[0], v[1], v[2], v[3]);
+          if (a.res2) {
+            const uint32_t w0 = r2v[h][t].x, w1 = r2v[h][t].y;
+            v[0] = v[0] * a.alpha2 + bf2f((uint16_t)w0); v[1] = v[1] * a.alpha2 + bf2f((uint16_t)(w0 >> 16));
+            v[2] = v[2] * a.alpha2 + bf2f((uint16_t)w1); v[3] = v[3] * a.alpha2 + bf2f((uint16_t)(w1 >> 16));
+          }
+          if (a.out_mode == 0) {
+            uint2 pk;
+            pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+            pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+            *(uint2*)((uint16_t*)a.y + ob) = pk;
           } else {
+            float4 o = old[h][t];
+            *(float4*)((float*)a.y + ob) = make_float4(o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]);
+          }
+        } else {  // scalar tail (out_c not a multiple of 4 or unaligned slices)
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-              if (co + i < a.out_c) yp[i] = v[i];
+          for (int i = 0; i < 4; ++i) {
+            if (co + i >= a.out_c) continue;
+            float x = v[i];
+            if (a.res1) x = x * a.alpha1 + bf2f(a.res1[pidx * a.r1_cs + a.r1_co + co + i]);
+            if (a.res2) x = x * a.alpha2 + bf2f(a.res2[pidx * a.r2_cs + a.r2_co + co + i]);
+            if (a.out_mode == 0) ((uint16_t*)a.y)[ob + i] = f2bf(x);
+            else if (a.out_mode == 2) ((float*)a.y)[ob + i] += x;
+            else ((float*)a.y)[ob + i] = x;
           }
         }
       }
@@ -424,7 +508,9 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
     return CLIMSR_EINVAL;
   }
   FwdGeom g;
-  fwd_geom(d->in_c, d->ks, d->stride, d->out_c, d->cc, 2, &g);
+  // 16x16 output tiles (64 px per wave) for the 64-channel layers; 8x16 otherwise
+  const int mw = (d->out_h >= 12 && fwd_nt(d->out_c) == 4) ? 4 : 2;
+  fwd_geom(d->in_c, d->ks, d->stride, d->out_c, d->cc, mw, &g);
   if (g.lds_total > 160 * 1024) {
     set_error("conv2d_fwd: LDS %zu exceeds 160 KiB (cc=%d)", g.lds_total, d->cc);
     return CLIMSR_EINVAL;
@@ -441,9 +527,12 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
   a.slope = ep->slope; a.alpha1 = ep->alpha1; a.alpha2 = ep->alpha2;
   a.r1_cs = ep->res1_cstride; a.r1_co = ep->res1_coff; a.r2_cs = ep->res2_cstride; a.r2_co = ep->res2_coff;
   a.lds_tab = (int)g.lds_tab; a.lds_x = (int)g.lds_x;
+  static int ablate = getenv("CLIMSR_ABLATE") ? atoi(getenv("CLIMSR_ABLATE")) : 0;
+  a.ablate = ablate;
   int rows = climsr_conv_packed_rows(d->out_c);
   int ncob = rows / (g.nt * 16);
   hipStream_t s = (hipStream_t)stream;
+  if (mw == 4) return launch_fwd<4, 4>(a, ncob, g.lds_total, s);
   switch (g.nt) {
     case 1: return launch_fwd<2, 1>(a, ncob, g.lds_total, s);
     case 2: return launch_fwd<2, 2>(a, ncob, g.lds_total, s);
@@ -470,6 +559,7 @@ struct WgArgs {
   int n, in_h, in_w, in_c, in_cs, in_co, up, ks, stride, pad, out_h, out_w, out_c, dz_cs;
   int tph, tpw, dzp, tiles_x, tiles_y, ntiles, nsplit, ntapb, ncib, co_rows, kw;
   int lds_x;
+  int ablate;
 };
 
 template <int NTC, int TB>
@@ -534,33 +624,49 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs a) {
     const int ox0 = tx * TW, oy0 = ty * WG_TH;
     const int iy0 = oy0 * a.stride - a.pad, ix0 = ox0 * a.stride - a.pad;
     __syncthreads();
-    for (int v = tid; v < nvec_x; v += 256) {
-      int pix = v >> 1;
-      int h = v & 1;
-      int ty_ = pix / a.tpw, tx_ = pix - (pix / a.tpw) * a.tpw;
-      int iy = iy0 + ty_, ix = ix0 + tx_;
-      int c = ci0 + h * 8;
-      uint4 val = make_uint4(0, 0, 0, 0);
-      if (iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c) {
-        long src = (((long)nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + c;
-        val = *(const uint4*)(a.x + src);
+    // batched staging (all loads of a round in flight before the first LDS store)
+    for (int base = 0; base < nvec_x + nvec_z; base += 256 * FWD_MAXV) {
+      uint4 buf[FWD_MAXV];
+#pragma unroll
+      for (int i = 0; i < FWD_MAXV; ++i) {
+        int v = base + tid + i * 256;
+        uint4 val = make_uint4(0, 0, 0, 0);
+        if (a.ablate & 1) {
+        } else if (v < nvec_x) {
+          int pix = v >> 1;
+          int h = v & 1;
+          int ty_ = pix / a.tpw, tx_ = pix - (pix / a.tpw) * a.tpw;
+          int iy = iy0 + ty_, ix = ix0 + tx_;
+          int c = ci0 + h * 8;
+          if (iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c)
+            val = *(const uint4*)(a.x + (((long)nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + c);
+        } else if (v < nvec_x + nvec_z) {
+          int vz = v - nvec_x;
+          int pix = vz / zvec;
+          int cv = vz - pix * zvec;
+          int oy = oy0 + pix / TW, ox = ox0 + (pix % TW);
+          int c = co0 + cv * 8;
+          if (oy < a.out_h && ox < a.out_w && c < a.dz_cs)
+            val = *(const uint4*)(a.dz + (((long)nimg * a.out_h + oy) * a.out_w + ox) * a.dz_cs + c);
+        }
+        buf[i] = val;
       }
-      *(uint4*)(xs + pix * WG_XP + h * 8) = val;
-    }
-    for (int v = tid; v < nvec_z; v += 256) {
-      int pix = v / zvec;
-      int cv = v - pix * zvec;
-      int oy = oy0 + pix / TW, ox = ox0 + (pix % TW);
-      int c = co0 + cv * 8;
-      uint4 val = make_uint4(0, 0, 0, 0);
-      if (oy < a.out_h && ox < a.out_w && c < a.dz_cs) {
-        val = *(const uint4*)(a.dz + (((long)nimg * a.out_h + oy) * a.out_w + ox) * a.dz_cs + c);
+#pragma unroll
+      for (int i = 0; i < FWD_MAXV; ++i) {
+        int v = base + tid + i * 256;
+        if (v < nvec_x) {
+          *(uint4*)(xs + (v >> 1) * WG_XP + (v & 1) * 8) = buf[i];
+        } else if (v < nvec_x + nvec_z) {
+          int vz = v - nvec_x;
+          int pix = vz / zvec;
+          *(uint4*)(zs + pix * a.dzp + (vz - pix * zvec) * 8) = buf[i];
+        }
       }
-      *(uint4*)(zs + pix * a.dzp + cv * 8) = val;
     }
     __syncthreads();
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
+      if (a.ablate & 2) break;
       const int kk = wave * 2 + s;  // k-step: output pixel rows 2kk, 2kk+1 of the tile
       // pixel handled as row q (+4) of this lane's tr reads
       const int k0 = kk * 32 + 8 * g + q;
@@ -713,6 +819,8 @@ extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, c
   a.tph = w.tph; a.tpw = w.tpw; a.dzp = w.dzp; a.tiles_x = w.tiles_x; a.tiles_y = w.tiles_y; a.ntiles = w.ntiles;
   a.nsplit = nsplit; a.ntapb = w.ntapb; a.ncib = w.ncib; a.co_rows = w.co_rows; a.kw = w.kw;
   a.lds_x = (int)w.lds_x;
+  static int ablate = getenv("CLIMSR_ABLATE") ? atoi(getenv("CLIMSR_ABLATE")) : 0;
+  a.ablate = ablate;
   int nblk = w.ntapb * w.ncib * w.ncob;
   hipStream_t s = (hipStream_t)stream;
 #define WG_CASE(NTC, TB) \

@@ -33,8 +33,9 @@ def _fwd_nt(out_c: int) -> int:
     return 4 if nt >= 3 else nt
 
 
-def fwd_kernel_name(out_c: int) -> str:
-    return f"conv_fwd_kernel<2, {_fwd_nt(out_c)}>"
+def fwd_kernel_name(out_c: int, out_h: int = 16) -> str:
+    nt = _fwd_nt(out_c)
+    return f"conv_fwd_kernel<{4 if (out_h >= 12 and nt == 4) else 2}, {nt}>"
 
 
 def wgrad_kernel_name(out_c: int, ks: int) -> str:
@@ -47,11 +48,11 @@ def wgrad_kernel_name(out_c: int, ks: int) -> str:
     return f"conv_wgrad_kernel<{ntc}, {tb}>"
 
 
-def _run(name, flops, fn):
+def _run(name, flops, fn, tag=""):
     if PROFILER is None:
         fn()
     else:
-        PROFILER(name, flops, fn)
+        PROFILER(name, flops, fn, tag)
 
 
 class ConvPlan:
@@ -125,9 +126,9 @@ class ConvPlan:
         ep = Epilogue(act, slope, alpha1, ptr(res1), res1_cs, res1_co, alpha2, ptr(res2), res2_cs, res2_co, out_mode, 0)
         b = ptr(self.bias) if (use_bias and self.bias is not None) else None
         flops = 2 * self.cin_real * self.cout * self.ks * self.ks * n * oh * ow
-        _run(fwd_kernel_name(self.cout), flops, lambda: check(
+        _run(fwd_kernel_name(self.cout, oh), flops, lambda: check(
             _lib.load().climsr_conv2d_fwd(ctypes.byref(d), ptr(x), ptr(self.wpk), b, ctypes.byref(ep), ptr(y), _lib.stream_ptr()),
-            f"conv fwd {self.name}"))
+            f"conv fwd {self.name}"), "fwd " + self.name)
 
     def dgrad(self, dz: torch.Tensor, dz_cs: int, out_h: int, out_w: int, g: torch.Tensor, g_cs: int, g_co: int, n: int,
               accumulate: bool = False, down2: bool = False, cout_t: Optional[int] = None) -> None:
@@ -139,9 +140,9 @@ class ConvPlan:
         d = ConvDesc(n, out_h, out_w, self.cin_t, dz_cs, 0, 1, self.ks, 1, pad_t, out_h, out_w, ct, g_cs, g_co, self.cc_t)
         ep = Epilogue(0, 0.0, 1.0, None, 0, 0, 1.0, None, 0, 0, OUT_F32_ADD if accumulate else OUT_F32, 1 if down2 else 0)
         flops = 2 * self.cout * ct * self.ks * self.ks * n * out_h * out_w
-        _run(fwd_kernel_name(ct), flops, lambda: check(
+        _run(fwd_kernel_name(ct, out_h), flops, lambda: check(
             _lib.load().climsr_conv2d_fwd(ctypes.byref(d), ptr(dz), ptr(self.wpk_t), None, ctypes.byref(ep), ptr(g),
-                                          _lib.stream_ptr()), f"conv dgrad {self.name}"))
+                                          _lib.stream_ptr()), f"conv dgrad {self.name}"), "dgrad " + self.name)
 
     def wgrad_desc(self, n, in_h, in_w, x_cs, x_co, up):
         oh, ow = self.out_hw(in_h, in_w, up)
@@ -164,7 +165,7 @@ class ConvPlan:
         flops = 2 * self.cin_real * self.cout * self.ks * self.ks * n * d.out_h * d.out_w
         _run(wgrad_kernel_name(self.cout, self.ks), flops, lambda: check(
             lib.climsr_conv2d_wgrad(ctypes.byref(d), ptr(x), ptr(dz), dz_cs, ptr(part), ptr(bpart) if has_b else None, ns, s),
-            f"conv wgrad {self.name}"))
+            f"conv wgrad {self.name}"), "wgrad " + self.name)
         check(lib.climsr_conv2d_wgrad_reduce(ptr(part), ptr(bpart) if has_b else None, ns, self.cout, self.cin_real, self.cin,
                                              self.ks, ptr(self.gw), ptr(self.gb) if has_b else None,
                                              1 if accumulate else 0, s), f"wgrad reduce {self.name}")

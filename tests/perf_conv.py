@@ -1,0 +1,68 @@
+"""Micro-benchmark of the conv kernels on the generator's hot shapes (run on the GPU box):
+    python tests/perf_conv.py [--batch 32]
+Prints per-op average launch time (HIP events, 20 reps after warm-up) and TFLOP/s."""
+import argparse
+import sys
+
+sys.path.insert(0, "/root/repo")
+import torch  # noqa: E402
+
+import climsr_amd  # noqa: E402,F401
+from climsr_amd.ops import ACT_LRELU, OUT_F32, ConvPlan, Workspace  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--batch", type=int, default=32)
+ap.add_argument("--reps", type=int, default=20)
+args = ap.parse_args()
+dev = "cuda"
+n = args.batch
+
+
+def timeit(fn, reps):
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps * 1e3  # us
+
+
+def plan(cin, cout, ks, up=1):
+    p = ConvPlan(cin, cout, ks, 1, None, f"{cin}->{cout}k{ks}")
+    w = (torch.randn(cout, cin, ks, ks, device=dev) * 0.05).contiguous()
+    b = torch.zeros(cout, device=dev)
+    p.bind(w, b)
+    p.pack()
+    p.gw = torch.zeros_like(w)
+    p.gb = torch.zeros_like(b)
+    return p
+
+
+rows = []
+ws = Workspace()
+for (cin, cout, ks, h, up) in [(64, 16, 3, 64, 1), (112, 16, 3, 64, 1), (128, 64, 3, 64, 1), (64, 64, 3, 128, 2), (64, 64, 3, 256, 1),
+                               (3, 64, 9, 256, 1), (64, 1, 3, 256, 1), (32, 1, 5, 256, 1)]:
+    p = plan(cin, cout, ks, up)
+    hin = h // up
+    dense = torch.randn(n, hin, hin, max(8, (cin + 7) // 8 * 8), device=dev).to(torch.bfloat16)
+    cs = dense.shape[-1]
+    ocs = (cout + 7) // 8 * 8
+    y = torch.zeros(n, h, h, ocs, device=dev, dtype=torch.bfloat16)
+    flops = 2 * cin * cout * ks * ks * n * h * h
+    t = timeit(lambda: p.fwd(dense, cs, 0, hin, hin, y, ocs, 0, n, up=up, act=ACT_LRELU), args.reps)
+    rows.append((f"fwd   {p.name} @{h}", t, flops))
+    dz = torch.randn(n, h, h, p.cin_t, device=dev).to(torch.bfloat16)
+    g = torch.zeros(n, hin, hin, p.cin, device=dev)
+    if up == 1:
+        t = timeit(lambda: p.dgrad(dz, p.cin_t, h, h, g, p.cin, 0, n, accumulate=True), args.reps)
+    else:
+        t = timeit(lambda: p.dgrad(dz, p.cin_t, h, h, g, p.cin, 0, n, accumulate=True, down2=True), args.reps)
+    rows.append((f"dgrad {p.name} @{h}", t, flops))
+    t = timeit(lambda: p.wgrad(dense, cs, 0, hin, hin, dz, p.cin_t, n, ws, accumulate=False, up=up), args.reps)
+    rows.append((f"wgrad {p.name} @{h}", t, flops))
+for name, t, f in rows:
+    print(f"{name:32s} {t:9.1f} us  {f / t / 1e6:8.1f} TFLOP/s")
