@@ -65,6 +65,28 @@ SIGNATURES = {
     "climsr_adamw_hparams": (c_int, [c_void_p, c_int, c_double, c_double, c_double, c_double, c_double, c_double, c_double,
                                      c_void_p, c_void_p]),
     "climsr_adamw_step": (c_int, [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "climsr_bn_forward": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_int, c_float, c_float, c_float, c_void_p,
+                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "climsr_bn_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_float,
+                                   c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "climsr_adaptive_pool_fwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
+                                         c_void_p]),
+    "climsr_adaptive_pool_bwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "climsr_linear_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p, c_int64,
+                                  c_void_p, c_void_p]),
+    "climsr_linear_dgrad": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
+    "climsr_linear_wgrad": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
+    "climsr_d_head_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "climsr_d_head_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p,
+                                  c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "climsr_relativistic_bce": (c_int, [c_void_p, c_void_p, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
+                                        c_void_p]),
+    "climsr_maxpool2_bf16": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "climsr_l1_loss_bf16": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
+    "climsr_f32_to_bf16": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
+    "climsr_bn_inference": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_int, c_float,
+                                    c_void_p, c_void_p]),
+    "climsr_increment_i64": (c_int, [c_void_p, c_void_p]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

@@ -1,0 +1,94 @@
+"""Task base (mirror of ``climsr.core.task.TaskSuperResolutionModule``, task.py:109-260).
+
+Keeps the reference's step API: ``forward(x, elevation, mask)`` (task.py:235-239),
+``common_step(batch) -> (hr, sr)`` (task.py:241-260) with batch keys ``lr, hr, elevation, mask``
+(climsr/consts/batch_items.py:2-5), and ``configure_optimizers`` returning one AdamW +
+OneCycleLR(interval="step") per network (task.py:173-226, 53-59).  Subclasses a
+``pytorch_lightning.LightningModule`` when Lightning is importable, otherwise a plain
+``nn.Module`` with the few Lightning attributes the step uses (``hparams``, ``log``, ``log_dict``),
+driven by ``climsr_amd.core.trainer.Trainer``.
+
+Divergences (documented in DESIGN.md): the statistics feather read of task.py:146-171 is skipped
+when ``data_path`` has no statistics (synthetic benchmarking); the stand-alone SRCNN
+generator with MSE loss (task.py:141) is outside this build's scope.
+"""
+from __future__ import annotations
+
+from types import SimpleNamespace
+from typing import Any, Dict, List, Optional, Tuple
+
+import torch
+from torch import Tensor
+
+from ..losses.l1 import L1Loss
+from .instantiator import HydraInstantiator
+from .optim import AdamW
+
+try:  # pragma: no cover - not installed in the build image
+    import pytorch_lightning as pl
+
+    _Base = pl.LightningModule
+except ImportError:  # the built-in trainer drives the same API
+    _Base = torch.nn.Module
+
+BATCH_KEYS = ("lr", "hr", "elevation", "mask")
+default_instantiator = HydraInstantiator()
+
+
+class TaskSuperResolutionModule(_Base):
+    def __init__(self, generator, optimizers: Optional[Dict[str, Any]] = None, schedulers: Optional[Dict[str, Any]] = None,
+                 discriminator=None, instantiator=default_instantiator, **kwargs):
+        super().__init__()
+        self.instantiator = instantiator
+        self.optimizer_cfgs = optimizers or {}
+        self.scheduler_cfgs = schedulers or {}
+        self.generator = instantiator.instantiate(generator)
+        self.discriminator = instantiator.instantiate(discriminator) if discriminator is not None else None
+        hp = dict(generator_type="esrgan")
+        hp.update(kwargs)
+        if _Base is torch.nn.Module:
+            self.hparams = SimpleNamespace(**hp)
+        else:  # pragma: no cover
+            self.save_hyperparameters(*kwargs.keys())
+        if getattr(self.hparams, "generator_type", "esrgan") == "srcnn":
+            raise NotImplementedError("stand-alone SRCNN + MSE task is outside this build's scope (SURVEY §2)")
+        self.loss = L1Loss()  # task.py:141
+        self.logged: Dict[str, Tensor] = {}
+
+    # -- Lightning-compat helpers (no host sync: values are kept as device tensors)
+    if _Base is torch.nn.Module:
+        def log(self, name, value, **kwargs):
+            self.logged[name] = value.detach() if isinstance(value, Tensor) else value
+
+        def log_dict(self, d, **kwargs):
+            for k, v in d.items():
+                self.log(k, v)
+
+    def forward(self, x: Tensor, elevation: Tensor = None, mask: Tensor = None) -> Tensor:
+        return self.generator(x, elevation, mask)
+
+    def common_step(self, batch: Dict[str, Tensor]) -> Tuple[Tensor, Tensor]:
+        lr, hr, elev, mask = (batch[k] for k in BATCH_KEYS)
+        sr = self(lr, elev, mask)
+        return hr, sr
+
+    def configure_optimizers(self, num_training_steps: int = 1000):
+        """AdamW (native, lr/betas/eps/weight_decay as conf/optimizers/adamw.yaml) + torch OneCycleLR
+        (conf/schedulers/one_cycle_schedule.yaml) per network, interval "step"."""
+        opts: List[torch.optim.Optimizer] = []
+        scheds: List[Dict[str, Any]] = []
+        nets = [("generator", self.generator)]
+        if self.discriminator is not None:
+            nets.append(("discriminator", self.discriminator))
+        for name, net in nets:
+            ocfg = dict(self.optimizer_cfgs.get(f"{name}_optimizer") or {"lr": 1e-4, "weight_decay": 1e-4})
+            scfg = dict(self.scheduler_cfgs.get(f"{name}_scheduler") or {"max_lr": ocfg.get("lr", 1e-4), "pct_start": 0.05,
+                                                                          "div_factor": 2, "final_div_factor": 100})
+            ocfg.pop("_target_", None)
+            opt = AdamW(net.parameters(), owner=net, **ocfg)
+            for k in ("_target_", "num_training_steps", "num_warmup_steps", "epochs"):
+                scfg.pop(k, None)
+            sch = torch.optim.lr_scheduler.OneCycleLR(opt, total_steps=num_training_steps, **scfg)
+            opts.append(opt)
+            scheds.append({"scheduler": sch, "interval": "step"})
+        return opts, scheds

@@ -1,0 +1,46 @@
+"""Built-in trainer loop with Lightning-1.x automatic-optimisation semantics (used when
+pytorch_lightning is absent, and by bench.py).  Per batch and per optimizer i:
+toggle (only optimizer i's params require grad), zero_grad, training_step(batch, idx[, i]),
+backward, optimizer i step; then every scheduler steps (interval "step", task.py:58-59).
+"""
+from __future__ import annotations
+
+from typing import Any, Dict, Iterable, List
+
+
+class Trainer:
+    def __init__(self, module, num_training_steps: int = 1000):
+        self.module = module
+        self.optimizers, self.schedulers = module.configure_optimizers(num_training_steps)
+        self.nets = [module.generator] + ([module.discriminator] if module.discriminator is not None else [])
+
+    def _toggle(self, i: int) -> None:
+        for j, net in enumerate(self.nets):
+            for p in net.parameters():
+                p.requires_grad_(j == i)
+
+    def training_batch(self, batch: Dict[str, Any], batch_idx: int) -> List[Any]:
+        outs = []
+        nopt = len(self.optimizers)
+        for i, opt in enumerate(self.optimizers):
+            if nopt > 1:
+                self._toggle(i)
+            opt.zero_grad(set_to_none=True)
+            out = self.module.training_step(batch, batch_idx, i) if nopt > 1 else self.module.training_step(batch, batch_idx)
+            loss = out["loss"] if isinstance(out, dict) else out
+            loss.backward()
+            opt.step()
+            outs.append(out)
+        if nopt > 1:
+            for net in self.nets:
+                for p in net.parameters():
+                    p.requires_grad_(True)
+        for s in self.schedulers:
+            s["scheduler"].step()
+        return outs
+
+    def fit(self, batches: Iterable[Dict[str, Any]]):
+        outs = []
+        for idx, b in enumerate(batches):
+            outs.append(self.training_batch(b, idx))
+        return outs

@@ -249,14 +249,18 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
 #pragma unroll
   for (int m = 0; m < MW; ++m) pixbase[m] = ((wave * MW + m) * a.stride * a.tpw + col * a.stride) * a.ccp;
 
-  const int lh = a.in_h * a.up, lw = a.in_w * a.up;
+  // up = 2: nearest x2 upsample on load (src = j >> 1); up = -2: zero insertion (src = j >> 1 for even j,
+  // else 0) = the input of the data gradient of a stride-2 conv
+  const int ufac = a.up < 0 ? -a.up : a.up;
+  const int lh = a.in_h * ufac, lw = a.in_w * ufac;
   const int iy0 = oy0 * a.stride - a.pad, ix0 = ox0 * a.stride - a.pad;
   const int cvec = a.cc / 8;
+  const int dilmask = a.up < 0 ? 1 : 0;
   const int nvec_x = a.tph * a.tpw * cvec;
   const int wvec_row = a.kcpad / 8;
   const int nvec_w = NT * 16 * wvec_row;
   const int nvec = nvec_x + nvec_w;
-  const int upsh = a.up == 2 ? 1 : 0;
+  const int upsh = ufac == 2 ? 1 : 0;
 
   // staging = one flat space of 16 B vectors: [0, nvec_x) input tile, [nvec_x, nvec) weight chunk
   auto gload = [&](int j, int v) -> uint4 {
@@ -268,7 +272,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
       int iy = iy0 + ty_, ix = ix0 + tx_;
       int c = j * a.cc + cg * 8;
       uint4 val = make_uint4(0, 0, 0, 0);
-      if (iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c) {
+      if (iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c && !((iy | ix) & dilmask)) {
         long src = (((long)nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + c;
         val = *(const uint4*)(a.x + src);
       }
@@ -497,7 +501,8 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
     set_error("conv2d_fwd: null argument");
     return CLIMSR_EINVAL;
   }
-  if (d->in_c % 8 || d->in_cstride % 8 || d->in_coff % 8 || d->cc % 8 || d->cc <= 0 || (d->up != 1 && d->up != 2) ||
+  if (d->in_c % 8 || d->in_cstride % 8 || d->in_coff % 8 || d->cc % 8 || d->cc <= 0 ||
+      (d->up != 1 && d->up != 2 && d->up != -2) ||
       (d->stride != 1 && d->stride != 2) || d->ks < 1 || d->n <= 0 || d->out_c <= 0 || d->in_coff + d->in_c > d->in_cstride) {
     set_error("conv2d_fwd: unsupported geometry (in_c=%d cs=%d coff=%d cc=%d up=%d stride=%d ks=%d)", d->in_c, d->in_cstride,
               d->in_coff, d->cc, d->up, d->stride, d->ks);
@@ -609,7 +614,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs a) {
     tapoff[u] = ((tap / a.ks) * a.tpw + (tap % a.ks)) * WG_XP;
   }
 
-  const int lh = a.in_h * a.up, lw = a.in_w * a.up;
+  const int lh = a.in_h * a.up, lw = a.in_w * a.up;  // up in {1, 2} here
   const int upsh = a.up == 2 ? 1 : 0;
   const int zvec = NTC * 2;  // 16B vectors of dz per pixel
   const int nvec_x = a.tph * a.tpw * 2;

@@ -1,0 +1,754 @@
+// Discriminator / perceptual-loss / GAN-loss kernels for CDNA4 (gfx950).
+//
+// Replaces, on the RFB-ESRGAN discriminator path (climsr/models/rfb_esrgan.py:26-69) and the GAN
+// task (climsr/task/pl_gan.py:28-61): nn.BatchNorm2d (train-mode batch statistics, running-stat
+// update), nn.AdaptiveAvgPool2d((14,14)), nn.Linear(100352,1024) + LeakyReLU + Linear(1024,1) +
+// Sigmoid, BCEWithLogitsLoss on the relativistic logits, and for the perceptual loss
+// (climsr/losses/perceptual.py) VGG's MaxPool2d(2,2) and the L1 between bf16 feature maps.
+// Deterministic: every reduction is a fixed-shape tree with fp64 partials.
+#include <math.h>
+
+#include "common.h"
+
+using namespace climsr;
+
+namespace {
+
+constexpr int BN_BLOCKS = 256;
+
+__device__ inline void unpack8(uint4 u, float* f) {
+  uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = bf2f((uint16_t)(w[i >> 1] >> ((i & 1) * 16)));
+}
+
+__device__ inline uint4 pack8(const float* f) {
+  uint4 u;
+  u.x = f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16);
+  u.y = f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16);
+  u.z = f2bf(f[4]) | ((uint32_t)f2bf(f[5]) << 16);
+  u.w = f2bf(f[6]) | ((uint32_t)f2bf(f[7]) << 16);
+  return u;
+}
+
+// ---------------------------------------------------------------------------------------------
+// BatchNorm statistics: per-channel sum / sum of squares over npix rows of an NHWC [npix][c]
+// tensor.  Block b owns a fixed pixel range; threads = (c/8 channel groups) x rows.  Partials are
+// fp64 [BN_BLOCKS][2][c]; the finish kernel sums them in block order.
+// mode 0: x = z (bf16), stats of z.  mode 1 (backward): d = da * lrelu'(a) (da fp32, a bf16),
+// xhat = (z-mean)*rstd; sums of d and d*xhat.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void bn_partial_kernel(long npix, int c, const uint16_t* __restrict__ z,
+                                                         const float* __restrict__ da, const uint16_t* __restrict__ a,
+                                                         const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                         float slope, int mode, double* __restrict__ part) {
+  extern __shared__ double shd[];  // [256][16]
+  const int groups = c / 8;
+  const int rows = 256 / groups;  // c <= 2048 -> groups <= 256
+  const int tid = threadIdx.x;
+  const int cg = tid % groups;
+  const int r = tid / groups;
+  const long p0 = (long)blockIdx.x * npix / gridDim.x;
+  const long p1 = (long)(blockIdx.x + 1) * npix / gridDim.x;
+  double s[8], q[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { s[i] = 0.0; q[i] = 0.0; }
+  float mu[8], rs[8];
+  if (mode == 1) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { mu[i] = mean[cg * 8 + i]; rs[i] = rstd[cg * 8 + i]; }
+  }
+  if (r < rows) {
+    for (long p = p0 + r; p < p1; p += rows) {
+      float zf[8];
+      unpack8(*(const uint4*)(z + p * c + cg * 8), zf);
+      if (mode == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { s[i] += zf[i]; q[i] += (double)zf[i] * zf[i]; }
+      } else {
+        float af[8];
+        unpack8(*(const uint4*)(a + p * c + cg * 8), af);
+        const float4* dp = (const float4*)(da + p * c + cg * 8);
+        float4 d0 = dp[0], d1 = dp[1];
+        float dd[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float d = af[i] > 0.f ? dd[i] : dd[i] * slope;
+          float xh = (zf[i] - mu[i]) * rs[i];
+          s[i] += d;
+          q[i] += (double)d * xh;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { shd[tid * 16 + i] = s[i]; shd[tid * 16 + 8 + i] = q[i]; }
+  __syncthreads();
+  if (tid < groups) {
+    double ts[8], tq[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { ts[i] = 0.0; tq[i] = 0.0; }
+    for (int rr = 0; rr < rows; ++rr) {
+      const double* src = shd + (rr * groups + tid) * 16;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { ts[i] += src[i]; tq[i] += src[8 + i]; }
+    }
+    double* out = part + (long)blockIdx.x * 2 * c;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { out[tid * 8 + i] = ts[i]; out[c + tid * 8 + i] = tq[i]; }
+  }
+}
+
+__global__ void bn_finish_stats_kernel(const double* __restrict__ part, int nblk, int c, long npix, float eps,
+                                       float momentum, float* mean, float* rstd, float* run_mean, float* run_var,
+                                       float* nbt) {
+  int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= c) return;
+  double s = 0.0, q = 0.0;
+  for (int b = 0; b < nblk; ++b) { s += part[(long)b * 2 * c + ch]; q += part[(long)b * 2 * c + c + ch]; }
+  double m = s / (double)npix;
+  double var = q / (double)npix - m * m;
+  if (var < 0.0) var = 0.0;
+  mean[ch] = (float)m;
+  rstd[ch] = (float)(1.0 / sqrt(var + (double)eps));
+  if (run_mean) {
+    double unb = npix > 1 ? var * (double)npix / (double)(npix - 1) : var;
+    run_mean[ch] = (float)((1.0 - momentum) * run_mean[ch] + momentum * m);
+    run_var[ch] = (float)((1.0 - momentum) * run_var[ch] + momentum * unb);
+  }
+  (void)nbt;
+}
+
+__global__ void bn_apply_kernel(long npix, int c, const uint16_t* __restrict__ z, const float* __restrict__ mean,
+                                const float* __restrict__ rstd, const float* __restrict__ gamma, const float* __restrict__ beta,
+                                int act, float slope, uint16_t* __restrict__ y) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int groups = c / 8;
+  if (idx >= npix * groups) return;
+  const long p = idx / groups;
+  const int c0 = (int)(idx % groups) * 8;
+  float f[8];
+  unpack8(*(const uint4*)(z + p * c + c0), f);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    float v = (f[i] - mean[c0 + i]) * rstd[c0 + i] * gamma[c0 + i] + beta[c0 + i];
+    f[i] = act_apply(v, act, slope);
+  }
+  *(uint4*)(y + p * c + c0) = pack8(f);
+}
+
+__global__ void bn_bwd_finish_kernel(const double* __restrict__ part, int nblk, int c, long npix, const float* __restrict__ gamma,
+                                     const float* __restrict__ rstd, float* dgamma, float* dbeta, int accumulate,
+                                     float* coef) {
+  int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= c) return;
+  double s = 0.0, q = 0.0;
+  for (int b = 0; b < nblk; ++b) { s += part[(long)b * 2 * c + ch]; q += part[(long)b * 2 * c + c + ch]; }
+  if (dgamma) dgamma[ch] = (accumulate ? dgamma[ch] : 0.f) + (float)q;
+  if (dbeta) dbeta[ch] = (accumulate ? dbeta[ch] : 0.f) + (float)s;
+  // dz = gamma*rstd * (d - s/n - xhat*q/n)
+  coef[ch] = gamma[ch] * rstd[ch];
+  coef[c + ch] = (float)(s / (double)npix);
+  coef[2 * c + ch] = (float)(q / (double)npix);
+}
+
+__global__ void bn_bwd_apply_kernel(long npix, int c, const float* __restrict__ da, const uint16_t* __restrict__ a,
+                                    const uint16_t* __restrict__ z, const float* __restrict__ mean, const float* __restrict__ rstd,
+                                    const float* __restrict__ coef, float slope, uint16_t* __restrict__ dz) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int groups = c / 8;
+  if (idx >= npix * groups) return;
+  const long p = idx / groups;
+  const int c0 = (int)(idx % groups) * 8;
+  float zf[8], af[8], o[8];
+  unpack8(*(const uint4*)(z + p * c + c0), zf);
+  unpack8(*(const uint4*)(a + p * c + c0), af);
+  const float4* dp = (const float4*)(da + p * c + c0);
+  float4 d0 = dp[0], d1 = dp[1];
+  float dd[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int ch = c0 + i;
+    float d = af[i] > 0.f ? dd[i] : dd[i] * slope;
+    float xh = (zf[i] - mean[ch]) * rstd[ch];
+    o[i] = coef[ch] * (d - coef[c + ch] - xh * coef[2 * c + ch]);
+  }
+  *(uint4*)(dz + p * c + c0) = pack8(o);
+}
+
+}  // namespace
+
+extern "C" int climsr_bn_forward(const uint16_t* z, int64_t npix, int c, const float* gamma, const float* beta, int act, float slope,
+                                 float eps, float momentum, double* workspace, float* mean, float* rstd, float* run_mean,
+                                 float* run_var, uint16_t* y, void* stream) {
+  if (!z || !gamma || !beta || !workspace || !mean || !rstd || !y || c % 8 || c > 2048 || npix <= 0) {
+    set_error("bn_forward: bad args (c=%d)", c);
+    return CLIMSR_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(bn_partial_kernel, dim3(BN_BLOCKS), dim3(256), 256 * 16 * sizeof(double), s, (long)npix, c, z, nullptr,
+                     nullptr, nullptr, nullptr, 0.f, 0, workspace);
+  hipLaunchKernelGGL(bn_finish_stats_kernel, dim3(ceil_div(c, 256)), dim3(256), 0, s, workspace, BN_BLOCKS, c, (long)npix, eps,
+                     momentum, mean, rstd, run_mean, run_var, nullptr);
+  long total = (long)npix * (c / 8);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, s, (long)npix, c, z, mean, rstd, gamma, beta, act,
+                     slope, y);
+  return check_launch("bn_forward");
+}
+
+__global__ void bn_inference_kernel(long npix, int c, const uint16_t* __restrict__ z, const float* __restrict__ rm,
+                                    const float* __restrict__ rv, float eps, const float* __restrict__ gamma,
+                                    const float* __restrict__ beta, int act, float slope, uint16_t* __restrict__ y) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int groups = c / 8;
+  if (idx >= npix * groups) return;
+  const long p = idx / groups;
+  const int c0 = (int)(idx % groups) * 8;
+  float f[8];
+  unpack8(*(const uint4*)(z + p * c + c0), f);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int ch = c0 + i;
+    float v = (f[i] - rm[ch]) * rsqrtf(rv[ch] + eps) * gamma[ch] + beta[ch];
+    f[i] = act_apply(v, act, slope);
+  }
+  *(uint4*)(y + p * c + c0) = pack8(f);
+}
+
+extern "C" int climsr_bn_inference(const uint16_t* z, int64_t npix, int c, const float* run_mean, const float* run_var, float eps,
+                                   const float* gamma, const float* beta, int act, float slope, uint16_t* y, void* stream) {
+  if (!z || !run_mean || !run_var || !gamma || !beta || !y || c % 8) {
+    set_error("bn_inference: bad args");
+    return CLIMSR_EINVAL;
+  }
+  long total = (long)npix * (c / 8);
+  hipLaunchKernelGGL(bn_inference_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, (long)npix, c, z, run_mean,
+                     run_var, eps, gamma, beta, act, slope, y);
+  return check_launch("bn_inference");
+}
+
+extern "C" int climsr_bn_backward(const float* da, const uint16_t* a, const uint16_t* z, int64_t npix, int c, const float* mean,
+                                  const float* rstd, const float* gamma, float slope, double* workspace, float* coef,
+                                  float* dgamma, float* dbeta, int accumulate, uint16_t* dz, void* stream) {
+  if (!da || !a || !z || !mean || !rstd || !gamma || !workspace || !coef || !dz || c % 8 || c > 2048) {
+    set_error("bn_backward: bad args");
+    return CLIMSR_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(bn_partial_kernel, dim3(BN_BLOCKS), dim3(256), 256 * 16 * sizeof(double), s, (long)npix, c, z, da, a, mean,
+                     rstd, slope, 1, workspace);
+  hipLaunchKernelGGL(bn_bwd_finish_kernel, dim3(ceil_div(c, 256)), dim3(256), 0, s, workspace, BN_BLOCKS, c, (long)npix, gamma,
+                     rstd, dgamma, dbeta, accumulate, coef);
+  long total = (long)npix * (c / 8);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, s, (long)npix, c, da, a, z, mean, rstd, coef,
+                     slope, dz);
+  return check_launch("bn_backward");
+}
+
+// ---------------------------------------------------------------------------------------------
+// nn.AdaptiveAvgPool2d((oh, ow)) on NHWC bf16, output flattened in torch's NCHW order
+// (torch.flatten(out, 1), rfb_esrgan.py:65-66): out[n][(c*oh + i)*ow + j]; optional transposed
+// copy out_t[(c*oh+i)*ow+j][n_pad] for the fc weight gradient.  Window i = [i*H/oh, ceil((i+1)*H/oh)).
+// ---------------------------------------------------------------------------------------------
+__global__ void adaptive_pool_fwd_kernel(const uint16_t* __restrict__ x, int n, int h, int w, int c, int oh, int ow,
+                                         uint16_t* __restrict__ out, uint16_t* __restrict__ out_t, int n_pad) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;  // over n * oh * ow * c (c fastest: coalesced reads)
+  long total = (long)n * oh * ow * c;
+  if (idx >= total) return;
+  const int ch = (int)(idx % c);
+  long t = idx / c;
+  const int j = (int)(t % ow);
+  t /= ow;
+  const int i = (int)(t % oh);
+  const int b = (int)(t / oh);
+  const int y0 = (i * h) / oh, y1 = ((i + 1) * h + oh - 1) / oh;
+  const int x0 = (j * w) / ow, x1 = ((j + 1) * w + ow - 1) / ow;
+  float s = 0.f;
+  for (int yy = y0; yy < y1; ++yy)
+    for (int xx = x0; xx < x1; ++xx) s += bf2f(x[(((long)b * h + yy) * w + xx) * c + ch]);
+  s /= (float)((y1 - y0) * (x1 - x0));
+  const long f = ((long)ch * oh + i) * ow + j;
+  const uint16_t v = f2bf(s);
+  out[(long)b * c * oh * ow + f] = v;
+  if (out_t) out_t[f * n_pad + b] = v;
+}
+
+__global__ void adaptive_pool_bwd_kernel(const float* __restrict__ dp, int n, int h, int w, int c, int oh, int ow,
+                                         float* __restrict__ dx) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;  // over n*h*w*c
+  long total = (long)n * h * w * c;
+  if (idx >= total) return;
+  const int ch = (int)(idx % c);
+  long t = idx / c;
+  const int xx = (int)(t % w);
+  t /= w;
+  const int yy = (int)(t % h);
+  const int b = (int)(t / h);
+  float s = 0.f;
+  // output windows containing (yy, xx): i with floor(i*h/oh) <= yy < ceil((i+1)*h/oh); the candidates
+  // lie in [floor(yy*oh/h) - 1, ceil((yy+1)*oh/h)] (covers both shrinking and growing pools)
+  const int ilo = max(0, (yy * oh) / h - 1), ihi = min(oh - 1, ((yy + 1) * oh + h - 1) / h);
+  const int jlo = max(0, (xx * ow) / w - 1), jhi = min(ow - 1, ((xx + 1) * ow + w - 1) / w);
+  for (int i = ilo; i <= ihi; ++i) {
+    const int y0 = (i * h) / oh, y1 = ((i + 1) * h + oh - 1) / oh;
+    if (yy < y0 || yy >= y1) continue;
+    for (int j = jlo; j <= jhi; ++j) {
+      const int x0 = (j * w) / ow, x1 = ((j + 1) * w + ow - 1) / ow;
+      if (xx < x0 || xx >= x1) continue;
+      s += dp[(long)b * c * oh * ow + ((long)ch * oh + i) * ow + j] / (float)((y1 - y0) * (x1 - x0));
+    }
+  }
+  dx[idx] = s;
+}
+
+extern "C" int climsr_adaptive_pool_fwd(const uint16_t* x, int n, int h, int w, int c, int oh, int ow, uint16_t* out,
+                                        uint16_t* out_t, int n_pad, void* stream) {
+  if (!x || !out || oh <= 0 || ow <= 0 || (out_t && n_pad < n)) {
+    set_error("adaptive_pool_fwd: bad args");
+    return CLIMSR_EINVAL;
+  }
+  long total = (long)n * oh * ow * c;
+  hipLaunchKernelGGL(adaptive_pool_fwd_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, x, n, h, w, c, oh, ow,
+                     out, out_t, n_pad);
+  return check_launch("adaptive_pool_fwd");
+}
+
+extern "C" int climsr_adaptive_pool_bwd(const float* dp, int n, int h, int w, int c, int oh, int ow, float* dx, void* stream) {
+  if (!dp || !dx || oh <= 0 || ow <= 0) {
+    set_error("adaptive_pool_bwd: bad args");
+    return CLIMSR_EINVAL;
+  }
+  long total = (long)n * h * w * c;
+  hipLaunchKernelGGL(adaptive_pool_bwd_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, dp, n, h, w, c, oh,
+                     ow, dx);
+  return check_launch("adaptive_pool_bwd");
+}
+
+// ---------------------------------------------------------------------------------------------
+// Linear layers (nn.Linear(100352, 1024), rfb_esrgan.py:57) on MFMA 16x16x32 bf16.
+// forward: y[n][o] = act(sum_k x[n][k] W[o][k] + b[o]); split-K partials, then reduce.
+//   A = W rows (o), B = x rows (n); both k-contiguous -> straight 16 B global loads, no LDS.
+//   Workgroup = 4 waves x 16 o; each wave keeps NF = n_pad/16 accumulators.
+// ---------------------------------------------------------------------------------------------
+template <int NF>
+__global__ __launch_bounds__(256) void linear_fwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, int n, int k,
+                                                         int o, int ksplit, float* __restrict__ part) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
+  const int o0 = blockIdx.x * 64 + wave * 16;
+  const int split = blockIdx.y;
+  const int kb = split * ksplit, ke = min(k, kb + ksplit);
+  f32x4 acc[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) acc[f] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const uint16_t* wrow = w + (long)(o0 + col) * k + g * 8;
+  const bool orow_ok = o0 + col < o;
+  for (int kk = kb; kk < ke; kk += 32) {
+    bf16x8 af = orow_ok ? *(const bf16x8*)(wrow + kk) : (bf16x8){};
+    bf16x8 bfr[NF];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const int nn = f * 16 + col;
+      bfr[f] = nn < n ? *(const bf16x8*)(x + (long)nn * k + kk + g * 8) : (bf16x8){};
+    }
+#pragma unroll
+    for (int f = 0; f < NF; ++f) acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[f], acc[f], 0, 0, 0);
+  }
+  // C: row = o (4g+i), col = n
+  float* dst = part + (long)split * n * o;
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    const int nn = f * 16 + col;
+    if (nn >= n) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int oo = o0 + g * 4 + i;
+      if (oo < o) dst[(long)nn * o + oo] = acc[f][i];
+    }
+  }
+}
+
+__global__ void linear_reduce_kernel(const float* __restrict__ part, int nsplit, int n, int o, const float* __restrict__ bias, int act,
+                                     float slope, float* __restrict__ y, uint16_t* __restrict__ ybf) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)n * o) return;
+  float s = 0.f;
+  for (int sp = 0; sp < nsplit; ++sp) s += part[(long)sp * n * o + idx];
+  if (bias) s += bias[idx % o];
+  s = act_apply(s, act, slope);
+  y[idx] = s;
+  if (ybf) ybf[idx] = f2bf(s);
+}
+
+extern "C" int climsr_linear_fwd(const uint16_t* x, const uint16_t* w, const float* bias, int n, int k, int o, int act, float slope,
+                                 float* workspace, int64_t ws_floats, float* y, void* stream) {
+  if (!x || !w || !y || !workspace || n <= 0 || n > 64 || k % 32 || o % 16) {
+    set_error("linear_fwd: bad args (n=%d k=%d o=%d; need n<=64, k%%32==0, o%%16==0)", n, k, o);
+    return CLIMSR_EINVAL;
+  }
+  const int oblk = ceil_div(o, 64);
+  int nsplit = ceil_div(1024, oblk);
+  int ksplit = round_up(ceil_div(k, nsplit), 32);
+  nsplit = ceil_div(k, ksplit);
+  if ((int64_t)nsplit * n * o > ws_floats) {
+    set_error("linear_fwd: workspace too small (%lld floats needed)", (long long)nsplit * n * o);
+    return CLIMSR_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int nf = (n + 15) / 16;
+  dim3 grid(oblk, nsplit);
+  if (nf == 1) hipLaunchKernelGGL(linear_fwd_kernel<1>, grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
+  else if (nf == 2) hipLaunchKernelGGL(linear_fwd_kernel<2>, grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
+  else hipLaunchKernelGGL(linear_fwd_kernel<4>, grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
+  hipLaunchKernelGGL(linear_reduce_kernel, dim3(ceil_div((long)n * o, 256)), dim3(256), 0, s, workspace, nsplit, n, o, bias, act, slope,
+                     y, (uint16_t*)nullptr);
+  return check_launch("linear_fwd");
+}
+
+// data gradient dx[n][k] = sum_o dy[n][o] W[o][k]:  A = dy rows (n, o-contiguous), B = W^T taken
+// from an LDS tile of W [o][64 k] with ds_read_b64_tr_b16.  Workgroup: 64 k (one 16-col frag per
+// wave) x n_pad rows, loop over o in 128-row LDS tiles.
+template <int NF>
+__global__ __launch_bounds__(256) void linear_dgrad_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ w, int n, int k,
+                                                           int o, float* __restrict__ dx, int accumulate) {
+  __shared__ __attribute__((aligned(16))) uint16_t ws_[128 * 72];  // 128 o rows x 64 k (+8 pad)
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
+  const int q = (lane & 15) >> 2, p = lane & 3;
+  const int k0 = blockIdx.x * 64;
+  f32x4 acc[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) acc[f] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int ob = 0; ob < o; ob += 128) {
+    __syncthreads();
+    // stage W[ob..ob+128][k0..k0+64]: 128 rows x 8 vectors
+    uint4 buf[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int v = tid + i * 256;
+      const int r = v >> 3, cv = v & 7;
+      buf[i] = (ob + r < o && k0 + cv * 8 < k) ? *(const uint4*)(w + (long)(ob + r) * k + k0 + cv * 8) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int v = tid + i * 256;
+      *(uint4*)(ws_ + (v >> 3) * 72 + (v & 7) * 8) = buf[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {  // 4 k-steps of 32 o
+      const int orow = ks * 32 + 8 * g + q;
+      s16x4 lo = ds_read_tr16(ws_ + orow * 72 + wave * 16 + 4 * p);
+      s16x4 hi = ds_read_tr16(ws_ + (orow + 4) * 72 + wave * 16 + 4 * p);
+      short v8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      bf16x8 bfr = __builtin_bit_cast(bf16x8, v8);
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        const int nn = f * 16 + col;
+        const int oo = ob + ks * 32 + g * 8;
+        bf16x8 af = (nn < n && oo < o) ? *(const bf16x8*)(dy + (long)nn * o + oo) : (bf16x8){};
+        acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[f], 0, 0, 0);
+      }
+    }
+  }
+  // C: row = n (4g+i within frag f), col = k
+  const int kk = k0 + wave * 16 + col;
+  if (kk >= k) return;
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int nn = f * 16 + g * 4 + i;
+      if (nn < n) {
+        float* d = dx + (long)nn * k + kk;
+        *d = (accumulate ? *d : 0.f) + acc[f][i];
+      }
+    }
+  }
+}
+
+extern "C" int climsr_linear_dgrad(const uint16_t* dy, const uint16_t* w, int n, int k, int o, float* dx, int accumulate,
+                                   void* stream) {
+  if (!dy || !w || !dx || n <= 0 || n > 64 || k % 64 || o % 32) {
+    set_error("linear_dgrad: bad args (n=%d k=%d o=%d)", n, k, o);
+    return CLIMSR_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int nf = (n + 15) / 16;
+  dim3 grid(k / 64);
+  if (nf == 1) hipLaunchKernelGGL(linear_dgrad_kernel<1>, grid, dim3(256), 0, s, dy, w, n, k, o, dx, accumulate);
+  else if (nf == 2) hipLaunchKernelGGL(linear_dgrad_kernel<2>, grid, dim3(256), 0, s, dy, w, n, k, o, dx, accumulate);
+  else hipLaunchKernelGGL(linear_dgrad_kernel<4>, grid, dim3(256), 0, s, dy, w, n, k, o, dx, accumulate);
+  return check_launch("linear_dgrad");
+}
+
+// weight gradient dW[o][k] (+)= sum_n dy[n][o] x[n][k] with K = n_pad (multiple of 32):
+// A = dy^T [o][n_pad], B = x^T [k][n_pad] (both n-contiguous).  Each wave: 16 o x 64 k.
+__global__ __launch_bounds__(256) void linear_wgrad_kernel(const uint16_t* __restrict__ dyt, const uint16_t* __restrict__ xt, int n_pad,
+                                                           int k, int o, float* __restrict__ dw, int accumulate) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
+  const int o0 = blockIdx.y * 64 + wave * 16;
+  const int k0 = blockIdx.x * 64;
+  f32x4 acc[4];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) acc[f] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int nb = 0; nb < n_pad; nb += 32) {
+    bf16x8 af = *(const bf16x8*)(dyt + (long)(o0 + col) * n_pad + nb + g * 8);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      bf16x8 bfr = *(const bf16x8*)(xt + (long)(k0 + f * 16 + col) * n_pad + nb + g * 8);
+      acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[f], 0, 0, 0);
+    }
+  }
+  // C: row = o (4g+i), col = k
+  float4 old[4][1];
+  (void)old;
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    const int kk = k0 + f * 16 + col;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float* d = dw + (long)(o0 + g * 4 + i) * k + kk;
+      *d = (accumulate ? *d : 0.f) + acc[f][i];
+    }
+  }
+}
+
+extern "C" int climsr_linear_wgrad(const uint16_t* dy_t, const uint16_t* x_t, int n_pad, int k, int o, float* dw, int accumulate,
+                                   void* stream) {
+  if (!dy_t || !x_t || !dw || n_pad % 32 || k % 64 || o % 64) {
+    set_error("linear_wgrad: bad args (n_pad=%d k=%d o=%d)", n_pad, k, o);
+    return CLIMSR_EINVAL;
+  }
+  hipLaunchKernelGGL(linear_wgrad_kernel, dim3(k / 64, o / 64), dim3(256), 0, (hipStream_t)stream, dy_t, x_t, n_pad, k, o, dw,
+                     accumulate);
+  return check_launch("linear_wgrad");
+}
+
+// ---------------------------------------------------------------------------------------------
+// Discriminator head after fc.0 + LeakyReLU: s = sigmoid(h . w2 + b2) (rfb_esrgan.py:59-60), and its
+// backward: du = ds*s*(1-s); dw2 += sum_n du h; db2 += sum du; du0 = du*w2*lrelu'(h);
+// db0 += sum_n du0; du0 written as bf16 [n][o] and transposed [o][n_pad] for the fc.0 grads.
+// One workgroup, n <= 64, fixed reduction order.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void d_head_fwd_kernel(const float* __restrict__ h, const float* __restrict__ w2,
+                                                         const float* __restrict__ b2, int n, int o, float* __restrict__ s) {
+  __shared__ float red[256];
+  for (int b = 0; b < n; ++b) {
+    float t = 0.f;
+    for (int j = threadIdx.x; j < o; j += 256) t += h[(long)b * o + j] * w2[j];
+    red[threadIdx.x] = t;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+      if (threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      float u = red[0] + b2[0];
+      s[b] = 1.f / (1.f + expf(-u));
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void d_head_bwd_kernel(const float* __restrict__ h, const float* __restrict__ s, const float* __restrict__ ds,
+                                                         const float* __restrict__ w2, int n, int o, int n_pad, float slope, float* dw2,
+                                                         float* db2, float* db0, int accumulate, uint16_t* __restrict__ du0,
+                                                         uint16_t* __restrict__ du0_t) {
+  for (int j = threadIdx.x; j < o; j += 256) {
+    float a_w2 = 0.f, a_b0 = 0.f;
+    for (int b = 0; b < n_pad; ++b) {
+      float v = 0.f;
+      if (b < n) {
+        const float du = ds[b] * s[b] * (1.f - s[b]);
+        const float hv = h[(long)b * o + j];
+        a_w2 += du * hv;
+        v = du * w2[j] * (hv > 0.f ? 1.f : slope);
+        a_b0 += v;
+        du0[(long)b * o + j] = f2bf(v);
+      }
+      du0_t[(long)j * n_pad + b] = f2bf(v);
+    }
+    if (dw2) dw2[j] = (accumulate ? dw2[j] : 0.f) + a_w2;
+    if (db0) db0[j] = (accumulate ? db0[j] : 0.f) + a_b0;
+  }
+  if (threadIdx.x == 0 && db2) {
+    float t = 0.f;
+    for (int b = 0; b < n; ++b) t += ds[b] * s[b] * (1.f - s[b]);
+    db2[0] = (accumulate ? db2[0] : 0.f) + t;
+  }
+}
+
+extern "C" int climsr_d_head_fwd(const float* h, const float* w2, const float* b2, int n, int o, float* s, void* stream) {
+  if (!h || !w2 || !b2 || !s || n <= 0) {
+    set_error("d_head_fwd: bad args");
+    return CLIMSR_EINVAL;
+  }
+  hipLaunchKernelGGL(d_head_fwd_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, h, w2, b2, n, o, s);
+  return check_launch("d_head_fwd");
+}
+
+extern "C" int climsr_d_head_bwd(const float* h, const float* s, const float* ds, const float* w2, int n, int o, int n_pad, float slope,
+                                 float* dw2, float* db2, float* db0, int accumulate, uint16_t* du0, uint16_t* du0_t, void* stream) {
+  if (!h || !s || !ds || !w2 || !du0 || !du0_t || n_pad < n) {
+    set_error("d_head_bwd: bad args");
+    return CLIMSR_EINVAL;
+  }
+  hipLaunchKernelGGL(d_head_bwd_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, h, s, ds, w2, n, o, n_pad, slope, dw2, db2, db0,
+                     accumulate, du0, du0_t);
+  return check_launch("d_head_bwd");
+}
+
+// ---------------------------------------------------------------------------------------------
+// Relativistic-average BCE-with-logits on the (sigmoid) scores (pl_gan.py:31-38 and :52-59):
+//   rf = s_r - mean(s_f), fr = s_f - mean(s_r)
+//   L = ( BCEwl(fr, t_fr) + BCEwl(rf, t_rf) ) / 2
+// loss_g: t_fr = 1, t_rf = 0;  loss_d: t_fr = 0, t_rf = 1.  With gscale != NULL also writes
+// g_r = gscale * dL/ds_r and g_f = gscale * dL/ds_f.  One workgroup, n <= 1024.
+// ---------------------------------------------------------------------------------------------
+__device__ inline double bcewl(double x, double t) { return fmax(x, 0.0) - x * t + log1p(exp(-fabs(x))); }
+
+__global__ void rel_bce_kernel(const float* __restrict__ sr, const float* __restrict__ sf, int n, float t_rf, float t_fr,
+                               float* __restrict__ loss, const float* __restrict__ gscale, float* __restrict__ gr,
+                               float* __restrict__ gf) {
+  if (threadIdx.x != 0) return;
+  double mr = 0.0, mf = 0.0;
+  for (int i = 0; i < n; ++i) { mr += sr[i]; mf += sf[i]; }
+  mr /= n;
+  mf /= n;
+  double l_rf = 0.0, l_fr = 0.0, sum_drf = 0.0, sum_dfr = 0.0;
+  for (int i = 0; i < n; ++i) {
+    const double rf = sr[i] - mf, fr = sf[i] - mr;
+    l_rf += bcewl(rf, t_rf);
+    l_fr += bcewl(fr, t_fr);
+    sum_drf += 0.5 / n * (1.0 / (1.0 + exp(-rf)) - t_rf);
+    sum_dfr += 0.5 / n * (1.0 / (1.0 + exp(-fr)) - t_fr);
+  }
+  if (loss) loss[0] = (float)((l_rf / n + l_fr / n) / 2.0);
+  if (gscale) {
+    const double gs = gscale[0];
+    for (int i = 0; i < n; ++i) {
+      const double rf = sr[i] - mf, fr = sf[i] - mr;
+      const double drf = 0.5 / n * (1.0 / (1.0 + exp(-rf)) - t_rf);
+      const double dfr = 0.5 / n * (1.0 / (1.0 + exp(-fr)) - t_fr);
+      gr[i] = (float)(gs * (drf - sum_dfr / n));
+      gf[i] = (float)(gs * (dfr - sum_drf / n));
+    }
+  }
+}
+
+extern "C" int climsr_relativistic_bce(const float* s_real, const float* s_fake, int n, float t_rf, float t_fr, float* loss,
+                                       const float* gscale, float* g_real, float* g_fake, void* stream) {
+  if (!s_real || !s_fake || n <= 0 || (gscale && (!g_real || !g_fake))) {
+    set_error("relativistic_bce: bad args");
+    return CLIMSR_EINVAL;
+  }
+  hipLaunchKernelGGL(rel_bce_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, s_real, s_fake, n, t_rf, t_fr, loss, gscale, g_real,
+                     g_fake);
+  return check_launch("relativistic_bce");
+}
+
+// ---------------------------------------------------------------------------------------------
+// VGG19 helpers (perceptual.py): MaxPool2d(2,2) on NHWC bf16, L1 mean between two bf16 tensors.
+// ---------------------------------------------------------------------------------------------
+__global__ void maxpool2_kernel(const uint16_t* __restrict__ x, int n, int h, int w, int c, uint16_t* __restrict__ y) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int oh = h / 2, ow = w / 2, groups = c / 8;
+  long total = (long)n * oh * ow * groups;
+  if (idx >= total) return;
+  const int cg = (int)(idx % groups);
+  long t = idx / groups;
+  const int j = (int)(t % ow);
+  t /= ow;
+  const int i = (int)(t % oh);
+  const int b = (int)(t / oh);
+  float m[8], f[8];
+  unpack8(*(const uint4*)(x + (((long)b * h + 2 * i) * w + 2 * j) * c + cg * 8), m);
+  const int dy[3] = {0, 1, 1}, dx[3] = {1, 0, 1};
+  for (int r = 0; r < 3; ++r) {
+    unpack8(*(const uint4*)(x + (((long)b * h + 2 * i + dy[r]) * w + 2 * j + dx[r]) * c + cg * 8), f);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) m[q] = fmaxf(m[q], f[q]);
+  }
+  *(uint4*)(y + (((long)b * oh + i) * ow + j) * c + cg * 8) = pack8(m);
+}
+
+extern "C" int climsr_maxpool2_bf16(const uint16_t* x, int n, int h, int w, int c, uint16_t* y, void* stream) {
+  if (!x || !y || c % 8 || h % 2 || w % 2) {
+    set_error("maxpool2_bf16: bad args");
+    return CLIMSR_EINVAL;
+  }
+  long total = (long)n * (h / 2) * (w / 2) * (c / 8);
+  hipLaunchKernelGGL(maxpool2_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, x, n, h, w, c, y);
+  return check_launch("maxpool2_bf16");
+}
+
+__global__ void l1_bf16_partial_kernel(const uint16_t* __restrict__ a, const uint16_t* __restrict__ b, long n8, double* ws) {
+  __shared__ double sh[256];
+  double s = 0.0;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    float fa[8], fb[8];
+    unpack8(((const uint4*)a)[i], fa);
+    unpack8(((const uint4*)b)[i], fb);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += fabsf(fa[q] - fb[q]);
+  }
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (threadIdx.x < st) sh[threadIdx.x] += sh[threadIdx.x + st];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) ws[blockIdx.x] = sh[0];
+}
+
+__global__ void l1_bf16_final_kernel(const double* ws, int nb, long n, float* out) {
+  if (threadIdx.x != 0) return;
+  double s = 0.0;
+  for (int i = 0; i < nb; ++i) s += ws[i];
+  out[0] = (float)(s / (double)n);
+}
+
+extern "C" int climsr_l1_loss_bf16(const uint16_t* a, const uint16_t* b, int64_t n, double* workspace, float* out, void* stream) {
+  if (!a || !b || !workspace || !out || n <= 0 || n % 8) {
+    set_error("l1_loss_bf16: bad args");
+    return CLIMSR_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(l1_bf16_partial_kernel, dim3(512), dim3(256), 0, s, a, b, (long)(n / 8), workspace);
+  hipLaunchKernelGGL(l1_bf16_final_kernel, dim3(1), dim3(64), 0, s, workspace, 512, (long)n, out);
+  return check_launch("l1_loss_bf16");
+}
+
+// bf16 copy of an fp32 matrix (the fc.0 weight's MFMA copy), vectorised
+__global__ void f32_to_bf16_kernel(const float* __restrict__ x, long n, uint16_t* __restrict__ y) {
+  long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (i + 7 < n) {
+    float4 a = *(const float4*)(x + i), b = *(const float4*)(x + i + 4);
+    float f[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    *(uint4*)(y + i) = pack8(f);
+  } else {
+    for (long j = i; j < n; ++j) y[j] = f2bf(x[j]);
+  }
+}
+
+__global__ void inc_i64_kernel(int64_t* p) {
+  if (threadIdx.x == 0) p[0] += 1;
+}
+
+extern "C" int climsr_increment_i64(int64_t* p, void* stream) {
+  if (!p) {
+    set_error("increment_i64: null");
+    return CLIMSR_EINVAL;
+  }
+  hipLaunchKernelGGL(inc_i64_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, p);
+  return check_launch("increment_i64");
+}
+
+extern "C" int climsr_f32_to_bf16(const float* x, int64_t n, uint16_t* y, void* stream) {
+  if (!x || !y || n < 0) {
+    set_error("f32_to_bf16: bad args");
+    return CLIMSR_EINVAL;
+  }
+  long threads = (n + 7) / 8;
+  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(ceil_div(threads > 0 ? threads : 1, 256)), dim3(256), 0, (hipStream_t)stream, x, (long)n, y);
+  return check_launch("f32_to_bf16");
+}

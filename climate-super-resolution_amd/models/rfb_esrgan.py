@@ -1,0 +1,261 @@
+"""RFB-ESRGAN discriminator (drop-in for ``climsr.models.rfb_esrgan.RFBESRGANDiscriminator``).
+
+Same constructor (``in_channels=1``), same ``features`` / ``fc`` submodules and ``state_dict`` keys
+(rfb_esrgan.py:26-61), ``forward(x: [N,1,H,W]) -> [N,1]`` in (0,1) (rfb_esrgan.py:63-69), honours
+``.train()`` / ``.eval()`` (batch statistics + running-stat update vs running statistics).  All
+arithmetic runs in libclimsr_hip: implicit-GEMM convs (stride 1/2; the stride-2 data gradient as a
+stride-1 conv over the zero-inserted gradient), BatchNorm fused with LeakyReLU(0.2), the adaptive
+16->14 average pool, fc.0 (100352->1024) on MFMA with split-K, and the LeakyReLU/fc.2/Sigmoid head.
+
+Each call is one autograd node.  Weight/BN-affine gradients land in one flat fp32 buffer and are
+only computed when the parameters require grad (Lightning toggles D off during the generator
+update, pl_gan.py:63-79); the input gradient (into the generator) is computed when the input
+requires grad.
+"""
+from __future__ import annotations
+
+from typing import Dict, List
+
+import torch
+import torch.nn as nn
+from torch import Tensor
+
+from .. import ops
+from ..core.flat import FlatParamsMixin
+from ..ops import ACT_LRELU, BatchedPacker, ConvPlan, Workspace
+
+POOL = 14
+
+
+def _bf16(shape, dev):
+    return torch.empty(shape, dtype=torch.bfloat16, device=dev)
+
+
+def _f32(shape, dev):
+    return torch.empty(shape, dtype=torch.float32, device=dev)
+
+
+class _DEngine:
+    def __init__(self, d: "RFBESRGANDiscriminator"):
+        self.d = d
+        dev = d.fc[0].weight.device
+        self.layers = []  # (conv module, bn module or None, ConvPlan)
+        feats = list(d.features)
+        for i, m in enumerate(feats):
+            if isinstance(m, nn.Conv2d):
+                bn = feats[i + 1] if i + 1 < len(feats) and isinstance(feats[i + 1], nn.BatchNorm2d) else None
+                plan = ConvPlan(m.in_channels, m.out_channels, 3, m.stride[0], 1, f"features.{i}")
+                plan.bind(m.weight, None, need_t=True)
+                self.layers.append((m, bn, plan))
+        self.packer = BatchedPacker([p for _c, _b, p in self.layers], dev)
+        self.fc0_bf16 = torch.empty(d.fc[0].weight.shape, dtype=torch.bfloat16, device=dev)
+        self.version = -1
+        self.ws = Workspace()
+        self.scratch: Dict[str, Tensor] = {}
+
+    def ensure_packed(self):
+        v = self.d._flat._version
+        if v != self.version:
+            self.repack()
+
+    def repack(self):
+        self.packer.run()
+        ops.f32_to_bf16(self.d.fc[0].weight, self.fc0_bf16)
+        self.version = self.d._flat._version
+
+    def _scr(self, key, shape, dtype, dev):
+        t = self.scratch.get(key)
+        if t is None or tuple(t.shape) != tuple(shape) or t.device != dev:
+            t = torch.empty(shape, dtype=dtype, device=dev)
+            self.scratch[key] = t
+        return t
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, x: Tensor, keep: bool, need_pt: bool):
+        d = self.d
+        n, cin, h, w = x.shape
+        dev = x.device
+        self.ensure_packed()
+        cpad = (cin + 7) // 8 * 8
+        x8 = torch.zeros((n, h, w, cpad), dtype=torch.bfloat16, device=dev)
+        ops.nchw_to_nhwc(x.contiguous().float(), x8, cpad, 0)
+        a_prev, cs_prev, hh, ww = x8, cpad, h, w
+        saved = []
+        training = d.training
+        bnws = self._scr("bnws", (256 * 2 * 512,), torch.float64, dev)
+        for conv, bn, plan in self.layers:
+            oh, ow = plan.out_hw(hh, ww)
+            c = plan.cout
+            if bn is None:
+                a = _bf16((n, oh, ow, c), dev)
+                plan.fwd(a_prev, cs_prev, 0, hh, ww, a, c, 0, n, act=ACT_LRELU, use_bias=False)
+                saved.append(dict(a_in=a_prev, cs_in=cs_prev, h_in=hh, w_in=ww, z=None, a=a, mean=None, rstd=None, oh=oh, ow=ow))
+            else:
+                z = _bf16((n, oh, ow, c), dev)
+                plan.fwd(a_prev, cs_prev, 0, hh, ww, z, c, 0, n, use_bias=False)
+                a = _bf16((n, oh, ow, c), dev)
+                npix = n * oh * ow
+                if training:
+                    mean, rstd = _f32((c,), dev), _f32((c,), dev)
+                    ops.bn_forward(z, npix, c, bn.weight, bn.bias, mean, rstd, a, bnws, bn.running_mean, bn.running_var,
+                                   eps=bn.eps, momentum=bn.momentum)
+                    ops.increment_i64(bn.num_batches_tracked)
+                else:
+                    mean = rstd = None
+                    ops.bn_inference(z, npix, c, bn.running_mean, bn.running_var, bn.weight, bn.bias, a, eps=bn.eps)
+                saved.append(dict(a_in=a_prev, cs_in=cs_prev, h_in=hh, w_in=ww, z=z, a=a, mean=mean, rstd=rstd, oh=oh, ow=ow))
+            a_prev, cs_prev, hh, ww = a, c, oh, ow
+        c = cs_prev
+        feat = c * POOL * POOL
+        n_pad = (n + 31) // 32 * 32
+        p = _bf16((n, feat), dev)
+        p_t = torch.zeros((feat, n_pad), dtype=torch.bfloat16, device=dev) if need_pt else None
+        ops.adaptive_pool_fwd(a_prev, n, hh, ww, c, POOL, POOL, p, p_t, n_pad)
+        fc0, fc2 = d.fc[0], d.fc[2]
+        hid = _f32((n, fc0.out_features), dev)
+        nsplit_max = 1024 // ((fc0.out_features + 63) // 64) + 1
+        lin_ws = self._scr("linws", (nsplit_max * n * fc0.out_features,), torch.float32, dev)
+        ops.linear_fwd(p, self.fc0_bf16, fc0.bias, n, feat, fc0.out_features, hid, lin_ws, act=ACT_LRELU, slope=0.2)
+        s = _f32((n, 1), dev)
+        ops.d_head_fwd(hid, fc2.weight, fc2.bias, n, fc0.out_features, s)
+        sv = None
+        if keep:
+            sv = dict(n=n, h=h, w=w, cpad=cpad, layers=saved, p_t=p_t, hid=hid, s=s, n_pad=n_pad, feat=feat, hh=hh, ww=ww, c=c)
+        return s, sv
+
+    # ------------------------------------------------------------------ backward
+    def backward(self, ds: Tensor, sv: dict, need_w: bool, need_x: bool, accumulate: bool):
+        d = self.d
+        dev = ds.device
+        n, n_pad, feat = sv["n"], sv["n_pad"], sv["feat"]
+        fc0, fc2 = d.fc[0], d.fc[2]
+        o = fc0.out_features
+        ds = ds.contiguous().float()
+        du0 = _bf16((n, o), dev)
+        du0_t = torch.zeros((o, n_pad), dtype=torch.bfloat16, device=dev)
+        acc = accumulate
+        ops.d_head_bwd(sv["hid"], sv["s"], ds, fc2.weight, n, o, n_pad, fc2.weight.grad if need_w else None,
+                       fc2.bias.grad if need_w else None, fc0.bias.grad if need_w else None, acc, du0, du0_t)
+        if need_w:
+            ops.linear_wgrad(du0_t, sv["p_t"], n_pad, feat, o, fc0.weight.grad, acc)
+        dp = self._scr("dp", (n, feat), torch.float32, dev)
+        ops.linear_dgrad(du0, self.fc0_bf16, n, feat, o, dp)
+        hh, ww, c = sv["hh"], sv["ww"], sv["c"]
+        da = _f32((n, hh, ww, c), dev)
+        ops.adaptive_pool_bwd(dp, n, hh, ww, c, POOL, POOL, da)
+        bnws = self._scr("bnws", (256 * 2 * 512,), torch.float64, dev)
+        coef = self._scr("bncoef", (3 * 512,), torch.float32, dev)
+        dx = None
+        for li in reversed(range(len(self.layers))):
+            conv, bn, plan = self.layers[li]
+            L = sv["layers"][li]
+            oh, ow, c = L["oh"], L["ow"], plan.cout
+            npix = n * oh * ow
+            cz = (c + 7) // 8 * 8
+            dz = _bf16((n, oh, ow, cz), dev)
+            if bn is not None:
+                ops.bn_backward(da, L["a"], L["z"], npix, c, L["mean"], L["rstd"], bn.weight, bnws, coef,
+                                bn.weight.grad if need_w else None, bn.bias.grad if need_w else None, acc, dz)
+            else:
+                ops.act_grad(npix, c, da, c, 0, L["a"], c, 0, ACT_LRELU, dz, cz)
+            if need_w:
+                plan.gw = conv.weight.grad
+                plan.gb = None
+                plan.wgrad(L["a_in"], L["cs_in"], 0, L["h_in"], L["w_in"], dz, cz, n, self.ws, acc)
+            if li > 0 or need_x:
+                g = _f32((n, L["h_in"], L["w_in"], plan.cin), dev)
+                plan.dgrad(dz, cz, oh, ow, g, plan.cin, 0, n)
+                da = g
+            if li == 0 and need_x:
+                dx = torch.empty((n, 1, sv["h"], sv["w"]), dtype=torch.float32, device=dev)
+                ops.nhwc_to_nchw(da, n, 1, sv["h"], sv["w"], plan.cin, 0, dx)
+        return dx
+
+
+class _DFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, box, *params):
+        engine, keep, need_pt = box
+        s, sv = engine.forward(x, keep, need_pt)
+        ctx.engine, ctx.sv = engine, sv
+        return s
+
+    @staticmethod
+    def backward(ctx, ds):
+        engine, sv = ctx.engine, ctx.sv
+        if sv is None:
+            raise RuntimeError("discriminator forward ran without saving activations")
+        need_w = any(ctx.needs_input_grad[2:])
+        need_x = ctx.needs_input_grad[0]
+        acc = engine.d.grads_as_views() if need_w else True
+        dx = engine.backward(ds, sv, need_w, need_x, acc)
+        ctx.sv = None
+        return (dx, None) + tuple(None for _ in range(len(ctx.needs_input_grad) - 2))
+
+
+class RFBESRGANDiscriminator(FlatParamsMixin, nn.Module):
+    r"""The main architecture of the discriminator. Similar to VGG structure (rfb_esrgan.py:23-69)."""
+
+    def __init__(self, in_channels=1):
+        super().__init__()
+        self.features = nn.Sequential(
+            nn.Conv2d(in_channels, 64, kernel_size=3, stride=1, padding=1, bias=False),
+            nn.LeakyReLU(negative_slope=0.2, inplace=True),
+            nn.Conv2d(64, 64, kernel_size=3, stride=2, padding=1, bias=False),
+            nn.BatchNorm2d(64),
+            nn.LeakyReLU(negative_slope=0.2, inplace=True),
+            nn.Conv2d(64, 128, kernel_size=3, stride=1, padding=1, bias=False),
+            nn.BatchNorm2d(128),
+            nn.LeakyReLU(negative_slope=0.2, inplace=True),
+            nn.Conv2d(128, 128, kernel_size=3, stride=2, padding=1, bias=False),
+            nn.BatchNorm2d(128),
+            nn.LeakyReLU(negative_slope=0.2, inplace=True),
+            nn.Conv2d(128, 256, kernel_size=3, stride=1, padding=1, bias=False),
+            nn.BatchNorm2d(256),
+            nn.LeakyReLU(negative_slope=0.2, inplace=True),
+            nn.Conv2d(256, 256, kernel_size=3, stride=2, padding=1, bias=False),
+            nn.BatchNorm2d(256),
+            nn.LeakyReLU(negative_slope=0.2, inplace=True),
+            nn.Conv2d(256, 512, kernel_size=3, stride=1, padding=1, bias=False),
+            nn.BatchNorm2d(512),
+            nn.LeakyReLU(negative_slope=0.2, inplace=True),
+            nn.Conv2d(512, 512, kernel_size=3, stride=2, padding=1, bias=False),
+            nn.BatchNorm2d(512),
+            nn.LeakyReLU(negative_slope=0.2, inplace=True),
+        )
+        self.avgpool = nn.AdaptiveAvgPool2d((POOL, POOL))
+        self.fc = nn.Sequential(
+            nn.Linear(512 * POOL * POOL, 1024),
+            nn.LeakyReLU(negative_slope=0.2, inplace=True),
+            nn.Linear(1024, 1),
+            nn.Sigmoid(),
+        )
+        self._flatten()
+        object.__setattr__(self, "_engine", None)
+
+    def _on_flat_moved(self):
+        object.__setattr__(self, "_engine", None)
+
+    def _apply(self, fn, recurse=True):
+        ret = super()._apply(fn, recurse)
+        object.__setattr__(self, "_engine", None)  # buffers (BN running stats) may have moved too
+        return ret
+
+    def engine(self) -> _DEngine:
+        self._ensure_flat()
+        if self._engine is None:
+            object.__setattr__(self, "_engine", _DEngine(self))
+        return self._engine
+
+    def repack_weights(self) -> None:
+        self.engine().repack()
+
+    def forward(self, input: Tensor) -> Tensor:
+        if not input.is_cuda:
+            raise RuntimeError("climsr_amd.RFBESRGANDiscriminator runs on the GPU only (no CPU fallback)")
+        eng = self.engine()
+        params = [p for p, _o, _n in self._flat_index]
+        grad_on = torch.is_grad_enabled()
+        need_w = grad_on and any(p.requires_grad for p in params)
+        keep = grad_on and (need_w or input.requires_grad)
+        return _DFn.apply(input, (eng, keep, need_w), *params)

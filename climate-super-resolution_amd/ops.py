@@ -132,12 +132,18 @@ class ConvPlan:
 
     def dgrad(self, dz: torch.Tensor, dz_cs: int, out_h: int, out_w: int, g: torch.Tensor, g_cs: int, g_co: int, n: int,
               accumulate: bool = False, down2: bool = False, cout_t: Optional[int] = None) -> None:
-        """Data gradient of a stride-1 conv: g[:, :, :, g_co:g_co+cin_real] (+)= conv^T(dz) (fp32).  With down2 the
-        result is summed over 2x2 pixel blocks (backward of the nearest x2 upsample feeding this conv)."""
-        assert self.stride == 1, "dgrad kernel covers stride-1 convs"
+        """Data gradient: g[:, :, :, g_co:g_co+cin_real] (+)= conv^T(dz) (fp32); (out_h, out_w) are dz's dims.  With
+        down2 the result is summed over 2x2 pixel blocks (backward of the nearest x2 upsample feeding this conv).
+        Stride-2 convs (pad 1, even input) run as a stride-1 conv over the zero-inserted dz."""
         ct = self.cout_t if cout_t is None else cout_t
         pad_t = self.ks - 1 - self.pad
-        d = ConvDesc(n, out_h, out_w, self.cin_t, dz_cs, 0, 1, self.ks, 1, pad_t, out_h, out_w, ct, g_cs, g_co, self.cc_t)
+        if self.stride == 1:
+            d = ConvDesc(n, out_h, out_w, self.cin_t, dz_cs, 0, 1, self.ks, 1, pad_t, out_h, out_w, ct, g_cs, g_co, self.cc_t)
+        else:  # stride 2: stride-1 conv over the zero-inserted gradient (logical size 2*out)
+            assert self.stride == 2 and not down2
+            d = ConvDesc(n, out_h, out_w, self.cin_t, dz_cs, 0, -2, self.ks, 1, pad_t, 2 * out_h, 2 * out_w, ct, g_cs, g_co,
+                         self.cc_t)
+            out_h, out_w = 2 * out_h, 2 * out_w
         ep = Epilogue(0, 0.0, 1.0, None, 0, 0, 1.0, None, 0, 0, OUT_F32_ADD if accumulate else OUT_F32, 1 if down2 else 0)
         flops = 2 * self.cout * ct * self.ks * self.ks * n * out_h * out_w
         _run(fwd_kernel_name(ct, out_h), flops, lambda: check(
@@ -232,3 +238,81 @@ class BatchedPacker:
     def run(self):
         check(_lib.load().climsr_pack_conv_weights_batched(ptr(self.table), self.n, self.max_elems, _lib.stream_ptr()),
               "pack batched")
+
+
+# ------------------------------------------------------------------ discriminator / VGG / GAN-loss ops
+def _L():
+    return _lib.load()
+
+
+def bn_forward(z, npix, c, gamma, beta, mean, rstd, y, ws, run_mean=None, run_var=None, act=ACT_LRELU, slope=0.2, eps=1e-5,
+               momentum=0.1):
+    check(_L().climsr_bn_forward(ptr(z), npix, c, ptr(gamma), ptr(beta), act, slope, eps, momentum, ptr(ws), ptr(mean), ptr(rstd),
+                                 ptr(run_mean), ptr(run_var), ptr(y), _lib.stream_ptr()), "bn_forward")
+
+
+def bn_inference(z, npix, c, run_mean, run_var, gamma, beta, y, act=ACT_LRELU, slope=0.2, eps=1e-5):
+    check(_L().climsr_bn_inference(ptr(z), npix, c, ptr(run_mean), ptr(run_var), eps, ptr(gamma), ptr(beta), act, slope, ptr(y),
+                                   _lib.stream_ptr()), "bn_inference")
+
+
+def bn_backward(da, a, z, npix, c, mean, rstd, gamma, ws, coef, dgamma, dbeta, accumulate, dz, slope=0.2):
+    check(_L().climsr_bn_backward(ptr(da), ptr(a), ptr(z), npix, c, ptr(mean), ptr(rstd), ptr(gamma), slope, ptr(ws), ptr(coef),
+                                  ptr(dgamma), ptr(dbeta), int(accumulate), ptr(dz), _lib.stream_ptr()), "bn_backward")
+
+
+def adaptive_pool_fwd(x, n, h, w, c, oh, ow, out, out_t=None, n_pad=0):
+    check(_L().climsr_adaptive_pool_fwd(ptr(x), n, h, w, c, oh, ow, ptr(out), ptr(out_t), n_pad, _lib.stream_ptr()),
+          "adaptive_pool_fwd")
+
+
+def adaptive_pool_bwd(dp, n, h, w, c, oh, ow, dx):
+    check(_L().climsr_adaptive_pool_bwd(ptr(dp), n, h, w, c, oh, ow, ptr(dx), _lib.stream_ptr()), "adaptive_pool_bwd")
+
+
+def linear_fwd(x, w, bias, n, k, o, y, ws, act=ACT_NONE, slope=0.2):
+    _run("linear_fwd_kernel", 2 * n * k * o, lambda: check(
+        _L().climsr_linear_fwd(ptr(x), ptr(w), ptr(bias), n, k, o, act, slope, ptr(ws), ws.numel(), ptr(y), _lib.stream_ptr()),
+        "linear_fwd"), "fwd fc.0")
+
+
+def linear_dgrad(dy, w, n, k, o, dx, accumulate=False):
+    _run("linear_dgrad_kernel", 2 * n * k * o, lambda: check(
+        _L().climsr_linear_dgrad(ptr(dy), ptr(w), n, k, o, ptr(dx), int(accumulate), _lib.stream_ptr()), "linear_dgrad"),
+        "dgrad fc.0")
+
+
+def linear_wgrad(dy_t, x_t, n_pad, k, o, dw, accumulate):
+    _run("linear_wgrad_kernel", 2 * n_pad * k * o, lambda: check(
+        _L().climsr_linear_wgrad(ptr(dy_t), ptr(x_t), n_pad, k, o, ptr(dw), int(accumulate), _lib.stream_ptr()), "linear_wgrad"),
+        "wgrad fc.0")
+
+
+def d_head_fwd(h, w2, b2, n, o, s):
+    check(_L().climsr_d_head_fwd(ptr(h), ptr(w2), ptr(b2), n, o, ptr(s), _lib.stream_ptr()), "d_head_fwd")
+
+
+def d_head_bwd(h, s, ds, w2, n, o, n_pad, dw2, db2, db0, accumulate, du0, du0_t, slope=0.2):
+    check(_L().climsr_d_head_bwd(ptr(h), ptr(s), ptr(ds), ptr(w2), n, o, n_pad, slope, ptr(dw2), ptr(db2), ptr(db0), int(accumulate),
+                                 ptr(du0), ptr(du0_t), _lib.stream_ptr()), "d_head_bwd")
+
+
+def relativistic_bce(s_real, s_fake, n, t_rf, t_fr, loss=None, gscale=None, g_real=None, g_fake=None):
+    check(_L().climsr_relativistic_bce(ptr(s_real), ptr(s_fake), n, t_rf, t_fr, ptr(loss), ptr(gscale), ptr(g_real), ptr(g_fake),
+                                       _lib.stream_ptr()), "relativistic_bce")
+
+
+def maxpool2(x, n, h, w, c, y):
+    check(_L().climsr_maxpool2_bf16(ptr(x), n, h, w, c, ptr(y), _lib.stream_ptr()), "maxpool2")
+
+
+def l1_bf16(a, b, n, ws, out):
+    check(_L().climsr_l1_loss_bf16(ptr(a), ptr(b), n, ptr(ws), ptr(out), _lib.stream_ptr()), "l1_bf16")
+
+
+def f32_to_bf16(x, y):
+    check(_L().climsr_f32_to_bf16(ptr(x), x.numel(), ptr(y), _lib.stream_ptr()), "f32_to_bf16")
+
+
+def increment_i64(t):
+    check(_L().climsr_increment_i64(ptr(t), _lib.stream_ptr()), "increment_i64")

@@ -39,7 +39,9 @@ typedef struct ClimsrConvDesc {
   int32_t in_h, in_w;          /* SOURCE spatial size (before the nearest upsample) */
   int32_t in_c;                /* channels consumed (multiple of 8) */
   int32_t in_cstride, in_coff; /* input buffer channels per pixel / first channel (multiples of 8) */
-  int32_t up;                  /* 1, or 2 = nearest x2 upsample on load (esrgan.py:94,97: src = dst >> 1) */
+  int32_t up;                  /* 1; 2 = nearest x2 upsample on load (esrgan.py:94,97: src = dst >> 1);
+                                  -2 = zero-insertion x2 (src = dst >> 1 for even dst, else 0): data gradient
+                                  of a stride-2 conv (rfb_esrgan.py:30-50), forward kernel only */
   int32_t ks, stride, pad;     /* kernel size (1,3,5,9), stride (1,2), zero padding */
   int32_t out_h, out_w;        /* output spatial size */
   int32_t out_c;               /* real output channels */
@@ -141,6 +143,58 @@ int climsr_adamw_hparams(double* state, int total_steps, double max_lr, double p
                          double final_div_factor, double beta2, double eps, double wd, float* hp, void* stream);
 /* Fused AdamW over flat fp32 buffers (conf/optimizers/adamw.yaml). */
 int climsr_adamw_step(int64_t n, float* p, const float* g, float* m, float* v, const float* hp, void* stream);
+
+/* ---------------- discriminator / perceptual loss / GAN loss (disc.hip) ---------------- */
+
+/* nn.BatchNorm2d in train mode over z [npix][c] (bf16 NHWC; c % 8 == 0, c <= 2048), fused with the
+ * following activation: y = act(gamma*(z-mean)*rstd + beta).  Saves mean/rstd for the backward and
+ * updates run_mean/run_var (momentum, unbiased var) when non-NULL (rfb_esrgan.py:32-50 BN + LeakyReLU).
+ * workspace >= 256*2*c doubles. */
+int climsr_bn_forward(const uint16_t* z, int64_t npix, int c, const float* gamma, const float* beta, int act, float slope,
+                      float eps, float momentum, double* workspace, float* mean, float* rstd, float* run_mean, float* run_var,
+                      uint16_t* y, void* stream);
+/* Eval-mode BN (running statistics) + activation (nn.BatchNorm2d.eval()). */
+int climsr_bn_inference(const uint16_t* z, int64_t npix, int c, const float* run_mean, const float* run_var, float eps,
+                        const float* gamma, const float* beta, int act, float slope, uint16_t* y, void* stream);
+/* *p += 1 on the device (BatchNorm num_batches_tracked). */
+int climsr_increment_i64(int64_t* p, void* stream);
+/* Backward of act(BN(z)): da = dL/d(act output) fp32, a = act output (bf16, sign gives lrelu'),
+ * dz (bf16) = BN input gradient; dgamma/dbeta (+)= .  coef >= 3*c floats scratch. */
+int climsr_bn_backward(const float* da, const uint16_t* a, const uint16_t* z, int64_t npix, int c, const float* mean,
+                       const float* rstd, const float* gamma, float slope, double* workspace, float* coef, float* dgamma,
+                       float* dbeta, int accumulate, uint16_t* dz, void* stream);
+
+/* nn.AdaptiveAvgPool2d((oh,ow)) (rfb_esrgan.py:54) on NHWC bf16 x [n][h][w][c]; out = torch.flatten
+ * order [n][c*oh*ow] bf16; out_t (optional) = its transpose [c*oh*ow][n_pad] for the fc.0 weight grad. */
+int climsr_adaptive_pool_fwd(const uint16_t* x, int n, int h, int w, int c, int oh, int ow, uint16_t* out, uint16_t* out_t,
+                             int n_pad, void* stream);
+/* Backward: dx [n][h][w][c] fp32 (overwritten) from dp [n][c*oh*ow] fp32. */
+int climsr_adaptive_pool_bwd(const float* dp, int n, int h, int w, int c, int oh, int ow, float* dx, void* stream);
+
+/* nn.Linear forward on MFMA: y[n][o] = act(x[n][k] . w[o][k] + b[o]) (fp32 out); n <= 64, k % 32 == 0,
+ * o % 16 == 0; split-K partials in workspace (ws_floats >= nsplit*n*o, nsplit <= 1024/ceil(o/64)). */
+int climsr_linear_fwd(const uint16_t* x, const uint16_t* w, const float* bias, int n, int k, int o, int act, float slope,
+                      float* workspace, int64_t ws_floats, float* y, void* stream);
+/* dx[n][k] (+)= dy[n][o] . w[o][k] (bf16 in, fp32 out); k % 64 == 0, o % 32 == 0. */
+int climsr_linear_dgrad(const uint16_t* dy, const uint16_t* w, int n, int k, int o, float* dx, int accumulate, void* stream);
+/* dw[o][k] (+)= sum_n dy_t[o][n] x_t[k][n] (K = n_pad, multiple of 32; k % 64 == 0, o % 64 == 0). */
+int climsr_linear_wgrad(const uint16_t* dy_t, const uint16_t* x_t, int n_pad, int k, int o, float* dw, int accumulate,
+                        void* stream);
+/* Discriminator head after fc.0+LeakyReLU (h [n][o] fp32): s[n] = sigmoid(h.w2 + b2) (rfb_esrgan.py:59-60). */
+int climsr_d_head_fwd(const float* h, const float* w2, const float* b2, int n, int o, float* s, void* stream);
+/* Head backward from ds[n]: dw2/db2/db0 (+)=; du0 = d(fc.0 pre-activation) as bf16 [n][o] and [o][n_pad]. */
+int climsr_d_head_bwd(const float* h, const float* s, const float* ds, const float* w2, int n, int o, int n_pad, float slope,
+                      float* dw2, float* db2, float* db0, int accumulate, uint16_t* du0, uint16_t* du0_t, void* stream);
+/* Relativistic-average BCEWithLogits (pl_gan.py:33-38, 54-59): loss = (BCE(s_f-mean(s_r), t_fr) +
+ * BCE(s_r-mean(s_f), t_rf))/2; with gscale (device scalar) also the gradients w.r.t. s_real/s_fake. */
+int climsr_relativistic_bce(const float* s_real, const float* s_fake, int n, float t_rf, float t_fr, float* loss,
+                            const float* gscale, float* g_real, float* g_fake, void* stream);
+/* VGG19 MaxPool2d(2,2) on NHWC bf16 (perceptual.py:16). */
+int climsr_maxpool2_bf16(const uint16_t* x, int n, int h, int w, int c, uint16_t* y, void* stream);
+/* mean |a-b| over n bf16 elements (n % 8 == 0); workspace >= 512 doubles (perceptual.py:31-34). */
+int climsr_l1_loss_bf16(const uint16_t* a, const uint16_t* b, int64_t n, double* workspace, float* out, void* stream);
+/* y = bf16(x) elementwise (MFMA copy of fp32 master weights). */
+int climsr_f32_to_bf16(const float* x, int64_t n, uint16_t* y, void* stream);
 
 #ifdef __cplusplus
 }

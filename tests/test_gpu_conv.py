@@ -169,3 +169,21 @@ def test_act_grad():
     act_grad(n * h * w, 16, gr.to(DEV), 128, 96, y.to(DEV), 128, 96, ACT_LRELU, dz, 16, scale=0.5)
     want = gr[..., 96:112] * 0.5 * torch.where(y[..., 96:112].float() > 0, 1.0, 0.2)
     assert torch.allclose(dz.float().cpu(), bf(want), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("cin,cout,h", [(64, 128, 32), (1, 64, 16), (256, 256, 16), (512, 512, 8)])
+def test_conv_dgrad_stride2_matches_autograd(cin, cout, h):
+    """Data gradient of the discriminator's stride-2 convs (rfb_esrgan.py:30-50) via zero insertion."""
+    n, w = 2, h
+    p, wt, b = make_plan(cin, cout, 3, stride=2)
+    g = torch.Generator().manual_seed(7)
+    oh, ow = h // 2, w // 2
+    dz = bf(torch.rand((n, cout, oh, ow), generator=g) * 2 - 1)
+    dzb = to_nhwc(dz)
+    gx = torch.zeros((n, h, w, p.cin), dtype=torch.float32, device=DEV)
+    p.dgrad(dzb, dzb.shape[-1], oh, ow, gx, p.cin, 0, n)
+    torch.cuda.synchronize()
+    x = torch.zeros((n, cin, h, w), dtype=torch.float64, requires_grad=True)
+    y = F.conv2d(x, bf(wt).double(), None, stride=2, padding=1)
+    (gref,) = torch.autograd.grad(y, x, dz.double())
+    check_close(from_nhwc(gx, cin).cpu(), gref, tol=2e-5, what="dgrad s2")
