@@ -26,6 +26,7 @@ import torch.distributed as dist  # noqa: E402
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
 G_FWD_FLOP_PER_PX = 721_880  # 23,654,563,840 MAC per 64^2 sample / 65,536 HR px * 2
+GAN_FLOP_PER_PX = 6_140_192  # (4 G + 9 D + 2 VGG) MAC * 2 / 65,536 at 256^2
 
 
 def parse():
@@ -40,6 +41,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--mode", choices=["pretrain", "gan"], default="pretrain",
+                    help="pretrain = BASELINE config 2 (the metric's workload); gan = config 3 (G + RFB-D + VGG19 perceptual)")
     return ap.parse_args()
 
 
@@ -125,12 +128,26 @@ def main():
 
     B, lr_size = args.batch, args.lr_size
     hr = 4 * lr_size
+    total_steps = max(1000, args.warmup + args.steps + 10)
     g = ESRGANGenerator(in_channels=3, out_channels=1, nf=64, nb=args.nb, gc=16, scale_factor=4)
     st = init_state(spec_from_shapes({k: tuple(v.shape) for k, v in g.state_dict().items()}))
     g.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in st.items()})
     g = g.to(dev)
-    total_steps = max(1000, args.warmup + args.steps + 10)
-    opt = GraphedAdamW(g, lr=1e-4, total_steps=total_steps, weight_decay=1e-4)
+    opt_g = GraphedAdamW(g, lr=1e-4, total_steps=total_steps, weight_decay=1e-4)
+    task = d = opt_d = None
+    if args.mode == "gan":
+        from climsr_amd.task.pl_gan import GANLightningModule
+
+        task = GANLightningModule(generator=g, discriminator={"_target_": "climsr_amd.models.rfb_esrgan.RFBESRGANDiscriminator",
+                                                              "in_channels": 1})
+        d = task.discriminator
+        dst = init_state(spec_from_shapes({k: tuple(v.shape) for k, v in d.state_dict().items()},
+                                          [n_ for n_, m_ in d.named_modules() if isinstance(m_, torch.nn.BatchNorm2d)]))
+        d.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in dst.items()})
+        task = task.to(dev)
+        g, d = task.generator, task.discriminator
+        opt_g = GraphedAdamW(g, lr=1e-4, total_steps=total_steps, weight_decay=1e-4)
+        opt_d = GraphedAdamW(d, lr=1e-4, total_steps=total_steps, weight_decay=1e-4)
 
     gen = torch.Generator(device="cpu").manual_seed(42 + rank)
     t = torch.rand((B, 1, hr, hr), generator=gen) * 2 - 1
@@ -139,35 +156,84 @@ def main():
     lr = torch.cat([t, e, m], 1)[:, :, ::4, ::4].contiguous()
     batch = {k: v.to(dev) for k, v in {"lr": lr, "hr": t, "elevation": e, "mask": m}.items()}
 
-    loss_buf = torch.zeros((), device=dev)
+    loss_buf = torch.zeros(2, device=dev)
 
-    def step():
-        for p in g.parameters():
-            p.grad = None  # zero_grad(set_to_none=True): backward overwrites the flat grad buffer
-        sr = g(batch["lr"], batch["elevation"], batch["mask"])
-        loss = l1_loss(sr, batch["hr"])
-        loss.backward()
+    def allreduce(net):
         if world > 1:
-            dist.all_reduce(g._flat_grad, op=dist.ReduceOp.AVG)
-        opt.step()
-        loss_buf.copy_(loss.detach())
+            dist.all_reduce(net._flat_grad, op=dist.ReduceOp.AVG)  # DDP gradient average over RCCL/xGMI
 
-    use_graph = not args.no_graph and world == 1
+    def toggle(net_on):
+        if d is None:
+            return
+        for net in (g, d):
+            for p in net.parameters():
+                p.requires_grad_(net is net_on)
+
+    # The step as segments; the RCCL all-reduce runs between captured segments (eagerly) so that
+    # multi-GPU runs keep one hipGraph per segment.
+    if args.mode == "pretrain":
+        def seg_g():
+            for p in g.parameters():
+                p.grad = None  # zero_grad(set_to_none=True): backward overwrites the flat grad buffer
+            sr = g(batch["lr"], batch["elevation"], batch["mask"])
+            loss = l1_loss(sr, batch["hr"])
+            loss.backward()
+            loss_buf[0].copy_(loss.detach())
+
+        segments = [(seg_g, g), (opt_g.step, None)]
+    else:
+        def seg_g():  # optimizer_idx 0 (pl_gan.py:63-79): D frozen
+            toggle(g)
+            for p in g.parameters():
+                p.grad = None
+            _hr, sr = task.common_step(batch)
+            _perc, _adv, _pix, lg = task.loss_g(batch["hr"], sr)
+            lg.backward()
+            loss_buf[0].copy_(lg.detach())
+
+        def seg_d():  # AdamW_G, then optimizer_idx 1 (pl_gan.py:81-97): fresh G forward, D update
+            opt_g.step()
+            toggle(d)
+            for p in d.parameters():
+                p.grad = None
+            _hr, sr = task.common_step(batch)
+            ld = task.loss_d(batch["hr"], sr)
+            ld.backward()
+            loss_buf[1].copy_(ld.detach())
+
+        segments = [(seg_g, g), (seg_d, d), (opt_d.step, None)]
+
+    def step_eager():
+        for fn, net in segments:
+            fn()
+            if net is not None:
+                allreduce(net)
+
+    use_graph = not args.no_graph
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
         for _ in range(2):
-            step()
+            step_eager()
     torch.cuda.current_stream().wait_stream(side)
     torch.cuda.synchronize()
-    graph = None
     if use_graph:
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            step()
-        run = graph.replay
+        graphs = []
+        pool = None
+        for fn, net in segments:
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr, pool=pool):
+                fn()
+            pool = gr.pool()
+            graphs.append((gr, net))
+
+        def run():
+            for gr, net in graphs:
+                gr.replay()
+                if net is not None:
+                    allreduce(net)
     else:
-        run = step
+        run = step_eager
     for _ in range(args.warmup):
         run()
     torch.cuda.synchronize()
@@ -175,8 +241,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         run()
+        if rank == 0 and args.steps >= 20 and (i + 1) % max(1, args.steps // 4) == 0:
+            print(f"[bench] step {i + 1}/{args.steps}", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -186,12 +254,14 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     ms = elapsed / args.steps * 1e3
-    loss_val = float(loss_buf.item())
+    loss_val = [float(v) for v in loss_buf.cpu()]
     mpix = world * B * hr * hr / 1e6 / (elapsed / args.steps)
+    step = step_eager
 
     roof = None
     step_frac = None
-    flop_step = 3 * G_FWD_FLOP_PER_PX * B * hr * hr  # fwd + dgrad + wgrad
+    flop_px = 3 * G_FWD_FLOP_PER_PX if args.mode == "pretrain" else GAN_FLOP_PER_PX
+    flop_step = flop_px * B * hr * hr  # SURVEY §8d algorithmic FLOPs per HR pixel
     step_tflops = flop_step / (ms / 1e3) / 1e12
     step_frac = step_tflops / PEAK_BF16_TFLOPS
     kern = {}
@@ -213,7 +283,7 @@ def main():
             print(json.dumps(timer.by_tag(), indent=0), file=sys.stderr)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.mode == "pretrain":
         cpu = cpu_baseline(args, hr)
 
     if rank == 0:
@@ -222,14 +292,17 @@ def main():
             "value": round(mpix, 3), "unit": "HR MPix/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (seed 42+rank: U(-1,1) temp/elev, Bernoulli(0.7) mask, LR = HR[::4,::4]); deterministic init",
-            "config": {"workload": "config 2: RRDB generator L1 pre-training step (fwd+L1+bwd+AdamW+OneCycleLR)",
+            "config": {"workload": ("config 2: RRDB generator L1 pre-training step (fwd+L1+bwd+AdamW+OneCycleLR)"
+                                    if args.mode == "pretrain" else
+                                    "config 3: full ESRGAN GAN step (2 G fwd, G bwd, 4 RFB-D calls, VGG19 perceptual, 2x AdamW)"),
                        "generator": f"ESRGAN nf64 nb{args.nb} gc16 x4", "global_batch": world * B, "per_gpu_batch": B,
-                       "lr_tile": lr_size, "hr_tile": hr, "parallelism": f"dp{world}", "hip_graph": use_graph},
+                       "lr_tile": lr_size, "hr_tile": hr, "parallelism": f"dp{world}", "hip_graph": use_graph,
+                       "mode": args.mode},
             "roofline": roof,
             "step_mfma": {"algorithmic_tflop_per_step": round(flop_step / 1e12, 3), "achieved_tflops": round(step_tflops, 1),
                           "frac": round(step_frac, 4)},
             "cpu_baseline": cpu,
-            "loss_last": round(loss_val, 6),
+            "loss_last": [round(v, 6) for v in loss_val],
             "kernels": kern,
         }
         print(json.dumps(out))
