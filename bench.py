@@ -158,9 +158,20 @@ def main():
 
     loss_buf = torch.zeros(2, device=dev)
 
+    from climsr_amd.core.ddp import GradAllReducer, broadcast_module
+
+    reducers = {}
+
     def allreduce(net):
-        if world > 1:
-            dist.all_reduce(net._flat_grad, op=dist.ReduceOp.AVG)  # DDP gradient average over RCCL/xGMI
+        if world > 1:  # DDP gradient average of the flat fp32 buffer over RCCL/xGMI, 256 MB buckets
+            if id(net) not in reducers:
+                reducers[id(net)] = GradAllReducer(net)
+            reducers[id(net)]()
+
+    if world > 1:
+        for net in (g, d):
+            if net is not None:
+                broadcast_module(net)
 
     def toggle(net_on):
         if d is None:
