@@ -259,42 +259,18 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
   const int nvec_x = a.tph * a.tpw * cvec;
   const int wvec_row = a.kcpad / 8;
   const int nvec_w = NT * 16 * wvec_row;
-  const int nvec = nvec_x + nvec_w;
   const int upsh = ufac == 2 ? 1 : 0;
 
-  // staging = one flat space of 16 B vectors: [0, nvec_x) input tile, [nvec_x, nvec) weight chunk
-  auto gload = [&](int j, int v) -> uint4 {
-    if (v < nvec_x) {
-      int pix = v / cvec;
-      int cg = v - pix * cvec;
-      int ty_ = pix / a.tpw;
-      int tx_ = pix - ty_ * a.tpw;
-      int iy = iy0 + ty_, ix = ix0 + tx_;
-      int c = j * a.cc + cg * 8;
-      uint4 val = make_uint4(0, 0, 0, 0);
-      if (iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c && !((iy | ix) & dilmask)) {
-        long src = (((long)nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + c;
-        val = *(const uint4*)(a.x + src);
-      }
-      return val;
-    }
-    v -= nvec_x;
-    int r = v / wvec_row;
-    int kv = v - r * wvec_row;
-    return *(const uint4*)(a.w + (long)(co_blk0 + r) * a.kpk + (long)j * a.kcpad + kv * 8);
-  };
-  auto lstore = [&](int v, uint4 val) {
-    if (v < nvec_x) {
-      int pix = v / cvec;
-      int cg = v - pix * cvec;
-      *(uint4*)(xs + pix * a.ccp + cg * 8) = val;
-    } else {
-      v -= nvec_x;
-      int r = v / wvec_row;
-      int kv = v - r * wvec_row;
-      *(uint4*)(ws + r * wpitch + kv * 8) = val;
-    }
-  };
+  // Staging index math is incremental: each thread's k-th vector is (tid + 256k); the pixel /
+  // channel-group / row decomposition of the first one costs a few divisions once per kernel, every
+  // later one only adds constants with carries (runtime integer division is ~40 VALU ops).
+  const int x_dp = 256 / cvec, x_dc = 256 - x_dp * cvec;  // +256 vectors = x_dp pixels + x_dc groups
+  const int x_dy = x_dp / a.tpw, x_dx = x_dp - x_dy * a.tpw;
+  const int x_pix0 = tid / cvec, x_cg0 = tid - x_pix0 * cvec;
+  const int x_ty0 = x_pix0 / a.tpw, x_tx0 = x_pix0 - x_ty0 * a.tpw;
+  const int w_dr = 256 / wvec_row, w_dk = 256 - w_dr * wvec_row;
+  const int w_r0 = tid / wvec_row, w_k0 = tid - w_r0 * wvec_row;
+  const int nrx = (nvec_x + 255) / 256, nrw = (nvec_w + 255) / 256;
   auto compute = [&]() {
     const int nks = a.kcpad / 32;
     for (int kstep = 0; kstep < nks; ++kstep) {
@@ -316,17 +292,54 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
   // first LDS store, so a chunk pays ~one memory latency instead of one per vector
   for (int j = 0; j < a.nchunk; ++j) {
     __syncthreads();
-    for (int base = 0; base < nvec; base += 256 * FWD_MAXV) {
-      uint4 buf[FWD_MAXV];
+    {  // input tile (logical coordinates: upsampled / zero-inserted; zero padding)
+      int ty_ = x_ty0, tx_ = x_tx0, cg = x_cg0;
+      for (int base = 0; base < nrx; base += FWD_MAXV) {
+        uint4 buf[FWD_MAXV];
+        int dst[FWD_MAXV];
 #pragma unroll
-      for (int i = 0; i < FWD_MAXV; ++i) {
-        int v = base + tid + i * 256;
-        if (v < nvec) buf[i] = (a.ablate & 1) ? make_uint4(0, 0, 0, 0) : gload(j, v);
+        for (int i = 0; i < FWD_MAXV; ++i) {
+          dst[i] = -1;
+          if (base + i < nrx && ty_ < a.tph) {
+            const int iy = iy0 + ty_, ix = ix0 + tx_;
+            const int c = j * a.cc + cg * 8;
+            uint4 val = make_uint4(0, 0, 0, 0);
+            if (!(a.ablate & 1) && iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c && !((iy | ix) & dilmask))
+              val = *(const uint4*)(a.x + (((long)nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + c);
+            buf[i] = val;
+            dst[i] = (ty_ * a.tpw + tx_) * a.ccp + cg * 8;
+          }
+          cg += x_dc;
+          tx_ += x_dx;
+          ty_ += x_dy;
+          if (cg >= cvec) { cg -= cvec; ++tx_; }
+          if (tx_ >= a.tpw) { tx_ -= a.tpw; ++ty_; }
+        }
+#pragma unroll
+        for (int i = 0; i < FWD_MAXV; ++i)
+          if (dst[i] >= 0) *(uint4*)(xs + dst[i]) = buf[i];
       }
+    }
+    {  // weight chunk rows [co_blk0, co_blk0 + 16*NT) x kcpad
+      int r = w_r0, kv = w_k0;
+      for (int base = 0; base < nrw; base += FWD_MAXV) {
+        uint4 buf[FWD_MAXV];
+        int dst[FWD_MAXV];
 #pragma unroll
-      for (int i = 0; i < FWD_MAXV; ++i) {
-        int v = base + tid + i * 256;
-        if (v < nvec) lstore(v, buf[i]);
+        for (int i = 0; i < FWD_MAXV; ++i) {
+          dst[i] = -1;
+          if (base + i < nrw && r < NT * 16) {
+            buf[i] = (a.ablate & 1) ? make_uint4(0, 0, 0, 0)
+                                    : *(const uint4*)(a.w + (long)(co_blk0 + r) * a.kpk + (long)j * a.kcpad + kv * 8);
+            dst[i] = r * wpitch + kv * 8;
+          }
+          kv += w_dk;
+          r += w_dr;
+          if (kv >= wvec_row) { kv -= wvec_row; ++r; }
+        }
+#pragma unroll
+        for (int i = 0; i < FWD_MAXV; ++i)
+          if (dst[i] >= 0) *(uint4*)(ws + dst[i]) = buf[i];
       }
     }
     __syncthreads();
@@ -616,7 +629,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs a) {
 
   const int lh = a.in_h * a.up, lw = a.in_w * a.up;  // up in {1, 2} here
   const int upsh = a.up == 2 ? 1 : 0;
-  const int zvec = NTC * 2;  // 16B vectors of dz per pixel
+  constexpr int zvec = NTC * 2;  // 16B vectors of dz per pixel
+  const int x_dy = 128 / a.tpw, x_dx = 128 - x_dy * a.tpw;  // +256 vectors = +128 pixels
+  const int x_ty0 = (tid >> 1) / a.tpw, x_tx0 = (tid >> 1) - x_ty0 * a.tpw;
   const int nvec_x = a.tph * a.tpw * 2;
   const int nvec_z = WG_TH * TW * zvec;
 
@@ -629,42 +644,59 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs a) {
     const int ox0 = tx * TW, oy0 = ty * WG_TH;
     const int iy0 = oy0 * a.stride - a.pad, ix0 = ox0 * a.stride - a.pad;
     __syncthreads();
-    // batched staging (all loads of a round in flight before the first LDS store)
-    for (int base = 0; base < nvec_x + nvec_z; base += 256 * FWD_MAXV) {
-      uint4 buf[FWD_MAXV];
+    // batched staging (all loads of a round in flight before the first LDS store); x-tile pixel
+    // coordinates advance incrementally (thread's pixels are (tid>>1) + 128k, channel half tid&1)
+    {
+      const int h = tid & 1;
+      int ty_ = x_ty0, tx_ = x_tx0;
+      const int nrx = (nvec_x + 255) / 256;
+      for (int base = 0; base < nrx; base += FWD_MAXV) {
+        uint4 buf[FWD_MAXV];
+        int dst[FWD_MAXV];
 #pragma unroll
-      for (int i = 0; i < FWD_MAXV; ++i) {
-        int v = base + tid + i * 256;
-        uint4 val = make_uint4(0, 0, 0, 0);
-        if (a.ablate & 1) {
-        } else if (v < nvec_x) {
-          int pix = v >> 1;
-          int h = v & 1;
-          int ty_ = pix / a.tpw, tx_ = pix - (pix / a.tpw) * a.tpw;
-          int iy = iy0 + ty_, ix = ix0 + tx_;
-          int c = ci0 + h * 8;
-          if (iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c)
-            val = *(const uint4*)(a.x + (((long)nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + c);
-        } else if (v < nvec_x + nvec_z) {
-          int vz = v - nvec_x;
-          int pix = vz / zvec;
-          int cv = vz - pix * zvec;
-          int oy = oy0 + pix / TW, ox = ox0 + (pix % TW);
-          int c = co0 + cv * 8;
-          if (oy < a.out_h && ox < a.out_w && c < a.dz_cs)
-            val = *(const uint4*)(a.dz + (((long)nimg * a.out_h + oy) * a.out_w + ox) * a.dz_cs + c);
+        for (int i = 0; i < FWD_MAXV; ++i) {
+          dst[i] = -1;
+          if (base + i < nrx && ty_ < a.tph) {
+            const int iy = iy0 + ty_, ix = ix0 + tx_;
+            const int c = ci0 + h * 8;
+            uint4 val = make_uint4(0, 0, 0, 0);
+            if (!(a.ablate & 1) && iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c)
+              val = *(const uint4*)(a.x + (((long)nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + c);
+            buf[i] = val;
+            dst[i] = (ty_ * a.tpw + tx_) * WG_XP + h * 8;
+          }
+          tx_ += x_dx;
+          ty_ += x_dy;
+          if (tx_ >= a.tpw) { tx_ -= a.tpw; ++ty_; }
         }
-        buf[i] = val;
-      }
 #pragma unroll
-      for (int i = 0; i < FWD_MAXV; ++i) {
-        int v = base + tid + i * 256;
-        if (v < nvec_x) {
-          *(uint4*)(xs + (v >> 1) * WG_XP + (v & 1) * 8) = buf[i];
-        } else if (v < nvec_x + nvec_z) {
-          int vz = v - nvec_x;
-          int pix = vz / zvec;
-          *(uint4*)(zs + pix * a.dzp + (vz - pix * zvec) * 8) = buf[i];
+        for (int i = 0; i < FWD_MAXV; ++i)
+          if (dst[i] >= 0) *(uint4*)(xs + dst[i]) = buf[i];
+      }
+      const int nrz = nvec_z / 256;  // exact: 256 px x zvec vectors
+      for (int base = 0; base < nrz; base += FWD_MAXV) {
+        uint4 buf[FWD_MAXV];
+#pragma unroll
+        for (int i = 0; i < FWD_MAXV; ++i) {
+          if (base + i < nrz) {
+            const int vz = tid + (base + i) * 256;
+            const int pix = vz / zvec;  // zvec = 2*NTC: compile-time power of two
+            const int cv = vz - pix * zvec;
+            const int oy = oy0 + pix / TW, ox = ox0 + (pix % TW);
+            const int c = co0 + cv * 8;
+            uint4 val = make_uint4(0, 0, 0, 0);
+            if (!(a.ablate & 1) && oy < a.out_h && ox < a.out_w && c < a.dz_cs)
+              val = *(const uint4*)(a.dz + (((long)nimg * a.out_h + oy) * a.out_w + ox) * a.dz_cs + c);
+            buf[i] = val;
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < FWD_MAXV; ++i) {
+          if (base + i < nrz) {
+            const int vz = tid + (base + i) * 256;
+            const int pix = vz / zvec;
+            *(uint4*)(zs + pix * a.dzp + (vz - pix * zvec) * 8) = buf[i];
+          }
         }
       }
     }
