@@ -495,6 +495,96 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Single-output-channel conv on VALU (v_dot2_f32_bf16): conv_last (64->1), srcnn.conv3 (32->1) and
+// the data gradient of srcnn.conv1 w.r.t. its first input channel (64->1, 9x9).  With Cout = 1 an
+// MFMA tile would waste 15 of 16 rows; here each thread owns one output pixel of a 16x16 tile, the
+// input tile (CO1_CC channels at a time) sits in LDS and the weights are wave-uniform scalar loads.
+// ------------------------------------------------------------------------------------------
+constexpr int CO1_CC = 32;
+
+__global__ __launch_bounds__(256) void conv_co1_kernel(FwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* xs = (uint16_t*)smem;
+  constexpr int XPITCH = CO1_CC + 8;
+  uint16_t* wsm = (uint16_t*)(smem + (size_t)(15 + a.ks) * (15 + a.ks) * XPITCH * 2);  // [tap][CO1_CC]
+  const int tid = threadIdx.x;
+  int bid = blockIdx.x;
+  const int tx = bid % a.tiles_x;
+  bid /= a.tiles_x;
+  const int ty = bid % a.tiles_y;
+  const int nimg = bid / a.tiles_y;
+  const int ox0 = tx * 16, oy0 = ty * 16;
+  const int py = tid >> 4, px = tid & 15;
+  const int tph = 15 + a.ks, tpw = 15 + a.ks;
+  const int iy0 = oy0 - a.pad, ix0 = ox0 - a.pad;
+  const int kcpad = a.kcpad;
+  float acc = 0.f;
+  constexpr int cvec = CO1_CC / 8;
+  const int nvec = tph * tpw * cvec;
+  for (int c0 = 0; c0 < a.in_c; c0 += CO1_CC) {
+    __syncthreads();
+    for (int base = 0; base < nvec; base += 256 * FWD_MAXV) {
+      uint4 buf[FWD_MAXV];
+#pragma unroll
+      for (int i = 0; i < FWD_MAXV; ++i) {
+        const int v = base + tid + i * 256;
+        uint4 val = make_uint4(0, 0, 0, 0);
+        if (v < nvec) {
+          const int pix = v / cvec, cg = v % cvec;  // cvec compile-time
+          const int yy = pix / tpw, xx = pix - (pix / tpw) * tpw;
+          const int iy = iy0 + yy, ix = ix0 + xx, c = c0 + cg * 8;
+          if (iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w && c < a.in_c)
+            val = *(const uint4*)(a.x + (((long)nimg * a.in_h + iy) * a.in_w + ix) * a.in_cs + a.in_co + c);
+        }
+        buf[i] = val;
+      }
+#pragma unroll
+      for (int i = 0; i < FWD_MAXV; ++i) {
+        const int v = base + tid + i * 256;
+        if (v < nvec) {
+          const int pix = v / cvec, cg = v % cvec;
+          *(uint4*)(xs + pix * XPITCH + cg * 8) = buf[i];
+        }
+      }
+    }
+    // weights of this channel chunk, [tap][CO1_CC] (packed row 0: k = (c/cc)*kcpad + tap*cc + c%cc)
+    for (int v = tid; v < a.ks * a.ks * cvec; v += 256) {
+      const int tap = v / cvec, cg = v % cvec, c = c0 + cg * 8;
+      uint4 val = make_uint4(0, 0, 0, 0);
+      if (c < a.in_c) val = *(const uint4*)(a.w + (c / a.cc) * kcpad + tap * a.cc + (c % a.cc));
+      *(uint4*)(wsm + tap * CO1_CC + cg * 8) = val;
+    }
+    __syncthreads();
+    const int cn = min(CO1_CC, a.in_c - c0);
+    for (int ky = 0; ky < a.ks; ++ky) {
+      for (int kx = 0; kx < a.ks; ++kx) {
+        const int tap = ky * a.ks + kx;
+        const uint16_t* xp = xs + ((py + ky) * tpw + px + kx) * XPITCH;
+        const uint16_t* wp = wsm + tap * CO1_CC;
+        for (int cg = 0; cg < cn; cg += 8) {
+          const uint4 wv = *(const uint4*)(wp + cg);  // same address in every lane: LDS broadcast
+          const uint4 xv = *(const uint4*)(xp + cg);
+          const uint32_t xw[4] = {xv.x, xv.y, xv.z, xv.w}, ww[4] = {wv.x, wv.y, wv.z, wv.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, xw[q]), __builtin_bit_cast(bf16x2, ww[q]), acc, false);
+        }
+      }
+    }
+  }
+  const int oy = oy0 + py, ox = ox0 + px;
+  if (oy >= a.out_h || ox >= a.out_w) return;
+  float v = acc + (a.bias ? a.bias[0] : 0.f);
+  v = act_apply(v, a.act, a.slope);
+  const long pidx = ((long)nimg * a.out_h + oy) * a.out_w + ox;
+  if (a.res1) v = v * a.alpha1 + bf2f(a.res1[pidx * a.r1_cs + a.r1_co]);
+  const long ob = pidx * a.out_cs + a.out_co;
+  if (a.out_mode == 0) ((uint16_t*)a.y)[ob] = f2bf(v);
+  else if (a.out_mode == 2) ((float*)a.y)[ob] += v;
+  else ((float*)a.y)[ob] = v;
+}
+
 template <int MW, int NT>
 static int launch_fwd(const FwdArgs& a, int ncob, size_t lds, hipStream_t s) {
   dim3 grid(a.tiles_x * a.tiles_y * a.n, ncob);
@@ -550,6 +640,13 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
   int rows = climsr_conv_packed_rows(d->out_c);
   int ncob = rows / (g.nt * 16);
   hipStream_t s = (hipStream_t)stream;
+  if (d->out_c == 1 && d->stride == 1 && d->up == 1 && !ep->down2 && !ep->res2) {
+    a.tiles_x = ceil_div(d->out_w, 16);
+    a.tiles_y = ceil_div(d->out_h, 16);
+    size_t lds = (size_t)(15 + d->ks) * (15 + d->ks) * (CO1_CC + 8) * 2 + (size_t)d->ks * d->ks * CO1_CC * 2;
+    hipLaunchKernelGGL(conv_co1_kernel, dim3(a.tiles_x * a.tiles_y * a.n), dim3(256), lds, s, a);
+    return check_launch("conv2d_fwd (co1)");
+  }
   if (mw == 4) return launch_fwd<4, 4>(a, ncob, g.lds_total, s);
   switch (g.nt) {
     case 1: return launch_fwd<2, 1>(a, ncob, g.lds_total, s);
@@ -580,7 +677,11 @@ struct WgArgs {
   int ablate;
 };
 
-template <int NTC, int TB>
+// CI4 = 1: inputs with <= 4 real channels (srcnn.conv1 / conv_first, 3 channels).  The x tile holds 4
+// channels per pixel and a B fragment's 16 columns are (4 taps x 4 channels): in the transposed read
+// each lane group p points at its own tap, so 81 taps need 21 fragments instead of 81 mostly-zero ones.
+// TB then counts tap groups of 4.
+template <int NTC, int TB, int CI4>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint16_t* xs = (uint16_t*)smem;
@@ -603,7 +704,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs a) {
   const int split = blockIdx.y;
   const int ci0 = cib * 16;
   const int co0 = cob * NTC * 16;
-  const int tap0 = tb * TB;
+  const int tap0 = tb * TB * (CI4 ? 4 : 1);
+  constexpr int XP = CI4 ? 4 : WG_XP;  // LDS x-tile pixel pitch (channels)
   const int ks2 = a.ks * a.ks;
   const bool do_bias = (cib == 0 && tb == 0 && a.bpart != nullptr);
 
@@ -619,20 +721,22 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs a) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) ones[i] = (__bf16)1.0f;
 
-  int tapoff[TB];
+  int tapoff[TB];  // per-lane LDS offset of fragment u's columns (4p..4p+3)
 #pragma unroll
   for (int u = 0; u < TB; ++u) {
-    int tap = tap0 + u;
+    int tap = CI4 ? tap0 + 4 * u + p : tap0 + u;
     if (tap >= ks2) tap = 0;  // weight rows past ks*ks are never written
-    tapoff[u] = ((tap / a.ks) * a.tpw + (tap % a.ks)) * WG_XP;
+    tapoff[u] = ((tap / a.ks) * a.tpw + (tap % a.ks)) * XP + (CI4 ? 0 : 4 * p);
   }
 
   const int lh = a.in_h * a.up, lw = a.in_w * a.up;  // up in {1, 2} here
   const int upsh = a.up == 2 ? 1 : 0;
   constexpr int zvec = NTC * 2;  // 16B vectors of dz per pixel
-  const int x_dy = 128 / a.tpw, x_dx = 128 - x_dy * a.tpw;  // +256 vectors = +128 pixels
-  const int x_ty0 = (tid >> 1) / a.tpw, x_tx0 = (tid >> 1) - x_ty0 * a.tpw;
-  const int nvec_x = a.tph * a.tpw * 2;
+  constexpr int XSTEP = CI4 ? 256 : 128;  // pixels advanced per 256 staging vectors
+  const int x_dy = XSTEP / a.tpw, x_dx = XSTEP - x_dy * a.tpw;
+  const int xpix0 = CI4 ? tid : (tid >> 1);
+  const int x_ty0 = xpix0 / a.tpw, x_tx0 = xpix0 - x_ty0 * a.tpw;
+  const int nvec_x = a.tph * a.tpw * (CI4 ? 1 : 2);
   const int nvec_z = WG_TH * TW * zvec;
 
   for (int tile = split; tile < a.ntiles; tile += a.nsplit) {
@@ -658,20 +762,32 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs a) {
           dst[i] = -1;
           if (base + i < nrx && ty_ < a.tph) {
             const int iy = iy0 + ty_, ix = ix0 + tx_;
-            const int c = ci0 + h * 8;
+            const int c = ci0 + (CI4 ? 0 : h * 8);
             uint4 val = make_uint4(0, 0, 0, 0);
-            if (!(a.ablate & 1) && iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c)
-              val = *(const uint4*)(a.x + (((long)nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + c);
+            const bool ok = !(a.ablate & 1) && iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c;
+            const long src = (((long)nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + c;
+            if (CI4) {
+              if (ok) {
+                uint2 v2 = *(const uint2*)(a.x + src);
+                val.x = v2.x;
+                val.y = v2.y;
+              }
+            } else if (ok) {
+              val = *(const uint4*)(a.x + src);
+            }
             buf[i] = val;
-            dst[i] = (ty_ * a.tpw + tx_) * WG_XP + h * 8;
+            dst[i] = (ty_ * a.tpw + tx_) * XP + (CI4 ? 0 : h * 8);
           }
           tx_ += x_dx;
           ty_ += x_dy;
           if (tx_ >= a.tpw) { tx_ -= a.tpw; ++ty_; }
         }
 #pragma unroll
-        for (int i = 0; i < FWD_MAXV; ++i)
-          if (dst[i] >= 0) *(uint4*)(xs + dst[i]) = buf[i];
+        for (int i = 0; i < FWD_MAXV; ++i) {
+          if (dst[i] < 0) continue;
+          if (CI4) *(uint2*)(xs + dst[i]) = make_uint2(buf[i].x, buf[i].y);
+          else *(uint4*)(xs + dst[i]) = buf[i];
+        }
       }
       const int nrz = nvec_z / 256;  // exact: 256 px x zvec vectors
       for (int base = 0; base < nrz; base += FWD_MAXV) {
@@ -717,8 +833,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs a) {
         short v8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         af[t] = __builtin_bit_cast(bf16x8, v8);
       }
-      const int xb0 = ((r0 * a.stride) * a.tpw + c0_ * a.stride) * WG_XP + 4 * p;
-      const int xb1 = ((r1 * a.stride) * a.tpw + c1_ * a.stride) * WG_XP + 4 * p;
+      const int xb0 = ((r0 * a.stride) * a.tpw + c0_ * a.stride) * XP;
+      const int xb1 = ((r1 * a.stride) * a.tpw + c1_ * a.stride) * XP;
       if (do_bias) {
 #pragma unroll
         for (int t = 0; t < NTC; ++t) accb[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], ones, accb[t], 0, 0, 0);
@@ -758,7 +874,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs a) {
     }
   }
   if (wave != 0) return;
-  const int ci = ci0 + col;
+  const int ci = CI4 ? (col & 3) : ci0 + col;
   float* slab = a.part + (long)split * a.co_rows * a.kw;
 #pragma unroll
   for (int t = 0; t < NTC; ++t) {
@@ -768,7 +884,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs a) {
       if (ci < a.in_c) {
 #pragma unroll
         for (int u = 0; u < TB; ++u) {
-          const int tap = tap0 + u;
+          const int tap = CI4 ? tap0 + 4 * u + (col >> 2) : tap0 + u;
           if (tap < ks2) slab[(long)co * a.kw + ci * ks2 + tap] = acc[t][u][i];
         }
       }
@@ -778,7 +894,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs a) {
 }
 
 struct WgPlan {
-  int ntc, tb, ntapb, ncib, ncob, co_rows, tiles_x, tiles_y, ntiles, tph, tpw, dzp, kw;
+  int ntc, tb, ntapb, ncib, ncob, co_rows, tiles_x, tiles_y, ntiles, tph, tpw, dzp, kw, ci4;
   size_t lds_x, lds_z, lds_total;
 };
 
@@ -786,10 +902,18 @@ static void wg_plan(const ClimsrConvDesc* d, WgPlan* w) {
   int rows = round_up(d->out_c, 16);
   w->ntc = rows >= 64 ? 4 : (rows >= 32 ? 2 : 1);
   int ks2 = d->ks * d->ks;
-  w->tb = ks2 >= 9 ? 9 : (ks2 >= 5 ? 5 : 1);
-  if (ks2 == 25) w->tb = 5;
-  w->ntapb = ceil_div(ks2, w->tb);
-  w->ncib = ceil_div(d->in_c, 16);
+  w->ci4 = d->in_c == 4;  // <= 4 real input channels: 4 taps x 4 channels per fragment
+  if (w->ci4) {
+    int groups = ceil_div(ks2, 4);
+    w->tb = groups <= 3 ? 3 : 7;
+    w->ntapb = ceil_div(groups, w->tb);
+    w->ncib = 1;
+  } else {
+    w->tb = ks2 >= 9 ? 9 : (ks2 >= 5 ? 5 : 1);
+    if (ks2 == 25) w->tb = 5;
+    w->ntapb = ceil_div(ks2, w->tb);
+    w->ncib = ceil_div(d->in_c, 16);
+  }
   w->ncob = ceil_div(rows, w->ntc * 16);
   w->co_rows = w->ncob * w->ntc * 16;
   w->tiles_x = ceil_div(d->out_w, TW);
@@ -799,7 +923,7 @@ static void wg_plan(const ClimsrConvDesc* d, WgPlan* w) {
   w->tpw = (TW - 1) * d->stride + d->ks;
   w->dzp = w->ntc * 16 + 8;
   w->kw = d->in_c * ks2;
-  w->lds_x = (size_t)w->tph * w->tpw * WG_XP * 2;
+  w->lds_x = (size_t)w->tph * w->tpw * (w->ci4 ? 4 : WG_XP) * 2;
   w->lds_x = (w->lds_x + 15) / 16 * 16;
   w->lds_z = (size_t)WG_TH * TW * w->dzp * 2;
   size_t red = (size_t)(w->ntc * w->tb + w->ntc) * 64 * 16;
@@ -823,9 +947,9 @@ extern "C" size_t climsr_conv2d_wgrad_workspace(const ClimsrConvDesc* d, int nsp
   return (size_t)nsplit * w.co_rows * w.kw + (size_t)nsplit * w.co_rows;
 }
 
-template <int NTC, int TB>
+template <int NTC, int TB, int CI4>
 static int launch_wg(const WgArgs& a, int nblk, size_t lds, hipStream_t s) {
-  auto k = conv_wgrad_kernel<NTC, TB>;
+  auto k = conv_wgrad_kernel<NTC, TB, CI4>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -837,7 +961,8 @@ static int launch_wg(const WgArgs& a, int nblk, size_t lds, hipStream_t s) {
 
 extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, const uint16_t* dz, int dz_cstride, float* partial,
                                    float* bias_partial, int nsplit, void* stream) {
-  if (!d || !x || !dz || !partial || nsplit <= 0 || d->in_c % 8 || d->in_cstride % 8 || d->in_coff % 8 || dz_cstride % 8 ||
+  if (!d || !x || !dz || !partial || nsplit <= 0 || (d->in_c % 8 && d->in_c != 4) || d->in_cstride % 8 || d->in_coff % 8 ||
+      dz_cstride % 8 ||
       (d->up != 1 && d->up != 2) || (d->stride != 1 && d->stride != 2)) {
     set_error("conv2d_wgrad: bad args");
     return CLIMSR_EINVAL;
@@ -860,11 +985,13 @@ extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, c
   a.ablate = ablate;
   int nblk = w.ntapb * w.ncib * w.ncob;
   hipStream_t s = (hipStream_t)stream;
-#define WG_CASE(NTC, TB) \
-  if (w.ntc == NTC && w.tb == TB) return launch_wg<NTC, TB>(a, nblk, w.lds_total, s);
-  WG_CASE(1, 1) WG_CASE(2, 1) WG_CASE(4, 1)
-  WG_CASE(1, 5) WG_CASE(2, 5) WG_CASE(4, 5)
-  WG_CASE(1, 9) WG_CASE(2, 9) WG_CASE(4, 9)
+#define WG_CASE(NTC, TB, CI4) \
+  if (w.ntc == NTC && w.tb == TB && w.ci4 == CI4) return launch_wg<NTC, TB, CI4>(a, nblk, w.lds_total, s);
+  WG_CASE(1, 1, 0) WG_CASE(2, 1, 0) WG_CASE(4, 1, 0)
+  WG_CASE(1, 5, 0) WG_CASE(2, 5, 0) WG_CASE(4, 5, 0)
+  WG_CASE(1, 9, 0) WG_CASE(2, 9, 0) WG_CASE(4, 9, 0)
+  WG_CASE(1, 3, 1) WG_CASE(2, 3, 1) WG_CASE(4, 3, 1)
+  WG_CASE(1, 7, 1) WG_CASE(2, 7, 1) WG_CASE(4, 7, 1)
 #undef WG_CASE
   set_error("conv2d_wgrad: no kernel for ntc=%d tb=%d", w.ntc, w.tb);
   return CLIMSR_EINVAL;

@@ -34,18 +34,23 @@ def _fwd_nt(out_c: int) -> int:
 
 
 def fwd_kernel_name(out_c: int, out_h: int = 16) -> str:
+    if out_c == 1:
+        return "conv_co1_kernel"
     nt = _fwd_nt(out_c)
     return f"conv_fwd_kernel<{4 if (out_h >= 12 and nt == 4) else 2}, {nt}>"
 
 
-def wgrad_kernel_name(out_c: int, ks: int) -> str:
+def wgrad_kernel_name(out_c: int, ks: int, ci4: bool = False) -> str:
     rows = round_up(out_c, 16)
     ntc = 4 if rows >= 64 else (2 if rows >= 32 else 1)
     k2 = ks * ks
-    tb = 9 if k2 >= 9 else (5 if k2 >= 5 else 1)
-    if k2 == 25:
-        tb = 5
-    return f"conv_wgrad_kernel<{ntc}, {tb}>"
+    if ci4:
+        tb = 3 if (k2 + 3) // 4 <= 3 else 7
+    else:
+        tb = 9 if k2 >= 9 else (5 if k2 >= 5 else 1)
+        if k2 == 25:
+            tb = 5
+    return f"conv_wgrad_kernel<{ntc}, {tb}, {int(ci4)}>"
 
 
 def _run(name, flops, fn, tag=""):
@@ -150,9 +155,14 @@ class ConvPlan:
             _lib.load().climsr_conv2d_fwd(ctypes.byref(d), ptr(dz), ptr(self.wpk_t), None, ctypes.byref(ep), ptr(g),
                                           _lib.stream_ptr()), f"conv dgrad {self.name}"), "dgrad " + self.name)
 
+    @property
+    def cin_w(self) -> int:
+        """Input channels as seen by the wgrad kernel: 4 selects the <=4-real-channel (tap-packed) variant."""
+        return 4 if self.cin_real <= 4 else self.cin
+
     def wgrad_desc(self, n, in_h, in_w, x_cs, x_co, up):
         oh, ow = self.out_hw(in_h, in_w, up)
-        return ConvDesc(n, in_h, in_w, self.cin, x_cs, x_co, up, self.ks, self.stride, self.pad, oh, ow, self.cout, 0, 0,
+        return ConvDesc(n, in_h, in_w, self.cin_w, x_cs, x_co, up, self.ks, self.stride, self.pad, oh, ow, self.cout, 0, 0,
                         self.cc)
 
     def wgrad(self, x: torch.Tensor, x_cs: int, x_co: int, in_h: int, in_w: int, dz: torch.Tensor, dz_cs: int, n: int,
@@ -163,16 +173,17 @@ class ConvPlan:
         ns = lib.climsr_conv2d_wgrad_splits(ctypes.byref(d))
         need = lib.climsr_conv2d_wgrad_workspace(ctypes.byref(d), ns)
         ws = workspace.get(need, x.device)
-        rows_c = need // (ns * (self.cin * self.ks * self.ks + 1))  # co_rows
+        cw = self.cin_w
+        rows_c = need // (ns * (cw * self.ks * self.ks + 1))  # co_rows
         part = ws
-        bpart = ws[ns * rows_c * self.cin * self.ks * self.ks:]
+        bpart = ws[ns * rows_c * cw * self.ks * self.ks:]
         s = _lib.stream_ptr()
         has_b = self.bias is not None and self.gb is not None
         flops = 2 * self.cin_real * self.cout * self.ks * self.ks * n * d.out_h * d.out_w
-        _run(wgrad_kernel_name(self.cout, self.ks), flops, lambda: check(
+        _run(wgrad_kernel_name(self.cout, self.ks, self.cin_w == 4), flops, lambda: check(
             lib.climsr_conv2d_wgrad(ctypes.byref(d), ptr(x), ptr(dz), dz_cs, ptr(part), ptr(bpart) if has_b else None, ns, s),
             f"conv wgrad {self.name}"), "wgrad " + self.name)
-        check(lib.climsr_conv2d_wgrad_reduce(ptr(part), ptr(bpart) if has_b else None, ns, self.cout, self.cin_real, self.cin,
+        check(lib.climsr_conv2d_wgrad_reduce(ptr(part), ptr(bpart) if has_b else None, ns, self.cout, self.cin_real, cw,
                                              self.ks, ptr(self.gw), ptr(self.gb) if has_b else None,
                                              1 if accumulate else 0, s), f"wgrad reduce {self.name}")
 

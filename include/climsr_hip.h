@@ -96,7 +96,8 @@ int climsr_pack_conv_weights_batched(const ClimsrPackDesc* descs, int ndesc, int
 int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, const uint16_t* wpk, const float* bias,
                       const ClimsrEpilogue* ep, void* y, void* stream);
 
-/* Weight (+ bias) gradient partials: partial[split][out_c_pad16][in_c*ks*ks] (OIHW order) and
+/* Weight (+ bias) gradient partials (d->in_c may be 4 = "at most 4 real input channels", which packs
+ * 4 taps x 4 channels per MFMA fragment; the input buffer still has a multiple-of-8 channel stride): partial[split][out_c_pad16][in_c*ks*ks] (OIHW order) and
  * bias_partial[split][out_c_pad16].  dz: bf16 NHWC [n][out_h][out_w][dz_cstride]. */
 int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, const uint16_t* dz, int dz_cstride,
                         float* partial, float* bias_partial, int nsplit, void* stream);

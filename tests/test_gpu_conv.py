@@ -137,6 +137,7 @@ def test_conv_dgrad_matches_autograd(cin, cout, ks, up, down, h, w):
 
 
 @pytest.mark.parametrize("cin,cout,ks,stride,up", [(64, 16, 3, 1, 1), (128, 64, 3, 1, 1), (112, 16, 3, 1, 1), (8, 64, 3, 1, 1),
+                                                   (3, 64, 3, 1, 1), (1, 64, 3, 1, 1), (3, 64, 5, 1, 1),
                                                    (64, 64, 3, 1, 2), (32, 1, 5, 1, 1), (3, 64, 9, 1, 1), (64, 32, 1, 1, 1),
                                                    (64, 128, 3, 2, 1), (64, 1, 3, 1, 1)])
 def test_conv_wgrad_matches_autograd(cin, cout, ks, stride, up):
@@ -187,3 +188,20 @@ def test_conv_dgrad_stride2_matches_autograd(cin, cout, h):
     y = F.conv2d(x, bf(wt).double(), None, stride=2, padding=1)
     (gref,) = torch.autograd.grad(y, x, dz.double())
     check_close(from_nhwc(gx, cin).cpu(), gref, tol=2e-5, what="dgrad s2")
+
+
+@pytest.mark.parametrize("cin,cout,ks,h,w", [(3, 64, 9, 40, 36), (1, 64, 3, 20, 20)])
+def test_conv_dgrad_single_output_channel(cin, cout, ks, h, w):
+    """dgrad restricted to input channel 0 (srcnn.conv1 w.r.t. conv_last's output): VALU dot2 kernel."""
+    n = 2
+    p, wt, b = make_plan(cin, cout, ks)
+    g = torch.Generator().manual_seed(8)
+    dz = bf(torch.rand((n, cout, h, w), generator=g) * 2 - 1)
+    dzb = to_nhwc(dz)
+    gx = torch.zeros((n, h, w, p.cin), dtype=torch.float32, device=DEV)
+    p.dgrad(dzb, dzb.shape[-1], h, w, gx, p.cin, 0, n, cout_t=1)
+    torch.cuda.synchronize()
+    x = torch.zeros((n, cin, h, w), dtype=torch.float64, requires_grad=True)
+    y = F.conv2d(x, bf(wt).double(), None, padding=ks // 2)
+    (gref,) = torch.autograd.grad(y, x, dz.double())
+    check_close(gx[..., :1].permute(0, 3, 1, 2).cpu(), gref[:, :1], tol=2e-5, what="dgrad co1")
