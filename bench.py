@@ -46,6 +46,23 @@ def parse():
     return ap.parse_args()
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
+    (profiles/r*_pmc_traffic.json: separate FETCH_SIZE / WRITE_SIZE passes of this bench,
+    FETCH_SIZE x2 gfx950 correction, MI355X_MICROARCH.md).  None if no summary covers it."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    for f in reversed(files):
+        try:
+            rec = json.load(open(f))["kernels"].get(kernel)
+        except (OSError, ValueError, KeyError):
+            continue
+        if rec:
+            return rec["hbm_bytes_per_launch"], os.path.basename(f)
+    return None, None
+
+
 class KernelTimer:
     """HIP-event timer around individual launches (ops.PROFILER hook), grouped by kernel name."""
 
@@ -288,6 +305,10 @@ def main():
         roof = {"bound": "mfma", "kernel": name, "launches_per_step": cnt, "avg_launch_us": round(avg_ms * 1e3, 2),
                 "flop_per_launch": flops // cnt, "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None}
+        tb, src = pmc_traffic(name)
+        if tb is not None:  # HBM bytes per launch (PMC) and the bandwidth they imply at the measured launch time
+            roof.update(traffic=round(tb / 1e6, 2), traffic_unit="MB/launch", traffic_source=src,
+                        traffic_gbs=round(tb / (avg_ms / 1e3) / 1e9, 1))
         kern = {k: {"launches": v[0], "ms_total": round(v[1], 3), "tflops": round(v[2] / (v[1] / 1e3) / 1e12, 1)}
                 for k, v in sorted(agg.items(), key=lambda kv: -kv[1][1])}
         if os.environ.get("CLIMSR_BENCH_DETAIL"):

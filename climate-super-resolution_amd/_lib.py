@@ -29,12 +29,26 @@ class Epilogue(ctypes.Structure):
     _fields_ = [("act", ctypes.c_int32), ("slope", c_float), ("alpha1", c_float), ("res1", c_void_p),
                 ("res1_cstride", ctypes.c_int32), ("res1_coff", ctypes.c_int32), ("alpha2", c_float), ("res2", c_void_p),
                 ("res2_cstride", ctypes.c_int32), ("res2_coff", ctypes.c_int32), ("out_mode", ctypes.c_int32),
-                ("down2", ctypes.c_int32)]
+                ("down2", ctypes.c_int32), ("res_f32", ctypes.c_int32), ("beta1", c_float), ("beta2", c_float),
+                ("aux_cstride", ctypes.c_int32), ("aux", c_void_p), ("aux_coff", ctypes.c_int32), ("aux_scale", c_float)]
+
+    def __init__(self, *args, **kw):
+        # plain residual adds unless a caller scales them (beta1 / beta2 are positional fields 13 / 14)
+        if len(args) <= 13:
+            kw.setdefault("beta1", 1.0)
+        if len(args) <= 14:
+            kw.setdefault("beta2", 1.0)
+        super().__init__(*args, **kw)
 
 
 class PackDesc(ctypes.Structure):
     _fields_ = [("w", c_void_p), ("out", c_void_p)] + [(n, ctypes.c_int32) for n in (
         "out_c", "in_c", "in_c_real", "out_c_real", "ks", "cc", "tflip", "reserved")]
+
+
+class PullPackDesc(ctypes.Structure):
+    _fields_ = [("out", c_void_p), ("seg_w", c_void_p * 5), ("seg_oc", ctypes.c_int32 * 5), ("seg_ic", ctypes.c_int32 * 5)] + [
+        (n, ctypes.c_int32) for n in ("nseg", "out_c", "in_c", "ks", "cc", "ci_off")]
 
 
 P = ctypes.POINTER
@@ -47,6 +61,7 @@ SIGNATURES = {
     "climsr_conv_packed_rows": (c_int, [c_int]),
     "climsr_pack_conv_weight": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "climsr_pack_conv_weights_batched": (c_int, [c_void_p, c_int, c_int64, c_void_p]),
+    "climsr_pack_pull_weights_batched": (c_int, [c_void_p, c_int, c_int64, c_void_p]),
     "climsr_conv2d_fwd": (c_int, [P(ConvDesc), c_void_p, c_void_p, c_void_p, P(Epilogue), c_void_p, c_void_p]),
     "climsr_conv2d_wgrad": (c_int, [P(ConvDesc), c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "climsr_conv2d_wgrad_reduce": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,

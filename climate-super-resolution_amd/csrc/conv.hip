@@ -83,7 +83,7 @@ static void fwd_geom(int in_c, int ks, int stride, int out_c, int cc, int mw, Fw
 using namespace climsr;
 
 extern "C" const char* climsr_last_error(void) { return g_err; }
-extern "C" int climsr_version(void) { return 1; }
+extern "C" int climsr_version(void) { return 2; }
 
 extern "C" int climsr_conv_chunk(int in_c, int ks, int out_c) {
   int cc = round_up(in_c, 8);
@@ -186,6 +186,47 @@ extern "C" int climsr_pack_conv_weights_batched(const ClimsrPackDesc* descs, int
   return check_launch("pack_conv_weights_batched");
 }
 
+// Pull data-gradient weights of a residual dense block (see climsr_hip.h): one launch packs all the
+// pull convs of a network (blockIdx.y = descriptor).
+__global__ void pack_pull_kernel(const ClimsrPullPackDesc* __restrict__ descs) {
+  const ClimsrPullPackDesc d = descs[blockIdx.y];
+  const int rows = climsr_rows_dev(d.out_c);
+  const int kcpad = (d.ks * d.ks * d.cc + 31) / 32 * 32;
+  const int kpk = (d.in_c + d.cc - 1) / d.cc * kcpad;
+  const long total = (long)rows * kpk;
+  const int kk2 = d.ks * d.ks;
+  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const int co = (int)(idx / kpk);
+    const int kk = (int)(idx % kpk);
+    const int j = kk / kcpad;
+    const int kr = kk % kcpad;
+    const int tap = kr / d.cc;
+    int c = j * d.cc + kr % d.cc;
+    float v = 0.f;
+    if (co < d.out_c && tap < kk2 && c < d.in_c) {
+      int s = 0;
+      while (s < d.nseg - 1 && c >= d.seg_oc[s]) c -= d.seg_oc[s++];
+      if (c < d.seg_oc[s]) {
+        const int ky = tap / d.ks, kx = tap % d.ks;
+        v = d.seg_w[s][(((long)c * d.seg_ic[s] + d.ci_off + co) * d.ks + (d.ks - 1 - ky)) * d.ks + (d.ks - 1 - kx)];
+      }
+    }
+    d.out[idx] = f2bf(v);
+  }
+}
+
+extern "C" int climsr_pack_pull_weights_batched(const ClimsrPullPackDesc* descs, int ndesc, int64_t max_elems, void* stream) {
+  if (!descs || ndesc <= 0 || ndesc > 65535) {
+    set_error("pack_pull_weights_batched: bad args");
+    return CLIMSR_EINVAL;
+  }
+  int gx = ceil_div(max_elems, 256);
+  if (gx > 128) gx = 128;
+  if (gx < 1) gx = 1;
+  hipLaunchKernelGGL(pack_pull_kernel, dim3(gx, ndesc), dim3(256), 0, (hipStream_t)stream, descs);
+  return check_launch("pack_pull_weights_batched");
+}
+
 // ------------------------------------------------------------------------------------------
 // Forward / data-gradient kernel
 // ------------------------------------------------------------------------------------------
@@ -194,18 +235,50 @@ struct FwdArgs {
   const uint16_t* w;
   const float* bias;
   void* y;
-  const uint16_t* res1;
-  const uint16_t* res2;
+  const void* res1;
+  const void* res2;
+  uint16_t* aux;
   int n, in_h, in_w, in_c, in_cs, in_co, up, ks, stride, pad, out_h, out_w, out_c, out_cs, out_co, cc;
   int tph, tpw, ccp, kcpad, nchunk, kpk, tiles_x, tiles_y;
   int act, out_mode, down2;
   float slope, alpha1, alpha2;
   int r1_cs, r1_co, r2_cs, r2_co;
+  int res_f32;
+  float beta1, beta2;
+  int aux_cs, aux_co;
+  float aux_scale;
   int lds_tab, lds_x;
-  int ablate;  // diagnostics only (CLIMSR_ABLATE): 1 skip global loads, 2 skip MFMA, 4 skip stores
+  int ablate;  // diagnostics only (CLIMSR_ABLATE): 1 skip global loads, 2 skip MFMA, 4 skip stores, 8 skip staging
 };
 
-template <int MW, int NT>
+// Epilogue residual operands: 4 consecutive channels, bf16 (8 B) or fp32 (16 B), kept raw until use so
+// that all loads of a round are in flight together.
+__device__ __forceinline__ uint4 load_res4(const void* p, bool f32, long idx) {
+  if (f32) return *(const uint4*)((const float*)p + idx);
+  const uint2 v = *(const uint2*)((const uint16_t*)p + idx);
+  return make_uint4(v.x, v.y, 0, 0);
+}
+__device__ __forceinline__ float res4_at(const uint4& r, bool f32, int i) {
+  if (f32) return __uint_as_float(i == 0 ? r.x : i == 1 ? r.y : i == 2 ? r.z : r.w);
+  const uint32_t w = (i < 2) ? r.x : r.y;
+  return bf2f((uint16_t)((i & 1) ? (w >> 16) : w));
+}
+__device__ __forceinline__ float res_at(const void* p, bool f32, long idx) {
+  return f32 ? ((const float*)p)[idx] : bf2f(((const uint16_t*)p)[idx]);
+}
+// v after bias (+ forward activation): apply res1 (residual, or activation-backward mask for act 3/4), res2
+__device__ __forceinline__ float ep_res(float v, int act, float slope, bool has1, float r1, float alpha1, float beta1, bool has2,
+                                        float r2, float alpha2, float beta2) {
+  if (act == 3) v = r1 > 0.f ? v : v * slope;
+  else if (act == 4) v = r1 > 0.f ? v : 0.f;
+  else if (has1) v = v * alpha1 + beta1 * r1;
+  if (has2) v = v * alpha2 + beta2 * r2;
+  return v;
+}
+
+// RF: the epilogue may read fp32 residuals (then one output row per round, to stay within 256 registers)
+// MV: staging vectors (16 B) per thread and stream held in registers per batch
+template <int MW, int NT, bool RF, int MV>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int* tab = (int*)smem;
@@ -288,59 +361,52 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
     }
   };
 
-  // batched staging: every thread issues up to FWD_MAXV independent 16 B global loads before the
-  // first LDS store, so a chunk pays ~one memory latency instead of one per vector
+  // batched staging: every thread issues up to MV input + MV weight 16 B global loads before the first
+  // LDS store, so a chunk pays ~one memory latency instead of one per vector
+  const int nbatch = nrx > nrw ? nrx : nrw;
   for (int j = 0; j < a.nchunk; ++j) {
     __syncthreads();
-    {  // input tile (logical coordinates: upsampled / zero-inserted; zero padding)
-      int ty_ = x_ty0, tx_ = x_tx0, cg = x_cg0;
-      for (int base = 0; base < nrx; base += FWD_MAXV) {
-        uint4 buf[FWD_MAXV];
-        int dst[FWD_MAXV];
+    int ty_ = x_ty0, tx_ = x_tx0, cg = x_cg0;  // input tile (logical coordinates: upsampled / zero-inserted)
+    int r = w_r0, kv = w_k0;                  // weight chunk rows [co_blk0, co_blk0 + 16*NT) x kcpad
+    for (int base = 0; base < ((a.ablate & 8) ? 0 : nbatch); base += MV) {
+      uint4 bx[MV], bw[MV];
+      int dx[MV], dw[MV];
 #pragma unroll
-        for (int i = 0; i < FWD_MAXV; ++i) {
-          dst[i] = -1;
-          if (base + i < nrx && ty_ < a.tph) {
-            const int iy = iy0 + ty_, ix = ix0 + tx_;
-            const int c = j * a.cc + cg * 8;
-            uint4 val = make_uint4(0, 0, 0, 0);
-            if (!(a.ablate & 1) && iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c && !((iy | ix) & dilmask))
-              val = *(const uint4*)(a.x + (((long)nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + c);
-            buf[i] = val;
-            dst[i] = (ty_ * a.tpw + tx_) * a.ccp + cg * 8;
-          }
-          cg += x_dc;
-          tx_ += x_dx;
-          ty_ += x_dy;
-          if (cg >= cvec) { cg -= cvec; ++tx_; }
-          if (tx_ >= a.tpw) { tx_ -= a.tpw; ++ty_; }
+      for (int i = 0; i < MV; ++i) {
+        dx[i] = -1;
+        if (base + i < nrx && ty_ < a.tph) {
+          const int iy = iy0 + ty_, ix = ix0 + tx_;
+          const int c = j * a.cc + cg * 8;
+          uint4 val = make_uint4(0, 0, 0, 0);
+          if (!(a.ablate & 1) && iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c && !((iy | ix) & dilmask))
+            val = *(const uint4*)(a.x + (((long)nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + c);
+          bx[i] = val;
+          dx[i] = (ty_ * a.tpw + tx_) * a.ccp + cg * 8;
         }
-#pragma unroll
-        for (int i = 0; i < FWD_MAXV; ++i)
-          if (dst[i] >= 0) *(uint4*)(xs + dst[i]) = buf[i];
+        cg += x_dc;
+        tx_ += x_dx;
+        ty_ += x_dy;
+        if (cg >= cvec) { cg -= cvec; ++tx_; }
+        if (tx_ >= a.tpw) { tx_ -= a.tpw; ++ty_; }
       }
-    }
-    {  // weight chunk rows [co_blk0, co_blk0 + 16*NT) x kcpad
-      int r = w_r0, kv = w_k0;
-      for (int base = 0; base < nrw; base += FWD_MAXV) {
-        uint4 buf[FWD_MAXV];
-        int dst[FWD_MAXV];
 #pragma unroll
-        for (int i = 0; i < FWD_MAXV; ++i) {
-          dst[i] = -1;
-          if (base + i < nrw && r < NT * 16) {
-            buf[i] = (a.ablate & 1) ? make_uint4(0, 0, 0, 0)
-                                    : *(const uint4*)(a.w + (long)(co_blk0 + r) * a.kpk + (long)j * a.kcpad + kv * 8);
-            dst[i] = r * wpitch + kv * 8;
-          }
-          kv += w_dk;
-          r += w_dr;
-          if (kv >= wvec_row) { kv -= wvec_row; ++r; }
+      for (int i = 0; i < MV; ++i) {
+        dw[i] = -1;
+        if (base + i < nrw && r < NT * 16) {
+          bw[i] = (a.ablate & 1) ? make_uint4(0, 0, 0, 0)
+                                 : *(const uint4*)(a.w + (long)(co_blk0 + r) * a.kpk + (long)j * a.kcpad + kv * 8);
+          dw[i] = r * wpitch + kv * 8;
         }
-#pragma unroll
-        for (int i = 0; i < FWD_MAXV; ++i)
-          if (dst[i] >= 0) *(uint4*)(ws + dst[i]) = buf[i];
+        kv += w_dk;
+        r += w_dr;
+        if (kv >= wvec_row) { kv -= wvec_row; ++r; }
       }
+#pragma unroll
+      for (int i = 0; i < MV; ++i)
+        if (dx[i] >= 0) *(uint4*)(xs + dx[i]) = bx[i];
+#pragma unroll
+      for (int i = 0; i < MV; ++i)
+        if (dw[i] >= 0) *(uint4*)(ws + dw[i]) = bw[i];
     }
     __syncthreads();
     if (!(a.ablate & 2)) compute();
@@ -418,12 +484,14 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
   }
   // two output rows (fragments) per round: operand loads for both rows are in flight together while
   // the register footprint stays at 2*NT fragments
+  const bool f1 = RF && (a.res_f32 & 1), f2 = RF && ((a.res_f32 >> 1) & 1);
+  constexpr int EPR = RF ? 1 : 2;  // output rows per epilogue round
 #pragma unroll
-  for (int mm = 0; mm < MW; mm += 2) {
-    uint2 r1v[2][NT], r2v[2][NT];
-    float4 old[2][NT];
+  for (int mm = 0; mm < MW; mm += EPR) {
+    uint4 r1v[EPR][NT], r2v[EPR][NT];
+    float4 old[EPR][NT];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < EPR; ++h) {
       const int m = mm + h;
       const int oy = oy0 + wave * MW + m;
       const bool pv = oy < a.out_h && ox < a.out_w;
@@ -432,18 +500,18 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
       for (int t = 0; t < NT; ++t) {
         const int co = co_blk0 + t * 16 + g * 4;
         const bool vec = pv && valign && co + 3 < a.out_c;
-        r1v[h][t] = make_uint2(0, 0);
-        r2v[h][t] = make_uint2(0, 0);
+        r1v[h][t] = make_uint4(0, 0, 0, 0);
+        r2v[h][t] = make_uint4(0, 0, 0, 0);
         old[h][t] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (vec) {
-          if (a.res1) r1v[h][t] = *(const uint2*)(a.res1 + pidx * a.r1_cs + a.r1_co + co);
-          if (a.res2) r2v[h][t] = *(const uint2*)(a.res2 + pidx * a.r2_cs + a.r2_co + co);
+          if (a.res1) r1v[h][t] = load_res4(a.res1, f1, pidx * a.r1_cs + a.r1_co + co);
+          if (a.res2) r2v[h][t] = load_res4(a.res2, f2, pidx * a.r2_cs + a.r2_co + co);
           if (a.out_mode == 2) old[h][t] = *(const float4*)((const float*)a.y + pidx * a.out_cs + a.out_co + co);
         }
       }
     }
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < EPR; ++h) {
       const int m = mm + h;
       const int oy = oy0 + wave * MW + m;
       const bool pv = oy < a.out_h && ox < a.out_w;
@@ -459,16 +527,10 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
         for (int i = 0; i < 4; ++i) v[i] = act_apply(acc[m][t][i] + bb[i], a.act, a.slope);
         const long ob = pidx * a.out_cs + a.out_co + co;
         if (vec) {
-          if (a.res1) {
-            const uint32_t w0 = r1v[h][t].x, w1 = r1v[h][t].y;
-            v[0] = v[0] * a.alpha1 + bf2f((uint16_t)w0); v[1] = v[1] * a.alpha1 + bf2f((uint16_t)(w0 >> 16));
-            v[2] = v[2] * a.alpha1 + bf2f((uint16_t)w1); v[3] = v[3] * a.alpha1 + bf2f((uint16_t)(w1 >> 16));
-          }
-          if (a.res2) {
-            const uint32_t w0 = r2v[h][t].x, w1 = r2v[h][t].y;
-            v[0] = v[0] * a.alpha2 + bf2f((uint16_t)w0); v[1] = v[1] * a.alpha2 + bf2f((uint16_t)(w0 >> 16));
-            v[2] = v[2] * a.alpha2 + bf2f((uint16_t)w1); v[3] = v[3] * a.alpha2 + bf2f((uint16_t)(w1 >> 16));
-          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            v[i] = ep_res(v[i], a.act, a.slope, a.res1 != nullptr, res4_at(r1v[h][t], f1, i), a.alpha1, a.beta1,
+                          a.res2 != nullptr, res4_at(r2v[h][t], f2, i), a.alpha2, a.beta2);
           if (a.out_mode == 0) {
             uint2 pk;
             pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
@@ -478,16 +540,24 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
             float4 o = old[h][t];
             *(float4*)((float*)a.y + ob) = make_float4(o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]);
           }
+          if (a.aux) {
+            uint2 pk;
+            pk.x = (uint32_t)f2bf(a.aux_scale * v[0]) | ((uint32_t)f2bf(a.aux_scale * v[1]) << 16);
+            pk.y = (uint32_t)f2bf(a.aux_scale * v[2]) | ((uint32_t)f2bf(a.aux_scale * v[3]) << 16);
+            *(uint2*)(a.aux + pidx * a.aux_cs + a.aux_co + co) = pk;
+          }
         } else {  // scalar tail (out_c not a multiple of 4 or unaligned slices)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             if (co + i >= a.out_c) continue;
-            float x = v[i];
-            if (a.res1) x = x * a.alpha1 + bf2f(a.res1[pidx * a.r1_cs + a.r1_co + co + i]);
-            if (a.res2) x = x * a.alpha2 + bf2f(a.res2[pidx * a.r2_cs + a.r2_co + co + i]);
+            const float r1 = a.res1 ? res_at(a.res1, f1, pidx * a.r1_cs + a.r1_co + co + i) : 0.f;
+            const float r2 = a.res2 ? res_at(a.res2, f2, pidx * a.r2_cs + a.r2_co + co + i) : 0.f;
+            const float x = ep_res(v[i], a.act, a.slope, a.res1 != nullptr, r1, a.alpha1, a.beta1, a.res2 != nullptr, r2,
+                                   a.alpha2, a.beta2);
             if (a.out_mode == 0) ((uint16_t*)a.y)[ob + i] = f2bf(x);
             else if (a.out_mode == 2) ((float*)a.y)[ob + i] += x;
             else ((float*)a.y)[ob + i] = x;
+            if (a.aux) a.aux[pidx * a.aux_cs + a.aux_co + co + i] = f2bf(a.aux_scale * x);
           }
         }
       }
@@ -578,20 +648,28 @@ __global__ __launch_bounds__(256) void conv_co1_kernel(FwdArgs a) {
   float v = acc + (a.bias ? a.bias[0] : 0.f);
   v = act_apply(v, a.act, a.slope);
   const long pidx = ((long)nimg * a.out_h + oy) * a.out_w + ox;
-  if (a.res1) v = v * a.alpha1 + bf2f(a.res1[pidx * a.r1_cs + a.r1_co]);
+  const bool f1 = a.res_f32 & 1, f2 = (a.res_f32 >> 1) & 1;
+  const float r1 = a.res1 ? res_at(a.res1, f1, pidx * a.r1_cs + a.r1_co) : 0.f;
+  const float r2 = a.res2 ? res_at(a.res2, f2, pidx * a.r2_cs + a.r2_co) : 0.f;
+  v = ep_res(v, a.act, a.slope, a.res1 != nullptr, r1, a.alpha1, a.beta1, a.res2 != nullptr, r2, a.alpha2, a.beta2);
   const long ob = pidx * a.out_cs + a.out_co;
   if (a.out_mode == 0) ((uint16_t*)a.y)[ob] = f2bf(v);
   else if (a.out_mode == 2) ((float*)a.y)[ob] += v;
   else ((float*)a.y)[ob] = v;
+  if (a.aux) a.aux[pidx * a.aux_cs + a.aux_co] = f2bf(a.aux_scale * v);
 }
 
 template <int MW, int NT>
 static int launch_fwd(const FwdArgs& a, int ncob, size_t lds, hipStream_t s) {
   dim3 grid(a.tiles_x * a.tiles_y * a.n, ncob);
-  auto k = conv_fwd_kernel<MW, NT>;
+  constexpr int MV = NT == 1 ? 6 : (NT == 2 ? 8 : 4);
+  auto k = a.res_f32 ? conv_fwd_kernel<MW, NT, true, MV> : conv_fwd_kernel<MW, NT, false, MV>;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)conv_fwd_kernel<MW, NT, true, MV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void*)conv_fwd_kernel<MW, NT, false, MV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
     attr_set = true;
   }
   hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a);
@@ -611,8 +689,16 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
               d->in_coff, d->cc, d->up, d->stride, d->ks);
     return CLIMSR_EINVAL;
   }
-  if (ep->down2 && (ep->out_mode == 0 || ep->res1 || ep->res2 || bias || ep->act || (d->out_h & 1) || (d->out_w & 1))) {
-    set_error("conv2d_fwd: down2 epilogue needs f32 output, no bias/act/residual, even output size");
+  if (ep->down2 && (ep->out_mode == 0 || ep->res1 || ep->res2 || ep->aux || bias || ep->act || (d->out_h & 1) || (d->out_w & 1))) {
+    set_error("conv2d_fwd: down2 epilogue needs f32 output, no bias/act/residual/aux, even output size");
+    return CLIMSR_EINVAL;
+  }
+  if (ep->act < 0 || ep->act > 4 || ((ep->act == 3 || ep->act == 4) && !ep->res1)) {
+    set_error("conv2d_fwd: act %d invalid (3/4 need res1 = the activation output)", ep->act);
+    return CLIMSR_EINVAL;
+  }
+  if (ep->aux && ((ep->aux_cstride | ep->aux_coff) & 3)) {
+    set_error("conv2d_fwd: aux channel stride/offset must be multiples of 4");
     return CLIMSR_EINVAL;
   }
   FwdGeom g;
@@ -625,7 +711,9 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
   }
   FwdArgs a;
   a.x = x; a.w = wpk; a.bias = bias; a.y = y;
-  a.res1 = (const uint16_t*)ep->res1; a.res2 = (const uint16_t*)ep->res2;
+  a.res1 = ep->res1; a.res2 = ep->res2; a.aux = (uint16_t*)ep->aux;
+  a.res_f32 = ep->res_f32; a.beta1 = ep->beta1; a.beta2 = ep->beta2;
+  a.aux_cs = ep->aux_cstride; a.aux_co = ep->aux_coff; a.aux_scale = ep->aux_scale;
   a.n = d->n; a.in_h = d->in_h; a.in_w = d->in_w; a.in_c = d->in_c; a.in_cs = d->in_cstride; a.in_co = d->in_coff;
   a.up = d->up; a.ks = d->ks; a.stride = d->stride; a.pad = d->pad; a.out_h = d->out_h; a.out_w = d->out_w;
   a.out_c = d->out_c; a.out_cs = d->out_cstride; a.out_co = d->out_coff; a.cc = d->cc;

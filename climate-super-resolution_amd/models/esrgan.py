@@ -24,8 +24,8 @@ import torch.nn as nn
 from torch import Tensor
 
 from ..core.flat import FlatParamsMixin
-from ..ops import (ACT_LRELU, ACT_NONE, ACT_RELU, OUT_F32, BatchedPacker, ConvPlan, Workspace, act_grad, axpby, nchw_to_nhwc,
-                   rdb_bwd_init)
+from ..ops import (ACT_LRELU, ACT_LRELU_BWD, ACT_NONE, ACT_RELU, OUT_F32, BatchedPacker, ConvPlan, PullPacker, PullPlan, Workspace,
+                   act_grad, axpby, nchw_to_nhwc)
 from .srcnn import SRCNN
 
 
@@ -107,10 +107,29 @@ class _Engine:
     # ------------------------------------------------------------------ weights
     def bind(self):
         gen = self.gen
+        nf, gc = self.nf, self.gc
         for name, p in self.plans.items():
             conv = self.modules[name]
-            p.bind(conv.weight, conv.bias, need_t=(name != "conv_first"))
-        self.packer = BatchedPacker(list(self.plans.values()), gen.conv_first.weight.device)
+            # RDB convs need no transposed weights: their data gradients run as pull convs (below)
+            p.bind(conv.weight, conv.bias, need_t=(name != "conv_first" and ".RDB" not in name))
+        dev = gen.conv_first.weight.device
+        self.packer = BatchedPacker(list(self.plans.values()), dev)
+        # Pull-form RDB backward: the dense concatenation's channel group j (0 = x, 1..4 = x1..x4) receives the
+        # transposed convs of conv j+1..conv5, whose output gradients sit side by side in one buffer
+        # dZ = [dZ1|dZ2|dZ3|dZ4|dZ5] (gc,gc,gc,gc,nf channels): group j's gradient is one conv over dZ[:, j*gc:].
+        self.pulls: List[List[PullPlan]] = []
+        for i in range(3 * self.nb):
+            blk, r = divmod(i, 3)
+            lst = []
+            for j in range(5):
+                segs = []
+                for k in range(j + 1, 6):
+                    w = self.modules[self.rdb_name(blk, r + 1, k)].weight
+                    segs.append((w, gc if k < 5 else nf, nf + (k - 1) * gc))
+                lst.append(PullPlan(segs, nf if j == 0 else gc, 0 if j == 0 else nf + (j - 1) * gc, 3,
+                                    f"RRDB_trunk.{blk}.RDB{r + 1}.pull{j}"))
+            self.pulls.append(lst)
+        self.pull_packer = PullPacker([p for lst in self.pulls for p in lst], dev)
         self.version = -1
 
     def bind_grads(self):
@@ -123,10 +142,12 @@ class _Engine:
         v = self.gen._flat._version
         if v != self.version:
             self.packer.run()
+            self.pull_packer.run()
             self.version = v
 
     def repack(self):
         self.packer.run()
+        self.pull_packer.run()
         self.version = self.gen._flat._version
 
     def rdb_name(self, i, r, c):
@@ -259,34 +280,39 @@ class _Engine:
         P["upconv1"].dgrad(dz_u1, nf, h2, w2, g_fea2, nf, 0, n, down2=True)
         # ---- trunk_conv + global skip (esrgan.py:90-91)
         dz64 = self._scratch("dz64", (n, h, w, nf), torch.bfloat16, dev)
-        dz16 = self._scratch("dz16", (n, h, w, gc), torch.bfloat16, dev)
         act_grad(npx_lr, nf, g_fea2, nf, 0, None, 0, 0, ACT_NONE, dz64, nf)
         dense = sv["dense"]
-        P["trunk_conv"].wgrad(dense[3 * nb], dc, 0, h, w, dz64, nf, n, ws, acc)
-        gX = self._scratch("gA", (n, h, w, dc), torch.float32, dev)
-        gY = self._scratch("gB", (n, h, w, dc), torch.float32, dev)
-        gskip = self._scratch("gskip", (n, h, w, nf), torch.float32, dev)
-        P["trunk_conv"].dgrad(dz64, nf, h, w, gX, dc, 0, n)
-        # ---- RRDB trunk, reverse (esrgan.py:32-54)
-        for i in reversed(range(3 * nb)):
+        L = 3 * nb
+        P["trunk_conv"].wgrad(dense[L], dc, 0, h, w, dz64, nf, n, ws, acc)
+        # G[k]: fp32 [n,h,w,nf] gradients at RDB boundaries (4-way rotation keeps each RRDB's skip gradient alive);
+        # dZ[k]: bf16 [n,h,w,dc] output gradients of one RDB's five convs, side by side (ping-pong)
+        G = [self._scratch(f"G{k}", (n, h, w, nf), torch.float32, dev) for k in range(4)]
+        dZ = [self._scratch(f"dZ{k}", (n, h, w, dc), torch.bfloat16, dev) for k in range(2)]
+        # the last RDB (r = 2) sees 0.2 * G at its output; its conv5 output gradient is 0.2 * that
+        P["trunk_conv"].dgrad(dz64, nf, h, w, G[L % 4], nf, 0, n, aux=dZ[(L - 1) % 2], aux_cs=dc, aux_co=4 * gc, aux_scale=0.04)
+        # ---- RRDB trunk, reverse (esrgan.py:32-54), pull form
+        for i in reversed(range(L)):
             blk, r = divmod(i, 3)
-            # r == 2: this RDB's output is the RRDB's (out*0.2 + x): save the skip gradient, scale by 0.2
-            a_o = 0.2 if r == 2 else 1.0
-            rdb_bwd_init(npx_lr, nf, dc, gX, gY, gskip, dz64, a_o, save_skip=(r == 2), add_skip=(r == 0))
-            src = dense[i]
-            c5 = P[self.rdb_name(blk, r + 1, 5)]
-            c5.wgrad(src, dc, 0, h, w, dz64, nf, n, ws, acc)
-            c5.dgrad(dz64, nf, h, w, gY, dc, 0, n, accumulate=True)
-            for c in (4, 3, 2, 1):
-                co = nf + (c - 1) * gc
-                act_grad(npx_lr, gc, gY, dc, co, src, dc, co, ACT_LRELU, dz16, gc)
-                pc = P[self.rdb_name(blk, r + 1, c)]
-                pc.wgrad(src, dc, 0, h, w, dz16, gc, n, ws, acc)
-                pc.dgrad(dz16, gc, h, w, gY, dc, 0, n, accumulate=True)
-            gX, gY = gY, gX
+            s_o = 0.2 if r == 2 else 1.0  # RDB3's output enters the RRDB output scaled by 0.2 (esrgan.py:54)
+            g_out, g_in, g_skip = G[(i + 1) % 4], G[i % 4], G[(3 * blk + 3) % 4]
+            dz, src, pulls = dZ[i % 2], dense[i], self.pulls[i]
+            # dZ_j = lrelu'(x_j) * sum_{k>j} conv_k^T(dZ_k)   (x_j = channels nf+(j-1)gc.. of the dense buffer)
+            for j in (4, 3, 2, 1):
+                pulls[j].fwd(dz, dc, j * gc, h, w, dz, dc, (j - 1) * gc, n, act=ACT_LRELU_BWD, use_bias=False,
+                             res1=src, res1_cs=dc, res1_co=nf + (j - 1) * gc)
+            # G_in = sum_k conv_k^T(dZ_k) + s_o * G_out (+ the RRDB skip gradient at its first RDB); the next
+            # (earlier) RDB's conv5 output gradient dZ5 = 0.2 * s_o' * G_in is written alongside
+            aux = dZ[(i - 1) % 2] if i > 0 else None
+            pulls[0].fwd(dz, dc, 0, h, w, g_in, nf, 0, n, use_bias=False, out_mode=OUT_F32,
+                         res1=g_out, res1_cs=nf, res1_co=0, beta1=s_o,
+                         res2=g_skip if r == 0 else None, res2_cs=nf, res2_co=0,
+                         aux=aux, aux_cs=dc, aux_co=4 * gc, aux_scale=0.2 * (0.2 if r == 0 else 1.0))
+            for k in range(1, 6):
+                off = (k - 1) * gc
+                self.plans[self.rdb_name(blk, r + 1, k)].wgrad(src, dc, 0, h, w, dz[..., off:], dc, n, ws, acc)
         # ---- conv_first: grad wrt fea = trunk path + global skip
-        axpby(npx_lr, nf, 1.0, g_fea2, nf, 0, 1.0, gX, dc, 0)
-        act_grad(npx_lr, nf, gX, dc, 0, None, 0, 0, ACT_NONE, dz64, nf)
+        axpby(npx_lr, nf, 1.0, g_fea2, nf, 0, 1.0, G[0], nf, 0)
+        act_grad(npx_lr, nf, G[0], nf, 0, None, 0, 0, ACT_NONE, dz64, nf)
         P["conv_first"].wgrad(sv["lr"], self.cin_pad, 0, h, w, dz64, nf, n, ws, acc)
 
 

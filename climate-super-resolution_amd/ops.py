@@ -13,9 +13,10 @@ from typing import Optional
 import torch
 
 from . import _lib
-from ._lib import ConvDesc, Epilogue, PackDesc, check, ptr
+from ._lib import ConvDesc, Epilogue, PackDesc, PullPackDesc, check, ptr
 
 ACT_NONE, ACT_LRELU, ACT_RELU = 0, 1, 2
+ACT_LRELU_BWD, ACT_RELU_BWD = 3, 4  # epilogue multiplies by act'(res1), res1 = the activation's output
 OUT_BF16, OUT_F32, OUT_F32_ADD = 0, 1, 2
 
 
@@ -33,11 +34,12 @@ def _fwd_nt(out_c: int) -> int:
     return 4 if nt >= 3 else nt
 
 
-def fwd_kernel_name(out_c: int, out_h: int = 16) -> str:
+def fwd_kernel_name(out_c: int, out_h: int = 16, res_f32: bool = False) -> str:
     if out_c == 1:
         return "conv_co1_kernel"
     nt = _fwd_nt(out_c)
-    return f"conv_fwd_kernel<{4 if (out_h >= 12 and nt == 4) else 2}, {nt}>"
+    mv = {1: 6, 2: 8, 4: 4}[nt]
+    return f"conv_fwd_kernel<{4 if (out_h >= 12 and nt == 4) else 2}, {nt}, {'true' if res_f32 else 'false'}, {mv}>"
 
 
 def wgrad_kernel_name(out_c: int, ks: int, ci4: bool = False) -> str:
@@ -124,19 +126,26 @@ class ConvPlan:
             n: int, up: int = 1, act: int = ACT_NONE, slope: float = 0.2, use_bias: bool = True,
             res1: Optional[torch.Tensor] = None, alpha1: float = 1.0, res1_cs: int = 0, res1_co: int = 0,
             res2: Optional[torch.Tensor] = None, alpha2: float = 1.0, res2_cs: int = 0, res2_co: int = 0,
-            out_mode: int = OUT_BF16) -> None:
+            out_mode: int = OUT_BF16, beta1: float = 1.0, beta2: float = 1.0, aux: Optional[torch.Tensor] = None,
+            aux_cs: int = 0, aux_co: int = 0, aux_scale: float = 1.0) -> None:
+        """y = epilogue(conv(x)); residuals res1/res2 may be bf16 or fp32 tensors (dtype decides), aux = optional
+        second bf16 output aux_scale * y."""
         oh, ow = self.out_hw(in_h, in_w, up)
         d = ConvDesc(n, in_h, in_w, self.cin, x_cs, x_co, up, self.ks, self.stride, self.pad, oh, ow, self.cout, y_cs, y_co,
                      self.cc)
-        ep = Epilogue(act, slope, alpha1, ptr(res1), res1_cs, res1_co, alpha2, ptr(res2), res2_cs, res2_co, out_mode, 0)
+        rf = (1 if res1 is not None and res1.dtype == torch.float32 else 0) | \
+             (2 if res2 is not None and res2.dtype == torch.float32 else 0)
+        ep = Epilogue(act, slope, alpha1, ptr(res1), res1_cs, res1_co, alpha2, ptr(res2), res2_cs, res2_co, out_mode, 0,
+                      rf, beta1, beta2, aux_cs, ptr(aux), aux_co, aux_scale)
         b = ptr(self.bias) if (use_bias and self.bias is not None) else None
         flops = 2 * self.cin_real * self.cout * self.ks * self.ks * n * oh * ow
-        _run(fwd_kernel_name(self.cout, oh), flops, lambda: check(
+        _run(fwd_kernel_name(self.cout, oh, rf != 0), flops, lambda: check(
             _lib.load().climsr_conv2d_fwd(ctypes.byref(d), ptr(x), ptr(self.wpk), b, ctypes.byref(ep), ptr(y), _lib.stream_ptr()),
             f"conv fwd {self.name}"), "fwd " + self.name)
 
     def dgrad(self, dz: torch.Tensor, dz_cs: int, out_h: int, out_w: int, g: torch.Tensor, g_cs: int, g_co: int, n: int,
-              accumulate: bool = False, down2: bool = False, cout_t: Optional[int] = None) -> None:
+              accumulate: bool = False, down2: bool = False, cout_t: Optional[int] = None, aux: Optional[torch.Tensor] = None,
+              aux_cs: int = 0, aux_co: int = 0, aux_scale: float = 1.0) -> None:
         """Data gradient: g[:, :, :, g_co:g_co+cin_real] (+)= conv^T(dz) (fp32); (out_h, out_w) are dz's dims.  With
         down2 the result is summed over 2x2 pixel blocks (backward of the nearest x2 upsample feeding this conv).
         Stride-2 convs (pad 1, even input) run as a stride-1 conv over the zero-inserted dz."""
@@ -149,7 +158,8 @@ class ConvPlan:
             d = ConvDesc(n, out_h, out_w, self.cin_t, dz_cs, 0, -2, self.ks, 1, pad_t, 2 * out_h, 2 * out_w, ct, g_cs, g_co,
                          self.cc_t)
             out_h, out_w = 2 * out_h, 2 * out_w
-        ep = Epilogue(0, 0.0, 1.0, None, 0, 0, 1.0, None, 0, 0, OUT_F32_ADD if accumulate else OUT_F32, 1 if down2 else 0)
+        ep = Epilogue(0, 0.0, 1.0, None, 0, 0, 1.0, None, 0, 0, OUT_F32_ADD if accumulate else OUT_F32, 1 if down2 else 0,
+                      0, 1.0, 1.0, aux_cs, ptr(aux), aux_co, aux_scale)
         flops = 2 * self.cout * ct * self.ks * self.ks * n * out_h * out_w
         _run(fwd_kernel_name(ct, out_h), flops, lambda: check(
             _lib.load().climsr_conv2d_fwd(ctypes.byref(d), ptr(dz), ptr(self.wpk_t), None, ctypes.byref(ep), ptr(g),
@@ -249,6 +259,42 @@ class BatchedPacker:
     def run(self):
         check(_lib.load().climsr_pack_conv_weights_batched(ptr(self.table), self.n, self.max_elems, _lib.stream_ptr()),
               "pack batched")
+
+
+class PullPlan(ConvPlan):
+    """Data gradient of one channel group of a residual dense block's concatenation, as ONE conv over the
+    side-by-side output gradients of every conv that reads the group (climsr_hip.h, ClimsrPullPackDesc).
+    ``segs`` = [(weight OIHW fp32, out_c, in_c_real)] of the consuming convs in dZ-channel order."""
+
+    def __init__(self, segs, out_c: int, ci_off: int, ks: int = 3, name: str = ""):
+        in_c = sum(oc for _w, oc, _ic in segs)
+        super().__init__(in_c, out_c, ks, 1, None, name)
+        self.segs, self.ci_off = segs, ci_off
+        self.wpk = torch.empty((self.rows, self.kpk), dtype=torch.bfloat16, device=segs[0][0].device)
+
+    def pull_desc(self) -> PullPackDesc:
+        d = PullPackDesc()
+        d.out = ptr(self.wpk)
+        for k, (w, oc, ic) in enumerate(self.segs):
+            assert w.dtype == torch.float32 and w.is_contiguous() and tuple(w.shape) == (oc, ic, self.ks, self.ks)
+            d.seg_w[k], d.seg_oc[k], d.seg_ic[k] = ptr(w), oc, ic
+        d.nseg, d.out_c, d.in_c, d.ks, d.cc, d.ci_off = len(self.segs), self.cout, self.cin, self.ks, self.cc, self.ci_off
+        return d
+
+
+class PullPacker:
+    """Every pull weight of a network packed by ONE launch (descriptor table resident on the device)."""
+
+    def __init__(self, pulls, device):
+        descs = [p.pull_desc() for p in pulls]
+        arr = (PullPackDesc * len(descs))(*descs)
+        self.table = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(device)
+        self.n = len(descs)
+        self.max_elems = max(p.rows * p.kpk for p in pulls)
+
+    def run(self):
+        check(_lib.load().climsr_pack_pull_weights_batched(ptr(self.table), self.n, self.max_elems, _lib.stream_ptr()),
+              "pack pull batched")
 
 
 # ------------------------------------------------------------------ discriminator / VGG / GAN-loss ops

@@ -49,18 +49,27 @@ typedef struct ClimsrConvDesc {
   int32_t cc;                  /* channel chunk of the packed weight layout (climsr_conv_chunk) */
 } ClimsrConvDesc;
 
-/* Fused epilogue: v = acc + bias; v = act(v); v = v*alpha1 + res1; v = v*alpha2 + res2; store. */
+/* Fused epilogue: v = acc + bias; v = act(v); v = v*alpha1 + beta1*res1; v = v*alpha2 + beta2*res2; store v
+ * (and, if aux != NULL, also aux = bf16(aux_scale * v)).
+ * act 3 / 4 are activation BACKWARDS: v *= act'(res1) for a leaky relu / relu whose OUTPUT is res1 (the
+ * derivative is read from its sign); res1 is then a mask source, not a residual. */
 typedef struct ClimsrEpilogue {
-  int32_t act;                  /* 0 none, 1 leaky relu(slope), 2 relu */
+  int32_t act;                  /* 0 none, 1 leaky relu(slope), 2 relu, 3 leaky relu backward, 4 relu backward */
   float slope;
   float alpha1;                 /* used when res1 != NULL */
-  const void* res1;             /* bf16 NHWC, same pixels as the output */
+  const void* res1;             /* bf16 (or fp32, res_f32 bit 0) NHWC, same pixels as the output */
   int32_t res1_cstride, res1_coff;
   float alpha2;
-  const void* res2;
+  const void* res2;             /* bf16 (or fp32, res_f32 bit 1) */
   int32_t res2_cstride, res2_coff;
   int32_t out_mode;             /* 0 bf16 store, 1 f32 store, 2 f32 accumulate (+=) */
   int32_t down2;                /* 1: sum 2x2 output pixels into out[y/2][x/2] (dgrad of a nearest x2 upsample) */
+  int32_t res_f32;              /* bit 0: res1 is fp32, bit 1: res2 is fp32 */
+  float beta1, beta2;           /* residual scales (1 for a plain residual add) */
+  int32_t aux_cstride;
+  void* aux;                    /* optional second output, bf16 NHWC, same pixels */
+  int32_t aux_coff;
+  float aux_scale;
 } ClimsrEpilogue;
 
 const char* climsr_last_error(void);
@@ -89,6 +98,21 @@ typedef struct ClimsrPackDesc {
 /* Pack many convs in one launch; `descs` is a DEVICE array of ndesc descriptors, max_elems the
  * largest packed size (rows*packed_k) among them.  Used after every optimiser step. */
 int climsr_pack_conv_weights_batched(const ClimsrPackDesc* descs, int ndesc, int64_t max_elems, void* stream);
+
+/* "Pull" data-gradient weights of a residual dense block (esrgan.py:17-38).  The gradient of one
+ * channel group of the dense concatenation (x, x1..x4) collects the transposed convs of EVERY later conv
+ * that reads it; with the output gradients of those convs stored side by side (dZ1|dZ2|dZ3|dZ4|dZ5) the
+ * sum is ONE conv over a contiguous channel suffix.  This packs its weights in the climsr_conv2d_fwd
+ * layout: out row co (group channel ci_off+co), input channel c of segment s (the conv seg_w[s], seg_oc[s]
+ * outputs, seg_ic[s] inputs): W_s[c - start_s][ci_off + co][ks-1-ky][ks-1-kx]. */
+typedef struct ClimsrPullPackDesc {
+  uint16_t* out;
+  const float* seg_w[5];
+  int32_t seg_oc[5];
+  int32_t seg_ic[5];
+  int32_t nseg, out_c, in_c, ks, cc, ci_off;
+} ClimsrPullPackDesc;
+int climsr_pack_pull_weights_batched(const ClimsrPullPackDesc* descs, int ndesc, int64_t max_elems, void* stream);
 
 /* Implicit-GEMM convolution on MFMA (bf16 in, fp32 accumulate), fused epilogue.
  * Forward of nn.Conv2d (esrgan.py:22-26,72-83; srcnn.py:9-11; rfb_esrgan.py:28-52) and, with

@@ -19,13 +19,23 @@ n = args.batch
 
 
 def timeit(fn, reps):
+    """Average GPU time per launch: `reps` launches captured in one hipGraph and replayed (no host overhead)."""
     for _ in range(3):
         fn()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(gr, stream=side):
+            for _ in range(reps):
+                fn()
+    torch.cuda.synchronize()
+    gr.replay()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
-    for _ in range(reps):
-        fn()
+    gr.replay()
     e.record()
     torch.cuda.synchronize()
     return s.elapsed_time(e) / reps * 1e3  # us
@@ -66,3 +76,19 @@ for (cin, cout, ks, h, up) in [(64, 16, 3, 64, 1), (112, 16, 3, 64, 1), (128, 64
     rows.append((f"wgrad {p.name} @{h}", t, flops))
 for name, t, f in rows:
     print(f"{name:32s} {t:9.1f} us  {f / t / 1e6:8.1f} TFLOP/s")
+
+# RDB-shaped launches as the generator issues them: 128-channel dense buffer, channel slices
+print("-- RDB (dense 128-ch buffer, slices) --")
+dc = 128
+dense = torch.randn(n, 64, 64, dc, device=dev).to(torch.bfloat16)
+for k in range(1, 6):
+    cin = 64 + 16 * (k - 1)
+    cout = 16 if k < 5 else 64
+    p = plan(cin, cout, 3)
+    if k < 5:
+        t = timeit(lambda: p.fwd(dense, dc, 0, 64, 64, dense, dc, cin, n, act=ACT_LRELU), args.reps)
+    else:
+        out = torch.empty(n, 64, 64, dc, device=dev, dtype=torch.bfloat16)
+        t = timeit(lambda: p.fwd(dense, dc, 0, 64, 64, out, dc, 0, n, res1=dense, res1_cs=dc, alpha1=0.2), args.reps)
+    f = 2 * cin * cout * 9 * n * 64 * 64
+    print(f"fwd conv{k} {cin}->{cout}".ljust(32), f"{t:9.1f} us  {f / t / 1e6:8.1f} TFLOP/s")

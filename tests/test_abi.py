@@ -50,8 +50,13 @@ def test_struct_layouts_match_header(lib):
     from climsr_amd import _lib
 
     assert ctypes.sizeof(_lib.ConvDesc) == 16 * 4
-    # ClimsrEpilogue: int, float, float, ptr, int, int, float, ptr, int, int, int, int (natural alignment)
-    assert ctypes.sizeof(_lib.Epilogue) == 64
+    # ClimsrEpilogue: int, float, float, ptr, int, int, float, ptr, int, int, int, int, int, float, float, int, ptr,
+    # int, float (natural alignment)
+    assert ctypes.sizeof(_lib.Epilogue) == 96
+    assert _lib.Epilogue.aux.offset == 80 and _lib.Epilogue.aux_scale.offset == 92
+    assert _lib.Epilogue().beta1 == 1.0 and _lib.Epilogue().beta2 == 1.0
+    # ClimsrPullPackDesc: ptr, ptr[5], int[5], int[5], 6 ints
+    assert ctypes.sizeof(_lib.PullPackDesc) == 8 + 40 + 20 + 20 + 24
     assert ctypes.sizeof(_lib.PackDesc) == 2 * 8 + 8 * 4
 
 
@@ -76,6 +81,11 @@ def test_argument_validation_does_not_touch_the_gpu(lib):
     assert lib.climsr_conv2d_fwd(ctypes.byref(d), 1, 1, None, ctypes.byref(ep), 1, None) == -1
     assert b"unsupported geometry" in lib.climsr_last_error()
     assert lib.climsr_conv2d_fwd(None, None, None, None, None, None, None) == -1
+    d = _lib.ConvDesc(2, 16, 16, 8, 8, 0, 1, 3, 1, 1, 16, 16, 16, 16, 0, 8)
+    ep = _lib.Epilogue(act=3)  # activation backward needs res1 (the activation output) as its mask source
+    assert lib.climsr_conv2d_fwd(ctypes.byref(d), 1, 1, None, ctypes.byref(ep), 1, None) == -1
+    assert b"act 3" in lib.climsr_last_error()
+    assert lib.climsr_pack_pull_weights_batched(None, 0, 0, None) == -1
     assert lib.climsr_adamw_step(0, None, None, None, None, None, None) == -1
     assert lib.climsr_l1_loss(None, None, 0, None, None, None) == -1
 

@@ -205,3 +205,60 @@ def test_conv_dgrad_single_output_channel(cin, cout, ks, h, w):
     y = F.conv2d(x, bf(wt).double(), None, padding=ks // 2)
     (gref,) = torch.autograd.grad(y, x, dz.double())
     check_close(gx[..., :1].permute(0, 3, 1, 2).cpu(), gref[:, :1], tol=2e-5, what="dgrad co1")
+
+
+def test_rdb_pull_backward_matches_torch():
+    """Pull-form RDB data gradient (esrgan.py:17-38): each group's gradient as ONE conv over the
+    side-by-side conv output gradients dZ = [dZ1|dZ2|dZ3|dZ4|dZ5], with the LeakyReLU backward read
+    from the stored activations (epilogue act 3), fp32 residuals with a scale, and the aux output.
+    Each step is checked against fp64 torch fed with the bf16 operands the kernel actually read."""
+    from climsr_amd.ops import ACT_LRELU_BWD, PullPacker, PullPlan
+
+    nf, gc, n, h, w = 64, 16, 2, 16, 20
+    dc = nf + 4 * gc
+    gen = torch.Generator().manual_seed(5)
+    ws = [((torch.rand((gc if k < 5 else nf, nf + (k - 1) * gc, 3, 3), generator=gen) * 2 - 1) / ((nf + (k - 1) * gc) * 9) ** 0.5)
+          for k in range(1, 6)]
+    wd = [t.to(DEV).contiguous() for t in ws]
+    pulls = []
+    for j in range(5):
+        segs = [(wd[k - 1], gc if k < 5 else nf, nf + (k - 1) * gc) for k in range(j + 1, 6)]
+        pulls.append(PullPlan(segs, nf if j == 0 else gc, 0 if j == 0 else nf + (j - 1) * gc, 3, f"pull{j}"))
+    PullPacker(pulls, torch.device(DEV)).run()
+    dense = bf(torch.rand((n, dc, h, w), generator=gen) * 2 - 1)  # x, x1..x4 (signs drive the lrelu mask)
+    dense_d = to_nhwc(dense)
+    dz = torch.zeros((n, h, w, dc), dtype=torch.bfloat16, device=DEV)
+    dz[..., 4 * gc:] = (torch.rand((n, h, w, nf), generator=gen) * 2 - 1).to(torch.bfloat16).to(DEV)  # dZ5
+    g_out = (torch.rand((n, h, w, nf), generator=gen) * 2 - 1).to(DEV)
+    g_skip = (torch.rand((n, h, w, nf), generator=gen) * 2 - 1).to(DEV)
+    for j in (4, 3, 2, 1):
+        pulls[j].fwd(dz, dc, j * gc, h, w, dz, dc, (j - 1) * gc, n, act=ACT_LRELU_BWD, use_bias=False, res1=dense_d, res1_cs=dc,
+                     res1_co=nf + (j - 1) * gc)
+    g_in = torch.empty((n, h, w, nf), dtype=torch.float32, device=DEV)
+    aux = torch.zeros((n, h, w, dc), dtype=torch.bfloat16, device=DEV)
+    pulls[0].fwd(dz, dc, 0, h, w, g_in, nf, 0, n, use_bias=False, out_mode=OUT_F32, res1=g_out, res1_cs=nf, res1_co=0, beta1=0.2,
+                 res2=g_skip, res2_cs=nf, res2_co=0, aux=aux, aux_cs=dc, aux_co=4 * gc, aux_scale=0.04)
+    torch.cuda.synchronize()
+    dzc = from_nhwc(dz, dc).double().cpu()  # channels: dZ1..dZ4 (gc each), dZ5 (nf)
+
+    def dz_of(k):
+        return dzc[:, (k - 1) * gc:k * gc] if k < 5 else dzc[:, 4 * gc:]
+
+    def pull_ref(j):
+        lo = 0 if j == 0 else nf + (j - 1) * gc
+        width = nf if j == 0 else gc
+        tot = 0
+        for k in range(j + 1, 6):
+            wk = bf(ws[k - 1]).double()
+            tot = tot + torch.nn.grad.conv2d_input((n, wk.shape[1], h, w), wk, dz_of(k), padding=1)[:, lo:lo + width]
+        return tot
+
+    for j in (4, 3, 2, 1):
+        xj = dense[:, nf + (j - 1) * gc:nf + j * gc].double()
+        want = pull_ref(j) * torch.where(xj > 0, 1.0, 0.2)
+        got = dz_of(j)
+        scale = want.abs().max().item()
+        assert (got - want).abs().max().item() <= 8e-3 * scale, f"dZ{j}"  # bf16 store: <= 1 ulp (2^-8) of the value
+    want = pull_ref(0) + 0.2 * from_nhwc(g_out, nf).double().cpu() + from_nhwc(g_skip, nf).double().cpu()
+    check_close(from_nhwc(g_in, nf).cpu(), want, 1e-5, "G_in")
+    check_close(from_nhwc(aux, nf, 4 * gc).cpu(), 0.04 * want, 8e-3, "aux")
