@@ -46,6 +46,11 @@ class PackDesc(ctypes.Structure):
         "out_c", "in_c", "in_c_real", "out_c_real", "ks", "cc", "tflip", "reserved")]
 
 
+class ReduceDesc(ctypes.Structure):
+    _fields_ = [("wgrad", c_void_p), ("bias_grad", c_void_p), ("row0", ctypes.c_int32), ("out_c", ctypes.c_int32),
+                ("in_c_real", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
 class PullPackDesc(ctypes.Structure):
     _fields_ = [("out", c_void_p), ("seg_w", c_void_p * 5), ("seg_oc", ctypes.c_int32 * 5), ("seg_ic", ctypes.c_int32 * 5)] + [
         (n, ctypes.c_int32) for n in ("nseg", "out_c", "in_c", "ks", "cc", "ci_off")]
@@ -67,6 +72,8 @@ SIGNATURES = {
     "climsr_conv2d_wgrad_reduce": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                                            c_void_p]),
     "climsr_conv2d_wgrad_splits": (c_int, [P(ConvDesc)]),
+    "climsr_conv2d_wgrad_reduce_rows": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int64, c_int,
+                                                c_void_p]),
     "climsr_conv2d_wgrad_workspace": (c_size_t, [P(ConvDesc), c_int]),
     "climsr_act_grad": (c_int, [c_int64, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_float, c_float,
                                 c_void_p, c_int, c_void_p]),

@@ -85,7 +85,12 @@ using namespace climsr;
 extern "C" const char* climsr_last_error(void) { return g_err; }
 extern "C" int climsr_version(void) { return 2; }
 
+// Convs with <= 16 outputs, 3x3 and <= 128 inputs (the residual dense block's conv1-4 and their pull data
+// gradients) run on conv_n16_kernel, whose packed K is tap-major with the channels padded to 32 per tap.
+static bool n16_shape(int in_c, int ks, int out_c) { return out_c <= 16 && ks == 3 && in_c <= 128; }
+
 extern "C" int climsr_conv_chunk(int in_c, int ks, int out_c) {
+  if (n16_shape(in_c, ks, out_c)) return in_c <= 32 ? 32 : (in_c <= 64 ? 64 : 128);
   int cc = round_up(in_c, 8);
   FwdGeom g;
   while (cc > 8) {
@@ -566,6 +571,222 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
+// Dense-block conv with <= 16 output channels (RDB conv1-4, esrgan.py:22-25, and their pull data
+// gradients): 3x3, stride 1, pad 1, <= 128 input channels.  One 16-row MFMA tile of outputs leaves the
+// generic kernel staging- and latency-bound; this one is built for memory-level parallelism:
+//  * workgroups are persistent (grid-stride over 8x16-pixel output tiles, 3 per CU) and the NEXT tile's
+//    input is loaded into registers while the current one is computed (one pixel per staging thread,
+//    compile-time channel offsets: no per-vector index math);
+//  * the 4 waves split the K dimension (32-channel blocks; NCB = blocks) x the tile rows (4/NCB groups),
+//    so a wave keeps only its 9 weight fragments in VGPRs (loaded once per workgroup);
+//  * a B fragment (16 pixels x 32 channels of one input row) is read from LDS once and feeds the three
+//    output rows that use it (ky = 0..2);
+//  * the per-channel-block partial sums meet in LDS; each wave finishes 2 output rows (fused epilogue).
+// Channels are padded to NCB*32 (zero weights, zero LDS pixels).
+// ------------------------------------------------------------------------------------------
+constexpr int N16_TH = 8;
+constexpr int N16_TPH = N16_TH + 2, N16_TPW = TW + 2;
+
+static int n16_ncb(int in_c) { return in_c <= 32 ? 1 : (in_c <= 64 ? 2 : 4); }
+
+template <int NCB>
+__global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* xs = (uint16_t*)smem;
+  float* part = (float*)smem;  // partial sums [cb][row][lane] (aliases the input tile after compute)
+  constexpr int CINP = NCB * 32, P = CINP + 8, CV = CINP / 8;
+  constexpr int RG = 4 / NCB, MW = N16_TH / RG;  // row groups, output rows per wave
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
+  const int cb = wave % NCB, rg = wave / NCB;
+  const int cvec = a.in_c / 8;
+
+  // this wave's A fragments (channel block cb, 9 taps), staged through LDS once per workgroup
+  constexpr int WROW = 9 * CINP + 8;
+  for (int v = tid; v < 16 * 9 * CV; v += 256) {
+    const int r = v / (9 * CV), k = v - r * (9 * CV);
+    *(uint4*)(xs + r * WROW + k * 8) = *(const uint4*)(a.w + (long)r * a.kpk + k * 8);
+  }
+  __syncthreads();
+  bf16x8 af[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) af[t] = *(const bf16x8*)(xs + col * WROW + t * CINP + cb * 32 + g * 8);
+
+  float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int co = g * 4;
+  if (a.bias) {
+    bv.x = co < a.out_c ? a.bias[co] : 0.f;
+    bv.y = co + 1 < a.out_c ? a.bias[co + 1] : 0.f;
+    bv.z = co + 2 < a.out_c ? a.bias[co + 2] : 0.f;
+    bv.w = co + 3 < a.out_c ? a.bias[co + 3] : 0.f;
+  }
+  const int ntiles = a.tiles_x * a.tiles_y * a.n;
+  const bool valign = ((a.out_cs | a.out_co) & 3) == 0 && (!a.res1 || ((a.r1_cs | a.r1_co) & 3) == 0) &&
+                      (!a.res2 || ((a.r2_cs | a.r2_co) & 3) == 0) && co + 3 < a.out_c;
+
+  // staging: vector v = tid + 256 i of the tile is (pixel v / CV, channel group v % CV); CV is a power of
+  // two, so consecutive lanes read consecutive 16 B of a pixel (coalesced) and the pad groups (>= cvec)
+  // are stored as zeros without a load
+  constexpr int NPIX = N16_TPH * N16_TPW, NV = (NPIX * CV + 255) / 256;
+  uint4 pre[NV];
+  auto issue = [&](int tile) {
+    int tt = tile;
+    const int tx = tt % a.tiles_x;
+    tt /= a.tiles_x;
+    const int ty = tt % a.tiles_y;
+    const int nimg = tt / a.tiles_y;
+    const int iy0 = ty * N16_TH - 1, ix0 = tx * TW - 1;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = tid + 256 * i;
+      const int pix = v / CV, j = v % CV;
+      const int py = pix / N16_TPW, px = pix - py * N16_TPW;
+      const int iy = iy0 + py, ix = ix0 + px;
+      pre[i] = make_uint4(0, 0, 0, 0);
+      if (v < NPIX * CV && j < cvec && !(a.ablate & 1) && iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w)
+        pre[i] = *(const uint4*)(a.x + (((long)nimg * a.in_h + iy) * a.in_w + ix) * a.in_cs + a.in_co + j * 8);
+    }
+  };
+  if (blockIdx.x < ntiles) issue(blockIdx.x);
+
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    int tt = tile;
+    const int tx = tt % a.tiles_x;
+    tt /= a.tiles_x;
+    const int ty = tt % a.tiles_y;
+    const int nimg = tt / a.tiles_y;
+    const int oy0 = ty * N16_TH, ox0 = tx * TW;
+    __syncthreads();  // the previous tile's LDS reads (partials) are done
+    if (!(a.ablate & 8)) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int v = tid + 256 * i;
+        if (v < NPIX * CV) *(uint4*)(xs + (v / CV) * P + (v % CV) * 8) = pre[i];
+      }
+    }
+    if (tile + (int)gridDim.x < ntiles) issue(tile + gridDim.x);  // lands while this tile computes
+    __syncthreads();
+    f32x4 acc[MW];
+#pragma unroll
+    for (int m = 0; m < MW; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (!(a.ablate & 2)) {
+      const uint16_t* xb = xs + ((rg * MW) * N16_TPW + col) * P + cb * 32 + g * 8;
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+        for (int ir = 0; ir < MW + 2; ++ir) {
+          const bf16x8 b = *(const bf16x8*)(xb + (ir * N16_TPW + kx) * P);
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky) {
+            const int m = ir - ky;
+            if (m >= 0 && m < MW) acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ky * 3 + kx], b, acc[m], 0, 0, 0);
+          }
+        }
+    }
+    __syncthreads();  // input tile reads done: the partials overwrite it
+#pragma unroll
+    for (int m = 0; m < MW; ++m) *(f32x4*)(part + ((cb * N16_TH + rg * MW + m) * 64 + lane) * 4) = acc[m];
+    __syncthreads();
+    if (a.ablate & 4) continue;
+    // epilogue: wave w finishes output rows 2w, 2w+1; lane owns channels co..co+3 of column ox0 + col
+    const int ox = ox0 + col;
+    f32x4 sum[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      sum[h] = *(const f32x4*)(part + ((0 * N16_TH + wave * 2 + h) * 64 + lane) * 4);
+#pragma unroll
+      for (int c = 1; c < NCB; ++c) sum[h] += *(const f32x4*)(part + ((c * N16_TH + wave * 2 + h) * 64 + lane) * 4);
+    }
+    uint2 r1v[2], r2v[2];
+    float4 old[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int oy = oy0 + wave * 2 + h;
+      const long pidx = ((long)nimg * a.out_h + oy) * a.out_w + ox;
+      r1v[h] = r2v[h] = make_uint2(0, 0);
+      old[h] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (oy < a.out_h && ox < a.out_w && valign) {
+        if (a.res1) r1v[h] = *(const uint2*)((const uint16_t*)a.res1 + pidx * a.r1_cs + a.r1_co + co);
+        if (a.res2) r2v[h] = *(const uint2*)((const uint16_t*)a.res2 + pidx * a.r2_cs + a.r2_co + co);
+        if (a.out_mode == 2) old[h] = *(const float4*)((const float*)a.y + pidx * a.out_cs + a.out_co + co);
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int oy = oy0 + wave * 2 + h;
+      if (oy >= a.out_h || ox >= a.out_w || co >= a.out_c) continue;
+      const long pidx = ((long)nimg * a.out_h + oy) * a.out_w + ox;
+      const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
+      float v[4];
+      const long ob = pidx * a.out_cs + a.out_co + co;
+      if (valign) {
+        const uint4 r1 = make_uint4(r1v[h].x, r1v[h].y, 0, 0), r2 = make_uint4(r2v[h].x, r2v[h].y, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          v[i] = ep_res(act_apply(sum[h][i] + bb[i], a.act, a.slope), a.act, a.slope, a.res1 != nullptr, res4_at(r1, false, i),
+                        a.alpha1, a.beta1, a.res2 != nullptr, res4_at(r2, false, i), a.alpha2, a.beta2);
+        if (a.out_mode == 0) {
+          uint2 pk;
+          pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+          pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+          *(uint2*)((uint16_t*)a.y + ob) = pk;
+        } else {
+          *(float4*)((float*)a.y + ob) = make_float4(old[h].x + v[0], old[h].y + v[1], old[h].z + v[2], old[h].w + v[3]);
+        }
+        if (a.aux) {
+          uint2 pk;
+          pk.x = (uint32_t)f2bf(a.aux_scale * v[0]) | ((uint32_t)f2bf(a.aux_scale * v[1]) << 16);
+          pk.y = (uint32_t)f2bf(a.aux_scale * v[2]) | ((uint32_t)f2bf(a.aux_scale * v[3]) << 16);
+          *(uint2*)(a.aux + pidx * a.aux_cs + a.aux_co + co) = pk;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (co + i >= a.out_c) continue;
+          const float r1 = a.res1 ? res_at(a.res1, false, pidx * a.r1_cs + a.r1_co + co + i) : 0.f;
+          const float r2 = a.res2 ? res_at(a.res2, false, pidx * a.r2_cs + a.r2_co + co + i) : 0.f;
+          const float x = ep_res(act_apply(sum[h][i] + bb[i], a.act, a.slope), a.act, a.slope, a.res1 != nullptr, r1, a.alpha1,
+                                 a.beta1, a.res2 != nullptr, r2, a.alpha2, a.beta2);
+          if (a.out_mode == 0) ((uint16_t*)a.y)[ob + i] = f2bf(x);
+          else if (a.out_mode == 2) ((float*)a.y)[ob + i] += x;
+          else ((float*)a.y)[ob + i] = x;
+          if (a.aux) a.aux[pidx * a.aux_cs + a.aux_co + co + i] = f2bf(a.aux_scale * x);
+        }
+      }
+    }
+  }
+}
+
+template <int NCB>
+static int launch_n16(const FwdArgs& a, hipStream_t s) {
+  auto k = conv_n16_kernel<NCB>;
+  size_t lds = (size_t)N16_TPH * N16_TPW * (NCB * 32 + 8) * 2;
+  const size_t lds_w = (size_t)16 * (9 * NCB * 32 + 8) * 2;        // weight staging (aliased)
+  const size_t lds_p = (size_t)NCB * N16_TH * 64 * 16;             // partial sums (aliased)
+  if (lds_w > lds) lds = lds_w;
+  if (lds_p > lds) lds = lds_p;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (ncu <= 0) ncu = 256;
+  }
+  static int per_cu = 0;
+  if (!per_cu) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, 256, lds) != hipSuccess || per_cu <= 0) per_cu = 2;
+  }
+  int ntiles = a.tiles_x * a.tiles_y * a.n;
+  int grid = ntiles < per_cu * ncu ? ntiles : per_cu * ncu;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, s, a);
+  return check_launch("conv2d_fwd (n16)");
+}
+
+// ------------------------------------------------------------------------------------------
 // Single-output-channel conv on VALU (v_dot2_f32_bf16): conv_last (64->1), srcnn.conv3 (32->1) and
 // the data gradient of srcnn.conv1 w.r.t. its first input channel (64->1, 9x9).  With Cout = 1 an
 // MFMA tile would waste 15 of 16 rows; here each thread owns one output pixel of a 16x16 tile, the
@@ -734,6 +955,16 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
     size_t lds = (size_t)(15 + d->ks) * (15 + d->ks) * (CO1_CC + 8) * 2 + (size_t)d->ks * d->ks * CO1_CC * 2;
     hipLaunchKernelGGL(conv_co1_kernel, dim3(a.tiles_x * a.tiles_y * a.n), dim3(256), lds, s, a);
     return check_launch("conv2d_fwd (co1)");
+  }
+  if (n16_shape(d->in_c, d->ks, d->out_c) && d->cc == 32 * n16_ncb(d->in_c) && d->stride == 1 && d->up == 1 && d->pad == 1 &&
+      !ep->down2 && !ep->res_f32 && d->out_h == d->in_h && d->out_w == d->in_w) {
+    a.tiles_x = ceil_div(d->out_w, TW);
+    a.tiles_y = ceil_div(d->out_h, N16_TH);
+    switch (d->cc / 32) {
+      case 1: return launch_n16<1>(a, s);
+      case 2: return launch_n16<2>(a, s);
+      default: return launch_n16<4>(a, s);
+    }
   }
   if (mw == 4) return launch_fwd<4, 4>(a, ncob, g.lds_total, s);
   switch (g.nt) {
@@ -981,6 +1212,138 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs a) {
   }
 }
 
+// Weight gradient for 3x3 stride-1 convs with 64k output and 64k input channels (the RDB conv5 / the
+// whole-RDB combined GEMM, trunk / upconv / HRconv): workgroup block = 64 co x 64 ci x 9 taps, wave w owns
+// ci 16w..16w+15 (4 co fragments x 9 taps = 36 accumulators), so the workgroup's 4 waves never reduce with
+// each other; the 8x16-pixel tiles of its split are walked with the NEXT tile's dz / x prefetched into
+// registers while the current one is on the MFMA pipe.  Partials: [split][co_rows][in_c*9] (as above).
+constexpr int W64_TH = 8;
+constexpr int W64_TPH = W64_TH + 2, W64_TPW = TW + 2;
+constexpr int W64_P = 64 + 8;  // LDS pixel pitch (channels) of both tiles
+constexpr int W64_NZ = W64_TH * TW * 8;              // 16 B vectors of a dz tile (128 px x 64 ch)
+constexpr int W64_NX = W64_TPH * W64_TPW * 8;         // of an x tile (180 px x 64 ch)
+constexpr int W64_VZ = W64_NZ / 256, W64_VX = (W64_NX + 255) / 256;
+
+__global__ __launch_bounds__(256, 1) void conv_wgrad64_kernel(WgArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* zs = (uint16_t*)smem;                       // [128 px][W64_P]
+  uint16_t* xs = zs + W64_TH * TW * W64_P;              // [180 px][W64_P]
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4;
+  const int q = (lane & 15) >> 2, p = lane & 3, col = lane & 15;
+  const int cib = blockIdx.x % a.ncib, cob = blockIdx.x / a.ncib;
+  const int split = blockIdx.y;
+  const int ci0 = cib * 64, co0 = cob * 64;
+  const bool do_bias = cib == 0 && a.bpart != nullptr;
+  const int lh = a.in_h * a.up, lw = a.in_w * a.up;
+  const int upsh = a.up == 2 ? 1 : 0;
+
+  f32x4 acc[4][9], accb[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    accb[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 9; ++u) acc[t][u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+  bf16x8 ones;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ones[i] = (__bf16)1.0f;
+  int tapoff[9];
+#pragma unroll
+  for (int u = 0; u < 9; ++u) tapoff[u] = ((u / 3) * W64_TPW + (u % 3)) * W64_P + wave * 16 + 4 * p;
+
+  uint4 pz[W64_VZ], px[W64_VX];
+  auto issue = [&](int tile) {
+    int tt = tile;
+    const int tx = tt % a.tiles_x;
+    tt /= a.tiles_x;
+    const int ty = tt % a.tiles_y;
+    const int nimg = tt / a.tiles_y;
+    const int oy0 = ty * W64_TH, ox0 = tx * TW;
+#pragma unroll
+    for (int i = 0; i < W64_VZ; ++i) {  // dz: pixel v/8, channel group v%8
+      const int v = tid + 256 * i;
+      const int pix = v >> 3, cg = v & 7;
+      const int oy = oy0 + (pix >> 4), ox = ox0 + (pix & 15);
+      pz[i] = make_uint4(0, 0, 0, 0);
+      if (!(a.ablate & 1) && oy < a.out_h && ox < a.out_w)
+        pz[i] = *(const uint4*)(a.dz + (((long)nimg * a.out_h + oy) * a.out_w + ox) * a.dz_cs + co0 + cg * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < W64_VX; ++i) {
+      const int v = tid + 256 * i;
+      const int pix = v >> 3, cg = v & 7;
+      const int py = pix / W64_TPW, pxx = pix - py * W64_TPW;
+      const int iy = oy0 - a.pad + py, ix = ox0 - a.pad + pxx;
+      px[i] = make_uint4(0, 0, 0, 0);
+      if (!(a.ablate & 1) && v < W64_NX && iy >= 0 && iy < lh && ix >= 0 && ix < lw)
+        px[i] = *(const uint4*)(a.x + (((long)nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + ci0 +
+                                cg * 8);
+    }
+  };
+  int tile = split;
+  if (tile < a.ntiles) issue(tile);
+  for (; tile < a.ntiles; tile += a.nsplit) {
+    __syncthreads();  // previous tile's fragment reads done
+#pragma unroll
+    for (int i = 0; i < W64_VZ; ++i) {
+      const int v = tid + 256 * i;
+      *(uint4*)(zs + (v >> 3) * W64_P + (v & 7) * 8) = pz[i];
+    }
+#pragma unroll
+    for (int i = 0; i < W64_VX; ++i) {
+      const int v = tid + 256 * i;
+      if (v < W64_NX) *(uint4*)(xs + (v >> 3) * W64_P + (v & 7) * 8) = px[i];
+    }
+    if (tile + a.nsplit < a.ntiles) issue(tile + a.nsplit);
+    __syncthreads();
+    if (a.ablate & 2) continue;
+#pragma unroll
+    for (int kk = 0; kk < W64_TH * TW / 32; ++kk) {  // k-step: output pixel rows 2kk, 2kk+1
+      const int k0 = kk * 32 + 8 * g + q, k1 = k0 + 4;
+      bf16x8 af[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const s16x4 lo = ds_read_tr16(zs + k0 * W64_P + t * 16 + 4 * p);
+        const s16x4 hi = ds_read_tr16(zs + k1 * W64_P + t * 16 + 4 * p);
+        const short v8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[t] = __builtin_bit_cast(bf16x8, v8);
+      }
+      if (do_bias && wave == 0) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) accb[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], ones, accb[t], 0, 0, 0);
+      }
+      const int xb0 = ((k0 >> 4) * W64_TPW + (k0 & 15)) * W64_P, xb1 = ((k1 >> 4) * W64_TPW + (k1 & 15)) * W64_P;
+#pragma unroll
+      for (int u = 0; u < 9; ++u) {
+        const s16x4 lo = ds_read_tr16(xs + xb0 + tapoff[u]);
+        const s16x4 hi = ds_read_tr16(xs + xb1 + tapoff[u]);
+        const short v8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const bf16x8 b = __builtin_bit_cast(bf16x8, v8);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], b, acc[t][u], 0, 0, 0);
+      }
+    }
+  }
+  // C[row = co][col = ci]: lane holds co = co0 + 16t + 4g + i, ci = ci0 + 16 wave + col
+  float* slab = a.part + (long)split * a.co_rows * a.kw;
+  const int ci = ci0 + wave * 16 + col;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = co0 + t * 16 + g * 4 + i;
+      float* row = slab + (long)co * a.kw + ci * 9;
+#pragma unroll
+      for (int u = 0; u < 9; ++u) row[u] = acc[t][u][i];
+      if (do_bias && wave == 0 && col == 0) a.bpart[(long)split * a.co_rows + co] = accb[t][i];
+    }
+  }
+}
+
+static bool w64_shape(const ClimsrConvDesc* d) {
+  return d->ks == 3 && d->stride == 1 && d->pad == 1 && d->out_c % 64 == 0 && d->in_c % 64 == 0 && d->in_c >= 64;
+}
+
 struct WgPlan {
   int ntc, tb, ntapb, ncib, ncob, co_rows, tiles_x, tiles_y, ntiles, tph, tpw, dzp, kw, ci4;
   size_t lds_x, lds_z, lds_total;
@@ -1020,6 +1383,13 @@ static void wg_plan(const ClimsrConvDesc* d, WgPlan* w) {
 }
 
 extern "C" int climsr_conv2d_wgrad_splits(const ClimsrConvDesc* d) {
+  if (w64_shape(d)) {  // one workgroup per CU: 256 / blocks splits
+    int blocks = (d->out_c / 64) * (d->in_c / 64);
+    int ntiles = d->n * ceil_div(d->out_w, TW) * ceil_div(d->out_h, W64_TH);
+    int ns = ceil_div(256, blocks);
+    if (ns > ntiles) ns = ntiles;
+    return ns < 1 ? 1 : ns;
+  }
   WgPlan w;
   wg_plan(d, &w);
   int base = w.ntapb * w.ncib * w.ncob;
@@ -1030,6 +1400,7 @@ extern "C" int climsr_conv2d_wgrad_splits(const ClimsrConvDesc* d) {
 }
 
 extern "C" size_t climsr_conv2d_wgrad_workspace(const ClimsrConvDesc* d, int nsplit) {
+  if (w64_shape(d)) return (size_t)nsplit * d->out_c * d->in_c * 9 + (size_t)nsplit * d->out_c;
   WgPlan w;
   wg_plan(d, &w);
   return (size_t)nsplit * w.co_rows * w.kw + (size_t)nsplit * w.co_rows;
@@ -1054,6 +1425,26 @@ extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, c
       (d->up != 1 && d->up != 2) || (d->stride != 1 && d->stride != 2)) {
     set_error("conv2d_wgrad: bad args");
     return CLIMSR_EINVAL;
+  }
+  if (w64_shape(d)) {
+    WgArgs a;
+    a.x = x; a.dz = dz; a.part = partial; a.bpart = bias_partial;
+    a.n = d->n; a.in_h = d->in_h; a.in_w = d->in_w; a.in_c = d->in_c; a.in_cs = d->in_cstride; a.in_co = d->in_coff;
+    a.up = d->up; a.ks = 3; a.stride = 1; a.pad = 1; a.out_h = d->out_h; a.out_w = d->out_w;
+    a.out_c = d->out_c; a.dz_cs = dz_cstride;
+    a.tiles_x = ceil_div(d->out_w, TW); a.tiles_y = ceil_div(d->out_h, W64_TH); a.ntiles = d->n * a.tiles_x * a.tiles_y;
+    a.nsplit = nsplit; a.ncib = d->in_c / 64; a.co_rows = d->out_c; a.kw = d->in_c * 9;
+    a.tph = W64_TPH; a.tpw = W64_TPW; a.dzp = W64_P; a.ntapb = 1; a.lds_x = 0;
+    static int ablate = getenv("CLIMSR_ABLATE") ? atoi(getenv("CLIMSR_ABLATE")) : 0;
+    a.ablate = ablate;
+    const size_t lds = (size_t)(W64_TH * TW + W64_TPH * W64_TPW) * W64_P * 2;
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute((const void*)conv_wgrad64_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr_set = true;
+    }
+    hipLaunchKernelGGL(conv_wgrad64_kernel, dim3((d->out_c / 64) * (d->in_c / 64), nsplit), dim3(256), lds, (hipStream_t)stream, a);
+    return check_launch("conv2d_wgrad (64x64 block)");
   }
   WgPlan w;
   wg_plan(d, &w);
@@ -1121,6 +1512,58 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
     if (accumulate) *dst += t;
     else *dst = t;
   }
+}
+
+// Row-sliced reduction of one wgrad partial matrix into several convs' OIHW gradients (the combined
+// residual-dense-block weight gradient: rows [row0, row0 + out_c) of the [co_rows][kw] partial are conv
+// d->wgrad's output channels, the first in_c_real*ks2 columns of each row its inputs x taps).
+__global__ __launch_bounds__(256) void wgrad_reduce_rows_kernel(const float* __restrict__ part, const float* __restrict__ bpart,
+                                                               int nsplit, int co_rows, int kw, int ks2,
+                                                               const ClimsrReduceDesc* __restrict__ descs, int accumulate) {
+  __shared__ float red[8][33];
+  const ClimsrReduceDesc d = descs[blockIdx.y];
+  const int lane = threadIdx.x & 31;
+  const int sg = threadIdx.x >> 5;
+  const long idx = (long)blockIdx.x * 32 + lane;
+  const long nw = (long)d.out_c * d.in_c_real * ks2;
+  const long total = nw + (d.bias_grad ? d.out_c : 0);
+  if ((long)blockIdx.x * 32 >= total) return;
+  const float* src = nullptr;
+  long sstride = 0;
+  if (idx < nw) {
+    const int co = (int)(idx / ((long)d.in_c_real * ks2));
+    const int rem = (int)(idx % ((long)d.in_c_real * ks2));
+    src = part + (long)(d.row0 + co) * kw + rem;
+    sstride = (long)co_rows * kw;
+  } else if (idx < total) {
+    src = bpart + d.row0 + (idx - nw);
+    sstride = co_rows;
+  }
+  float acc = 0.f;
+  if (src)
+    for (int sp = sg; sp < nsplit; sp += 8) acc += src[(long)sp * sstride];
+  red[sg][lane] = acc;
+  __syncthreads();
+  if (sg == 0 && idx < total) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t += red[i][lane];
+    float* dst = (idx < nw) ? (d.wgrad + idx) : (d.bias_grad + (idx - nw));
+    if (accumulate) *dst += t;
+    else *dst = t;
+  }
+}
+
+extern "C" int climsr_conv2d_wgrad_reduce_rows(const float* partial, const float* bias_partial, int nsplit, int co_rows, int kw,
+                                               int ks, const ClimsrReduceDesc* descs, int ndesc, int64_t max_elems,
+                                               int accumulate, void* stream) {
+  if (!partial || !descs || nsplit <= 0 || ndesc <= 0 || ndesc > 65535 || ks <= 0) {
+    set_error("conv2d_wgrad_reduce_rows: bad args");
+    return CLIMSR_EINVAL;
+  }
+  hipLaunchKernelGGL(wgrad_reduce_rows_kernel, dim3(ceil_div(max_elems, 32), ndesc), dim3(256), 0, (hipStream_t)stream, partial,
+                     bias_partial, nsplit, co_rows, kw, ks * ks, descs, accumulate);
+  return check_launch("conv2d_wgrad_reduce_rows");
 }
 
 extern "C" int climsr_conv2d_wgrad_reduce(const float* partial, const float* bias_partial, int nsplit, int out_c, int in_c_real,

@@ -24,8 +24,8 @@ import torch.nn as nn
 from torch import Tensor
 
 from ..core.flat import FlatParamsMixin
-from ..ops import (ACT_LRELU, ACT_LRELU_BWD, ACT_NONE, ACT_RELU, OUT_F32, BatchedPacker, ConvPlan, PullPacker, PullPlan, Workspace,
-                   act_grad, axpby, nchw_to_nhwc)
+from ..ops import (ACT_LRELU, ACT_LRELU_BWD, ACT_NONE, ACT_RELU, OUT_F32, BatchedPacker, ConvPlan, GroupedWgrad, PullPacker, PullPlan,
+                   Workspace, act_grad, axpby, nchw_to_nhwc)
 from .srcnn import SRCNN
 
 
@@ -130,6 +130,12 @@ class _Engine:
                                     f"RRDB_trunk.{blk}.RDB{r + 1}.pull{j}"))
             self.pulls.append(lst)
         self.pull_packer = PullPacker([p for lst in self.pulls for p in lst], dev)
+        # the five weight gradients of an RDB: one GEMM over dZ (all dc channels) x the dense buffer (dc channels)
+        self.rdb_wgrads: List[GroupedWgrad] = []
+        for i in range(3 * self.nb if self.dc % 64 == 0 else 0):
+            blk, r = divmod(i, 3)
+            convs = [self.plans[self.rdb_name(blk, r + 1, k)] for k in range(1, 6)]
+            self.rdb_wgrads.append(GroupedWgrad(convs, self.dc, f"RRDB_trunk.{blk}.RDB{r + 1}"))
         self.version = -1
 
     def bind_grads(self):
@@ -307,9 +313,12 @@ class _Engine:
                          res1=g_out, res1_cs=nf, res1_co=0, beta1=s_o,
                          res2=g_skip if r == 0 else None, res2_cs=nf, res2_co=0,
                          aux=aux, aux_cs=dc, aux_co=4 * gc, aux_scale=0.2 * (0.2 if r == 0 else 1.0))
-            for k in range(1, 6):
-                off = (k - 1) * gc
-                self.plans[self.rdb_name(blk, r + 1, k)].wgrad(src, dc, 0, h, w, dz[..., off:], dc, n, ws, acc)
+            if self.dc % 64 == 0:
+                self.rdb_wgrads[i].run(src, dc, 0, h, w, dz, dc, n, ws, acc)
+            else:
+                for k in range(1, 6):
+                    off = (k - 1) * gc
+                    self.plans[self.rdb_name(blk, r + 1, k)].wgrad(src, dc, 0, h, w, dz[..., off:], dc, n, ws, acc)
         # ---- conv_first: grad wrt fea = trunk path + global skip
         axpby(npx_lr, nf, 1.0, g_fea2, nf, 0, 1.0, G[0], nf, 0)
         act_grad(npx_lr, nf, G[0], nf, 0, None, 0, 0, ACT_NONE, dz64, nf)

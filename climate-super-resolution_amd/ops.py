@@ -13,7 +13,7 @@ from typing import Optional
 import torch
 
 from . import _lib
-from ._lib import ConvDesc, Epilogue, PackDesc, PullPackDesc, check, ptr
+from ._lib import ConvDesc, Epilogue, PackDesc, PullPackDesc, ReduceDesc, check, ptr
 
 ACT_NONE, ACT_LRELU, ACT_RELU = 0, 1, 2
 ACT_LRELU_BWD, ACT_RELU_BWD = 3, 4  # epilogue multiplies by act'(res1), res1 = the activation's output
@@ -34,15 +34,20 @@ def _fwd_nt(out_c: int) -> int:
     return 4 if nt >= 3 else nt
 
 
-def fwd_kernel_name(out_c: int, out_h: int = 16, res_f32: bool = False) -> str:
+def fwd_kernel_name(out_c: int, out_h: int = 16, res_f32: bool = False, cin: int = 0, ks: int = 0, stride: int = 1,
+                    up: int = 1) -> str:
     if out_c == 1:
         return "conv_co1_kernel"
+    if out_c <= 16 and ks == 3 and cin <= 128 and stride == 1 and up == 1 and not res_f32:
+        return f"conv_n16_kernel<{1 if cin <= 32 else 2 if cin <= 64 else 4}>"
     nt = _fwd_nt(out_c)
     mv = {1: 6, 2: 8, 4: 4}[nt]
     return f"conv_fwd_kernel<{4 if (out_h >= 12 and nt == 4) else 2}, {nt}, {'true' if res_f32 else 'false'}, {mv}>"
 
 
-def wgrad_kernel_name(out_c: int, ks: int, ci4: bool = False) -> str:
+def wgrad_kernel_name(out_c: int, ks: int, ci4: bool = False, cin: int = 0, stride: int = 1) -> str:
+    if ks == 3 and stride == 1 and out_c % 64 == 0 and cin % 64 == 0 and cin >= 64:
+        return "conv_wgrad64_kernel"
     rows = round_up(out_c, 16)
     ntc = 4 if rows >= 64 else (2 if rows >= 32 else 1)
     k2 = ks * ks
@@ -139,7 +144,7 @@ class ConvPlan:
                       rf, beta1, beta2, aux_cs, ptr(aux), aux_co, aux_scale)
         b = ptr(self.bias) if (use_bias and self.bias is not None) else None
         flops = 2 * self.cin_real * self.cout * self.ks * self.ks * n * oh * ow
-        _run(fwd_kernel_name(self.cout, oh, rf != 0), flops, lambda: check(
+        _run(fwd_kernel_name(self.cout, oh, rf != 0, self.cin, self.ks, self.stride, up), flops, lambda: check(
             _lib.load().climsr_conv2d_fwd(ctypes.byref(d), ptr(x), ptr(self.wpk), b, ctypes.byref(ep), ptr(y), _lib.stream_ptr()),
             f"conv fwd {self.name}"), "fwd " + self.name)
 
@@ -161,7 +166,7 @@ class ConvPlan:
         ep = Epilogue(0, 0.0, 1.0, None, 0, 0, 1.0, None, 0, 0, OUT_F32_ADD if accumulate else OUT_F32, 1 if down2 else 0,
                       0, 1.0, 1.0, aux_cs, ptr(aux), aux_co, aux_scale)
         flops = 2 * self.cout * ct * self.ks * self.ks * n * out_h * out_w
-        _run(fwd_kernel_name(ct, out_h), flops, lambda: check(
+        _run(fwd_kernel_name(ct, out_h, False, self.cin_t, self.ks, 1, 1 if self.stride == 1 else -2), flops, lambda: check(
             _lib.load().climsr_conv2d_fwd(ctypes.byref(d), ptr(dz), ptr(self.wpk_t), None, ctypes.byref(ep), ptr(g),
                                           _lib.stream_ptr()), f"conv dgrad {self.name}"), "dgrad " + self.name)
 
@@ -190,12 +195,61 @@ class ConvPlan:
         s = _lib.stream_ptr()
         has_b = self.bias is not None and self.gb is not None
         flops = 2 * self.cin_real * self.cout * self.ks * self.ks * n * d.out_h * d.out_w
-        _run(wgrad_kernel_name(self.cout, self.ks, self.cin_w == 4), flops, lambda: check(
+        _run(wgrad_kernel_name(self.cout, self.ks, self.cin_w == 4, self.cin_w, self.stride), flops, lambda: check(
             lib.climsr_conv2d_wgrad(ctypes.byref(d), ptr(x), ptr(dz), dz_cs, ptr(part), ptr(bpart) if has_b else None, ns, s),
             f"conv wgrad {self.name}"), "wgrad " + self.name)
         check(lib.climsr_conv2d_wgrad_reduce(ptr(part), ptr(bpart) if has_b else None, ns, self.cout, self.cin_real, cw,
                                              self.ks, ptr(self.gw), ptr(self.gb) if has_b else None,
                                              1 if accumulate else 0, s), f"wgrad reduce {self.name}")
+
+
+class GroupedWgrad:
+    """Weight/bias gradients of several 3x3 convs that read channel prefixes of ONE input buffer and whose
+    output gradients sit side by side in ONE buffer (the residual dense block: conv_k reads x..x_{k-1},
+    dZ = [dZ1|..|dZ5]): one wgrad GEMM over all output-gradient channels x all input channels, then one
+    row-sliced reduction into every conv's OIHW gradient (upper-triangle blocks are computed and dropped)."""
+
+    def __init__(self, plans, in_c: int, name: str = ""):
+        self.plans, self.in_c, self.name = plans, in_c, name
+        self.out_c = sum(p.cout for p in plans)
+        assert self.out_c % 64 == 0 and in_c % 64 == 0 and all(p.ks == 3 and p.stride == 1 for p in plans)
+        self.row0 = []
+        r = 0
+        for p in plans:
+            self.row0.append(r)
+            r += p.cout
+        self.max_elems = max(p.cout * p.cin_real * 9 + p.cout for p in plans)
+        self._key = None
+        self.table = None
+
+    def _table(self, dev):
+        key = tuple((ptr(p.gw), ptr(p.gb)) for p in self.plans)
+        if key != self._key:
+            descs = [ReduceDesc(ptr(p.gw), ptr(p.gb) if p.bias is not None else None, r0, p.cout, p.cin_real, 0)
+                     for p, r0 in zip(self.plans, self.row0)]
+            arr = (ReduceDesc * len(descs))(*descs)
+            self.table = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(dev)
+            self._key = key
+        return self.table
+
+    def run(self, x: torch.Tensor, x_cs: int, x_co: int, in_h: int, in_w: int, dz: torch.Tensor, dz_cs: int, n: int,
+            workspace: "Workspace", accumulate: bool) -> None:
+        lib = _lib.load()
+        d = ConvDesc(n, in_h, in_w, self.in_c, x_cs, x_co, 1, 3, 1, 1, in_h, in_w, self.out_c, 0, 0, 8)
+        ns = lib.climsr_conv2d_wgrad_splits(ctypes.byref(d))
+        need = lib.climsr_conv2d_wgrad_workspace(ctypes.byref(d), ns)
+        ws = workspace.get(need, x.device)
+        part = ws
+        bpart = ws[ns * self.out_c * self.in_c * 9:]
+        s = _lib.stream_ptr()
+        flops = sum(2 * p.cin_real * p.cout * 9 for p in self.plans) * n * in_h * in_w
+        _run("conv_wgrad64_kernel", flops, lambda: check(
+            lib.climsr_conv2d_wgrad(ctypes.byref(d), ptr(x), ptr(dz), dz_cs, ptr(part), ptr(bpart), ns, s),
+            f"grouped wgrad {self.name}"), "wgrad " + self.name)
+        tab = self._table(x.device)
+        check(lib.climsr_conv2d_wgrad_reduce_rows(ptr(part), ptr(bpart), ns, self.out_c, self.in_c * 9, 3, ptr(tab),
+                                                  len(self.plans), self.max_elems, 1 if accumulate else 0, s),
+              f"grouped wgrad reduce {self.name}")
 
 
 class Workspace:

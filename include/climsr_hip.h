@@ -128,6 +128,19 @@ int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, const uint16
 /* Sum the split partials into OIHW fp32 grads (accumulate=1: +=).  bias_grad may be NULL. */
 int climsr_conv2d_wgrad_reduce(const float* partial, const float* bias_partial, int nsplit, int out_c, int in_c_real,
                                int in_c, int ks, float* wgrad, float* bias_grad, int accumulate, void* stream);
+/* One conv of a row-sliced wgrad reduction: output channels = partial rows [row0, row0+out_c), inputs =
+ * the first in_c_real*ks*ks columns of each row; wgrad OIHW fp32, bias_grad may be NULL. */
+typedef struct ClimsrReduceDesc {
+  float* wgrad;
+  float* bias_grad;
+  int32_t row0, out_c, in_c_real, reserved;
+} ClimsrReduceDesc;
+/* Sum the split partials of ONE climsr_conv2d_wgrad call (partial [nsplit][co_rows][kw]) into several
+ * convs at once (descs: DEVICE array; max_elems = largest out_c*in_c_real*ks*ks + out_c).  Used for the
+ * residual dense block, whose five weight gradients are one GEMM over the side-by-side conv output
+ * gradients (esrgan.py:22-26). */
+int climsr_conv2d_wgrad_reduce_rows(const float* partial, const float* bias_partial, int nsplit, int co_rows, int kw, int ks,
+                                    const ClimsrReduceDesc* descs, int ndesc, int64_t max_elems, int accumulate, void* stream);
 /* Split count and workspace floats climsr_conv2d_wgrad needs for this geometry. */
 int climsr_conv2d_wgrad_splits(const ClimsrConvDesc* d);
 size_t climsr_conv2d_wgrad_workspace(const ClimsrConvDesc* d, int nsplit);

@@ -13,6 +13,7 @@ from climsr_amd.ops import ACT_LRELU, OUT_F32, ConvPlan, Workspace  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=32)
 ap.add_argument("--reps", type=int, default=20)
+ap.add_argument("--rdb-only", action="store_true")
 args = ap.parse_args()
 dev = "cuda"
 n = args.batch
@@ -54,7 +55,7 @@ def plan(cin, cout, ks, up=1):
 
 rows = []
 ws = Workspace()
-for (cin, cout, ks, h, up) in [(64, 16, 3, 64, 1), (112, 16, 3, 64, 1), (128, 64, 3, 64, 1), (64, 64, 3, 128, 2), (64, 64, 3, 256, 1),
+for (cin, cout, ks, h, up) in [] if args.rdb_only else [(64, 16, 3, 64, 1), (112, 16, 3, 64, 1), (128, 64, 3, 64, 1), (64, 64, 3, 128, 2), (64, 64, 3, 256, 1),
                                (3, 64, 9, 256, 1), (64, 1, 3, 256, 1), (32, 1, 5, 256, 1)]:
     p = plan(cin, cout, ks, up)
     hin = h // up
