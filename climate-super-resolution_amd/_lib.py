@@ -62,6 +62,7 @@ SIGNATURES = {
     "climsr_last_error": (ctypes.c_char_p, []),
     "climsr_version": (c_int, []),
     "climsr_conv_chunk": (c_int, [c_int, c_int, c_int]),
+    "climsr_conv_chunk_ex": (c_int, [c_int, c_int, c_int, c_int]),
     "climsr_conv_packed_k": (c_int, [c_int, c_int, c_int]),
     "climsr_conv_packed_rows": (c_int, [c_int]),
     "climsr_pack_conv_weight": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),

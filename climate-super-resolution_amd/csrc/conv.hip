@@ -89,8 +89,9 @@ extern "C" int climsr_version(void) { return 2; }
 // gradients) run on conv_n16_kernel, whose packed K is tap-major with the channels padded to 32 per tap.
 static bool n16_shape(int in_c, int ks, int out_c) { return out_c <= 16 && ks == 3 && in_c <= 128; }
 
-extern "C" int climsr_conv_chunk(int in_c, int ks, int out_c) {
-  if (n16_shape(in_c, ks, out_c)) return in_c <= 32 ? 32 : (in_c <= 64 ? 64 : 128);
+extern "C" int climsr_conv_chunk_ex(int in_c, int ks, int out_c, int stride) {
+  if (stride == 1 && n16_shape(in_c, ks, out_c))  // conv_n16: one chunk, padded to 32/64/128
+    return in_c <= 32 ? 32 : (in_c <= 64 ? 64 : 128);
   int cc = round_up(in_c, 8);
   FwdGeom g;
   while (cc > 8) {
@@ -102,6 +103,8 @@ extern "C" int climsr_conv_chunk(int in_c, int ks, int out_c) {
   }
   return cc;
 }
+
+extern "C" int climsr_conv_chunk(int in_c, int ks, int out_c) { return climsr_conv_chunk_ex(in_c, ks, out_c, 1); }
 
 extern "C" int climsr_conv_packed_k(int in_c, int ks, int cc) {
   return ceil_div(in_c, cc) * round_up(ks * ks * cc, 32);
@@ -283,6 +286,122 @@ __device__ __forceinline__ float ep_res(float v, int act, float slope, bool has1
 
 // RF: the epilogue may read fp32 residuals (then one output row per round, to stay within 256 registers)
 // MV: staging vectors (16 B) per thread and stream held in registers per batch
+// 8 consecutive channels of a residual / output operand (16 B bf16 or 32 B fp32)
+struct Raw8 {
+  uint4 lo, hi;
+};
+__device__ __forceinline__ Raw8 load8(const void* p, bool f32, long idx) {
+  Raw8 r;
+  if (f32) {
+    r.lo = *(const uint4*)((const float*)p + idx);
+    r.hi = *(const uint4*)((const float*)p + idx + 4);
+  } else {
+    r.lo = *(const uint4*)((const uint16_t*)p + idx);
+    r.hi = make_uint4(0, 0, 0, 0);
+  }
+  return r;
+}
+__device__ __forceinline__ float raw8_at(const Raw8& r, bool f32, int i) {
+  if (f32) {
+    const uint4& q = i < 4 ? r.lo : r.hi;
+    const int k = i & 3;
+    return __uint_as_float(k == 0 ? q.x : k == 1 ? q.y : k == 2 ? q.z : q.w);
+  }
+  const int k = i >> 1;
+  const uint32_t w = k == 0 ? r.lo.x : k == 1 ? r.lo.y : k == 2 ? r.lo.z : r.lo.w;
+  return bf2f((uint16_t)((i & 1) ? (w >> 16) : w));
+}
+__device__ __forceinline__ uint4 pack8_bf16(const float* v, float scale) {
+  uint4 o;
+  o.x = (uint32_t)f2bf(scale * v[0]) | ((uint32_t)f2bf(scale * v[1]) << 16);
+  o.y = (uint32_t)f2bf(scale * v[2]) | ((uint32_t)f2bf(scale * v[3]) << 16);
+  o.z = (uint32_t)f2bf(scale * v[4]) | ((uint32_t)f2bf(scale * v[5]) << 16);
+  o.w = (uint32_t)f2bf(scale * v[6]) | ((uint32_t)f2bf(scale * v[7]) << 16);
+  return o;
+}
+
+// Store epilogue for a tile of fp32 results staged in LDS as [pixel][channel] (pitch ep floats): each lane
+// owns 8 consecutive channels of one pixel, so global stores / residual loads are 16 B (bf16) or 32 B
+// (fp32) per lane and 8 lanes cover a 64-channel pixel row (8 B per lane stores are issue-bound).
+// npx pixels (pixel p -> output (oy0 + p / 16, ox0 + p % 16)), nch channels starting at co0.
+template <bool RF, int NPX, int NCH, int NLANE>
+__device__ __forceinline__ void store_tile_lds(const FwdArgs& a, const float* eb, int ep, int lane, int nimg, int oy0, int ox0,
+                                               int co0) {
+  constexpr int NG = NCH / 8, NIT = NPX * NG;
+  const bool f1 = RF && (a.res_f32 & 1), f2 = RF && ((a.res_f32 >> 1) & 1);
+  const bool vec = (a.out_c & 7) == 0 && ((a.out_cs | a.out_co) & 7) == 0 && (!a.res1 || ((a.r1_cs | a.r1_co) & 7) == 0) &&
+                   (!a.res2 || ((a.r2_cs | a.r2_co) & 7) == 0) && (!a.aux || ((a.aux_cs | a.aux_co) & 7) == 0);
+  constexpr int IB = 2;  // items per round: their global loads are in flight together
+#pragma unroll
+  for (int base = 0; base < (NIT + NLANE - 1) / NLANE; base += IB) {
+    Raw8 r1[IB], r2[IB], old[IB];
+    int pidxs[IB];
+    bool ok[IB];
+#pragma unroll
+    for (int j = 0; j < IB; ++j) {
+      const int it = (base + j) * NLANE + lane;
+      const int pl = it / NG, cg = it - (it / NG) * NG;
+      const int oy = oy0 + pl / 16, ox = ox0 + (pl & 15);
+      const int co = co0 + cg * 8;
+      ok[j] = it < NIT && oy < a.out_h && ox < a.out_w && co < a.out_c;
+      pidxs[j] = ((nimg * a.out_h + oy) * a.out_w + ox);
+      r1[j].lo = r1[j].hi = r2[j].lo = r2[j].hi = old[j].lo = old[j].hi = make_uint4(0, 0, 0, 0);
+      if (ok[j] && vec && co + 7 < a.out_c) {
+        const long pidx = pidxs[j];
+        if (a.res1) r1[j] = load8(a.res1, f1, pidx * a.r1_cs + a.r1_co + co);
+        if (a.res2) r2[j] = load8(a.res2, f2, pidx * a.r2_cs + a.r2_co + co);
+        if (a.out_mode == 2) old[j] = load8(a.y, true, pidx * a.out_cs + a.out_co + co);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < IB; ++j) {
+      if (!ok[j]) continue;
+      const int it = (base + j) * NLANE + lane;
+      const int pl = it / NG, cg = it - (it / NG) * NG;
+      const int co = co0 + cg * 8;
+      const long pidx = pidxs[j];
+      const float4 s0 = *(const float4*)(eb + pl * ep + cg * 8), s1 = *(const float4*)(eb + pl * ep + cg * 8 + 4);
+      float v[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+      const long ob = pidx * a.out_cs + a.out_co + co;
+      if (vec && co + 7 < a.out_c) {
+        float4 b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0;
+        if (a.bias) {
+          b0 = *(const float4*)(a.bias + co);
+          b1 = *(const float4*)(a.bias + co + 4);
+        }
+        const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          v[i] = ep_res(act_apply(v[i] + bb[i], a.act, a.slope), a.act, a.slope, a.res1 != nullptr, raw8_at(r1[j], f1, i), a.alpha1,
+                        a.beta1, a.res2 != nullptr, raw8_at(r2[j], f2, i), a.alpha2, a.beta2);
+        if (a.out_mode == 0) {
+          *(uint4*)((uint16_t*)a.y + ob) = pack8_bf16(v, 1.f);
+        } else {
+          float o[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] = v[i] + (a.out_mode == 2 ? raw8_at(old[j], true, i) : 0.f);
+          *(float4*)((float*)a.y + ob) = make_float4(o[0], o[1], o[2], o[3]);
+          *(float4*)((float*)a.y + ob + 4) = make_float4(o[4], o[5], o[6], o[7]);
+        }
+        if (a.aux) *(uint4*)(a.aux + pidx * a.aux_cs + a.aux_co + co) = pack8_bf16(v, a.aux_scale);
+      } else {  // scalar tail (channel counts / slices not multiples of 8)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          if (co + i >= a.out_c) continue;
+          const float r1v = a.res1 ? res_at(a.res1, f1, pidx * a.r1_cs + a.r1_co + co + i) : 0.f;
+          const float r2v = a.res2 ? res_at(a.res2, f2, pidx * a.r2_cs + a.r2_co + co + i) : 0.f;
+          const float x = ep_res(act_apply(v[i] + (a.bias ? a.bias[co + i] : 0.f), a.act, a.slope), a.act, a.slope,
+                                 a.res1 != nullptr, r1v, a.alpha1, a.beta1, a.res2 != nullptr, r2v, a.alpha2, a.beta2);
+          if (a.out_mode == 0) ((uint16_t*)a.y)[ob + i] = f2bf(x);
+          else if (a.out_mode == 2) ((float*)a.y)[ob + i] += x;
+          else ((float*)a.y)[ob + i] = x;
+          if (a.aux) a.aux[pidx * a.aux_cs + a.aux_co + co + i] = f2bf(a.aux_scale * x);
+        }
+      }
+    }
+  }
+}
+
 template <int MW, int NT, bool RF, int MV>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -470,104 +589,16 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
     }
     return;
   }
-  // vector path needs 4-channel-aligned rows (true for every layer of the generator)
-  const bool valign = ((a.out_cs | a.out_co) & 3) == 0 && (!a.res1 || ((a.r1_cs | a.r1_co) & 3) == 0) &&
-                      (!a.res2 || ((a.r2_cs | a.r2_co) & 3) == 0);
-  float4 bv[NT];
+  // coalesced epilogue: the wave's MW x 16 pixels x 16 NT channels go through its own LDS region
+  constexpr int EPP = NT * 16 + 4;  // LDS pitch (floats) of a staged pixel
+  float* eb = (float*)smem + wave * (MW * 16 * EPP);
+  __syncthreads();  // every wave is done with the staged operands (the regions alias them)
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int co = co_blk0 + t * 16 + g * 4;
-    bv[t] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (a.bias) {
-      if (co + 3 < a.out_c) bv[t] = *(const float4*)(a.bias + co);
-      else {
-        if (co < a.out_c) bv[t].x = a.bias[co];
-        if (co + 1 < a.out_c) bv[t].y = a.bias[co + 1];
-        if (co + 2 < a.out_c) bv[t].z = a.bias[co + 2];
-      }
-    }
-  }
-  // two output rows (fragments) per round: operand loads for both rows are in flight together while
-  // the register footprint stays at 2*NT fragments
-  const bool f1 = RF && (a.res_f32 & 1), f2 = RF && ((a.res_f32 >> 1) & 1);
-  constexpr int EPR = RF ? 1 : 2;  // output rows per epilogue round
+  for (int m = 0; m < MW; ++m)
 #pragma unroll
-  for (int mm = 0; mm < MW; mm += EPR) {
-    uint4 r1v[EPR][NT], r2v[EPR][NT];
-    float4 old[EPR][NT];
-#pragma unroll
-    for (int h = 0; h < EPR; ++h) {
-      const int m = mm + h;
-      const int oy = oy0 + wave * MW + m;
-      const bool pv = oy < a.out_h && ox < a.out_w;
-      const long pidx = ((long)nimg * a.out_h + oy) * a.out_w + ox;
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const int co = co_blk0 + t * 16 + g * 4;
-        const bool vec = pv && valign && co + 3 < a.out_c;
-        r1v[h][t] = make_uint4(0, 0, 0, 0);
-        r2v[h][t] = make_uint4(0, 0, 0, 0);
-        old[h][t] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (vec) {
-          if (a.res1) r1v[h][t] = load_res4(a.res1, f1, pidx * a.r1_cs + a.r1_co + co);
-          if (a.res2) r2v[h][t] = load_res4(a.res2, f2, pidx * a.r2_cs + a.r2_co + co);
-          if (a.out_mode == 2) old[h][t] = *(const float4*)((const float*)a.y + pidx * a.out_cs + a.out_co + co);
-        }
-      }
-    }
-#pragma unroll
-    for (int h = 0; h < EPR; ++h) {
-      const int m = mm + h;
-      const int oy = oy0 + wave * MW + m;
-      const bool pv = oy < a.out_h && ox < a.out_w;
-      const long pidx = ((long)nimg * a.out_h + oy) * a.out_w + ox;
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const int co = co_blk0 + t * 16 + g * 4;
-        if (!pv || co >= a.out_c) continue;
-        const bool vec = valign && co + 3 < a.out_c;
-        const float bb[4] = {bv[t].x, bv[t].y, bv[t].z, bv[t].w};
-        float v[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = act_apply(acc[m][t][i] + bb[i], a.act, a.slope);
-        const long ob = pidx * a.out_cs + a.out_co + co;
-        if (vec) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            v[i] = ep_res(v[i], a.act, a.slope, a.res1 != nullptr, res4_at(r1v[h][t], f1, i), a.alpha1, a.beta1,
-                          a.res2 != nullptr, res4_at(r2v[h][t], f2, i), a.alpha2, a.beta2);
-          if (a.out_mode == 0) {
-            uint2 pk;
-            pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-            pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-            *(uint2*)((uint16_t*)a.y + ob) = pk;
-          } else {
-            float4 o = old[h][t];
-            *(float4*)((float*)a.y + ob) = make_float4(o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]);
-          }
-          if (a.aux) {
-            uint2 pk;
-            pk.x = (uint32_t)f2bf(a.aux_scale * v[0]) | ((uint32_t)f2bf(a.aux_scale * v[1]) << 16);
-            pk.y = (uint32_t)f2bf(a.aux_scale * v[2]) | ((uint32_t)f2bf(a.aux_scale * v[3]) << 16);
-            *(uint2*)(a.aux + pidx * a.aux_cs + a.aux_co + co) = pk;
-          }
-        } else {  // scalar tail (out_c not a multiple of 4 or unaligned slices)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            if (co + i >= a.out_c) continue;
-            const float r1 = a.res1 ? res_at(a.res1, f1, pidx * a.r1_cs + a.r1_co + co + i) : 0.f;
-            const float r2 = a.res2 ? res_at(a.res2, f2, pidx * a.r2_cs + a.r2_co + co + i) : 0.f;
-            const float x = ep_res(v[i], a.act, a.slope, a.res1 != nullptr, r1, a.alpha1, a.beta1, a.res2 != nullptr, r2,
-                                   a.alpha2, a.beta2);
-            if (a.out_mode == 0) ((uint16_t*)a.y)[ob + i] = f2bf(x);
-            else if (a.out_mode == 2) ((float*)a.y)[ob + i] += x;
-            else ((float*)a.y)[ob + i] = x;
-            if (a.aux) a.aux[pidx * a.aux_cs + a.aux_co + co + i] = f2bf(a.aux_scale * x);
-          }
-        }
-      }
-    }
-  }
+    for (int t = 0; t < NT; ++t) *(f32x4*)(eb + (m * 16 + col) * EPP + t * 16 + g * 4) = acc[m][t];
+  __syncthreads();  // orders the staging writes before the transposed reads (they use another vector type)
+  store_tile_lds<RF, MW * 16, NT * 16, 64>(a, eb, EPP, lane, nimg, oy0 + wave * MW, ox0, co_blk0);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -671,16 +702,19 @@ __global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs
     if (!(a.ablate & 2)) {
       const uint16_t* xb = xs + ((rg * MW) * N16_TPW + col) * P + cb * 32 + g * 8;
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx)
+      for (int kx = 0; kx < 3; ++kx) {
+        bf16x8 b[MW + 2];  // all input rows of this kx in flight before the first MFMA
 #pragma unroll
-        for (int ir = 0; ir < MW + 2; ++ir) {
-          const bf16x8 b = *(const bf16x8*)(xb + (ir * N16_TPW + kx) * P);
+        for (int ir = 0; ir < MW + 2; ++ir) b[ir] = *(const bf16x8*)(xb + (ir * N16_TPW + kx) * P);
+        __builtin_amdgcn_sched_barrier(0);  // keep the reads batched (the scheduler would re-serialise them)
+#pragma unroll
+        for (int ir = 0; ir < MW + 2; ++ir)
 #pragma unroll
           for (int ky = 0; ky < 3; ++ky) {
             const int m = ir - ky;
-            if (m >= 0 && m < MW) acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ky * 3 + kx], b, acc[m], 0, 0, 0);
+            if (m >= 0 && m < MW) acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ky * 3 + kx], b[ir], acc[m], 0, 0, 0);
           }
-        }
+      }
     }
     __syncthreads();  // input tile reads done: the partials overwrite it
 #pragma unroll
@@ -787,6 +821,253 @@ static int launch_n16(const FwdArgs& a, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------------------
+// 3x3 stride-1 conv with 17..64 outputs and <= 128 inputs (RDB conv5 and its pull gradient, trunk_conv,
+// upconv1/2 with the nearest x2 upsample on load, HRconv, and their data gradients without a 2x2 sum).
+// One 8-wave workgroup per CU walks 8x16-pixel output tiles (persistent), next tile prefetched into
+// registers.  Wave w = (co block w%4, K half w/4) keeps its 16 x (9 taps x Cin/2) weight fragments in
+// VGPRs for the whole launch (no per-tile weight restaging), reads each input-row B fragment once for the
+// three output rows it feeds, and the two K halves meet through LDS (each finishes 4 of the 8 rows).
+// ------------------------------------------------------------------------------------------
+constexpr int C64_TH = 8;
+constexpr int C64_TPH = C64_TH + 2, C64_TPW = TW + 2;
+
+static bool co64_shape(int in_c, int ks, int out_c) { return ks == 3 && out_c > 16 && out_c <= 64 && in_c <= 128; }
+
+template <int NCB, bool RF>
+__global__ __launch_bounds__(512, 1) void conv_co64_kernel(FwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* xs = (uint16_t*)smem;
+  float* part = (float*)smem;  // [cob 4][kh 2][row 4][lane 64][4] (aliases the input tile after compute)
+  constexpr int CINP = NCB * 32, P = CINP + 8, CV = CINP / 8;
+  constexpr int NCBH = (NCB + 1) / 2;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
+  const int cob = wave & 3, kh = wave >> 2;
+  const int cb0 = kh * NCBH;
+  const int cvec = a.in_c / 8;
+  const int upsh = a.up == 2 ? 1 : 0;
+  const int lh = a.in_h << upsh, lw = a.in_w << upsh;
+
+  // A fragments of this wave: rows co = 16 cob + col, k = tap * CINP + 32 cb + 8 g (packed with cc = CINP)
+  bf16x8 af[9][NCBH];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int c = 0; c < NCBH; ++c) {
+      af[t][c] = (bf16x8){};
+      if (cb0 + c < NCB && !(a.ablate & 16))
+        af[t][c] = *(const bf16x8*)(a.w + (long)(cob * 16 + col) * a.kpk + t * CINP + (cb0 + c) * 32 + g * 8);
+    }
+  const int co = cob * 16 + g * 4;
+  float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (a.bias) {
+    bv.x = co < a.out_c ? a.bias[co] : 0.f;
+    bv.y = co + 1 < a.out_c ? a.bias[co + 1] : 0.f;
+    bv.z = co + 2 < a.out_c ? a.bias[co + 2] : 0.f;
+    bv.w = co + 3 < a.out_c ? a.bias[co + 3] : 0.f;
+  }
+  const int ntiles = a.tiles_x * a.tiles_y * a.n;
+  const bool f1 = RF && (a.res_f32 & 1), f2 = RF && ((a.res_f32 >> 1) & 1);
+  const bool valign = ((a.out_cs | a.out_co) & 3) == 0 && (!a.res1 || ((a.r1_cs | a.r1_co) & 3) == 0) &&
+                      (!a.res2 || ((a.r2_cs | a.r2_co) & 3) == 0) && co + 3 < a.out_c;
+
+  constexpr int NPIX = C64_TPH * C64_TPW, NV = (NPIX * CV + 511) / 512;
+  uint4 pre[NV];
+  auto issue = [&](int tile) {
+    int tt = tile;
+    const int tx = tt % a.tiles_x;
+    tt /= a.tiles_x;
+    const int ty = tt % a.tiles_y;
+    const int nimg = tt / a.tiles_y;
+    const int iy0 = ty * C64_TH - 1, ix0 = tx * TW - 1;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = tid + 512 * i;
+      const int pix = v / CV, j = v % CV;
+      const int py = pix / C64_TPW, px = pix - py * C64_TPW;
+      const int iy = iy0 + py, ix = ix0 + px;
+      pre[i] = make_uint4(0, 0, 0, 0);
+      if (v < NPIX * CV && j < cvec && !(a.ablate & 1) && iy >= 0 && iy < lh && ix >= 0 && ix < lw)
+        pre[i] = *(const uint4*)(a.x + (((long)nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + j * 8);
+    }
+  };
+  if (blockIdx.x < ntiles) issue(blockIdx.x);
+
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    int tt = tile;
+    const int tx = tt % a.tiles_x;
+    tt /= a.tiles_x;
+    const int ty = tt % a.tiles_y;
+    const int nimg = tt / a.tiles_y;
+    const int oy0 = ty * C64_TH, ox0 = tx * TW;
+    __syncthreads();  // previous tile's partial reads are done
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = tid + 512 * i;
+      if (v < NPIX * CV) *(uint4*)(xs + (v / CV) * P + (v % CV) * 8) = pre[i];
+    }
+    if (tile + (int)gridDim.x < ntiles) issue(tile + gridDim.x);
+    __syncthreads();
+    f32x4 acc[C64_TH];
+#pragma unroll
+    for (int m = 0; m < C64_TH; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (!(a.ablate & 2)) {
+      const uint16_t* xb = xs + col * P + g * 8;
+#pragma unroll
+      for (int c = 0; c < NCBH; ++c) {
+        if (cb0 + c >= NCB) break;
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          bf16x8 b[C64_TH + 2];  // all input rows of this (channel block, kx) in flight before the first MFMA
+#pragma unroll
+          for (int ir = 0; ir < C64_TH + 2; ++ir) b[ir] = *(const bf16x8*)(xb + (ir * C64_TPW + kx) * P + (cb0 + c) * 32);
+          __builtin_amdgcn_sched_barrier(0);  // keep the reads batched (the scheduler would re-serialise them)
+#pragma unroll
+          for (int ir = 0; ir < C64_TH + 2; ++ir)
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky) {
+              const int m = ir - ky;
+              if (m >= 0 && m < C64_TH) acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ky * 3 + kx][c], b[ir], acc[m], 0, 0, 0);
+            }
+        }
+      }
+    }
+    f32x4 sum[4];
+    if (!(a.ablate & 32)) {
+      __syncthreads();  // input tile reads done: partials overwrite it
+      // hand the partner K half the 4 rows it finishes; keep (and complete) my 4
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        *(f32x4*)(part + (((cob * 2 + kh) * 4 + m) * 64 + lane) * 4) = acc[(1 - kh) * 4 + m];
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        sum[m] = acc[kh * 4 + m] + *(const f32x4*)(part + (((cob * 2 + (1 - kh)) * 4 + m) * 64 + lane) * 4);
+    } else {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) sum[m] = acc[kh * 4 + m];
+    }
+    if (a.ablate & 4) continue;
+    // epilogue: rows oy0 + 4 kh + m, column ox0 + col, channels co..co+3
+    const int ox = ox0 + col;
+    if (a.down2) {  // 2x2 sum (data gradient of a nearest x2 upsample): rows (m, m+1), columns via lane ^ 1
+      const int dh = a.out_h >> 1, dw = a.out_w >> 1;
+#pragma unroll
+      for (int m = 0; m < 4; m += 2) {
+        const int oy = oy0 + kh * 4 + m;
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float sm = sum[m][i] + sum[m + 1][i];
+          sm += __shfl_xor(sm, 1);
+          v[i] = sm;
+        }
+        if ((col & 1) || oy >= a.out_h || ox >= a.out_w || co >= a.out_c) continue;
+        float* yp = (float*)a.y + (((long)nimg * dh + (oy >> 1)) * dw + (ox >> 1)) * a.out_cs + a.out_co + co;
+        if (valign) {
+          float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (a.out_mode == 2) o = *(const float4*)yp;
+          *(float4*)yp = make_float4(o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (co + i < a.out_c) yp[i] = (a.out_mode == 2 ? yp[i] : 0.f) + v[i];
+        }
+      }
+      continue;
+    }
+#pragma unroll
+    for (int mm = 0; mm < 4; mm += 2) {  // two rows per round: loads of both in flight, half the registers
+      uint4 r1v[2], r2v[2];
+      float4 old[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int oy = oy0 + kh * 4 + mm + h;
+        const long pidx = ((long)nimg * a.out_h + oy) * a.out_w + ox;
+        r1v[h] = r2v[h] = make_uint4(0, 0, 0, 0);
+        old[h] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (oy < a.out_h && ox < a.out_w && valign) {
+          if (a.res1) r1v[h] = load_res4(a.res1, f1, pidx * a.r1_cs + a.r1_co + co);
+          if (a.res2) r2v[h] = load_res4(a.res2, f2, pidx * a.r2_cs + a.r2_co + co);
+          if (a.out_mode == 2) old[h] = *(const float4*)((const float*)a.y + pidx * a.out_cs + a.out_co + co);
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int m = mm + h;
+        const int oy = oy0 + kh * 4 + m;
+        if (oy >= a.out_h || ox >= a.out_w || co >= a.out_c) continue;
+        const long pidx = ((long)nimg * a.out_h + oy) * a.out_w + ox;
+        const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
+        float v[4];
+        const long ob = pidx * a.out_cs + a.out_co + co;
+        if (valign) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            v[i] = ep_res(act_apply(sum[m][i] + bb[i], a.act, a.slope), a.act, a.slope, a.res1 != nullptr, res4_at(r1v[h], f1, i),
+                          a.alpha1, a.beta1, a.res2 != nullptr, res4_at(r2v[h], f2, i), a.alpha2, a.beta2);
+          if (a.out_mode == 0) {
+            uint2 pk;
+            pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+            pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+            *(uint2*)((uint16_t*)a.y + ob) = pk;
+          } else {
+            *(float4*)((float*)a.y + ob) = make_float4(old[h].x + v[0], old[h].y + v[1], old[h].z + v[2], old[h].w + v[3]);
+          }
+          if (a.aux) {
+            uint2 pk;
+            pk.x = (uint32_t)f2bf(a.aux_scale * v[0]) | ((uint32_t)f2bf(a.aux_scale * v[1]) << 16);
+            pk.y = (uint32_t)f2bf(a.aux_scale * v[2]) | ((uint32_t)f2bf(a.aux_scale * v[3]) << 16);
+            *(uint2*)(a.aux + pidx * a.aux_cs + a.aux_co + co) = pk;
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (co + i >= a.out_c) continue;
+            const float r1 = a.res1 ? res_at(a.res1, f1, pidx * a.r1_cs + a.r1_co + co + i) : 0.f;
+            const float r2 = a.res2 ? res_at(a.res2, f2, pidx * a.r2_cs + a.r2_co + co + i) : 0.f;
+            const float x = ep_res(act_apply(sum[m][i] + bb[i], a.act, a.slope), a.act, a.slope, a.res1 != nullptr, r1, a.alpha1,
+                                   a.beta1, a.res2 != nullptr, r2, a.alpha2, a.beta2);
+            if (a.out_mode == 0) ((uint16_t*)a.y)[ob + i] = f2bf(x);
+            else if (a.out_mode == 2) ((float*)a.y)[ob + i] += x;
+            else ((float*)a.y)[ob + i] = x;
+            if (a.aux) a.aux[pidx * a.aux_cs + a.aux_co + co + i] = f2bf(a.aux_scale * x);
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int NCB, bool RF>
+static int launch_co64_t(const FwdArgs& a, hipStream_t s) {
+  auto k = conv_co64_kernel<NCB, RF>;
+  size_t lds = (size_t)C64_TPH * C64_TPW * (NCB * 32 + 8) * 2;
+  const size_t lds_p = (size_t)4 * 2 * 4 * 64 * 16;
+  if (lds_p > lds) lds = lds_p;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (ncu <= 0) ncu = 256;
+  }
+  const int ntiles = a.tiles_x * a.tiles_y * a.n;
+  const int grid = ntiles < ncu ? ntiles : ncu;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(512), lds, s, a);
+  return check_launch("conv2d_fwd (co64)");
+}
+
+template <int NCB>
+static int launch_co64(const FwdArgs& a, hipStream_t s) {
+  return a.res_f32 ? launch_co64_t<NCB, true>(a, s) : launch_co64_t<NCB, false>(a, s);
+}
+
+// ------------------------------------------------------------------------------------------
 // Single-output-channel conv on VALU (v_dot2_f32_bf16): conv_last (64->1), srcnn.conv3 (32->1) and
 // the data gradient of srcnn.conv1 w.r.t. its first input channel (64->1, 9x9).  With Cout = 1 an
 // MFMA tile would waste 15 of 16 rows; here each thread owns one output pixel of a 16x16 tile, the
@@ -883,6 +1164,8 @@ __global__ __launch_bounds__(256) void conv_co1_kernel(FwdArgs a) {
 template <int MW, int NT>
 static int launch_fwd(const FwdArgs& a, int ncob, size_t lds, hipStream_t s) {
   dim3 grid(a.tiles_x * a.tiles_y * a.n, ncob);
+  const size_t lds_ep = (size_t)4 * MW * 16 * (NT * 16 + 4) * 4;  // epilogue staging (aliases the operands)
+  if (lds_ep > lds) lds = lds_ep;
   constexpr int MV = NT == 1 ? 6 : (NT == 2 ? 8 : 4);
   auto k = a.res_f32 ? conv_fwd_kernel<MW, NT, true, MV> : conv_fwd_kernel<MW, NT, false, MV>;
   static bool attr_set = false;
@@ -926,10 +1209,6 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
   // 16x16 output tiles (64 px per wave) for the 64-channel layers; 8x16 otherwise
   const int mw = (d->out_h >= 12 && fwd_nt(d->out_c) == 4) ? 4 : 2;
   fwd_geom(d->in_c, d->ks, d->stride, d->out_c, d->cc, mw, &g);
-  if (g.lds_total > 160 * 1024) {
-    set_error("conv2d_fwd: LDS %zu exceeds 160 KiB (cc=%d)", g.lds_total, d->cc);
-    return CLIMSR_EINVAL;
-  }
   FwdArgs a;
   a.x = x; a.w = wpk; a.bias = bias; a.y = y;
   a.res1 = ep->res1; a.res2 = ep->res2; a.aux = (uint16_t*)ep->aux;
@@ -965,6 +1244,22 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
       case 2: return launch_n16<2>(a, s);
       default: return launch_n16<4>(a, s);
     }
+  }
+  // conv_co64_kernel (A fragments register-resident, K halves per wave) measured slower than the generic
+  // kernel on every shape (register-capped at 8 waves/CU); kept for reference, not dispatched.
+  if (false && co64_shape(d->in_c, d->ks, d->out_c) && d->cc == 32 * n16_ncb(d->in_c) && d->stride == 1 && d->pad == 1 &&
+      (d->up == 1 || d->up == 2) && d->out_h == d->in_h * d->up && d->out_w == d->in_w * d->up) {
+    a.tiles_x = ceil_div(d->out_w, TW);
+    a.tiles_y = ceil_div(d->out_h, C64_TH);
+    switch (d->cc / 32) {
+      case 1: return launch_co64<1>(a, s);
+      case 2: return launch_co64<2>(a, s);
+      default: return launch_co64<4>(a, s);
+    }
+  }
+  if (g.lds_total > 160 * 1024) {
+    set_error("conv2d_fwd: LDS %zu exceeds 160 KiB (cc=%d)", g.lds_total, d->cc);
+    return CLIMSR_EINVAL;
   }
   if (mw == 4) return launch_fwd<4, 4>(a, ncob, g.lds_total, s);
   switch (g.nt) {

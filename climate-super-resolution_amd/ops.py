@@ -76,13 +76,13 @@ class ConvPlan:
         self.cin_real, self.cout, self.ks, self.stride = cin_real, cout, ks, stride
         self.pad = ks // 2 if pad is None else pad
         self.cin = round_up(cin_real, 8)
-        self.cc = lib.climsr_conv_chunk(self.cin, ks, cout)
+        self.cc = lib.climsr_conv_chunk_ex(self.cin, ks, cout, stride)
         self.kpk = lib.climsr_conv_packed_k(self.cin, ks, self.cc)
         self.rows = lib.climsr_conv_packed_rows(cout)
         # transposed conv (data gradient): in = cout (padded to 8), out = cin_real
         self.cin_t = round_up(cout, 8)
         self.cout_t = cin_real
-        self.cc_t = lib.climsr_conv_chunk(self.cin_t, ks, self.cout_t)
+        self.cc_t = lib.climsr_conv_chunk_ex(self.cin_t, ks, self.cout_t, stride)
         self.kpk_t = lib.climsr_conv_packed_k(self.cin_t, ks, self.cc_t)
         self.rows_t = lib.climsr_conv_packed_rows(self.cout_t)
         self.wpk: Optional[torch.Tensor] = None

@@ -75,8 +75,11 @@ typedef struct ClimsrEpilogue {
 const char* climsr_last_error(void);
 int climsr_version(void);
 
-/* Channel chunk used by the packed weight layout for a conv with `in_c` input channels. */
+/* Channel chunk used by the packed weight layout for a conv with `in_c` input channels: stride 1 (and
+ * every data gradient of a stride-1 conv); _ex takes the stride (a stride-2 conv and its data gradient,
+ * which runs over the zero-inserted gradient, use stride 2). */
 int climsr_conv_chunk(int in_c, int ks, int out_c);
+int climsr_conv_chunk_ex(int in_c, int ks, int out_c, int stride);
 /* Number of bf16 elements per output-channel row of the packed weight (nchunk * Kc_pad). */
 int climsr_conv_packed_k(int in_c, int ks, int cc);
 

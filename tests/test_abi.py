@@ -65,12 +65,13 @@ def test_geometry_helpers(lib):
     # chunking keeps the staged LDS tile within budget; packed K is a multiple of 32 per chunk
     for cin, ks, cout in [(64, 3, 16), (128, 3, 64), (112, 3, 16), (8, 9, 64), (512, 3, 512)]:
         cc = lib.climsr_conv_chunk(cin, ks, cout)
-        if cout <= 16 and ks == 3 and cin <= 128:  # dense-block kernel: one chunk, channels padded to 32/64/128
+        if cout <= 16 and ks == 3 and cin <= 128:  # n16 kernel: one chunk, channels padded to 32/64/128
             assert cc == (32 if cin <= 32 else 64 if cin <= 64 else 128)
         else:
             assert cc % 8 == 0 and 8 <= cc <= cin
         k = lib.climsr_conv_packed_k(cin, ks, cc)
         assert k % 32 == 0 and k >= ks * ks * cin
+    assert lib.climsr_conv_chunk_ex(112, 3, 16, 2) != 128  # stride 2: generic chunk
     assert lib.climsr_conv_packed_rows(1) == 16
     assert lib.climsr_conv_packed_rows(48) == 64
     assert lib.climsr_conv_packed_rows(512) == 512
