@@ -545,9 +545,13 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
   // fragment before the first store, so their latencies overlap instead of serialising.
   const int ox = ox0 + col;
   if (a.down2) {
-    // sum the 2x2 block: rows (m, m+1) are in this wave (MW even, oy0 even); columns pair via lane^1
+    // sum the 2x2 block: rows (m, m+1) are in this wave (MW even, oy0 even); columns pair via lane^1.
+    // Optional activation backward (act 3/4, res1 = the activation output at the LOW-res pixel), bf16 or
+    // fp32 (=, +=) store and a bf16 aux copy.
     const int dh = a.out_h >> 1, dw = a.out_w >> 1;
+    const bool mask = a.act == 3 || a.act == 4;
     float4 old[MW / 2][NT];
+    uint2 r1v[MW / 2][NT];
 #pragma unroll
     for (int m = 0; m < MW; m += 2) {
       const int oy = oy0 + wave * MW + m;
@@ -556,8 +560,10 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
       for (int t = 0; t < NT; ++t) {
         const int co = co_blk0 + t * 16 + g * 4;
         old[m / 2][t] = make_float4(0.f, 0.f, 0.f, 0.f);
-        const bool ok = (col & 1) == 0 && oy < a.out_h && ox < a.out_w && co + 3 < a.out_c && a.out_mode == 2;
-        if (ok) old[m / 2][t] = *(const float4*)((const float*)a.y + pidx * a.out_cs + a.out_co + co);
+        r1v[m / 2][t] = make_uint2(0, 0);
+        const bool ok = (col & 1) == 0 && oy < a.out_h && ox < a.out_w && co + 3 < a.out_c;
+        if (ok && a.out_mode == 2) old[m / 2][t] = *(const float4*)((const float*)a.y + pidx * a.out_cs + a.out_co + co);
+        if (ok && mask) r1v[m / 2][t] = *(const uint2*)((const uint16_t*)a.res1 + pidx * a.r1_cs + a.r1_co + co);
       }
     }
 #pragma unroll
@@ -575,14 +581,40 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
         }
         const int co = co_blk0 + t * 16 + g * 4;
         if ((col & 1) == 0 && oy < a.out_h && ox < a.out_w) {
-          float* yp = (float*)a.y + pidx * a.out_cs + a.out_co + co;
+          const long ob = pidx * a.out_cs + a.out_co + co;
           if (co + 3 < a.out_c) {
-            float4 o = old[m / 2][t];
-            *(float4*)yp = make_float4(o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]);
+            const uint4 r1 = make_uint4(r1v[m / 2][t].x, r1v[m / 2][t].y, 0, 0);
+            if (mask) {
+#pragma unroll
+              for (int i = 0; i < 4; ++i) v[i] = ep_res(v[i], a.act, a.slope, true, res4_at(r1, false, i), 1.f, 1.f, false, 0.f, 1.f, 1.f);
+            }
+            if (a.out_mode == 0) {
+              uint2 pk;
+              pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+              pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+              *(uint2*)((uint16_t*)a.y + ob) = pk;
+            } else {
+              float4 o = old[m / 2][t];
+              *(float4*)((float*)a.y + ob) = make_float4(o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]);
+            }
+            if (a.aux) {
+              uint2 pk;
+              pk.x = (uint32_t)f2bf(a.aux_scale * v[0]) | ((uint32_t)f2bf(a.aux_scale * v[1]) << 16);
+              pk.y = (uint32_t)f2bf(a.aux_scale * v[2]) | ((uint32_t)f2bf(a.aux_scale * v[3]) << 16);
+              *(uint2*)(a.aux + pidx * a.aux_cs + a.aux_co + co) = pk;
+            }
           } else {
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-              if (co + i < a.out_c) yp[i] = (a.out_mode == 2 ? yp[i] : 0.f) + v[i];
+            for (int i = 0; i < 4; ++i) {
+              if (co + i >= a.out_c) continue;
+              float x = v[i];
+              if (mask) x = ep_res(x, a.act, a.slope, true, res_at(a.res1, false, pidx * a.r1_cs + a.r1_co + co + i), 1.f, 1.f, false,
+                                   0.f, 1.f, 1.f);
+              if (a.out_mode == 0) ((uint16_t*)a.y)[ob + i] = f2bf(x);
+              else if (a.out_mode == 2) ((float*)a.y)[ob + i] += x;
+              else ((float*)a.y)[ob + i] = x;
+              if (a.aux) a.aux[pidx * a.aux_cs + a.aux_co + co + i] = f2bf(a.aux_scale * x);
+            }
           }
         }
       }
@@ -1193,8 +1225,9 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
               d->in_coff, d->cc, d->up, d->stride, d->ks);
     return CLIMSR_EINVAL;
   }
-  if (ep->down2 && (ep->out_mode == 0 || ep->res1 || ep->res2 || ep->aux || bias || ep->act || (d->out_h & 1) || (d->out_w & 1))) {
-    set_error("conv2d_fwd: down2 epilogue needs f32 output, no bias/act/residual/aux, even output size");
+  if (ep->down2 && (ep->res2 || ep->res_f32 || bias || ep->act == 1 || ep->act == 2 || (ep->res1 && ep->act < 3) ||
+                    (d->out_h & 1) || (d->out_w & 1))) {
+    set_error("conv2d_fwd: down2 epilogue: no bias / forward activation / residual (act 3/4 mask only), even output size");
     return CLIMSR_EINVAL;
   }
   if (ep->act < 0 || ep->act > 4 || ((ep->act == 3 || ep->act == 4) && !ep->res1)) {

@@ -24,7 +24,7 @@ import torch.nn as nn
 from torch import Tensor
 
 from ..core.flat import FlatParamsMixin
-from ..ops import (ACT_LRELU, ACT_LRELU_BWD, ACT_NONE, ACT_RELU, OUT_F32, BatchedPacker, ConvPlan, GroupedWgrad, PullPacker, PullPlan,
+from ..ops import (ACT_LRELU, ACT_LRELU_BWD, ACT_NONE, ACT_RELU, ACT_RELU_BWD, OUT_F32, BatchedPacker, ConvPlan, GroupedWgrad, PullPacker, PullPlan,
                    Workspace, act_grad, axpby, nchw_to_nhwc)
 from .srcnn import SRCNN
 
@@ -248,45 +248,40 @@ class _Engine:
         npx_hr = n * hh * ww
         npx_lr = n * h * w
         gout = gout.contiguous().float()
-        gbig = self._scratch("gbig", (n, hh, ww, nf), torch.float32, dev)
-        dzbig = self._scratch("dzbig", (n, hh, ww, nf), torch.bfloat16, dev)
+        # HR-resolution output gradients stay bf16: every data gradient applies the next activation's
+        # backward in its epilogue (no fp32 [N,4H,4W,64] intermediates, no separate act_grad passes)
+        dzA = self._scratch("dzA", (n, hh, ww, nf), torch.bfloat16, dev)
+        dzB = self._scratch("dzB", (n, hh, ww, nf), torch.bfloat16, dev)
         dz8 = self._scratch("dz8", (n, hh, ww, 8), torch.bfloat16, dev)
-        # ---- SRCNN tail (srcnn.py:13-18)
-        act_grad(npx_hr, 1, gout, 1, 0, None, 0, 0, ACT_NONE, dz8, 8)
-        P["srcnn.conv3"].wgrad(sv["s2"], 32, 0, hh, ww, dz8, 8, n, ws, acc)
-        g32 = self._scratch("g32", (n, hh, ww, 32), torch.float32, dev)
-        P["srcnn.conv3"].dgrad(dz8, 8, hh, ww, g32, 32, 0, n)
         dz32 = self._scratch("dz32", (n, hh, ww, 32), torch.bfloat16, dev)
-        act_grad(npx_hr, 32, g32, 32, 0, sv["s2"], 32, 0, ACT_RELU, dz32, 32)
+        # ---- SRCNN tail (srcnn.py:13-18)
+        act_grad(npx_hr, 1, gout, 1, 0, None, 0, 0, ACT_NONE, dz8, 8)  # also zeroes dz8's pad channels
+        P["srcnn.conv3"].wgrad(sv["s2"], 32, 0, hh, ww, dz8, 8, n, ws, acc)
+        P["srcnn.conv3"].dgrad(dz8, 8, hh, ww, dz32, 32, 0, n, act=ACT_RELU_BWD, res1=sv["s2"], res1_cs=32, res1_co=0)
         P["srcnn.conv2"].wgrad(sv["s1"], 64, 0, hh, ww, dz32, 32, n, ws, acc)
-        P["srcnn.conv2"].dgrad(dz32, 32, hh, ww, gbig, nf, 0, n)
-        act_grad(npx_hr, 64, gbig, nf, 0, sv["s1"], 64, 0, ACT_RELU, dzbig, 64)
-        P["srcnn.conv1"].wgrad(sv["tail"], 8, 0, hh, ww, dzbig, 64, n, ws, acc)
-        gtail = self._scratch("gtail", (n, hh, ww, 8), torch.float32, dev)
-        P["srcnn.conv1"].dgrad(dzbig, 64, hh, ww, gtail, 8, 0, n, cout_t=1)  # only d(out) is needed
+        P["srcnn.conv2"].dgrad(dz32, 32, hh, ww, dzA, nf, 0, n, act=ACT_RELU_BWD, res1=sv["s1"], res1_cs=64, res1_co=0)
+        P["srcnn.conv1"].wgrad(sv["tail"], 8, 0, hh, ww, dzA, 64, n, ws, acc)
+        # only d(out) (tail channel 0) is needed; channels 1..7 of dz8 stay 0
+        P["srcnn.conv1"].dgrad(dzA, 64, hh, ww, dz8, 8, 0, n, cout_t=1)
         # ---- conv_last / HRconv (esrgan.py:99)
-        act_grad(npx_hr, 1, gtail, 8, 0, None, 0, 0, ACT_NONE, dz8, 8)
         P["conv_last"].wgrad(sv["hr"], nf, 0, hh, ww, dz8, 8, n, ws, acc)
-        P["conv_last"].dgrad(dz8, 8, hh, ww, gbig, nf, 0, n)
-        act_grad(npx_hr, nf, gbig, nf, 0, sv["hr"], nf, 0, ACT_LRELU, dzbig, nf)
-        P["HRconv"].wgrad(sv["u2"], nf, 0, hh, ww, dzbig, nf, n, ws, acc)
-        P["HRconv"].dgrad(dzbig, nf, hh, ww, gbig, nf, 0, n)
+        P["conv_last"].dgrad(dz8, 8, hh, ww, dzA, nf, 0, n, act=ACT_LRELU_BWD, res1=sv["hr"], res1_cs=nf, res1_co=0)
+        P["HRconv"].wgrad(sv["u2"], nf, 0, hh, ww, dzA, nf, n, ws, acc)
         # ---- upsampling (esrgan.py:94-97)
-        g_u1 = self._scratch("g_u1", (n, h2, w2, nf), torch.float32, dev)
         dz_u1 = self._scratch("dz_u1", (n, h2, w2, nf), torch.bfloat16, dev)
         if sf == 4:
-            act_grad(npx_hr, nf, gbig, nf, 0, sv["u2"], nf, 0, ACT_LRELU, dzbig, nf)
-            P["upconv2"].wgrad(sv["u1"], nf, 0, h2, w2, dzbig, nf, n, ws, acc, up=2)
-            P["upconv2"].dgrad(dzbig, nf, hh, ww, g_u1, nf, 0, n, down2=True)
-            act_grad(n * h2 * w2, nf, g_u1, nf, 0, sv["u1"], nf, 0, ACT_LRELU, dz_u1, nf)
+            P["HRconv"].dgrad(dzA, nf, hh, ww, dzB, nf, 0, n, act=ACT_LRELU_BWD, res1=sv["u2"], res1_cs=nf, res1_co=0)
+            P["upconv2"].wgrad(sv["u1"], nf, 0, h2, w2, dzB, nf, n, ws, acc, up=2)
+            P["upconv2"].dgrad(dzB, nf, hh, ww, dz_u1, nf, 0, n, down2=True, act=ACT_LRELU_BWD, res1=sv["u1"], res1_cs=nf,
+                               res1_co=0)
         else:
-            act_grad(npx_hr, nf, gbig, nf, 0, sv["u1"], nf, 0, ACT_LRELU, dz_u1, nf)
+            P["HRconv"].dgrad(dzA, nf, hh, ww, dz_u1, nf, 0, n, act=ACT_LRELU_BWD, res1=sv["u1"], res1_cs=nf, res1_co=0)
         g_fea2 = self._scratch("g_fea2", (n, h, w, nf), torch.float32, dev)
-        P["upconv1"].wgrad(sv["fea2"], nf, 0, h, w, dz_u1, nf, n, ws, acc, up=2)
-        P["upconv1"].dgrad(dz_u1, nf, h2, w2, g_fea2, nf, 0, n, down2=True)
-        # ---- trunk_conv + global skip (esrgan.py:90-91)
         dz64 = self._scratch("dz64", (n, h, w, nf), torch.bfloat16, dev)
-        act_grad(npx_lr, nf, g_fea2, nf, 0, None, 0, 0, ACT_NONE, dz64, nf)
+        P["upconv1"].wgrad(sv["fea2"], nf, 0, h, w, dz_u1, nf, n, ws, acc, up=2)
+        # fp32 gradient of fea2 (it also feeds the global skip) + its bf16 copy for trunk_conv's weight gradient
+        P["upconv1"].dgrad(dz_u1, nf, h2, w2, g_fea2, nf, 0, n, down2=True, aux=dz64, aux_cs=nf, aux_co=0)
+        # ---- trunk_conv + global skip (esrgan.py:90-91)
         dense = sv["dense"]
         L = 3 * nb
         P["trunk_conv"].wgrad(dense[L], dc, 0, h, w, dz64, nf, n, ws, acc)

@@ -150,9 +150,12 @@ class ConvPlan:
 
     def dgrad(self, dz: torch.Tensor, dz_cs: int, out_h: int, out_w: int, g: torch.Tensor, g_cs: int, g_co: int, n: int,
               accumulate: bool = False, down2: bool = False, cout_t: Optional[int] = None, aux: Optional[torch.Tensor] = None,
-              aux_cs: int = 0, aux_co: int = 0, aux_scale: float = 1.0) -> None:
-        """Data gradient: g[:, :, :, g_co:g_co+cin_real] (+)= conv^T(dz) (fp32); (out_h, out_w) are dz's dims.  With
-        down2 the result is summed over 2x2 pixel blocks (backward of the nearest x2 upsample feeding this conv).
+              aux_cs: int = 0, aux_co: int = 0, aux_scale: float = 1.0, act: int = ACT_NONE, res1: Optional[torch.Tensor] = None,
+              res1_cs: int = 0, res1_co: int = 0) -> None:
+        """Data gradient: g[:, :, :, g_co:g_co+cin_real] (+)= conv^T(dz); (out_h, out_w) are dz's dims.  g is fp32
+        (= or += with accumulate), or bf16: then it is the NEXT layer's conv output gradient directly, with
+        act = ACT_LRELU_BWD / ACT_RELU_BWD applied from that layer's stored activation res1.  With down2 the
+        result is summed over 2x2 pixel blocks (backward of the nearest x2 upsample feeding this conv).
         Stride-2 convs (pad 1, even input) run as a stride-1 conv over the zero-inserted dz."""
         ct = self.cout_t if cout_t is None else cout_t
         pad_t = self.ks - 1 - self.pad
@@ -163,8 +166,9 @@ class ConvPlan:
             d = ConvDesc(n, out_h, out_w, self.cin_t, dz_cs, 0, -2, self.ks, 1, pad_t, 2 * out_h, 2 * out_w, ct, g_cs, g_co,
                          self.cc_t)
             out_h, out_w = 2 * out_h, 2 * out_w
-        ep = Epilogue(0, 0.0, 1.0, None, 0, 0, 1.0, None, 0, 0, OUT_F32_ADD if accumulate else OUT_F32, 1 if down2 else 0,
-                      0, 1.0, 1.0, aux_cs, ptr(aux), aux_co, aux_scale)
+        mode = OUT_BF16 if g.dtype == torch.bfloat16 else (OUT_F32_ADD if accumulate else OUT_F32)
+        ep = Epilogue(act, 0.2 if act == ACT_LRELU_BWD else 0.0, 1.0, ptr(res1), res1_cs, res1_co, 1.0, None, 0, 0, mode,
+                      1 if down2 else 0, 0, 1.0, 1.0, aux_cs, ptr(aux), aux_co, aux_scale)
         flops = 2 * self.cout * ct * self.ks * self.ks * n * out_h * out_w
         _run(fwd_kernel_name(ct, out_h, False, self.cin_t, self.ks, 1, 1 if self.stride == 1 else -2), flops, lambda: check(
             _lib.load().climsr_conv2d_fwd(ctypes.byref(d), ptr(dz), ptr(self.wpk_t), None, ctypes.byref(ep), ptr(g),

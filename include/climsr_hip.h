@@ -63,7 +63,8 @@ typedef struct ClimsrEpilogue {
   const void* res2;             /* bf16 (or fp32, res_f32 bit 1) */
   int32_t res2_cstride, res2_coff;
   int32_t out_mode;             /* 0 bf16 store, 1 f32 store, 2 f32 accumulate (+=) */
-  int32_t down2;                /* 1: sum 2x2 output pixels into out[y/2][x/2] (dgrad of a nearest x2 upsample) */
+  int32_t down2;                /* 1: sum 2x2 output pixels into out[y/2][x/2] (dgrad of a nearest x2 upsample); then no
+                                   bias / forward act / residual, act 3/4 read res1 at the half-resolution pixel */
   int32_t res_f32;              /* bit 0: res1 is fp32, bit 1: res2 is fp32 */
   float beta1, beta2;           /* residual scales (1 for a plain residual add) */
   int32_t aux_cstride;
