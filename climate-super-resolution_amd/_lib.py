@@ -51,6 +51,13 @@ class ReduceDesc(ctypes.Structure):
                 ("in_c_real", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
+class ChainDesc(ctypes.Structure):
+    _fields_ = [("base", c_void_p), ("bcs", ctypes.c_int32), ("boff", ctypes.c_int32), ("out", c_void_p), ("ocs", ctypes.c_int32),
+                ("ooff", ctypes.c_int32 * 4), ("wt", c_void_p * 4), ("bias", c_void_p * 4), ("mask", c_void_p),
+                ("mcs", ctypes.c_int32), ("moff", ctypes.c_int32 * 4), ("act", ctypes.c_int32), ("slope", c_float),
+                ("n", ctypes.c_int32), ("h", ctypes.c_int32), ("w", ctypes.c_int32)]
+
+
 class PullPackDesc(ctypes.Structure):
     _fields_ = [("out", c_void_p), ("seg_w", c_void_p * 5), ("seg_oc", ctypes.c_int32 * 5), ("seg_ic", ctypes.c_int32 * 5)] + [
         (n, ctypes.c_int32) for n in ("nseg", "out_c", "in_c", "ks", "cc", "ci_off")]
@@ -68,6 +75,8 @@ SIGNATURES = {
     "climsr_pack_conv_weight": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "climsr_pack_conv_weights_batched": (c_int, [c_void_p, c_int, c_int64, c_void_p]),
     "climsr_pack_pull_weights_batched": (c_int, [c_void_p, c_int, c_int64, c_void_p]),
+    "climsr_rdb_chain": (c_int, [P(ChainDesc), c_void_p]),
+    "climsr_rdb_chain_kp": (c_int, [c_int]),
     "climsr_conv2d_fwd": (c_int, [P(ConvDesc), c_void_p, c_void_p, c_void_p, P(Epilogue), c_void_p, c_void_p]),
     "climsr_conv2d_wgrad": (c_int, [P(ConvDesc), c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "climsr_conv2d_wgrad_reduce": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,

@@ -17,6 +17,7 @@ node whose arithmetic is entirely HIP (libclimsr_hip.so):
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -25,7 +26,7 @@ from torch import Tensor
 
 from ..core.flat import FlatParamsMixin
 from ..ops import (ACT_LRELU, ACT_LRELU_BWD, ACT_NONE, ACT_RELU, ACT_RELU_BWD, OUT_F32, BatchedPacker, ConvPlan, GroupedWgrad, PullPacker, PullPlan,
-                   Workspace, act_grad, axpby, nchw_to_nhwc)
+                   RdbChain, Workspace, act_grad, axpby, nchw_to_nhwc)
 from .srcnn import SRCNN
 
 
@@ -113,7 +114,16 @@ class _Engine:
             # RDB convs need no transposed weights: their data gradients run as pull convs (below)
             p.bind(conv.weight, conv.bias, need_t=(name != "conv_first" and ".RDB" not in name))
         dev = gen.conv_first.weight.device
-        self.packer = BatchedPacker(list(self.plans.values()), dev)
+        # conv1..conv4 of every RDB (and their pull gradients) as one fused row-streaming launch each (nf 64, gc 16).
+        # Measured slower than the four conv_n16 launches so far (barrier-bound: the four levels' work per step is
+        # unequal), so it is opt-in (CLIMSR_RDB_CHAIN=1) and parity-tested against the per-conv path.
+        self.chains: List[RdbChain] = []
+        if nf == 64 and gc == 16 and os.environ.get("CLIMSR_RDB_CHAIN") == "1":
+            for i in range(3 * self.nb):
+                blk, r = divmod(i, 3)
+                self.chains.append(RdbChain([self.plans[self.rdb_name(blk, r + 1, k)] for k in range(1, 6)],
+                                            f"RRDB_trunk.{blk}.RDB{r + 1}"))
+        self.packer = BatchedPacker(list(self.plans.values()), dev, [d for ch in self.chains for d in ch.pack_descs()])
         # Pull-form RDB backward: the dense concatenation's channel group j (0 = x, 1..4 = x1..x4) receives the
         # transposed convs of conv j+1..conv5, whose output gradients sit side by side in one buffer
         # dZ = [dZ1|dZ2|dZ3|dZ4|dZ5] (gc,gc,gc,gc,nf channels): group j's gradient is one conv over dZ[:, j*gc:].
@@ -129,7 +139,8 @@ class _Engine:
                 lst.append(PullPlan(segs, nf if j == 0 else gc, 0 if j == 0 else nf + (j - 1) * gc, 3,
                                     f"RRDB_trunk.{blk}.RDB{r + 1}.pull{j}"))
             self.pulls.append(lst)
-        self.pull_packer = PullPacker([p for lst in self.pulls for p in lst], dev)
+        self.pull_packer = PullPacker([p for lst in self.pulls for p in (lst[:1] if self.chains else lst)], dev,
+                                      [d for ch in self.chains for d in ch.pull_descs()])
         # the five weight gradients of an RDB: one GEMM over dZ (all dc channels) x the dense buffer (dc channels)
         self.rdb_wgrads: List[GroupedWgrad] = []
         for i in range(3 * self.nb if self.dc % 64 == 0 else 0):
@@ -193,8 +204,11 @@ class _Engine:
             dst = dense[i + 1] if keep else dense[(i + 1) % 2]
             if r == 0 and not keep:  # remember the RRDB input for its residual
                 axpby_bf16_copy(src, rrdb_in, n * h * w, nf, dc)
-            for c in range(1, 5):
-                P[self.rdb_name(blk, r + 1, c)].fwd(src, dc, 0, h, w, src, dc, nf + (c - 1) * gc, n, act=ACT_LRELU)
+            if self.chains:
+                self.chains[i].forward(src, dc, n, h, w)
+            else:
+                for c in range(1, 5):
+                    P[self.rdb_name(blk, r + 1, c)].fwd(src, dc, 0, h, w, src, dc, nf + (c - 1) * gc, n, act=ACT_LRELU)
             res2 = None
             if r == 2:
                 res2 = dense[3 * blk] if keep else rrdb_in
@@ -298,9 +312,12 @@ class _Engine:
             g_out, g_in, g_skip = G[(i + 1) % 4], G[i % 4], G[(3 * blk + 3) % 4]
             dz, src, pulls = dZ[i % 2], dense[i], self.pulls[i]
             # dZ_j = lrelu'(x_j) * sum_{k>j} conv_k^T(dZ_k)   (x_j = channels nf+(j-1)gc.. of the dense buffer)
-            for j in (4, 3, 2, 1):
-                pulls[j].fwd(dz, dc, j * gc, h, w, dz, dc, (j - 1) * gc, n, act=ACT_LRELU_BWD, use_bias=False,
-                             res1=src, res1_cs=dc, res1_co=nf + (j - 1) * gc)
+            if self.chains:
+                self.chains[i].pull(dz, src, dc, n, h, w)
+            else:
+                for j in (4, 3, 2, 1):
+                    pulls[j].fwd(dz, dc, j * gc, h, w, dz, dc, (j - 1) * gc, n, act=ACT_LRELU_BWD, use_bias=False,
+                                 res1=src, res1_cs=dc, res1_co=nf + (j - 1) * gc)
             # G_in = sum_k conv_k^T(dZ_k) + s_o * G_out (+ the RRDB skip gradient at its first RDB); the next
             # (earlier) RDB's conv5 output gradient dZ5 = 0.2 * s_o' * G_in is written alongside
             aux = dZ[(i - 1) % 2] if i > 0 else None

@@ -13,7 +13,7 @@ from typing import Optional
 import torch
 
 from . import _lib
-from ._lib import ConvDesc, Epilogue, PackDesc, PullPackDesc, ReduceDesc, check, ptr
+from ._lib import ChainDesc, ConvDesc, Epilogue, PackDesc, PullPackDesc, ReduceDesc, check, ptr
 
 ACT_NONE, ACT_LRELU, ACT_RELU = 0, 1, 2
 ACT_LRELU_BWD, ACT_RELU_BWD = 3, 4  # epilogue multiplies by act'(res1), res1 = the activation's output
@@ -300,10 +300,11 @@ def rdb_bwd_init(npix: int, nf: int, dc: int, gx: torch.Tensor, gy: torch.Tensor
 class BatchedPacker:
     """All weight packs of a network as ONE launch (descriptor table resident on the device)."""
 
-    def __init__(self, plans, device):
+    def __init__(self, plans, device, extra=()):
         descs = []
         for p in plans:
             descs += p.pack_descs()
+        descs += list(extra)
         arr = (PackDesc * len(descs))(*descs)
         raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
         self.table = raw.to(device)
@@ -313,6 +314,8 @@ class BatchedPacker:
         for p in plans:
             if p.wpk_t is not None:
                 self.max_elems = max(self.max_elems, p.rows_t * p.kpk_t)
+        for d in extra:
+            self.max_elems = max(self.max_elems, 16 * 9 * d.cc)
 
     def run(self):
         check(_lib.load().climsr_pack_conv_weights_batched(ptr(self.table), self.n, self.max_elems, _lib.stream_ptr()),
@@ -340,15 +343,78 @@ class PullPlan(ConvPlan):
         return d
 
 
+class RdbChain:
+    """The four 16-output convs of a residual dense block (esrgan.py:22-37) as ONE row-streaming launch
+    (csrc/rdb_chain.hip), forward (conv1..conv4 -> x1..x4) and pull backward (pull4..pull1 -> dZ4..dZ1).
+    convs: the block's five ConvPlans (bound).  Needs nf = 64, gc = 16."""
+
+    def __init__(self, convs, name: str = ""):
+        lib = _lib.load()
+        self.convs, self.name = convs, name
+        dev = convs[0].weight.device
+        self.kp = [lib.climsr_rdb_chain_kp(L) for L in range(1, 5)]
+        self.w_fwd = [torch.empty((16, 9 * kp), dtype=torch.bfloat16, device=dev) for kp in self.kp]
+        self.w_pull = [torch.empty((16, 9 * kp), dtype=torch.bfloat16, device=dev) for kp in self.kp]
+
+    def pack_descs(self):
+        out = []
+        for L in range(1, 5):
+            c = self.convs[L - 1]
+            out.append(PackDesc(ptr(c.weight), ptr(self.w_fwd[L - 1]), 16, self.kp[L - 1], c.cin_real, 16, 3, self.kp[L - 1], 0, 0))
+        return out
+
+    def pull_descs(self):
+        out = []
+        for L in range(1, 5):
+            j = 5 - L  # this level produces dZ_j, the gradient of x_j (channels 64 + 16(j-1) of the block input)
+            d = PullPackDesc()
+            d.out = ptr(self.w_pull[L - 1])
+            order = [5] + list(range(4, j, -1))  # base dZ5, then dZ4, dZ3, ... (chain channel order)
+            for si, k in enumerate(order):
+                c = self.convs[k - 1]
+                d.seg_w[si], d.seg_oc[si], d.seg_ic[si] = ptr(c.weight), c.cout, c.cin_real
+            d.nseg, d.out_c, d.in_c, d.ks, d.cc, d.ci_off = len(order), 16, sum(self.convs[k - 1].cout for k in order), 3, \
+                self.kp[L - 1], 64 + 16 * (j - 1)
+            out.append(d)
+        return out
+
+    def _launch(self, d, tag):
+        flops = sum(2 * self.convs[L].cin_real * 16 * 9 for L in range(4)) * d.n * d.h * d.w
+        _run("rdb_chain_kernel", flops, lambda: check(_lib.load().climsr_rdb_chain(ctypes.byref(d), _lib.stream_ptr()),
+                                                      f"rdb chain {self.name}"), tag + " " + self.name)
+
+    def forward(self, dense: torch.Tensor, dc: int, n: int, h: int, w: int, slope: float = 0.2) -> None:
+        d = ChainDesc()
+        d.base, d.bcs, d.boff, d.out, d.ocs = ptr(dense), dc, 0, ptr(dense), dc
+        for L in range(4):
+            d.ooff[L] = 64 + 16 * L
+            d.wt[L] = ptr(self.w_fwd[L])
+            d.bias[L] = ptr(self.convs[L].bias)
+        d.mask, d.mcs, d.act, d.slope, d.n, d.h, d.w = None, 0, ACT_LRELU, slope, n, h, w
+        self._launch(d, "fwd")
+
+    def pull(self, dz: torch.Tensor, dense: torch.Tensor, dc: int, n: int, h: int, w: int, slope: float = 0.2) -> None:
+        d = ChainDesc()
+        d.base, d.bcs, d.boff, d.out, d.ocs = ptr(dz), dc, 64, ptr(dz), dc
+        for L in range(4):
+            j = 4 - L  # level L+1 produces dZ_j
+            d.ooff[L] = 16 * (j - 1)
+            d.wt[L] = ptr(self.w_pull[L])
+            d.bias[L] = None
+            d.moff[L] = 64 + 16 * (j - 1)
+        d.mask, d.mcs, d.act, d.slope, d.n, d.h, d.w = ptr(dense), dc, ACT_LRELU_BWD, slope, n, h, w
+        self._launch(d, "pull")
+
+
 class PullPacker:
     """Every pull weight of a network packed by ONE launch (descriptor table resident on the device)."""
 
-    def __init__(self, pulls, device):
-        descs = [p.pull_desc() for p in pulls]
+    def __init__(self, pulls, device, extra=()):
+        descs = [p.pull_desc() for p in pulls] + list(extra)
         arr = (PullPackDesc * len(descs))(*descs)
         self.table = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(device)
         self.n = len(descs)
-        self.max_elems = max(p.rows * p.kpk for p in pulls)
+        self.max_elems = max([p.rows * p.kpk for p in pulls] + [16 * 9 * d.cc for d in extra])
 
     def run(self):
         check(_lib.load().climsr_pack_pull_weights_batched(ptr(self.table), self.n, self.max_elems, _lib.stream_ptr()),

@@ -118,6 +118,30 @@ typedef struct ClimsrPullPackDesc {
 } ClimsrPullPackDesc;
 int climsr_pack_pull_weights_batched(const ClimsrPullPackDesc* descs, int ndesc, int64_t max_elems, void* stream);
 
+/* The four 16-output 3x3 convs of a residual dense block as one row-streaming launch (esrgan.py:22-37):
+ * level L (1..4) reads [base (64 ch at boff) | outputs of levels 1..L-1] and writes 16 bf16 channels at
+ * out[.., ooff[L-1]].  Forward: act 1 (leaky relu, bias[L-1]) = conv1..conv4 writing x1..x4 into the dense
+ * buffer; pull backward: act 3 (leaky-relu derivative read from mask[.., moff[L-1]], no bias) = pull4..pull1
+ * writing dZ4..dZ1.  wt[L-1]: bf16 [16][9*KP] with k = tap*KP + channel, KP = climsr_rdb_chain_kp(L), channel
+ * order base | out1 | out2 | out3 (pack with climsr_pack_conv_weights_batched / _pull_weights_batched, cc = KP). */
+typedef struct ClimsrChainDesc {
+  const uint16_t* base;
+  int32_t bcs, boff;
+  uint16_t* out;
+  int32_t ocs;
+  int32_t ooff[4];
+  const uint16_t* wt[4];
+  const float* bias[4];
+  const uint16_t* mask;
+  int32_t mcs;
+  int32_t moff[4];
+  int32_t act;
+  float slope;
+  int32_t n, h, w;
+} ClimsrChainDesc;
+int climsr_rdb_chain(const ClimsrChainDesc* d, void* stream);
+int climsr_rdb_chain_kp(int level);
+
 /* Implicit-GEMM convolution on MFMA (bf16 in, fp32 accumulate), fused epilogue.
  * Forward of nn.Conv2d (esrgan.py:22-26,72-83; srcnn.py:9-11; rfb_esrgan.py:28-52) and, with
  * transpose_flip weights, its data gradient (stride 1). */

@@ -93,3 +93,27 @@ for k in range(1, 6):
         t = timeit(lambda: p.fwd(dense, dc, 0, 64, 64, out, dc, 0, n, res1=dense, res1_cs=dc, alpha1=0.2), args.reps)
     f = 2 * cin * cout * 9 * n * 64 * 64
     print(f"fwd conv{k} {cin}->{cout}".ljust(32), f"{t:9.1f} us  {f / t / 1e6:8.1f} TFLOP/s")
+
+# fused RDB chain (conv1..conv4 / pull4..pull1 in one launch)
+from climsr_amd.ops import BatchedPacker, PullPacker, RdbChain  # noqa: E402
+
+cplans = []
+for k in range(1, 6):
+    cin = 64 + 16 * (k - 1)
+    cplans.append(plan(cin, 16 if k < 5 else 64, 3))
+chain = RdbChain(cplans, "perf")
+BatchedPacker(cplans, torch.device(dev), chain.pack_descs()).run()
+PullPacker([], torch.device(dev), chain.pull_descs()).run() if False else None
+from climsr_amd import _lib as _l  # noqa: E402
+import ctypes as _ct  # noqa: E402
+
+pd = chain.pull_descs()
+arr = (_l.PullPackDesc * len(pd))(*pd)
+tab = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(dev)
+_l.check(_l.load().climsr_pack_pull_weights_batched(tab.data_ptr(), len(pd), 16 * 9 * 128, _l.stream_ptr()), "pack")
+f = sum(2 * (64 + 16 * k) * 16 * 9 for k in range(4)) * n * 64 * 64
+t = timeit(lambda: chain.forward(dense, dc, n, 64, 64), args.reps)
+print("chain fwd conv1..4".ljust(32), f"{t:9.1f} us  {f / t / 1e6:8.1f} TFLOP/s")
+dzb = torch.randn(n, 64, 64, dc, device=dev).to(torch.bfloat16)
+t = timeit(lambda: chain.pull(dzb, dense, dc, n, 64, 64), args.reps)
+print("chain pull4..1".ljust(32), f"{t:9.1f} us  {f / t / 1e6:8.1f} TFLOP/s")

@@ -262,3 +262,51 @@ def test_rdb_pull_backward_matches_torch():
     want = pull_ref(0) + 0.2 * from_nhwc(g_out, nf).double().cpu() + from_nhwc(g_skip, nf).double().cpu()
     check_close(from_nhwc(g_in, nf).cpu(), want, 1e-5, "G_in")
     check_close(from_nhwc(aux, nf, 4 * gc).cpu(), 0.04 * want, 8e-3, "aux")
+
+
+@pytest.mark.parametrize("h,w", [(16, 32), (37, 45)])
+def test_rdb_chain_matches_per_conv(h, w):
+    """The fused RDB chain (csrc/rdb_chain.hip: conv1..conv4 forward and pull4..pull1 backward in one
+    row-streaming launch with recomputed halos) against the same math run conv by conv (n16 kernel).
+    Both are bf16 MFMA with fp32 accumulation; outputs agree to bf16 rounding (1 ulp of the value), the
+    chain's level inputs being the same bf16 values the per-conv path reads back from HBM."""
+    from climsr_amd.ops import ACT_LRELU_BWD, BatchedPacker, PullPacker, PullPlan, RdbChain
+
+    nf, gc, n = 64, 16, 2
+    dc = nf + 4 * gc
+    gen = torch.Generator().manual_seed(9)
+    plans = []
+    for k in range(1, 6):
+        cin, cout = nf + (k - 1) * gc, (gc if k < 5 else nf)
+        p = ConvPlan(cin, cout, 3, 1, None, f"conv{k}")
+        wt = ((torch.rand((cout, cin, 3, 3), generator=gen) * 2 - 1) / (cin * 9) ** 0.5).to(DEV).contiguous()
+        b = ((torch.rand((cout,), generator=gen) * 2 - 1) * 0.1).to(DEV)
+        p.bind(wt, b, need_t=False)
+        plans.append(p)
+    chain = RdbChain(plans, "t")
+    pulls = []
+    for j in range(5):
+        segs = [(plans[k - 1].weight, gc if k < 5 else nf, nf + (k - 1) * gc) for k in range(j + 1, 6)]
+        pulls.append(PullPlan(segs, nf if j == 0 else gc, 0 if j == 0 else nf + (j - 1) * gc, 3, f"pull{j}"))
+    BatchedPacker(plans, torch.device(DEV), chain.pack_descs()).run()
+    PullPacker(pulls, torch.device(DEV), chain.pull_descs()).run()
+    x = (torch.rand((n, h, w, dc), generator=gen) * 2 - 1).to(torch.bfloat16).to(DEV)
+    ref = x.clone()
+    for k in range(1, 5):
+        plans[k - 1].fwd(ref, dc, 0, h, w, ref, dc, nf + (k - 1) * gc, n, act=ACT_LRELU)
+    got = x.clone()
+    chain.forward(got, dc, n, h, w)
+    dz0 = torch.zeros((n, h, w, dc), dtype=torch.bfloat16, device=DEV)
+    dz0[..., 4 * gc:] = (torch.rand((n, h, w, nf), generator=gen) * 2 - 1).to(torch.bfloat16).to(DEV)
+    dref = dz0.clone()
+    for j in (4, 3, 2, 1):
+        pulls[j].fwd(dref, dc, j * gc, h, w, dref, dc, (j - 1) * gc, n, act=ACT_LRELU_BWD, use_bias=False, res1=ref, res1_cs=dc,
+                     res1_co=nf + (j - 1) * gc)
+    dgot = dz0.clone()
+    chain.pull(dgot, ref, dc, n, h, w)
+    torch.cuda.synchronize()
+    for name, a_, b_ in (("x1..x4", got[..., nf:], ref[..., nf:]), ("dZ1..dZ4", dgot[..., :4 * gc], dref[..., :4 * gc])):
+        a64, b64 = a_.double(), b_.double()
+        err = ((a64 - b64).abs() - 2 ** -7 * b64.abs()).max().item()
+        assert err <= 1e-3 * b64.abs().max().item(), f"{name}: excess error {err}"
+    assert torch.equal(got[..., :nf], x[..., :nf]) and torch.equal(dgot[..., 4 * gc:], dz0[..., 4 * gc:])
