@@ -154,7 +154,7 @@ __global__ void bn_bwd_finish_kernel(const double* __restrict__ part, int nblk, 
 
 __global__ void bn_bwd_apply_kernel(long npix, int c, const float* __restrict__ da, const uint16_t* __restrict__ a,
                                     const uint16_t* __restrict__ z, const float* __restrict__ mean, const float* __restrict__ rstd,
-                                    const float* __restrict__ coef, float slope, uint16_t* __restrict__ dz) {
+                                    const float* __restrict__ coef, float slope, float out_slope, uint16_t* __restrict__ dz) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int groups = c / 8;
   if (idx >= npix * groups) return;
@@ -172,6 +172,8 @@ __global__ void bn_bwd_apply_kernel(long npix, int c, const float* __restrict__ 
     float d = af[i] > 0.f ? dd[i] : dd[i] * slope;
     float xh = (zf[i] - mean[ch]) * rstd[ch];
     o[i] = coef[ch] * (d - coef[c + ch] - xh * coef[2 * c + ch]);
+    // BN input produced by a LeakyReLU (discriminator.py:17-18: conv -> LeakyReLU -> BN): chain its derivative
+    if (out_slope != 1.f && zf[i] <= 0.f) o[i] *= out_slope;
   }
   *(uint4*)(dz + p * c + c0) = pack8(o);
 }
@@ -228,7 +230,7 @@ extern "C" int climsr_bn_inference(const uint16_t* z, int64_t npix, int c, const
 }
 
 extern "C" int climsr_bn_backward(const float* da, const uint16_t* a, const uint16_t* z, int64_t npix, int c, const float* mean,
-                                  const float* rstd, const float* gamma, float slope, double* workspace, float* coef,
+                                  const float* rstd, const float* gamma, float slope, float out_slope, double* workspace, float* coef,
                                   float* dgamma, float* dbeta, int accumulate, uint16_t* dz, void* stream) {
   if (!da || !a || !z || !mean || !rstd || !gamma || !workspace || !coef || !dz || c % 8 || c > 2048) {
     set_error("bn_backward: bad args");
@@ -241,7 +243,7 @@ extern "C" int climsr_bn_backward(const float* da, const uint16_t* a, const uint
                      rstd, dgamma, dbeta, accumulate, coef);
   long total = (long)npix * (c / 8);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, s, (long)npix, c, da, a, z, mean, rstd, coef,
-                     slope, dz);
+                     slope, out_slope, dz);
   return check_launch("bn_backward");
 }
 
@@ -530,7 +532,7 @@ extern "C" int climsr_linear_wgrad(const uint16_t* dy_t, const uint16_t* x_t, in
 // One workgroup, n <= 64, fixed reduction order.
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void d_head_fwd_kernel(const float* __restrict__ h, const float* __restrict__ w2,
-                                                         const float* __restrict__ b2, int n, int o, float* __restrict__ s) {
+                                                         const float* __restrict__ b2, int n, int o, int sigmoid, float* __restrict__ s) {
   __shared__ float red[256];
   for (int b = 0; b < n; ++b) {
     float t = 0.f;
@@ -543,22 +545,22 @@ __global__ __launch_bounds__(256) void d_head_fwd_kernel(const float* __restrict
     }
     if (threadIdx.x == 0) {
       float u = red[0] + b2[0];
-      s[b] = 1.f / (1.f + expf(-u));
+      s[b] = sigmoid ? 1.f / (1.f + expf(-u)) : u;
     }
     __syncthreads();
   }
 }
 
 __global__ __launch_bounds__(256) void d_head_bwd_kernel(const float* __restrict__ h, const float* __restrict__ s, const float* __restrict__ ds,
-                                                         const float* __restrict__ w2, int n, int o, int n_pad, float slope, float* dw2,
-                                                         float* db2, float* db0, int accumulate, uint16_t* __restrict__ du0,
+                                                         const float* __restrict__ w2, int n, int o, int n_pad, float slope, int sigmoid,
+                                                         float* dw2, float* db2, float* db0, int accumulate, uint16_t* __restrict__ du0,
                                                          uint16_t* __restrict__ du0_t) {
   for (int j = threadIdx.x; j < o; j += 256) {
     float a_w2 = 0.f, a_b0 = 0.f;
     for (int b = 0; b < n_pad; ++b) {
       float v = 0.f;
       if (b < n) {
-        const float du = ds[b] * s[b] * (1.f - s[b]);
+        const float du = sigmoid ? ds[b] * s[b] * (1.f - s[b]) : ds[b];
         const float hv = h[(long)b * o + j];
         a_w2 += du * hv;
         v = du * w2[j] * (hv > 0.f ? 1.f : slope);
@@ -572,28 +574,30 @@ __global__ __launch_bounds__(256) void d_head_bwd_kernel(const float* __restrict
   }
   if (threadIdx.x == 0 && db2) {
     float t = 0.f;
-    for (int b = 0; b < n; ++b) t += ds[b] * s[b] * (1.f - s[b]);
+    for (int b = 0; b < n; ++b) t += sigmoid ? ds[b] * s[b] * (1.f - s[b]) : ds[b];
     db2[0] = (accumulate ? db2[0] : 0.f) + t;
   }
 }
 
-extern "C" int climsr_d_head_fwd(const float* h, const float* w2, const float* b2, int n, int o, float* s, void* stream) {
+extern "C" int climsr_d_head_fwd(const float* h, const float* w2, const float* b2, int n, int o, int sigmoid, float* s,
+                                 void* stream) {
   if (!h || !w2 || !b2 || !s || n <= 0) {
     set_error("d_head_fwd: bad args");
     return CLIMSR_EINVAL;
   }
-  hipLaunchKernelGGL(d_head_fwd_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, h, w2, b2, n, o, s);
+  hipLaunchKernelGGL(d_head_fwd_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, h, w2, b2, n, o, sigmoid, s);
   return check_launch("d_head_fwd");
 }
 
 extern "C" int climsr_d_head_bwd(const float* h, const float* s, const float* ds, const float* w2, int n, int o, int n_pad, float slope,
-                                 float* dw2, float* db2, float* db0, int accumulate, uint16_t* du0, uint16_t* du0_t, void* stream) {
+                                 int sigmoid, float* dw2, float* db2, float* db0, int accumulate, uint16_t* du0, uint16_t* du0_t,
+                                 void* stream) {
   if (!h || !s || !ds || !w2 || !du0 || !du0_t || n_pad < n) {
     set_error("d_head_bwd: bad args");
     return CLIMSR_EINVAL;
   }
-  hipLaunchKernelGGL(d_head_bwd_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, h, s, ds, w2, n, o, n_pad, slope, dw2, db2, db0,
-                     accumulate, du0, du0_t);
+  hipLaunchKernelGGL(d_head_bwd_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, h, s, ds, w2, n, o, n_pad, slope, sigmoid, dw2, db2,
+                     db0, accumulate, du0, du0_t);
   return check_launch("d_head_bwd");
 }
 
@@ -751,4 +755,69 @@ extern "C" int climsr_f32_to_bf16(const float* x, int64_t n, uint16_t* y, void* 
   long threads = (n + 7) / 8;
   hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(ceil_div(threads > 0 ? threads : 1, 256)), dim3(256), 0, (hipStream_t)stream, x, (long)n, y);
   return check_launch("f32_to_bf16");
+}
+
+// ---------------------------------------------------------------------------------------------
+// nn.ReflectionPad2d(1) (discriminator.py:15,21) on NHWC bf16 and its backward (fp32 fold): padded
+// row -1 mirrors row 1, row h mirrors row h-2 (same for columns).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int refl1(int i, int n) { return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i); }
+
+__global__ void reflect_pad1_kernel(const uint16_t* __restrict__ x, int n, int h, int w, int cs, uint16_t* __restrict__ y) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;  // over n*(h+2)*(w+2)*(cs/8)
+  const int groups = cs / 8;
+  const long total = (long)n * (h + 2) * (w + 2) * groups;
+  if (idx >= total) return;
+  const int cg = (int)(idx % groups);
+  long t = idx / groups;
+  const int px = (int)(t % (w + 2));
+  t /= (w + 2);
+  const int py = (int)(t % (h + 2));
+  const int b = (int)(t / (h + 2));
+  const int sy = refl1(py - 1, h), sx = refl1(px - 1, w);
+  *(uint4*)(y + idx * 8) = *(const uint4*)(x + (((long)b * h + sy) * w + sx) * cs + cg * 8);
+}
+
+__global__ void reflect_pad1_bwd_kernel(const float* __restrict__ gp, int n, int h, int w, int c, float* __restrict__ g) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;  // over n*h*w*c
+  const long total = (long)n * h * w * c;
+  if (idx >= total) return;
+  const int ch = (int)(idx % c);
+  long t = idx / c;
+  const int x = (int)(t % w);
+  t /= w;
+  const int y = (int)(t % h);
+  const int b = (int)(t / h);
+  // padded rows / columns that read (y, x): p = y+1, plus the mirror p = 0 (y == 1) and p = h+1 (y == h-2)
+  int rows[3], cols[3], nr = 0, nc = 0;
+  rows[nr++] = y + 1;
+  if (y == 1) rows[nr++] = 0;
+  if (y == h - 2) rows[nr++] = h + 1;
+  cols[nc++] = x + 1;
+  if (x == 1) cols[nc++] = 0;
+  if (x == w - 2) cols[nc++] = w + 1;
+  float s = 0.f;
+  for (int i = 0; i < nr; ++i)
+    for (int j = 0; j < nc; ++j) s += gp[(((long)b * (h + 2) + rows[i]) * (w + 2) + cols[j]) * c + ch];
+  g[idx] = s;
+}
+
+extern "C" int climsr_reflect_pad1_bf16(const uint16_t* x, int n, int h, int w, int cstride, uint16_t* y, void* stream) {
+  if (!x || !y || n <= 0 || h < 2 || w < 2 || cstride % 8) {
+    set_error("reflect_pad1_bf16: bad args");
+    return CLIMSR_EINVAL;
+  }
+  const long total = (long)n * (h + 2) * (w + 2) * (cstride / 8);
+  hipLaunchKernelGGL(reflect_pad1_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, x, n, h, w, cstride, y);
+  return check_launch("reflect_pad1_bf16");
+}
+
+extern "C" int climsr_reflect_pad1_bwd_f32(const float* gp, int n, int h, int w, int c, float* g, void* stream) {
+  if (!gp || !g || n <= 0 || h < 3 || w < 3 || c <= 0) {
+    set_error("reflect_pad1_bwd_f32: bad args");
+    return CLIMSR_EINVAL;
+  }
+  const long total = (long)n * h * w * c;
+  hipLaunchKernelGGL(reflect_pad1_bwd_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, gp, n, h, w, c, g);
+  return check_launch("reflect_pad1_bwd_f32");
 }

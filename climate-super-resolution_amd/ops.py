@@ -159,13 +159,14 @@ class ConvPlan:
         Stride-2 convs (pad 1, even input) run as a stride-1 conv over the zero-inserted dz."""
         ct = self.cout_t if cout_t is None else cout_t
         pad_t = self.ks - 1 - self.pad
-        if self.stride == 1:
-            d = ConvDesc(n, out_h, out_w, self.cin_t, dz_cs, 0, 1, self.ks, 1, pad_t, out_h, out_w, ct, g_cs, g_co, self.cc_t)
+        if self.stride == 1:  # input size = out + ks - 1 - 2 pad (== out for 'same' convs)
+            ih, iw = out_h + 2 * pad_t - self.ks + 1, out_w + 2 * pad_t - self.ks + 1
+            d = ConvDesc(n, out_h, out_w, self.cin_t, dz_cs, 0, 1, self.ks, 1, pad_t, ih, iw, ct, g_cs, g_co, self.cc_t)
         else:  # stride 2: stride-1 conv over the zero-inserted gradient (logical size 2*out)
             assert self.stride == 2 and not down2
-            d = ConvDesc(n, out_h, out_w, self.cin_t, dz_cs, 0, -2, self.ks, 1, pad_t, 2 * out_h, 2 * out_w, ct, g_cs, g_co,
-                         self.cc_t)
-            out_h, out_w = 2 * out_h, 2 * out_w
+            ih, iw = 2 * out_h + 2 * pad_t - self.ks + 1, 2 * out_w + 2 * pad_t - self.ks + 1
+            d = ConvDesc(n, out_h, out_w, self.cin_t, dz_cs, 0, -2, self.ks, 1, pad_t, ih, iw, ct, g_cs, g_co, self.cc_t)
+        out_h, out_w = ih, iw
         mode = OUT_BF16 if g.dtype == torch.bfloat16 else (OUT_F32_ADD if accumulate else OUT_F32)
         ep = Epilogue(act, 0.2 if act == ACT_LRELU_BWD else 0.0, 1.0, ptr(res1), res1_cs, res1_co, 1.0, None, 0, 0, mode,
                       1 if down2 else 0, 0, 1.0, 1.0, aux_cs, ptr(aux), aux_co, aux_scale)
@@ -437,9 +438,17 @@ def bn_inference(z, npix, c, run_mean, run_var, gamma, beta, y, act=ACT_LRELU, s
                                    _lib.stream_ptr()), "bn_inference")
 
 
-def bn_backward(da, a, z, npix, c, mean, rstd, gamma, ws, coef, dgamma, dbeta, accumulate, dz, slope=0.2):
-    check(_L().climsr_bn_backward(ptr(da), ptr(a), ptr(z), npix, c, ptr(mean), ptr(rstd), ptr(gamma), slope, ptr(ws), ptr(coef),
-                                  ptr(dgamma), ptr(dbeta), int(accumulate), ptr(dz), _lib.stream_ptr()), "bn_backward")
+def bn_backward(da, a, z, npix, c, mean, rstd, gamma, ws, coef, dgamma, dbeta, accumulate, dz, slope=0.2, out_slope=1.0):
+    check(_L().climsr_bn_backward(ptr(da), ptr(a), ptr(z), npix, c, ptr(mean), ptr(rstd), ptr(gamma), slope, out_slope, ptr(ws),
+                                  ptr(coef), ptr(dgamma), ptr(dbeta), int(accumulate), ptr(dz), _lib.stream_ptr()), "bn_backward")
+
+
+def reflect_pad1(x, n, h, w, cs, y):
+    check(_L().climsr_reflect_pad1_bf16(ptr(x), n, h, w, cs, ptr(y), _lib.stream_ptr()), "reflect_pad1")
+
+
+def reflect_pad1_bwd(gp, n, h, w, c, g):
+    check(_L().climsr_reflect_pad1_bwd_f32(ptr(gp), n, h, w, c, ptr(g), _lib.stream_ptr()), "reflect_pad1_bwd")
 
 
 def adaptive_pool_fwd(x, n, h, w, c, oh, ow, out, out_t=None, n_pad=0):
@@ -469,13 +478,13 @@ def linear_wgrad(dy_t, x_t, n_pad, k, o, dw, accumulate):
         "wgrad fc.0")
 
 
-def d_head_fwd(h, w2, b2, n, o, s):
-    check(_L().climsr_d_head_fwd(ptr(h), ptr(w2), ptr(b2), n, o, ptr(s), _lib.stream_ptr()), "d_head_fwd")
+def d_head_fwd(h, w2, b2, n, o, s, sigmoid=True):
+    check(_L().climsr_d_head_fwd(ptr(h), ptr(w2), ptr(b2), n, o, int(sigmoid), ptr(s), _lib.stream_ptr()), "d_head_fwd")
 
 
-def d_head_bwd(h, s, ds, w2, n, o, n_pad, dw2, db2, db0, accumulate, du0, du0_t, slope=0.2):
-    check(_L().climsr_d_head_bwd(ptr(h), ptr(s), ptr(ds), ptr(w2), n, o, n_pad, slope, ptr(dw2), ptr(db2), ptr(db0), int(accumulate),
-                                 ptr(du0), ptr(du0_t), _lib.stream_ptr()), "d_head_bwd")
+def d_head_bwd(h, s, ds, w2, n, o, n_pad, dw2, db2, db0, accumulate, du0, du0_t, slope=0.2, sigmoid=True):
+    check(_L().climsr_d_head_bwd(ptr(h), ptr(s), ptr(ds), ptr(w2), n, o, n_pad, slope, int(sigmoid), ptr(dw2), ptr(db2), ptr(db0),
+                                 int(accumulate), ptr(du0), ptr(du0_t), _lib.stream_ptr()), "d_head_bwd")
 
 
 def relativistic_bce(s_real, s_fake, n, t_rf, t_fr, loss=None, gscale=None, g_real=None, g_fake=None):

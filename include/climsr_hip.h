@@ -224,11 +224,13 @@ int climsr_bn_inference(const uint16_t* z, int64_t npix, int c, const float* run
                         const float* gamma, const float* beta, int act, float slope, uint16_t* y, void* stream);
 /* *p += 1 on the device (BatchNorm num_batches_tracked). */
 int climsr_increment_i64(int64_t* p, void* stream);
-/* Backward of act(BN(z)): da = dL/d(act output) fp32, a = act output (bf16, sign gives lrelu'),
- * dz (bf16) = BN input gradient; dgamma/dbeta (+)= .  coef >= 3*c floats scratch. */
+/* Backward of act(BN(z)): da = dL/d(act output) fp32, a = act output (bf16, sign gives lrelu'; slope 1 =
+ * no activation), dz (bf16) = BN input gradient; dgamma/dbeta (+)= .  coef >= 3*c floats scratch.
+ * out_slope != 1: z itself is a LeakyReLU output (plain discriminator, discriminator.py:17-18) and dz is
+ * carried through its derivative (z <= 0 -> * out_slope). */
 int climsr_bn_backward(const float* da, const uint16_t* a, const uint16_t* z, int64_t npix, int c, const float* mean,
-                       const float* rstd, const float* gamma, float slope, double* workspace, float* coef, float* dgamma,
-                       float* dbeta, int accumulate, uint16_t* dz, void* stream);
+                       const float* rstd, const float* gamma, float slope, float out_slope, double* workspace, float* coef,
+                       float* dgamma, float* dbeta, int accumulate, uint16_t* dz, void* stream);
 
 /* nn.AdaptiveAvgPool2d((oh,ow)) (rfb_esrgan.py:54) on NHWC bf16 x [n][h][w][c]; out = torch.flatten
  * order [n][c*oh*ow] bf16; out_t (optional) = its transpose [c*oh*ow][n_pad] for the fc.0 weight grad. */
@@ -246,11 +248,18 @@ int climsr_linear_dgrad(const uint16_t* dy, const uint16_t* w, int n, int k, int
 /* dw[o][k] (+)= sum_n dy_t[o][n] x_t[k][n] (K = n_pad, multiple of 32; k % 64 == 0, o % 64 == 0). */
 int climsr_linear_wgrad(const uint16_t* dy_t, const uint16_t* x_t, int n_pad, int k, int o, float* dw, int accumulate,
                         void* stream);
-/* Discriminator head after fc.0+LeakyReLU (h [n][o] fp32): s[n] = sigmoid(h.w2 + b2) (rfb_esrgan.py:59-60). */
-int climsr_d_head_fwd(const float* h, const float* w2, const float* b2, int n, int o, float* s, void* stream);
-/* Head backward from ds[n]: dw2/db2/db0 (+)=; du0 = d(fc.0 pre-activation) as bf16 [n][o] and [o][n_pad]. */
+/* Discriminator head after fc.0 (+LeakyReLU) (h [n][o] fp32): s[n] = sigmoid(h.w2 + b2) (rfb_esrgan.py:59-60),
+ * or h.w2 + b2 with sigmoid = 0 (plain discriminator's classification.1, discriminator.py:40). */
+int climsr_d_head_fwd(const float* h, const float* w2, const float* b2, int n, int o, int sigmoid, float* s, void* stream);
+/* Head backward from ds[n]: dw2/db2/db0 (+)=; du0 = d(fc.0 pre-activation) as bf16 [n][o] and [o][n_pad]
+ * (slope = the LeakyReLU between fc.0 and the head; 1 = none). */
 int climsr_d_head_bwd(const float* h, const float* s, const float* ds, const float* w2, int n, int o, int n_pad, float slope,
-                      float* dw2, float* db2, float* db0, int accumulate, uint16_t* du0, uint16_t* du0_t, void* stream);
+                      int sigmoid, float* dw2, float* db2, float* db0, int accumulate, uint16_t* du0, uint16_t* du0_t,
+                      void* stream);
+/* nn.ReflectionPad2d(1) (discriminator.py:15,21): y [n][h+2][w+2][cstride] bf16 from x [n][h][w][cstride]. */
+int climsr_reflect_pad1_bf16(const uint16_t* x, int n, int h, int w, int cstride, uint16_t* y, void* stream);
+/* Its backward: g [n][h][w][c] fp32 = sum of the padded gradient gp [n][h+2][w+2][c] over the mirrored reads. */
+int climsr_reflect_pad1_bwd_f32(const float* gp, int n, int h, int w, int c, float* g, void* stream);
 /* Relativistic-average BCEWithLogits (pl_gan.py:33-38, 54-59): loss = (BCE(s_f-mean(s_r), t_fr) +
  * BCE(s_r-mean(s_f), t_rf))/2; with gscale (device scalar) also the gradients w.r.t. s_real/s_fake. */
 int climsr_relativistic_bce(const float* s_real, const float* s_fake, int n, float t_rf, float t_fr, float* loss,

@@ -105,3 +105,19 @@ def test_product_has_no_cpu_fallback():
     e = torch.zeros(1, 1, 32, 32)
     with pytest.raises(RuntimeError, match="GPU only"):
         g(x, e, e)
+
+
+def test_plain_discriminator_drop_in_keys():
+    """climsr_amd.models.discriminator.Discriminator has the reference's state_dict (discriminator.py:6-40)."""
+    import torch
+
+    from climsr_amd.models.discriminator import Discriminator
+    from oracle import climsr_ref as ref
+
+    d = Discriminator()
+    sd = d.state_dict()
+    shapes = ref.plain_discriminator_shapes()
+    assert set(sd) == set(shapes)
+    assert all(tuple(sd[k].shape) == tuple(shapes[k]) for k in sd)
+    with pytest.raises(RuntimeError, match="GPU only"):
+        d(torch.zeros(1, 1, 128, 128))
