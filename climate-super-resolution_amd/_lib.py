@@ -78,6 +78,7 @@ SIGNATURES = {
     "climsr_rdb_chain": (c_int, [P(ChainDesc), c_void_p]),
     "climsr_rdb_chain_kp": (c_int, [c_int]),
     "climsr_conv2d_fwd": (c_int, [P(ConvDesc), c_void_p, c_void_p, c_void_p, P(Epilogue), c_void_p, c_void_p]),
+    "climsr_conv2d_fwd_kernel": (ctypes.c_char_p, [P(ConvDesc), c_void_p, P(Epilogue)]),
     "climsr_conv2d_wgrad": (c_int, [P(ConvDesc), c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "climsr_conv2d_wgrad_reduce": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                                            c_void_p]),

@@ -26,6 +26,10 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
 }
 
+// dry run (climsr_conv2d_fwd_kernel): the dispatcher records the kernel it would launch instead of launching
+static thread_local bool g_dry = false;
+static thread_local char g_dry_name[96] = "";
+
 int check_launch(const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
@@ -88,10 +92,17 @@ extern "C" int climsr_version(void) { return 2; }
 // Convs with <= 16 outputs, 3x3 and <= 128 inputs (the residual dense block's conv1-4 and their pull data
 // gradients) run on conv_n16_kernel, whose packed K is tap-major with the channels padded to 32 per tap.
 static bool n16_shape(int in_c, int ks, int out_c) { return out_c <= 16 && ks == 3 && in_c <= 128; }
+static bool pw_disabled() {
+  static int v = getenv("CLIMSR_NO_PW") ? atoi(getenv("CLIMSR_NO_PW")) : 0;
+  return v != 0;
+}
+
+static bool pw_fits(int in_c, int ks, int out_c);
 
 extern "C" int climsr_conv_chunk_ex(int in_c, int ks, int out_c, int stride) {
   if (stride == 1 && n16_shape(in_c, ks, out_c))  // conv_n16: one chunk, padded to 32/64/128
     return in_c <= 32 ? 32 : (in_c <= 64 ? 64 : 128);
+  if (stride == 1 && pw_fits(in_c, ks, out_c)) return round_up(in_c, 8);  // conv_pw: the whole K in one chunk
   int cc = round_up(in_c, 8);
   FwdGeom g;
   while (cc > 8) {
@@ -824,6 +835,10 @@ __global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs
 
 template <int NCB>
 static int launch_n16(const FwdArgs& a, hipStream_t s) {
+  if (g_dry) {
+    snprintf(g_dry_name, sizeof(g_dry_name), "conv_n16_kernel<%d>", NCB);
+    return CLIMSR_OK;
+  }
   auto k = conv_n16_kernel<NCB>;
   size_t lds = (size_t)N16_TPH * N16_TPW * (NCB * 32 + 8) * 2;
   const size_t lds_w = (size_t)16 * (9 * NCB * 32 + 8) * 2;        // weight staging (aliased)
@@ -1193,12 +1208,253 @@ __global__ __launch_bounds__(256) void conv_co1_kernel(FwdArgs a) {
   if (a.aux) a.aux[pidx * a.aux_cs + a.aux_co] = f2bf(a.aux_scale * v);
 }
 
+// ------------------------------------------------------------------------------------------
+// Weights-resident persistent conv: one workgroup per CU stages the WHOLE packed weight matrix
+// (<= 64 output channels, one channel chunk) into LDS once and walks its share of the output tiles,
+// the next tile's input prefetched into registers while the current one is on the MFMA pipe.  For the
+// HR-resolution convs (HRconv / upconv1-2 with the upsample on load, srcnn.conv1 9x9 and conv2 5x5,
+// their data gradients, trunk_conv / conv_first) the generic kernel restages the weights for every
+// 256-pixel tile (8k tiles per launch at 256^2).  Stride 1 only; epilogue = the generic one.
+// ------------------------------------------------------------------------------------------
+constexpr int PW_PV = 12;  // prefetched 16 B input vectors per thread (tile <= 3072 vectors)
+
+struct PwGeom {
+  int mw, tph, tpw, ccp, kcpad, nvx;
+  size_t lds_tab, lds_w, lds_x, lds_ep, lds_total;
+};
+
+static bool pw_geom(const ClimsrConvDesc* d, int nt, int mw, PwGeom* g, int nw = 4) {
+  if (d->stride != 1 || d->cc < d->in_c) return false;
+  g->mw = mw;
+  g->tph = nw * mw + d->ks - 1;
+  g->tpw = TW + d->ks - 1;
+  g->ccp = d->cc + XPAD;
+  g->kcpad = round_up(d->ks * d->ks * d->cc, 32);
+  g->nvx = g->tph * g->tpw * (d->cc / 8);
+  g->lds_tab = ((size_t)(g->kcpad / 8) * 4 + 15) / 16 * 16;
+  g->lds_w = (size_t)nt * 16 * (g->kcpad + WPAD) * 2;
+  g->lds_x = (size_t)g->tph * g->tpw * g->ccp * 2;
+  g->lds_ep = (size_t)nw * mw * 16 * (nt * 16 + 4) * 4;
+  g->lds_total = g->lds_tab + g->lds_w + (g->lds_x > g->lds_ep ? g->lds_x : g->lds_ep);
+  return g->nvx <= 64 * nw * PW_PV && g->lds_total <= 160 * 1024;
+}
+
+static bool pw_fits(int in_c, int ks, int out_c) {
+  const int nt = fwd_nt(out_c);
+  if (out_c <= 16 || out_c > 64 || (nt != 2 && nt != 4)) return false;
+  ClimsrConvDesc d{};
+  d.in_c = round_up(in_c, 8);
+  d.cc = d.in_c;
+  d.ks = ks;
+  d.stride = 1;
+  PwGeom g;
+  return pw_geom(&d, nt, 2, &g, 4);
+}
+
+template <int NW, int MW, int NT, bool RF, int PV>
+__global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
+  constexpr int NTHR = 64 * NW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int* tab = (int*)smem;
+  uint16_t* ws = (uint16_t*)(smem + a.lds_tab);
+  uint16_t* xs = (uint16_t*)(smem + a.lds_tab + a.lds_x);  // lds_x carries the weight region size here
+  float* ebase = (float*)xs;                               // epilogue staging aliases the input tile
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
+  const int wpitch = a.kcpad + WPAD;
+  const int ks2 = a.ks * a.ks;
+  for (int i = tid; i < a.kcpad / 8; i += NTHR) {  // tap table (one chunk)
+    const int kr = i * 8;
+    int tap = kr / a.cc, c = kr - tap * a.cc;
+    if (tap >= ks2) { tap = 0; c = 0; }
+    const int ky = tap / a.ks, kx = tap - ky * a.ks;
+    tab[i] = (ky * a.tpw + kx) * a.ccp + c;
+  }
+  {  // the whole weight matrix, once
+    const int wvec_row = a.kcpad / 8;
+    for (int v = tid; v < NT * 16 * wvec_row; v += NTHR) {
+      const int r = v / wvec_row, kv = v - r * wvec_row;
+      *(uint4*)(ws + r * wpitch + kv * 8) = *(const uint4*)(a.w + (long)r * a.kpk + kv * 8);
+    }
+  }
+  const int ufac = a.up, upsh = a.up == 2 ? 1 : 0;
+  const int lh = a.in_h * ufac, lw = a.in_w * ufac;
+  const int cvec = a.cc / 8;
+  const int nvec_x = a.tph * a.tpw * cvec;
+  const int x_dp = NTHR / cvec, x_dc = NTHR - x_dp * cvec;
+  const int x_dy = x_dp / a.tpw, x_dx = x_dp - x_dy * a.tpw;
+  const int x_pix0 = tid / cvec, x_cg0 = tid - x_pix0 * cvec;
+  const int x_ty0 = x_pix0 / a.tpw, x_tx0 = x_pix0 - x_ty0 * a.tpw;
+  const int ntiles = a.tiles_x * a.tiles_y * a.n;
+
+  uint4 pre[PV];
+  auto issue = [&](int tile) {
+    int tt = tile;
+    const int tx = tt % a.tiles_x;
+    tt /= a.tiles_x;
+    const int ty = tt % a.tiles_y;
+    const int nimg = tt / a.tiles_y;
+    const int iy0 = ty * (NW * MW) - a.pad, ix0 = tx * TW - a.pad;
+    int ty_ = x_ty0, tx_ = x_tx0, cg = x_cg0;
+#pragma unroll
+    for (int i = 0; i < PV; ++i) {
+      pre[i] = make_uint4(0, 0, 0, 0);
+      if (tid + NTHR * i < nvec_x) {
+        const int iy = iy0 + ty_, ix = ix0 + tx_;
+        const int c = cg * 8;
+        if (!(a.ablate & 1) && iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c)
+          pre[i] = *(const uint4*)(a.x + (((long)nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + c);
+      }
+      cg += x_dc;
+      tx_ += x_dx;
+      ty_ += x_dy;
+      if (cg >= cvec) { cg -= cvec; ++tx_; }
+      if (tx_ >= a.tpw) { tx_ -= a.tpw; ++ty_; }
+    }
+  };
+  if (blockIdx.x < ntiles) issue(blockIdx.x);
+
+  int pixbase[MW];
+#pragma unroll
+  for (int m = 0; m < MW; ++m) pixbase[m] = ((wave * MW + m) * a.tpw + col) * a.ccp;
+
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    int tt = tile;
+    const int tx = tt % a.tiles_x;
+    tt /= a.tiles_x;
+    const int ty = tt % a.tiles_y;
+    const int nimg = tt / a.tiles_y;
+    const int ox0 = tx * TW, oy0 = ty * (NW * MW);
+    __syncthreads();  // previous tile's epilogue reads of the aliased region are done
+    {
+      int ty_ = x_ty0, tx_ = x_tx0, cg = x_cg0;
+#pragma unroll
+      for (int i = 0; i < PV; ++i) {
+        if (tid + NTHR * i < nvec_x) *(uint4*)(xs + (ty_ * a.tpw + tx_) * a.ccp + cg * 8) = pre[i];
+        cg += x_dc;
+        tx_ += x_dx;
+        ty_ += x_dy;
+        if (cg >= cvec) { cg -= cvec; ++tx_; }
+        if (tx_ >= a.tpw) { tx_ -= a.tpw; ++ty_; }
+      }
+    }
+    if (tile + (int)gridDim.x < ntiles) issue(tile + gridDim.x);  // lands while this tile computes
+    __syncthreads();
+    f32x4 acc[MW][NT];
+#pragma unroll
+    for (int m = 0; m < MW; ++m)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[m][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (!(a.ablate & 2)) {
+      const int nks = a.kcpad / 32;
+      for (int kstep = 0; kstep < nks; ++kstep) {
+        const int off = tab[kstep * 4 + g];
+        bf16x8 af[NT], bfr[MW];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) af[t] = *(const bf16x8*)(ws + (t * 16 + col) * wpitch + kstep * 32 + g * 8);
+#pragma unroll
+        for (int m = 0; m < MW; ++m) bfr[m] = *(const bf16x8*)(xs + pixbase[m] + off);
+#pragma unroll
+        for (int m = 0; m < MW; ++m)
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bfr[m], acc[m][t], 0, 0, 0);
+      }
+    }
+    if (a.ablate & 4) {
+      if (acc[0][0][0] == 123.f) ((float*)a.y)[0] = 0.f;
+      continue;
+    }
+    const int ox = ox0 + col;
+    if (a.down2) {  // 2x2 sum (data gradient of the nearest upsample): rows (m, m+1), columns via lane ^ 1
+      const int dh = a.out_h >> 1, dw = a.out_w >> 1;
+      const bool mask = a.act == 3 || a.act == 4;
+#pragma unroll
+      for (int m = 0; m < MW; m += 2) {
+        const int oy = oy0 + wave * MW + m;
+        const long pidx = ((long)nimg * dh + (oy >> 1)) * dw + (ox >> 1);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          float v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float sm = acc[m][t][i] + acc[m + 1][t][i];
+            sm += __shfl_xor(sm, 1);
+            v[i] = sm;
+          }
+          const int co = t * 16 + g * 4;
+          if ((col & 1) || oy >= a.out_h || ox >= a.out_w) continue;
+          const long ob = pidx * a.out_cs + a.out_co + co;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (co + i >= a.out_c) continue;
+            float x = v[i];
+            if (mask) x = ep_res(x, a.act, a.slope, true, res_at(a.res1, false, pidx * a.r1_cs + a.r1_co + co + i), 1.f, 1.f, false, 0.f,
+                                 1.f, 1.f);
+            if (a.out_mode == 0) ((uint16_t*)a.y)[ob + i] = f2bf(x);
+            else if (a.out_mode == 2) ((float*)a.y)[ob + i] += x;
+            else ((float*)a.y)[ob + i] = x;
+            if (a.aux) a.aux[pidx * a.aux_cs + a.aux_co + co + i] = f2bf(a.aux_scale * x);
+          }
+        }
+      }
+      continue;
+    }
+    constexpr int EPP = NT * 16 + 4;
+    float* eb = ebase + wave * (MW * 16 * EPP);
+    __syncthreads();  // all waves are done reading the input tile (the staging region aliases it)
+#pragma unroll
+    for (int m = 0; m < MW; ++m)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) *(f32x4*)(eb + (m * 16 + col) * EPP + t * 16 + g * 4) = acc[m][t];
+    __syncthreads();
+    store_tile_lds<RF, MW * 16, NT * 16, 64>(a, eb, EPP, lane, nimg, oy0 + wave * MW, ox0, 0);
+  }
+}
+
+template <int NW, int MW, int NT, int PV>
+static int launch_pw(const FwdArgs& a0, const PwGeom& g, hipStream_t s) {
+  if (g_dry) {
+    snprintf(g_dry_name, sizeof(g_dry_name), "conv_pw_kernel<%d, %d, %d, %s, %d>", NW, MW, NT, a0.res_f32 ? "true" : "false", PV);
+    return CLIMSR_OK;
+  }
+  FwdArgs a = a0;
+  a.tph = g.tph; a.tpw = g.tpw; a.ccp = g.ccp; a.kcpad = g.kcpad;
+  a.tiles_x = ceil_div(a.out_w, TW);
+  a.tiles_y = ceil_div(a.out_h, NW * MW);
+  a.lds_tab = (int)g.lds_tab;
+  a.lds_x = (int)g.lds_w;  // offset of the input tile = tab + weights
+  auto k = a.res_f32 ? conv_pw_kernel<NW, MW, NT, true, PV> : conv_pw_kernel<NW, MW, NT, false, PV>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)conv_pw_kernel<NW, MW, NT, true, PV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void*)conv_pw_kernel<NW, MW, NT, false, PV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr_set = true;
+  }
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (ncu <= 0) ncu = 256;
+  }
+  const int ntiles = a.tiles_x * a.tiles_y * a.n;
+  const int grid = ntiles < ncu ? ntiles : ncu;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(64 * NW), g.lds_total, s, a);
+  return check_launch("conv2d_fwd (pw)");
+}
+
 template <int MW, int NT>
 static int launch_fwd(const FwdArgs& a, int ncob, size_t lds, hipStream_t s) {
   dim3 grid(a.tiles_x * a.tiles_y * a.n, ncob);
   const size_t lds_ep = (size_t)4 * MW * 16 * (NT * 16 + 4) * 4;  // epilogue staging (aliases the operands)
   if (lds_ep > lds) lds = lds_ep;
   constexpr int MV = NT == 1 ? 6 : (NT == 2 ? 8 : 4);
+  if (g_dry) {
+    snprintf(g_dry_name, sizeof(g_dry_name), "conv_fwd_kernel<%d, %d, %s, %d>", MW, NT, a.res_f32 ? "true" : "false", MV);
+    return CLIMSR_OK;
+  }
   auto k = a.res_f32 ? conv_fwd_kernel<MW, NT, true, MV> : conv_fwd_kernel<MW, NT, false, MV>;
   static bool attr_set = false;
   if (!attr_set) {
@@ -1265,6 +1521,10 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
     a.tiles_x = ceil_div(d->out_w, 16);
     a.tiles_y = ceil_div(d->out_h, 16);
     size_t lds = (size_t)(15 + d->ks) * (15 + d->ks) * (CO1_CC + 8) * 2 + (size_t)d->ks * d->ks * CO1_CC * 2;
+    if (g_dry) {
+      snprintf(g_dry_name, sizeof(g_dry_name), "conv_co1_kernel");
+      return CLIMSR_OK;
+    }
     hipLaunchKernelGGL(conv_co1_kernel, dim3(a.tiles_x * a.tiles_y * a.n), dim3(256), lds, s, a);
     return check_launch("conv2d_fwd (co1)");
   }
@@ -1290,6 +1550,17 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
       default: return launch_co64<4>(a, s);
     }
   }
+  {  // weights-resident persistent kernel for one-chunk convs with 17..64 outputs (large-pixel-count layers)
+    const int nt = fwd_nt(d->out_c);
+    const long npx = (long)d->n * d->out_h * d->out_w;
+    PwGeom pg;
+    if (ncob == 1 && (nt == 4 || nt == 2) && d->up != -2 && npx >= 4096 && !pw_disabled()) {
+      // 8 waves x 2 rows (two waves per SIMD) when the LDS allows, else 4 waves x 2 rows
+      if (pw_geom(d, nt, 2, &pg, 8) && pg.nvx <= 512 * 7 && d->out_h >= 16)
+        return nt == 4 ? launch_pw<8, 2, 4, 7>(a, pg, s) : launch_pw<8, 2, 2, 7>(a, pg, s);
+      if (pw_geom(d, nt, 2, &pg, 4)) return nt == 4 ? launch_pw<4, 2, 4, 12>(a, pg, s) : launch_pw<4, 2, 2, 12>(a, pg, s);
+    }
+  }
   if (g.lds_total > 160 * 1024) {
     set_error("conv2d_fwd: LDS %zu exceeds 160 KiB (cc=%d)", g.lds_total, d->cc);
     return CLIMSR_EINVAL;
@@ -1300,6 +1571,15 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
     case 2: return launch_fwd<2, 2>(a, ncob, g.lds_total, s);
     default: return launch_fwd<2, 4>(a, ncob, g.lds_total, s);
   }
+}
+
+extern "C" const char* climsr_conv2d_fwd_kernel(const ClimsrConvDesc* d, const float* bias, const ClimsrEpilogue* ep) {
+  static uint16_t dummy[8];
+  g_dry = true;
+  g_dry_name[0] = 0;
+  const int rc = climsr_conv2d_fwd(d, dummy, dummy, bias, ep, dummy, nullptr);
+  g_dry = false;
+  return rc == CLIMSR_OK ? g_dry_name : "";
 }
 
 // ------------------------------------------------------------------------------------------

@@ -147,6 +147,9 @@ int climsr_rdb_chain_kp(int level);
  * transpose_flip weights, its data gradient (stride 1). */
 int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, const uint16_t* wpk, const float* bias,
                       const ClimsrEpilogue* ep, void* y, void* stream);
+/* Name of the kernel climsr_conv2d_fwd launches for these arguments (as rocprof reports it; "" if invalid).
+ * Launches nothing; used to label per-kernel timings and PMC traffic. */
+const char* climsr_conv2d_fwd_kernel(const ClimsrConvDesc* d, const float* bias, const ClimsrEpilogue* ep);
 
 /* Weight (+ bias) gradient partials (d->in_c may be 4 = "at most 4 real input channels", which packs
  * 4 taps x 4 channels per MFMA fragment; the input buffer still has a multiple-of-8 channel stride): partial[split][out_c_pad16][in_c*ks*ks] (OIHW order) and
