@@ -860,6 +860,7 @@ static int launch_n16(const FwdArgs& a, hipStream_t s) {
   static int per_cu = 0;
   if (!per_cu) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, 256, lds) != hipSuccess || per_cu <= 0) per_cu = 2;
+    if (getenv("CLIMSR_N16_PER_CU")) per_cu = atoi(getenv("CLIMSR_N16_PER_CU"));  // tuning experiments
   }
   int ntiles = a.tiles_x * a.tiles_y * a.n;
   int grid = ntiles < per_cu * ncu ? ntiles : per_cu * ncu;
