@@ -63,6 +63,23 @@ class PullPackDesc(ctypes.Structure):
         (n, ctypes.c_int32) for n in ("nseg", "out_c", "in_c", "ks", "cc", "ci_off")]
 
 
+class TileDesc(ctypes.Structure):
+    _fields_ = [(n, c_void_p) for n in ("hr_raw", "elev_raw", "hr_min", "hr_max", "elev_minmax", "xform", "lr", "hr", "elev",
+                                        "mask", "nearest", "elev_lr", "hr_lr")] + [
+        (n, c_double) for n in ("range_a", "range_b", "eps", "nan_sub", "zs_hr_mean", "zs_hr_std", "zs_hr_nan_sub",
+                                "zs_elev_mean", "zs_elev_std", "zs_elev_nan_sub")] + [("elev_missing", c_float)] + [
+        (n, ctypes.c_int32) for n in ("method", "n", "h", "w", "scale", "lr_c", "srcnn", "use_elev", "use_mask")]
+
+
+SR_METRICS = 17
+
+
+class MetricsDesc(ctypes.Structure):
+    _fields_ = [(n, c_void_p) for n in ("sr", "hr", "original", "mask", "min", "max", "workspace", "out")] + [
+        (n, c_double) for n in ("range_a", "range_b", "eps", "zs_mean", "zs_std")] + [("acc_eps", c_float * 8)] + [
+        (n, ctypes.c_int32) for n in ("n", "h", "w", "method")]
+
+
 P = ctypes.POINTER
 # name -> (restype, argtypes); must match include/climsr_hip.h exactly (tests/test_abi.py checks the symbols)
 SIGNATURES = {
@@ -122,6 +139,12 @@ SIGNATURES = {
     "climsr_bn_inference": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_int, c_float,
                                     c_void_p, c_void_p]),
     "climsr_increment_i64": (c_int, [c_void_p, c_void_p]),
+    "climsr_tile_minmax_f32": (c_int, [c_void_p, c_int, c_int64, c_float, c_int, c_void_p, c_void_p]),
+    "climsr_tile_prepare": (c_int, [P(TileDesc), c_void_p]),
+    "climsr_resize_cubic_f32": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p]),
+    "climsr_sr_metrics_workspace": (c_size_t, []),
+    "climsr_sr_metrics": (c_int, [P(MetricsDesc), c_void_p]),
+    "climsr_regression_accuracy_update": (c_int, [c_void_p, c_void_p, c_int64, c_float, c_void_p, c_void_p]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

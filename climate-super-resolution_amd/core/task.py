@@ -21,6 +21,7 @@ import torch
 from torch import Tensor
 
 from ..losses.l1 import L1Loss
+from ..metrics.sr_metrics import SRMetrics
 from .instantiator import HydraInstantiator
 from .optim import AdamW
 
@@ -54,6 +55,10 @@ class TaskSuperResolutionModule(_Base):
             raise NotImplementedError("stand-alone SRCNN + MSE task is outside this build's scope (SURVEY §2)")
         self.loss = L1Loss()  # task.py:141
         self.logged: Dict[str, Tensor] = {}
+        zs = dict(getattr(self.hparams, "standardization_stats", None) or {})
+        self.metrics = SRMetrics(normalization_method=getattr(self.hparams, "normalization_method", "minmax"),
+                                 normalization_range=tuple(getattr(self.hparams, "normalization_range", (-1.0, 1.0))),
+                                 zscore_mean=zs.get("mean", 0.0), zscore_std=zs.get("std", 1.0))
 
     # -- Lightning-compat helpers (no host sync: values are kept as device tensors)
     if _Base is torch.nn.Module:
@@ -92,3 +97,31 @@ class TaskSuperResolutionModule(_Base):
             opts.append(opt)
             scheds.append({"scheduler": sch, "interval": "step"})
         return opts, scheds
+
+    # -- validation / test (task.py:262-294, 336-391): metrics fused on device (climsr_amd.metrics)
+    def common_val_test_step(self, batch: Any, prefix: str = "val") -> Dict[str, Tensor]:
+        original, mask = batch["original_data"], batch["mask"]
+        hr, sr = self.common_step(batch)
+        sr_copy = sr.detach().clone()
+        metric_dict = self.metrics(sr.detach(), hr, original, mask, batch.get("min"), batch.get("max"), prefix=prefix)
+        land = mask.bool()
+        hr.masked_fill_(~land, 0.0)  # the reference masks the batch's hr in place (task.py:289-290)
+        original.masked_fill_(~land, 0.0)
+        metric_dict["sr"] = sr_copy
+        return metric_dict
+
+    def validation_step(self, batch: Any, batch_idx: int, dataloader_idx: Optional[int] = None) -> Dict[str, Tensor]:
+        """pl_generator_pre_training.py:35-50."""
+        metric_dict = self.common_val_test_step(batch, prefix="val")
+        metric_dict.pop("sr", None)
+        self.log_dict(metric_dict, prog_bar=False, on_step=False, on_epoch=True)
+        return metric_dict
+
+    def test_step(self, batch: Any, batch_idx: int, dataloader_idx: Optional[int] = None) -> Dict[str, Tensor]:
+        """pl_generator_pre_training.py:52-64."""
+        return self.common_val_test_step(batch, prefix="test")
+
+    def validation_epoch_end(self, outputs: List[Any]) -> None:
+        """hp_metric = mean of the epoch's val/rmse (task.py:387-391)."""
+        hp_metric = torch.stack([o["val/rmse"] for o in outputs]).mean()
+        self.log("hp_metric", hp_metric)

@@ -1,5 +1,5 @@
 """GAN task (mirror of climsr/task/pl_gan.py:12-97) on the native G, D, VGG and losses."""
-from typing import Any, Dict, Tuple
+from typing import Any, Dict, Optional, Tuple
 
 import torch
 from torch import Tensor
@@ -53,3 +53,15 @@ class GANLightningModule(TaskSuperResolutionModule):
             loss_d = self.loss_d(hr, sr)
             self.log("train/loss_D", loss_d, prog_bar=True, on_step=True, on_epoch=False)
             return {"loss": loss_d, "log": {"train/loss_D": loss_d}}
+
+    def validation_step(self, batch: Any, batch_idx: int, dataloader_idx: Optional[int] = None) -> Dict[str, Any]:
+        """pl_gan.py:99-130: metrics, then loss_g on the (mask-zeroed) hr and the unmasked sr."""
+        hr = batch["hr"]
+        metric_dict = self.common_val_test_step(batch)
+        with torch.no_grad():
+            perceptual_loss, adversarial_loss, _, loss_g = self.loss_g(hr, metric_dict["sr"])
+        metric_dict.pop("sr", None)
+        metric_dict.update({"val/perceptual_loss": perceptual_loss, "val/adversarial_loss": adversarial_loss,
+                            "val/loss_G": loss_g})
+        self.log_dict(metric_dict, on_step=False, on_epoch=True)
+        return metric_dict

@@ -274,6 +274,79 @@ int climsr_l1_loss_bf16(const uint16_t* a, const uint16_t* b, int64_t n, double*
 /* y = bf16(x) elementwise (MFMA copy of fp32 master weights). */
 int climsr_f32_to_bf16(const float* x, int64_t n, uint16_t* y, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * On-device tile pipeline.  Replaces the per-sample CPU work of
+ * ClimateDataset.__getitem__ (climsr/data/sr/climate_dataset.py:220-275), _get_training_sample
+ * (:144-189), _get_val_test_sample (:191-218), _common_to_tensor / _concat_if_needed (:95-142) and
+ * MinMaxScaler / StandardScaler._normalize (climsr/data/normalization.py:37-61, 99-113) for a batch
+ * of raw tiles already in HBM.  All tensors are contiguous fp32 NCHW ([n][1][h][w] per plane).
+ * --------------------------------------------------------------------------------------------- */
+typedef struct {
+  const float* hr_raw;       /* [n][h][w] raw tile (NaN = no data / sea) */
+  const float* elev_raw;     /* [n][h][w] raw elevation (== elev_missing -> NaN); NULL if !use_elev */
+  const double* hr_min;      /* [n] per-tile (or global) min / max, float64 as in the stats tables (method 0) */
+  const double* hr_max;
+  const float* elev_minmax;  /* [n][2] nanmin / nanmax of the elevation tile (climsr_tile_minmax_f32; method 0) */
+  const int32_t* xform;      /* [n] bit0 np.flipud, bit1 np.fliplr, bits2-3 np.rot90 factor (applied in that order);
+                                NULL = identity (val / test) */
+  float* lr;                 /* [n][lr_c][h/scale][w/scale]; SRCNN: [n][lr_c][h][w] */
+  float* hr;                 /* [n][1][h][w] normalised HR */
+  float* elev;               /* [n][1][h][w] normalised elevation, or NULL */
+  float* mask;               /* [n][1][h][w] land mask 1/0 (~isnan(original)), or NULL */
+  float* nearest;            /* [n][1][h][w] nearest upscale of the LR temperature (val/test `nearest`), or NULL */
+  float* elev_lr;            /* [n][1][h/scale][w/scale] (val/test `elevation_lr`), or NULL */
+  float* hr_lr;              /* [n][1][h/scale][w/scale] LR temperature plane (input of the `cubic` upscale), or NULL */
+  double range_a, range_b;   /* MinMaxScaler feature_range (normalize_range, default (-1, 1)) */
+  double eps;                /* 1e-8 (both scalers) */
+  double nan_sub;            /* MinMaxScaler nan_substitution (0.0) */
+  double zs_hr_mean, zs_hr_std, zs_hr_nan_sub;      /* StandardScaler (method 1); nan_sub applied only if != 0 */
+  double zs_elev_mean, zs_elev_std, zs_elev_nan_sub;
+  float elev_missing;        /* consts.world_clim.elevation_missing_indicator = -32768 */
+  int32_t method;            /* 0 minmax, 1 zscore, 2 none */
+  int32_t n, h, w, scale;    /* h, w multiples of scale; h == w when xform is given */
+  int32_t lr_c;              /* 1 + use_elev + use_mask */
+  int32_t srcnn, use_elev, use_mask;
+} ClimsrTileDesc;
+
+/* out[2t], out[2t+1] = np.nanmin / np.nanmax of tile t (count floats each), treating value == missing as NaN
+ * when use_missing (MinMaxScaler._normalize without min/max, normalization.py:45-50).  All-NaN -> NaN. */
+int climsr_tile_minmax_f32(const float* x, int n, int64_t count, float missing, int use_missing, float* out, void* stream);
+/* The fused flip / rot90 / normalise / mask / decimate / concat pass.  One launch per batch. */
+int climsr_tile_prepare(const ClimsrTileDesc* d, void* stream);
+/* cv2.resize(..., INTER_CUBIC) of fp32 planes [n][sh][sw] -> [n][dh][dw] (the val/test `cubic` item,
+ * climate_dataset.py:195): A = -0.75, replicate border, horizontal then vertical pass. */
+int climsr_resize_cubic_f32(const float* src, int n, int sh, int sw, float* dst, int dh, int dw, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Validation / test metrics on device: TaskSuperResolutionModule.
+ * common_val_test_step + compute_metrics (climsr/core/task.py:262-294, 336-372) with the torchmetrics
+ * definitions the reference instantiates (task.py:296-323) and RegressionAccuracy
+ * (climsr/metrics/regression_accuracy.py:6-22).  Deterministic: fixed-order fp64 block partials.
+ * out[CLIMSR_SR_METRICS] = acc@{eps[0..7]}, psnr, ssim, mae, mse, rmse, mape, smape, r2, l1(normalised).
+ * --------------------------------------------------------------------------------------------- */
+#define CLIMSR_SR_METRICS 17
+typedef struct {
+  const float* sr;         /* [n][1][h][w] normalised generator output */
+  const float* hr;         /* [n][1][h][w] normalised HR */
+  const float* original;   /* [n][1][h][w] raw HR (NaN at sea; zeroed by the mask like task.py:291) */
+  const float* mask;       /* [n][1][h][w] land mask (0 = sea) */
+  const double* min;       /* [n] per-sample min / max of the batch (method 0 denormalisation) */
+  const double* max;
+  double* workspace;       /* climsr_sr_metrics_workspace() bytes */
+  double* out;             /* [CLIMSR_SR_METRICS] */
+  double range_a, range_b, eps;
+  double zs_mean, zs_std;  /* method 1: StandardScaler._denormalize */
+  float acc_eps[8];        /* RegressionAccuracy eps list (task.py:297-304) */
+  int32_t n, h, w;         /* h, w >= 11 (SSIM window) */
+  int32_t method;          /* 0 minmax, 1 zscore, 2 identity */
+} ClimsrMetricsDesc;
+
+size_t climsr_sr_metrics_workspace(void);
+int climsr_sr_metrics(const ClimsrMetricsDesc* d, void* stream);
+/* RegressionAccuracy.update: counts[0] += #(|p - t| <= eps) (float32), counts[1] += n.  int64 device counters. */
+int climsr_regression_accuracy_update(const float* preds, const float* target, int64_t n, float eps, int64_t* counts,
+                                      void* stream);
+
 #ifdef __cplusplus
 }
 #endif

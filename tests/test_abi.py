@@ -60,6 +60,33 @@ def test_struct_layouts_match_header(lib):
     assert ctypes.sizeof(_lib.PackDesc) == 2 * 8 + 8 * 4
 
 
+STRUCTS = {"ConvDesc": "ClimsrConvDesc", "Epilogue": "ClimsrEpilogue", "PackDesc": "ClimsrPackDesc",
+           "ReduceDesc": "ClimsrReduceDesc", "ChainDesc": "ClimsrChainDesc", "PullPackDesc": "ClimsrPullPackDesc",
+           "TileDesc": "ClimsrTileDesc", "MetricsDesc": "ClimsrMetricsDesc"}
+
+
+def test_struct_offsets_match_gcc(lib, tmp_path):
+    """Every ctypes mirror has the size and field offsets gcc gives the header's C struct."""
+    from climsr_amd import _lib
+
+    lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "climsr_hip.h"', "int main(void) {"]
+    for py, c in STRUCTS.items():
+        lines.append(f'printf("{py} size %zu\\n", sizeof({c}));')
+        for f in getattr(_lib, py)._fields_:
+            lines.append(f'printf("{py} {f[0]} %zu\\n", offsetof({c}, {f[0]}));')
+    lines += ["return 0;", "}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.dirname(HEADER), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    for row in filter(None, out):
+        py, field, val = row.split()
+        cls = getattr(_lib, py)
+        got = ctypes.sizeof(cls) if field == "size" else getattr(cls, field).offset
+        assert got == int(val), f"{py}.{field}: ctypes {got} != C {val}"
+
+
 def test_geometry_helpers(lib):
     assert lib.climsr_version() >= 1
     # chunking keeps the staged LDS tile within budget; packed K is a multiple of 32 per chunk
