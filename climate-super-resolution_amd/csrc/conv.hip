@@ -661,6 +661,26 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
 constexpr int N16_TH = 8;
 constexpr int N16_TPH = N16_TH + 2, N16_TPW = TW + 2;
 
+// Persistent tile walk, XCD-aware.  Workgroups are dispatched round-robin over the 8 XCDs and each XCD
+// has its own L2, so block b walks a contiguous span of tiles owned by XCD b % 8: tiles that run at the
+// same time on one XCD are spatial neighbours and share their input halo rows in that L2.
+struct TileWalk {
+  int first, step, end;
+  __device__ explicit TileWalk(int ntiles) {
+    const int grid = (int)gridDim.x, b = (int)blockIdx.x;
+    if (grid % 8 == 0 && grid >= 64) {
+      const int span = (ntiles + 7) / 8, xcd = b % 8;
+      first = xcd * span + b / 8;
+      step = grid / 8;
+      end = min(ntiles, (xcd + 1) * span);
+    } else {
+      first = b;
+      step = grid;
+      end = ntiles;
+    }
+  }
+};
+
 static int n16_ncb(int in_c) { return in_c <= 32 ? 1 : (in_c <= 64 ? 2 : 4); }
 
 template <int NCB>
@@ -673,17 +693,6 @@ __global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
   const int cb = wave % NCB, rg = wave / NCB;
   const int cvec = a.in_c / 8;
-
-  // this wave's A fragments (channel block cb, 9 taps), staged through LDS once per workgroup
-  constexpr int WROW = 9 * CINP + 8;
-  for (int v = tid; v < 16 * 9 * CV; v += 256) {
-    const int r = v / (9 * CV), k = v - r * (9 * CV);
-    *(uint4*)(xs + r * WROW + k * 8) = *(const uint4*)(a.w + (long)r * a.kpk + k * 8);
-  }
-  __syncthreads();
-  bf16x8 af[9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t) af[t] = *(const bf16x8*)(xs + col * WROW + t * CINP + cb * 32 + g * 8);
 
   float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
   const int co = g * 4;
@@ -720,9 +729,15 @@ __global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs
         pre[i] = *(const uint4*)(a.x + (((long)nimg * a.in_h + iy) * a.in_w + ix) * a.in_cs + a.in_co + j * 8);
     }
   };
-  if (blockIdx.x < ntiles) issue(blockIdx.x);
+  const TileWalk walk(ntiles);
+  if (walk.first < walk.end) issue(walk.first);
+  // this wave's A fragments (channel block cb, 9 taps; packed rows are tap-major with CINP channels per
+  // tap), loaded once per workgroup straight into VGPRs while the first tile's input is in flight
+  bf16x8 af[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) af[t] = *(const bf16x8*)(a.w + (long)col * a.kpk + t * CINP + cb * 32 + g * 8);
 
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  for (int tile = walk.first; tile < walk.end; tile += walk.step) {
     int tt = tile;
     const int tx = tt % a.tiles_x;
     tt /= a.tiles_x;
@@ -737,7 +752,7 @@ __global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs
         if (v < NPIX * CV) *(uint4*)(xs + (v / CV) * P + (v % CV) * 8) = pre[i];
       }
     }
-    if (tile + (int)gridDim.x < ntiles) issue(tile + gridDim.x);  // lands while this tile computes
+    if (tile + walk.step < walk.end) issue(tile + walk.step);  // lands while this tile computes
     __syncthreads();
     f32x4 acc[MW];
 #pragma unroll
@@ -841,9 +856,7 @@ static int launch_n16(const FwdArgs& a, hipStream_t s) {
   }
   auto k = conv_n16_kernel<NCB>;
   size_t lds = (size_t)N16_TPH * N16_TPW * (NCB * 32 + 8) * 2;
-  const size_t lds_w = (size_t)16 * (9 * NCB * 32 + 8) * 2;        // weight staging (aliased)
   const size_t lds_p = (size_t)NCB * N16_TH * 64 * 16;             // partial sums (aliased)
-  if (lds_w > lds) lds = lds_w;
   if (lds_p > lds) lds = lds_p;
   static bool attr_set = false;
   if (!attr_set) {
@@ -1116,6 +1129,129 @@ static int launch_co64(const FwdArgs& a, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------------------
+// Single-output-channel conv on MFMA (conv_last 64->1 3x3, srcnn.conv3 32->1 5x5 and the data gradient
+// of srcnn.conv1 w.r.t. its first input channel, 64->1 9x9).  The horizontal taps go into the MFMA N
+// dimension: per output row y and input column x',
+//     T[y][x'][kx] = sum_{ky, ci} x[y + ky - R][x'][ci] * w[ky][kx][ci]        (M = x', N = kx, K = ky x ci)
+//     out[y][x]    = sum_kx T[y][x + kx - R][kx]                               (shift-sum through LDS)
+// so the 16-wide N tile carries KS useful columns instead of 1 (KS/16 vs 1/16 of the MFMA).  A wave
+// computes 4 output rows x 64 columns (5 M-fragments of x'), streaming its 4 + KS - 1 input rows straight
+// from global memory (16 B per lane, next row in flight during the current row's MFMAs); every input row
+// feeds the up-to-4 output rows it touches.  Weights sit in VGPRs for the whole wave.
+// ------------------------------------------------------------------------------------------
+constexpr int CO1M_NF = 5, CO1M_COLS = 64, CO1M_ROWS = 4;
+
+static bool co1m_shape(const ClimsrConvDesc* d) {
+  return d->out_c == 1 && d->stride == 1 && d->up == 1 && (d->ks == 3 || d->ks == 5 || d->ks == 9) && d->pad == d->ks / 2 &&
+         d->in_c <= 64 && d->in_c % 8 == 0 && d->cc % 8 == 0 && d->out_h == d->in_h && d->out_w == d->in_w;
+}
+
+template <int KS, int NCH>
+__global__ __launch_bounds__(256, 2) void conv_co1m_kernel(FwdArgs a) {
+  constexpr int R = KS / 2, NR = CO1M_ROWS + KS - 1;
+  __shared__ float sc[4][CO1M_NF * 16][17];  // per-wave T rows (x' x kx), padded pitch
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
+  const int x0 = blockIdx.x * CO1M_COLS, y0 = (blockIdx.y * 4 + wave) * CO1M_ROWS, nimg = blockIdx.z;
+  // B fragments: B[k = ci][n = kx] of tap row ky, channel block c (packed row 0: k = (ci/cc)*kcpad + tap*cc + ci%cc)
+  bf16x8 bw[KS][NCH];
+#pragma unroll
+  for (int ky = 0; ky < KS; ++ky)
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int ci = c * 32 + g * 8;
+      bw[ky][c] = (bf16x8){};
+      if (col < KS && ci < a.in_c)
+        bw[ky][c] = *(const bf16x8*)(a.w + (long)(ci / a.cc) * a.kcpad + (ky * KS + col) * a.cc + (ci % a.cc));
+    }
+  f32x4 acc[CO1M_ROWS][CO1M_NF];
+#pragma unroll
+  for (int r = 0; r < CO1M_ROWS; ++r)
+#pragma unroll
+    for (int f = 0; f < CO1M_NF; ++f) acc[r][f] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 xa[2][CO1M_NF][NCH];
+  auto load_row = [&](int buf, int iyr) {
+    const int iy = y0 - R + iyr;
+    const bool rowok = iy >= 0 && iy < a.in_h;
+#pragma unroll
+    for (int f = 0; f < CO1M_NF; ++f) {
+      const int ix = x0 - R + f * 16 + col;
+      const bool ok = rowok && ix >= 0 && ix < a.in_w;
+      const long base = (((long)nimg * a.in_h + iy) * a.in_w + ix) * a.in_cs + a.in_co;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int ci = c * 32 + g * 8;
+        xa[buf][f][c] = (bf16x8){};
+        if (ok && ci < a.in_c) xa[buf][f][c] = *(const bf16x8*)(a.x + base + ci);
+      }
+    }
+  };
+  load_row(0, 0);
+#pragma unroll
+  for (int iyr = 0; iyr < NR; ++iyr) {
+    if (iyr + 1 < NR) load_row((iyr + 1) & 1, iyr + 1);
+#pragma unroll
+    for (int ky = 0; ky < KS; ++ky) {
+      const int r = iyr - ky;  // output row fed by input row iyr through tap row ky
+      if (r < 0 || r >= CO1M_ROWS) continue;
+#pragma unroll
+      for (int f = 0; f < CO1M_NF; ++f)
+#pragma unroll
+        for (int c = 0; c < NCH; ++c)
+          acc[r][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[iyr & 1][f][c], bw[ky][c], acc[r][f], 0, 0, 0);
+    }
+  }
+  // shift-sum: out[x0 + l] = sum_kx T[x' = l + kx][kx]; then the fused epilogue (same as conv_co1_kernel)
+  const float bias = a.bias ? a.bias[0] : 0.f;
+  const bool f1 = a.res_f32 & 1;
+#pragma unroll
+  for (int r = 0; r < CO1M_ROWS; ++r) {
+#pragma unroll
+    for (int f = 0; f < CO1M_NF; ++f)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sc[wave][f * 16 + g * 4 + i][col] = acc[r][f][i];
+    float v = 0.f;
+#pragma unroll
+    for (int kx = 0; kx < KS; ++kx) v += sc[wave][lane + kx][kx];
+    const int oy = y0 + r, ox = x0 + lane;
+    if (oy < a.out_h && ox < a.out_w) {
+      v = act_apply(v + bias, a.act, a.slope);
+      const long pidx = ((long)nimg * a.out_h + oy) * a.out_w + ox;
+      const float r1 = a.res1 ? res_at(a.res1, f1, pidx * a.r1_cs + a.r1_co) : 0.f;
+      v = ep_res(v, a.act, a.slope, a.res1 != nullptr, r1, a.alpha1, a.beta1, false, 0.f, 1.f, 1.f);
+      const long ob = pidx * a.out_cs + a.out_co;
+      if (a.out_mode == 0) ((uint16_t*)a.y)[ob] = f2bf(v);
+      else if (a.out_mode == 2) ((float*)a.y)[ob] += v;
+      else ((float*)a.y)[ob] = v;
+      if (a.aux) a.aux[pidx * a.aux_cs + a.aux_co] = f2bf(a.aux_scale * v);
+    }
+  }
+}
+
+template <int KS, int NCH>
+static int launch_co1m(const FwdArgs& a, hipStream_t s) {
+  if (g_dry) {
+    snprintf(g_dry_name, sizeof(g_dry_name), "conv_co1m_kernel<%d, %d>", KS, NCH);
+    return CLIMSR_OK;
+  }
+  dim3 grid(ceil_div(a.out_w, CO1M_COLS), ceil_div(a.out_h, 4 * CO1M_ROWS), a.n);
+  hipLaunchKernelGGL((conv_co1m_kernel<KS, NCH>), grid, dim3(256), 0, s, a);
+  return check_launch("conv2d_fwd (co1m)");
+}
+
+static int dispatch_co1m(const ClimsrConvDesc* d, const FwdArgs& a, hipStream_t s) {
+  const int nch = d->in_c <= 32 ? 1 : 2;
+  switch (d->ks * 10 + nch) {
+    case 31: return launch_co1m<3, 1>(a, s);
+    case 32: return launch_co1m<3, 2>(a, s);
+    case 51: return launch_co1m<5, 1>(a, s);
+    case 52: return launch_co1m<5, 2>(a, s);
+    case 91: return launch_co1m<9, 1>(a, s);
+    default: return launch_co1m<9, 2>(a, s);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // Single-output-channel conv on VALU (v_dot2_f32_bf16): conv_last (64->1), srcnn.conv3 (32->1) and
 // the data gradient of srcnn.conv1 w.r.t. its first input channel (64->1, 9x9).  With Cout = 1 an
 // MFMA tile would waste 15 of 16 rows; here each thread owns one output pixel of a 16x16 tile, the
@@ -1313,13 +1449,14 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
       if (tx_ >= a.tpw) { tx_ -= a.tpw; ++ty_; }
     }
   };
-  if (blockIdx.x < ntiles) issue(blockIdx.x);
+  const TileWalk walk(ntiles);
+  if (walk.first < walk.end) issue(walk.first);
 
   int pixbase[MW];
 #pragma unroll
   for (int m = 0; m < MW; ++m) pixbase[m] = ((wave * MW + m) * a.tpw + col) * a.ccp;
 
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  for (int tile = walk.first; tile < walk.end; tile += walk.step) {
     int tt = tile;
     const int tx = tt % a.tiles_x;
     tt /= a.tiles_x;
@@ -1339,7 +1476,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
         if (tx_ >= a.tpw) { tx_ -= a.tpw; ++ty_; }
       }
     }
-    if (tile + (int)gridDim.x < ntiles) issue(tile + gridDim.x);  // lands while this tile computes
+    if (tile + walk.step < walk.end) issue(tile + walk.step);  // lands while this tile computes
     __syncthreads();
     f32x4 acc[MW][NT];
 #pragma unroll
@@ -1518,6 +1655,8 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
   int rows = climsr_conv_packed_rows(d->out_c);
   int ncob = rows / (g.nt * 16);
   hipStream_t s = (hipStream_t)stream;
+  if (d->out_c == 1 && d->stride == 1 && d->up == 1 && !ep->down2 && !ep->res2 && co1m_shape(d) && !getenv("CLIMSR_NO_CO1M"))
+    return dispatch_co1m(d, a, s);
   if (d->out_c == 1 && d->stride == 1 && d->up == 1 && !ep->down2 && !ep->res2) {
     a.tiles_x = ceil_div(d->out_w, 16);
     a.tiles_y = ceil_div(d->out_h, 16);

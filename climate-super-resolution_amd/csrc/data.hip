@@ -13,6 +13,9 @@
 // MAE, MSE, RMSE, MAPE, SMAPE, R2 and the normalised L1, as one fused deterministic reduction (fixed
 // block partials, single-block final sum) plus a separable-Gaussian SSIM pass.  Nothing syncs the
 // host: SSIM's data range and constants are read from the first pass's device results.
+//
+// Built with -ffp-contract=off (Makefile): the normalisation reproduces numpy's one-rounding-per-
+// operation arithmetic bit for bit, which a fused multiply-add would break.
 #include <math.h>
 
 #include "common.h"
@@ -279,8 +282,8 @@ extern "C" int climsr_resize_cubic_f32(const float* src, int n, int sh, int sw, 
 // validation / test metrics
 // ------------------------------------------------------------------------------------------
 namespace {
-constexpr int MET_BLOCKS = 256;
-constexpr int SSIM_BLOCKS = 512;
+constexpr int MET_BLOCKS = 1024;  // 4 blocks of 4 waves per CU: the fused pass is load-latency bound
+constexpr int SSIM_BLOCKS = 1024;
 constexpr int SSIM_T = 32;                 // output tile edge
 constexpr int SSIM_K = 11, SSIM_R = 5;     // torchmetrics SSIM defaults: kernel 11, sigma 1.5
 constexpr int SSIM_IN = SSIM_T + 2 * SSIM_R;
@@ -294,7 +297,13 @@ constexpr int WS_STATS = MET_BLOCKS * P_SLOTS;
 constexpr int WS_SSIM = WS_STATS + 32;
 }  // namespace
 
-__device__ __forceinline__ void masked_values(const ClimsrMetricsDesc& d, long i, float& pn, float& tn, double& pd, double& td) {
+struct Denorm {
+  int t = -1;
+  double scale = 1.0, add = 0.0;
+};
+
+__device__ __forceinline__ void masked_values(const ClimsrMetricsDesc& d, long i, Denorm& dn, float& pn, float& tn, double& pd,
+                                              double& td) {
   const int hw = d.h * d.w;
   const int t = (int)(i / hw);
   const bool land = d.mask[i] != 0.f;  // `(~mask.bool())` -> 0
@@ -303,10 +312,13 @@ __device__ __forceinline__ void masked_values(const ClimsrMetricsDesc& d, long i
   tn = land ? d.hr[i] : 0.f;
   double den;
   if (d.method == 0) {  // MinMaxScaler._denormalize with float64 min/max tensors (task.py:281-285)
-    double mn = d.min[t], mx = d.max[t];
-    double scale = __ddiv_rn(d.range_b - d.range_a, __dadd_rn(__dsub_rn(mx, mn), d.eps));
-    double add = __dsub_rn(d.range_a, __dmul_rn(mn, scale));
-    den = __ddiv_rn(__dsub_rn((double)sr, add), scale);
+    if (t != dn.t) {    // per-sample constants, recomputed only when the grid-stride loop crosses a sample
+      double mn = d.min[t], mx = d.max[t];
+      dn.scale = __ddiv_rn(d.range_b - d.range_a, __dadd_rn(__dsub_rn(mx, mn), d.eps));
+      dn.add = __dsub_rn(d.range_a, __dmul_rn(mn, dn.scale));
+      dn.t = t;
+    }
+    den = __ddiv_rn(__dsub_rn((double)sr, dn.add), dn.scale);
   } else if (d.method == 1) {  // StandardScaler._denormalize: float32 tensor * python float
     den = (double)__fadd_rn(__fmul_rn(sr, (float)d.zs_std), (float)d.zs_mean);
   } else {
@@ -324,10 +336,11 @@ __global__ void __launch_bounds__(256) metrics_partial_kernel(ClimsrMetricsDesc 
   float pnmin = INFINITY, pnmax = -INFINITY, tnmin = INFINITY, tnmax = -INFINITY;
   const long total = (long)d.n * d.h * d.w;
   const float MEPS = 1.17e-06f;  // torchmetrics MAPE / SMAPE epsilon
+  Denorm dn_cache;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     float pn, tn;
     double pd, td;
-    masked_values(d, i, pn, tn, pd, td);
+    masked_values(d, i, dn_cache, pn, tn, pd, td);
     double dd = pd - td;
     double ad = fabs(dd);
     acc[P_ABS] += ad;
@@ -383,18 +396,21 @@ __global__ void __launch_bounds__(256) metrics_partial_kernel(ClimsrMetricsDesc 
   }
 }
 
-__global__ void metrics_stats_kernel(ClimsrMetricsDesc d) {
-  // one thread per slot, fixed block order -> deterministic
-  int k = threadIdx.x;
-  if (k >= P_SLOTS) return;
-  double x = d.workspace[k];
-  for (int b = 1; b < MET_BLOCKS; ++b) {
-    double y = d.workspace[(long)b * P_SLOTS + k];
-    if (k < P_NSUM) x += y;
-    else if ((k - P_NSUM) % 2 == 0) x = fmin(x, y);
-    else x = fmax(x, y);
+__device__ __forceinline__ double combine(int k, double x, double y) {
+  if (k < P_NSUM) return x + y;
+  return ((k - P_NSUM) % 2 == 0) ? fmin(x, y) : fmax(x, y);
+}
+
+// One block of 16 waves; wave w combines slots w, w+16: lane l folds partials l, l+64, ... in order, then a
+// fixed shuffle tree -> deterministic, no block-wide barriers.
+__global__ void __launch_bounds__(1024) metrics_stats_kernel(ClimsrMetricsDesc d) {
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int k = wv; k < P_SLOTS; k += 16) {
+    double x = d.workspace[(long)lane * P_SLOTS + k];
+    for (int b = lane + 64; b < MET_BLOCKS; b += 64) x = combine(k, x, d.workspace[(long)b * P_SLOTS + k]);
+    for (int o = 32; o > 0; o >>= 1) x = combine(k, x, __shfl_down(x, o));
+    if (lane == 0) d.workspace[WS_STATS + k] = x;
   }
-  d.workspace[WS_STATS + k] = x;
 }
 
 // SSIM over the masked normalised maps: 5 Gaussian-filtered maps (p, t, p², t², pt), reflect padding
@@ -430,10 +446,12 @@ __global__ void __launch_bounds__(256) ssim_kernel(ClimsrMetricsDesc d) {
       int iy = e / SSIM_IN, ix = e % SSIM_IN;
       int gy = oy0 + iy, gx = ox0 + ix;  // input row/col (crop offset cancels the window radius)
       float pn = 0.f, tn = 0.f;
-      if (gy < d.h && gx < d.w) {
+      if (gy < d.h && gx < d.w) {  // normalised maps only: SSIM never sees the denormalised values
         long i = ((long)b * d.h + gy) * d.w + gx;
-        double pd, td;
-        masked_values(d, i, pn, tn, pd, td);
+        if (d.mask[i] != 0.f) {
+          pn = d.sr[i];
+          tn = d.hr[i];
+        }
       }
       sp[iy][ix] = pn;
       st[iy][ix] = tn;
@@ -481,7 +499,14 @@ __global__ void __launch_bounds__(256) ssim_kernel(ClimsrMetricsDesc d) {
   if (threadIdx.x == 0) d.workspace[WS_SSIM + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
-__global__ void metrics_final_kernel(ClimsrMetricsDesc d, int ssim_blocks) {
+__global__ void __launch_bounds__(SSIM_BLOCKS) metrics_final_kernel(ClimsrMetricsDesc d, int ssim_blocks) {
+  __shared__ double sh[SSIM_BLOCKS];
+  sh[threadIdx.x] = (int)threadIdx.x < ssim_blocks ? d.workspace[WS_SSIM + threadIdx.x] : 0.0;
+  __syncthreads();
+  for (int o = SSIM_BLOCKS / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    __syncthreads();
+  }
   if (threadIdx.x != 0) return;
   const double* s = d.workspace + WS_STATS;
   const double n = (double)d.n * d.h * d.w;
@@ -490,9 +515,7 @@ __global__ void metrics_final_kernel(ClimsrMetricsDesc d, int ssim_blocks) {
   const double mse = s[P_SQ] / n;
   const double range = s[P_TD_MAX] - s[P_TD_MIN];           // PSNR(data_range=None): target max - min
   out[8] = (2.0 * log(range) - log(mse)) * (10.0 / log(10.0));
-  double ss = 0.0;
-  for (int b = 0; b < ssim_blocks; ++b) ss += d.workspace[WS_SSIM + b];
-  out[9] = ss / ((double)d.n * (d.h - 2 * SSIM_R) * (d.w - 2 * SSIM_R));
+  out[9] = sh[0] / ((double)d.n * (d.h - 2 * SSIM_R) * (d.w - 2 * SSIM_R));
   out[10] = s[P_ABS] / n;       // MAE
   out[11] = mse;                // MSE
   out[12] = sqrt(mse);          // RMSE (MeanSquaredError(squared=False))
@@ -514,12 +537,12 @@ extern "C" int climsr_sr_metrics(const ClimsrMetricsDesc* d, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const ClimsrMetricsDesc dd = *d;
   hipLaunchKernelGGL(metrics_partial_kernel, dim3(MET_BLOCKS), dim3(256), 0, s, dd);
-  hipLaunchKernelGGL(metrics_stats_kernel, dim3(1), dim3(64), 0, s, dd);
+  hipLaunchKernelGGL(metrics_stats_kernel, dim3(1), dim3(1024), 0, s, dd);
   const int oh = d->h - 2 * SSIM_R, ow = d->w - 2 * SSIM_R;
   long ntiles = (long)d->n * ((oh + SSIM_T - 1) / SSIM_T) * ((ow + SSIM_T - 1) / SSIM_T);
   int sb = (int)(ntiles < SSIM_BLOCKS ? ntiles : SSIM_BLOCKS);
   hipLaunchKernelGGL(ssim_kernel, dim3(sb), dim3(256), 0, s, dd);
-  hipLaunchKernelGGL(metrics_final_kernel, dim3(1), dim3(64), 0, s, dd, sb);
+  hipLaunchKernelGGL(metrics_final_kernel, dim3(1), dim3(SSIM_BLOCKS), 0, s, dd, sb);
   return check_launch("sr_metrics");
 }
 

@@ -48,7 +48,7 @@ class SRMetrics:
             raise RuntimeError("SRMetrics runs in libclimsr_hip.so: inputs must be CUDA tensors")
         n, c, h, w = sr.shape
         if c != 1:
-            raise ValueError("SRMetrics expects single-channel [n, 1, h, w] maps (the reference's out_channels=1)")
+            raise ValueError(f"SRMetrics expects single-channel [n, 1, h, w] maps (the reference's out_channels=1), got {tuple(sr.shape)}")
         dev = sr.device
         f32 = lambda t: t.detach().to(device=dev, dtype=torch.float32).reshape(n, 1, h, w).contiguous()  # noqa: E731
         sr_, hr_, orig_, mask_ = f32(sr), f32(hr), f32(original), f32(mask)

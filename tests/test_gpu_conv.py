@@ -60,6 +60,10 @@ CASES = [
     (3, 64, 9, 1, 1, 1, 20, 20),     # srcnn conv1
     (64, 32, 1, 1, 1, 2, 16, 16),    # srcnn conv2
     (32, 1, 5, 1, 1, 2, 16, 16),     # srcnn conv3
+    (64, 1, 3, 1, 1, 2, 37, 70),     # conv_last on the MFMA co1 kernel: ragged rows, two column blocks
+    (32, 1, 5, 1, 1, 1, 33, 130),    # srcnn conv3, three column blocks
+    (24, 1, 5, 1, 1, 1, 20, 20),     # co1 with a partial 32-channel block
+    (64, 1, 9, 1, 1, 1, 21, 67),     # 9x9 single output (the srcnn.conv1 data-gradient shape)
     (64, 128, 3, 2, 1, 2, 32, 32),   # D stride-2
     (256, 512, 3, 1, 1, 1, 8, 8),    # D / VGG wide
 ]
@@ -190,9 +194,9 @@ def test_conv_dgrad_stride2_matches_autograd(cin, cout, h):
     check_close(from_nhwc(gx, cin).cpu(), gref, tol=2e-5, what="dgrad s2")
 
 
-@pytest.mark.parametrize("cin,cout,ks,h,w", [(3, 64, 9, 40, 36), (1, 64, 3, 20, 20)])
+@pytest.mark.parametrize("cin,cout,ks,h,w", [(3, 64, 9, 40, 36), (1, 64, 3, 20, 20), (3, 64, 9, 70, 67)])
 def test_conv_dgrad_single_output_channel(cin, cout, ks, h, w):
-    """dgrad restricted to input channel 0 (srcnn.conv1 w.r.t. conv_last's output): VALU dot2 kernel."""
+    """dgrad restricted to input channel 0 (srcnn.conv1 w.r.t. conv_last's output): single-output MFMA kernel."""
     n = 2
     p, wt, b = make_plan(cin, cout, ks)
     g = torch.Generator().manual_seed(8)

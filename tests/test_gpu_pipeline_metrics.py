@@ -44,6 +44,14 @@ def bits_equal(a, b):
                                                   np.ascontiguousarray(b, np.float32).view(np.uint32))
 
 
+def describe(a, b):
+    if a.shape != b.shape:
+        return f"shape {a.shape} vs {b.shape}"
+    bad = np.argwhere(np.ascontiguousarray(a, np.float32).view(np.uint32) != np.ascontiguousarray(b, np.float32).view(np.uint32))
+    first = tuple(bad[0])
+    return f"{len(bad)} of {a.size} differ; first {first}: {a[first]!r} vs {b[first]!r}; max|d| {np.nanmax(np.abs(a - b))}"
+
+
 @pytest.mark.parametrize("case", list(CASES))
 def test_pipeline_matches_reference_golden(golden, case):
     method, gen, stage = CASES[case]
@@ -52,7 +60,7 @@ def test_pipeline_matches_reference_golden(golden, case):
                        stage, zs)
     keys = ["lr", "hr", "elevation", "mask"] + (["nearest", "elevation_lr", "hr_lr"] if stage != "train" else [])
     for k in keys:
-        assert bits_equal(got[k], golden[f"{case}/{k}"]), f"{case}/{k}"
+        assert bits_equal(got[k], golden[f"{case}/{k}"]), f"{case}/{k}: {describe(got[k], golden[f'{case}/{k}'])}"
     if stage != "train":
         assert np.array_equal(np.isnan(got["original_data"][:, 0]), np.isnan(golden["hr_raw"]))
 
@@ -70,7 +78,7 @@ def test_pipeline_training_size_matches_oracle():
     got = run_pipeline(hr, elev, mn, mx, codes, "minmax", "esrgan", "train")
     want = dr.prepare_batch(hr, elev, mn, mx, codes)
     for k in ("lr", "hr", "elevation", "mask"):
-        assert bits_equal(got[k], want[k]), k
+        assert bits_equal(got[k], want[k]), f"{k}: {describe(got[k], want[k])}"
 
 
 def test_cubic_upscale_matches_restated_cv2():
@@ -138,7 +146,8 @@ def test_sr_metrics_match_oracle():
 def test_validation_step_through_task():
     from climsr_amd.task.pl_generator_pre_training import SuperResolutionLightningModule
 
-    task = SuperResolutionLightningModule(generator={"_target_": "climsr_amd.models.esrgan.ESRGANGenerator", "nb": 1},
+    task = SuperResolutionLightningModule(generator={"_target_": "climsr_amd.models.esrgan.ESRGANGenerator", "nb": 1, "gc": 16,
+                                                     "in_channels": 3, "out_channels": 1},
                                           normalization_method="minmax", normalization_range=(-1.0, 1.0))
     task.to(DEV)
     rs = np.random.RandomState(14)
