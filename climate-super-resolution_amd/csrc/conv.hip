@@ -2088,6 +2088,153 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad64_kernel(WgArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Weight gradient of a single-output-channel conv (conv_last 64->1 3x3, srcnn.conv3 32->1 5x5).  The
+// generic wgrad puts the one output channel in the MFMA M dimension (1 of 16 rows useful); here the
+// horizontal taps take that role instead.  Per dz row y and input row iy = y + ky - R:
+//     D_ky[kx][ci] += sum_x' dz[y][x' - kx] * X[iy][x'][ci]           (M = kx, N = ci, K = x')
+// A = the dz row shifted by kx (a Toeplitz fragment: 8 consecutive dz values per lane, read 16 B-aligned
+// from one of 8 pre-shifted LDS copies of the row), B = the input row transposed by ds_read_tr16_b64.
+// A wave streams a segment of SEG dz rows of one 64-column strip; each staged input row feeds the KS
+// dz rows it pairs with.  Block partials (4 waves summed in LDS) go to the wgrad_reduce layout
+// part[split][16][in_c * ks^2] (row 0), bpart[split][16].
+// ------------------------------------------------------------------------------------------
+constexpr int WCO1_XT = 96, WCO1_DZL = 128;
+
+static bool wco1_shape(const ClimsrConvDesc* d) {
+  return d->out_c == 1 && d->stride == 1 && d->up == 1 && (d->ks == 3 || d->ks == 5) && d->pad == d->ks / 2 &&
+         d->in_c % 16 == 0 && d->in_c <= 64 && d->out_h == d->in_h && d->out_w == d->in_w;
+}
+
+static int wco1_splits(const ClimsrConvDesc* d) {
+  const long rows = (long)d->n * d->out_h * ceil_div(d->out_w, 64);
+  long ns = rows / (4 * 8);  // >= 8 dz rows per wave
+  if (ns > 512) ns = 512;
+  return ns < 1 ? 1 : (int)ns;
+}
+
+template <int KS, int NCF>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_co1m_kernel(WgArgs a) {
+  constexpr int R = KS / 2, CI = NCF * 16, XP = CI + 8, NV = ((64 + KS - 1) * (CI / 8) + 63) / 64;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
+  uint16_t* xs = (uint16_t*)smem + wave * (WCO1_XT * XP);                                   // [x'][ci]
+  uint16_t* ring = (uint16_t*)smem + 4 * WCO1_XT * XP + wave * (KS * 8 * WCO1_DZL);         // [slot][copy][m]
+  for (int i = lane; i < WCO1_XT * XP / 8; i += 64) ((uint4*)xs)[i] = make_uint4(0, 0, 0, 0);
+  for (int i = lane; i < KS * 8 * WCO1_DZL / 8; i += 64) ((uint4*)ring)[i] = make_uint4(0, 0, 0, 0);
+
+  f32x4 acc[KS][NCF];
+#pragma unroll
+  for (int k = 0; k < KS; ++k)
+#pragma unroll
+    for (int c = 0; c < NCF; ++c) acc[k][c] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;
+
+  const int nstrip = (a.out_w + 63) / 64;
+  const int seg_rows = a.tph;  // dz rows per segment (host-chosen)
+  const int nrs = (a.out_h + seg_rows - 1) / seg_rows;
+  const long nseg = (long)a.n * nstrip * nrs;
+  const int gw = blockIdx.x * 4 + wave, nw = gridDim.x * 4;
+  for (long seg = gw; seg < nseg; seg += nw) {
+    const int rs = (int)(seg % nrs);
+    const int strip = (int)((seg / nrs) % nstrip);
+    const int nimg = (int)(seg / ((long)nrs * nstrip));
+    const int x0 = strip * 64, ya = rs * seg_rows, yb = min(a.out_h, ya + seg_rows);
+    for (int iy = ya - R; iy < yb + R; ++iy) {
+      // stage input row iy: x' in [0, 64 + KS - 1) <-> input column x0 - R + x'
+      uint4 v[NV];
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int e = lane + 64 * i, xq = e / (CI / 8), cg = e % (CI / 8);
+        const int ix = x0 - R + xq;
+        v[i] = make_uint4(0, 0, 0, 0);
+        if (xq < 64 + KS - 1 && iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w && cg * 8 < a.in_c)
+          v[i] = *(const uint4*)(a.x + (((long)nimg * a.in_h + iy) * a.in_w + ix) * a.in_cs + a.in_co + cg * 8);
+      }
+      // the dz row paired with tap row 0 enters the ring: 8 copies, copy q holds D[m - 16 - q]
+      const int ynew = iy + R;
+      float dzv = 0.f;
+      if (ynew >= ya && ynew < yb && x0 + lane < a.out_w)
+        dzv = bf2f(a.dz[(((long)nimg * a.out_h + ynew) * a.out_w + x0 + lane) * a.dz_cs]);
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int e = lane + 64 * i, xq = e / (CI / 8), cg = e % (CI / 8);
+        if (xq < 64 + KS - 1) *(uint4*)(xs + xq * XP + cg * 8) = v[i];
+      }
+      if (ynew >= ya && ynew < yb) {
+        bsum += dzv;
+        uint16_t* slot = ring + (ynew % KS) * (8 * WCO1_DZL);
+        const uint16_t b = f2bf(dzv);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) slot[q * WCO1_DZL + lane + 16 + q] = b;
+      }
+      // B fragments of this input row (x' = 32 s + 8 g + j, ci = 16 c + col), shared by every tap row
+      bf16x8 bx[3][NCF];
+#pragma unroll
+      for (int st = 0; st < 3; ++st)
+#pragma unroll
+        for (int c = 0; c < NCF; ++c) {
+          const uint16_t* p0 = xs + (st * 32 + g * 8 + (col >> 2)) * XP + c * 16 + (col & 3) * 4;
+          const s16x4 lo = ds_read_tr16(p0), hi = ds_read_tr16(p0 + 4 * XP);
+          bx[st][c] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+#pragma unroll
+      for (int ky = 0; ky < KS; ++ky) {
+        const int y = iy - ky + R;
+        if (y < ya || y >= yb) continue;
+        const uint16_t* slot = ring + (y % KS) * (8 * WCO1_DZL);
+#pragma unroll
+        for (int st = 0; st < 3; ++st) {
+          const int aoff = st * 32 + g * 8 - col;  // D index of element j = 0 (lane's kx = col)
+          const int q = (-aoff) & 7;
+          bf16x8 at = *(const bf16x8*)(slot + q * WCO1_DZL + aoff + 16 + q);
+          if (col >= KS) at = (bf16x8){};
+#pragma unroll
+          for (int c = 0; c < NCF; ++c) acc[ky][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at, bx[st][c], acc[ky][c], 0, 0, 0);
+        }
+      }
+    }
+    // the next segment rewrites every ring position it reads (rows outside [ya, yb) are skipped)
+  }
+  // block reduction: C[kx = 4g + i][ci = 16c + col] of tap row ky
+  for (int o = 32; o > 0; o >>= 1) bsum += __shfl_down(bsum, o);
+  __syncthreads();
+  float* red = (float*)smem;  // [wave][ky][c][lane][4]
+#pragma unroll
+  for (int ky = 0; ky < KS; ++ky)
+#pragma unroll
+    for (int c = 0; c < NCF; ++c) *(f32x4*)(red + (((wave * KS + ky) * NCF + c) * 64 + lane) * 4) = acc[ky][c];
+  __shared__ float bred[4];
+  if (lane == 0) bred[wave] = bsum;
+  __syncthreads();
+  const int ks2 = KS * KS;
+  float* part = a.part + (long)blockIdx.x * 16 * a.kw;
+  constexpr int PER = KS * NCF * 64 * 4;
+  for (int e = tid; e < PER; e += 256) {
+    const int i = e & 3, ln = (e >> 2) & 63, c = (e >> 8) % NCF, ky = (e >> 8) / NCF;
+    const int kx = (ln >> 4) * 4 + i, ci = c * 16 + (ln & 15);
+    if (kx >= KS || ci >= a.in_c) continue;
+    const float t = red[e] + red[e + PER] + red[e + 2 * PER] + red[e + 3 * PER];
+    part[ci * ks2 + ky * KS + kx] = t;
+  }
+  if (tid == 0 && a.bpart) a.bpart[blockIdx.x * 16] = bred[0] + bred[1] + bred[2] + bred[3];
+}
+
+template <int KS, int NCF>
+static int launch_wco1(const WgArgs& a, hipStream_t s) {
+  auto k = conv_wgrad_co1m_kernel<KS, NCF>;  // (+16 B of static LDS: the dynamic cap leaves room for it)
+  const size_t lds_x = (size_t)4 * WCO1_XT * (NCF * 16 + 8) * 2 + (size_t)4 * KS * 8 * WCO1_DZL * 2;
+  const size_t lds_r = (size_t)4 * KS * NCF * 64 * 16;
+  const size_t lds = lds_x > lds_r ? lds_x : lds_r;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(k, dim3(a.nsplit), dim3(256), lds, s, a);
+  return check_launch("conv2d_wgrad (co1m)");
+}
+
 static bool w64_shape(const ClimsrConvDesc* d) {
   return d->ks == 3 && d->stride == 1 && d->pad == 1 && d->out_c % 64 == 0 && d->in_c % 64 == 0 && d->in_c >= 64;
 }
@@ -2131,6 +2278,7 @@ static void wg_plan(const ClimsrConvDesc* d, WgPlan* w) {
 }
 
 extern "C" int climsr_conv2d_wgrad_splits(const ClimsrConvDesc* d) {
+  if (wco1_shape(d) && !getenv("CLIMSR_NO_CO1M")) return wco1_splits(d);
   if (w64_shape(d)) {  // one workgroup per CU: 256 / blocks splits
     int blocks = (d->out_c / 64) * (d->in_c / 64);
     int ntiles = d->n * ceil_div(d->out_w, TW) * ceil_div(d->out_h, W64_TH);
@@ -2148,6 +2296,7 @@ extern "C" int climsr_conv2d_wgrad_splits(const ClimsrConvDesc* d) {
 }
 
 extern "C" size_t climsr_conv2d_wgrad_workspace(const ClimsrConvDesc* d, int nsplit) {
+  if (wco1_shape(d) && !getenv("CLIMSR_NO_CO1M")) return (size_t)nsplit * 16 * d->in_c * d->ks * d->ks + (size_t)nsplit * 16;
   if (w64_shape(d)) return (size_t)nsplit * d->out_c * d->in_c * 9 + (size_t)nsplit * d->out_c;
   WgPlan w;
   wg_plan(d, &w);
@@ -2173,6 +2322,28 @@ extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, c
       (d->up != 1 && d->up != 2) || (d->stride != 1 && d->stride != 2)) {
     set_error("conv2d_wgrad: bad args");
     return CLIMSR_EINVAL;
+  }
+  if (wco1_shape(d) && !getenv("CLIMSR_NO_CO1M")) {
+    WgArgs a{};
+    a.x = x; a.dz = dz; a.part = partial; a.bpart = bias_partial;
+    a.n = d->n; a.in_h = d->in_h; a.in_w = d->in_w; a.in_c = d->in_c; a.in_cs = d->in_cstride; a.in_co = d->in_coff;
+    a.out_h = d->out_h; a.out_w = d->out_w; a.out_c = 1; a.dz_cs = dz_cstride; a.ks = d->ks; a.pad = d->pad;
+    a.nsplit = nsplit; a.kw = d->in_c * d->ks * d->ks; a.co_rows = 16;
+    const long rows = (long)d->n * d->out_h * ceil_div(d->out_w, 64);
+    a.tph = ceil_div(rows, (long)nsplit * 4);  // dz rows per wave segment (~one segment per wave)
+    if (a.tph < 4) a.tph = 4;
+    if (a.tph > d->out_h) a.tph = d->out_h;
+    hipStream_t s = (hipStream_t)stream;
+    switch (d->ks * 10 + d->in_c / 16) {
+      case 31: return launch_wco1<3, 1>(a, s);
+      case 32: return launch_wco1<3, 2>(a, s);
+      case 33: return launch_wco1<3, 3>(a, s);
+      case 34: return launch_wco1<3, 4>(a, s);
+      case 51: return launch_wco1<5, 1>(a, s);
+      case 52: return launch_wco1<5, 2>(a, s);
+      case 53: return launch_wco1<5, 3>(a, s);
+      default: return launch_wco1<5, 4>(a, s);
+    }
   }
   if (w64_shape(d)) {
     WgArgs a;

@@ -165,6 +165,27 @@ def test_conv_wgrad_matches_autograd(cin, cout, ks, stride, up):
     check_close(p.gb.cpu(), gb, tol=2e-5, what="bgrad")
 
 
+@pytest.mark.parametrize("cin,ks,n,h,w", [(64, 3, 3, 70, 150), (32, 5, 2, 45, 131), (16, 3, 1, 9, 64), (48, 5, 2, 33, 65)])
+def test_conv_wgrad_single_output_channel(cin, ks, n, h, w):
+    """conv_last / srcnn.conv3 weight gradient on the Toeplitz-fragment MFMA kernel: several 64-column strips,
+    ragged last strip, segments that end mid-image."""
+    p, wt, b = make_plan(cin, 1, ks)
+    g = torch.Generator().manual_seed(9)
+    x = bf(torch.rand((n, cin, h, w), generator=g) * 2 - 1)
+    dz = bf(torch.rand((n, 1, h, w), generator=g) * 2 - 1)
+    xb, dzb = to_nhwc(x), to_nhwc(dz)
+    p.gw = torch.zeros_like(p.weight)
+    p.gb = torch.zeros_like(p.bias)
+    p.wgrad(xb, xb.shape[-1], 0, h, w, dzb, dzb.shape[-1], n, Workspace(), accumulate=False)
+    torch.cuda.synchronize()
+    wr = bf(wt).double().requires_grad_(True)
+    br = b.double().requires_grad_(True)
+    y = F.conv2d(x.double(), wr, br, padding=ks // 2)
+    gw, gb = torch.autograd.grad(y, (wr, br), dz.double())
+    check_close(p.gw.cpu(), gw, tol=2e-5, what="wgrad co1")
+    check_close(p.gb.cpu(), gb, tol=2e-5, what="bgrad co1")
+
+
 def test_act_grad():
     n, h, w = 2, 8, 8
     g = torch.Generator().manual_seed(6)
