@@ -1,0 +1,153 @@
+// RCAN pieces that are not convolutions (climsr/models/rcan.py):
+//  * channel attention of an RCAB (CALayer, rcan.py:50-69): global average pool -> 1x1 conv -> ReLU ->
+//    1x1 conv -> sigmoid -> x * y, and the block residual (RCAB.forward, rcan.py:104-107) fused with the
+//    scaling into one pass that also emits the bf16 copy the next conv reads;
+//  * nn.PixelShuffle(r) of the Upsampler (rcan.py:17-47) on NHWC bf16: a pure index map, bit-exact.
+// All HBM-bound elementwise / reduction work: 16 B per lane where the layout allows, deterministic
+// fixed-order reductions.
+#include "common.h"
+
+using namespace climsr;
+
+namespace {
+constexpr int POOL_SPLIT = 64;  // pixel slices per image of the pooling pass
+}
+
+// partial[n][split][c] = sum over the split's pixels of x[n][p][c] (fp32 NHWC, cstride)
+__global__ __launch_bounds__(256) void channel_sum_partial_kernel(const float* __restrict__ x, long hw, int c, int cs,
+                                                                  double* __restrict__ part) {
+  const int nimg = blockIdx.y, sp = blockIdx.x;
+  const long p0 = hw * sp / POOL_SPLIT, p1 = hw * (sp + 1) / POOL_SPLIT;
+  const int lanes_per_px = c < 256 ? c : 256;  // threads along channels
+  const int pstep = 256 / lanes_per_px;
+  const int ci = threadIdx.x % lanes_per_px, pl = threadIdx.x / lanes_per_px;
+  __shared__ double sh[256];
+  for (int c0 = 0; c0 < c; c0 += lanes_per_px) {
+    double acc = 0.0;
+    if (pl < pstep && c0 + ci < c)
+      for (long p = p0 + pl; p < p1; p += pstep) acc += (double)x[((long)nimg * hw + p) * cs + c0 + ci];
+    sh[threadIdx.x] = acc;
+    __syncthreads();
+    if (pl == 0 && c0 + ci < c) {
+      double t = 0.0;
+      for (int k = 0; k < pstep; ++k) t += sh[k * lanes_per_px + ci];
+      part[((long)nimg * POOL_SPLIT + sp) * c + c0 + ci] = t;
+    }
+    __syncthreads();
+  }
+}
+
+// s[n][c] = sigmoid(W2 relu(W1 mean + b1) + b2)  (conv_du of CALayer on the pooled [n, c, 1, 1] map)
+__global__ void ca_mlp_kernel(const double* __restrict__ part, long hw, int c, int cr, const float* __restrict__ w1,
+                              const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2,
+                              float* __restrict__ s) {
+  extern __shared__ float sm[];
+  float* mean = sm;      // [c]
+  float* hid = sm + c;   // [cr]
+  const int nimg = blockIdx.x;
+  for (int i = threadIdx.x; i < c; i += blockDim.x) {
+    double t = 0.0;
+    for (int sp = 0; sp < POOL_SPLIT; ++sp) t += part[((long)nimg * POOL_SPLIT + sp) * c + i];
+    mean[i] = (float)(t / (double)hw);
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < cr; j += blockDim.x) {
+    float t = b1 ? b1[j] : 0.f;
+    for (int i = 0; i < c; ++i) t += w1[j * c + i] * mean[i];
+    hid[j] = t > 0.f ? t : 0.f;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < c; i += blockDim.x) {
+    float t = b2 ? b2[i] : 0.f;
+    for (int j = 0; j < cr; ++j) t += w2[i * cr + j] * hid[j];
+    s[nimg * c + i] = 1.f / (1.f + expf(-t));
+  }
+}
+
+extern "C" int climsr_channel_attention(const float* u, int n, int64_t hw, int c, int u_cstride, const float* w1, const float* b1,
+                                        const float* w2, const float* b2, int cr, double* workspace, float* s, void* stream) {
+  if (!u || !w1 || !w2 || !workspace || !s || n <= 0 || hw <= 0 || c <= 0 || cr <= 0 || u_cstride < c) {
+    set_error("channel_attention: bad args");
+    return CLIMSR_EINVAL;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(channel_sum_partial_kernel, dim3(POOL_SPLIT, n), dim3(256), 0, st, u, (long)hw, c, u_cstride, workspace);
+  hipLaunchKernelGGL(ca_mlp_kernel, dim3(n), dim3(256), (size_t)(c + cr) * sizeof(float), st, workspace, (long)hw, c, cr, w1, b1,
+                     w2, b2, s);
+  return check_launch("channel_attention");
+}
+
+extern "C" size_t climsr_channel_attention_workspace(int n, int c) { return (size_t)n * POOL_SPLIT * c * sizeof(double); }
+
+// xres[p][c] = u[p][c] * s[n][c] + xres[p][c];  xb[p][c] = bf16(xres[p][c])   (RCAB: body(x) + x)
+__global__ __launch_bounds__(256) void ca_scale_add_kernel(const float* __restrict__ u, int u_cs, const float* __restrict__ s,
+                                                           float* __restrict__ xres, uint16_t* __restrict__ xb, int xb_cs, long hw,
+                                                           int c, long total4) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total4) return;
+  const int cg = c / 4;
+  const long pix = i / cg;
+  const int c0 = (int)(i % cg) * 4;
+  const int nimg = (int)(pix / hw);
+  const float4 uv = *(const float4*)(u + pix * u_cs + c0);
+  const float4 sv = *(const float4*)(s + (long)nimg * c + c0);
+  float4 r = *(const float4*)(xres + pix * c + c0);
+  r.x = uv.x * sv.x + r.x;
+  r.y = uv.y * sv.y + r.y;
+  r.z = uv.z * sv.z + r.z;
+  r.w = uv.w * sv.w + r.w;
+  *(float4*)(xres + pix * c + c0) = r;
+  uint2 pk;
+  pk.x = (uint32_t)f2bf(r.x) | ((uint32_t)f2bf(r.y) << 16);
+  pk.y = (uint32_t)f2bf(r.z) | ((uint32_t)f2bf(r.w) << 16);
+  *(uint2*)(xb + pix * xb_cs + c0) = pk;
+}
+
+extern "C" int climsr_ca_scale_add(const float* u, int u_cstride, const float* s, float* xres, uint16_t* xb, int xb_cstride, int n,
+                                   int64_t hw, int c, void* stream) {
+  if (!u || !s || !xres || !xb || n <= 0 || hw <= 0 || c % 4 || u_cstride % 4 || xb_cstride % 4 || u_cstride < c ||
+      xb_cstride < c) {
+    set_error("ca_scale_add: bad args (c, strides multiples of 4)");
+    return CLIMSR_EINVAL;
+  }
+  const long total4 = (long)n * hw * (c / 4);
+  hipLaunchKernelGGL(ca_scale_add_kernel, dim3(ceil_div(total4, 256)), dim3(256), 0, (hipStream_t)stream, u, u_cstride, s, xres, xb,
+                     xb_cstride, (long)hw, c, total4);
+  return check_launch("ca_scale_add");
+}
+
+// nn.PixelShuffle(r) on NHWC: y[n][y*r+i][x*r+j][co] = x[n][y][x][co*r*r + i*r + j]; one thread per output
+// (pixel, 8 channels): 8 gathered 2 B reads from one input pixel's channel vector, one 16 B store.
+__global__ __launch_bounds__(256) void pixel_shuffle_kernel(const uint16_t* __restrict__ x, int h, int w, int c_out, int r,
+                                                            int in_cs, uint16_t* __restrict__ y, int out_cs, long total) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int cg = c_out / 8;
+  const long opix = i / cg;
+  const int co0 = (int)(i % cg) * 8;
+  const int ow = w * r, oh = h * r;
+  const int ox = (int)(opix % ow);
+  const long t = opix / ow;
+  const int oy = (int)(t % oh);
+  const long nimg = t / oh;
+  const int yy = oy / r, ii = oy - yy * r, xx = ox / r, jj = ox - xx * r;
+  const uint16_t* src = x + ((nimg * h + yy) * w + xx) * in_cs + ii * r + jj;
+  const int rr = r * r;
+  uint32_t v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] = (uint32_t)src[(co0 + 2 * k) * rr] | ((uint32_t)src[(co0 + 2 * k + 1) * rr] << 16);
+  *(uint4*)(y + opix * out_cs + co0) = make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+extern "C" int climsr_pixel_shuffle_bf16(const uint16_t* x, int n, int h, int w, int c_out, int r, int in_cstride, uint16_t* y,
+                                         int out_cstride, void* stream) {
+  if (!x || !y || n <= 0 || h <= 0 || w <= 0 || r < 1 || c_out % 8 || out_cstride % 8 || out_cstride < c_out ||
+      in_cstride < c_out * r * r) {
+    set_error("pixel_shuffle: bad args (c_out, out_cstride multiples of 8; in_cstride >= c_out*r*r)");
+    return CLIMSR_EINVAL;
+  }
+  const long total = (long)n * h * r * w * r * (c_out / 8);
+  hipLaunchKernelGGL(pixel_shuffle_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, x, h, w, c_out, r,
+                     in_cstride, y, out_cstride, total);
+  return check_launch("pixel_shuffle");
+}

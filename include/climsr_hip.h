@@ -347,6 +347,24 @@ int climsr_sr_metrics(const ClimsrMetricsDesc* d, void* stream);
 int climsr_regression_accuracy_update(const float* preds, const float* target, int64_t n, float eps, int64_t* counts,
                                       void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * RCAN (climsr/models/rcan.py).
+ * --------------------------------------------------------------------------------------------- */
+/* CALayer (rcan.py:50-69): s[n][c] = sigmoid(w2 . relu(w1 . mean_p u[n][p][:] + b1) + b2), u fp32 NHWC
+ * [n][hw][u_cstride]; w1 [cr][c], w2 [c][cr] (the 1x1 conv_du weights); workspace
+ * climsr_channel_attention_workspace(n, c) bytes.  Deterministic (fixed-order fp64 pooling). */
+size_t climsr_channel_attention_workspace(int n, int c);
+int climsr_channel_attention(const float* u, int n, int64_t hw, int c, int u_cstride, const float* w1, const float* b1,
+                             const float* w2, const float* b2, int cr, double* workspace, float* s, void* stream);
+/* RCAB residual with the attention scale (rcan.py:104-107): xres = u * s + xres (fp32 [n][hw][c]) and
+ * xb = bf16(xres) ([n][hw][xb_cstride], the next conv's input).  c, strides multiples of 4. */
+int climsr_ca_scale_add(const float* u, int u_cstride, const float* s, float* xres, uint16_t* xb, int xb_cstride, int n,
+                        int64_t hw, int c, void* stream);
+/* nn.PixelShuffle(r) (Upsampler, rcan.py:17-47) on NHWC bf16: y[n][y*r+i][x*r+j][co] = x[n][y][x][co*r*r+i*r+j].
+ * Bit-exact index map; c_out and out_cstride multiples of 8. */
+int climsr_pixel_shuffle_bf16(const uint16_t* x, int n, int h, int w, int c_out, int r, int in_cstride, uint16_t* y,
+                              int out_cstride, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
