@@ -41,8 +41,13 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--mode", choices=["pretrain", "gan"], default="pretrain",
-                    help="pretrain = BASELINE config 2 (the metric's workload); gan = config 3 (G + RFB-D + VGG19 perceptual)")
+    ap.add_argument("--mode", choices=["pretrain", "gan", "infer"], default="pretrain",
+                    help="pretrain = BASELINE config 2 (the metric's workload); gan = config 3 (G + RFB-D + VGG19 perceptual); "
+                         "infer = config 5 (whole-grid inference)")
+    ap.add_argument("--model", choices=["rcan", "esrgan"], default="rcan",
+                    help="infer mode: RCAN 10x20 (conf/inference.yaml's default) or the ESRGAN generator")
+    ap.add_argument("--grid-h", type=int, default=360, help="infer mode: LR grid rows (CRU-TS 0.5 deg: 360)")
+    ap.add_argument("--grid-w", type=int, default=720, help="infer mode: LR grid columns (720)")
     return ap.parse_args()
 
 
@@ -125,6 +130,140 @@ def cpu_baseline(args, hr):
                       f"{n} steps ({dt * 1e3:.0f} ms/step)"}
 
 
+def run_infer(args, world, rank, dev):
+    """BASELINE config 5: one whole CRU-TS grid (LR 720x360 -> HR 2880x1440) per step, forward only, one replica
+    per GPU (the path does not shard within a grid: `scaling` weak, every rank infers its own grid)."""
+    from climsr_amd import ops
+    from climsr_amd.core.init import init_state, spec_from_shapes
+
+    H, W = args.grid_h, args.grid_w
+    if args.model == "rcan":
+        from climsr_amd.models.rcan import RCAN
+
+        net = RCAN(n_resgroups=10, n_resblocks=20, n_feats=64, reduction=16, scaling_factor=4, in_channels=3, out_channels=1)
+        desc = "RCAN 10 groups x 20 RCABs, nf64, x4 (conf/generator/rcan.yaml)"
+    else:
+        from climsr_amd.models.esrgan import ESRGANGenerator
+
+        net = ESRGANGenerator(in_channels=3, out_channels=1, nf=64, nb=args.nb, gc=16, scale_factor=4)
+        desc = f"ESRGAN nf64 nb{args.nb} gc16 x4"
+    st = init_state(spec_from_shapes({k: tuple(v.shape) for k, v in net.state_dict().items()}))
+    net.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in st.items()})
+    net = net.to(dev).eval()
+    gen = torch.Generator(device="cpu").manual_seed(42 + rank)
+    hh, ww = 4 * H, 4 * W
+    t = torch.rand((1, 1, hh, ww), generator=gen) * 2 - 1
+    e = torch.rand((1, 1, hh, ww), generator=gen) * 2 - 1
+    m = (torch.rand((1, 1, hh, ww), generator=gen) < 0.7).float()
+    lr = torch.cat([t, e, m], 1)[:, :, ::4, ::4].contiguous().to(dev)
+    e, m = e.to(dev), m.to(dev)
+    out = {}
+
+    def fwd():
+        out["sr"] = net(lr, e, m)
+
+    with torch.no_grad():
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            fwd()
+            fwd()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        run = fwd
+        if not args.no_graph:
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr):
+                fwd()
+            run = gr.replay
+        for _ in range(args.warmup):
+            run()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            run()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            elapsed = float(tt.item())
+        ms = elapsed / args.steps * 1e3
+        mpix = world * hh * ww / 1e6 / (elapsed / args.steps)
+        roof, kern = None, {}
+        if not args.no_kernel_timing:
+            timer = KernelTimer()
+            ops.PROFILER = timer
+            fwd()
+            ops.PROFILER = None
+            agg = timer.summary()
+            name, (cnt, tot_ms, flops) = max(agg.items(), key=lambda kv: kv[1][1])
+            avg_ms = tot_ms / cnt
+            achieved = flops / cnt / (avg_ms / 1e3) / 1e12
+            roof = {"bound": "mfma", "kernel": name, "launches_per_step": cnt, "avg_launch_us": round(avg_ms * 1e3, 2),
+                    "flop_per_launch": flops // cnt, "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None}
+            kern = {k: {"launches": v[0], "ms_total": round(v[1], 3), "tflops": round(v[2] / (v[1] / 1e3) / 1e12, 1)}
+                    for k, v in sorted(agg.items(), key=lambda kv: -kv[1][1])}
+            flop_fwd = sum(v[2] for v in agg.values())
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_infer(args, {k: v.detach().cpu().float() for k, v in net.state_dict().items()})
+    if rank == 0:
+        res = {
+            "metric": "HR MPix/s whole-grid inference (config 5: 720x360 -> 2880x1440, 4x SR)",
+            "value": round(mpix, 3), "unit": "HR MPix/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic grid (seed 42+rank: U(-1,1) temp/elev, Bernoulli(0.7) mask, LR = HR[::4,::4]); deterministic init",
+            "config": {"workload": f"config 5: whole-grid inference, LR {W}x{H} -> HR {ww}x{hh}, one grid per GPU per step",
+                       "model": desc, "batch": 1, "parallelism": f"replicas{world}", "hip_graph": not args.no_graph,
+                       "mode": "infer"},
+            "roofline": roof,
+            "step_mfma": ({"algorithmic_tflop_per_step": round(flop_fwd / 1e12, 3),
+                           "achieved_tflops": round(flop_fwd / (ms / 1e3) / 1e12, 1),
+                           "frac": round(flop_fwd / (ms / 1e3) / 1e12 / PEAK_BF16_TFLOPS, 4)} if roof else None),
+            "cpu_baseline": cpu,
+            "kernels": kern,
+        }
+        print(json.dumps(res))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline_infer(args, state):
+    """Oracle fp32 PyTorch-CPU forward of the same network on a bounded crop of the grid (LR 45x90)."""
+    from oracle import climsr_ref as ref
+
+    threads = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(threads)
+    h, w = 45, 90
+    g = torch.Generator().manual_seed(7)
+    x = torch.rand((1, 3, h, w), generator=g)
+    e = torch.rand((1, 1, 4 * h, 4 * w), generator=g)
+    m = torch.rand((1, 1, 4 * h, 4 * w), generator=g)
+    if args.model == "rcan":
+        fn = lambda: ref.rcan_forward(state, x, e, m, 10, 20, 4)  # noqa: E731
+    else:
+        fn = lambda: ref.generator_forward(state, x, e, m, args.nb)  # noqa: E731
+    with torch.no_grad():
+        fn()
+        t0 = time.perf_counter()
+        n = 0
+        while True:
+            fn()
+            n += 1
+            if time.perf_counter() - t0 >= args.cpu_seconds or n >= 20:
+                break
+    dt = (time.perf_counter() - t0) / n
+    return {"value": round(16 * h * w / 1e6 / dt, 5), "unit": "HR MPix/s", "cores": threads, "kind": "port",
+            "sample": f"oracle {args.model} forward (fp32 PyTorch-CPU), LR {w}x{h} crop of the grid, {n} runs ({dt * 1e3:.0f} ms each)"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -137,6 +276,9 @@ def main():
     torch.cuda.set_device(dev)
 
     import climsr_amd  # noqa: F401
+
+    if args.mode == "infer":
+        return run_infer(args, world, rank, dev)
     from climsr_amd import ops
     from climsr_amd.core.init import init_state, spec_from_shapes
     from climsr_amd.core.optim import GraphedAdamW

@@ -10,47 +10,64 @@
 using namespace climsr;
 
 namespace {
-constexpr int POOL_SPLIT = 64;  // pixel slices per image of the pooling pass
+constexpr int POOL_SPLIT = 256;  // pixel slices per image of the pooling pass (>= 1 block per CU for one grid)
 }
 
-// partial[n][split][c] = sum over the split's pixels of x[n][p][c] (fp32 NHWC, cstride)
+// part[n][split][c] = sum over the split's pixels of x[n][p][c] (fp32 NHWC, cstride).  A block is
+// (c/4 float4 lanes) x (256 / (c/4) pixel lanes); fp32 per-thread sums, fp64 across the block.
 __global__ __launch_bounds__(256) void channel_sum_partial_kernel(const float* __restrict__ x, long hw, int c, int cs,
                                                                   double* __restrict__ part) {
   const int nimg = blockIdx.y, sp = blockIdx.x;
   const long p0 = hw * sp / POOL_SPLIT, p1 = hw * (sp + 1) / POOL_SPLIT;
-  const int lanes_per_px = c < 256 ? c : 256;  // threads along channels
-  const int pstep = 256 / lanes_per_px;
-  const int ci = threadIdx.x % lanes_per_px, pl = threadIdx.x / lanes_per_px;
-  __shared__ double sh[256];
-  for (int c0 = 0; c0 < c; c0 += lanes_per_px) {
-    double acc = 0.0;
-    if (pl < pstep && c0 + ci < c)
-      for (long p = p0 + pl; p < p1; p += pstep) acc += (double)x[((long)nimg * hw + p) * cs + c0 + ci];
-    sh[threadIdx.x] = acc;
-    __syncthreads();
-    if (pl == 0 && c0 + ci < c) {
-      double t = 0.0;
-      for (int k = 0; k < pstep; ++k) t += sh[k * lanes_per_px + ci];
-      part[((long)nimg * POOL_SPLIT + sp) * c + c0 + ci] = t;
+  __shared__ double sh[256 * 4];
+  const int cg = c / 4;  // host guarantees c % 4 == 0, cs % 4 == 0, cg <= 256
+  const int plan = 256 / cg;
+  const int g = threadIdx.x % cg, pl = threadIdx.x / cg;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (pl < plan)
+    for (long p = p0 + pl; p < p1; p += plan) {
+      const float4 v = *(const float4*)(x + ((long)nimg * hw + p) * cs + g * 4);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
-    __syncthreads();
+  sh[threadIdx.x * 4 + 0] = acc.x;
+  sh[threadIdx.x * 4 + 1] = acc.y;
+  sh[threadIdx.x * 4 + 2] = acc.z;
+  sh[threadIdx.x * 4 + 3] = acc.w;
+  __syncthreads();
+  for (int ch = threadIdx.x; ch < c; ch += 256) {
+    const int gg = ch / 4, q = ch % 4;
+    double t = 0.0;
+    for (int k = 0; k < plan; ++k) t += sh[(k * cg + gg) * 4 + q];
+    part[((long)nimg * POOL_SPLIT + sp) * c + ch] = t;
   }
 }
 
 // s[n][c] = sigmoid(W2 relu(W1 mean + b1) + b2)  (conv_du of CALayer on the pooled [n, c, 1, 1] map)
-__global__ void ca_mlp_kernel(const double* __restrict__ part, long hw, int c, int cr, const float* __restrict__ w1,
+__global__ __launch_bounds__(1024) void ca_mlp_kernel(const double* __restrict__ part, long hw, int c, int cr, const float* __restrict__ w1,
                               const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2,
                               float* __restrict__ s) {
   extern __shared__ float sm[];
   float* mean = sm;      // [c]
   float* hid = sm + c;   // [cr]
+  constexpr int NT = 1024;
+  __shared__ double grp[NT];
   const int nimg = blockIdx.x;
-  for (int i = threadIdx.x; i < c; i += blockDim.x) {
+  const int cw = c < NT ? c : NT;  // channels per round
+  const int G = NT / cw;           // split groups summed in parallel, then combined in a fixed order
+  for (int c0 = 0; c0 < c; c0 += cw) {
+    const int i = c0 + (int)threadIdx.x % cw, gi = (int)threadIdx.x / cw;
     double t = 0.0;
-    for (int sp = 0; sp < POOL_SPLIT; ++sp) t += part[((long)nimg * POOL_SPLIT + sp) * c + i];
-    mean[i] = (float)(t / (double)hw);
+    if (i < c && gi < G)
+      for (int sp = gi; sp < POOL_SPLIT; sp += G) t += part[((long)nimg * POOL_SPLIT + sp) * c + i];
+    grp[threadIdx.x] = t;
+    __syncthreads();
+    if ((int)threadIdx.x < cw && c0 + (int)threadIdx.x < c) {
+      double m = 0.0;
+      for (int k = 0; k < G; ++k) m += grp[k * cw + threadIdx.x];
+      mean[c0 + threadIdx.x] = (float)(m / (double)hw);
+    }
+    __syncthreads();
   }
-  __syncthreads();
   for (int j = threadIdx.x; j < cr; j += blockDim.x) {
     float t = b1 ? b1[j] : 0.f;
     for (int i = 0; i < c; ++i) t += w1[j * c + i] * mean[i];
@@ -66,13 +83,14 @@ __global__ void ca_mlp_kernel(const double* __restrict__ part, long hw, int c, i
 
 extern "C" int climsr_channel_attention(const float* u, int n, int64_t hw, int c, int u_cstride, const float* w1, const float* b1,
                                         const float* w2, const float* b2, int cr, double* workspace, float* s, void* stream) {
-  if (!u || !w1 || !w2 || !workspace || !s || n <= 0 || hw <= 0 || c <= 0 || cr <= 0 || u_cstride < c) {
-    set_error("channel_attention: bad args");
+  if (!u || !w1 || !w2 || !workspace || !s || n <= 0 || hw <= 0 || c <= 0 || cr <= 0 || u_cstride < c || c % 4 || u_cstride % 4 ||
+      c > 1024) {
+    set_error("channel_attention: bad args (c, u_cstride multiples of 4, c <= 1024)");
     return CLIMSR_EINVAL;
   }
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(channel_sum_partial_kernel, dim3(POOL_SPLIT, n), dim3(256), 0, st, u, (long)hw, c, u_cstride, workspace);
-  hipLaunchKernelGGL(ca_mlp_kernel, dim3(n), dim3(256), (size_t)(c + cr) * sizeof(float), st, workspace, (long)hw, c, cr, w1, b1,
+  hipLaunchKernelGGL(ca_mlp_kernel, dim3(n), dim3(1024), (size_t)(c + cr) * sizeof(float), st, workspace, (long)hw, c, cr, w1, b1,
                      w2, b2, s);
   return check_launch("channel_attention");
 }

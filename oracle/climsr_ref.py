@@ -226,6 +226,38 @@ def generator_forward(p: Params, x: torch.Tensor, elev: torch.Tensor, mask: torc
     return srcnn_forward(p, torch.cat([out, elev, mask], 1))
 
 
+def pixel_shuffle(x: torch.Tensor, r: int) -> torch.Tensor:
+    """``nn.PixelShuffle(r)`` (rcan.py:33,40) as an explicit index map: out[c][y*r+i][x*r+j] = in[c*r*r+i*r+j][y][x]."""
+    n, c4, h, w = x.shape
+    c = c4 // (r * r)
+    return x.reshape(n, c, r, r, h, w).permute(0, 1, 4, 2, 5, 3).reshape(n, c, h * r, w * r)
+
+
+def rcan_forward(p: Params, x: torch.Tensor, elev: torch.Tensor, mask: torch.Tensor, n_resgroups: int, n_resblocks: int,
+                 scaling_factor: int = 4) -> torch.Tensor:
+    """``RCAN.forward`` (rcan.py:181-192): head, residual groups of RCABs with channel attention (rcan.py:50-107),
+    body skip, Upsampler (conv + PixelShuffle per x2 stage, or one x3 stage), last conv, SRCNN."""
+    h = _conv(p, "head.0", x)
+    t = h
+    for g in range(n_resgroups):
+        gin = t
+        for b in range(n_resblocks):
+            pre = f"body.{g}.body.{b}.body"
+            u = _conv(p, pre + ".2", F.relu(_conv(p, pre + ".0", t)))
+            y = u.mean(dim=(2, 3), keepdim=True)                                   # AdaptiveAvgPool2d(1)
+            y = torch.sigmoid(_conv(p, pre + ".3.conv_du.2", F.relu(_conv(p, pre + ".3.conv_du.0", y))))
+            t = u * y + t
+        t = _conv(p, f"body.{g}.body.{n_resblocks}", t) + gin
+    t = _conv(p, f"body.{n_resgroups}", t) + h
+    if scaling_factor in (2, 4):
+        for k in range(int(math.log2(scaling_factor))):
+            t = pixel_shuffle(_conv(p, f"tail.0.{2 * k}", t), 2)
+    else:
+        t = pixel_shuffle(_conv(p, "tail.0.0", t), 3)
+    out = _conv(p, "tail.1", t)
+    return srcnn_forward(p, torch.cat([out, elev, mask], 1))
+
+
 def batch_norm_train(x: torch.Tensor, p: Params, pre: str, training: bool, momentum: float = 0.1,
                      eps: float = 1e-5, update: bool = True) -> torch.Tensor:
     """``nn.BatchNorm2d`` (train: batch stats over N,H,W with biased var for normalisation, unbiased var
