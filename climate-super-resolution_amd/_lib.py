@@ -145,6 +145,8 @@ SIGNATURES = {
     "climsr_sr_metrics_workspace": (c_size_t, []),
     "climsr_sr_metrics": (c_int, [P(MetricsDesc), c_void_p]),
     "climsr_regression_accuracy_update": (c_int, [c_void_p, c_void_p, c_int64, c_float, c_void_p, c_void_p]),
+    "climsr_denormalize_mask": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_double, c_double, c_int, c_int64, c_void_p,
+                                        c_void_p]),
     "climsr_channel_attention_workspace": (c_size_t, [c_int, c_int]),
     "climsr_channel_attention": (c_int, [c_void_p, c_int, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                          c_void_p, c_void_p, c_void_p]),

@@ -22,6 +22,8 @@ from torch import Tensor
 
 from ..losses.l1 import L1Loss
 from ..metrics.sr_metrics import SRMetrics
+from .checkpoint import load_from_checkpoint as _load_from_checkpoint
+from .checkpoint import save_checkpoint as _save_checkpoint
 from .instantiator import HydraInstantiator
 from .optim import AdamW
 
@@ -40,6 +42,7 @@ class TaskSuperResolutionModule(_Base):
     def __init__(self, generator, optimizers: Optional[Dict[str, Any]] = None, schedulers: Optional[Dict[str, Any]] = None,
                  discriminator=None, instantiator=default_instantiator, **kwargs):
         super().__init__()
+        self._init_cfgs = dict(generator=generator, discriminator=discriminator, optimizers=optimizers, schedulers=schedulers)
         self.instantiator = instantiator
         self.optimizer_cfgs = optimizers or {}
         self.scheduler_cfgs = schedulers or {}
@@ -125,3 +128,23 @@ class TaskSuperResolutionModule(_Base):
         """hp_metric = mean of the epoch's val/rmse (task.py:387-391)."""
         hp_metric = torch.stack([o["val/rmse"] for o in outputs]).mean()
         self.log("hp_metric", hp_metric)
+
+    # -- checkpoints (Lightning layout, SURVEY §8f row 4; climsr_amd.core.checkpoint)
+    def hyper_parameters(self) -> Dict[str, Any]:
+        hp = dict(vars(self.hparams)) if hasattr(self.hparams, "__dict__") else dict(self.hparams)
+        for k, v in self._init_cfgs.items():
+            if isinstance(v, dict):  # Hydra configs (plain dicts); instantiated modules are not re-creatable
+                hp[k] = v
+        return hp
+
+    def save_checkpoint(self, path: str, epoch: int = 0, global_step: int = 0, optimizers=(), schedulers=()):
+        return _save_checkpoint(self, path, epoch, global_step, optimizers, schedulers, self.hyper_parameters())
+
+    if _Base is torch.nn.Module:
+        @classmethod
+        def load_from_checkpoint(cls, checkpoint_path: str, strict: bool = False, trusted: bool = False, map_location="cpu",
+                                 **kwargs):
+            """Lightning's ``load_from_checkpoint`` (inference.py:143, cli/train.py:92,115): hyper-parameters from the
+            file (overridable by kwargs), then the ``generator.`` / ``discriminator.`` weights."""
+            return _load_from_checkpoint(cls, checkpoint_path, strict=strict, trusted=trusted, map_location=map_location,
+                                         **kwargs)

@@ -572,3 +572,32 @@ extern "C" int climsr_regression_accuracy_update(const float* preds, const float
                      (unsigned long long*)counts);
   return check_launch("regression_accuracy");
 }
+
+// ------------------------------------------------------------------------------------------
+// Inference output (inference.py:73-80): MinMaxScaler.denormalize of the SR map with the grid's float64
+// min / max (numpy float64 arithmetic, one rounding to float32 at the end), NaN where the land mask is 0.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void denormalize_mask_kernel(const float* __restrict__ sr, const float* __restrict__ mask,
+                                                               const double* __restrict__ mn, const double* __restrict__ mx,
+                                                               double a, double b, double eps, long hw, long total,
+                                                               float* __restrict__ out) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int t = (int)(i / hw);
+  const double scale = __ddiv_rn(b - a, __dadd_rn(__dsub_rn(mx[t], mn[t]), eps));
+  const double add = __dsub_rn(a, __dmul_rn(mn[t], scale));
+  const float v = (float)__ddiv_rn(__dsub_rn((double)sr[i], add), scale);
+  out[i] = (mask && mask[i] == 0.f) ? NAN : v;
+}
+
+extern "C" int climsr_denormalize_mask(const float* sr, const float* mask, const double* min, const double* max, double range_a,
+                                       double range_b, int n, int64_t hw, float* out, void* stream) {
+  if (!sr || !min || !max || !out || n <= 0 || hw <= 0) {
+    set_error("denormalize_mask: bad args");
+    return CLIMSR_EINVAL;
+  }
+  const long total = (long)n * hw;
+  hipLaunchKernelGGL(denormalize_mask_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, sr, mask, min, max,
+                     range_a, range_b, 1e-8, (long)hw, total, out);
+  return check_launch("denormalize_mask");
+}

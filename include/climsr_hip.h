@@ -347,6 +347,11 @@ int climsr_sr_metrics(const ClimsrMetricsDesc* d, void* stream);
 int climsr_regression_accuracy_update(const float* preds, const float* target, int64_t n, float eps, int64_t* counts,
                                       void* stream);
 
+/* Inference output (inference.py:73-80): out = MinMaxScaler.denormalize(sr, min[t], max[t]) per sample t
+ * (float64 arithmetic, normalization.py:63-84) and NaN where mask == 0 (mask may be NULL).  [n][hw] fp32. */
+int climsr_denormalize_mask(const float* sr, const float* mask, const double* min, const double* max, double range_a,
+                            double range_b, int n, int64_t hw, float* out, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * RCAN (climsr/models/rcan.py).
  * --------------------------------------------------------------------------------------------- */

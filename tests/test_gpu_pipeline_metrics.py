@@ -166,3 +166,26 @@ def test_validation_step_through_task():
     assert float(batch["hr"][:, :, :10].abs().max()) == 0.0  # hr masked in place like task.py:290
     task.validation_epoch_end([out, out])
     assert abs(task.logged["hp_metric"].item() - out["val/rmse"].item()) < 1e-12
+
+
+def test_inference_denormalize_mask_and_writer(tmp_path):
+    """inference.py:73-80: float64 denormalisation of the SR map, NaN over the sea, one raster per grid."""
+    from climsr_amd.inference import denormalize_mask, inference_on_full_images
+
+    rs = np.random.RandomState(21)
+    sr = rs.rand(2, 1, 12, 20).astype(np.float32) * 2 - 1
+    mask = (rs.rand(2, 1, 12, 20) > 0.3).astype(np.float32)
+    mn, mx = np.array([-7.25, 1.5]), np.array([31.0, 17.75])
+    got = denormalize_mask(torch.from_numpy(sr).to(DEV), torch.from_numpy(mask).to(DEV), mn, mx).cpu().numpy()
+    want = np.where(mask > 0, dr.minmax_denormalize(sr, mn, mx), np.nan).astype(np.float32)
+    assert np.array_equal(np.isnan(got), np.isnan(want))
+    assert bits_equal(np.nan_to_num(got), np.nan_to_num(want))
+
+    class Identity(torch.nn.Module):
+        def forward(self, lr, elev, mask):
+            return lr[:, :1]
+
+    batch = {"lr": torch.from_numpy(sr).to(DEV), "elevation": torch.zeros(2, 1, 12, 20, device=DEV),
+             "mask": torch.from_numpy(mask).to(DEV), "min": mn, "max": mx, "filename": ["a.tif", "b.tif"]}
+    paths = inference_on_full_images(Identity(), [batch], str(tmp_path))
+    assert len(paths) == 2 and bits_equal(np.nan_to_num(np.load(paths[1])), np.nan_to_num(want[1, 0]))
