@@ -98,10 +98,12 @@ static bool pw_disabled() {
 }
 
 static bool pw_fits(int in_c, int ks, int out_c);
+static bool c64_fits(int in_c, int ks, int out_c, int stride);
 
 extern "C" int climsr_conv_chunk_ex(int in_c, int ks, int out_c, int stride) {
   if (stride == 1 && n16_shape(in_c, ks, out_c))  // conv_n16: one chunk, padded to 32/64/128
     return in_c <= 32 ? 32 : (in_c <= 64 ? 64 : 128);
+  if (c64_fits(in_c, ks, out_c, stride)) return in_c;  // conv_c64: the whole K in one chunk
   if (stride == 1 && pw_fits(in_c, ks, out_c)) return round_up(in_c, 8);  // conv_pw: the whole K in one chunk
   int cc = round_up(in_c, 8);
   FwdGeom g;
@@ -1583,6 +1585,179 @@ static int launch_pw(const FwdArgs& a0, const PwGeom& g, hipStream_t s) {
   return check_launch("conv2d_fwd (pw)");
 }
 
+// ------------------------------------------------------------------------------------------
+// 64-output 3x3 conv, stride 1, one channel chunk of 64 or 128 inputs (RDB conv5, the 128->64 pull gradient,
+// trunk_conv, HRconv and the 64->64 data gradients).  Built around the two rates that bound it:
+//  * A (weights) never touches LDS: wave w owns output channels 16w..16w+15 with ALL its 9 x Cin weight
+//    fragments in VGPRs for the whole launch (36 x Cin/32 registers);
+//  * every B fragment (16 pixels x 32 channels of one input row) read from LDS feeds the 3 output rows it
+//    touches (ky reuse): 0.42 LDS fragment reads per MFMA instead of 0.75-1 in the LDS-weight kernels;
+//  * the input tile is filled by global_load_lds (16 B per lane, no VGPR staging) into a lane-linear LDS image
+//    whose 16 B channel slots are XOR-swizzled by pixel (source address pre-swizzled, reads swizzled the same
+//    way: conflict-free ds_read_b128), double-buffered so tile t+1 lands while tile t computes; one barrier
+//    per tile.  Persistent XCD-aware tile walk, one workgroup per CU.
+// ------------------------------------------------------------------------------------------
+constexpr int C64_TH2 = 8;                       // output rows per tile
+constexpr int C64_IR = C64_TH2 + 2, C64_IC = TW + 2;  // input tile rows / columns
+__device__ __attribute__((aligned(16))) uint4 g_zero16[4];
+
+// Opt-in (CLIMSR_C64=1): measured 5-15 % slower than the generic kernel on conv5 / pull-x (one 4-wave workgroup per
+// CU cannot hide the LDS and epilogue latency) and mixed on the 256^2 64->64 convs (17 % faster than conv_pw in
+// isolation, slower inside the step).  Kept, parity-tested, as the starting point of a K-split 8-wave version.
+static bool c64_fits(int in_c, int ks, int out_c, int stride) {
+  static const bool on = getenv("CLIMSR_C64") != nullptr;
+  return on && ks == 3 && stride == 1 && out_c == 64 && (in_c == 64 || in_c == 128);
+}
+
+template <int NCH, bool SB>
+__global__ __launch_bounds__(256, NCH == 2 ? 2 : 1) void conv_c64_kernel(FwdArgs a) {
+  constexpr int CG = NCH * 4;                                   // 16 B channel slots per pixel
+  constexpr int NSLOT = C64_IR * C64_IC * CG;                   // slots of one input tile
+  constexpr int NINST = (NSLOT + 63) / 64;                      // glds instructions per tile (1 KiB each)
+  constexpr int BUF = NINST * 1024;                             // bytes of one LDS buffer
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
+
+  bf16x8 af[9][NCH];  // rows co = 16 wave + col, k = tap * cc + 32 c + 8 g
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) af[t][c] = *(const bf16x8*)(a.w + (long)(wave * 16 + col) * a.kpk + t * a.cc + c * 32 + g * 8);
+  const int co = wave * 16 + g * 4;
+  float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (a.bias) bv = make_float4(a.bias[co], a.bias[co + 1], a.bias[co + 2], a.bias[co + 3]);
+  const bool f1 = (a.res_f32 & 1) != 0, f2 = ((a.res_f32 >> 1) & 1) != 0;
+  const int ntiles = a.tiles_x * a.tiles_y * a.n;
+
+  // slot s -> (input row r, column px, stored channel group gs); the global source holds group gs ^ (px & 7)
+  auto issue = [&](int tile, int buf) {
+    int tt = tile;
+    const int tx = tt % a.tiles_x;
+    tt /= a.tiles_x;
+    const int ty = tt % a.tiles_y;
+    const int nimg = tt / a.tiles_y;
+    const int iy0 = ty * C64_TH2 - 1, ix0 = tx * TW - 1;
+    char* base = smem + buf * BUF;
+    for (int k = wave; k < NINST; k += 4) {
+      const int sl = k * 64 + lane;
+      const int pix = sl / CG, gs = sl - pix * CG;
+      const int r = pix / C64_IC, px = pix - r * C64_IC;
+      const int iy = iy0 + r, ix = ix0 + px;
+      const void* src = g_zero16;
+      if (sl < NSLOT && iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w)
+        src = a.x + (((long)nimg * a.in_h + iy) * a.in_w + ix) * a.in_cs + a.in_co + (gs ^ (px & 7)) * 8;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(base + k * 1024), 16, 0, 0);
+    }
+  };
+
+  const TileWalk walk(ntiles);
+  if (walk.first < walk.end) issue(walk.first, 0);
+  int buf = 0;
+  for (int tile = walk.first; tile < walk.end; tile += walk.step, buf ^= 1) {
+    __syncthreads();  // this tile's LDS image has landed (the barrier drains every wave's loads) and the
+                      // other buffer is no longer read (previous tile's compute is done)
+    if (tile + walk.step < walk.end) issue(tile + walk.step, buf ^ 1);
+    int tt = tile;
+    const int tx = tt % a.tiles_x;
+    tt /= a.tiles_x;
+    const int ty = tt % a.tiles_y;
+    const int nimg = tt / a.tiles_y;
+    const int oy0 = ty * C64_TH2, ox0 = tx * TW;
+
+    f32x4 acc[C64_TH2];
+#pragma unroll
+    for (int m = 0; m < C64_TH2; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const char* xb = smem + buf * BUF;
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const int px = col + kx;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int gsw = ((c * 4 + g) ^ (px & 7)) * 16;
+        bf16x8 b[C64_IR];
+#pragma unroll
+        for (int r = 0; r < C64_IR; ++r) b[r] = *(const bf16x8*)(xb + (r * C64_IC + px) * (CG * 16) + gsw);
+        if (SB) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int r = 0; r < C64_IR; ++r)
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky) {
+            const int m = r - ky;
+            if (m >= 0 && m < C64_TH2) acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ky * 3 + kx][c], b[r], acc[m], 0, 0, 0);
+          }
+      }
+    }
+    // epilogue: lane owns channels co..co+3 of pixel (oy0 + m, ox0 + col)
+    const int ox = ox0 + col;
+    if (ox >= a.out_w) continue;
+#pragma unroll
+    for (int m = 0; m < C64_TH2; ++m) {
+      const int oy = oy0 + m;
+      if (oy >= a.out_h) break;
+      const long pidx = ((long)nimg * a.out_h + oy) * a.out_w + ox;
+      const uint4 r1 = a.res1 ? load_res4(a.res1, f1, pidx * a.r1_cs + a.r1_co + co) : make_uint4(0, 0, 0, 0);
+      const uint4 r2 = a.res2 ? load_res4(a.res2, f2, pidx * a.r2_cs + a.r2_co + co) : make_uint4(0, 0, 0, 0);
+      const long ob = pidx * a.out_cs + a.out_co + co;
+      float4 old = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (a.out_mode == 2) old = *(const float4*)((const float*)a.y + ob);
+      const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        v[i] = ep_res(act_apply(acc[m][i] + bb[i], a.act, a.slope), a.act, a.slope, a.res1 != nullptr, res4_at(r1, f1, i), a.alpha1,
+                      a.beta1, a.res2 != nullptr, res4_at(r2, f2, i), a.alpha2, a.beta2);
+      if (a.out_mode == 0) {
+        uint2 pk;
+        pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        *(uint2*)((uint16_t*)a.y + ob) = pk;
+      } else {
+        *(float4*)((float*)a.y + ob) = make_float4(old.x + v[0], old.y + v[1], old.z + v[2], old.w + v[3]);
+      }
+      if (a.aux) {
+        uint2 pk;
+        pk.x = (uint32_t)f2bf(a.aux_scale * v[0]) | ((uint32_t)f2bf(a.aux_scale * v[1]) << 16);
+        pk.y = (uint32_t)f2bf(a.aux_scale * v[2]) | ((uint32_t)f2bf(a.aux_scale * v[3]) << 16);
+        *(uint2*)(a.aux + pidx * a.aux_cs + a.aux_co + co) = pk;
+      }
+    }
+  }
+}
+
+template <int NCH>
+static int launch_c64(const FwdArgs& a0, hipStream_t s) {
+  static const bool sb = getenv("CLIMSR_C64_SB") != nullptr;
+  static const int wpc = getenv("CLIMSR_C64_WPC") ? atoi(getenv("CLIMSR_C64_WPC")) : (NCH == 2 ? 2 : 1);
+  if (g_dry) {
+    snprintf(g_dry_name, sizeof(g_dry_name), "conv_c64_kernel<%d, %s>", NCH, sb ? "true" : "false");
+    return CLIMSR_OK;
+  }
+  FwdArgs a = a0;
+  a.tiles_x = ceil_div(a.out_w, TW);
+  a.tiles_y = ceil_div(a.out_h, C64_TH2);
+  constexpr int NINST = (C64_IR * C64_IC * NCH * 4 + 63) / 64;
+  const size_t lds = (size_t)2 * NINST * 1024;
+  auto k = sb ? conv_c64_kernel<NCH, true> : conv_c64_kernel<NCH, false>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)conv_c64_kernel<NCH, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)conv_c64_kernel<NCH, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (ncu <= 0) ncu = 256;
+  }
+  const int ntiles = a.tiles_x * a.tiles_y * a.n;
+  const int grid = ntiles < wpc * ncu ? ntiles : wpc * ncu;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, s, a);
+  return check_launch("conv2d_fwd (c64)");
+}
+
 template <int MW, int NT>
 static int launch_fwd(const FwdArgs& a, int ncob, size_t lds, hipStream_t s) {
   dim3 grid(a.tiles_x * a.tiles_y * a.n, ncob);
@@ -1690,6 +1865,10 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
       default: return launch_co64<4>(a, s);
     }
   }
+  if (c64_fits(d->in_c, d->ks, d->out_c, d->stride) && d->cc == d->in_c && d->pad == 1 && d->up == 1 && !ep->down2 &&
+      d->out_h == d->in_h && d->out_w == d->in_w && ((d->out_cstride | d->out_coff) & 3) == 0 &&
+      (!ep->res1 || ((ep->res1_cstride | ep->res1_coff) & 3) == 0) && (!ep->res2 || ((ep->res2_cstride | ep->res2_coff) & 3) == 0))
+    return d->in_c == 128 ? launch_c64<4>(a, s) : launch_c64<2>(a, s);
   {  // weights-resident persistent kernel for one-chunk convs with 17..64 outputs (large-pixel-count layers)
     const int nt = fwd_nt(d->out_c);
     const long npx = (long)d->n * d->out_h * d->out_w;
