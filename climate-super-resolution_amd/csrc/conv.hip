@@ -1758,6 +1758,188 @@ static int launch_c64(const FwdArgs& a0, hipStream_t s) {
   return check_launch("conv2d_fwd (c64)");
 }
 
+// ------------------------------------------------------------------------------------------
+// 1x1 conv as a streaming GEMM (srcnn.conv2 64->32 and its 32->64 data gradient with the ReLU mask):
+// out[p][co] = epilogue(sum_ci x[p][ci] w[co][ci]).  Nothing is reused across pixels except the weights, so
+// nothing goes through LDS: the weight fragments sit in VGPRs, each lane loads its 16 B channel slice of a
+// pixel straight into the B fragment (16 pixels x 32 channels per load round), U groups of 16 pixels are in
+// flight per wave, and the fused epilogue stores 4 consecutive channels per lane.  HBM-bound by design.
+// ------------------------------------------------------------------------------------------
+constexpr int PT_U = 4;  // 16-pixel groups per wave iteration
+
+static bool pt_shape(const ClimsrConvDesc* d, const ClimsrEpilogue* ep) {
+  return d->ks == 1 && d->stride == 1 && d->up == 1 && d->pad == 0 && !ep->down2 && d->in_c % 32 == 0 && d->in_c <= 128 &&
+         d->cc == d->in_c && d->out_c % 16 == 0 && d->out_c <= 64 && d->out_h == d->in_h && d->out_w == d->in_w &&
+         ((d->out_cstride | d->out_coff) & 3) == 0 && (!ep->res1 || ((ep->res1_cstride | ep->res1_coff) & 3) == 0) &&
+         (!ep->res2 || ((ep->res2_cstride | ep->res2_coff) & 3) == 0) && !getenv("CLIMSR_NO_PT");
+}
+
+template <int NCOF, int NKC>
+__global__ __launch_bounds__(256) void conv_pt_kernel(FwdArgs a, long npix) {
+  __shared__ float tsm[NCOF == 4 ? 4 * 16 * 68 : 1];
+  const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
+  bf16x8 af[NCOF][NKC];
+#pragma unroll
+  for (int f = 0; f < NCOF; ++f)
+#pragma unroll
+    for (int k = 0; k < NKC; ++k) af[f][k] = *(const bf16x8*)(a.w + (long)(f * 16 + col) * a.kpk + k * 32 + g * 8);
+  float bb[NCOF][4];
+#pragma unroll
+  for (int f = 0; f < NCOF; ++f)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bb[f][i] = a.bias ? a.bias[f * 16 + g * 4 + i] : 0.f;
+  const bool f1 = (a.res_f32 & 1) != 0, f2 = ((a.res_f32 >> 1) & 1) != 0;
+  const long ngroups = (npix + 15) / 16;
+  const long wave_id = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
+  for (long g0 = wave_id * PT_U; g0 < ngroups; g0 += nwaves * PT_U) {
+    bf16x8 bx[PT_U][NKC];
+#pragma unroll
+    for (int u = 0; u < PT_U; ++u) {
+      const long p = (g0 + u) * 16 + col;
+#pragma unroll
+      for (int k = 0; k < NKC; ++k) {
+        bx[u][k] = (bf16x8){};
+        if (p < npix) bx[u][k] = *(const bf16x8*)(a.x + p * a.in_cs + a.in_co + k * 32 + g * 8);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < PT_U; ++u) {
+      const long p = (g0 + u) * 16 + col;
+      f32x4 acc[NCOF];
+#pragma unroll
+      for (int f = 0; f < NCOF; ++f) {
+        acc[f] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < NKC; ++k) acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[f][k], bx[u][k], acc[f], 0, 0, 0);
+      }
+      if (NCOF == 4) {  // 64 outputs: transpose through this wave's LDS so each lane owns 16 channels of one pixel and a
+                        // store instruction covers whole 128 B lines (the 8 B-per-lane layout touches 16 lines per store)
+        float* tw = tsm + (threadIdx.x >> 6) * (16 * 68);
+#pragma unroll
+        for (int f = 0; f < NCOF; ++f)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) tw[col * 68 + f * 16 + g * 4 + i] = acc[f][i];
+        const int pp = lane >> 2, c0 = (lane & 3) * 16;
+        const long q = (g0 + u) * 16 + pp;
+        float v[16];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const f32x4 t4 = *(const f32x4*)(tw + pp * 68 + c0 + 4 * j);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[4 * j + i] = t4[i];
+        }
+        if (q < npix) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int co = c0 + 4 * j;
+            const uint4 r1 = a.res1 ? load_res4(a.res1, f1, q * a.r1_cs + a.r1_co + co) : make_uint4(0, 0, 0, 0);
+            const uint4 r2 = a.res2 ? load_res4(a.res2, f2, q * a.r2_cs + a.r2_co + co) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float bsv = a.bias ? a.bias[co + i] : 0.f;
+              v[4 * j + i] = ep_res(act_apply(v[4 * j + i] + bsv, a.act, a.slope), a.act, a.slope, a.res1 != nullptr,
+                                    res4_at(r1, f1, i), a.alpha1, a.beta1, a.res2 != nullptr, res4_at(r2, f2, i), a.alpha2, a.beta2);
+            }
+          }
+          const long ob = q * a.out_cs + a.out_co + c0;
+          if (a.out_mode == 0) {
+            uint4 w0, w1;
+            w0.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+            w0.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+            w0.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+            w0.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+            w1.x = (uint32_t)f2bf(v[8]) | ((uint32_t)f2bf(v[9]) << 16);
+            w1.y = (uint32_t)f2bf(v[10]) | ((uint32_t)f2bf(v[11]) << 16);
+            w1.z = (uint32_t)f2bf(v[12]) | ((uint32_t)f2bf(v[13]) << 16);
+            w1.w = (uint32_t)f2bf(v[14]) | ((uint32_t)f2bf(v[15]) << 16);
+            *(uint4*)((uint16_t*)a.y + ob) = w0;
+            *(uint4*)((uint16_t*)a.y + ob + 8) = w1;
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+              if (a.out_mode == 2) o = *(const float4*)((const float*)a.y + ob + 4 * j);
+              *(float4*)((float*)a.y + ob + 4 * j) =
+                  make_float4(o.x + v[4 * j], o.y + v[4 * j + 1], o.z + v[4 * j + 2], o.w + v[4 * j + 3]);
+            }
+          }
+          if (a.aux) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              uint2 pk;
+              pk.x = (uint32_t)f2bf(a.aux_scale * v[4 * j]) | ((uint32_t)f2bf(a.aux_scale * v[4 * j + 1]) << 16);
+              pk.y = (uint32_t)f2bf(a.aux_scale * v[4 * j + 2]) | ((uint32_t)f2bf(a.aux_scale * v[4 * j + 3]) << 16);
+              *(uint2*)(a.aux + q * a.aux_cs + a.aux_co + c0 + 4 * j) = pk;
+            }
+          }
+        }
+        continue;
+      }
+      if (p >= npix) continue;
+#pragma unroll
+      for (int f = 0; f < NCOF; ++f) {
+        const int co = f * 16 + g * 4;
+        if (co >= a.out_c) continue;
+        const uint4 r1 = a.res1 ? load_res4(a.res1, f1, p * a.r1_cs + a.r1_co + co) : make_uint4(0, 0, 0, 0);
+        const uint4 r2 = a.res2 ? load_res4(a.res2, f2, p * a.r2_cs + a.r2_co + co) : make_uint4(0, 0, 0, 0);
+        const long ob = p * a.out_cs + a.out_co + co;
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          v[i] = ep_res(act_apply(acc[f][i] + bb[f][i], a.act, a.slope), a.act, a.slope, a.res1 != nullptr, res4_at(r1, f1, i),
+                        a.alpha1, a.beta1, a.res2 != nullptr, res4_at(r2, f2, i), a.alpha2, a.beta2);
+        if (a.out_mode == 0) {
+          uint2 pk;
+          pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+          pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+          *(uint2*)((uint16_t*)a.y + ob) = pk;
+        } else {
+          float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (a.out_mode == 2) o = *(const float4*)((const float*)a.y + ob);
+          *(float4*)((float*)a.y + ob) = make_float4(o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]);
+        }
+        if (a.aux) {
+          uint2 pk;
+          pk.x = (uint32_t)f2bf(a.aux_scale * v[0]) | ((uint32_t)f2bf(a.aux_scale * v[1]) << 16);
+          pk.y = (uint32_t)f2bf(a.aux_scale * v[2]) | ((uint32_t)f2bf(a.aux_scale * v[3]) << 16);
+          *(uint2*)(a.aux + p * a.aux_cs + a.aux_co + co) = pk;
+        }
+      }
+    }
+  }
+}
+
+template <int NCOF, int NKC>
+static int launch_pt(const FwdArgs& a, hipStream_t s) {
+  if (g_dry) {
+    snprintf(g_dry_name, sizeof(g_dry_name), "conv_pt_kernel<%d, %d>", NCOF, NKC);
+    return CLIMSR_OK;
+  }
+  const long npix = (long)a.n * a.out_h * a.out_w;
+  const long groups = (npix + 15) / 16;
+  long blocks = (groups + 4 * PT_U - 1) / (4 * PT_U);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL((conv_pt_kernel<NCOF, NKC>), dim3((unsigned)blocks), dim3(256), 0, s, a, npix);
+  return check_launch("conv2d_fwd (pt)");
+}
+
+static int dispatch_pt(const ClimsrConvDesc* d, const FwdArgs& a, hipStream_t s) {
+  const int ncof = (d->out_c + 15) / 16, nkc = d->in_c / 32;
+  switch (ncof * 10 + nkc) {
+    case 11: return launch_pt<1, 1>(a, s);
+    case 12: return launch_pt<1, 2>(a, s);
+    case 14: return launch_pt<1, 4>(a, s);
+    case 21: return launch_pt<2, 1>(a, s);
+    case 22: return launch_pt<2, 2>(a, s);
+    case 24: return launch_pt<2, 4>(a, s);
+    case 41: return launch_pt<4, 1>(a, s);
+    case 42: return launch_pt<4, 2>(a, s);
+    case 44: return launch_pt<4, 4>(a, s);
+    default: set_error("conv_pt: no instance for %d outputs / %d inputs", d->out_c, d->in_c); return CLIMSR_EINVAL;
+  }
+}
+
 template <int MW, int NT>
 static int launch_fwd(const FwdArgs& a, int ncob, size_t lds, hipStream_t s) {
   dim3 grid(a.tiles_x * a.tiles_y * a.n, ncob);
@@ -1865,6 +2047,9 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
       default: return launch_co64<4>(a, s);
     }
   }
+  if (pt_shape(d, ep) && (d->out_c == 16 || d->out_c == 32 || d->out_c == 64) &&
+      (d->in_c == 32 || d->in_c == 64 || d->in_c == 128))
+    return dispatch_pt(d, a, s);
   if (c64_fits(d->in_c, d->ks, d->out_c, d->stride) && d->cc == d->in_c && d->pad == 1 && d->up == 1 && !ep->down2 &&
       d->out_h == d->in_h && d->out_w == d->in_w && ((d->out_cstride | d->out_coff) & 3) == 0 &&
       (!ep->res1 || ((ep->res1_cstride | ep->res1_coff) & 3) == 0) && (!ep->res2 || ((ep->res2_cstride | ep->res2_coff) & 3) == 0))
