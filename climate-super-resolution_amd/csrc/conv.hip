@@ -1813,23 +1813,24 @@ __global__ __launch_bounds__(256) void conv_pt_kernel(FwdArgs a, long npix) {
 #pragma unroll
         for (int k = 0; k < NKC; ++k) acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[f][k], bx[u][k], acc[f], 0, 0, 0);
       }
-      if (NCOF == 4) {  // 64 outputs: transpose through this wave's LDS so each lane owns 16 channels of one pixel and a
-                        // store instruction covers whole 128 B lines (the 8 B-per-lane layout touches 16 lines per store)
+      if (NCOF == 4) {  // transpose through this wave's LDS so each lane owns 16 channels of one pixel and a store
+                        // instruction covers whole lines (the 8 B-per-lane MFMA layout touches 16 lines per store)
         float* tw = tsm + (threadIdx.x >> 6) * (16 * 68);
 #pragma unroll
         for (int f = 0; f < NCOF; ++f)
 #pragma unroll
           for (int i = 0; i < 4; ++i) tw[col * 68 + f * 16 + g * 4 + i] = acc[f][i];
-        const int pp = lane >> 2, c0 = (lane & 3) * 16;
+        const int pp = lane / NCOF, c0 = (lane % NCOF) * 16;  // NCOF lanes per pixel
         const long q = (g0 + u) * 16 + pp;
         float v[16];
+        const int ppr = pp < 16 ? pp : 15;  // lanes beyond the 16 pixels (NCOF 2) read a valid row and store nothing
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const f32x4 t4 = *(const f32x4*)(tw + pp * 68 + c0 + 4 * j);
+          const f32x4 t4 = *(const f32x4*)(tw + ppr * 68 + c0 + 4 * j);
 #pragma unroll
           for (int i = 0; i < 4; ++i) v[4 * j + i] = t4[i];
         }
-        if (q < npix) {
+        if (pp < 16 && q < npix) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int co = c0 + 4 * j;
