@@ -2335,13 +2335,18 @@ constexpr int W64_TPH = W64_TH + 2, W64_TPW = TW + 2;
 constexpr int W64_P = 64 + 8;  // LDS pixel pitch (channels) of both tiles
 constexpr int W64_NZ = W64_TH * TW * 8;              // 16 B vectors of a dz tile (128 px x 64 ch)
 constexpr int W64_NX = W64_TPH * W64_TPW * 8;         // of an x tile (180 px x 64 ch)
-constexpr int W64_VZ = W64_NZ / 256, W64_VX = (W64_NX + 255) / 256;
 
-__global__ __launch_bounds__(256, 1) void conv_wgrad64_kernel(WgArgs a) {
+// TS = 2: 8 waves, wave w owns ci block w & 3 and taps [0,5) or [5,9) (w >> 2): 20 accumulators instead of 36, so
+// two waves share each SIMD (latency hiding) at the price of each wave re-reading the shared dz fragments.
+template <int TS>
+__global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
+  constexpr int NTHR = 256 * TS, NU = TS == 1 ? 9 : 5;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint16_t* zs = (uint16_t*)smem;                       // [128 px][W64_P]
   uint16_t* xs = zs + W64_TH * TW * W64_P;              // [180 px][W64_P]
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
+  const int wave = (tid >> 6) & 3, tg = TS == 1 ? 0 : tid >> 8;  // ci block, tap group
+  const int u0 = tg * 5;
   const int q = (lane & 15) >> 2, p = lane & 3, col = lane & 15;
   const int cib = blockIdx.x % a.ncib, cob = blockIdx.x / a.ncib;
   const int split = blockIdx.y;
@@ -2350,21 +2355,29 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad64_kernel(WgArgs a) {
   const int lh = a.in_h * a.up, lw = a.in_w * a.up;
   const int upsh = a.up == 2 ? 1 : 0;
 
-  f32x4 acc[4][9], accb[4];
+  f32x4 acc[4][NU], accb[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     accb[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int u = 0; u < 9; ++u) acc[t][u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < NU; ++u) acc[t][u] = (f32x4){0.f, 0.f, 0.f, 0.f};
   }
   bf16x8 ones;
 #pragma unroll
   for (int i = 0; i < 8; ++i) ones[i] = (__bf16)1.0f;
-  int tapoff[9];
+  int tapoff[NU];
 #pragma unroll
-  for (int u = 0; u < 9; ++u) tapoff[u] = ((u / 3) * W64_TPW + (u % 3)) * W64_P + wave * 16 + 4 * p;
+  for (int u = 0; u < NU; ++u) {
+    if constexpr (TS == 1) {
+      tapoff[u] = ((u / 3) * W64_TPW + (u % 3)) * W64_P + wave * 16 + 4 * p;
+    } else {
+      const int tp = u0 + u < 9 ? u0 + u : 8;
+      tapoff[u] = ((tp / 3) * W64_TPW + (tp % 3)) * W64_P + wave * 16 + 4 * p;
+    }
+  }
 
-  uint4 pz[W64_VZ], px[W64_VX];
+  constexpr int VZ = W64_NZ / NTHR, VX = (W64_NX + NTHR - 1) / NTHR;
+  uint4 pz[VZ], px[VX];
   auto issue = [&](int tile) {
     int tt = tile;
     const int tx = tt % a.tiles_x;
@@ -2373,8 +2386,8 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad64_kernel(WgArgs a) {
     const int nimg = tt / a.tiles_y;
     const int oy0 = ty * W64_TH, ox0 = tx * TW;
 #pragma unroll
-    for (int i = 0; i < W64_VZ; ++i) {  // dz: pixel v/8, channel group v%8
-      const int v = tid + 256 * i;
+    for (int i = 0; i < VZ; ++i) {  // dz: pixel v/8, channel group v%8
+      const int v = tid + NTHR * i;
       const int pix = v >> 3, cg = v & 7;
       const int oy = oy0 + (pix >> 4), ox = ox0 + (pix & 15);
       pz[i] = make_uint4(0, 0, 0, 0);
@@ -2382,8 +2395,8 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad64_kernel(WgArgs a) {
         pz[i] = *(const uint4*)(a.dz + (((long)nimg * a.out_h + oy) * a.out_w + ox) * a.dz_cs + co0 + cg * 8);
     }
 #pragma unroll
-    for (int i = 0; i < W64_VX; ++i) {
-      const int v = tid + 256 * i;
+    for (int i = 0; i < VX; ++i) {
+      const int v = tid + NTHR * i;
       const int pix = v >> 3, cg = v & 7;
       const int py = pix / W64_TPW, pxx = pix - py * W64_TPW;
       const int iy = oy0 - a.pad + py, ix = ox0 - a.pad + pxx;
@@ -2398,13 +2411,13 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad64_kernel(WgArgs a) {
   for (; tile < a.ntiles; tile += a.nsplit) {
     __syncthreads();  // previous tile's fragment reads done
 #pragma unroll
-    for (int i = 0; i < W64_VZ; ++i) {
-      const int v = tid + 256 * i;
+    for (int i = 0; i < VZ; ++i) {
+      const int v = tid + NTHR * i;
       *(uint4*)(zs + (v >> 3) * W64_P + (v & 7) * 8) = pz[i];
     }
 #pragma unroll
-    for (int i = 0; i < W64_VX; ++i) {
-      const int v = tid + 256 * i;
+    for (int i = 0; i < VX; ++i) {
+      const int v = tid + NTHR * i;
       if (v < W64_NX) *(uint4*)(xs + (v >> 3) * W64_P + (v & 7) * 8) = px[i];
     }
     if (tile + a.nsplit < a.ntiles) issue(tile + a.nsplit);
@@ -2421,13 +2434,14 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad64_kernel(WgArgs a) {
         const short v8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         af[t] = __builtin_bit_cast(bf16x8, v8);
       }
-      if (do_bias && wave == 0) {
+      if (do_bias && wave == 0 && tg == 0) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) accb[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], ones, accb[t], 0, 0, 0);
       }
       const int xb0 = ((k0 >> 4) * W64_TPW + (k0 & 15)) * W64_P, xb1 = ((k1 >> 4) * W64_TPW + (k1 & 15)) * W64_P;
 #pragma unroll
-      for (int u = 0; u < 9; ++u) {
+      for (int u = 0; u < NU; ++u) {
+        if (TS == 2 && u == NU - 1 && tg == 1) continue;  // tap group 1 has 4 taps (5..8)
         const s16x4 lo = ds_read_tr16(xs + xb0 + tapoff[u]);
         const s16x4 hi = ds_read_tr16(xs + xb1 + tapoff[u]);
         const short v8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -2447,8 +2461,11 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad64_kernel(WgArgs a) {
       const int co = co0 + t * 16 + g * 4 + i;
       float* row = slab + (long)co * a.kw + ci * 9;
 #pragma unroll
-      for (int u = 0; u < 9; ++u) row[u] = acc[t][u][i];
-      if (do_bias && wave == 0 && col == 0) a.bpart[(long)split * a.co_rows + co] = accb[t][i];
+      for (int u = 0; u < NU; ++u) {
+        if constexpr (TS == 1) row[u] = acc[t][u][i];
+        else if (u0 + u < 9) row[u0 + u] = acc[t][u][i];
+      }
+      if (do_bias && wave == 0 && tg == 0 && col == 0) a.bpart[(long)split * a.co_rows + co] = accb[t][i];
     }
   }
 }
@@ -2722,12 +2739,20 @@ extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, c
     static int ablate = getenv("CLIMSR_ABLATE") ? atoi(getenv("CLIMSR_ABLATE")) : 0;
     a.ablate = ablate;
     const size_t lds = (size_t)(W64_TH * TW + W64_TPH * W64_TPW) * W64_P * 2;
+    // 8 waves (tap-split) pay off on the large-pixel-count convs (HRconv / upconv at 256^2: +8 %) and lose on the
+    // 64^2 dense-block GEMM (-19 %), measured with tests/perf_conv.py
+    static const int ts2_env = getenv("CLIMSR_W64_TS2") ? atoi(getenv("CLIMSR_W64_TS2")) : -1;
+    const bool ts2 = ts2_env >= 0 ? ts2_env != 0 : (long)d->n * d->out_h * d->out_w >= (1L << 20);
     static bool attr_set = false;
     if (!attr_set) {
-      (void)hipFuncSetAttribute((const void*)conv_wgrad64_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)conv_wgrad64_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)conv_wgrad64_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       attr_set = true;
     }
-    hipLaunchKernelGGL(conv_wgrad64_kernel, dim3((d->out_c / 64) * (d->in_c / 64), nsplit), dim3(256), lds, (hipStream_t)stream, a);
+    if (ts2)
+      hipLaunchKernelGGL(conv_wgrad64_kernel<2>, dim3((d->out_c / 64) * (d->in_c / 64), nsplit), dim3(512), lds, (hipStream_t)stream, a);
+    else
+      hipLaunchKernelGGL(conv_wgrad64_kernel<1>, dim3((d->out_c / 64) * (d->in_c / 64), nsplit), dim3(256), lds, (hipStream_t)stream, a);
     return check_launch("conv2d_wgrad (64x64 block)");
   }
   WgPlan w;
