@@ -46,6 +46,11 @@ def fwd_kernel_name(out_c: int, out_h: int = 16, res_f32: bool = False, cin: int
 
 
 def wgrad_kernel_name(out_c: int, ks: int, ci4: bool = False, cin: int = 0, stride: int = 1, pad: int = 1) -> str:
+    """Mirrors climsr_conv2d_wgrad's dispatch (profiler labels only)."""
+    if ks == 1 and stride == 1 and pad == 0 and cin == 64 and out_c % 16 == 0 and out_c <= 64:
+        return f"conv_wgrad_pt_kernel<{out_c // 16}>"
+    if out_c == 1 and stride == 1 and ks in (3, 5) and pad == ks // 2 and cin % 16 == 0 and cin <= 64:
+        return f"conv_wgrad_co1m_kernel<{ks}, {cin // 16}>"
     if ks == 3 and stride == 1 and pad == 1 and out_c % 64 == 0 and cin % 64 == 0 and cin >= 64:
         return "conv_wgrad64_kernel"
     rows = round_up(out_c, 16)

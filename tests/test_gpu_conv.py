@@ -186,6 +186,26 @@ def test_conv_wgrad_single_output_channel(cin, ks, n, h, w):
     check_close(p.gb.cpu(), gb, tol=2e-5, what="bgrad co1")
 
 
+@pytest.mark.parametrize("cout,n,h,w", [(32, 3, 70, 150), (64, 2, 33, 47), (16, 1, 9, 13)])
+def test_conv_wgrad_1x1_single_pass(cout, n, h, w):
+    """srcnn.conv2-shaped 1x1 weight gradient (64 inputs) on the single-pass pixel-range kernel, ragged chunks."""
+    p, wt, b = make_plan(64, cout, 1)
+    g = torch.Generator().manual_seed(10)
+    x = bf(torch.rand((n, 64, h, w), generator=g) * 2 - 1)
+    dz = bf(torch.rand((n, cout, h, w), generator=g) * 2 - 1)
+    xb, dzb = to_nhwc(x), to_nhwc(dz)
+    p.gw = torch.zeros_like(p.weight)
+    p.gb = torch.zeros_like(p.bias)
+    p.wgrad(xb, xb.shape[-1], 0, h, w, dzb, dzb.shape[-1], n, Workspace(), accumulate=False)
+    torch.cuda.synchronize()
+    wr = bf(wt).double().requires_grad_(True)
+    br = b.double().requires_grad_(True)
+    y = F.conv2d(x.double(), wr, br)
+    gw, gb = torch.autograd.grad(y, (wr, br), dz.double())
+    check_close(p.gw.cpu(), gw, tol=2e-5, what="wgrad 1x1")
+    check_close(p.gb.cpu(), gb, tol=2e-5, what="bgrad 1x1")
+
+
 def test_act_grad():
     n, h, w = 2, 8, 8
     g = torch.Generator().manual_seed(6)
