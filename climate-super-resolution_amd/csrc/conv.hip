@@ -2113,7 +2113,10 @@ struct WgArgs {
 // channels per pixel and a B fragment's 16 columns are (4 taps x 4 channels): in the transposed read
 // each lane group p points at its own tap, so 81 taps need 21 fragments instead of 81 mostly-zero ones.
 // TB then counts tap groups of 4.
-template <int NTC, int TB, int CI4>
+// WS (wave-split taps, CI4 9x9 = srcnn.conv1): one workgroup covers ALL tap groups, wave w owns groups
+// [TB w, TB w + TB) over every pixel of the tile, so dz is read once per launch (the tap-blocked form re-reads it
+// per block: 1 GB fetched for 0.3 GB of data) and no cross-wave reduction is needed.
+template <int NTC, int TB, int CI4, bool WS = false>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint16_t* xs = (uint16_t*)smem;
@@ -2136,10 +2139,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs a) {
   const int split = blockIdx.y;
   const int ci0 = cib * 16;
   const int co0 = cob * NTC * 16;
-  const int tap0 = tb * TB * (CI4 ? 4 : 1);
+  const int tap0 = (WS ? wave : tb) * TB * (CI4 ? 4 : 1);
   constexpr int XP = CI4 ? 4 : WG_XP;  // LDS x-tile pixel pitch (channels)
   const int ks2 = a.ks * a.ks;
-  const bool do_bias = (cib == 0 && tb == 0 && a.bpart != nullptr);
+  const bool do_bias = (cib == 0 && tb == 0 && a.bpart != nullptr) && (!WS || wave == 0);
 
   f32x4 acc[NTC][TB];
   f32x4 accb[NTC];
@@ -2250,9 +2253,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs a) {
     }
     __syncthreads();
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < (WS ? 8 : 2); ++s) {
       if (a.ablate & 2) break;
-      const int kk = wave * 2 + s;  // k-step: output pixel rows 2kk, 2kk+1 of the tile
+      const int kk = WS ? s : wave * 2 + s;  // k-step: output pixel rows 2kk, 2kk+1 of the tile
       // pixel handled as row q (+4) of this lane's tr reads
       const int k0 = kk * 32 + 8 * g + q;
       const int k1 = k0 + 4;
@@ -2285,7 +2288,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs a) {
 
   // cross-wave reduction through LDS (waves 1..3 -> wave 0)
   constexpr int NF = NTC * TB;
-  for (int r = 1; r < 4; ++r) {
+  for (int r = 1; r < (WS ? 1 : 4); ++r) {
     __syncthreads();
     if (wave == r) {
 #pragma unroll
@@ -2305,7 +2308,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs a) {
       }
     }
   }
-  if (wave != 0) return;
+  if (!WS && wave != 0) return;
   const int ci = CI4 ? (col & 3) : ci0 + col;
   float* slab = a.part + (long)split * a.co_rows * a.kw;
 #pragma unroll
@@ -2755,6 +2758,10 @@ static void wg_plan(const ClimsrConvDesc* d, WgPlan* w) {
   if (red > w->lds_total) w->lds_total = red;
 }
 
+static bool wg_ws(const ClimsrConvDesc* d, const WgPlan& w) {
+  return w.ci4 && d->ks == 9 && w.ncob == 1 && w.ntc == 4 && d->stride == 1 && !getenv("CLIMSR_NO_WGWS");
+}
+
 extern "C" int climsr_conv2d_wgrad_splits(const ClimsrConvDesc* d) {
   if (wpt_shape(d)) return wpt_splits(d);
   if (wco1_shape(d) && !getenv("CLIMSR_NO_CO1M")) return wco1_splits(d);
@@ -2767,7 +2774,7 @@ extern "C" int climsr_conv2d_wgrad_splits(const ClimsrConvDesc* d) {
   }
   WgPlan w;
   wg_plan(d, &w);
-  int base = w.ntapb * w.ncib * w.ncob;
+  int base = wg_ws(d, w) ? 1 : w.ntapb * w.ncib * w.ncob;
   int ns = ceil_div(512, base);
   if (ns > w.ntiles) ns = w.ntiles;
   if (ns < 1) ns = 1;
@@ -2891,6 +2898,17 @@ extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, c
   a.ablate = ablate;
   int nblk = w.ntapb * w.ncib * w.ncob;
   hipStream_t s = (hipStream_t)stream;
+  if (wg_ws(d, w)) {  // all 21 tap groups per workgroup, 6 per wave
+    a.ntapb = 1;
+    auto k = conv_wgrad_kernel<4, 6, 1, true>;
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr_set = true;
+    }
+    hipLaunchKernelGGL(k, dim3(1, nsplit), dim3(256), w.lds_total, s, a);
+    return check_launch("conv2d_wgrad (ci4, wave-split taps)");
+  }
 #define WG_CASE(NTC, TB, CI4) \
   if (w.ntc == NTC && w.tb == TB && w.ci4 == CI4) return launch_wg<NTC, TB, CI4>(a, nblk, w.lds_total, s);
   WG_CASE(1, 1, 0) WG_CASE(2, 1, 0) WG_CASE(4, 1, 0)
