@@ -170,28 +170,41 @@ extern "C" int climsr_pack_conv_weight(const float* w, int out_c, int in_c, int 
   return check_launch("pack_conv_weight");
 }
 
-// Batched form: one launch packs every conv of a network (blockIdx.y = descriptor).
+// Batched form: one launch packs every conv of a network (blockIdx.y = descriptor).  Each thread writes 8
+// consecutive packed elements (one 16 B store; cc and kcpad are multiples of 8, so the 8 share the chunk and
+// the tap) with 32-bit index math (a packed matrix is < 2^31 elements).
+__device__ __forceinline__ uint4 pack8(const float (&v)[8]) {
+  uint4 o;
+  o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+  o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+  o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+  o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+  return o;
+}
 __global__ void pack_batched_kernel(const ClimsrPackDesc* __restrict__ descs) {
   const ClimsrPackDesc d = descs[blockIdx.y];
   const int rows = climsr_rows_dev(d.out_c);
   const int kcpad = (d.ks * d.ks * d.cc + 31) / 32 * 32;
   const int kpk = (d.in_c + d.cc - 1) / d.cc * kcpad;
-  const long total = (long)rows * kpk;
+  const int total8 = rows * kpk / 8, kpk8 = kpk / 8, kc8 = kcpad / 8;
   const int kk2 = d.ks * d.ks;
-  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
-    int co = (int)(idx / kpk);
-    int kk = (int)(idx % kpk);
-    int j = kk / kcpad;
-    int kr = kk % kcpad;
-    int tap = kr / d.cc;
-    int c = j * d.cc + kr % d.cc;
-    float v = 0.f;
-    if (co < d.out_c_real && tap < kk2 && c < d.in_c_real) {
-      int ky = tap / d.ks, kx = tap % d.ks;
-      if (!d.tflip) v = d.w[(((long)co * d.in_c_real + c) * d.ks + ky) * d.ks + kx];
-      else v = d.w[(((long)c * d.out_c_real + co) * d.ks + (d.ks - 1 - ky)) * d.ks + (d.ks - 1 - kx)];
+  for (int i8 = blockIdx.x * blockDim.x + threadIdx.x; i8 < total8; i8 += gridDim.x * blockDim.x) {
+    const int co = i8 / kpk8, kk8 = i8 - co * kpk8;
+    const int j = kk8 / kc8, kr = (kk8 - j * kc8) * 8;
+    const int tap = kr / d.cc, c0 = j * d.cc + kr - tap * d.cc;
+    float v[8];
+    const bool ok = co < d.out_c_real && tap < kk2;
+    const int ky = tap / d.ks, kx = tap - (tap / d.ks) * d.ks;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = c0 + e;
+      v[e] = 0.f;
+      if (ok && c < d.in_c_real) {
+        if (!d.tflip) v[e] = d.w[((co * d.in_c_real + c) * d.ks + ky) * d.ks + kx];
+        else v[e] = d.w[((c * d.out_c_real + co) * d.ks + (d.ks - 1 - ky)) * d.ks + (d.ks - 1 - kx)];
+      }
     }
-    d.out[idx] = f2bf(v);
+    *(uint4*)(d.out + (long)i8 * 8) = pack8(v);
   }
 }
 
@@ -200,8 +213,8 @@ extern "C" int climsr_pack_conv_weights_batched(const ClimsrPackDesc* descs, int
     set_error("pack_conv_weights_batched: bad args");
     return CLIMSR_EINVAL;
   }
-  int gx = ceil_div(max_elems, 256);
-  if (gx > 128) gx = 128;
+  int gx = ceil_div(max_elems / 8, 256);
+  if (gx > 64) gx = 64;
   if (gx < 1) gx = 1;
   hipLaunchKernelGGL(pack_batched_kernel, dim3(gx, ndesc), dim3(256), 0, (hipStream_t)stream, descs);
   return check_launch("pack_conv_weights_batched");
@@ -214,25 +227,29 @@ __global__ void pack_pull_kernel(const ClimsrPullPackDesc* __restrict__ descs) {
   const int rows = climsr_rows_dev(d.out_c);
   const int kcpad = (d.ks * d.ks * d.cc + 31) / 32 * 32;
   const int kpk = (d.in_c + d.cc - 1) / d.cc * kcpad;
-  const long total = (long)rows * kpk;
+  const int total8 = rows * kpk / 8, kpk8 = kpk / 8, kc8 = kcpad / 8;
   const int kk2 = d.ks * d.ks;
-  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
-    const int co = (int)(idx / kpk);
-    const int kk = (int)(idx % kpk);
-    const int j = kk / kcpad;
-    const int kr = kk % kcpad;
+  for (int i8 = blockIdx.x * blockDim.x + threadIdx.x; i8 < total8; i8 += gridDim.x * blockDim.x) {
+    const int co = i8 / kpk8, kk8 = i8 - co * kpk8;
+    const int j = kk8 / kc8, kr = (kk8 - j * kc8) * 8;
     const int tap = kr / d.cc;
-    int c = j * d.cc + kr % d.cc;
-    float v = 0.f;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = 0.f;
+    const int cabs = j * d.cc + kr - tap * d.cc;
+    int c = cabs;
     if (co < d.out_c && tap < kk2 && c < d.in_c) {
+      // segments are multiples of 8 channels wide: the 8 elements share one
       int s = 0;
       while (s < d.nseg - 1 && c >= d.seg_oc[s]) c -= d.seg_oc[s++];
-      if (c < d.seg_oc[s]) {
-        const int ky = tap / d.ks, kx = tap % d.ks;
-        v = d.seg_w[s][(((long)c * d.seg_ic[s] + d.ci_off + co) * d.ks + (d.ks - 1 - ky)) * d.ks + (d.ks - 1 - kx)];
-      }
+      const int ky = tap / d.ks, kx = tap - ky * d.ks;
+      const float* src = d.seg_w[s] + ((c * d.seg_ic[s] + d.ci_off + co) * d.ks + (d.ks - 1 - ky)) * d.ks + (d.ks - 1 - kx);
+      const int cstr = d.seg_ic[s] * kk2;
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (c + e < d.seg_oc[s] && cabs + e < d.in_c) v[e] = src[e * cstr];
     }
-    d.out[idx] = f2bf(v);
+    *(uint4*)(d.out + (long)i8 * 8) = pack8(v);
   }
 }
 
@@ -241,8 +258,8 @@ extern "C" int climsr_pack_pull_weights_batched(const ClimsrPullPackDesc* descs,
     set_error("pack_pull_weights_batched: bad args");
     return CLIMSR_EINVAL;
   }
-  int gx = ceil_div(max_elems, 256);
-  if (gx > 128) gx = 128;
+  int gx = ceil_div(max_elems / 8, 256);
+  if (gx > 64) gx = 64;
   if (gx < 1) gx = 1;
   hipLaunchKernelGGL(pack_pull_kernel, dim3(gx, ndesc), dim3(256), 0, (hipStream_t)stream, descs);
   return check_launch("pack_pull_weights_batched");
@@ -415,7 +432,10 @@ __device__ __forceinline__ void store_tile_lds(const FwdArgs& a, const float* eb
   }
 }
 
-template <int MW, int NT, bool RF, int MV>
+// PF > 0: software-pipelined chunks.  Chunk j+1's input and weight vectors (at most PFX + PFW per thread) are
+// loaded into registers while chunk j is on the MFMA pipe, so a multi-chunk tile (RDB conv5 / pull-x: four
+// 32-channel chunks) pays one staging latency instead of one per chunk.
+template <int MW, int NT, bool RF, int MV, int PFX = 0, int PFW = 0>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int* tab = (int*)smem;
@@ -498,6 +518,65 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
     }
   };
 
+  if constexpr (PFX > 0) {
+    uint4 px[PFX], pw[PFW];
+    auto issue = [&](int j) {
+      int ty_ = x_ty0, tx_ = x_tx0, cg = x_cg0;
+#pragma unroll
+      for (int i = 0; i < PFX; ++i) {
+        px[i] = make_uint4(0, 0, 0, 0);
+        if (i < nrx && ty_ < a.tph) {
+          const int iy = iy0 + ty_, ix = ix0 + tx_;
+          const int c = j * a.cc + cg * 8;
+          if (!(a.ablate & 1) && iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c && !((iy | ix) & dilmask))
+            px[i] = *(const uint4*)(a.x + (((long)nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + c);
+        }
+        cg += x_dc;
+        tx_ += x_dx;
+        ty_ += x_dy;
+        if (cg >= cvec) { cg -= cvec; ++tx_; }
+        if (tx_ >= a.tpw) { tx_ -= a.tpw; ++ty_; }
+      }
+      int r = w_r0, kv = w_k0;
+#pragma unroll
+      for (int i = 0; i < PFW; ++i) {
+        pw[i] = make_uint4(0, 0, 0, 0);
+        if (i < nrw && r < NT * 16 && !(a.ablate & 1))
+          pw[i] = *(const uint4*)(a.w + (long)(co_blk0 + r) * a.kpk + (long)j * a.kcpad + kv * 8);
+        kv += w_dk;
+        r += w_dr;
+        if (kv >= wvec_row) { kv -= wvec_row; ++r; }
+      }
+    };
+    auto stash = [&]() {
+      int ty_ = x_ty0, tx_ = x_tx0, cg = x_cg0;
+#pragma unroll
+      for (int i = 0; i < PFX; ++i) {
+        if (i < nrx && ty_ < a.tph) *(uint4*)(xs + (ty_ * a.tpw + tx_) * a.ccp + cg * 8) = px[i];
+        cg += x_dc;
+        tx_ += x_dx;
+        ty_ += x_dy;
+        if (cg >= cvec) { cg -= cvec; ++tx_; }
+        if (tx_ >= a.tpw) { tx_ -= a.tpw; ++ty_; }
+      }
+      int r = w_r0, kv = w_k0;
+#pragma unroll
+      for (int i = 0; i < PFW; ++i) {
+        if (i < nrw && r < NT * 16) *(uint4*)(ws + r * wpitch + kv * 8) = pw[i];
+        kv += w_dk;
+        r += w_dr;
+        if (kv >= wvec_row) { kv -= wvec_row; ++r; }
+      }
+    };
+    issue(0);
+    for (int j = 0; j < a.nchunk; ++j) {
+      __syncthreads();  // chunk j-1's fragment reads are done
+      if (!(a.ablate & 8)) stash();
+      if (j + 1 < a.nchunk) issue(j + 1);  // lands while chunk j computes
+      __syncthreads();
+      if (!(a.ablate & 2)) compute();
+    }
+  } else {
   // batched staging: every thread issues up to MV input + MV weight 16 B global loads before the first
   // LDS store, so a chunk pays ~one memory latency instead of one per vector
   const int nbatch = nrx > nrw ? nrx : nrw;
@@ -547,6 +626,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
     }
     __syncthreads();
     if (!(a.ablate & 2)) compute();
+  }
   }
   if (a.ablate & 4) {
     if (acc[0][0][0] == 123.f) ((float*)a.y)[0] = 0.f;  // keep the accumulators live
@@ -1941,27 +2021,33 @@ static int dispatch_pt(const ClimsrConvDesc* d, const FwdArgs& a, hipStream_t s)
   }
 }
 
-template <int MW, int NT>
+template <int MW, int NT, int PFX = 0, int PFW = 0>
 static int launch_fwd(const FwdArgs& a, int ncob, size_t lds, hipStream_t s) {
   dim3 grid(a.tiles_x * a.tiles_y * a.n, ncob);
   const size_t lds_ep = (size_t)4 * MW * 16 * (NT * 16 + 4) * 4;  // epilogue staging (aliases the operands)
   if (lds_ep > lds) lds = lds_ep;
   constexpr int MV = NT == 1 ? 6 : (NT == 2 ? 8 : 4);
   if (g_dry) {
-    snprintf(g_dry_name, sizeof(g_dry_name), "conv_fwd_kernel<%d, %d, %s, %d>", MW, NT, a.res_f32 ? "true" : "false", MV);
+    if (PFX) snprintf(g_dry_name, sizeof(g_dry_name), "conv_fwd_kernel<%d, %d, %s, %d, %d, %d>", MW, NT, a.res_f32 ? "true" : "false", MV, PFX, PFW);
+    else snprintf(g_dry_name, sizeof(g_dry_name), "conv_fwd_kernel<%d, %d, %s, %d>", MW, NT, a.res_f32 ? "true" : "false", MV);
     return CLIMSR_OK;
   }
-  auto k = a.res_f32 ? conv_fwd_kernel<MW, NT, true, MV> : conv_fwd_kernel<MW, NT, false, MV>;
+  auto k = a.res_f32 ? conv_fwd_kernel<MW, NT, true, MV, PFX, PFW> : conv_fwd_kernel<MW, NT, false, MV, PFX, PFW>;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)conv_fwd_kernel<MW, NT, true, MV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)conv_fwd_kernel<MW, NT, true, MV, PFX, PFW>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
-    (void)hipFuncSetAttribute((const void*)conv_fwd_kernel<MW, NT, false, MV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)conv_fwd_kernel<MW, NT, false, MV, PFX, PFW>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     attr_set = true;
   }
   hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a);
   return check_launch("conv2d_fwd");
+}
+
+static bool fwd_pf_disabled() {
+  static const bool v = getenv("CLIMSR_NO_FWD_PF") != nullptr;
+  return v;
 }
 
 extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, const uint16_t* wpk, const float* bias,
@@ -2070,7 +2156,12 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
     set_error("conv2d_fwd: LDS %zu exceeds 160 KiB (cc=%d)", g.lds_total, d->cc);
     return CLIMSR_EINVAL;
   }
-  if (mw == 4) return launch_fwd<4, 4>(a, ncob, g.lds_total, s);
+  if (mw == 4) {
+    // multi-chunk tiles whose per-thread staging fits 6 input + 9 weight vectors: chunk-pipelined variant
+    const int nrx = ceil_div(g.tph * g.tpw * (d->cc / 8), 256), nrw = ceil_div(g.nt * 16 * (g.kcpad / 8), 256);
+    if (g.nchunk > 1 && nrx <= 6 && nrw <= 9 && !fwd_pf_disabled()) return launch_fwd<4, 4, 6, 9>(a, ncob, g.lds_total, s);
+    return launch_fwd<4, 4>(a, ncob, g.lds_total, s);
+  }
   switch (g.nt) {
     case 1: return launch_fwd<2, 1>(a, ncob, g.lds_total, s);
     case 2: return launch_fwd<2, 2>(a, ncob, g.lds_total, s);
