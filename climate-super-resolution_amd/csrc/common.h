@@ -33,6 +33,27 @@ __device__ __forceinline__ s16x4 ds_read_tr16(const void* lds_ptr) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)(lds_ptr));
 }
 
+// Buffer resource over [base, base + bytes): a raw buffer load whose byte offset is >= bytes returns zeros
+// (hardware range check), so halo / padding lanes get zeros without a branch around the load (a branch
+// around a load makes hipcc wait vmcnt(0) right there, which serialises a register prefetch).
+constexpr uint32_t BUF_OOB = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint4 buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+// Workgroup barrier for LDS-only hand-offs: orders this wave's LDS accesses (lgkmcnt) but not its global
+// loads / stores, so register prefetches and epilogue stores stay in flight across it.  __syncthreads()'s
+// release fence waits vmcnt(0), which drains a prefetch issued before it.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 

@@ -43,8 +43,12 @@ int check_launch(const char* what) {
 // Tiling constants
 // ------------------------------------------------------------------------------------------
 constexpr int TW = 16;            // output tile width (one MFMA N-fragment of pixels)
-constexpr int XPAD = 8;           // channel padding of the LDS input tile (bank spread)
-constexpr int WPAD = 8;           // k padding of the LDS weight tile rows
+// LDS pitches of the staged operand tiles.  A 16 x 32-channel MFMA fragment is read with ds_read_b128 (lane
+// 16g + col: row col, channels 8g..8g+7); its four 16-lane bank groups are conflict-free when the row pitch
+// is 16 (mod 32) bf16 elements, and 2-way conflicted at 8 (mod 32) (measured SQ_LDS_BANK_CONFLICT 43 % of
+// the LDS cycles of conv5 with the old +8 pads).
+static inline int xpitch(int cc) { return cc + ((16 - cc % 32) + 32) % 32; }  // >= cc, == 16 (mod 32)
+constexpr int WPAD = 16;          // k padding of the LDS weight tile rows (kcpad is a multiple of 32)
 constexpr int FWD_LDS_BUDGET = 80 * 1024;  // two workgroups per CU
 constexpr int FWD_MAXV = 8;             // 16 B staging vectors per thread held in registers (prefetch)
 
@@ -69,7 +73,7 @@ static void fwd_geom(int in_c, int ks, int stride, int out_c, int cc, int mw, Fw
   g->th = 4 * mw;
   g->tph = (g->th - 1) * stride + ks;
   g->tpw = (TW - 1) * stride + ks;
-  g->ccp = cc + XPAD;
+  g->ccp = xpitch(cc);
   g->kc = ks * ks * cc;
   g->kcpad = round_up(g->kc, 32);
   g->nchunk = ceil_div(in_c, cc);
@@ -253,10 +257,64 @@ __global__ void pack_pull_kernel(const ClimsrPullPackDesc* __restrict__ descs) {
   }
 }
 
+// Row-per-workgroup packing (blockIdx.x strides over the packed rows co, blockIdx.y = descriptor): the
+// row's source weights W_s[c][ci_off + co][.][.] are 9 contiguous floats per input channel c, read in
+// those runs into an LDS [tap][channel] image (tap flipped), then the packed row is written as coalesced
+// 16 B vectors.  (The element-per-thread kernel above gathers 8 floats 36*seg_ic bytes apart per output
+// vector: 128 us per step for the generator's 165 pull convs.)
+constexpr int PULL_ROW_MAX = 4096;  // in_c * ks^2 floats staged per row
+__global__ __launch_bounds__(256) void pack_pull_row_kernel(const ClimsrPullPackDesc* __restrict__ descs) {
+  __shared__ float img[PULL_ROW_MAX];
+  // the segment arrays are indexed dynamically: read them from the descriptor in global memory (a private
+  // copy of the struct would live in scratch)
+  const ClimsrPullPackDesc* dp = descs + blockIdx.y;
+  const ClimsrPullPackDesc d = *dp;
+  const int rows = climsr_rows_dev(d.out_c);
+  const int kk2 = d.ks * d.ks;
+  const int kcpad = (kk2 * d.cc + 31) / 32 * 32;
+  const int kpk = (d.in_c + d.cc - 1) / d.cc * kcpad;
+  const int kc8 = kcpad / 8;
+  const bool staged = d.in_c * kk2 <= PULL_ROW_MAX;
+  // source of (channel cabs, source tap t) of row co, 0 past the segments
+  auto src_at = [&](int co, int cabs, int t) -> float {
+    int c = cabs, s = 0;
+    while (s < d.nseg - 1 && c >= dp->seg_oc[s]) c -= dp->seg_oc[s++];
+    return c < dp->seg_oc[s] ? dp->seg_w[s][((long)c * dp->seg_ic[s] + d.ci_off + co) * kk2 + t] : 0.f;
+  };
+  for (int co = blockIdx.x; co < rows; co += gridDim.x) {
+    if (staged) {
+      __syncthreads();  // the previous row's reads of img are done
+      if (co < d.out_c)
+        for (int e = threadIdx.x; e < d.in_c * kk2; e += blockDim.x) {
+          const int cabs = e / kk2, t = e - cabs * kk2;
+          img[(kk2 - 1 - t) * d.in_c + cabs] = src_at(co, cabs, t);  // (ks-1-ky, ks-1-kx) = tap kk2-1-t
+        }
+      __syncthreads();
+    }
+    uint16_t* out = d.out + (long)co * kpk;
+    for (int i8 = threadIdx.x; i8 < kpk / 8; i8 += blockDim.x) {
+      const int j = i8 / kc8, kr = (i8 - j * kc8) * 8;
+      const int tap = kr / d.cc, cabs = j * d.cc + kr - tap * d.cc;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const bool ok = co < d.out_c && tap < kk2 && cabs + e < d.in_c;
+        v[e] = !ok ? 0.f : staged ? img[tap * d.in_c + cabs + e] : src_at(co, cabs + e, kk2 - 1 - tap);
+      }
+      *(uint4*)(out + i8 * 8) = pack8(v);
+    }
+  }
+}
+
 extern "C" int climsr_pack_pull_weights_batched(const ClimsrPullPackDesc* descs, int ndesc, int64_t max_elems, void* stream) {
   if (!descs || ndesc <= 0 || ndesc > 65535) {
     set_error("pack_pull_weights_batched: bad args");
     return CLIMSR_EINVAL;
+  }
+  if (!getenv("CLIMSR_PULL_PACK_ELEM")) {
+    // rows per descriptor are on the device: 64 row slots (the RDB pulls have 16 or 64 rows), more rows loop
+    hipLaunchKernelGGL(pack_pull_row_kernel, dim3(64, ndesc), dim3(256), 0, (hipStream_t)stream, descs);
+    return check_launch("pack_pull_weights_batched");
   }
   int gx = ceil_div(max_elems / 8, 256);
   if (gx > 64) gx = 64;
@@ -331,6 +389,27 @@ __device__ __forceinline__ Raw8 load8(const void* p, bool f32, long idx) {
   }
   return r;
 }
+// Branch-free epilogue operand loads: an optional operand (null pointer) gets a zero-record buffer resource,
+// whose loads return 0 without touching memory, and lanes without a valid pixel load at offset 0 (their
+// values are never used).  No branch around a load, so every load of a round is in flight together
+// (hipcc waits vmcnt(0) at each load that sits under a condition, even a wave-uniform one).  Operand
+// extents are < 4 GiB (checked on the host: climsr_conv2d_fwd).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t opt_rsrc(const void* p) { return buf_rsrc(p, p ? 0xFFFFFFFFu : 0u); }
+__device__ __forceinline__ Raw8 load8b(__amdgpu_buffer_rsrc_t r, bool f32, long idx) {
+  Raw8 v;
+  if (f32) {
+    v.lo = buf_load16(r, (uint32_t)(idx * 4));
+    v.hi = buf_load16(r, (uint32_t)(idx * 4 + 16));
+  } else {
+    v.lo = buf_load16(r, (uint32_t)(idx * 2));
+    v.hi = make_uint4(0, 0, 0, 0);
+  }
+  return v;
+}
+__device__ __forceinline__ uint2 buf_load8(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+  return make_uint2(v[0], v[1]);
+}
 __device__ __forceinline__ float raw8_at(const Raw8& r, bool f32, int i) {
   if (f32) {
     const uint4& q = i < 4 ? r.lo : r.hi;
@@ -361,7 +440,8 @@ __device__ __forceinline__ void store_tile_lds(const FwdArgs& a, const float* eb
   const bool f1 = RF && (a.res_f32 & 1), f2 = RF && ((a.res_f32 >> 1) & 1);
   const bool vec = (a.out_c & 7) == 0 && ((a.out_cs | a.out_co) & 7) == 0 && (!a.res1 || ((a.r1_cs | a.r1_co) & 7) == 0) &&
                    (!a.res2 || ((a.r2_cs | a.r2_co) & 7) == 0) && (!a.aux || ((a.aux_cs | a.aux_co) & 7) == 0);
-  constexpr int IB = 2;  // items per round: their global loads are in flight together
+  constexpr int IB = RF ? 2 : 4;  // items per round: their global loads are in flight together
+  const __amdgpu_buffer_rsrc_t rr1 = opt_rsrc(a.res1), rr2 = opt_rsrc(a.res2), rry = opt_rsrc(a.out_mode == 2 ? a.y : nullptr);
 #pragma unroll
   for (int base = 0; base < (NIT + NLANE - 1) / NLANE; base += IB) {
     Raw8 r1[IB], r2[IB], old[IB];
@@ -375,13 +455,12 @@ __device__ __forceinline__ void store_tile_lds(const FwdArgs& a, const float* eb
       const int co = co0 + cg * 8;
       ok[j] = it < NIT && oy < a.out_h && ox < a.out_w && co < a.out_c;
       pidxs[j] = ((nimg * a.out_h + oy) * a.out_w + ox);
-      r1[j].lo = r1[j].hi = r2[j].lo = r2[j].hi = old[j].lo = old[j].hi = make_uint4(0, 0, 0, 0);
-      if (ok[j] && vec && co + 7 < a.out_c) {
-        const long pidx = pidxs[j];
-        if (a.res1) r1[j] = load8(a.res1, f1, pidx * a.r1_cs + a.r1_co + co);
-        if (a.res2) r2[j] = load8(a.res2, f2, pidx * a.r2_cs + a.r2_co + co);
-        if (a.out_mode == 2) old[j] = load8(a.y, true, pidx * a.out_cs + a.out_co + co);
-      }
+      const bool ld = ok[j] && vec && co + 7 < a.out_c;  // else the values are unused
+      const long pidx = ld ? pidxs[j] : 0;
+      const int c = ld ? co : 0;
+      r1[j] = load8b(rr1, f1, pidx * a.r1_cs + (ld ? a.r1_co : 0) + c);
+      r2[j] = load8b(rr2, f2, pidx * a.r2_cs + (ld ? a.r2_co : 0) + c);
+      old[j] = load8b(rry, true, pidx * a.out_cs + (ld ? a.out_co : 0) + c);
     }
 #pragma unroll
     for (int j = 0; j < IB; ++j) {
@@ -645,6 +724,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
     const bool mask = a.act == 3 || a.act == 4;
     float4 old[MW / 2][NT];
     uint2 r1v[MW / 2][NT];
+    const __amdgpu_buffer_rsrc_t ry2 = opt_rsrc(a.out_mode == 2 ? a.y : nullptr), rm1 = opt_rsrc(mask ? a.res1 : nullptr);
 #pragma unroll
     for (int m = 0; m < MW; m += 2) {
       const int oy = oy0 + wave * MW + m;
@@ -652,11 +732,11 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int co = co_blk0 + t * 16 + g * 4;
-        old[m / 2][t] = make_float4(0.f, 0.f, 0.f, 0.f);
-        r1v[m / 2][t] = make_uint2(0, 0);
         const bool ok = (col & 1) == 0 && oy < a.out_h && ox < a.out_w && co + 3 < a.out_c;
-        if (ok && a.out_mode == 2) old[m / 2][t] = *(const float4*)((const float*)a.y + pidx * a.out_cs + a.out_co + co);
-        if (ok && mask) r1v[m / 2][t] = *(const uint2*)((const uint16_t*)a.res1 + pidx * a.r1_cs + a.r1_co + co);
+        const long q = ok ? pidx : 0;
+        const uint4 o4 = buf_load16(ry2, (uint32_t)((q * a.out_cs + (ok ? a.out_co + co : 0)) * 4));
+        old[m / 2][t] = make_float4(__uint_as_float(o4.x), __uint_as_float(o4.y), __uint_as_float(o4.z), __uint_as_float(o4.w));
+        r1v[m / 2][t] = buf_load8(rm1, (uint32_t)((q * a.r1_cs + (ok ? a.r1_co + co : 0)) * 2));
       }
     }
 #pragma unroll
@@ -770,7 +850,7 @@ __global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint16_t* xs = (uint16_t*)smem;
   float* part = (float*)smem;  // partial sums [cb][row][lane] (aliases the input tile after compute)
-  constexpr int CINP = NCB * 32, P = CINP + 8, CV = CINP / 8;
+  constexpr int CINP = NCB * 32, P = CINP + 16, CV = CINP / 8;  // P == 16 (mod 32): conflict-free fragment reads
   constexpr int RG = 4 / NCB, MW = N16_TH / RG;  // row groups, output rows per wave
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
   const int cb = wave % NCB, rg = wave / NCB;
@@ -793,8 +873,12 @@ __global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs
   // are stored as zeros without a load
   constexpr int NPIX = N16_TPH * N16_TPW, NV = (NPIX * CV + 255) / 256;
   uint4 pre[NV];
-  auto issue = [&](int tile) {
-    int tt = tile;
+  // buffer loads: out-of-image / pad-channel vectors take an out-of-range offset and read as zeros, so the
+  // next tile's loads stay in flight through the current tile's compute (no branch, no early vmcnt wait)
+  const __amdgpu_buffer_rsrc_t xr = buf_rsrc(a.x, (uint32_t)((long)a.n * a.in_h * a.in_w * a.in_cs * 2));
+  auto issue = [&](int tile) {  // tile < 0: no next tile, every lane takes the out-of-range offset
+    const bool live = tile >= 0;
+    int tt = live ? tile : 0;
     const int tx = tt % a.tiles_x;
     tt /= a.tiles_x;
     const int ty = tt % a.tiles_y;
@@ -806,18 +890,22 @@ __global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs
       const int pix = v / CV, j = v % CV;
       const int py = pix / N16_TPW, px = pix - py * N16_TPW;
       const int iy = iy0 + py, ix = ix0 + px;
-      pre[i] = make_uint4(0, 0, 0, 0);
-      if (v < NPIX * CV && j < cvec && !(a.ablate & 1) && iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w)
-        pre[i] = *(const uint4*)(a.x + (((long)nimg * a.in_h + iy) * a.in_w + ix) * a.in_cs + a.in_co + j * 8);
+      const bool ok = live && v < NPIX * CV && j < cvec && !(a.ablate & 1) && iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w;
+      const uint32_t off = (uint32_t)(((((nimg * a.in_h + iy) * a.in_w + ix) * a.in_cs) + a.in_co + j * 8) * 2);
+      pre[i] = buf_load16(xr, ok ? off : BUF_OOB);
     }
   };
   const TileWalk walk(ntiles);
   if (walk.first < walk.end) issue(walk.first);
+  const __amdgpu_buffer_rsrc_t er1 = opt_rsrc(a.res1), er2 = opt_rsrc(a.res2), ery = opt_rsrc(a.out_mode == 2 ? a.y : nullptr);
   // this wave's A fragments (channel block cb, 9 taps; packed rows are tap-major with CINP channels per
   // tap), loaded once per workgroup straight into VGPRs while the first tile's input is in flight
   bf16x8 af[9];
 #pragma unroll
   for (int t = 0; t < 9; ++t) af[t] = *(const bf16x8*)(a.w + (long)col * a.kpk + t * CINP + cb * 32 + g * 8);
+  // retire them here: the loop below then has no loop-carried VMEM results, and hipcc's wait counting
+  // inside it stays exact (no vmcnt(0) before the prefetch can land)
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 
   for (int tile = walk.first; tile < walk.end; tile += walk.step) {
     int tt = tile;
@@ -826,7 +914,7 @@ __global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs
     const int ty = tt % a.tiles_y;
     const int nimg = tt / a.tiles_y;
     const int oy0 = ty * N16_TH, ox0 = tx * TW;
-    __syncthreads();  // the previous tile's LDS reads (partials) are done
+    lds_barrier();  // the previous tile's LDS reads (partials) are done
     if (!(a.ablate & 8)) {
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
@@ -834,8 +922,9 @@ __global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs
         if (v < NPIX * CV) *(uint4*)(xs + (v / CV) * P + (v % CV) * 8) = pre[i];
       }
     }
-    if (tile + walk.step < walk.end) issue(tile + walk.step);  // lands while this tile computes
-    __syncthreads();
+    issue(tile + walk.step < walk.end ? tile + walk.step : -1);  // lands while this tile computes (unconditional:
+                                                                  // a branch around it makes hipcc drain it)
+    lds_barrier();
     f32x4 acc[MW];
 #pragma unroll
     for (int m = 0; m < MW; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -856,10 +945,10 @@ __global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs
           }
       }
     }
-    __syncthreads();  // input tile reads done: the partials overwrite it
+    lds_barrier();  // input tile reads done: the partials overwrite it
 #pragma unroll
     for (int m = 0; m < MW; ++m) *(f32x4*)(part + ((cb * N16_TH + rg * MW + m) * 64 + lane) * 4) = acc[m];
-    __syncthreads();
+    lds_barrier();
     if (a.ablate & 4) continue;
     // epilogue: wave w finishes output rows 2w, 2w+1; lane owns channels co..co+3 of column ox0 + col
     const int ox = ox0 + col;
@@ -873,16 +962,15 @@ __global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs
     uint2 r1v[2], r2v[2];
     float4 old[2];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < 2; ++h) {  // branch-free (opt_rsrc): both rows' operand loads in flight together
       const int oy = oy0 + wave * 2 + h;
-      const long pidx = ((long)nimg * a.out_h + oy) * a.out_w + ox;
-      r1v[h] = r2v[h] = make_uint2(0, 0);
-      old[h] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (oy < a.out_h && ox < a.out_w && valign) {
-        if (a.res1) r1v[h] = *(const uint2*)((const uint16_t*)a.res1 + pidx * a.r1_cs + a.r1_co + co);
-        if (a.res2) r2v[h] = *(const uint2*)((const uint16_t*)a.res2 + pidx * a.r2_cs + a.r2_co + co);
-        if (a.out_mode == 2) old[h] = *(const float4*)((const float*)a.y + pidx * a.out_cs + a.out_co + co);
-      }
+      const bool ld = oy < a.out_h && ox < a.out_w && valign;
+      const long pidx = ld ? ((long)nimg * a.out_h + oy) * a.out_w + ox : 0;
+      const int c = ld ? co : 0;
+      r1v[h] = buf_load8(er1, (uint32_t)((pidx * a.r1_cs + (ld ? a.r1_co : 0) + c) * 2));
+      r2v[h] = buf_load8(er2, (uint32_t)((pidx * a.r2_cs + (ld ? a.r2_co : 0) + c) * 2));
+      const uint4 o4 = buf_load16(ery, (uint32_t)((pidx * a.out_cs + (ld ? a.out_co : 0) + c) * 4));
+      old[h] = make_float4(__uint_as_float(o4.x), __uint_as_float(o4.y), __uint_as_float(o4.z), __uint_as_float(o4.w));
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -937,7 +1025,7 @@ static int launch_n16(const FwdArgs& a, hipStream_t s) {
     return CLIMSR_OK;
   }
   auto k = conv_n16_kernel<NCB>;
-  size_t lds = (size_t)N16_TPH * N16_TPW * (NCB * 32 + 8) * 2;
+  size_t lds = (size_t)N16_TPH * N16_TPW * (NCB * 32 + 16) * 2;
   const size_t lds_p = (size_t)NCB * N16_TH * 64 * 16;             // partial sums (aliased)
   if (lds_p > lds) lds = lds_p;
   static bool attr_set = false;
@@ -981,7 +1069,7 @@ __global__ __launch_bounds__(512, 1) void conv_co64_kernel(FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint16_t* xs = (uint16_t*)smem;
   float* part = (float*)smem;  // [cob 4][kh 2][row 4][lane 64][4] (aliases the input tile after compute)
-  constexpr int CINP = NCB * 32, P = CINP + 8, CV = CINP / 8;
+  constexpr int CINP = NCB * 32, P = CINP + 16, CV = CINP / 8;  // P == 16 (mod 32): conflict-free fragment reads
   constexpr int NCBH = (NCB + 1) / 2;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
   const int cob = wave & 3, kh = wave >> 2;
@@ -1184,7 +1272,7 @@ __global__ __launch_bounds__(512, 1) void conv_co64_kernel(FwdArgs a) {
 template <int NCB, bool RF>
 static int launch_co64_t(const FwdArgs& a, hipStream_t s) {
   auto k = conv_co64_kernel<NCB, RF>;
-  size_t lds = (size_t)C64_TPH * C64_TPW * (NCB * 32 + 8) * 2;
+  size_t lds = (size_t)C64_TPH * C64_TPW * (NCB * 32 + 16) * 2;
   const size_t lds_p = (size_t)4 * 2 * 4 * 64 * 16;
   if (lds_p > lds) lds = lds_p;
   static bool attr_set = false;
@@ -1447,7 +1535,7 @@ static bool pw_geom(const ClimsrConvDesc* d, int nt, int mw, PwGeom* g, int nw =
   g->mw = mw;
   g->tph = nw * mw + d->ks - 1;
   g->tpw = TW + d->ks - 1;
-  g->ccp = d->cc + XPAD;
+  g->ccp = xpitch(d->cc);
   g->kcpad = round_up(d->ks * d->ks * d->cc, 32);
   g->nvx = g->tph * g->tpw * (d->cc / 8);
   g->lds_tab = ((size_t)(g->kcpad / 8) * 4 + 15) / 16 * 16;
@@ -1489,11 +1577,23 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
     const int ky = tap / a.ks, kx = tap - ky * a.ks;
     tab[i] = (ky * a.tpw + kx) * a.ccp + c;
   }
-  {  // the whole weight matrix, once
-    const int wvec_row = a.kcpad / 8;
-    for (int v = tid; v < NT * 16 * wvec_row; v += NTHR) {
-      const int r = v / wvec_row, kv = v - r * wvec_row;
-      *(uint4*)(ws + r * wpitch + kv * 8) = *(const uint4*)(a.w + (long)r * a.kpk + kv * 8);
+  {  // the whole weight matrix, once: 8 vectors per thread in flight per batch (buffer loads, no branch)
+    const int wvec_row = a.kcpad / 8, nvw = NT * 16 * wvec_row;
+    const __amdgpu_buffer_rsrc_t wr = buf_rsrc(a.w, 0xFFFFFFFFu);
+    for (int v0 = 0; v0 < nvw; v0 += 8 * NTHR) {
+      uint4 wv[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int v = v0 + tid + i * NTHR;
+        const int r = v / wvec_row, kv = v - r * wvec_row;
+        wv[i] = buf_load16(wr, v < nvw ? (uint32_t)((r * a.kpk + kv * 8) * 2) : 0u);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int v = v0 + tid + i * NTHR;
+        const int r = v / wvec_row, kv = v - r * wvec_row;
+        if (v < nvw) *(uint4*)(ws + r * wpitch + kv * 8) = wv[i];
+      }
     }
   }
   const int ufac = a.up, upsh = a.up == 2 ? 1 : 0;
@@ -1507,8 +1607,12 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
   const int ntiles = a.tiles_x * a.tiles_y * a.n;
 
   uint4 pre[PV];
-  auto issue = [&](int tile) {
-    int tt = tile;
+  // buffer loads (zeros out of range) and an unconditional call: the next tile's loads stay in flight
+  // through this tile's compute (see conv_n16_kernel)
+  const __amdgpu_buffer_rsrc_t xr = buf_rsrc(a.x, (uint32_t)((long)a.n * a.in_h * a.in_w * a.in_cs * 2));
+  auto issue = [&](int tile) {  // tile < 0: nothing to load
+    const bool live = tile >= 0;
+    int tt = live ? tile : 0;
     const int tx = tt % a.tiles_x;
     tt /= a.tiles_x;
     const int ty = tt % a.tiles_y;
@@ -1517,12 +1621,12 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
     int ty_ = x_ty0, tx_ = x_tx0, cg = x_cg0;
 #pragma unroll
     for (int i = 0; i < PV; ++i) {
-      pre[i] = make_uint4(0, 0, 0, 0);
-      if (tid + NTHR * i < nvec_x) {
+      {
         const int iy = iy0 + ty_, ix = ix0 + tx_;
         const int c = cg * 8;
-        if (!(a.ablate & 1) && iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c)
-          pre[i] = *(const uint4*)(a.x + (((long)nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + c);
+        const bool ok = live && tid + NTHR * i < nvec_x && !(a.ablate & 1) && iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c;
+        const uint32_t off = (uint32_t)((((nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + c) * 2);
+        pre[i] = buf_load16(xr, ok ? off : BUF_OOB);
       }
       cg += x_dc;
       tx_ += x_dx;
@@ -1545,7 +1649,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
     const int ty = tt % a.tiles_y;
     const int nimg = tt / a.tiles_y;
     const int ox0 = tx * TW, oy0 = ty * (NW * MW);
-    __syncthreads();  // previous tile's epilogue reads of the aliased region are done
+    lds_barrier();  // previous tile's epilogue reads of the aliased region are done
     {
       int ty_ = x_ty0, tx_ = x_tx0, cg = x_cg0;
 #pragma unroll
@@ -1558,8 +1662,8 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
         if (tx_ >= a.tpw) { tx_ -= a.tpw; ++ty_; }
       }
     }
-    if (tile + walk.step < walk.end) issue(tile + walk.step);  // lands while this tile computes
-    __syncthreads();
+    issue(tile + walk.step < walk.end ? tile + walk.step : -1);  // lands while this tile computes
+    lds_barrier();
     f32x4 acc[MW][NT];
 #pragma unroll
     for (int m = 0; m < MW; ++m)
@@ -1621,12 +1725,12 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
     }
     constexpr int EPP = NT * 16 + 4;
     float* eb = ebase + wave * (MW * 16 * EPP);
-    __syncthreads();  // all waves are done reading the input tile (the staging region aliases it)
+    lds_barrier();  // all waves are done reading the input tile (the staging region aliases it)
 #pragma unroll
     for (int m = 0; m < MW; ++m)
 #pragma unroll
       for (int t = 0; t < NT; ++t) *(f32x4*)(eb + (m * 16 + col) * EPP + t * 16 + g * 4) = acc[m][t];
-    __syncthreads();
+    lds_barrier();
     store_tile_lds<RF, MW * 16, NT * 16, 64>(a, eb, EPP, lane, nimg, oy0 + wave * MW, ox0, 0);
   }
 }
@@ -2076,6 +2180,17 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
     set_error("conv2d_fwd: aux channel stride/offset must be multiples of 4");
     return CLIMSR_EINVAL;
   }
+  {  // epilogue operands are read through 32-bit buffer offsets (opt_rsrc)
+    const long opx = (long)d->n * d->out_h * d->out_w;
+    const long r1b = ep->res1 ? opx * ep->res1_cstride * ((ep->res_f32 & 1) ? 4 : 2) : 0;
+    const long r2b = ep->res2 ? opx * ep->res2_cstride * ((ep->res_f32 & 2) ? 4 : 2) : 0;
+    const long yb = opx * d->out_cstride * (ep->out_mode == 0 ? 2 : 4);
+    if (r1b >= (1L << 32) - 64 || r2b >= (1L << 32) - 64 || yb >= (1L << 32) - 64) {
+      set_error("conv2d_fwd: output / residual operand of %ld B exceeds 32-bit buffer addressing (split the batch)",
+                r1b > r2b ? (r1b > yb ? r1b : yb) : (r2b > yb ? r2b : yb));
+      return CLIMSR_EINVAL;
+    }
+  }
   FwdGeom g;
   // 16x16 output tiles (64 px per wave) for the 64-channel layers; 8x16 otherwise
   const int mw = (d->out_h >= 12 && fwd_nt(d->out_c) == 4) ? 4 : 2;
@@ -2113,7 +2228,8 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
     return check_launch("conv2d_fwd (co1)");
   }
   if (n16_shape(d->in_c, d->ks, d->out_c) && d->cc == 32 * n16_ncb(d->in_c) && d->stride == 1 && d->up == 1 && d->pad == 1 &&
-      !ep->down2 && !ep->res_f32 && d->out_h == d->in_h && d->out_w == d->in_w) {
+      !ep->down2 && !ep->res_f32 && d->out_h == d->in_h && d->out_w == d->in_w &&
+      (long)d->n * d->in_h * d->in_w * d->in_cstride * 2 < (1L << 31)) {  // 32-bit buffer offsets
     a.tiles_x = ceil_div(d->out_w, TW);
     a.tiles_y = ceil_div(d->out_h, N16_TH);
     switch (d->cc / 32) {
@@ -2145,7 +2261,8 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
     const int nt = fwd_nt(d->out_c);
     const long npx = (long)d->n * d->out_h * d->out_w;
     PwGeom pg;
-    if (ncob == 1 && (nt == 4 || nt == 2) && d->up != -2 && npx >= 4096 && !pw_disabled()) {
+    if (ncob == 1 && (nt == 4 || nt == 2) && d->up != -2 && npx >= 4096 && !pw_disabled() &&
+        (long)d->n * d->in_h * d->in_w * d->in_cstride * 2 < (1L << 31)) {  // 32-bit buffer offsets
       // 8 waves x 2 rows (two waves per SIMD) when the LDS allows, else 4 waves x 2 rows
       if (pw_geom(d, nt, 2, &pg, 8) && pg.nvx <= 512 * 7 && d->out_h >= 16)
         return nt == 4 ? launch_pw<8, 2, 4, 7>(a, pg, s) : launch_pw<8, 2, 2, 7>(a, pg, s);
