@@ -73,19 +73,43 @@ class KernelTimer:
 
     def __init__(self):
         self.rec = []
+        self.fns = {}
 
-    def __call__(self, name, flops, fn, tag=""):
+    def __call__(self, name, flops, fn, tag="", nbytes=0):
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         s.record()
         fn()
         e.record()
-        self.rec.append((name, flops, s, e, tag))
+        self.rec.append((name, flops, s, e, tag, nbytes))
+        self.fns.setdefault(name, []).append(fn)
+
+    def graph_us(self, name, reps=3):
+        """Average launch duration of `name` with its launches of one step replayed back to back from a
+        hipGraph (HIP events around the replay): the per-launch event pairs above also time the dispatch gap,
+        this matches rocprofv3's kernel durations."""
+        fns = self.fns[name]
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(gr, stream=side):
+                for fn in fns:
+                    fn()
+        torch.cuda.synchronize()
+        gr.replay()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            gr.replay()
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) * 1e3 / (reps * len(fns))
 
     def by_tag(self, top=25):
         torch.cuda.synchronize()
         agg = {}
-        for name, flops, s, e, tag in self.rec:
+        for name, flops, s, e, tag, _b in self.rec:
             key = name + " | " + ".".join(t for t in tag.split(".") if not t.isdigit() and not t.startswith("RDB"))
             a = agg.setdefault(key, [0, 0.0, 0])
             a[0] += 1
@@ -95,14 +119,36 @@ class KernelTimer:
         return {k: {"n": v[0], "ms": round(v[1], 3), "tflops": round(v[2] / (v[1] / 1e3) / 1e12, 1)} for k, v in rows}
 
     def summary(self):
+        """{kernel: [launches, ms, algorithmic flops, algorithmic bytes]}"""
         torch.cuda.synchronize()
         agg = {}
-        for name, flops, s, e, _tag in self.rec:
-            a = agg.setdefault(name, [0, 0.0, 0])
+        for name, flops, s, e, _tag, nbytes in self.rec:
+            a = agg.setdefault(name, [0, 0.0, 0, 0])
             a[0] += 1
             a[1] += s.elapsed_time(e)
             a[2] += flops
+            a[3] += nbytes
         return agg
+
+
+def roofline_entry(name, cnt, tot_ms, flops, nbytes, graph_us=None):
+    """Roofline of one kernel: bound = the resource its algorithmic intensity saturates first (MFMA when
+    flops/bytes >= the ridge 2500 TFLOP/s / 8 TB/s = 312 FLOP/B, else HBM); achieved = algorithmic work per
+    launch / average launch time, in that resource's unit."""
+    avg_s = (graph_us / 1e6) if graph_us else tot_ms / cnt / 1e3
+    ridge = PEAK_BF16_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
+    ai = flops / nbytes if nbytes else float("inf")
+    out = {"kernel": name, "launches_per_step": cnt, "avg_launch_us": round(avg_s * 1e6, 2),
+           "avg_launch_us_source": "hipGraph replay of the step's launches of this kernel" if graph_us else "per-launch HIP events",
+           "eager_event_us": round(tot_ms / cnt * 1e3, 2), "flop_per_launch": flops // cnt,
+           "bytes_per_launch": nbytes // cnt, "intensity_flop_per_byte": round(ai, 1) if nbytes else None,
+           "tflops": round(flops / cnt / avg_s / 1e12, 2), "gbs": round(nbytes / cnt / avg_s / 1e9, 1) if nbytes else None}
+    if ai >= ridge:
+        out.update(bound="mfma", achieved=out["tflops"], peak=PEAK_BF16_TFLOPS, unit="TFLOP/s")
+    else:
+        out.update(bound="hbm", achieved=out["gbs"], peak=PEAK_HBM_GBS, unit="GB/s")
+    out["frac"] = round(out["achieved"] / out["peak"], 4)
+    return out
 
 
 def cpu_baseline(args, hr):
@@ -202,13 +248,13 @@ def run_infer(args, world, rank, dev):
             fwd()
             ops.PROFILER = None
             agg = timer.summary()
-            name, (cnt, tot_ms, flops) = max(agg.items(), key=lambda kv: kv[1][1])
-            avg_ms = tot_ms / cnt
-            achieved = flops / cnt / (avg_ms / 1e3) / 1e12
-            roof = {"bound": "mfma", "kernel": name, "launches_per_step": cnt, "avg_launch_us": round(avg_ms * 1e3, 2),
-                    "flop_per_launch": flops // cnt, "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None}
-            kern = {k: {"launches": v[0], "ms_total": round(v[1], 3), "tflops": round(v[2] / (v[1] / 1e3) / 1e12, 1)}
+            name, (cnt, tot_ms, flops, nbytes) = max(agg.items(), key=lambda kv: kv[1][1])
+            r = roofline_entry(name, cnt, tot_ms, flops, nbytes, timer.graph_us(name))
+            roof = {"bound": r["bound"], "achieved": r["achieved"], "peak": r["peak"], "unit": r["unit"], "frac": r["frac"],
+                    "traffic": None}
+            roof.update({k: v for k, v in r.items() if k not in roof})
+            kern = {k: {"launches": v[0], "ms_total": round(v[1], 3), "tflops": round(v[2] / (v[1] / 1e3) / 1e12, 1),
+                        "gbs": round(v[3] / (v[1] / 1e3) / 1e9, 1) if v[3] else None}
                     for k, v in sorted(agg.items(), key=lambda kv: -kv[1][1])}
             flop_fwd = sum(v[2] for v in agg.values())
     cpu = None
@@ -441,17 +487,18 @@ def main():
         step()
         ops.PROFILER = None
         agg = timer.summary()
-        name, (cnt, tot_ms, flops) = max(agg.items(), key=lambda kv: kv[1][1])
+        name, (cnt, tot_ms, flops, nbytes) = max(agg.items(), key=lambda kv: kv[1][1])
         avg_ms = tot_ms / cnt
-        achieved = flops / cnt / (avg_ms / 1e3) / 1e12
-        roof = {"bound": "mfma", "kernel": name, "launches_per_step": cnt, "avg_launch_us": round(avg_ms * 1e3, 2),
-                "flop_per_launch": flops // cnt, "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None}
-        tb, src = pmc_traffic(name)
+        r = roofline_entry(name, cnt, tot_ms, flops, nbytes, timer.graph_us(name))
+        roof = {"bound": r["bound"], "achieved": r["achieved"], "peak": r["peak"], "unit": r["unit"], "frac": r["frac"],
+                "traffic": None}
+        roof.update({k: v for k, v in r.items() if k not in roof})
+        tb, src = pmc_traffic(name) if args.mode == "pretrain" else (None, None)  # the PMC summaries are of config 2
         if tb is not None:  # HBM bytes per launch (PMC) and the bandwidth they imply at the measured launch time
             roof.update(traffic=round(tb / 1e6, 2), traffic_unit="MB/launch", traffic_source=src,
-                        traffic_gbs=round(tb / (avg_ms / 1e3) / 1e9, 1))
-        kern = {k: {"launches": v[0], "ms_total": round(v[1], 3), "tflops": round(v[2] / (v[1] / 1e3) / 1e12, 1)}
+                        traffic_gbs=round(tb / (r["avg_launch_us"] / 1e6) / 1e9, 1))
+        kern = {k: {"launches": v[0], "ms_total": round(v[1], 3), "tflops": round(v[2] / (v[1] / 1e3) / 1e12, 1),
+                    "gbs": round(v[3] / (v[1] / 1e3) / 1e9, 1) if v[3] else None}
                 for k, v in sorted(agg.items(), key=lambda kv: -kv[1][1])}
         if os.environ.get("CLIMSR_BENCH_DETAIL"):
             print(json.dumps(timer.by_tag(), indent=0), file=sys.stderr)

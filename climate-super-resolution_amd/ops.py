@@ -25,7 +25,8 @@ def round_up(a: int, b: int) -> int:
 
 
 # Optional launch observer (bench.py's per-kernel HIP-event timer).  Called as
-# PROFILER(kernel_name, algorithmic_flops, launch_fn); must call launch_fn() exactly once.
+# PROFILER(kernel_name, algorithmic_flops, launch_fn, tag, algorithmic_bytes); must call launch_fn() exactly
+# once.  algorithmic_bytes = every operand read once and every result written once (no halo re-reads).
 PROFILER = None
 
 
@@ -72,11 +73,15 @@ def _kname(d, bias, ep) -> str:
     return _lib.load().climsr_conv2d_fwd_kernel(ctypes.byref(d), bias, ctypes.byref(ep)).decode()
 
 
-def _run(name, flops, fn, tag=""):
+def _run(name, flops, fn, tag="", nbytes=0):
     if PROFILER is None:
         fn()
     else:
-        PROFILER(name, flops, fn, tag)
+        PROFILER(name, flops, fn, tag, nbytes)
+
+
+def _esize(t: Optional[torch.Tensor]) -> int:
+    return 0 if t is None else t.element_size()
 
 
 class ConvPlan:
@@ -156,9 +161,13 @@ class ConvPlan:
                       rf, beta1, beta2, aux_cs, ptr(aux), aux_co, aux_scale)
         b = ptr(self.bias) if (use_bias and self.bias is not None) else None
         flops = 2 * self.cin_real * self.cout * self.ks * self.ks * n * oh * ow
+        opx = n * oh * ow
+        nbytes = (n * in_h * in_w * self.cin_real * 2 + self.rows * self.kpk * 2 +
+                  opx * self.cout * (y.element_size() * (2 if out_mode == OUT_F32_ADD else 1) + _esize(res1) + _esize(res2) +
+                                     _esize(aux)))
         _run(_kname(d, b, ep), flops, lambda: check(
             _lib.load().climsr_conv2d_fwd(ctypes.byref(d), ptr(x), ptr(self.wpk), b, ctypes.byref(ep), ptr(y), _lib.stream_ptr()),
-            f"conv fwd {self.name}"), "fwd " + self.name)
+            f"conv fwd {self.name}"), "fwd " + self.name, nbytes)
 
     def dgrad(self, dz: torch.Tensor, dz_cs: int, out_h: int, out_w: int, g: torch.Tensor, g_cs: int, g_co: int, n: int,
               accumulate: bool = False, down2: bool = False, cout_t: Optional[int] = None, aux: Optional[torch.Tensor] = None,
@@ -183,9 +192,12 @@ class ConvPlan:
         ep = Epilogue(act, 0.2 if act == ACT_LRELU_BWD else 0.0, 1.0, ptr(res1), res1_cs, res1_co, 1.0, None, 0, 0, mode,
                       1 if down2 else 0, 0, 1.0, 1.0, aux_cs, ptr(aux), aux_co, aux_scale)
         flops = 2 * self.cout * ct * self.ks * self.ks * n * out_h * out_w
+        gpx = n * out_h * out_w // (4 if down2 else 1)  # result pixels (after the 2x2 sum)
+        nbytes = (n * d.in_h * d.in_w * self.cout * 2 + self.rows_t * self.kpk_t * 2 +
+                  gpx * ct * (g.element_size() * (2 if mode == OUT_F32_ADD else 1) + _esize(res1) + _esize(aux)))
         _run(_kname(d, None, ep), flops, lambda: check(
             _lib.load().climsr_conv2d_fwd(ctypes.byref(d), ptr(dz), ptr(self.wpk_t), None, ctypes.byref(ep), ptr(g),
-                                          _lib.stream_ptr()), f"conv dgrad {self.name}"), "dgrad " + self.name)
+                                          _lib.stream_ptr()), f"conv dgrad {self.name}"), "dgrad " + self.name, nbytes)
 
     @property
     def cin_w(self) -> int:
@@ -212,9 +224,10 @@ class ConvPlan:
         s = _lib.stream_ptr()
         has_b = self.bias is not None and self.gb is not None
         flops = 2 * self.cin_real * self.cout * self.ks * self.ks * n * d.out_h * d.out_w
+        nbytes = n * in_h * in_w * self.cin_real * 2 + n * d.out_h * d.out_w * self.cout * 2 + self.cout * self.cin_real * self.ks ** 2 * 4
         _run(wgrad_kernel_name(self.cout, self.ks, self.cin_w == 4, self.cin_w, self.stride, self.pad), flops, lambda: check(
             lib.climsr_conv2d_wgrad(ctypes.byref(d), ptr(x), ptr(dz), dz_cs, ptr(part), ptr(bpart) if has_b else None, ns, s),
-            f"conv wgrad {self.name}"), "wgrad " + self.name)
+            f"conv wgrad {self.name}"), "wgrad " + self.name, nbytes)
         check(lib.climsr_conv2d_wgrad_reduce(ptr(part), ptr(bpart) if has_b else None, ns, self.cout, self.cin_real, cw,
                                              self.ks, ptr(self.gw), ptr(self.gb) if has_b else None,
                                              1 if accumulate else 0, s), f"wgrad reduce {self.name}")
@@ -260,9 +273,10 @@ class GroupedWgrad:
         bpart = ws[ns * self.out_c * self.in_c * 9:]
         s = _lib.stream_ptr()
         flops = sum(2 * p.cin_real * p.cout * 9 for p in self.plans) * n * in_h * in_w
+        nbytes = n * in_h * in_w * (self.in_c + self.out_c) * 2 + sum(p.cout * p.cin_real * 9 * 4 for p in self.plans)
         _run("conv_wgrad64_kernel", flops, lambda: check(
             lib.climsr_conv2d_wgrad(ctypes.byref(d), ptr(x), ptr(dz), dz_cs, ptr(part), ptr(bpart), ns, s),
-            f"grouped wgrad {self.name}"), "wgrad " + self.name)
+            f"grouped wgrad {self.name}"), "wgrad " + self.name, nbytes)
         tab = self._table(x.device)
         check(lib.climsr_conv2d_wgrad_reduce_rows(ptr(part), ptr(bpart), ns, self.out_c, self.in_c * 9, 3, ptr(tab),
                                                   len(self.plans), self.max_elems, 1 if accumulate else 0, s),
