@@ -580,21 +580,33 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
   const int w_dr = 256 / wvec_row, w_dk = 256 - w_dr * wvec_row;
   const int w_r0 = tid / wvec_row, w_k0 = tid - w_r0 * wvec_row;
   const int nrx = (nvec_x + 255) / 256, nrw = (nvec_w + 255) / 256;
+  // k-steps software-pipelined two deep: the fragments of k-step s+1 are read from LDS while the MFMAs of
+  // k-step s run (one wave per SIMD pair cannot hide the ds_read latency otherwise)
   auto compute = [&]() {
     const int nks = a.kcpad / 32;
-    for (int kstep = 0; kstep < nks; ++kstep) {
-      const int off = tab[kstep * 4 + g];
-      bf16x8 af[NT];
-      bf16x8 bfr[MW];
+    bf16x8 afA[NT], bfA[MW], afB[NT], bfB[MW];
+    auto ld = [&](int ks, bf16x8(&af)[NT], bf16x8(&bf)[MW]) {
+      const int off = tab[ks * 4 + g];
 #pragma unroll
-      for (int t = 0; t < NT; ++t) af[t] = *(const bf16x8*)(ws + (t * 16 + col) * wpitch + kstep * 32 + g * 8);
+      for (int t = 0; t < NT; ++t) af[t] = *(const bf16x8*)(ws + (t * 16 + col) * wpitch + ks * 32 + g * 8);
 #pragma unroll
-      for (int m = 0; m < MW; ++m) bfr[m] = *(const bf16x8*)(xs + pixbase[m] + off);
+      for (int m = 0; m < MW; ++m) bf[m] = *(const bf16x8*)(xs + pixbase[m] + off);
+    };
+    auto mm = [&](const bf16x8(&af)[NT], const bf16x8(&bf)[MW]) {
 #pragma unroll
       for (int m = 0; m < MW; ++m)
 #pragma unroll
-        for (int t = 0; t < NT; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bfr[m], acc[m][t], 0, 0, 0);
+        for (int t = 0; t < NT; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bf[m], acc[m][t], 0, 0, 0);
+    };
+    ld(0, afA, bfA);
+    int ks = 0;
+    for (; ks + 2 <= nks; ks += 2) {
+      ld(ks + 1, afB, bfB);
+      mm(afA, bfA);
+      ld(ks + 2 < nks ? ks + 2 : nks - 1, afA, bfA);  // unconditional (clamped): no branch around the reads
+      mm(afB, bfB);
     }
+    if (ks < nks) mm(afA, bfA);  // odd k-step count: the last one is already loaded
   };
 
   if constexpr (PFX > 0) {
@@ -2634,7 +2646,7 @@ __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
     if (tile + a.nsplit < a.ntiles) issue(tile + a.nsplit);
     __syncthreads();
     if (a.ablate & 2) continue;
-#pragma unroll
+#pragma unroll 2
     for (int kk = 0; kk < W64_TH * TW / 32; ++kk) {  // k-step: output pixel rows 2kk, 2kk+1
       const int k0 = kk * 32 + 8 * g + q, k1 = k0 + 4;
       bf16x8 af[4];
