@@ -857,8 +857,17 @@ struct TileWalk {
 
 static int n16_ncb(int in_c) { return in_c <= 32 ? 1 : (in_c <= 64 ? 2 : 4); }
 
-template <int NCB>
+// EP: epilogue specialisation (the per-tile epilogue is branch- and SALU-heavy when every option is a runtime
+// flag): 0 = generic (runtime flags), 1 = forward (bias + leaky relu, bf16 out), 2 = pull (leaky-relu
+// derivative from the bf16 activation res1, no bias, bf16 out).  The host picks 1/2 only when they match.
+template <int NCB, int EP>
 __global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs a) {
+  const bool has_bias = EP == 1 ? true : EP == 2 ? false : a.bias != nullptr;
+  const bool has_r1 = EP == 1 ? false : EP == 2 ? true : a.res1 != nullptr;
+  const bool has_r2 = EP != 0 ? false : a.res2 != nullptr;
+  const bool has_aux = EP != 0 ? false : a.aux != nullptr;
+  const int out_mode = EP != 0 ? 0 : a.out_mode;
+  const int act = EP == 1 ? 1 : EP == 2 ? 3 : a.act;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint16_t* xs = (uint16_t*)smem;
   float* part = (float*)smem;  // partial sums [cb][row][lane] (aliases the input tile after compute)
@@ -870,15 +879,15 @@ __global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs
 
   float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
   const int co = g * 4;
-  if (a.bias) {
+  if (has_bias) {
     bv.x = co < a.out_c ? a.bias[co] : 0.f;
     bv.y = co + 1 < a.out_c ? a.bias[co + 1] : 0.f;
     bv.z = co + 2 < a.out_c ? a.bias[co + 2] : 0.f;
     bv.w = co + 3 < a.out_c ? a.bias[co + 3] : 0.f;
   }
   const int ntiles = a.tiles_x * a.tiles_y * a.n;
-  const bool valign = ((a.out_cs | a.out_co) & 3) == 0 && (!a.res1 || ((a.r1_cs | a.r1_co) & 3) == 0) &&
-                      (!a.res2 || ((a.r2_cs | a.r2_co) & 3) == 0) && co + 3 < a.out_c;
+  const bool valign = EP != 0 || (((a.out_cs | a.out_co) & 3) == 0 && (!a.res1 || ((a.r1_cs | a.r1_co) & 3) == 0) &&
+                                   (!a.res2 || ((a.r2_cs | a.r2_co) & 3) == 0) && co + 3 < a.out_c);
 
   // staging: vector v = tid + 256 i of the tile is (pixel v / CV, channel group v % CV); CV is a power of
   // two, so consecutive lanes read consecutive 16 B of a pixel (coalesced) and the pad groups (>= cvec)
@@ -909,7 +918,8 @@ __global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs
   };
   const TileWalk walk(ntiles);
   if (walk.first < walk.end) issue(walk.first);
-  const __amdgpu_buffer_rsrc_t er1 = opt_rsrc(a.res1), er2 = opt_rsrc(a.res2), ery = opt_rsrc(a.out_mode == 2 ? a.y : nullptr);
+  const __amdgpu_buffer_rsrc_t er1 = opt_rsrc(has_r1 ? a.res1 : nullptr), er2 = opt_rsrc(has_r2 ? a.res2 : nullptr),
+                               ery = opt_rsrc(out_mode == 2 ? a.y : nullptr);
   // this wave's A fragments (channel block cb, 9 taps; packed rows are tap-major with CINP channels per
   // tap), loaded once per workgroup straight into VGPRs while the first tile's input is in flight
   bf16x8 af[9];
@@ -979,9 +989,10 @@ __global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs
       const bool ld = oy < a.out_h && ox < a.out_w && valign;
       const long pidx = ld ? ((long)nimg * a.out_h + oy) * a.out_w + ox : 0;
       const int c = ld ? co : 0;
-      r1v[h] = buf_load8(er1, (uint32_t)((pidx * a.r1_cs + (ld ? a.r1_co : 0) + c) * 2));
-      r2v[h] = buf_load8(er2, (uint32_t)((pidx * a.r2_cs + (ld ? a.r2_co : 0) + c) * 2));
-      const uint4 o4 = buf_load16(ery, (uint32_t)((pidx * a.out_cs + (ld ? a.out_co : 0) + c) * 4));
+      r1v[h] = has_r1 ? buf_load8(er1, (uint32_t)((pidx * a.r1_cs + (ld ? a.r1_co : 0) + c) * 2)) : make_uint2(0, 0);
+      r2v[h] = has_r2 ? buf_load8(er2, (uint32_t)((pidx * a.r2_cs + (ld ? a.r2_co : 0) + c) * 2)) : make_uint2(0, 0);
+      const uint4 o4 = out_mode == 2 ? buf_load16(ery, (uint32_t)((pidx * a.out_cs + (ld ? a.out_co : 0) + c) * 4))
+                                     : make_uint4(0, 0, 0, 0);
       old[h] = make_float4(__uint_as_float(o4.x), __uint_as_float(o4.y), __uint_as_float(o4.z), __uint_as_float(o4.w));
     }
 #pragma unroll
@@ -996,9 +1007,9 @@ __global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs
         const uint4 r1 = make_uint4(r1v[h].x, r1v[h].y, 0, 0), r2 = make_uint4(r2v[h].x, r2v[h].y, 0, 0);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          v[i] = ep_res(act_apply(sum[h][i] + bb[i], a.act, a.slope), a.act, a.slope, a.res1 != nullptr, res4_at(r1, false, i),
-                        a.alpha1, a.beta1, a.res2 != nullptr, res4_at(r2, false, i), a.alpha2, a.beta2);
-        if (a.out_mode == 0) {
+          v[i] = ep_res(act_apply(sum[h][i] + bb[i], act, a.slope), act, a.slope, has_r1, res4_at(r1, false, i), a.alpha1,
+                        a.beta1, has_r2, res4_at(r2, false, i), a.alpha2, a.beta2);
+        if (out_mode == 0) {
           uint2 pk;
           pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
           pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
@@ -1006,7 +1017,7 @@ __global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs
         } else {
           *(float4*)((float*)a.y + ob) = make_float4(old[h].x + v[0], old[h].y + v[1], old[h].z + v[2], old[h].w + v[3]);
         }
-        if (a.aux) {
+        if (has_aux) {
           uint2 pk;
           pk.x = (uint32_t)f2bf(a.aux_scale * v[0]) | ((uint32_t)f2bf(a.aux_scale * v[1]) << 16);
           pk.y = (uint32_t)f2bf(a.aux_scale * v[2]) | ((uint32_t)f2bf(a.aux_scale * v[3]) << 16);
@@ -1030,13 +1041,13 @@ __global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs
   }
 }
 
-template <int NCB>
+template <int NCB, int EP>
 static int launch_n16(const FwdArgs& a, hipStream_t s) {
   if (g_dry) {
-    snprintf(g_dry_name, sizeof(g_dry_name), "conv_n16_kernel<%d>", NCB);
+    snprintf(g_dry_name, sizeof(g_dry_name), "conv_n16_kernel<%d, %d>", NCB, EP);
     return CLIMSR_OK;
   }
-  auto k = conv_n16_kernel<NCB>;
+  auto k = conv_n16_kernel<NCB, EP>;
   size_t lds = (size_t)N16_TPH * N16_TPW * (NCB * 32 + 16) * 2;
   const size_t lds_p = (size_t)NCB * N16_TH * 64 * 16;             // partial sums (aliased)
   if (lds_p > lds) lds = lds_p;
@@ -2244,10 +2255,23 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
       (long)d->n * d->in_h * d->in_w * d->in_cstride * 2 < (1L << 31)) {  // 32-bit buffer offsets
     a.tiles_x = ceil_div(d->out_w, TW);
     a.tiles_y = ceil_div(d->out_h, N16_TH);
-    switch (d->cc / 32) {
-      case 1: return launch_n16<1>(a, s);
-      case 2: return launch_n16<2>(a, s);
-      default: return launch_n16<4>(a, s);
+    // epilogue specialisations (see conv_n16_kernel): forward conv1-4 and the pull data gradients
+    const bool al = ((a.out_cs | a.out_co) & 3) == 0 && d->out_c == 16;
+    const int ep_mode = (al && a.act == 1 && a.bias && !a.res1 && !a.res2 && !a.aux && a.out_mode == 0) ? 1
+                        : (al && a.act == 3 && !a.bias && a.res1 && !(a.res_f32 & 1) && ((a.r1_cs | a.r1_co) & 3) == 0 &&
+                           !a.res2 && !a.aux && a.out_mode == 0)
+                            ? 2
+                            : 0;
+    switch ((d->cc / 32) * 4 + ep_mode) {
+      case 4: return launch_n16<1, 0>(a, s);
+      case 5: return launch_n16<1, 1>(a, s);
+      case 6: return launch_n16<1, 2>(a, s);
+      case 8: return launch_n16<2, 0>(a, s);
+      case 9: return launch_n16<2, 1>(a, s);
+      case 10: return launch_n16<2, 2>(a, s);
+      case 17: return launch_n16<4, 1>(a, s);
+      case 18: return launch_n16<4, 2>(a, s);
+      default: return launch_n16<4, 0>(a, s);
     }
   }
   // conv_co64_kernel (A fragments register-resident, K halves per wave) measured slower than the generic

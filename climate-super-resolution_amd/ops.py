@@ -30,22 +30,6 @@ def round_up(a: int, b: int) -> int:
 PROFILER = None
 
 
-def _fwd_nt(out_c: int) -> int:
-    nt = (out_c + 15) // 16
-    return 4 if nt >= 3 else nt
-
-
-def fwd_kernel_name(out_c: int, out_h: int = 16, res_f32: bool = False, cin: int = 0, ks: int = 0, stride: int = 1,
-                    up: int = 1) -> str:
-    if out_c == 1:
-        return "conv_co1_kernel"
-    if out_c <= 16 and ks == 3 and cin <= 128 and stride == 1 and up == 1 and not res_f32:
-        return f"conv_n16_kernel<{1 if cin <= 32 else 2 if cin <= 64 else 4}>"
-    nt = _fwd_nt(out_c)
-    mv = {1: 6, 2: 8, 4: 4}[nt]
-    return f"conv_fwd_kernel<{4 if (out_h >= 12 and nt == 4) else 2}, {nt}, {'true' if res_f32 else 'false'}, {mv}>"
-
-
 def wgrad_kernel_name(out_c: int, ks: int, ci4: bool = False, cin: int = 0, stride: int = 1, pad: int = 1) -> str:
     """Mirrors climsr_conv2d_wgrad's dispatch (profiler labels only)."""
     if ks == 1 and stride == 1 and pad == 0 and cin == 64 and out_c % 16 == 0 and out_c <= 64:
@@ -226,8 +210,8 @@ class ConvPlan:
         flops = 2 * self.cin_real * self.cout * self.ks * self.ks * n * d.out_h * d.out_w
         nbytes = n * in_h * in_w * self.cin_real * 2 + n * d.out_h * d.out_w * self.cout * 2 + self.cout * self.cin_real * self.ks ** 2 * 4
         _run(wgrad_kernel_name(self.cout, self.ks, self.cin_w == 4, self.cin_w, self.stride, self.pad), flops, lambda: check(
-            lib.climsr_conv2d_wgrad(ctypes.byref(d), ptr(x), ptr(dz), dz_cs, ptr(part), ptr(bpart) if has_b else None, ns, s),
-            f"conv wgrad {self.name}"), "wgrad " + self.name, nbytes)
+            lib.climsr_conv2d_wgrad(ctypes.byref(d), ptr(x), ptr(dz), dz_cs, ptr(part), ptr(bpart) if has_b else None, ns,
+                                    _lib.stream_ptr()), f"conv wgrad {self.name}"), "wgrad " + self.name, nbytes)
         check(lib.climsr_conv2d_wgrad_reduce(ptr(part), ptr(bpart) if has_b else None, ns, self.cout, self.cin_real, cw,
                                              self.ks, ptr(self.gw), ptr(self.gb) if has_b else None,
                                              1 if accumulate else 0, s), f"wgrad reduce {self.name}")
@@ -275,7 +259,7 @@ class GroupedWgrad:
         flops = sum(2 * p.cin_real * p.cout * 9 for p in self.plans) * n * in_h * in_w
         nbytes = n * in_h * in_w * (self.in_c + self.out_c) * 2 + sum(p.cout * p.cin_real * 9 * 4 for p in self.plans)
         _run("conv_wgrad64_kernel", flops, lambda: check(
-            lib.climsr_conv2d_wgrad(ctypes.byref(d), ptr(x), ptr(dz), dz_cs, ptr(part), ptr(bpart), ns, s),
+            lib.climsr_conv2d_wgrad(ctypes.byref(d), ptr(x), ptr(dz), dz_cs, ptr(part), ptr(bpart), ns, _lib.stream_ptr()),
             f"grouped wgrad {self.name}"), "wgrad " + self.name, nbytes)
         tab = self._table(x.device)
         check(lib.climsr_conv2d_wgrad_reduce_rows(ptr(part), ptr(bpart), ns, self.out_c, self.in_c * 9, 3, ptr(tab),
