@@ -433,15 +433,26 @@ __device__ __forceinline__ uint4 pack8_bf16(const float* v, float scale) {
 // owns 8 consecutive channels of one pixel, so global stores / residual loads are 16 B (bf16) or 32 B
 // (fp32) per lane and 8 lanes cover a 64-channel pixel row (8 B per lane stores are issue-bound).
 // npx pixels (pixel p -> output (oy0 + p / 16, ox0 + p % 16)), nch channels starting at co0.
-template <bool RF, int NPX, int NCH, int NLANE>
+// EP (epilogue specialisation, picked on the host only when the arguments match; 0 = every option a runtime
+// flag): 1 = residual forward (bias, no activation, bf16 residual(s), bf16 output: RDB conv5, trunk_conv),
+// 2 = fp32 data gradient (no bias / activation, fp32 residual(s), fp32 '=' output, optional bf16 aux: pull-x).
+template <bool RF, int NPX, int NCH, int NLANE, int EP = 0>
 __device__ __forceinline__ void store_tile_lds(const FwdArgs& a, const float* eb, int ep, int lane, int nimg, int oy0, int ox0,
                                                int co0) {
   constexpr int NG = NCH / 8, NIT = NPX * NG;
-  const bool f1 = RF && (a.res_f32 & 1), f2 = RF && ((a.res_f32 >> 1) & 1);
-  const bool vec = (a.out_c & 7) == 0 && ((a.out_cs | a.out_co) & 7) == 0 && (!a.res1 || ((a.r1_cs | a.r1_co) & 7) == 0) &&
-                   (!a.res2 || ((a.r2_cs | a.r2_co) & 7) == 0) && (!a.aux || ((a.aux_cs | a.aux_co) & 7) == 0);
+  const bool f1 = EP == 1 ? false : EP == 2 ? true : RF && (a.res_f32 & 1);
+  const bool f2 = EP == 1 ? false : EP == 2 ? true : RF && ((a.res_f32 >> 1) & 1);
+  const bool has_bias = EP == 1 ? true : EP == 2 ? false : a.bias != nullptr;
+  const int act = EP != 0 ? 0 : a.act;
+  const bool has1 = EP != 0 ? true : a.res1 != nullptr;
+  const bool has2 = a.res2 != nullptr;
+  const int out_mode = EP == 1 ? 0 : EP == 2 ? 1 : a.out_mode;
+  const bool has_aux = EP == 1 ? false : a.aux != nullptr;
+  const bool vec = EP != 0 || ((a.out_c & 7) == 0 && ((a.out_cs | a.out_co) & 7) == 0 && (!a.res1 || ((a.r1_cs | a.r1_co) & 7) == 0) &&
+                               (!a.res2 || ((a.r2_cs | a.r2_co) & 7) == 0) && (!a.aux || ((a.aux_cs | a.aux_co) & 7) == 0));
   constexpr int IB = RF ? 2 : 4;  // items per round: their global loads are in flight together
-  const __amdgpu_buffer_rsrc_t rr1 = opt_rsrc(a.res1), rr2 = opt_rsrc(a.res2), rry = opt_rsrc(a.out_mode == 2 ? a.y : nullptr);
+  const __amdgpu_buffer_rsrc_t rr1 = opt_rsrc(has1 ? a.res1 : nullptr), rr2 = opt_rsrc(a.res2),
+                               rry = opt_rsrc(out_mode == 2 ? a.y : nullptr);
 #pragma unroll
   for (int base = 0; base < (NIT + NLANE - 1) / NLANE; base += IB) {
     Raw8 r1[IB], r2[IB], old[IB];
@@ -460,7 +471,8 @@ __device__ __forceinline__ void store_tile_lds(const FwdArgs& a, const float* eb
       const int c = ld ? co : 0;
       r1[j] = load8b(rr1, f1, pidx * a.r1_cs + (ld ? a.r1_co : 0) + c);
       r2[j] = load8b(rr2, f2, pidx * a.r2_cs + (ld ? a.r2_co : 0) + c);
-      old[j] = load8b(rry, true, pidx * a.out_cs + (ld ? a.out_co : 0) + c);
+      if (out_mode == 2) old[j] = load8b(rry, true, pidx * a.out_cs + (ld ? a.out_co : 0) + c);
+      else old[j].lo = old[j].hi = make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int j = 0; j < IB; ++j) {
@@ -474,26 +486,26 @@ __device__ __forceinline__ void store_tile_lds(const FwdArgs& a, const float* eb
       const long ob = pidx * a.out_cs + a.out_co + co;
       if (vec && co + 7 < a.out_c) {
         float4 b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0;
-        if (a.bias) {
+        if (has_bias) {
           b0 = *(const float4*)(a.bias + co);
           b1 = *(const float4*)(a.bias + co + 4);
         }
         const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
         for (int i = 0; i < 8; ++i)
-          v[i] = ep_res(act_apply(v[i] + bb[i], a.act, a.slope), a.act, a.slope, a.res1 != nullptr, raw8_at(r1[j], f1, i), a.alpha1,
-                        a.beta1, a.res2 != nullptr, raw8_at(r2[j], f2, i), a.alpha2, a.beta2);
-        if (a.out_mode == 0) {
+          v[i] = ep_res(act_apply(v[i] + bb[i], act, a.slope), act, a.slope, has1, raw8_at(r1[j], f1, i), a.alpha1, a.beta1, has2,
+                        raw8_at(r2[j], f2, i), a.alpha2, a.beta2);
+        if (out_mode == 0) {
           *(uint4*)((uint16_t*)a.y + ob) = pack8_bf16(v, 1.f);
         } else {
           float o[8];
 #pragma unroll
-          for (int i = 0; i < 8; ++i) o[i] = v[i] + (a.out_mode == 2 ? raw8_at(old[j], true, i) : 0.f);
+          for (int i = 0; i < 8; ++i) o[i] = v[i] + (out_mode == 2 ? raw8_at(old[j], true, i) : 0.f);
           *(float4*)((float*)a.y + ob) = make_float4(o[0], o[1], o[2], o[3]);
           *(float4*)((float*)a.y + ob + 4) = make_float4(o[4], o[5], o[6], o[7]);
         }
-        if (a.aux) *(uint4*)(a.aux + pidx * a.aux_cs + a.aux_co + co) = pack8_bf16(v, a.aux_scale);
-      } else {  // scalar tail (channel counts / slices not multiples of 8)
+        if (has_aux) *(uint4*)(a.aux + pidx * a.aux_cs + a.aux_co + co) = pack8_bf16(v, a.aux_scale);
+      } else if (EP == 0) {  // scalar tail (channel counts / slices not multiples of 8)
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           if (co + i >= a.out_c) continue;
@@ -514,7 +526,7 @@ __device__ __forceinline__ void store_tile_lds(const FwdArgs& a, const float* eb
 // PF > 0: software-pipelined chunks.  Chunk j+1's input and weight vectors (at most PFX + PFW per thread) are
 // loaded into registers while chunk j is on the MFMA pipe, so a multi-chunk tile (RDB conv5 / pull-x: four
 // 32-channel chunks) pays one staging latency instead of one per chunk.
-template <int MW, int NT, bool RF, int MV, int PFX = 0, int PFW = 0>
+template <int MW, int NT, bool RF, int MV, int PFX = 0, int PFW = 0, int EP = 0>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int* tab = (int*)smem;
@@ -728,7 +740,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
   // All global reads of the epilogue (bias, residuals, accumulate targets) are issued for every
   // fragment before the first store, so their latencies overlap instead of serialising.
   const int ox = ox0 + col;
-  if (a.down2) {
+  if (EP == 0 && a.down2) {
     // sum the 2x2 block: rows (m, m+1) are in this wave (MW even, oy0 even); columns pair via lane^1.
     // Optional activation backward (act 3/4, res1 = the activation output at the LOW-res pixel), bf16 or
     // fp32 (=, +=) store and a bf16 aux copy.
@@ -815,7 +827,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) *(f32x4*)(eb + (m * 16 + col) * EPP + t * 16 + g * 4) = acc[m][t];
   __syncthreads();  // orders the staging writes before the transposed reads (they use another vector type)
-  store_tile_lds<RF, MW * 16, NT * 16, 64>(a, eb, EPP, lane, nimg, oy0 + wave * MW, ox0, co_blk0);
+  store_tile_lds<RF, MW * 16, NT * 16, 64, EP>(a, eb, EPP, lane, nimg, oy0 + wave * MW, ox0, co_blk0);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2148,28 +2160,33 @@ static int dispatch_pt(const ClimsrConvDesc* d, const FwdArgs& a, hipStream_t s)
   }
 }
 
-template <int MW, int NT, int PFX = 0, int PFW = 0>
-static int launch_fwd(const FwdArgs& a, int ncob, size_t lds, hipStream_t s) {
+template <int MW, int NT, int PFX = 0, int PFW = 0, int EP = 0>
+static int launch_fwd_ep(const FwdArgs& a, int ncob, size_t lds, hipStream_t s) {
   dim3 grid(a.tiles_x * a.tiles_y * a.n, ncob);
   const size_t lds_ep = (size_t)4 * MW * 16 * (NT * 16 + 4) * 4;  // epilogue staging (aliases the operands)
   if (lds_ep > lds) lds = lds_ep;
   constexpr int MV = NT == 1 ? 6 : (NT == 2 ? 8 : 4);
   if (g_dry) {
-    if (PFX) snprintf(g_dry_name, sizeof(g_dry_name), "conv_fwd_kernel<%d, %d, %s, %d, %d, %d>", MW, NT, a.res_f32 ? "true" : "false", MV, PFX, PFW);
+    if (PFX) snprintf(g_dry_name, sizeof(g_dry_name), "conv_fwd_kernel<%d, %d, %s, %d, %d, %d, %d>", MW, NT, a.res_f32 ? "true" : "false", MV, PFX, PFW, EP);
     else snprintf(g_dry_name, sizeof(g_dry_name), "conv_fwd_kernel<%d, %d, %s, %d>", MW, NT, a.res_f32 ? "true" : "false", MV);
     return CLIMSR_OK;
   }
-  auto k = a.res_f32 ? conv_fwd_kernel<MW, NT, true, MV, PFX, PFW> : conv_fwd_kernel<MW, NT, false, MV, PFX, PFW>;
+  auto k = a.res_f32 ? conv_fwd_kernel<MW, NT, true, MV, PFX, PFW, EP> : conv_fwd_kernel<MW, NT, false, MV, PFX, PFW, EP>;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)conv_fwd_kernel<MW, NT, true, MV, PFX, PFW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)conv_fwd_kernel<MW, NT, true, MV, PFX, PFW, EP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
-    (void)hipFuncSetAttribute((const void*)conv_fwd_kernel<MW, NT, false, MV, PFX, PFW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)conv_fwd_kernel<MW, NT, false, MV, PFX, PFW, EP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     attr_set = true;
   }
   hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a);
   return check_launch("conv2d_fwd");
+}
+
+template <int MW, int NT, int PFX = 0, int PFW = 0>
+static int launch_fwd(const FwdArgs& a, int ncob, size_t lds, hipStream_t s) {
+  return launch_fwd_ep<MW, NT, PFX, PFW, 0>(a, ncob, lds, s);
 }
 
 static bool fwd_pf_disabled() {
@@ -2312,7 +2329,16 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
   if (mw == 4) {
     // multi-chunk tiles whose per-thread staging fits 6 input + 9 weight vectors: chunk-pipelined variant
     const int nrx = ceil_div(g.tph * g.tpw * (d->cc / 8), 256), nrw = ceil_div(g.nt * 16 * (g.kcpad / 8), 256);
-    if (g.nchunk > 1 && nrx <= 6 && nrw <= 9 && !fwd_pf_disabled()) return launch_fwd<4, 4, 6, 9>(a, ncob, g.lds_total, s);
+    if (g.nchunk > 1 && nrx <= 6 && nrw <= 9 && !fwd_pf_disabled()) {
+      // epilogue specialisations (store_tile_lds EP): residual forward (conv5, trunk_conv) / fp32 pull-x
+      const bool v8 = (a.out_c & 7) == 0 && ((a.out_cs | a.out_co) & 7) == 0 && ((a.r1_cs | a.r1_co) & 7) == 0 &&
+                      (!a.res2 || ((a.r2_cs | a.r2_co) & 7) == 0) && (!a.aux || ((a.aux_cs | a.aux_co) & 7) == 0) && !a.down2 &&
+                      a.act == 0 && a.res1;
+      if (v8 && a.bias && a.res_f32 == 0 && a.out_mode == 0 && !a.aux) return launch_fwd_ep<4, 4, 6, 9, 1>(a, ncob, g.lds_total, s);
+      if (v8 && !a.bias && (a.res_f32 & 1) && (!a.res2 || (a.res_f32 & 2)) && a.out_mode == 1)
+        return launch_fwd_ep<4, 4, 6, 9, 2>(a, ncob, g.lds_total, s);
+      return launch_fwd<4, 4, 6, 9>(a, ncob, g.lds_total, s);
+    }
     return launch_fwd<4, 4>(a, ncob, g.lds_total, s);
   }
   switch (g.nt) {
