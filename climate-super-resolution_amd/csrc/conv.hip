@@ -440,18 +440,20 @@ template <bool RF, int NPX, int NCH, int NLANE, int EP = 0>
 __device__ __forceinline__ void store_tile_lds(const FwdArgs& a, const float* eb, int ep, int lane, int nimg, int oy0, int ox0,
                                                int co0) {
   constexpr int NG = NCH / 8, NIT = NPX * NG;
-  const bool f1 = EP == 1 ? false : EP == 2 ? true : RF && (a.res_f32 & 1);
-  const bool f2 = EP == 1 ? false : EP == 2 ? true : RF && ((a.res_f32 >> 1) & 1);
-  const bool has_bias = EP == 1 ? true : EP == 2 ? false : a.bias != nullptr;
-  const int act = EP != 0 ? 0 : a.act;
-  const bool has1 = EP != 0 ? true : a.res1 != nullptr;
-  const bool has2 = a.res2 != nullptr;
-  const int out_mode = EP == 1 ? 0 : EP == 2 ? 1 : a.out_mode;
-  const bool has_aux = EP == 1 ? false : a.aux != nullptr;
+  // EP 3 = activation forward (bias + leaky relu / relu, bf16 out); 4 = activation backward (act' read from
+  // the bf16 activation res1, no bias, bf16 out): the HR-resolution layers (conv_pw_kernel)
+  const bool f1 = (EP == 1 || EP >= 3) ? false : EP == 2 ? true : RF && (a.res_f32 & 1);
+  const bool f2 = (EP == 1 || EP >= 3) ? false : EP == 2 ? true : RF && ((a.res_f32 >> 1) & 1);
+  const bool has_bias = (EP == 1 || EP == 3) ? true : (EP == 2 || EP == 4) ? false : a.bias != nullptr;
+  const int act = (EP == 1 || EP == 2) ? 0 : a.act;
+  const bool has1 = (EP == 1 || EP == 2 || EP == 4) ? true : EP == 3 ? false : a.res1 != nullptr;
+  const bool has2 = EP >= 3 ? false : a.res2 != nullptr;
+  const int out_mode = (EP == 1 || EP >= 3) ? 0 : EP == 2 ? 1 : a.out_mode;
+  const bool has_aux = (EP == 1 || EP >= 3) ? false : a.aux != nullptr;
   const bool vec = EP != 0 || ((a.out_c & 7) == 0 && ((a.out_cs | a.out_co) & 7) == 0 && (!a.res1 || ((a.r1_cs | a.r1_co) & 7) == 0) &&
                                (!a.res2 || ((a.r2_cs | a.r2_co) & 7) == 0) && (!a.aux || ((a.aux_cs | a.aux_co) & 7) == 0));
   constexpr int IB = RF ? 2 : 4;  // items per round: their global loads are in flight together
-  const __amdgpu_buffer_rsrc_t rr1 = opt_rsrc(has1 ? a.res1 : nullptr), rr2 = opt_rsrc(a.res2),
+  const __amdgpu_buffer_rsrc_t rr1 = opt_rsrc(has1 ? a.res1 : nullptr), rr2 = opt_rsrc(has2 ? a.res2 : nullptr),
                                rry = opt_rsrc(out_mode == 2 ? a.y : nullptr);
 #pragma unroll
   for (int base = 0; base < (NIT + NLANE - 1) / NLANE; base += IB) {
@@ -469,9 +471,12 @@ __device__ __forceinline__ void store_tile_lds(const FwdArgs& a, const float* eb
       const bool ld = ok[j] && vec && co + 7 < a.out_c;  // else the values are unused
       const long pidx = ld ? pidxs[j] : 0;
       const int c = ld ? co : 0;
-      r1[j] = load8b(rr1, f1, pidx * a.r1_cs + (ld ? a.r1_co : 0) + c);
-      r2[j] = load8b(rr2, f2, pidx * a.r2_cs + (ld ? a.r2_co : 0) + c);
-      if (out_mode == 2) old[j] = load8b(rry, true, pidx * a.out_cs + (ld ? a.out_co : 0) + c);
+      // (EP 0: unconditional, a null operand reads zeros; EP > 0: compile-time known)
+      if (EP == 0 || has1) r1[j] = load8b(rr1, f1, pidx * a.r1_cs + (ld ? a.r1_co : 0) + c);
+      else r1[j].lo = r1[j].hi = make_uint4(0, 0, 0, 0);
+      if (EP == 0 || has2) r2[j] = load8b(rr2, f2, pidx * a.r2_cs + (ld ? a.r2_co : 0) + c);
+      else r2[j].lo = r2[j].hi = make_uint4(0, 0, 0, 0);
+      if (EP == 0 || out_mode == 2) old[j] = load8b(rry, true, pidx * a.out_cs + (ld ? a.out_co : 0) + c);
       else old[j].lo = old[j].hi = make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
@@ -1593,7 +1598,7 @@ static bool pw_fits(int in_c, int ks, int out_c) {
   return pw_geom(&d, nt, 2, &g, 4);
 }
 
-template <int NW, int MW, int NT, bool RF, int PV>
+template <int NW, int MW, int NT, bool RF, int PV, int EP = 0>
 __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
   constexpr int NTHR = 64 * NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1724,7 +1729,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
       continue;
     }
     const int ox = ox0 + col;
-    if (a.down2) {  // 2x2 sum (data gradient of the nearest upsample): rows (m, m+1), columns via lane ^ 1
+    if (EP == 0 && a.down2) {  // 2x2 sum (data gradient of the nearest upsample): rows (m, m+1), columns via lane ^ 1
       const int dh = a.out_h >> 1, dw = a.out_w >> 1;
       const bool mask = a.act == 3 || a.act == 4;
 #pragma unroll
@@ -1766,14 +1771,14 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) *(f32x4*)(eb + (m * 16 + col) * EPP + t * 16 + g * 4) = acc[m][t];
     lds_barrier();
-    store_tile_lds<RF, MW * 16, NT * 16, 64>(a, eb, EPP, lane, nimg, oy0 + wave * MW, ox0, 0);
+    store_tile_lds<RF, MW * 16, NT * 16, 64, EP>(a, eb, EPP, lane, nimg, oy0 + wave * MW, ox0, 0);
   }
 }
 
-template <int NW, int MW, int NT, int PV>
+template <int NW, int MW, int NT, int PV, int EP = 0>
 static int launch_pw(const FwdArgs& a0, const PwGeom& g, hipStream_t s) {
   if (g_dry) {
-    snprintf(g_dry_name, sizeof(g_dry_name), "conv_pw_kernel<%d, %d, %d, %s, %d>", NW, MW, NT, a0.res_f32 ? "true" : "false", PV);
+    snprintf(g_dry_name, sizeof(g_dry_name), "conv_pw_kernel<%d, %d, %d, %s, %d, %d>", NW, MW, NT, a0.res_f32 ? "true" : "false", PV, EP);
     return CLIMSR_OK;
   }
   FwdArgs a = a0;
@@ -1782,12 +1787,12 @@ static int launch_pw(const FwdArgs& a0, const PwGeom& g, hipStream_t s) {
   a.tiles_y = ceil_div(a.out_h, NW * MW);
   a.lds_tab = (int)g.lds_tab;
   a.lds_x = (int)g.lds_w;  // offset of the input tile = tab + weights
-  auto k = a.res_f32 ? conv_pw_kernel<NW, MW, NT, true, PV> : conv_pw_kernel<NW, MW, NT, false, PV>;
+  auto k = a.res_f32 ? conv_pw_kernel<NW, MW, NT, true, PV, EP> : conv_pw_kernel<NW, MW, NT, false, PV, EP>;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)conv_pw_kernel<NW, MW, NT, true, PV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)conv_pw_kernel<NW, MW, NT, true, PV, EP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
-    (void)hipFuncSetAttribute((const void*)conv_pw_kernel<NW, MW, NT, false, PV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)conv_pw_kernel<NW, MW, NT, false, PV, EP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     attr_set = true;
   }
@@ -2317,8 +2322,17 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
     if (ncob == 1 && (nt == 4 || nt == 2) && d->up != -2 && npx >= 4096 && !pw_disabled() &&
         (long)d->n * d->in_h * d->in_w * d->in_cstride * 2 < (1L << 31)) {  // 32-bit buffer offsets
       // 8 waves x 2 rows (two waves per SIMD) when the LDS allows, else 4 waves x 2 rows
-      if (pw_geom(d, nt, 2, &pg, 8) && pg.nvx <= 512 * 7 && d->out_h >= 16)
-        return nt == 4 ? launch_pw<8, 2, 4, 7>(a, pg, s) : launch_pw<8, 2, 2, 7>(a, pg, s);
+      if (pw_geom(d, nt, 2, &pg, 8) && pg.nvx <= 512 * 7 && d->out_h >= 16) {
+        // epilogue specialisations (store_tile_lds EP 3 / 4): activation forward / activation backward
+        const bool v8 = (a.out_c & 7) == 0 && ((a.out_cs | a.out_co) & 7) == 0 && !a.down2 && !a.res2 && !a.aux &&
+                        a.out_mode == 0 && a.res_f32 == 0;
+        const int epm = (v8 && a.bias && !a.res1 && (a.act == 1 || a.act == 2)) ? 3
+                        : (v8 && !a.bias && a.res1 && ((a.r1_cs | a.r1_co) & 7) == 0 && (a.act == 3 || a.act == 4)) ? 4 : 0;
+        if (nt == 4) return epm == 3 ? launch_pw<8, 2, 4, 7, 3>(a, pg, s) : epm == 4 ? launch_pw<8, 2, 4, 7, 4>(a, pg, s)
+                                                                                    : launch_pw<8, 2, 4, 7>(a, pg, s);
+        return epm == 3 ? launch_pw<8, 2, 2, 7, 3>(a, pg, s) : epm == 4 ? launch_pw<8, 2, 2, 7, 4>(a, pg, s)
+                                                                        : launch_pw<8, 2, 2, 7>(a, pg, s);
+      }
       if (pw_geom(d, nt, 2, &pg, 4)) return nt == 4 ? launch_pw<4, 2, 4, 12>(a, pg, s) : launch_pw<4, 2, 2, 12>(a, pg, s);
     }
   }
