@@ -1729,6 +1729,44 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
       continue;
     }
     const int ox = ox0 + col;
+    if constexpr (EP == 5) {  // 2x2 sum + activation backward (act' of the bf16 low-res activation res1), bf16 out,
+                              // 4 channels (8 B) per lane; all operand loads issued before the first store
+      const int dh = a.out_h >> 1, dw = a.out_w >> 1;
+      const __amdgpu_buffer_rsrc_t rm1 = opt_rsrc(a.res1);
+      uint2 r1v[MW / 2][NT];
+#pragma unroll
+      for (int m = 0; m < MW; m += 2) {
+        const int oy = oy0 + wave * MW + m;
+        const bool ok = !(col & 1) && oy < a.out_h && ox < a.out_w;
+        const long q = ok ? ((long)nimg * dh + (oy >> 1)) * dw + (ox >> 1) : 0;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) r1v[m / 2][t] = buf_load8(rm1, (uint32_t)((q * a.r1_cs + (ok ? a.r1_co + t * 16 + g * 4 : 0)) * 2));
+      }
+#pragma unroll
+      for (int m = 0; m < MW; m += 2) {
+        const int oy = oy0 + wave * MW + m;
+        const long pidx = ((long)nimg * dh + (oy >> 1)) * dw + (ox >> 1);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          float v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float sm = acc[m][t][i] + acc[m + 1][t][i];
+            sm += __shfl_xor(sm, 1);
+            v[i] = sm;
+          }
+          if ((col & 1) || oy >= a.out_h || ox >= a.out_w) continue;
+          const uint4 r1 = make_uint4(r1v[m / 2][t].x, r1v[m / 2][t].y, 0, 0);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = ep_res(v[i], a.act, a.slope, true, res4_at(r1, false, i), 1.f, 1.f, false, 0.f, 1.f, 1.f);
+          uint2 pk;
+          pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+          pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+          *(uint2*)((uint16_t*)a.y + pidx * a.out_cs + a.out_co + t * 16 + g * 4) = pk;
+        }
+      }
+      continue;
+    }
     if (EP == 0 && a.down2) {  // 2x2 sum (data gradient of the nearest upsample): rows (m, m+1), columns via lane ^ 1
       const int dh = a.out_h >> 1, dw = a.out_w >> 1;
       const bool mask = a.act == 3 || a.act == 4;
@@ -2326,10 +2364,13 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
         // epilogue specialisations (store_tile_lds EP 3 / 4): activation forward / activation backward
         const bool v8 = (a.out_c & 7) == 0 && ((a.out_cs | a.out_co) & 7) == 0 && !a.down2 && !a.res2 && !a.aux &&
                         a.out_mode == 0 && a.res_f32 == 0;
+        const bool d2 = a.down2 && a.out_c == 64 && ((a.out_cs | a.out_co) & 3) == 0 && !a.bias && a.res1 && a.res_f32 == 0 &&
+                        ((a.r1_cs | a.r1_co) & 3) == 0 && (a.act == 3 || a.act == 4) && !a.res2 && !a.aux && a.out_mode == 0;
         const int epm = (v8 && a.bias && !a.res1 && (a.act == 1 || a.act == 2)) ? 3
-                        : (v8 && !a.bias && a.res1 && ((a.r1_cs | a.r1_co) & 7) == 0 && (a.act == 3 || a.act == 4)) ? 4 : 0;
+                        : (v8 && !a.bias && a.res1 && ((a.r1_cs | a.r1_co) & 7) == 0 && (a.act == 3 || a.act == 4)) ? 4
+                        : d2 ? 5 : 0;
         if (nt == 4) return epm == 3 ? launch_pw<8, 2, 4, 7, 3>(a, pg, s) : epm == 4 ? launch_pw<8, 2, 4, 7, 4>(a, pg, s)
-                                                                                    : launch_pw<8, 2, 4, 7>(a, pg, s);
+                            : epm == 5 ? launch_pw<8, 2, 4, 7, 5>(a, pg, s) : launch_pw<8, 2, 4, 7>(a, pg, s);
         return epm == 3 ? launch_pw<8, 2, 2, 7, 3>(a, pg, s) : epm == 4 ? launch_pw<8, 2, 2, 7, 4>(a, pg, s)
                                                                         : launch_pw<8, 2, 2, 7>(a, pg, s);
       }
