@@ -58,14 +58,14 @@ def pmc_traffic(kernel):
     import glob
 
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
-    for f in reversed(files):
-        try:
-            rec = json.load(open(f))["kernels"].get(kernel)
-        except (OSError, ValueError, KeyError):
-            continue
-        if rec:
-            return rec["hbm_bytes_per_launch"], os.path.basename(f)
-    return None, None
+    if not files:
+        return None, None
+    f = files[-1]  # only the newest build's counters: an older build's bytes would describe other code
+    try:
+        rec = json.load(open(f))["kernels"].get(kernel)
+    except (OSError, ValueError, KeyError):
+        return None, None
+    return (rec["hbm_bytes_per_launch"], os.path.basename(f)) if rec else (None, None)
 
 
 class KernelTimer:

@@ -30,14 +30,14 @@ def round_up(a: int, b: int) -> int:
 PROFILER = None
 
 
-def wgrad_kernel_name(out_c: int, ks: int, ci4: bool = False, cin: int = 0, stride: int = 1, pad: int = 1) -> str:
-    """Mirrors climsr_conv2d_wgrad's dispatch (profiler labels only)."""
+def wgrad_kernel_name(out_c: int, ks: int, ci4: bool = False, cin: int = 0, stride: int = 1, pad: int = 1, npx: int = 0) -> str:
+    """Mirrors climsr_conv2d_wgrad's dispatch (profiler labels only); npx = output pixels (n * h * w)."""
     if ks == 1 and stride == 1 and pad == 0 and cin == 64 and out_c % 16 == 0 and out_c <= 64:
         return f"conv_wgrad_pt_kernel<{out_c // 16}>"
     if out_c == 1 and stride == 1 and ks in (3, 5) and pad == ks // 2 and cin % 16 == 0 and cin <= 64:
         return f"conv_wgrad_co1m_kernel<{ks}, {cin // 16}>"
     if ks == 3 and stride == 1 and pad == 1 and out_c % 64 == 0 and cin % 64 == 0 and cin >= 64:
-        return "conv_wgrad64_kernel"
+        return f"conv_wgrad64_kernel<{2 if npx >= (1 << 20) else 1}>"  # 8-wave tap split at >= 1M pixels
     rows = round_up(out_c, 16)
     ntc = 4 if rows >= 64 else (2 if rows >= 32 else 1)
     k2 = ks * ks
@@ -209,7 +209,8 @@ class ConvPlan:
         has_b = self.bias is not None and self.gb is not None
         flops = 2 * self.cin_real * self.cout * self.ks * self.ks * n * d.out_h * d.out_w
         nbytes = n * in_h * in_w * self.cin_real * 2 + n * d.out_h * d.out_w * self.cout * 2 + self.cout * self.cin_real * self.ks ** 2 * 4
-        _run(wgrad_kernel_name(self.cout, self.ks, self.cin_w == 4, self.cin_w, self.stride, self.pad), flops, lambda: check(
+        _run(wgrad_kernel_name(self.cout, self.ks, self.cin_w == 4, self.cin_w, self.stride, self.pad, n * d.out_h * d.out_w), flops,
+             lambda: check(
             lib.climsr_conv2d_wgrad(ctypes.byref(d), ptr(x), ptr(dz), dz_cs, ptr(part), ptr(bpart) if has_b else None, ns,
                                     _lib.stream_ptr()), f"conv wgrad {self.name}"), "wgrad " + self.name, nbytes)
         check(lib.climsr_conv2d_wgrad_reduce(ptr(part), ptr(bpart) if has_b else None, ns, self.cout, self.cin_real, cw,
@@ -258,7 +259,7 @@ class GroupedWgrad:
         s = _lib.stream_ptr()
         flops = sum(2 * p.cin_real * p.cout * 9 for p in self.plans) * n * in_h * in_w
         nbytes = n * in_h * in_w * (self.in_c + self.out_c) * 2 + sum(p.cout * p.cin_real * 9 * 4 for p in self.plans)
-        _run("conv_wgrad64_kernel", flops, lambda: check(
+        _run(f"conv_wgrad64_kernel<{2 if n * in_h * in_w >= (1 << 20) else 1}>", flops, lambda: check(
             lib.climsr_conv2d_wgrad(ctypes.byref(d), ptr(x), ptr(dz), dz_cs, ptr(part), ptr(bpart), ns, _lib.stream_ptr()),
             f"grouped wgrad {self.name}"), "wgrad " + self.name, nbytes)
         tab = self._table(x.device)
