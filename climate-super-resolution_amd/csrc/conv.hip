@@ -2036,7 +2036,9 @@ static bool pt_shape(const ClimsrConvDesc* d, const ClimsrEpilogue* ep) {
          (!ep->res2 || ((ep->res2_cstride | ep->res2_coff) & 3) == 0) && !getenv("CLIMSR_NO_PT");
 }
 
-template <int NCOF, int NKC>
+// EP: 0 generic (runtime flags); 3 activation forward (bias + leaky relu / relu, bf16 out); 4 activation backward
+// (act' from the bf16 activation res1, no bias, bf16 out) -- srcnn.conv2's forward and data gradient.
+template <int NCOF, int NKC, int EP = 0>
 __global__ __launch_bounds__(256) void conv_pt_kernel(FwdArgs a, long npix) {
   __shared__ float tsm[NCOF == 4 ? 4 * 16 * 68 : 1];
   const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
@@ -2049,22 +2051,41 @@ __global__ __launch_bounds__(256) void conv_pt_kernel(FwdArgs a, long npix) {
 #pragma unroll
   for (int f = 0; f < NCOF; ++f)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) bb[f][i] = a.bias ? a.bias[f * 16 + g * 4 + i] : 0.f;
-  const bool f1 = (a.res_f32 & 1) != 0, f2 = ((a.res_f32 >> 1) & 1) != 0;
+    for (int i = 0; i < 4; ++i)
+      bb[f][i] = ((EP == 3 || (EP == 0 && a.bias)) && f * 16 + g * 4 + i < a.out_c) ? a.bias[f * 16 + g * 4 + i] : 0.f;
+  const bool f1 = EP != 0 ? false : (a.res_f32 & 1) != 0, f2 = EP != 0 ? false : ((a.res_f32 >> 1) & 1) != 0;
+  const bool has_bias = EP == 3 ? true : EP == 4 ? false : a.bias != nullptr;
+  const bool has1 = EP == 3 ? false : EP == 4 ? true : a.res1 != nullptr;
+  const bool has2 = EP != 0 ? false : a.res2 != nullptr;
+  const bool has_aux = EP != 0 ? false : a.aux != nullptr;
+  const int out_mode = EP != 0 ? 0 : a.out_mode;
   const long ngroups = (npix + 15) / 16;
   const long wave_id = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
-  for (long g0 = wave_id * PT_U; g0 < ngroups; g0 += nwaves * PT_U) {
-    bf16x8 bx[PT_U][NKC];
+  // input groups are loaded one iteration ahead with range-checked buffer loads (zeros past npix, no branch),
+  // so the next group's loads are in flight through this group's epilogue
+  const __amdgpu_buffer_rsrc_t xr = buf_rsrc(a.x, (uint32_t)(npix * a.in_cs * 2));
+  const __amdgpu_buffer_rsrc_t rr1 = opt_rsrc(has1 ? a.res1 : nullptr), rr2 = opt_rsrc(has2 ? a.res2 : nullptr);
+  bf16x8 bn[PT_U][NKC];
+  auto ldx = [&](long g0) {
 #pragma unroll
     for (int u = 0; u < PT_U; ++u) {
       const long p = (g0 + u) * 16 + col;
 #pragma unroll
       for (int k = 0; k < NKC; ++k) {
-        bx[u][k] = (bf16x8){};
-        if (p < npix) bx[u][k] = *(const bf16x8*)(a.x + p * a.in_cs + a.in_co + k * 32 + g * 8);
+        const uint4 v = buf_load16(xr, p < npix ? (uint32_t)((p * a.in_cs + a.in_co + k * 32 + g * 8) * 2) : BUF_OOB);
+        bn[u][k] = __builtin_bit_cast(bf16x8, v);
       }
     }
+  };
+  ldx(wave_id * PT_U);
+  for (long g0 = wave_id * PT_U; g0 < ngroups; g0 += nwaves * PT_U) {
+    bf16x8 bx[PT_U][NKC];
+#pragma unroll
+    for (int u = 0; u < PT_U; ++u)
+#pragma unroll
+      for (int k = 0; k < NKC; ++k) bx[u][k] = bn[u][k];
+    ldx(g0 + nwaves * PT_U);
 #pragma unroll
     for (int u = 0; u < PT_U; ++u) {
       const long p = (g0 + u) * 16 + col;
@@ -2092,21 +2113,34 @@ __global__ __launch_bounds__(256) void conv_pt_kernel(FwdArgs a, long npix) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) v[4 * j + i] = t4[i];
         }
-        if (pp < 16 && q < npix) {
+        const bool okq = pp < 16 && q < npix;
+        uint4 r1s[4], r2s[4];  // every residual load of this pixel before the first use (branch-free)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const long qq = okq ? q : 0;
+          const int co = okq ? c0 + 4 * j : 0;
+          if (EP == 0 || has1) {
+            if (f1) r1s[j] = buf_load16(rr1, (uint32_t)((qq * a.r1_cs + (okq ? a.r1_co : 0) + co) * 4));
+            else { const uint2 t2 = buf_load8(rr1, (uint32_t)((qq * a.r1_cs + (okq ? a.r1_co : 0) + co) * 2)); r1s[j] = make_uint4(t2.x, t2.y, 0, 0); }
+          } else r1s[j] = make_uint4(0, 0, 0, 0);
+          if (EP == 0 || has2) {
+            if (f2) r2s[j] = buf_load16(rr2, (uint32_t)((qq * a.r2_cs + (okq ? a.r2_co : 0) + co) * 4));
+            else { const uint2 t2 = buf_load8(rr2, (uint32_t)((qq * a.r2_cs + (okq ? a.r2_co : 0) + co) * 2)); r2s[j] = make_uint4(t2.x, t2.y, 0, 0); }
+          } else r2s[j] = make_uint4(0, 0, 0, 0);
+        }
+        if (okq) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int co = c0 + 4 * j;
-            const uint4 r1 = a.res1 ? load_res4(a.res1, f1, q * a.r1_cs + a.r1_co + co) : make_uint4(0, 0, 0, 0);
-            const uint4 r2 = a.res2 ? load_res4(a.res2, f2, q * a.r2_cs + a.r2_co + co) : make_uint4(0, 0, 0, 0);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-              const float bsv = a.bias ? a.bias[co + i] : 0.f;
-              v[4 * j + i] = ep_res(act_apply(v[4 * j + i] + bsv, a.act, a.slope), a.act, a.slope, a.res1 != nullptr,
-                                    res4_at(r1, f1, i), a.alpha1, a.beta1, a.res2 != nullptr, res4_at(r2, f2, i), a.alpha2, a.beta2);
+              const float bsv = has_bias ? a.bias[co + i] : 0.f;
+              v[4 * j + i] = ep_res(act_apply(v[4 * j + i] + bsv, a.act, a.slope), a.act, a.slope, has1, res4_at(r1s[j], f1, i),
+                                    a.alpha1, a.beta1, has2, res4_at(r2s[j], f2, i), a.alpha2, a.beta2);
             }
           }
           const long ob = q * a.out_cs + a.out_co + c0;
-          if (a.out_mode == 0) {
+          if (out_mode == 0) {
             uint4 w0, w1;
             w0.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
             w0.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
@@ -2122,12 +2156,12 @@ __global__ __launch_bounds__(256) void conv_pt_kernel(FwdArgs a, long npix) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-              if (a.out_mode == 2) o = *(const float4*)((const float*)a.y + ob + 4 * j);
+              if (out_mode == 2) o = *(const float4*)((const float*)a.y + ob + 4 * j);
               *(float4*)((float*)a.y + ob + 4 * j) =
                   make_float4(o.x + v[4 * j], o.y + v[4 * j + 1], o.z + v[4 * j + 2], o.w + v[4 * j + 3]);
             }
           }
-          if (a.aux) {
+          if (has_aux) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               uint2 pk;
@@ -2139,30 +2173,45 @@ __global__ __launch_bounds__(256) void conv_pt_kernel(FwdArgs a, long npix) {
         }
         continue;
       }
+      uint4 r1s[NCOF], r2s[NCOF];  // all residual loads of this pixel first (branch-free)
+#pragma unroll
+      for (int f = 0; f < NCOF; ++f) {
+        const int co = f * 16 + g * 4;
+        const bool okf = p < npix && co < a.out_c;
+        const long pp = okf ? p : 0;
+        const int cc = okf ? co : 0;
+        if (EP == 0 || has1) {
+          if (f1) r1s[f] = buf_load16(rr1, (uint32_t)((pp * a.r1_cs + (okf ? a.r1_co : 0) + cc) * 4));
+          else { const uint2 t2 = buf_load8(rr1, (uint32_t)((pp * a.r1_cs + (okf ? a.r1_co : 0) + cc) * 2)); r1s[f] = make_uint4(t2.x, t2.y, 0, 0); }
+        } else r1s[f] = make_uint4(0, 0, 0, 0);
+        if (EP == 0 || has2) {
+          if (f2) r2s[f] = buf_load16(rr2, (uint32_t)((pp * a.r2_cs + (okf ? a.r2_co : 0) + cc) * 4));
+          else { const uint2 t2 = buf_load8(rr2, (uint32_t)((pp * a.r2_cs + (okf ? a.r2_co : 0) + cc) * 2)); r2s[f] = make_uint4(t2.x, t2.y, 0, 0); }
+        } else r2s[f] = make_uint4(0, 0, 0, 0);
+      }
       if (p >= npix) continue;
 #pragma unroll
       for (int f = 0; f < NCOF; ++f) {
         const int co = f * 16 + g * 4;
         if (co >= a.out_c) continue;
-        const uint4 r1 = a.res1 ? load_res4(a.res1, f1, p * a.r1_cs + a.r1_co + co) : make_uint4(0, 0, 0, 0);
-        const uint4 r2 = a.res2 ? load_res4(a.res2, f2, p * a.r2_cs + a.r2_co + co) : make_uint4(0, 0, 0, 0);
+        const uint4 r1 = r1s[f], r2 = r2s[f];
         const long ob = p * a.out_cs + a.out_co + co;
         float v[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          v[i] = ep_res(act_apply(acc[f][i] + bb[f][i], a.act, a.slope), a.act, a.slope, a.res1 != nullptr, res4_at(r1, f1, i),
-                        a.alpha1, a.beta1, a.res2 != nullptr, res4_at(r2, f2, i), a.alpha2, a.beta2);
-        if (a.out_mode == 0) {
+          v[i] = ep_res(act_apply(acc[f][i] + bb[f][i], a.act, a.slope), a.act, a.slope, has1, res4_at(r1, f1, i), a.alpha1,
+                        a.beta1, has2, res4_at(r2, f2, i), a.alpha2, a.beta2);
+        if (out_mode == 0) {
           uint2 pk;
           pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
           pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
           *(uint2*)((uint16_t*)a.y + ob) = pk;
         } else {
           float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (a.out_mode == 2) o = *(const float4*)((const float*)a.y + ob);
+          if (out_mode == 2) o = *(const float4*)((const float*)a.y + ob);
           *(float4*)((float*)a.y + ob) = make_float4(o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]);
         }
-        if (a.aux) {
+        if (has_aux) {
           uint2 pk;
           pk.x = (uint32_t)f2bf(a.aux_scale * v[0]) | ((uint32_t)f2bf(a.aux_scale * v[1]) << 16);
           pk.y = (uint32_t)f2bf(a.aux_scale * v[2]) | ((uint32_t)f2bf(a.aux_scale * v[3]) << 16);
@@ -2175,15 +2224,21 @@ __global__ __launch_bounds__(256) void conv_pt_kernel(FwdArgs a, long npix) {
 
 template <int NCOF, int NKC>
 static int launch_pt(const FwdArgs& a, hipStream_t s) {
+  // epilogue specialisations: activation forward (3) / activation backward from a bf16 activation (4)
+  const bool plain = !a.res2 && !a.aux && a.out_mode == 0 && a.res_f32 == 0 && a.out_c == NCOF * 16;
+  const int ep = (plain && a.bias && !a.res1 && (a.act == 1 || a.act == 2)) ? 3
+                 : (plain && !a.bias && a.res1 && (a.act == 3 || a.act == 4)) ? 4 : 0;
   if (g_dry) {
-    snprintf(g_dry_name, sizeof(g_dry_name), "conv_pt_kernel<%d, %d>", NCOF, NKC);
+    snprintf(g_dry_name, sizeof(g_dry_name), "conv_pt_kernel<%d, %d, %d>", NCOF, NKC, ep);
     return CLIMSR_OK;
   }
   const long npix = (long)a.n * a.out_h * a.out_w;
   const long groups = (npix + 15) / 16;
   long blocks = (groups + 4 * PT_U - 1) / (4 * PT_U);
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL((conv_pt_kernel<NCOF, NKC>), dim3((unsigned)blocks), dim3(256), 0, s, a, npix);
+  if (ep == 3) hipLaunchKernelGGL((conv_pt_kernel<NCOF, NKC, 3>), dim3((unsigned)blocks), dim3(256), 0, s, a, npix);
+  else if (ep == 4) hipLaunchKernelGGL((conv_pt_kernel<NCOF, NKC, 4>), dim3((unsigned)blocks), dim3(256), 0, s, a, npix);
+  else hipLaunchKernelGGL((conv_pt_kernel<NCOF, NKC, 0>), dim3((unsigned)blocks), dim3(256), 0, s, a, npix);
   return check_launch("conv2d_fwd (pt)");
 }
 
