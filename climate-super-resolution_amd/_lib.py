@@ -96,6 +96,8 @@ SIGNATURES = {
     "climsr_rdb_chain_kp": (c_int, [c_int]),
     "climsr_conv2d_fwd": (c_int, [P(ConvDesc), c_void_p, c_void_p, c_void_p, P(Epilogue), c_void_p, c_void_p]),
     "climsr_conv2d_fwd_kernel": (ctypes.c_char_p, [P(ConvDesc), c_void_p, P(Epilogue)]),
+    "climsr_dgrad_single_output": (c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int,
+                                           c_float, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p]),
     "climsr_conv2d_wgrad": (c_int, [P(ConvDesc), c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "climsr_conv2d_wgrad_reduce": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                                            c_void_p]),

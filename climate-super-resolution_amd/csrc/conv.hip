@@ -2222,6 +2222,106 @@ __global__ __launch_bounds__(256) void conv_pt_kernel(FwdArgs a, long npix) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Data gradient of a conv with ONE output channel (conv_last 64->1 3x3, srcnn.conv3 32->1 5x5; esrgan.py:99,
+// srcnn.py:17): g[q][c] = act'(res1[q][c]) * sum_{ky,kx} W[0][c][ky][kx] * dz[q - (ky,kx) + pad].  A 1 -> C
+// stencil, not a GEMM (K = ks^2 taps of one channel): one 16x16-pixel tile per workgroup, the dz tile (+halo)
+// and the fp32 weights in LDS, each thread one pixel x 8 channels per step (16 B residual load, 16 B store).
+// Bound by HBM (the residual read and the output write).  The implicit-GEMM path padded K to 32 and ran the
+// epilogue of a 64-output MFMA tile per 2 input channels (conv_last dgrad 222 us, srcnn.conv3 dgrad 144 us).
+// ------------------------------------------------------------------------------------------
+constexpr int S1_T = 16;
+// LPP = C / 8 lanes share a pixel (8 channels each), so a wave's 16 B stores / residual loads cover whole
+// 128 B (C = 64) or 64 B (C = 32) pixel rows; weights in LDS as [tap][C] (two 16 B reads per tap).
+template <int KS, int LPP>
+__global__ __launch_bounds__(256) void dgrad_ci1_kernel(int n, int h, int w, int pad, const uint16_t* __restrict__ dz, int dz_cs,
+                                                        int dz_co, const float* __restrict__ wt, int act, float slope,
+                                                        const uint16_t* __restrict__ res1, int r1_cs, int r1_co, uint16_t* __restrict__ out,
+                                                        int out_cs, int out_co) {
+  constexpr int TP = S1_T + KS - 1, C = LPP * 8, PPS = 256 / LPP, NPASS = S1_T * S1_T / PPS;
+  __shared__ float dzt[TP * TP];
+  __shared__ __attribute__((aligned(16))) float wl[KS * KS * C];
+  const int tid = threadIdx.x, cg = tid % LPP, ps = tid / LPP;
+  const int tiles_x = (w + S1_T - 1) / S1_T, tiles_y = (h + S1_T - 1) / S1_T;
+  int b = blockIdx.x;
+  const int bx = b % tiles_x;
+  b /= tiles_x;
+  const int by = b % tiles_y, img = b / tiles_y;
+  const int x0 = bx * S1_T, y0 = by * S1_T;
+  // tile row r <-> dz row y0 - (KS - 1) + pad + r (same for columns)
+  const int ry0 = y0 - (KS - 1) + pad, rx0 = x0 - (KS - 1) + pad;
+  // every residual load of this thread first (they land while the tile is staged and the sums computed)
+  uint4 rv[NPASS];
+#pragma unroll
+  for (int k = 0; k < NPASS; ++k) {
+    const int pix = k * PPS + ps, qy = y0 + pix / S1_T, qx = x0 + pix % S1_T;
+    const bool ok = act && qy < h && qx < w;
+    rv[k] = ok ? *(const uint4*)(res1 + (((long)img * h + qy) * w + qx) * r1_cs + r1_co + cg * 8) : make_uint4(0, 0, 0, 0);
+  }
+  for (int i = tid; i < TP * TP; i += 256) {
+    const int r = i / TP, c = i - r * TP;
+    const int yy = ry0 + r, xx = rx0 + c;
+    dzt[i] = (yy >= 0 && yy < h && xx >= 0 && xx < w) ? bf2f(dz[(((long)img * h + yy) * w + xx) * dz_cs + dz_co]) : 0.f;
+  }
+  for (int i = tid; i < C * KS * KS; i += 256) {  // OIHW [c][tap] -> [tap][c]
+    const int c = i / (KS * KS), t = i - c * (KS * KS);
+    wl[t * C + c] = wt[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NPASS; ++k) {
+    const int pix = k * PPS + ps, ty = pix / S1_T, tx = pix % S1_T;
+    const int qy = y0 + ty, qx = x0 + tx;
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ky = 0; ky < KS; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < KS; ++kx) {  // out[q] += W[c][ky][kx] * dz[q - (ky, kx) + pad]
+        const float d = dzt[(ty + KS - 1 - ky) * TP + tx + KS - 1 - kx];
+        const float4 w0 = *(const float4*)(wl + (ky * KS + kx) * C + cg * 8), w1 = *(const float4*)(wl + (ky * KS + kx) * C + cg * 8 + 4);
+        v[0] += w0.x * d; v[1] += w0.y * d; v[2] += w0.z * d; v[3] += w0.w * d;
+        v[4] += w1.x * d; v[5] += w1.y * d; v[6] += w1.z * d; v[7] += w1.w * d;
+      }
+    if (qy >= h || qx >= w) continue;
+    if (act) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t wd = i < 2 ? rv[k].x : i < 4 ? rv[k].y : i < 6 ? rv[k].z : rv[k].w;
+        const float r = bf2f((uint16_t)((i & 1) ? (wd >> 16) : wd));
+        v[i] = r > 0.f ? v[i] : (act == 3 ? v[i] * slope : 0.f);
+      }
+    }
+    *(uint4*)(out + (((long)img * h + qy) * w + qx) * out_cs + out_co + cg * 8) = pack8_bf16(v, 1.f);
+  }
+}
+
+extern "C" int climsr_dgrad_single_output(int n, int h, int w, int ks, int pad, const uint16_t* dz, int dz_cstride, int dz_coff,
+                                          const float* weight, int c, int act, float slope, const uint16_t* res1, int res1_cstride,
+                                          int res1_coff, uint16_t* out, int out_cstride, int out_coff, void* stream) {
+  if (!dz || !weight || !out || n <= 0 || h <= 0 || w <= 0 || (ks != 3 && ks != 5) || pad != ks / 2 || c <= 0 || c > 64 || c % 8 ||
+      (out_cstride | out_coff) % 8 || (act != 0 && act != 3 && act != 4) || (act && (!res1 || (res1_cstride | res1_coff) % 8))) {
+    set_error("dgrad_single_output: unsupported arguments (ks %d pad %d c %d act %d)", ks, pad, c, act);
+    return CLIMSR_EINVAL;
+  }
+  const long tiles = (long)n * ((h + S1_T - 1) / S1_T) * ((w + S1_T - 1) / S1_T);
+  if (g_dry) {
+    snprintf(g_dry_name, sizeof(g_dry_name), "dgrad_ci1_kernel<%d>", ks);
+    return CLIMSR_OK;
+  }
+#define CLIMSR_CI1(KS_, LPP_)                                                                                              \
+  hipLaunchKernelGGL((dgrad_ci1_kernel<KS_, LPP_>), dim3((unsigned)tiles), dim3(256), 0, (hipStream_t)stream, n, h, w, pad, dz, \
+                     dz_cstride, dz_coff, weight, act, slope, res1, res1_cstride, res1_coff, out, out_cstride, out_coff)
+  switch (ks * 100 + c / 8) {
+    case 308: CLIMSR_CI1(3, 8); break;
+    case 304: CLIMSR_CI1(3, 4); break;
+    case 508: CLIMSR_CI1(5, 8); break;
+    case 504: CLIMSR_CI1(5, 4); break;
+    default: set_error("dgrad_single_output: no instance for ks %d, %d channels (32 or 64)", ks, c); return CLIMSR_EINVAL;
+  }
+#undef CLIMSR_CI1
+  return check_launch("dgrad_single_output");
+}
+
 template <int NCOF, int NKC>
 static int launch_pt(const FwdArgs& a, hipStream_t s) {
   // epilogue specialisations: activation forward (3) / activation backward from a bf16 activation (4)
@@ -2632,7 +2732,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs a) {
       }
     }
     __syncthreads();
-#pragma unroll
+#pragma unroll 2  // (a full unroll of the WS variant's 8 k-steps made hipcc copy the accumulators AGPR<->VGPR)
     for (int s = 0; s < (WS ? 8 : 2); ++s) {
       if (a.ablate & 2) break;
       const int kk = WS ? s : wave * 2 + s;  // k-step: output pixel rows 2kk, 2kk+1 of the tile

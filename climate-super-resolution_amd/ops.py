@@ -8,6 +8,7 @@ tensors (bf16 or fp32) addressed by (channel stride, channel offset).
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional
 
 import torch
@@ -28,6 +29,7 @@ def round_up(a: int, b: int) -> int:
 # PROFILER(kernel_name, algorithmic_flops, launch_fn, tag, algorithmic_bytes); must call launch_fn() exactly
 # once.  algorithmic_bytes = every operand read once and every result written once (no halo re-reads).
 PROFILER = None
+_NO_CI1 = os.environ.get("CLIMSR_NO_CI1") == "1"  # A/B switch: single-output dgrads through the implicit GEMM
 
 
 def wgrad_kernel_name(out_c: int, ks: int, ci4: bool = False, cin: int = 0, stride: int = 1, pad: int = 1, npx: int = 0) -> str:
@@ -163,6 +165,17 @@ class ConvPlan:
         result is summed over 2x2 pixel blocks (backward of the nearest x2 upsample feeding this conv).
         Stride-2 convs (pad 1, even input) run as a stride-1 conv over the zero-inserted dz."""
         ct = self.cout_t if cout_t is None else cout_t
+        if (self.cout == 1 and self.stride == 1 and self.ks in (3, 5) and self.pad == self.ks // 2 and g.dtype == torch.bfloat16
+                and not down2 and aux is None and act in (ACT_NONE, ACT_LRELU_BWD, ACT_RELU_BWD) and ct == self.cin_real
+                and ct in (32, 64) and not _NO_CI1):
+            # one output channel: its data gradient is a 1 -> C stencil (climsr_dgrad_single_output), not a GEMM
+            hw = n * out_h * out_w
+            nbytes = hw * 2 + hw * ct * 2 * (2 if res1 is not None else 1)
+            _run(f"dgrad_ci1_kernel<{self.ks}>", 2 * ct * self.ks * self.ks * hw, lambda: check(
+                _lib.load().climsr_dgrad_single_output(n, out_h, out_w, self.ks, self.pad, ptr(dz), dz_cs, 0, ptr(self.weight), ct, act,
+                                                       0.2, ptr(res1), res1_cs, res1_co, ptr(g), g_cs, g_co, _lib.stream_ptr()),
+                f"conv dgrad {self.name}"), "dgrad " + self.name, nbytes)
+            return
         pad_t = self.ks - 1 - self.pad
         if self.stride == 1:  # input size = out + ks - 1 - 2 pad (== out for 'same' convs)
             ih, iw = out_h + 2 * pad_t - self.ks + 1, out_w + 2 * pad_t - self.ks + 1

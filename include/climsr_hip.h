@@ -154,6 +154,14 @@ const char* climsr_conv2d_fwd_kernel(const ClimsrConvDesc* d, const float* bias,
 /* Weight (+ bias) gradient partials (d->in_c may be 4 = "at most 4 real input channels", which packs
  * 4 taps x 4 channels per MFMA fragment; the input buffer still has a multiple-of-8 channel stride): partial[split][out_c_pad16][in_c*ks*ks] (OIHW order) and
  * bias_partial[split][out_c_pad16].  dz: bf16 NHWC [n][out_h][out_w][dz_cstride]. */
+/* Data gradient of a stride-1 'same' conv with ONE output channel (conv_last esrgan.py:99, srcnn.conv3
+ * srcnn.py:17), replacing their nn.Conv2d backward: out[q][c] = act'(res1[q][c]) * sum_{ky,kx} w[c][ky][kx] *
+ * dz[q - (ky, kx) + pad], bf16 NHWC in / out (channel stride / offset), fp32 OIHW weight [1][c][ks][ks],
+ * ks 3 or 5, c 32 or 64, act 0 (none), 3 (leaky-relu derivative, slope) or 4 (relu derivative)
+ * taken from the bf16 activation res1.  Async on `stream`. */
+int climsr_dgrad_single_output(int n, int h, int w, int ks, int pad, const uint16_t* dz, int dz_cstride, int dz_coff,
+                               const float* weight, int c, int act, float slope, const uint16_t* res1, int res1_cstride,
+                               int res1_coff, uint16_t* out, int out_cstride, int out_coff, void* stream);
 int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, const uint16_t* dz, int dz_cstride,
                         float* partial, float* bias_partial, int nsplit, void* stream);
 /* Sum the split partials into OIHW fp32 grads (accumulate=1: +=).  bias_grad may be NULL. */

@@ -116,6 +116,37 @@ def test_conv_fwd_epilogue_slices_and_residuals():
     check_close(from_nhwc(out, 64).cpu(), want, what="double residual")
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,ks,act,h,w", [(64, 3, 3, 20, 37), (32, 5, 4, 33, 18), (64, 3, 0, 16, 16)])
+def test_dgrad_single_output_stencil(cin, ks, act, h, w):
+    """climsr_dgrad_single_output (conv_last / srcnn.conv3 data gradients, esrgan.py:99, srcnn.py:17) vs autograd of
+    F.conv2d with the same fp32 weights, the activation derivative taken from a bf16 activation; bf16 output
+    (tolerance: bf16 rounding of the result, rel 1e-2)."""
+    from climsr_amd.ops import ACT_LRELU_BWD, ACT_NONE, ACT_RELU_BWD
+
+    n = 2
+    p, wt, _b = make_plan(cin, 1, ks)
+    g = torch.Generator().manual_seed(7)
+    dz = bf(torch.rand((n, 1, h, w), generator=g) * 2 - 1)
+    dz8 = to_nhwc(dz, cs=8)
+    a = bf(torch.rand((n, cin, h, w), generator=g) * 2 - 1)
+    ab = to_nhwc(a)
+    out = torch.zeros((n, h, w, cin), dtype=torch.bfloat16, device=DEV)
+    act_code = {0: ACT_NONE, 3: ACT_LRELU_BWD, 4: ACT_RELU_BWD}[act]
+    p.dgrad(dz8, 8, h, w, out, cin, 0, n, act=act_code, res1=ab if act else None, res1_cs=cin, res1_co=0)
+    torch.cuda.synchronize()
+    x = torch.zeros((n, cin, h, w), dtype=torch.float64, requires_grad=True)
+    y = F.conv2d(x, wt.double().cpu(), None, padding=ks // 2)
+    (gref,) = torch.autograd.grad(y, x, dz.double())
+    if act == 3:
+        gref = torch.where(a.double() > 0, gref, gref * 0.2)
+    elif act == 4:
+        gref = torch.where(a.double() > 0, gref, torch.zeros_like(gref))
+    got = from_nhwc(out, cin).cpu().double()
+    err = (got - gref).abs().max().item()
+    assert err <= 1e-2 * gref.abs().max().item() + 1e-6, f"single-output dgrad max err {err}"
+
+
 @pytest.mark.parametrize("cin,cout,ks,up,down,h,w", [(64, 16, 3, 1, False, 16, 16), (128, 64, 3, 1, False, 16, 16),
                                                      (80, 16, 3, 1, False, 16, 16), (64, 64, 3, 2, True, 16, 16),
                                                      (32, 1, 5, 1, False, 16, 16), (3, 64, 9, 1, False, 16, 16),
