@@ -441,15 +441,17 @@ __device__ __forceinline__ void store_tile_lds(const FwdArgs& a, const float* eb
                                                int co0) {
   constexpr int NG = NCH / 8, NIT = NPX * NG;
   // EP 3 = activation forward (bias + leaky relu / relu, bf16 out); 4 = activation backward (act' read from
-  // the bf16 activation res1, no bias, bf16 out): the HR-resolution layers (conv_pw_kernel)
-  const bool f1 = (EP == 1 || EP >= 3) ? false : EP == 2 ? true : RF && (a.res_f32 & 1);
-  const bool f2 = (EP == 1 || EP >= 3) ? false : EP == 2 ? true : RF && ((a.res_f32 >> 1) & 1);
-  const bool has_bias = (EP == 1 || EP == 3) ? true : (EP == 2 || EP == 4) ? false : a.bias != nullptr;
-  const int act = (EP == 1 || EP == 2) ? 0 : a.act;
-  const bool has1 = (EP == 1 || EP == 2 || EP == 4) ? true : EP == 3 ? false : a.res1 != nullptr;
-  const bool has2 = EP >= 3 ? false : a.res2 != nullptr;
-  const int out_mode = (EP == 1 || EP >= 3) ? 0 : EP == 2 ? 1 : a.out_mode;
-  const bool has_aux = (EP == 1 || EP >= 3) ? false : a.aux != nullptr;
+  // the bf16 activation res1, no bias, bf16 out): the HR-resolution layers (conv_pw_kernel); 6 = activation
+  // forward without bias (discriminator convs); 7 = plain fp32 '=' output (data gradients feeding a BN /
+  // activation backward); 8 = plain bf16 output (pre-BN discriminator convs).
+  const bool f1 = EP == 2 ? true : EP != 0 ? false : RF && (a.res_f32 & 1);
+  const bool f2 = EP == 2 ? true : EP != 0 ? false : RF && ((a.res_f32 >> 1) & 1);
+  const bool has_bias = (EP == 1 || EP == 3) ? true : EP != 0 ? false : a.bias != nullptr;
+  const int act = (EP == 1 || EP == 2 || EP == 7 || EP == 8) ? 0 : a.act;
+  const bool has1 = (EP == 1 || EP == 2 || EP == 4) ? true : EP != 0 ? false : a.res1 != nullptr;
+  const bool has2 = (EP == 0 || EP == 1 || EP == 2) ? a.res2 != nullptr : false;
+  const int out_mode = (EP == 2 || EP == 7) ? 1 : EP != 0 ? 0 : a.out_mode;
+  const bool has_aux = (EP == 0 || EP == 2) ? a.aux != nullptr : false;
   const bool vec = EP != 0 || ((a.out_c & 7) == 0 && ((a.out_cs | a.out_co) & 7) == 0 && (!a.res1 || ((a.r1_cs | a.r1_co) & 7) == 0) &&
                                (!a.res2 || ((a.r2_cs | a.r2_co) & 7) == 0) && (!a.aux || ((a.aux_cs | a.aux_co) & 7) == 0));
   constexpr int IB = RF ? 2 : 4;  // items per round: their global loads are in flight together
@@ -2366,6 +2368,7 @@ static int launch_fwd_ep(const FwdArgs& a, int ncob, size_t lds, hipStream_t s) 
   constexpr int MV = NT == 1 ? 6 : (NT == 2 ? 8 : 4);
   if (g_dry) {
     if (PFX) snprintf(g_dry_name, sizeof(g_dry_name), "conv_fwd_kernel<%d, %d, %s, %d, %d, %d, %d>", MW, NT, a.res_f32 ? "true" : "false", MV, PFX, PFW, EP);
+    else if (EP) snprintf(g_dry_name, sizeof(g_dry_name), "conv_fwd_kernel<%d, %d, %s, %d, 0, 0, %d>", MW, NT, a.res_f32 ? "true" : "false", MV, EP);
     else snprintf(g_dry_name, sizeof(g_dry_name), "conv_fwd_kernel<%d, %d, %s, %d>", MW, NT, a.res_f32 ? "true" : "false", MV);
     return CLIMSR_OK;
   }
@@ -2390,6 +2393,15 @@ static int launch_fwd(const FwdArgs& a, int ncob, size_t lds, hipStream_t s) {
 static bool fwd_pf_disabled() {
   static const bool v = getenv("CLIMSR_NO_FWD_PF") != nullptr;
   return v;
+}
+
+// Epilogue specialisations without residuals (store_tile_lds EP 3 / 6 / 7 / 8), or 0: activation forward with
+// (3) / without (6) bias, plain fp32 '=' output (7), plain bf16 output (8).  Needs 8-channel-aligned slices.
+static int plain_ep(const FwdArgs& a) {
+  if ((a.out_c & 7) || ((a.out_cs | a.out_co) & 7) || a.down2 || a.res1 || a.res2 || a.aux || a.res_f32) return 0;
+  if (a.out_mode == 0 && (a.act == 1 || a.act == 2)) return a.bias ? 3 : 6;
+  if (a.act == 0 && !a.bias) return a.out_mode == 1 ? 7 : a.out_mode == 0 ? 8 : 0;
+  return 0;
 }
 
 extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, const uint16_t* wpk, const float* bias,
@@ -2524,6 +2536,14 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
         const int epm = (v8 && a.bias && !a.res1 && (a.act == 1 || a.act == 2)) ? 3
                         : (v8 && !a.bias && a.res1 && ((a.r1_cs | a.r1_co) & 7) == 0 && (a.act == 3 || a.act == 4)) ? 4
                         : d2 ? 5 : 0;
+        if (nt == 4 && epm == 0) {
+          switch (plain_ep(a)) {
+            case 6: return launch_pw<8, 2, 4, 7, 6>(a, pg, s);
+            case 7: return launch_pw<8, 2, 4, 7, 7>(a, pg, s);
+            case 8: return launch_pw<8, 2, 4, 7, 8>(a, pg, s);
+            default: break;
+          }
+        }
         if (nt == 4) return epm == 3 ? launch_pw<8, 2, 4, 7, 3>(a, pg, s) : epm == 4 ? launch_pw<8, 2, 4, 7, 4>(a, pg, s)
                             : epm == 5 ? launch_pw<8, 2, 4, 7, 5>(a, pg, s) : launch_pw<8, 2, 4, 7>(a, pg, s);
         return epm == 3 ? launch_pw<8, 2, 2, 7, 3>(a, pg, s) : epm == 4 ? launch_pw<8, 2, 2, 7, 4>(a, pg, s)
@@ -2547,7 +2567,20 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
       if (v8 && a.bias && a.res_f32 == 0 && a.out_mode == 0 && !a.aux) return launch_fwd_ep<4, 4, 6, 9, 1>(a, ncob, g.lds_total, s);
       if (v8 && !a.bias && (a.res_f32 & 1) && (!a.res2 || (a.res_f32 & 2)) && a.out_mode == 1)
         return launch_fwd_ep<4, 4, 6, 9, 2>(a, ncob, g.lds_total, s);
-      return launch_fwd<4, 4, 6, 9>(a, ncob, g.lds_total, s);
+      switch (plain_ep(a)) {
+        case 3: return launch_fwd_ep<4, 4, 6, 9, 3>(a, ncob, g.lds_total, s);
+        case 6: return launch_fwd_ep<4, 4, 6, 9, 6>(a, ncob, g.lds_total, s);
+        case 7: return launch_fwd_ep<4, 4, 6, 9, 7>(a, ncob, g.lds_total, s);
+        case 8: return launch_fwd_ep<4, 4, 6, 9, 8>(a, ncob, g.lds_total, s);
+        default: return launch_fwd<4, 4, 6, 9>(a, ncob, g.lds_total, s);
+      }
+    }
+    switch (plain_ep(a)) {
+      case 3: return launch_fwd_ep<4, 4, 0, 0, 3>(a, ncob, g.lds_total, s);
+      case 6: return launch_fwd_ep<4, 4, 0, 0, 6>(a, ncob, g.lds_total, s);
+      case 7: return launch_fwd_ep<4, 4, 0, 0, 7>(a, ncob, g.lds_total, s);
+      case 8: return launch_fwd_ep<4, 4, 0, 0, 8>(a, ncob, g.lds_total, s);
+      default: break;
     }
     return launch_fwd<4, 4>(a, ncob, g.lds_total, s);
   }
