@@ -363,12 +363,38 @@ def main():
 
     loss_buf = torch.zeros(2, device=dev)
 
-    from climsr_amd.core.ddp import GradAllReducer, broadcast_module
+    from climsr_amd.core.ddp import GradAllReducer, OverlappedGradAllReducer, broadcast_module
 
     reducers = {}
+    # Overlapped DDP (default for N > 1; CLIMSR_DDP_OVERLAP=0 restores the all-reduce after the backward;
+    # CLIMSR_DDP_OVERLAP_TEST=1 runs the overlapped structure at N = 1 with no-op reductions, to check it):
+    # the backward reports finished gradient slices through the modules' grad-ready hooks, each slice is
+    # all-reduced asynchronously while the rest of the backward runs, and the hipGraph of a segment is split
+    # at those points so the replay can launch them in the same places.
+    overlap = (world > 1 and os.environ.get("CLIMSR_DDP_OVERLAP", "1") != "0") or os.environ.get("CLIMSR_DDP_OVERLAP_TEST") == "1"
+    ov = {}
+    if overlap:
+        for net in (g, d):
+            if net is not None:
+                ov[id(net)] = OverlappedGradAllReducer(net)
+    # backward calls per step that accumulate into a network's gradients: D gets two in loss_d (real and
+    # fake, pl_gan.py:51-61); G one (pass 0)
+    hook_calls = {id(d): 2} if d is not None else {}
+
+    def set_hook(net, fn):
+        if net is d:
+            net.set_grad_ready_hook(fn, calls_per_step=hook_calls[id(d)])
+        else:
+            net.set_grad_ready_hook(fn)
+
+    for net in (g, d):
+        if net is not None and overlap:
+            set_hook(net, ov[id(net)].ready)
 
     def allreduce(net):
-        if world > 1:  # DDP gradient average of the flat fp32 buffer over RCCL/xGMI, 256 MB buckets
+        if overlap:
+            ov[id(net)].finish()
+        elif world > 1:  # DDP gradient average of the flat fp32 buffer over RCCL/xGMI, 256 MB buckets
             if id(net) not in reducers:
                 reducers[id(net)] = GradAllReducer(net)
             reducers[id(net)]()
@@ -435,17 +461,39 @@ def main():
     torch.cuda.synchronize()
     if use_graph:
         graphs = []
-        pool = None
+        pool = torch.cuda.graph_pool_handle()
+        cap = torch.cuda.Stream()
         for fn, net in segments:
-            gr = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gr, pool=pool):
+            # one segment = one or more graphs: with the overlapped DDP the grad-ready hook (it runs on the
+            # autograd thread, on the capture stream) ends the current capture and begins the next one
+            # ("relaxed" capture: begin and end may be on different threads)
+            subs, los = [torch.cuda.CUDAGraph()], []
+
+            def split(lo, subs=subs, los=los):
+                subs[-1].capture_end()
+                los.append(lo)
+                subs.append(torch.cuda.CUDAGraph())
+                subs[-1].capture_begin(pool=pool, capture_error_mode="relaxed")
+
+            if net is not None and overlap:
+                set_hook(net, split)
+            torch.cuda.synchronize()
+            cap.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(cap):
+                subs[0].capture_begin(pool=pool, capture_error_mode="relaxed")
                 fn()
-            pool = gr.pool()
-            graphs.append((gr, net))
+                subs[-1].capture_end()
+            torch.cuda.current_stream().wait_stream(cap)
+            if net is not None and overlap:
+                set_hook(net, ov[id(net)].ready)
+            graphs.append((list(zip(subs, los + [None])), net))
 
         def run():
-            for gr, net in graphs:
-                gr.replay()
+            for subs, net in graphs:
+                for gr, lo in subs:
+                    gr.replay()
+                    if lo is not None:
+                        ov[id(net)].ready(lo)  # this slice's all-reduce overlaps the next graph
                 if net is not None:
                     allreduce(net)
     else:
@@ -518,6 +566,7 @@ def main():
                                     "config 3: full ESRGAN GAN step (2 G fwd, G bwd, 4 RFB-D calls, VGG19 perceptual, 2x AdamW)"),
                        "generator": f"ESRGAN nf64 nb{args.nb} gc16 x4", "global_batch": world * B, "per_gpu_batch": B,
                        "lr_tile": lr_size, "hr_tile": hr, "parallelism": f"dp{world}", "hip_graph": use_graph,
+                       "ddp_overlap": overlap, "graph_segments": [len(sg) for sg, _n in graphs] if use_graph else None,
                        "mode": args.mode},
             "roofline": roof,
             "step_mfma": {"algorithmic_tflop_per_step": round(flop_step / 1e12, 3), "achieved_tflops": round(step_tflops, 1),

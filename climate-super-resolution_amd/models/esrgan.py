@@ -331,6 +331,10 @@ class _Engine:
                 for k in range(1, 6):
                     off = (k - 1) * gc
                     self.plans[self.rdb_name(blk, r + 1, k)].wgrad(src, dc, 0, h, w, dz[..., off:], dc, n, ws, acc)
+            hook = self.gen._grad_ready_hook
+            if hook is not None and r == 0 and blk in self.gen._grad_ready_blocks:
+                # every gradient from RRDB_trunk.<blk> on (flat order: trunk blocks, tail convs) is final
+                hook(self.gen._block_flat_lo(blk))
         # ---- conv_first: grad wrt fea = trunk path + global skip
         axpby(npx_lr, nf, 1.0, g_fea2, nf, 0, 1.0, G[0], nf, 0)
         act_grad(npx_lr, nf, G[0], nf, 0, None, 0, 0, ACT_NONE, dz64, nf)
@@ -384,6 +388,24 @@ class ESRGANGenerator(FlatParamsMixin, nn.Module):
         self.srcnn = SRCNN(in_channels=3, out_channels=out_channels)
         self._flatten()
         object.__setattr__(self, "_engine", None)
+        object.__setattr__(self, "_grad_ready_hook", None)
+        object.__setattr__(self, "_grad_ready_blocks", ())
+
+    def set_grad_ready_hook(self, fn, blocks=None) -> None:
+        """Call ``fn(lo)`` during backward when every flat-gradient entry at offset >= lo is final: after the
+        RRDB blocks in ``blocks`` (default: about every quarter of the trunk).  Used by the overlapped DDP
+        all-reduce (core/ddp.OverlappedGradAllReducer); ``fn=None`` removes it."""
+        if blocks is None:
+            blocks = tuple(sorted({b for b in (3 * self.nb // 4, self.nb // 2, self.nb // 4) if 0 < b < self.nb}, reverse=True))
+        object.__setattr__(self, "_grad_ready_hook", fn)
+        object.__setattr__(self, "_grad_ready_blocks", tuple(blocks) if fn is not None else ())
+
+    def _block_flat_lo(self, blk: int) -> int:
+        p = self.RRDB_trunk[blk].RDB1.conv1.weight
+        for q, off, _n in self._flat_index:
+            if q is p:
+                return off
+        raise KeyError(f"RRDB_trunk.{blk} not in the flat parameter index")
 
     def _on_flat_moved(self):
         object.__setattr__(self, "_engine", None)

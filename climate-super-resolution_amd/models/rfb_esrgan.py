@@ -138,6 +138,13 @@ class _DEngine:
                        fc2.bias.grad if need_w else None, fc0.bias.grad if need_w else None, acc, du0, du0_t)
         if need_w:
             ops.linear_wgrad(du0_t, sv["p_t"], n_pad, feat, o, fc0.weight.grad, acc)
+            hook = d._grad_ready_hook
+            if hook is not None:  # fc.0 / fc.2 (the last flat entries, 103 M of 107 M parameters) are final once
+                # every backward of the step has accumulated into them (loss_d runs D twice, pl_gan.py:51-61)
+                object.__setattr__(d, "_ready_calls", d._ready_calls + 1)
+                if d._ready_calls >= d._ready_need:
+                    object.__setattr__(d, "_ready_calls", 0)
+                    hook(d._fc_flat_lo())
         dp = self._scr("dp", (n, feat), torch.float32, dev)
         ops.linear_dgrad(du0, self.fc0_bf16, n, feat, o, dp)
         hh, ww, c = sv["hh"], sv["ww"], sv["c"]
@@ -232,6 +239,25 @@ class RFBESRGANDiscriminator(FlatParamsMixin, nn.Module):
         )
         self._flatten()
         object.__setattr__(self, "_engine", None)
+        object.__setattr__(self, "_grad_ready_hook", None)
+        object.__setattr__(self, "_ready_calls", 0)
+        object.__setattr__(self, "_ready_need", 1)
+
+    def set_grad_ready_hook(self, fn, calls_per_step: int = 1) -> None:
+        """Call ``fn(lo)`` during backward once the fc gradients (flat offsets >= lo; 103 M of the 107 M
+        parameters, computed first) are final (core/ddp.OverlappedGradAllReducer): on the
+        ``calls_per_step``-th weight-gradient backward of the step (the D loss backpropagates through two D
+        calls, real and fake, pl_gan.py:51-61, so it passes 2).  ``fn=None`` removes it."""
+        object.__setattr__(self, "_grad_ready_hook", fn)
+        object.__setattr__(self, "_ready_calls", 0)
+        object.__setattr__(self, "_ready_need", max(1, int(calls_per_step)))
+
+    def _fc_flat_lo(self) -> int:
+        p = self.fc[0].weight
+        for q, off, _n in self._flat_index:
+            if q is p:
+                return off
+        raise KeyError("fc.0.weight not in the flat parameter index")
 
     def _on_flat_moved(self):
         object.__setattr__(self, "_engine", None)

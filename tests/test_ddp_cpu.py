@@ -80,3 +80,43 @@ def test_rank_seeds_differ():
     from climsr_amd.core.ddp import rank_seed
 
     assert [rank_seed(42, r) for r in range(4)] == [42, 43, 44, 45]
+
+
+def _ov_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from climsr_amd.core.ddp import OverlappedGradAllReducer
+
+        class M:  # the reducer only needs the flat gradient buffer
+            _flat_grad = torch.arange(20, dtype=torch.float32) * (rank + 1)
+
+        red = OverlappedGradAllReducer(M())
+        red.ready(14)   # [14, 20) final
+        red.ready(14)   # repeated report: no new bucket
+        red.ready(5)    # [5, 14)
+        red.finish()    # [0, 5)
+        buckets = list(red.launched)
+        ok = bool(torch.allclose(M._flat_grad, torch.arange(20, dtype=torch.float32) * 1.5))
+        red.finish()    # a step with no ready(): one whole-buffer bucket
+        q.put((rank, ok, buckets, list(red.launched)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_overlapped_reducer_gloo_world2():
+    """Backward-overlapped DDP buckets (core/ddp.OverlappedGradAllReducer): the slices reported ready are
+    reduced once each, in report order, and the step's result is the all-rank average."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ov_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok, buckets, second in res:
+        assert ok, f"rank {rank}: averaged gradient mismatch"
+        assert buckets == [(14, 20), (5, 14), (0, 5)], buckets
+        assert second == [(0, 20)], second
