@@ -894,7 +894,7 @@ __global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs
   constexpr int RG = 4 / NCB, MW = N16_TH / RG;  // row groups, output rows per wave
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
   const int cb = wave % NCB, rg = wave / NCB;
-  const int cvec = a.in_c / 8;
+  const int cvec = a.in_c / 8, cvec32 = (a.in_c + 31) / 32 * 4;  // real / 32-block-rounded 16 B channel groups
 
   float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
   const int co = g * 4;
@@ -960,7 +960,8 @@ __global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
         const int v = tid + 256 * i;
-        if (v < NPIX * CV) *(uint4*)(xs + (v / CV) * P + (v % CV) * 8) = pre[i];
+        // channel groups of fully padded 32-channel blocks are never read (their waves skip the MFMAs)
+        if (v < NPIX * CV && (v % CV) < cvec32) *(uint4*)(xs + (v / CV) * P + (v % CV) * 8) = pre[i];
       }
     }
     issue(tile + walk.step < walk.end ? tile + walk.step : -1);  // lands while this tile computes (unconditional:
@@ -969,7 +970,7 @@ __global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs
     f32x4 acc[MW];
 #pragma unroll
     for (int m = 0; m < MW; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    if (!(a.ablate & 2)) {
+    if (!(a.ablate & 2) && cb * 32 < a.in_c) {  // a wave whose 32-channel block is all padding adds zeros
       const uint16_t* xb = xs + ((rg * MW) * N16_TPW + col) * P + cb * 32 + g * 8;
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
@@ -2574,6 +2575,12 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
         case 8: return launch_fwd_ep<4, 4, 6, 9, 8>(a, ncob, g.lds_total, s);
         default: return launch_fwd<4, 4, 6, 9>(a, ncob, g.lds_total, s);
       }
+    }
+    // large input tiles (stride 2: 33x33 pixels per 16x16 outputs) with several chunks: the deeper-prefetch
+    // variant (one workgroup per CU already, so the 18 staging vectors per thread cost no occupancy)
+    if (g.nchunk > 1 && nrx <= 18 && nrw <= 9 && !fwd_pf_disabled()) {
+      if (plain_ep(a) == 8) return launch_fwd_ep<4, 4, 18, 9, 8>(a, ncob, g.lds_total, s);
+      return launch_fwd<4, 4, 18, 9>(a, ncob, g.lds_total, s);
     }
     switch (plain_ep(a)) {
       case 3: return launch_fwd_ep<4, 4, 0, 0, 3>(a, ncob, g.lds_total, s);
