@@ -1,18 +1,25 @@
 """Benchmark: HR MPix/s per training step of 4x ESRGAN SR on synthetic 64->256 tiles (BASELINE.json).
 
-Default workload = BASELINE config 2: RRDB generator (nf 64, nb 11, gc 16; conf/generator/esrgan.yaml)
-L1 pre-training step (pl_generator_pre_training.py:18-33: forward, L1Loss, backward, AdamW,
-OneCycleLR), per-GPU batch 32, bf16 MFMA compute, fp32 master weights / optimiser state.  The whole
-step (forward + loss + backward + AdamW + weight repack) is captured once in a hipGraph and replayed.
+Default workload = BASELINE config 3 (the metric's step, BASELINE.md §2 "both optimizer passes"): the full
+ESRGAN GAN training step of ``GANLightningModule.training_step`` (pl_gan.py:63-97) -- generator pass (G
+forward, RFB discriminator on hr and sr, VGG19 perceptual + relativistic adversarial + L1 losses, G backward,
+AdamW_G), then the discriminator pass (fresh G forward, D on hr and sr.detach(), D backward, AdamW_D) and both
+OneCycleLR steps -- with the RRDB generator (nf 64, nb 11, gc 16; conf/generator/esrgan.yaml), per-GPU batch
+32, bf16 MFMA compute, fp32 master weights / optimiser state.  Each step segment is captured once as a hipGraph
+and replayed.  The config-2 L1 pre-training step is measured in the same run and reported as ``config2``.
 
-Multi-GPU: one process per GPU (torchrun), per-rank seeded tiles (seed 42 + rank), the flat fp32
-gradient buffer is averaged with one RCCL all-reduce per step (DDP semantics), every rank steps its
-own replica.  Rank 0 prints ONE JSON line.
+Multi-GPU: ``--gpus N`` launches N ranks itself (one process per GPU, RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_ADDR=127.0.0.1 / MASTER_PORT in each child's environment; the launcher never touches the GPU) unless a
+launcher (torchrun) already set WORLD_SIZE.  Per-rank seeded tiles (seed 42 + rank); the flat fp32 gradient
+buffers are averaged over RCCL (DDP semantics, overlapped with the backward); every rank steps its own
+replica.  Rank 0 prints ONE JSON line.
 """
 import argparse
 import json
 import os
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
@@ -29,35 +36,111 @@ G_FWD_FLOP_PER_PX = 721_880  # 23,654,563,840 MAC per 64^2 sample 
 GAN_FLOP_PER_PX = 6_140_192  # (4 G + 9 D + 2 VGG) MAC * 2 / 65,536 at 256^2
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--median-steps", type=int, default=50,
+                    help="extra steps timed one by one (HIP events) after the timed loop: median per-step time")
     ap.add_argument("--batch", type=int, default=32, help="per-GPU batch")
     ap.add_argument("--lr-size", type=int, default=64)
     ap.add_argument("--nb", type=int, default=11)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--no-config2", action="store_true", help="gan mode: skip the config-2 (L1 pretrain) sub-record")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--mode", choices=["pretrain", "gan", "infer"], default="pretrain",
-                    help="pretrain = BASELINE config 2 (the metric's workload); gan = config 3 (G + RFB-D + VGG19 perceptual); "
-                         "infer = config 5 (whole-grid inference)")
+    ap.add_argument("--mode", choices=["pretrain", "gan", "infer"], default="gan",
+                    help="gan = BASELINE config 3 (the metric's step: G + RFB-D + VGG19 perceptual, both optimizer passes); "
+                         "pretrain = config 2 (L1 pre-training); infer = config 5 (whole-grid inference)")
     ap.add_argument("--model", choices=["rcan", "esrgan"], default="rcan",
                     help="infer mode: RCAN 10x20 (conf/inference.yaml's default) or the ESRGAN generator")
     ap.add_argument("--grid-h", type=int, default=360, help="infer mode: LR grid rows (CRU-TS 0.5 deg: 360)")
     ap.add_argument("--grid-w", type=int, default=720, help="infer mode: LR grid columns (720)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
-    (profiles/r*_pmc_traffic.json: separate FETCH_SIZE / WRITE_SIZE passes of this bench,
+# ------------------------------------------------------------------------------------------- launcher
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def child_envs(n: int, port: int, base=None):
+    """Environment of each of the n ranks (torchrun's variables; one node, rendezvous on 127.0.0.1)."""
+    base = dict(os.environ if base is None else base)
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver (RCCL)
+        envs.append(e)
+    return envs
+
+
+def launch(n: int, cmd, timeout=None) -> int:
+    """Start n child processes of ``cmd`` (one per GPU) and wait for all of them.  Rank 0's stdout is passed
+    through; every rank's stderr is inherited.  If a rank fails, the others are killed (by PID) and its exit
+    code is returned.  The launcher itself never initialises the GPU."""
+    port = free_port()
+    procs = []
+    for r, env in enumerate(child_envs(n, port)):
+        procs.append(subprocess.Popen(cmd, env=env, stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    t0 = time.time()
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
+                    q.kill()
+        if timeout is not None and time.time() - t0 > timeout:
+            for q in live:
+                q.kill()
+            return rc or 124
+        time.sleep(0.05)
+    return rc
+
+
+def cpu_info():
+    """Host CPU model, affinity cores and the cgroup CPU quota (the GPU box shows the whole machine's CPUs but
+    grants one GPU a share of them)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return {"cpu_model": model, "affinity_cores": aff, "cgroup_quota_cores": quota,
+            "threads": min(aff, quota) if quota else aff}
+
+
+def pmc_traffic(kernel, mode):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of this workload
+    (profiles/r*_<mode>_pmc_traffic.json: separate FETCH_SIZE / WRITE_SIZE passes of this bench,
     FETCH_SIZE x2 gfx950 correction, MI355X_MICROARCH.md).  None if no summary covers it."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{mode}_pmc_traffic.json")))
     if not files:
         return None, None
     f = files[-1]  # only the newest build's counters: an older build's bytes would describe other code
@@ -151,29 +234,42 @@ def roofline_entry(name, cnt, tot_ms, flops, nbytes, graph_us=None):
     return out
 
 
-def cpu_baseline(args, hr):
-    """Oracle (PyTorch-CPU fp32 eager) L1-pretrain step on the host cores, bounded sample."""
+def cpu_baseline(args, hr, mode):
+    """Oracle (PyTorch-CPU fp32 eager restatement of the same step, oracle/climsr_ref.py) on the host cores,
+    bounded sample: batch 2 at the benchmark's tile size, ~args.cpu_seconds of steps after one warm-up step."""
     from oracle import climsr_ref as ref
-    from tests.helpers import gen_params
+    from tests.helpers import gen_params, rfb_d_params, vgg_params
 
-    threads = min(16, len(os.sched_getaffinity(0)))
+    info = cpu_info()
+    threads = info["threads"]
     torch.set_num_threads(threads)
     b = 2
     p = {k: v.float() for k, v in gen_params(args.nb, torch.float32).items()}
     opt = ref.AdamWState(p, list(p.keys()), lr=1e-4, total_steps=1000)
     bt = ref.synthetic_batch(b, hr)
-    ref.pretrain_step(p, opt, bt, args.nb)  # warm-up
+    if mode == "pretrain":
+        fn = lambda: ref.pretrain_step(p, opt, bt, args.nb)  # noqa: E731
+        what = "L1-pretrain step (config 2)"
+    else:
+        dp = {k: (v.float() if v.is_floating_point() else v) for k, v in rfb_d_params().items()}
+        vp = {k: v.float() for k, v in vgg_params().items()}
+        opt_d = ref.AdamWState(dp, ref.trainable_keys(dp), lr=1e-4, total_steps=1000)
+        fn = lambda: ref.gan_step(p, dp, vp, opt, opt_d, bt, args.nb)  # noqa: E731
+        what = "full GAN step (config 3: G + RFB-D + VGG19 perceptual, both optimizer passes)"
+    fn()  # warm-up
     t0 = time.perf_counter()
     n = 0
     while True:
-        ref.pretrain_step(p, opt, bt, args.nb)
+        fn()
         n += 1
         if time.perf_counter() - t0 >= args.cpu_seconds or n >= 50:
             break
     dt = (time.perf_counter() - t0) / n
     return {"value": round(b * hr * hr / 1e6 / dt, 5), "unit": "HR MPix/s", "cores": threads, "kind": "port",
-            "sample": f"oracle L1-pretrain step (fp32 PyTorch-CPU eager), batch {b}, {hr // 4}->{hr}, nb={args.nb}, "
-                      f"{n} steps ({dt * 1e3:.0f} ms/step)"}
+            "sample": f"oracle {what}, fp32 PyTorch-CPU eager, batch {b}, {hr // 4}->{hr}, nb={args.nb}, "
+                      f"{n} steps ({dt * 1e3:.0f} ms/step)",
+            "cpu_model": info["cpu_model"], "affinity_cores": info["affinity_cores"],
+            "cgroup_quota_cores": info["cgroup_quota_cores"]}
 
 
 def run_infer(args, world, rank, dev):
@@ -285,7 +381,7 @@ def cpu_baseline_infer(args, state):
     """Oracle fp32 PyTorch-CPU forward of the same network on a bounded crop of the grid (LR 45x90)."""
     from oracle import climsr_ref as ref
 
-    threads = min(16, len(os.sched_getaffinity(0)))
+    threads = cpu_info()["threads"]
     torch.set_num_threads(threads)
     h, w = 45, 90
     g = torch.Generator().manual_seed(7)
@@ -310,37 +406,23 @@ def cpu_baseline_infer(args, state):
             "sample": f"oracle {args.model} forward (fp32 PyTorch-CPU), LR {w}x{h} crop of the grid, {n} runs ({dt * 1e3:.0f} ms each)"}
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-
-    import climsr_amd  # noqa: F401
-
-    if args.mode == "infer":
-        return run_infer(args, world, rank, dev)
-    from climsr_amd import ops
+def build_train(args, mode, world, dev):
+    """Models, optimisers, synthetic batch and the step segments of one training workload."""
     from climsr_amd.core.init import init_state, spec_from_shapes
     from climsr_amd.core.optim import GraphedAdamW
     from climsr_amd.losses.l1 import l1_loss
     from climsr_amd.models.esrgan import ESRGANGenerator
 
+    rank = int(os.environ.get("RANK", "0"))
     B, lr_size = args.batch, args.lr_size
     hr = 4 * lr_size
-    total_steps = max(1000, args.warmup + args.steps + 10)
+    total_steps = max(1000, 2 * (args.warmup + args.steps + args.median_steps) + 10)
     g = ESRGANGenerator(in_channels=3, out_channels=1, nf=64, nb=args.nb, gc=16, scale_factor=4)
     st = init_state(spec_from_shapes({k: tuple(v.shape) for k, v in g.state_dict().items()}))
     g.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in st.items()})
     g = g.to(dev)
-    opt_g = GraphedAdamW(g, lr=1e-4, total_steps=total_steps, weight_decay=1e-4)
     task = d = opt_d = None
-    if args.mode == "gan":
+    if mode == "gan":
         from climsr_amd.task.pl_gan import GANLightningModule
 
         task = GANLightningModule(generator=g, discriminator={"_target_": "climsr_amd.models.rfb_esrgan.RFBESRGANDiscriminator",
@@ -351,8 +433,8 @@ def main():
         d.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in dst.items()})
         task = task.to(dev)
         g, d = task.generator, task.discriminator
-        opt_g = GraphedAdamW(g, lr=1e-4, total_steps=total_steps, weight_decay=1e-4)
         opt_d = GraphedAdamW(d, lr=1e-4, total_steps=total_steps, weight_decay=1e-4)
+    opt_g = GraphedAdamW(g, lr=1e-4, total_steps=total_steps, weight_decay=1e-4)
 
     gen = torch.Generator(device="cpu").manual_seed(42 + rank)
     t = torch.rand((B, 1, hr, hr), generator=gen) * 2 - 1
@@ -360,60 +442,14 @@ def main():
     m = (torch.rand((B, 1, hr, hr), generator=gen) < 0.7).float()
     lr = torch.cat([t, e, m], 1)[:, :, ::4, ::4].contiguous()
     batch = {k: v.to(dev) for k, v in {"lr": lr, "hr": t, "elevation": e, "mask": m}.items()}
-
     loss_buf = torch.zeros(2, device=dev)
 
-    from climsr_amd.core.ddp import GradAllReducer, OverlappedGradAllReducer, broadcast_module
-
-    reducers = {}
-    # Overlapped DDP (default for N > 1; CLIMSR_DDP_OVERLAP=0 restores the all-reduce after the backward;
-    # CLIMSR_DDP_OVERLAP_TEST=1 runs the overlapped structure at N = 1 with no-op reductions, to check it):
-    # the backward reports finished gradient slices through the modules' grad-ready hooks, each slice is
-    # all-reduced asynchronously while the rest of the backward runs, and the hipGraph of a segment is split
-    # at those points so the replay can launch them in the same places.
-    overlap = (world > 1 and os.environ.get("CLIMSR_DDP_OVERLAP", "1") != "0") or os.environ.get("CLIMSR_DDP_OVERLAP_TEST") == "1"
-    ov = {}
-    if overlap:
-        for net in (g, d):
-            if net is not None:
-                ov[id(net)] = OverlappedGradAllReducer(net)
-    # backward calls per step that accumulate into a network's gradients: D gets two in loss_d (real and
-    # fake, pl_gan.py:51-61); G one (pass 0)
-    hook_calls = {id(d): 2} if d is not None else {}
-
-    def set_hook(net, fn):
-        if net is d:
-            net.set_grad_ready_hook(fn, calls_per_step=hook_calls[id(d)])
-        else:
-            net.set_grad_ready_hook(fn)
-
-    for net in (g, d):
-        if net is not None and overlap:
-            set_hook(net, ov[id(net)].ready)
-
-    def allreduce(net):
-        if overlap:
-            ov[id(net)].finish()
-        elif world > 1:  # DDP gradient average of the flat fp32 buffer over RCCL/xGMI, 256 MB buckets
-            if id(net) not in reducers:
-                reducers[id(net)] = GradAllReducer(net)
-            reducers[id(net)]()
-
-    if world > 1:
-        for net in (g, d):
-            if net is not None:
-                broadcast_module(net)
-
     def toggle(net_on):
-        if d is None:
-            return
         for net in (g, d):
             for p in net.parameters():
                 p.requires_grad_(net is net_on)
 
-    # The step as segments; the RCCL all-reduce runs between captured segments (eagerly) so that
-    # multi-GPU runs keep one hipGraph per segment.
-    if args.mode == "pretrain":
+    if mode == "pretrain":
         def seg_g():
             for p in g.parameters():
                 p.grad = None  # zero_grad(set_to_none=True): backward overwrites the flat grad buffer
@@ -444,6 +480,52 @@ def main():
             loss_buf[1].copy_(ld.detach())
 
         segments = [(seg_g, g), (seg_d, d), (opt_d.step, None)]
+    return dict(g=g, d=d, segments=segments, loss_buf=loss_buf, B=B, hr=hr, lr_size=lr_size)
+
+
+def measure_train(args, mode, world, rank, dev, kernel_timing=True):
+    """Capture the step of ``mode`` (hipGraph segments), run W warm-up steps, time exactly K steps between a barrier +
+    synchronize on both sides (max over ranks), then ``median_steps`` more steps one HIP-event pair each."""
+    from climsr_amd import ops
+    from climsr_amd.core.ddp import GradAllReducer, OverlappedGradAllReducer, broadcast_module
+
+    w = build_train(args, mode, world, dev)
+    g, d, segments, loss_buf, B, hr = w["g"], w["d"], w["segments"], w["loss_buf"], w["B"], w["hr"]
+    nets = [n_ for n_ in (g, d) if n_ is not None]
+
+    reducers = {}
+    # Overlapped DDP (default for N > 1; CLIMSR_DDP_OVERLAP=0 restores the all-reduce after the backward;
+    # CLIMSR_DDP_OVERLAP_TEST=1 runs the overlapped structure at N = 1 with no-op reductions, to check it):
+    # the backward reports finished gradient slices through the modules' grad-ready hooks, each slice is
+    # all-reduced asynchronously while the rest of the backward runs, and the hipGraph of a segment is split
+    # at those points so the replay can launch them in the same places.
+    overlap = (world > 1 and os.environ.get("CLIMSR_DDP_OVERLAP", "1") != "0") or os.environ.get("CLIMSR_DDP_OVERLAP_TEST") == "1"
+    ov = {id(n_): OverlappedGradAllReducer(n_) for n_ in nets} if overlap else {}
+    # backward calls per step that accumulate into a network's gradients: D gets two in loss_d (real and
+    # fake, pl_gan.py:51-61); G one (pass 0)
+    hook_calls = {id(d): 2} if d is not None else {}
+
+    def set_hook(net, fn):
+        if net is d:
+            net.set_grad_ready_hook(fn, calls_per_step=hook_calls[id(d)])
+        else:
+            net.set_grad_ready_hook(fn)
+
+    for net in nets:
+        if overlap:
+            set_hook(net, ov[id(net)].ready)
+
+    def allreduce(net):
+        if overlap:
+            ov[id(net)].finish()
+        elif world > 1:  # DDP gradient average of the flat fp32 buffer over RCCL/xGMI, 256 MB buckets
+            if id(net) not in reducers:
+                reducers[id(net)] = GradAllReducer(net)
+            reducers[id(net)]()
+
+    if world > 1:
+        for net in nets:
+            broadcast_module(net)
 
     def step_eager():
         for fn, net in segments:
@@ -459,8 +541,8 @@ def main():
             step_eager()
     torch.cuda.current_stream().wait_stream(side)
     torch.cuda.synchronize()
+    graphs = []
     if use_graph:
-        graphs = []
         pool = torch.cuda.graph_pool_handle()
         cap = torch.cuda.Stream()
         for fn, net in segments:
@@ -498,87 +580,161 @@ def main():
                     allreduce(net)
     else:
         run = step_eager
+
+    def barrier_sync():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def max_over_ranks(v):
+        if world == 1:
+            return v
+        tt = torch.tensor([v], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return float(tt.item())
+
     for _ in range(args.warmup):
         run()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    barrier_sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
         run()
         if rank == 0 and args.steps >= 20 and (i + 1) % max(1, args.steps // 4) == 0:
-            print(f"[bench] step {i + 1}/{args.steps}", file=sys.stderr, flush=True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+            print(f"[bench] {mode} step {i + 1}/{args.steps}", file=sys.stderr, flush=True)
+    barrier_sync()
+    elapsed = max_over_ranks(time.perf_counter() - t0)
     ms = elapsed / args.steps * 1e3
-    loss_val = [float(v) for v in loss_buf.cpu()]
     mpix = world * B * hr * hr / 1e6 / (elapsed / args.steps)
-    step = step_eager
 
-    roof = None
-    step_frac = None
-    flop_px = 3 * G_FWD_FLOP_PER_PX if args.mode == "pretrain" else GAN_FLOP_PER_PX
+    med = None
+    if args.median_steps > 0:  # per-step HIP events on the replay stream, back to back
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.median_steps + 1)]
+        evs[0].record()
+        for i in range(args.median_steps):
+            run()
+            evs[i + 1].record()
+        torch.cuda.synchronize()
+        per = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.median_steps)]
+        med_ms = max_over_ranks(statistics.median(per))
+        med = {"steps": args.median_steps, "after_warmup_steps": args.warmup + args.steps, "ms_per_step": round(med_ms, 3),
+               "value": round(world * B * hr * hr / 1e6 / (med_ms / 1e3), 3), "min_ms": round(min(per), 3),
+               "max_ms": round(max(per), 3), "source": "per-step HIP events (median over steps, max over ranks)"}
+    loss_val = [float(v) for v in loss_buf.cpu()]
+
+    flop_px = 3 * G_FWD_FLOP_PER_PX if mode == "pretrain" else GAN_FLOP_PER_PX
     flop_step = flop_px * B * hr * hr  # SURVEY §8d algorithmic FLOPs per HR pixel
     step_tflops = flop_step / (ms / 1e3) / 1e12
-    step_frac = step_tflops / PEAK_BF16_TFLOPS
-    kern = {}
-    if not args.no_kernel_timing:
-        timer = KernelTimer()
-        ops.PROFILER = timer
-        step()
-        ops.PROFILER = None
-        agg = timer.summary()
-        name, (cnt, tot_ms, flops, nbytes) = max(agg.items(), key=lambda kv: kv[1][1])
-        avg_ms = tot_ms / cnt
-        r = roofline_entry(name, cnt, tot_ms, flops, nbytes, timer.graph_us(name))
-        roof = {"bound": r["bound"], "achieved": r["achieved"], "peak": r["peak"], "unit": r["unit"], "frac": r["frac"],
-                "traffic": None}
-        roof.update({k: v for k, v in r.items() if k not in roof})
-        tb, src = pmc_traffic(name) if args.mode == "pretrain" else (None, None)  # the PMC summaries are of config 2
-        if tb is not None:  # HBM bytes per launch (PMC) and the bandwidth they imply at the measured launch time
-            roof.update(traffic=round(tb / 1e6, 2), traffic_unit="MB/launch", traffic_source=src,
-                        traffic_gbs=round(tb / (r["avg_launch_us"] / 1e6) / 1e9, 1))
-        kern = {k: {"launches": v[0], "ms_total": round(v[1], 3), "tflops": round(v[2] / (v[1] / 1e3) / 1e12, 1),
-                    "gbs": round(v[3] / (v[1] / 1e3) / 1e9, 1) if v[3] else None}
-                for k, v in sorted(agg.items(), key=lambda kv: -kv[1][1])}
-        if os.environ.get("CLIMSR_BENCH_DETAIL"):
-            print(json.dumps(timer.by_tag(), indent=0), file=sys.stderr)
+    rec = {"mode": mode, "ms": ms, "mpix": mpix, "median": med, "loss_last": [round(v, 6) for v in loss_val],
+           "use_graph": use_graph, "overlap": overlap, "graph_segments": [len(sg) for sg, _n in graphs] if use_graph else None,
+           "B": B, "hr": hr, "lr_size": w["lr_size"],
+           "step_mfma": {"algorithmic_tflop_per_step": round(flop_step / 1e12, 3), "achieved_tflops": round(step_tflops, 1),
+                         "frac": round(step_tflops / PEAK_BF16_TFLOPS, 4)}}
+    if kernel_timing:
+        rec.update(kernel_profile(step_eager, mode, ops))
+    return rec
 
+
+def kernel_profile(step, mode, ops):
+    """Every native launch of one eager step timed with HIP events on its stream (ops.PROFILER sees each C-ABI
+    call: convs, BN, linear, pooling, losses, AdamW, weight packing); the launch with the largest total time
+    names the roofline kernel, whose average launch time is re-measured from a hipGraph replay of its launches.
+    ``unattributed_ms`` = eager step time - sum of the timed launches (torch fills / copies, launch gaps)."""
+    timer = KernelTimer()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ops.PROFILER = timer
+    try:
+        s.record()
+        step()
+        e.record()
+    finally:
+        ops.PROFILER = None
+    torch.cuda.synchronize()
+    eager_ms = s.elapsed_time(e)
+    agg = timer.summary()
+    name, (cnt, tot_ms, flops, nbytes) = max(agg.items(), key=lambda kv: kv[1][1])
+    r = roofline_entry(name, cnt, tot_ms, flops, nbytes, timer.graph_us(name))
+    roof = {"bound": r["bound"], "achieved": r["achieved"], "peak": r["peak"], "unit": r["unit"], "frac": r["frac"], "traffic": None}
+    roof.update({k: v for k, v in r.items() if k not in roof})
+    tb, src = pmc_traffic(name, mode)
+    if tb is not None:  # HBM bytes per launch (PMC) and the bandwidth they imply at the measured launch time
+        roof.update(traffic=round(tb / 1e6, 2), traffic_unit="MB/launch", traffic_source=src,
+                    traffic_gbs=round(tb / (r["avg_launch_us"] / 1e6) / 1e9, 1),
+                    traffic_over_algorithmic=round(tb / max(1, r["bytes_per_launch"]), 2))
+    timed = sum(v[1] for v in agg.values())
+    kern = {k: {"launches": v[0], "ms_total": round(v[1], 3),
+                "tflops": round(v[2] / (v[1] / 1e3) / 1e12, 1) if v[2] else None,
+                "gbs": round(v[3] / (v[1] / 1e3) / 1e9, 1) if v[3] else None}
+            for k, v in sorted(agg.items(), key=lambda kv: -kv[1][1])}
+    if os.environ.get("CLIMSR_BENCH_DETAIL"):
+        print(json.dumps(timer.by_tag(top=60), indent=0), file=sys.stderr)
+    return {"roofline": roof, "kernels": kern,
+            "profile": {"eager_step_ms": round(eager_ms, 3), "timed_launch_ms": round(timed, 3),
+                        "unattributed_ms": round(eager_ms - timed, 3), "native_launches": sum(v[0] for v in agg.values())}}
+
+
+WORKLOAD = {"pretrain": "config 2: RRDB generator L1 pre-training step (fwd+L1+bwd+AdamW+OneCycleLR)",
+            "gan": "config 3: full ESRGAN GAN step (pl_gan.py:63-97: G pass = G fwd + D(hr), D(sr) + VGG19 perceptual + "
+                   "L1 + G bwd + AdamW_G; D pass = G fwd + D(hr), D(sr) + D bwd + AdamW_D; OneCycleLR x2)"}
+
+
+def main(argv=None):
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # the driver's `bench.py --gpus N` without a launcher: fan out N ranks ourselves (no GPU touched here)
+        return launch(args.gpus, [sys.executable, "-u", os.path.abspath(__file__)] + (sys.argv[1:] if argv is None else argv))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    rccl_world = dist.get_world_size() if dist.is_initialized() else 1
+
+    import climsr_amd  # noqa: F401
+
+    if args.mode == "infer":
+        return run_infer(args, world, rank, dev)
+    rec = measure_train(args, args.mode, world, rank, dev, kernel_timing=not args.no_kernel_timing)
+    sub = None
+    if args.mode == "gan" and not args.no_config2:
+        r2 = measure_train(args, "pretrain", world, rank, dev, kernel_timing=not args.no_kernel_timing)
+        sub = {"metric": "HR MPix/s per training step (4x SR, 64->256 tiles)", "workload": WORKLOAD["pretrain"],
+               "value": round(r2["mpix"], 3), "ms_per_step": round(r2["ms"], 3), "median": r2["median"],
+               "step_mfma": r2["step_mfma"], "roofline": r2.get("roofline"), "loss_last": r2["loss_last"]}
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.mode == "pretrain":
-        cpu = cpu_baseline(args, hr)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, rec["hr"], args.mode)
 
     if rank == 0:
         out = {
             "metric": "HR MPix/s per training step (4x SR, 64->256 tiles)",
-            "value": round(mpix, 3), "unit": "HR MPix/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "value": round(rec["mpix"], 3), "unit": "HR MPix/s", "n_gpus": world, "rccl_world": rccl_world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(rec["ms"], 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (seed 42+rank: U(-1,1) temp/elev, Bernoulli(0.7) mask, LR = HR[::4,::4]); deterministic init",
-            "config": {"workload": ("config 2: RRDB generator L1 pre-training step (fwd+L1+bwd+AdamW+OneCycleLR)"
-                                    if args.mode == "pretrain" else
-                                    "config 3: full ESRGAN GAN step (2 G fwd, G bwd, 4 RFB-D calls, VGG19 perceptual, 2x AdamW)"),
-                       "generator": f"ESRGAN nf64 nb{args.nb} gc16 x4", "global_batch": world * B, "per_gpu_batch": B,
-                       "lr_tile": lr_size, "hr_tile": hr, "parallelism": f"dp{world}", "hip_graph": use_graph,
-                       "ddp_overlap": overlap, "graph_segments": [len(sg) for sg, _n in graphs] if use_graph else None,
-                       "mode": args.mode},
-            "roofline": roof,
-            "step_mfma": {"algorithmic_tflop_per_step": round(flop_step / 1e12, 3), "achieved_tflops": round(step_tflops, 1),
-                          "frac": round(step_frac, 4)},
+            "config": {"workload": WORKLOAD[args.mode], "generator": f"ESRGAN nf64 nb{args.nb} gc16 x4",
+                       "discriminator": "RFBESRGANDiscriminator" if args.mode == "gan" else None,
+                       "global_batch": world * rec["B"], "per_gpu_batch": rec["B"], "lr_tile": rec["lr_size"], "hr_tile": rec["hr"],
+                       "parallelism": f"dp{world}", "hip_graph": rec["use_graph"], "ddp_overlap": rec["overlap"],
+                       "graph_segments": rec["graph_segments"], "mode": args.mode},
+            "median": rec["median"],
+            "roofline": rec.get("roofline"),
+            "step_mfma": rec["step_mfma"],
             "cpu_baseline": cpu,
-            "loss_last": [round(v, 6) for v in loss_val],
-            "kernels": kern,
+            "loss_last": rec["loss_last"],
+            "config2": sub,
+            "profile": rec.get("profile"),
+            "kernels": rec.get("kernels", {}),
         }
-        print(json.dumps(out))
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -43,15 +43,42 @@ class HydraInstantiator:
         return self.instantiate(cfg, instantiator=self, **(model_data_kwargs or {}))
 
     def optimizer(self, model: torch.nn.Module, cfg):
-        return self.instantiate(cfg, model.parameters())
+        """instantiator.py:48-49.  For a native (flat-parameter) network ``torch.optim.AdamW`` resolves to the fused
+        ``climsr_amd.core.optim.AdamW`` (same hyper-parameters and param_groups, so OneCycleLR drives it unchanged);
+        any other optimizer is instantiated as configured and re-packs the network's bf16 MFMA weights after each
+        step (the kernels read those, not the fp32 masters)."""
+        cfg = dict(cfg)
+        native = hasattr(model, "_flat") and hasattr(model, "repack_weights")
+        if native and cfg.get("_target_") in ("torch.optim.AdamW", "climsr_amd.core.optim.AdamW"):
+            from .optim import AdamW
+
+            params = {k: v for k, v in cfg.items() if not k.startswith("_")}
+            return AdamW(model.parameters(), owner=model, **params)
+        opt = self.instantiate(cfg, model.parameters())
+        if native:
+            step = opt.step
+
+            def step_and_repack(*a, **kw):
+                out = step(*a, **kw)
+                model.repack_weights()
+                return out
+
+            opt.step = step_and_repack
+        return opt
 
     def scheduler(self, cfg, optimizer):
+        """instantiator.py:51-64: torch.optim schedulers get OneCycleLR's total_steps from num_training_steps and lose
+        the two step keys; only torch.optim and transformers schedulers are accepted."""
         cfg = dict(cfg)
-        if cfg.get("_target_", "").startswith("torch.optim"):
-            if cfg.get("_target_").endswith("OneCycleLR"):
+        target = cfg.get("_target_", "")
+        if target.startswith("torch.optim"):
+            if target.endswith("OneCycleLR"):
                 cfg["total_steps"] = cfg.get("num_training_steps")
-            cfg.pop("num_training_steps", None)
-            cfg.pop("num_warmup_steps", None)
+            cfg.pop("num_training_steps")
+            cfg.pop("num_warmup_steps")
+        elif not target.startswith("transformers"):
+            raise ValueError("Only LR schedulers from `torch.optim` and `transformers` library are supported. "
+                             f"If you want to support {target}, you must add your own instantiation logic here.")
         return self.instantiate(cfg, optimizer=optimizer)
 
     def instantiate(self, *args, **kwargs):

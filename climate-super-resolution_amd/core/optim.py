@@ -12,7 +12,8 @@ from typing import Iterable, List, Optional
 import torch
 
 from .. import _lib
-from .._lib import check, ptr
+from .._lib import ptr
+from ..ops import _launch
 
 
 def _flat_owner(params: List[torch.Tensor]):
@@ -77,8 +78,8 @@ class AdamW(torch.optim.Optimizer):
                 if "m" not in st:
                     st["m"] = torch.zeros_like(flat)
                     st["v"] = torch.zeros_like(flat)
-                check(lib.climsr_adamw_step(flat.numel(), ptr(flat), ptr(gflat), ptr(st["m"]), ptr(st["v"]), ptr(hp),
-                                            _lib.stream_ptr()), "adamw")
+                _launch("adamw", lambda: lib.climsr_adamw_step(flat.numel(), ptr(flat), ptr(gflat), ptr(st["m"]), ptr(st["v"]),
+                                                               ptr(hp), _lib.stream_ptr()), nbytes=28 * flat.numel())
             else:
                 for p in params:
                     ps = self.state[p]
@@ -86,8 +87,8 @@ class AdamW(torch.optim.Optimizer):
                         ps["m"] = torch.zeros_like(p)
                         ps["v"] = torch.zeros_like(p)
                     g = p.grad.contiguous()
-                    check(lib.climsr_adamw_step(p.numel(), ptr(p), ptr(g), ptr(ps["m"]), ptr(ps["v"]), ptr(hp),
-                                                _lib.stream_ptr()), "adamw")
+                    _launch("adamw", lambda: lib.climsr_adamw_step(p.numel(), ptr(p), ptr(g), ptr(ps["m"]), ptr(ps["v"]), ptr(hp),
+                                                                   _lib.stream_ptr()), nbytes=28 * p.numel())
         if self.owner is not None:
             self.owner.repack_weights()
         return loss
@@ -116,8 +117,9 @@ class GraphedAdamW:
         lib = _lib.load()
         s = _lib.stream_ptr()
         ts, lr, pct, div, fdiv, b2, eps, wd = self.cfg
-        check(lib.climsr_adamw_hparams(ptr(self.state), ts, lr, pct, div, fdiv, b2, eps, wd, ptr(self.hp), s), "adamw_hparams")
+        _launch("adamw_hparams", lambda: lib.climsr_adamw_hparams(ptr(self.state), ts, lr, pct, div, fdiv, b2, eps, wd, ptr(self.hp),
+                                                                  s))
         flat = self.module._flat
-        check(lib.climsr_adamw_step(flat.numel(), ptr(flat), ptr(self.module._flat_grad), ptr(self.m), ptr(self.v), ptr(self.hp),
-                                    s), "adamw")
+        _launch("adamw", lambda: lib.climsr_adamw_step(flat.numel(), ptr(flat), ptr(self.module._flat_grad), ptr(self.m), ptr(self.v),
+                                                       ptr(self.hp), s), nbytes=28 * flat.numel())
         self.module.engine().repack()

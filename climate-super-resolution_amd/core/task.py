@@ -25,7 +25,6 @@ from ..metrics.sr_metrics import SRMetrics
 from .checkpoint import load_from_checkpoint as _load_from_checkpoint
 from .checkpoint import save_checkpoint as _save_checkpoint
 from .instantiator import HydraInstantiator
-from .optim import AdamW
 
 try:  # pragma: no cover - not installed in the build image
     import pytorch_lightning as pl
@@ -35,6 +34,20 @@ except ImportError:  # the built-in trainer drives the same API
     _Base = torch.nn.Module
 
 BATCH_KEYS = ("lr", "hr", "elevation", "mask")
+
+
+def _cfg_dict(cfg):
+    """A Hydra/OmegaConf node or mapping as a plain dict (None stays None)."""
+    if cfg is None:
+        return None
+    try:  # pragma: no cover - omegaconf is not installed in the build image
+        from omegaconf import OmegaConf
+
+        if OmegaConf.is_config(cfg):
+            return OmegaConf.to_container(cfg, resolve=True)
+    except ImportError:
+        pass
+    return dict(cfg)
 default_instantiator = HydraInstantiator()
 
 
@@ -80,26 +93,75 @@ class TaskSuperResolutionModule(_Base):
         sr = self(lr, elev, mask)
         return hr, sr
 
-    def configure_optimizers(self, num_training_steps: int = 1000):
-        """AdamW (native, lr/betas/eps/weight_decay as conf/optimizers/adamw.yaml) + torch OneCycleLR
-        (conf/schedulers/one_cycle_schedule.yaml) per network, interval "step"."""
-        opts: List[torch.optim.Optimizer] = []
-        scheds: List[Dict[str, Any]] = []
+    # -- optimisers / schedulers (task.py:173-226 + LitSuperResolutionModule.configure_optimizers / num_training_steps /
+    #    compute_warmup, task.py:53-92)
+    DEFAULT_OPTIMIZER = {"_target_": "torch.optim.AdamW", "lr": 1e-4, "weight_decay": 1e-4}          # conf/optimizers/adamw.yaml
+    DEFAULT_SCHEDULER = {"_target_": "torch.optim.lr_scheduler.OneCycleLR", "max_lr": 1e-4,           # one_cycle_schedule.yaml
+                         "num_training_steps": -1, "pct_start": 0.05, "div_factor": 2, "final_div_factor": 100}
+
+    @property
+    def num_training_steps(self) -> int:
+        """Total training steps inferred from the trainer and its datamodule (task.py:61-83)."""
+        t = getattr(self, "trainer", None)
+        if t is None:
+            raise RuntimeError("num_training_steps: no trainer attached; set the scheduler cfg's num_training_steps")
+        ltb = t.limit_train_batches
+        if isinstance(ltb, int) and ltb != 0:
+            dataset_size = ltb
+        elif isinstance(ltb, float):  # a fraction of the batches
+            dataset_size = int(len(t.datamodule.train_dataloader()) * ltb)
+        else:
+            dataset_size = len(t.datamodule.train_dataloader())
+        num_devices = max(1, getattr(t, "num_gpus", 0) or 0, getattr(t, "num_processes", 0) or 0)
+        if getattr(t, "tpu_cores", None):
+            num_devices = max(num_devices, t.tpu_cores)
+        effective_batch_size = t.accumulate_grad_batches * num_devices
+        max_estimated_steps = (dataset_size // effective_batch_size) * t.max_epochs
+        if t.max_steps and -1 < t.max_steps < max_estimated_steps:
+            return t.max_steps
+        return max_estimated_steps
+
+    def compute_warmup(self, num_training_steps: int, num_warmup_steps):
+        """task.py:85-92: < 0 = infer from the trainer; a float < 1 warm-up is a fraction of the steps."""
+        if num_training_steps < 0:
+            num_training_steps = self.num_training_steps
+        if isinstance(num_warmup_steps, float) and num_warmup_steps < 1.0:
+            num_warmup_steps *= num_training_steps
+        return num_training_steps, num_warmup_steps
+
+    def configure_optimizers(self):
+        """The Lightning hook (task.py:173-226): infer the step count from the generator scheduler cfg's
+        ``num_training_steps`` (-1 = from the trainer / datamodule), write it and the warm-up into every scheduler
+        cfg, then build one optimizer + scheduler per network through the instantiator
+        (``HydraInstantiator.optimizer`` / ``.scheduler``, instantiator.py:48-64); schedulers step per batch.
+        Missing cfgs default to conf/optimizers/adamw.yaml + conf/schedulers/one_cycle_schedule.yaml (the
+        reference has no default and would fail)."""
+        if self.instantiator is None:
+            raise RuntimeError("To train you must provide an instantiator to instantiate the optimizer and scheduler "
+                               "or override `configure_optimizers` in the `LightningModule`.")
         nets = [("generator", self.generator)]
         if self.discriminator is not None:
             nets.append(("discriminator", self.discriminator))
-        for name, net in nets:
-            ocfg = dict(self.optimizer_cfgs.get(f"{name}_optimizer") or {"lr": 1e-4, "weight_decay": 1e-4})
-            scfg = dict(self.scheduler_cfgs.get(f"{name}_scheduler") or {"max_lr": ocfg.get("lr", 1e-4), "pct_start": 0.05,
-                                                                          "div_factor": 2, "final_div_factor": 100})
-            ocfg.pop("_target_", None)
-            opt = AdamW(net.parameters(), owner=net, **ocfg)
-            for k in ("_target_", "num_training_steps", "num_warmup_steps", "epochs"):
-                scfg.pop(k, None)
-            sch = torch.optim.lr_scheduler.OneCycleLR(opt, total_steps=num_training_steps, **scfg)
-            opts.append(opt)
-            scheds.append({"scheduler": sch, "interval": "step"})
-        return opts, scheds
+        ocfgs = {n: _cfg_dict(self.optimizer_cfgs.get(f"{n}_optimizer")) for n, _ in nets}
+        scfgs = {n: _cfg_dict(self.scheduler_cfgs.get(f"{n}_scheduler")) for n, _ in nets}
+        for n, _ in nets:
+            if ocfgs[n] is None:
+                ocfgs[n] = dict(self.DEFAULT_OPTIMIZER)
+            if scfgs[n] is None:
+                scfgs[n] = dict(self.DEFAULT_SCHEDULER, max_lr=ocfgs[n].get("lr", 1e-4))
+        g = scfgs["generator"]
+        num_training_steps, num_warmup_steps = self.compute_warmup(num_training_steps=g.get("num_training_steps", -1),
+                                                                   num_warmup_steps=g.get("num_warmup_steps", None))
+        for n, _ in nets:
+            scfgs[n]["num_training_steps"] = num_training_steps
+            scfgs[n]["num_warmup_steps"] = num_warmup_steps
+        self.inferred_training_steps = num_training_steps
+        self._optimizers, self._schedulers = [], []
+        for n, net in nets:
+            opt = self.instantiator.optimizer(net, ocfgs[n])
+            self._optimizers.append(opt)
+            self._schedulers.append(self.instantiator.scheduler(scfgs[n], opt))
+        return self._optimizers, [{"scheduler": s, "interval": "step"} for s in self._schedulers]
 
     # -- validation / test (task.py:262-294, 336-391): metrics fused on device (climsr_amd.metrics)
     def common_val_test_step(self, batch: Any, prefix: str = "val") -> Dict[str, Tensor]:

@@ -30,6 +30,16 @@ void set_error(const char* fmt, ...) {
 static thread_local bool g_dry = false;
 static thread_local char g_dry_name[96] = "";
 
+// true (and the kernel's name recorded) when the dispatcher runs dry: the caller returns before launching
+static bool dry_run(const char* fmt, ...) {
+  if (!g_dry) return false;
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_dry_name, sizeof(g_dry_name), fmt, ap);
+  va_end(ap);
+  return true;
+}
+
 int check_launch(const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
@@ -2307,10 +2317,7 @@ extern "C" int climsr_dgrad_single_output(int n, int h, int w, int ks, int pad, 
     return CLIMSR_EINVAL;
   }
   const long tiles = (long)n * ((h + S1_T - 1) / S1_T) * ((w + S1_T - 1) / S1_T);
-  if (g_dry) {
-    snprintf(g_dry_name, sizeof(g_dry_name), "dgrad_ci1_kernel<%d>", ks);
-    return CLIMSR_OK;
-  }
+  if (dry_run("dgrad_ci1_kernel<%d, %d>", ks, c / 8)) return CLIMSR_OK;
 #define CLIMSR_CI1(KS_, LPP_)                                                                                              \
   hipLaunchKernelGGL((dgrad_ci1_kernel<KS_, LPP_>), dim3((unsigned)tiles), dim3(256), 0, (hipStream_t)stream, n, h, w, pad, dz, \
                      dz_cstride, dz_coff, weight, act, slope, res1, res1_cstride, res1_coff, out, out_cstride, out_coff)
@@ -2607,6 +2614,20 @@ extern "C" const char* climsr_conv2d_fwd_kernel(const ClimsrConvDesc* d, const f
   return rc == CLIMSR_OK ? g_dry_name : "";
 }
 
+extern "C" int climsr_dgrad_single_output(int n, int h, int w, int ks, int pad, const uint16_t* dz, int dz_cstride, int dz_coff,
+                                          const float* weight, int c, int act, float slope, const uint16_t* res1, int res1_cstride,
+                                          int res1_coff, uint16_t* out, int out_cstride, int out_coff, void* stream);
+
+extern "C" const char* climsr_dgrad_single_output_kernel(int ks, int c, int act) {
+  static uint16_t dummy[8];
+  static float wdummy[8];
+  g_dry = true;
+  g_dry_name[0] = 0;
+  const int rc = climsr_dgrad_single_output(1, 1, 1, ks, ks / 2, dummy, 8, 0, wdummy, c, act, 0.2f, dummy, 8, 0, dummy, c, 0, nullptr);
+  g_dry = false;
+  return rc == CLIMSR_OK ? g_dry_name : "";
+}
+
 // ------------------------------------------------------------------------------------------
 // Weight gradient: dW[co][ci][tap] = sum_px dz[px][co] * x[px*stride + tap - pad][ci]
 // GEMM: M = co (A = dz^T), N = ci (B = x), K = pixels.  Both operands are pixel-major in NHWC, so
@@ -2853,20 +2874,27 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs a) {
 // ci 16w..16w+15 (4 co fragments x 9 taps = 36 accumulators), so the workgroup's 4 waves never reduce with
 // each other; the 8x16-pixel tiles of its split are walked with the NEXT tile's dz / x prefetched into
 // registers while the current one is on the MFMA pipe.  Partials: [split][co_rows][in_c*9] (as above).
-constexpr int W64_TH = 8;
-constexpr int W64_TPH = W64_TH + 2, W64_TPW = TW + 2;
+// Stride 2 (the discriminator's features.2/8/14/20): 4 x 16 output tiles whose (2*4+1) x (2*16+1) input
+// footprint is staged whole; tap (r, s) of output pixel k reads tile pixel (2*row(k) + r, 2*col(k) + s).
 constexpr int W64_P = 64 + 8;  // LDS pixel pitch (channels) of both tiles
-constexpr int W64_NZ = W64_TH * TW * 8;              // 16 B vectors of a dz tile (128 px x 64 ch)
-constexpr int W64_NX = W64_TPH * W64_TPW * 8;         // of an x tile (180 px x 64 ch)
+template <int S>
+struct W64 {
+  static constexpr int TH = S == 1 ? 8 : 4;                    // output tile rows (x TW = 16 columns)
+  static constexpr int TPH = S * (TH - 1) + 3, TPW = S * (TW - 1) + 3;  // staged input footprint
+  static constexpr int NZ = TH * TW * 8;                      // 16 B vectors of a dz tile (TH*16 px x 64 ch)
+  static constexpr int NX = TPH * TPW * 8;                    // of an x tile
+  static constexpr size_t LDS = (size_t)(TH * TW + TPH * TPW) * W64_P * 2;
+};
 
 // TS = 2: 8 waves, wave w owns ci block w & 3 and taps [0,5) or [5,9) (w >> 2): 20 accumulators instead of 36, so
 // two waves share each SIMD (latency hiding) at the price of each wave re-reading the shared dz fragments.
-template <int TS>
+template <int TS, int S = 1>
 __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
   constexpr int NTHR = 256 * TS, NU = TS == 1 ? 9 : 5;
+  constexpr int TH = W64<S>::TH, TPW = W64<S>::TPW, NZ = W64<S>::NZ, NX = W64<S>::NX;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint16_t* zs = (uint16_t*)smem;                       // [128 px][W64_P]
-  uint16_t* xs = zs + W64_TH * TW * W64_P;              // [180 px][W64_P]
+  uint16_t* zs = (uint16_t*)smem;                       // [TH*16 px][W64_P]
+  uint16_t* xs = zs + TH * TW * W64_P;                  // [TPH*TPW px][W64_P]
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
   const int wave = (tid >> 6) & 3, tg = TS == 1 ? 0 : tid >> 8;  // ci block, tap group
   const int u0 = tg * 5;
@@ -2892,14 +2920,14 @@ __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
     if constexpr (TS == 1) {
-      tapoff[u] = ((u / 3) * W64_TPW + (u % 3)) * W64_P + wave * 16 + 4 * p;
+      tapoff[u] = ((u / 3) * TPW + (u % 3)) * W64_P + wave * 16 + 4 * p;
     } else {
       const int tp = u0 + u < 9 ? u0 + u : 8;
-      tapoff[u] = ((tp / 3) * W64_TPW + (tp % 3)) * W64_P + wave * 16 + 4 * p;
+      tapoff[u] = ((tp / 3) * TPW + (tp % 3)) * W64_P + wave * 16 + 4 * p;
     }
   }
 
-  constexpr int VZ = W64_NZ / NTHR, VX = (W64_NX + NTHR - 1) / NTHR;
+  constexpr int VZ = NZ / NTHR, VX = (NX + NTHR - 1) / NTHR;
   uint4 pz[VZ], px[VX];
   auto issue = [&](int tile) {
     int tt = tile;
@@ -2907,24 +2935,24 @@ __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
     tt /= a.tiles_x;
     const int ty = tt % a.tiles_y;
     const int nimg = tt / a.tiles_y;
-    const int oy0 = ty * W64_TH, ox0 = tx * TW;
+    const int oy0 = ty * TH, ox0 = tx * TW;
 #pragma unroll
     for (int i = 0; i < VZ; ++i) {  // dz: pixel v/8, channel group v%8
       const int v = tid + NTHR * i;
       const int pix = v >> 3, cg = v & 7;
       const int oy = oy0 + (pix >> 4), ox = ox0 + (pix & 15);
       pz[i] = make_uint4(0, 0, 0, 0);
-      if (!(a.ablate & 1) && oy < a.out_h && ox < a.out_w)
+      if (oy < a.out_h && ox < a.out_w)
         pz[i] = *(const uint4*)(a.dz + (((long)nimg * a.out_h + oy) * a.out_w + ox) * a.dz_cs + co0 + cg * 8);
     }
 #pragma unroll
     for (int i = 0; i < VX; ++i) {
       const int v = tid + NTHR * i;
       const int pix = v >> 3, cg = v & 7;
-      const int py = pix / W64_TPW, pxx = pix - py * W64_TPW;
-      const int iy = oy0 - a.pad + py, ix = ox0 - a.pad + pxx;
+      const int py = pix / TPW, pxx = pix - py * TPW;
+      const int iy = S * oy0 - a.pad + py, ix = S * ox0 - a.pad + pxx;
       px[i] = make_uint4(0, 0, 0, 0);
-      if (!(a.ablate & 1) && v < W64_NX && iy >= 0 && iy < lh && ix >= 0 && ix < lw)
+      if (v < NX && iy >= 0 && iy < lh && ix >= 0 && ix < lw)
         px[i] = *(const uint4*)(a.x + (((long)nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + ci0 +
                                 cg * 8);
     }
@@ -2941,13 +2969,12 @@ __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
 #pragma unroll
     for (int i = 0; i < VX; ++i) {
       const int v = tid + NTHR * i;
-      if (v < W64_NX) *(uint4*)(xs + (v >> 3) * W64_P + (v & 7) * 8) = px[i];
+      if (v < NX) *(uint4*)(xs + (v >> 3) * W64_P + (v & 7) * 8) = px[i];
     }
     if (tile + a.nsplit < a.ntiles) issue(tile + a.nsplit);
     __syncthreads();
-    if (a.ablate & 2) continue;
 #pragma unroll 2
-    for (int kk = 0; kk < W64_TH * TW / 32; ++kk) {  // k-step: output pixel rows 2kk, 2kk+1
+    for (int kk = 0; kk < TH * TW / 32; ++kk) {  // k-step: output pixel rows 2kk, 2kk+1
       const int k0 = kk * 32 + 8 * g + q, k1 = k0 + 4;
       bf16x8 af[4];
 #pragma unroll
@@ -2961,7 +2988,7 @@ __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) accb[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], ones, accb[t], 0, 0, 0);
       }
-      const int xb0 = ((k0 >> 4) * W64_TPW + (k0 & 15)) * W64_P, xb1 = ((k1 >> 4) * W64_TPW + (k1 & 15)) * W64_P;
+      const int xb0 = (S * (k0 >> 4) * TPW + S * (k0 & 15)) * W64_P, xb1 = (S * (k1 >> 4) * TPW + S * (k1 & 15)) * W64_P;
 #pragma unroll
       for (int u = 0; u < NU; ++u) {
         if (TS == 2 && u == NU - 1 && tg == 1) continue;  // tap group 1 has 4 taps (5..8)
@@ -3223,6 +3250,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_co1m_kernel(WgArgs a) {
 
 template <int KS, int NCF>
 static int launch_wco1(const WgArgs& a, hipStream_t s) {
+  if (dry_run("conv_wgrad_co1m_kernel<%d, %d>", KS, NCF)) return CLIMSR_OK;
   auto k = conv_wgrad_co1m_kernel<KS, NCF>;  // (+16 B of static LDS: the dynamic cap leaves room for it)
   const size_t lds_x = (size_t)4 * WCO1_XT * (NCF * 16 + 8) * 2 + (size_t)4 * KS * 8 * WCO1_DZL * 2;
   const size_t lds_r = (size_t)4 * KS * NCF * 64 * 16;
@@ -3237,8 +3265,10 @@ static int launch_wco1(const WgArgs& a, hipStream_t s) {
 }
 
 static bool w64_shape(const ClimsrConvDesc* d) {
-  return d->ks == 3 && d->stride == 1 && d->pad == 1 && d->out_c % 64 == 0 && d->in_c % 64 == 0 && d->in_c >= 64;
+  return d->ks == 3 && d->pad == 1 && d->out_c % 64 == 0 && d->in_c % 64 == 0 && d->in_c >= 64 &&
+         (d->stride == 1 || (d->stride == 2 && d->up == 1));
 }
+static int w64_th(const ClimsrConvDesc* d) { return d->stride == 2 ? W64<2>::TH : W64<1>::TH; }
 
 struct WgPlan {
   int ntc, tb, ntapb, ncib, ncob, co_rows, tiles_x, tiles_y, ntiles, tph, tpw, dzp, kw, ci4;
@@ -3287,7 +3317,7 @@ extern "C" int climsr_conv2d_wgrad_splits(const ClimsrConvDesc* d) {
   if (wco1_shape(d) && !getenv("CLIMSR_NO_CO1M")) return wco1_splits(d);
   if (w64_shape(d)) {  // one workgroup per CU: 256 / blocks splits
     int blocks = (d->out_c / 64) * (d->in_c / 64);
-    int ntiles = d->n * ceil_div(d->out_w, TW) * ceil_div(d->out_h, W64_TH);
+    int ntiles = d->n * ceil_div(d->out_w, TW) * ceil_div(d->out_h, w64_th(d));
     int ns = ceil_div(256, blocks);
     if (ns > ntiles) ns = ntiles;
     return ns < 1 ? 1 : ns;
@@ -3316,6 +3346,7 @@ extern "C" size_t climsr_conv2d_wgrad_workspace(const ClimsrConvDesc* d, int nsp
 
 template <int NTC, int TB, int CI4>
 static int launch_wg(const WgArgs& a, int nblk, size_t lds, hipStream_t s) {
+  if (dry_run("conv_wgrad_kernel<%d, %d, %d, false>", NTC, TB, CI4)) return CLIMSR_OK;
   auto k = conv_wgrad_kernel<NTC, TB, CI4>;
   static bool attr_set = false;
   if (!attr_set) {
@@ -3342,6 +3373,7 @@ extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, c
     const int rows = round_up(d->out_c, 16), ntc = rows >= 64 ? 4 : (rows >= 32 ? 2 : 1);
     a.co_rows = ceil_div(rows, ntc * 16) * ntc * 16;
     hipStream_t s = (hipStream_t)stream;
+    if (dry_run("conv_wgrad_pt_kernel<%d>", d->out_c / 16 < 4 ? d->out_c / 16 : 4)) return CLIMSR_OK;
     switch (d->out_c / 16) {
       case 1: hipLaunchKernelGGL(conv_wgrad_pt_kernel<1>, dim3(nsplit), dim3(256), 0, s, a); break;
       case 2: hipLaunchKernelGGL(conv_wgrad_pt_kernel<2>, dim3(nsplit), dim3(256), 0, s, a); break;
@@ -3378,26 +3410,34 @@ extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, c
     a.n = d->n; a.in_h = d->in_h; a.in_w = d->in_w; a.in_c = d->in_c; a.in_cs = d->in_cstride; a.in_co = d->in_coff;
     a.up = d->up; a.ks = 3; a.stride = 1; a.pad = 1; a.out_h = d->out_h; a.out_w = d->out_w;
     a.out_c = d->out_c; a.dz_cs = dz_cstride;
-    a.tiles_x = ceil_div(d->out_w, TW); a.tiles_y = ceil_div(d->out_h, W64_TH); a.ntiles = d->n * a.tiles_x * a.tiles_y;
+    a.tiles_x = ceil_div(d->out_w, TW); a.tiles_y = ceil_div(d->out_h, w64_th(d)); a.ntiles = d->n * a.tiles_x * a.tiles_y;
     a.nsplit = nsplit; a.ncib = d->in_c / 64; a.co_rows = d->out_c; a.kw = d->in_c * 9;
-    a.tph = W64_TPH; a.tpw = W64_TPW; a.dzp = W64_P; a.ntapb = 1; a.lds_x = 0;
-    static int ablate = getenv("CLIMSR_ABLATE") ? atoi(getenv("CLIMSR_ABLATE")) : 0;
-    a.ablate = ablate;
-    const size_t lds = (size_t)(W64_TH * TW + W64_TPH * W64_TPW) * W64_P * 2;
+    a.dzp = W64_P; a.ntapb = 1; a.lds_x = 0; a.ablate = 0;
+    a.stride = d->stride;
     // 8 waves (tap-split) pay off on the large-pixel-count convs (HRconv / upconv at 256^2: +8 %) and lose on the
     // 64^2 dense-block GEMM (-19 %), measured with tests/perf_conv.py
-    static const int ts2_env = getenv("CLIMSR_W64_TS2") ? atoi(getenv("CLIMSR_W64_TS2")) : -1;
-    const bool ts2 = ts2_env >= 0 ? ts2_env != 0 : (long)d->n * d->out_h * d->out_w >= (1L << 20);
+    const bool ts2 = d->stride == 1 && (long)d->n * d->out_h * d->out_w >= (1L << 20);
     static bool attr_set = false;
     if (!attr_set) {
-      (void)hipFuncSetAttribute((const void*)conv_wgrad64_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      (void)hipFuncSetAttribute((const void*)conv_wgrad64_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)conv_wgrad64_kernel<1, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)conv_wgrad64_kernel<2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)conv_wgrad64_kernel<1, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       attr_set = true;
     }
-    if (ts2)
-      hipLaunchKernelGGL(conv_wgrad64_kernel<2>, dim3((d->out_c / 64) * (d->in_c / 64), nsplit), dim3(512), lds, (hipStream_t)stream, a);
-    else
-      hipLaunchKernelGGL(conv_wgrad64_kernel<1>, dim3((d->out_c / 64) * (d->in_c / 64), nsplit), dim3(256), lds, (hipStream_t)stream, a);
+    const dim3 grid((d->out_c / 64) * (d->in_c / 64), nsplit);
+    if (d->stride == 2) {
+      a.tph = W64<2>::TPH; a.tpw = W64<2>::TPW;
+      if (dry_run("conv_wgrad64_kernel<1, 2>")) return CLIMSR_OK;
+      hipLaunchKernelGGL((conv_wgrad64_kernel<1, 2>), grid, dim3(256), W64<2>::LDS, (hipStream_t)stream, a);
+    } else if (ts2) {
+      a.tph = W64<1>::TPH; a.tpw = W64<1>::TPW;
+      if (dry_run("conv_wgrad64_kernel<2, 1>")) return CLIMSR_OK;
+      hipLaunchKernelGGL((conv_wgrad64_kernel<2, 1>), grid, dim3(512), W64<1>::LDS, (hipStream_t)stream, a);
+    } else {
+      a.tph = W64<1>::TPH; a.tpw = W64<1>::TPW;
+      if (dry_run("conv_wgrad64_kernel<1, 1>")) return CLIMSR_OK;
+      hipLaunchKernelGGL((conv_wgrad64_kernel<1, 1>), grid, dim3(256), W64<1>::LDS, (hipStream_t)stream, a);
+    }
     return check_launch("conv2d_wgrad (64x64 block)");
   }
   WgPlan w;
@@ -3420,6 +3460,7 @@ extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, c
   hipStream_t s = (hipStream_t)stream;
   if (wg_ws(d, w)) {  // all 21 tap groups per workgroup, 6 per wave
     a.ntapb = 1;
+    if (dry_run("conv_wgrad_kernel<4, 6, 1, true>")) return CLIMSR_OK;
     auto k = conv_wgrad_kernel<4, 6, 1, true>;
     static bool attr_set = false;
     if (!attr_set) {
@@ -3439,6 +3480,16 @@ extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, c
 #undef WG_CASE
   set_error("conv2d_wgrad: no kernel for ntc=%d tb=%d", w.ntc, w.tb);
   return CLIMSR_EINVAL;
+}
+
+extern "C" const char* climsr_conv2d_wgrad_kernel(const ClimsrConvDesc* d) {
+  static uint16_t dummy[8];
+  static float fdummy[8];
+  g_dry = true;
+  g_dry_name[0] = 0;
+  const int rc = climsr_conv2d_wgrad(d, dummy, dummy, 8, fdummy, fdummy, climsr_conv2d_wgrad_splits(d), nullptr);
+  g_dry = false;
+  return rc == CLIMSR_OK ? g_dry_name : "";
 }
 
 // 256 threads = 32 consecutive outputs x 8 split groups (8 independent load chains per output,

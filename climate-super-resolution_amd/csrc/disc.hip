@@ -14,8 +14,6 @@ using namespace climsr;
 
 namespace {
 
-constexpr int BN_BLOCKS = 256;
-
 __device__ inline void unpack8(uint4 u, float* f) {
   uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
@@ -32,218 +30,339 @@ __device__ inline uint4 pack8(const float* f) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// BatchNorm statistics: per-channel sum / sum of squares over npix rows of an NHWC [npix][c]
-// tensor.  Block b owns a fixed pixel range; threads = (c/8 channel groups) x rows.  Partials are
-// fp64 [BN_BLOCKS][2][c]; the finish kernel sums them in block order.
-// mode 0: x = z (bf16), stats of z.  mode 1 (backward): d = da * lrelu'(a) (da fp32, a bf16),
-// xhat = (z-mean)*rstd; sums of d and d*xhat.
+// BatchNorm2d (train mode) over an NHWC [npix][c] bf16 tensor (rfb_esrgan.py:32-50; discriminator.py:17-18).
+//
+// Thread layout shared by the statistics and apply kernels: G = c/8 channel groups (one uint4 = 8 bf16
+// channels per load), R = 256/G pixel rows per 256-thread block; thread (cg = tid % G, r = tid / G) owns the
+// 8 channels cg*8.. for every R-th pixel of its block's range, so each block streams one contiguous
+// [pixels x c] slab (coalesced) and a thread's per-channel constants live in registers.  Pixel counts fit
+// in 32 bits (npix * c < 2^31 is checked on the host), so there is no 64-bit division anywhere.
+//
+// Statistics: every thread accumulates fp32 over <= BN_PX_PER_THREAD pixels (4 loads in flight), the block
+// combines its R rows in fp64 in a fixed order and writes fp64 partials [P][2][c]; the finish kernel sums the
+// P partials (8 slices per channel, fixed order) -> deterministic for a given shape.
+// mode 0 (forward): sums of z and z^2.  mode 1 (backward): d = da * lrelu'(a); sums of d and d * xhat,
+// xhat = (z - mean) * rstd.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void bn_partial_kernel(long npix, int c, const uint16_t* __restrict__ z,
-                                                         const float* __restrict__ da, const uint16_t* __restrict__ a,
-                                                         const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                         float slope, int mode, double* __restrict__ part) {
-  extern __shared__ double shd[];  // [256][16]
-  const int groups = c / 8;
-  const int rows = 256 / groups;  // c <= 2048 -> groups <= 256
+constexpr int BN_MAX_PARTS = 2048;
+constexpr long BN_TARGET_BLOCKS = 1024;  // >= 4 blocks (16 waves) per CU in flight for these streaming kernels
+
+struct BnGrid {
+  int parts;    // statistics blocks P
+  int per_blk;  // pixels per statistics block (multiple of R)
+};
+
+// Pixels per thread: as many as keep >= BN_TARGET_BLOCKS blocks (4..64), so small late layers (512 ch x 8 K px)
+// still fill the chip and large early ones amortise the partials.
+static inline int bn_px_per_thread(long npix, int c) {
+  const long threads_px = npix * (c / 8) / (BN_TARGET_BLOCKS * 256);
+  return (int)(threads_px < 4 ? 4 : threads_px > 64 ? 64 : threads_px);
+}
+
+static inline BnGrid bn_grid(long npix, int c) {
+  const int G = c / 8;
+  const int R = 256 / G;
+  long per = (long)R * bn_px_per_thread(npix, c);
+  const long need = (npix + BN_MAX_PARTS - 1) / BN_MAX_PARTS;
+  if (per < need) per = (need + R - 1) / R * R;
+  return BnGrid{(int)((npix + per - 1) / per), (int)per};
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void bn_stats_kernel(int npix, int c, int per_blk, const uint16_t* __restrict__ z,
+                                                       const float* __restrict__ da, const uint16_t* __restrict__ a,
+                                                       const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                       float slope, double* __restrict__ part) {
+  __shared__ float ls[2][2048];  // [sum | sumsq][R][c] (R * c <= 2048)
+  const int G = c >> 3;
+  const int R = 256 / G;
   const int tid = threadIdx.x;
-  const int cg = tid % groups;
-  const int r = tid / groups;
-  const long p0 = (long)blockIdx.x * npix / gridDim.x;
-  const long p1 = (long)(blockIdx.x + 1) * npix / gridDim.x;
-  double s[8], q[8];
+  const int cg = tid % G;
+  const int r = tid / G;
+  const int p0 = blockIdx.x * per_blk;
+  const int p1 = min(p0 + per_blk, npix);
+  float s[8], q[8], mu[8], rs[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) { s[i] = 0.0; q[i] = 0.0; }
-  float mu[8], rs[8];
-  if (mode == 1) {
+  for (int i = 0; i < 8; ++i) { s[i] = 0.f; q[i] = 0.f; mu[i] = 0.f; rs[i] = 0.f; }
+  if (r < R) {
+    if (MODE == 1) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) { mu[i] = mean[cg * 8 + i]; rs[i] = rstd[cg * 8 + i]; }
-  }
-  if (r < rows) {
-    for (long p = p0 + r; p < p1; p += rows) {
+      for (int i = 0; i < 8; ++i) { mu[i] = mean[cg * 8 + i]; rs[i] = rstd[cg * 8 + i]; }
+    }
+    auto accum = [&](int p) {
       float zf[8];
-      unpack8(*(const uint4*)(z + p * c + cg * 8), zf);
-      if (mode == 0) {
+      unpack8(*(const uint4*)(z + (size_t)p * c + cg * 8), zf);
+      if (MODE == 0) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) { s[i] += zf[i]; q[i] += (double)zf[i] * zf[i]; }
+        for (int i = 0; i < 8; ++i) { s[i] += zf[i]; q[i] = fmaf(zf[i], zf[i], q[i]); }
       } else {
         float af[8];
-        unpack8(*(const uint4*)(a + p * c + cg * 8), af);
-        const float4* dp = (const float4*)(da + p * c + cg * 8);
-        float4 d0 = dp[0], d1 = dp[1];
-        float dd[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+        unpack8(*(const uint4*)(a + (size_t)p * c + cg * 8), af);
+        const float4* dp = (const float4*)(da + (size_t)p * c + cg * 8);
+        const float4 d0 = dp[0], d1 = dp[1];
+        const float dd[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          float d = af[i] > 0.f ? dd[i] : dd[i] * slope;
-          float xh = (zf[i] - mu[i]) * rs[i];
+          const float d = af[i] > 0.f ? dd[i] : dd[i] * slope;
           s[i] += d;
-          q[i] += (double)d * xh;
+          q[i] = fmaf(d, (zf[i] - mu[i]) * rs[i], q[i]);
         }
       }
+    };
+    int p = p0 + r;
+    for (; p + 3 * R < p1; p += 4 * R) {
+      accum(p);
+      accum(p + R);
+      accum(p + 2 * R);
+      accum(p + 3 * R);
+    }
+    for (; p < p1; p += R) accum(p);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      ls[0][r * c + cg * 8 + i] = s[i];
+      ls[1][r * c + cg * 8 + i] = q[i];
     }
   }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) { shd[tid * 16 + i] = s[i]; shd[tid * 16 + 8 + i] = q[i]; }
   __syncthreads();
-  if (tid < groups) {
-    double ts[8], tq[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) { ts[i] = 0.0; tq[i] = 0.0; }
-    for (int rr = 0; rr < rows; ++rr) {
-      const double* src = shd + (rr * groups + tid) * 16;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) { ts[i] += src[i]; tq[i] += src[8 + i]; }
+  for (int ch = tid; ch < c; ch += 256) {
+    double ts = 0.0, tq = 0.0;
+    for (int rr = 0; rr < R; ++rr) {
+      ts += (double)ls[0][rr * c + ch];
+      tq += (double)ls[1][rr * c + ch];
     }
-    double* out = part + (long)blockIdx.x * 2 * c;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) { out[tid * 8 + i] = ts[i]; out[c + tid * 8 + i] = tq[i]; }
+    double* out = part + (size_t)blockIdx.x * 2 * c;
+    out[ch] = ts;
+    out[c + ch] = tq;
   }
 }
 
-__global__ void bn_finish_stats_kernel(const double* __restrict__ part, int nblk, int c, long npix, float eps,
-                                       float momentum, float* mean, float* rstd, float* run_mean, float* run_var,
-                                       float* nbt) {
-  int ch = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch >= c) return;
-  double s = 0.0, q = 0.0;
-  for (int b = 0; b < nblk; ++b) { s += part[(long)b * 2 * c + ch]; q += part[(long)b * 2 * c + c + ch]; }
-  double m = s / (double)npix;
+// Sum of the P partials of channel ch: a block owns 8 channels (one 64 B row segment) x 32 slices; slice sl sums
+// partials sl, sl+32, ... with 4 independent chains, then the 32 slice sums are added in a fixed order.
+__device__ inline void bn_sum_parts(const double* __restrict__ part, int parts, int c, double* red, double& s, double& q,
+                                    int& ch) {
+  const int lane = threadIdx.x & 7, sl = threadIdx.x >> 3;
+  ch = blockIdx.x * 8 + lane;
+  double ts[4] = {0.0, 0.0, 0.0, 0.0}, tq[4] = {0.0, 0.0, 0.0, 0.0};
+  if (ch < c) {
+    int b = sl;
+    for (; b + 96 < parts; b += 128) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        ts[u] += part[(size_t)(b + 32 * u) * 2 * c + ch];
+        tq[u] += part[(size_t)(b + 32 * u) * 2 * c + c + ch];
+      }
+    }
+    for (; b < parts; b += 32) {
+      ts[0] += part[(size_t)b * 2 * c + ch];
+      tq[0] += part[(size_t)b * 2 * c + c + ch];
+    }
+  }
+  red[threadIdx.x] = (ts[0] + ts[1]) + (ts[2] + ts[3]);
+  red[256 + threadIdx.x] = (tq[0] + tq[1]) + (tq[2] + tq[3]);
+  __syncthreads();
+  s = 0.0;
+  q = 0.0;
+  if (sl == 0) {
+    for (int k = 0; k < 32; ++k) {
+      s += red[k * 8 + lane];
+      q += red[256 + k * 8 + lane];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_finish_stats_kernel(const double* __restrict__ part, int parts, int c, int npix,
+                                                              float eps, float momentum, float* mean, float* rstd,
+                                                              float* run_mean, float* run_var, int64_t* nbt) {
+  __shared__ double red[512];
+  double s, q;
+  int ch;
+  bn_sum_parts(part, parts, c, red, s, q, ch);
+  if ((threadIdx.x >> 3) != 0 || ch >= c) return;
+  const double m = s / (double)npix;
   double var = q / (double)npix - m * m;
   if (var < 0.0) var = 0.0;
   mean[ch] = (float)m;
   rstd[ch] = (float)(1.0 / sqrt(var + (double)eps));
   if (run_mean) {
-    double unb = npix > 1 ? var * (double)npix / (double)(npix - 1) : var;
+    const double unb = npix > 1 ? var * (double)npix / (double)(npix - 1) : var;
     run_mean[ch] = (float)((1.0 - momentum) * run_mean[ch] + momentum * m);
     run_var[ch] = (float)((1.0 - momentum) * run_var[ch] + momentum * unb);
   }
-  (void)nbt;
+  if (nbt && ch == 0) *nbt += 1;  // BatchNorm2d.num_batches_tracked
 }
 
-__global__ void bn_apply_kernel(long npix, int c, const uint16_t* __restrict__ z, const float* __restrict__ mean,
-                                const float* __restrict__ rstd, const float* __restrict__ gamma, const float* __restrict__ beta,
-                                int act, float slope, uint16_t* __restrict__ y) {
-  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int groups = c / 8;
-  if (idx >= npix * groups) return;
-  const long p = idx / groups;
-  const int c0 = (int)(idx % groups) * 8;
-  float f[8];
-  unpack8(*(const uint4*)(z + p * c + c0), f);
+// y = act(z * scale + shift) with scale = gamma*rstd, shift = beta - mean*scale (mode 0: batch statistics
+// mean/rstd; mode 1: running statistics, rstd = rsqrt(var + eps)).
+template <int MODE>
+__global__ __launch_bounds__(256) void bn_apply_kernel(int npix, int c, int per_blk, const uint16_t* __restrict__ z,
+                                                       const float* __restrict__ mean, const float* __restrict__ var_or_rstd,
+                                                       float eps, const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                       int act, float slope, uint16_t* __restrict__ y) {
+  const int G = c >> 3;
+  const int R = 256 / G;
+  const int cg = threadIdx.x % G;
+  const int r = threadIdx.x / G;
+  if (r >= R) return;
+  float sc[8], sh[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    float v = (f[i] - mean[c0 + i]) * rstd[c0 + i] * gamma[c0 + i] + beta[c0 + i];
-    f[i] = act_apply(v, act, slope);
+    const int ch = cg * 8 + i;
+    const float rs = MODE == 0 ? var_or_rstd[ch] : rsqrtf(var_or_rstd[ch] + eps);
+    sc[i] = gamma[ch] * rs;
+    sh[i] = beta[ch] - mean[ch] * sc[i];
   }
-  *(uint4*)(y + p * c + c0) = pack8(f);
+  const int p0 = blockIdx.x * per_blk;
+  const int p1 = min(p0 + per_blk, npix);
+  auto one = [&](int p) {
+    float f[8];
+    const size_t off = (size_t)p * c + cg * 8;
+    unpack8(*(const uint4*)(z + off), f);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = act_apply(fmaf(f[i], sc[i], sh[i]), act, slope);
+    *(uint4*)(y + off) = pack8(f);
+  };
+  int p = p0 + r;
+  for (; p + 3 * R < p1; p += 4 * R) {
+    one(p);
+    one(p + R);
+    one(p + 2 * R);
+    one(p + 3 * R);
+  }
+  for (; p < p1; p += R) one(p);
 }
 
-__global__ void bn_bwd_finish_kernel(const double* __restrict__ part, int nblk, int c, long npix, const float* __restrict__ gamma,
-                                     const float* __restrict__ rstd, float* dgamma, float* dbeta, int accumulate,
-                                     float* coef) {
-  int ch = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch >= c) return;
-  double s = 0.0, q = 0.0;
-  for (int b = 0; b < nblk; ++b) { s += part[(long)b * 2 * c + ch]; q += part[(long)b * 2 * c + c + ch]; }
+// Backward coefficients: dgamma (+)= sum(d*xhat), dbeta (+)= sum(d); coef = {gamma*rstd, mean(d), mean(d*xhat)}.
+__global__ __launch_bounds__(256) void bn_bwd_finish_kernel(const double* __restrict__ part, int parts, int c, int npix,
+                                                            const float* __restrict__ gamma, const float* __restrict__ rstd,
+                                                            float* dgamma, float* dbeta, int accumulate, float* coef) {
+  __shared__ double red[512];
+  double s, q;
+  int ch;
+  bn_sum_parts(part, parts, c, red, s, q, ch);
+  if ((threadIdx.x >> 3) != 0 || ch >= c) return;
   if (dgamma) dgamma[ch] = (accumulate ? dgamma[ch] : 0.f) + (float)q;
   if (dbeta) dbeta[ch] = (accumulate ? dbeta[ch] : 0.f) + (float)s;
-  // dz = gamma*rstd * (d - s/n - xhat*q/n)
   coef[ch] = gamma[ch] * rstd[ch];
   coef[c + ch] = (float)(s / (double)npix);
   coef[2 * c + ch] = (float)(q / (double)npix);
 }
 
-__global__ void bn_bwd_apply_kernel(long npix, int c, const float* __restrict__ da, const uint16_t* __restrict__ a,
-                                    const uint16_t* __restrict__ z, const float* __restrict__ mean, const float* __restrict__ rstd,
-                                    const float* __restrict__ coef, float slope, float out_slope, uint16_t* __restrict__ dz) {
-  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int groups = c / 8;
-  if (idx >= npix * groups) return;
-  const long p = idx / groups;
-  const int c0 = (int)(idx % groups) * 8;
-  float zf[8], af[8], o[8];
-  unpack8(*(const uint4*)(z + p * c + c0), zf);
-  unpack8(*(const uint4*)(a + p * c + c0), af);
-  const float4* dp = (const float4*)(da + p * c + c0);
-  float4 d0 = dp[0], d1 = dp[1];
-  float dd[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+// dz = gamma*rstd * (d - mean(d) - xhat * mean(d*xhat)), d = da * lrelu'(a); out_slope != 1: z is itself a
+// LeakyReLU output (plain discriminator) and dz carries its derivative too.
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(int npix, int c, int per_blk, const float* __restrict__ da,
+                                                           const uint16_t* __restrict__ a, const uint16_t* __restrict__ z,
+                                                           const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                           const float* __restrict__ coef, float slope, float out_slope,
+                                                           uint16_t* __restrict__ dz) {
+  const int G = c >> 3;
+  const int R = 256 / G;
+  const int cg = threadIdx.x % G;
+  const int r = threadIdx.x / G;
+  if (r >= R) return;
+  float k[8], m1[8], m2[8], mu[8], rs[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int ch = c0 + i;
-    float d = af[i] > 0.f ? dd[i] : dd[i] * slope;
-    float xh = (zf[i] - mean[ch]) * rstd[ch];
-    o[i] = coef[ch] * (d - coef[c + ch] - xh * coef[2 * c + ch]);
-    // BN input produced by a LeakyReLU (discriminator.py:17-18: conv -> LeakyReLU -> BN): chain its derivative
-    if (out_slope != 1.f && zf[i] <= 0.f) o[i] *= out_slope;
+    const int ch = cg * 8 + i;
+    k[i] = coef[ch];
+    m1[i] = coef[c + ch];
+    m2[i] = coef[2 * c + ch];
+    mu[i] = mean[ch];
+    rs[i] = rstd[ch];
   }
-  *(uint4*)(dz + p * c + c0) = pack8(o);
+  const int p0 = blockIdx.x * per_blk;
+  const int p1 = min(p0 + per_blk, npix);
+  auto one = [&](int p) {
+    const size_t off = (size_t)p * c + cg * 8;
+    float zf[8], af[8], o[8];
+    unpack8(*(const uint4*)(z + off), zf);
+    unpack8(*(const uint4*)(a + off), af);
+    const float4* dp = (const float4*)(da + off);
+    const float4 d0 = dp[0], d1 = dp[1];
+    const float dd[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float d = af[i] > 0.f ? dd[i] : dd[i] * slope;
+      const float xh = (zf[i] - mu[i]) * rs[i];
+      o[i] = k[i] * (d - m1[i] - xh * m2[i]);
+      if (out_slope != 1.f && zf[i] <= 0.f) o[i] *= out_slope;
+    }
+    *(uint4*)(dz + off) = pack8(o);
+  };
+  int p = p0 + r;
+  for (; p + 3 * R < p1; p += 4 * R) {
+    one(p);
+    one(p + R);
+    one(p + 2 * R);
+    one(p + 3 * R);
+  }
+  for (; p < p1; p += R) one(p);
 }
+
+static inline int bn_apply_grid(long npix, int c, int* per_blk) {
+  const int R = 256 / (c / 8);
+  *per_blk = R * bn_px_per_thread(npix, c);
+  return ceil_div(npix, *per_blk);
+}
+
+static bool bn_shape_ok(int64_t npix, int c) { return c > 0 && c % 8 == 0 && c <= 2048 && npix > 0 && npix * (int64_t)c < (1ll << 31); }
 
 }  // namespace
 
+extern "C" int64_t climsr_bn_workspace_doubles(int64_t npix, int c) {
+  if (!bn_shape_ok(npix, c)) return 0;
+  return (int64_t)bn_grid(npix, c).parts * 2 * c;
+}
+
 extern "C" int climsr_bn_forward(const uint16_t* z, int64_t npix, int c, const float* gamma, const float* beta, int act, float slope,
                                  float eps, float momentum, double* workspace, float* mean, float* rstd, float* run_mean,
-                                 float* run_var, uint16_t* y, void* stream) {
-  if (!z || !gamma || !beta || !workspace || !mean || !rstd || !y || c % 8 || c > 2048 || npix <= 0) {
-    set_error("bn_forward: bad args (c=%d)", c);
+                                 float* run_var, int64_t* num_batches_tracked, uint16_t* y, void* stream) {
+  if (!z || !gamma || !beta || !workspace || !mean || !rstd || !y || !bn_shape_ok(npix, c)) {
+    set_error("bn_forward: bad args (c=%d, npix=%lld)", c, (long long)npix);
     return CLIMSR_EINVAL;
   }
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(bn_partial_kernel, dim3(BN_BLOCKS), dim3(256), 256 * 16 * sizeof(double), s, (long)npix, c, z, nullptr,
-                     nullptr, nullptr, nullptr, 0.f, 0, workspace);
-  hipLaunchKernelGGL(bn_finish_stats_kernel, dim3(ceil_div(c, 256)), dim3(256), 0, s, workspace, BN_BLOCKS, c, (long)npix, eps,
-                     momentum, mean, rstd, run_mean, run_var, nullptr);
-  long total = (long)npix * (c / 8);
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, s, (long)npix, c, z, mean, rstd, gamma, beta, act,
-                     slope, y);
+  const BnGrid g = bn_grid(npix, c);
+  hipLaunchKernelGGL(bn_stats_kernel<0>, dim3(g.parts), dim3(256), 0, s, (int)npix, c, g.per_blk, z, nullptr, nullptr, nullptr,
+                     nullptr, 0.f, workspace);
+  hipLaunchKernelGGL(bn_finish_stats_kernel, dim3(ceil_div(c, 8)), dim3(256), 0, s, workspace, g.parts, c, (int)npix, eps,
+                     momentum, mean, rstd, run_mean, run_var, num_batches_tracked);
+  int per;
+  const int nb = bn_apply_grid(npix, c, &per);
+  hipLaunchKernelGGL(bn_apply_kernel<0>, dim3(nb), dim3(256), 0, s, (int)npix, c, per, z, mean, rstd, 0.f, gamma, beta, act, slope,
+                     y);
   return check_launch("bn_forward");
-}
-
-__global__ void bn_inference_kernel(long npix, int c, const uint16_t* __restrict__ z, const float* __restrict__ rm,
-                                    const float* __restrict__ rv, float eps, const float* __restrict__ gamma,
-                                    const float* __restrict__ beta, int act, float slope, uint16_t* __restrict__ y) {
-  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int groups = c / 8;
-  if (idx >= npix * groups) return;
-  const long p = idx / groups;
-  const int c0 = (int)(idx % groups) * 8;
-  float f[8];
-  unpack8(*(const uint4*)(z + p * c + c0), f);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int ch = c0 + i;
-    float v = (f[i] - rm[ch]) * rsqrtf(rv[ch] + eps) * gamma[ch] + beta[ch];
-    f[i] = act_apply(v, act, slope);
-  }
-  *(uint4*)(y + p * c + c0) = pack8(f);
 }
 
 extern "C" int climsr_bn_inference(const uint16_t* z, int64_t npix, int c, const float* run_mean, const float* run_var, float eps,
                                    const float* gamma, const float* beta, int act, float slope, uint16_t* y, void* stream) {
-  if (!z || !run_mean || !run_var || !gamma || !beta || !y || c % 8) {
+  if (!z || !run_mean || !run_var || !gamma || !beta || !y || !bn_shape_ok(npix, c)) {
     set_error("bn_inference: bad args");
     return CLIMSR_EINVAL;
   }
-  long total = (long)npix * (c / 8);
-  hipLaunchKernelGGL(bn_inference_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, (long)npix, c, z, run_mean,
-                     run_var, eps, gamma, beta, act, slope, y);
+  int per;
+  const int nb = bn_apply_grid(npix, c, &per);
+  hipLaunchKernelGGL(bn_apply_kernel<1>, dim3(nb), dim3(256), 0, (hipStream_t)stream, (int)npix, c, per, z, run_mean, run_var, eps,
+                     gamma, beta, act, slope, y);
   return check_launch("bn_inference");
 }
 
 extern "C" int climsr_bn_backward(const float* da, const uint16_t* a, const uint16_t* z, int64_t npix, int c, const float* mean,
                                   const float* rstd, const float* gamma, float slope, float out_slope, double* workspace, float* coef,
                                   float* dgamma, float* dbeta, int accumulate, uint16_t* dz, void* stream) {
-  if (!da || !a || !z || !mean || !rstd || !gamma || !workspace || !coef || !dz || c % 8 || c > 2048) {
+  if (!da || !a || !z || !mean || !rstd || !gamma || !workspace || !coef || !dz || !bn_shape_ok(npix, c)) {
     set_error("bn_backward: bad args");
     return CLIMSR_EINVAL;
   }
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(bn_partial_kernel, dim3(BN_BLOCKS), dim3(256), 256 * 16 * sizeof(double), s, (long)npix, c, z, da, a, mean,
-                     rstd, slope, 1, workspace);
-  hipLaunchKernelGGL(bn_bwd_finish_kernel, dim3(ceil_div(c, 256)), dim3(256), 0, s, workspace, BN_BLOCKS, c, (long)npix, gamma,
-                     rstd, dgamma, dbeta, accumulate, coef);
-  long total = (long)npix * (c / 8);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, s, (long)npix, c, da, a, z, mean, rstd, coef,
-                     slope, out_slope, dz);
+  const BnGrid g = bn_grid(npix, c);
+  hipLaunchKernelGGL(bn_stats_kernel<1>, dim3(g.parts), dim3(256), 0, s, (int)npix, c, g.per_blk, z, da, a, mean, rstd, slope,
+                     workspace);
+  hipLaunchKernelGGL(bn_bwd_finish_kernel, dim3(ceil_div(c, 8)), dim3(256), 0, s, workspace, g.parts, c, (int)npix, gamma, rstd,
+                     dgamma, dbeta, accumulate, coef);
+  int per;
+  const int nb = bn_apply_grid(npix, c, &per);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(nb), dim3(256), 0, s, (int)npix, c, per, da, a, z, mean, rstd, coef, slope, out_slope,
+                     dz);
   return check_launch("bn_backward");
 }
 

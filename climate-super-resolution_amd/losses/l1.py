@@ -6,7 +6,8 @@ Forward: deterministic two-pass reduction (fp64 partials) in libclimsr_hip; back
 import torch
 
 from .. import _lib
-from .._lib import check, ptr
+from .._lib import ptr
+from ..ops import _launch
 
 
 class _L1Fn(torch.autograd.Function):
@@ -17,7 +18,8 @@ class _L1Fn(torch.autograd.Function):
         assert a.shape == b.shape and a.is_cuda
         ws = torch.empty(1024, dtype=torch.float64, device=a.device)
         out = torch.empty((), dtype=torch.float32, device=a.device)
-        check(_lib.load().climsr_l1_loss(ptr(a), ptr(b), a.numel(), ptr(ws), ptr(out), _lib.stream_ptr()), "l1_loss")
+        _launch("l1_loss", lambda: _lib.load().climsr_l1_loss(ptr(a), ptr(b), a.numel(), ptr(ws), ptr(out), _lib.stream_ptr()),
+                nbytes=8 * a.numel())
         ctx.save_for_backward(a, b)
         return out
 
@@ -28,10 +30,12 @@ class _L1Fn(torch.autograd.Function):
         ga = torch.empty_like(a) if ctx.needs_input_grad[0] else None
         gb = None
         if ga is not None:
-            check(_lib.load().climsr_l1_loss_grad(ptr(a), ptr(b), a.numel(), ptr(g), ptr(ga), _lib.stream_ptr()), "l1_grad")
+            _launch("l1_grad", lambda: _lib.load().climsr_l1_loss_grad(ptr(a), ptr(b), a.numel(), ptr(g), ptr(ga), _lib.stream_ptr()),
+                    nbytes=12 * a.numel())
         if ctx.needs_input_grad[1]:
             gb = torch.empty_like(b)
-            check(_lib.load().climsr_l1_loss_grad(ptr(b), ptr(a), b.numel(), ptr(g), ptr(gb), _lib.stream_ptr()), "l1_grad")
+            _launch("l1_grad", lambda: _lib.load().climsr_l1_loss_grad(ptr(b), ptr(a), b.numel(), ptr(g), ptr(gb), _lib.stream_ptr()),
+                    nbytes=12 * b.numel())
         return ga, gb
 
 

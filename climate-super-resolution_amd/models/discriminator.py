@@ -95,7 +95,6 @@ class _PlainDEngine:
         ops.nchw_to_nhwc(x.contiguous().float(), a, cpad, 0)
         cs, hh, ww = cpad, h, w
         saved = []
-        bnws = self._scr("bnws", (256 * 2 * 512,), torch.float64, dev)
         for L in self.layers:
             plan = L["plan"]
             if L["rpad"]:
@@ -121,9 +120,9 @@ class _PlainDEngine:
                 npix = n * oh * ow
                 if d.training:
                     mean, rstd = _f32((c,), dev), _f32((c,), dev)
-                    ops.bn_forward(t, npix, c, bn.weight, bn.bias, mean, rstd, out, bnws, bn.running_mean, bn.running_var,
-                                   act=ACT_NONE, eps=bn.eps, momentum=bn.momentum)
-                    ops.increment_i64(bn.num_batches_tracked)
+                    ops.bn_forward(t, npix, c, bn.weight, bn.bias, mean, rstd, out, ops.bn_workspace(npix, c, self.scratch, dev),
+                                   bn.running_mean, bn.running_var, act=ACT_NONE, eps=bn.eps, momentum=bn.momentum,
+                                   num_batches_tracked=bn.num_batches_tracked)
                     rec.update(mean=mean, rstd=rstd)
                 else:
                     ops.bn_inference(t, npix, c, bn.running_mean, bn.running_var, bn.weight, bn.bias, out, act=ACT_NONE, eps=bn.eps)
@@ -179,7 +178,6 @@ class _PlainDEngine:
         hh, ww, c = sv["hh"], sv["ww"], sv["c"]
         da = _f32((n, hh, ww, c), dev)
         ops.adaptive_pool_bwd(dp, n, hh, ww, c, hh, ww, da)
-        bnws = self._scr("bnws", (256 * 2 * 512,), torch.float64, dev)
         coef = self._scr("bncoef", (3 * 512,), torch.float32, dev)
         dx = None
         for li in reversed(range(len(self.layers))):
@@ -191,7 +189,7 @@ class _PlainDEngine:
             cz = (c + 7) // 8 * 8
             dz = _bf16((n, oh, ow, cz), dev)
             if bn is not None:  # d(BN input) through the LeakyReLU that produced it
-                ops.bn_backward(da, R["t"], R["t"], npix, c, R["mean"], R["rstd"], bn.weight, bnws, coef,
+                ops.bn_backward(da, R["t"], R["t"], npix, c, R["mean"], R["rstd"], bn.weight, ops.bn_workspace(npix, c, self.scratch, dev), coef,
                                 bn.weight.grad if need_w else None, bn.bias.grad if need_w else None, acc, dz, slope=1.0,
                                 out_slope=slope)
             elif slope is not None:

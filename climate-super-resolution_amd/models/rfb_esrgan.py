@@ -82,7 +82,6 @@ class _DEngine:
         a_prev, cs_prev, hh, ww = x8, cpad, h, w
         saved = []
         training = d.training
-        bnws = self._scr("bnws", (256 * 2 * 512,), torch.float64, dev)
         for conv, bn, plan in self.layers:
             oh, ow = plan.out_hw(hh, ww)
             c = plan.cout
@@ -97,9 +96,9 @@ class _DEngine:
                 npix = n * oh * ow
                 if training:
                     mean, rstd = _f32((c,), dev), _f32((c,), dev)
-                    ops.bn_forward(z, npix, c, bn.weight, bn.bias, mean, rstd, a, bnws, bn.running_mean, bn.running_var,
-                                   eps=bn.eps, momentum=bn.momentum)
-                    ops.increment_i64(bn.num_batches_tracked)
+                    ops.bn_forward(z, npix, c, bn.weight, bn.bias, mean, rstd, a, ops.bn_workspace(npix, c, self.scratch, dev),
+                                   bn.running_mean, bn.running_var, eps=bn.eps, momentum=bn.momentum,
+                                   num_batches_tracked=bn.num_batches_tracked)
                 else:
                     mean = rstd = None
                     ops.bn_inference(z, npix, c, bn.running_mean, bn.running_var, bn.weight, bn.bias, a, eps=bn.eps)
@@ -150,7 +149,6 @@ class _DEngine:
         hh, ww, c = sv["hh"], sv["ww"], sv["c"]
         da = _f32((n, hh, ww, c), dev)
         ops.adaptive_pool_bwd(dp, n, hh, ww, c, POOL, POOL, da)
-        bnws = self._scr("bnws", (256 * 2 * 512,), torch.float64, dev)
         coef = self._scr("bncoef", (3 * 512,), torch.float32, dev)
         dx = None
         for li in reversed(range(len(self.layers))):
@@ -161,7 +159,7 @@ class _DEngine:
             cz = (c + 7) // 8 * 8
             dz = _bf16((n, oh, ow, cz), dev)
             if bn is not None:
-                ops.bn_backward(da, L["a"], L["z"], npix, c, L["mean"], L["rstd"], bn.weight, bnws, coef,
+                ops.bn_backward(da, L["a"], L["z"], npix, c, L["mean"], L["rstd"], bn.weight, ops.bn_workspace(npix, c, self.scratch, dev), coef,
                                 bn.weight.grad if need_w else None, bn.bias.grad if need_w else None, acc, dz)
             else:
                 ops.act_grad(npix, c, da, c, 0, L["a"], c, 0, ACT_LRELU, dz, cz)

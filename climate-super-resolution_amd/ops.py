@@ -29,27 +29,6 @@ def round_up(a: int, b: int) -> int:
 # PROFILER(kernel_name, algorithmic_flops, launch_fn, tag, algorithmic_bytes); must call launch_fn() exactly
 # once.  algorithmic_bytes = every operand read once and every result written once (no halo re-reads).
 PROFILER = None
-_NO_CI1 = os.environ.get("CLIMSR_NO_CI1") == "1"  # A/B switch: single-output dgrads through the implicit GEMM
-
-
-def wgrad_kernel_name(out_c: int, ks: int, ci4: bool = False, cin: int = 0, stride: int = 1, pad: int = 1, npx: int = 0) -> str:
-    """Mirrors climsr_conv2d_wgrad's dispatch (profiler labels only); npx = output pixels (n * h * w)."""
-    if ks == 1 and stride == 1 and pad == 0 and cin == 64 and out_c % 16 == 0 and out_c <= 64:
-        return f"conv_wgrad_pt_kernel<{out_c // 16}>"
-    if out_c == 1 and stride == 1 and ks in (3, 5) and pad == ks // 2 and cin % 16 == 0 and cin <= 64:
-        return f"conv_wgrad_co1m_kernel<{ks}, {cin // 16}>"
-    if ks == 3 and stride == 1 and pad == 1 and out_c % 64 == 0 and cin % 64 == 0 and cin >= 64:
-        return f"conv_wgrad64_kernel<{2 if npx >= (1 << 20) else 1}>"  # 8-wave tap split at >= 1M pixels
-    rows = round_up(out_c, 16)
-    ntc = 4 if rows >= 64 else (2 if rows >= 32 else 1)
-    k2 = ks * ks
-    if ci4:
-        tb = 3 if (k2 + 3) // 4 <= 3 else 7
-    else:
-        tb = 9 if k2 >= 9 else (5 if k2 >= 5 else 1)
-        if k2 == 25:
-            tb = 5
-    return f"conv_wgrad_kernel<{ntc}, {tb}, {int(ci4)}>"
 
 
 def _kname(d, bias, ep) -> str:
@@ -64,6 +43,14 @@ def _run(name, flops, fn, tag="", nbytes=0):
         fn()
     else:
         PROFILER(name, flops, fn, tag, nbytes)
+
+
+def _launch(label: str, call, nbytes: int = 0, flops: int = 0) -> None:
+    """Run one C-ABI entry point (``call`` returns its status) under the launch observer, raising on error."""
+    if PROFILER is None:
+        check(call(), label)
+    else:
+        PROFILER(label, flops, lambda: check(call(), label), label, nbytes)
 
 
 def _esize(t: Optional[torch.Tensor]) -> int:
@@ -111,11 +98,11 @@ class ConvPlan:
         s = _lib.stream_ptr() if stream is None else stream
         w = self.weight
         assert w is not None and w.dtype == torch.float32 and w.is_contiguous()
-        check(lib.climsr_pack_conv_weight(ptr(w), self.cout, self.cin, self.cin_real, self.cout, self.ks, self.cc, 0,
-                                          ptr(self.wpk), s), f"pack {self.name}")
+        _launch(f"pack {self.name}", lambda: lib.climsr_pack_conv_weight(ptr(w), self.cout, self.cin, self.cin_real, self.cout, self.ks, self.cc, 0,
+                                          ptr(self.wpk), s))
         if self.wpk_t is not None:
-            check(lib.climsr_pack_conv_weight(ptr(w), self.cout_t, self.cin_t, self.cout, self.cout_t, self.ks, self.cc_t, 1,
-                                              ptr(self.wpk_t), s), f"pack_t {self.name}")
+            _launch(f"pack_t {self.name}", lambda: lib.climsr_pack_conv_weight(ptr(w), self.cout_t, self.cin_t, self.cout, self.cout_t, self.ks, self.cc_t, 1,
+                                              ptr(self.wpk_t), s))
 
     def pack_descs(self):
         out = [PackDesc(ptr(self.weight), ptr(self.wpk), self.cout, self.cin, self.cin_real, self.cout, self.ks, self.cc, 0, 0)]
@@ -167,11 +154,12 @@ class ConvPlan:
         ct = self.cout_t if cout_t is None else cout_t
         if (self.cout == 1 and self.stride == 1 and self.ks in (3, 5) and self.pad == self.ks // 2 and g.dtype == torch.bfloat16
                 and not down2 and aux is None and act in (ACT_NONE, ACT_LRELU_BWD, ACT_RELU_BWD) and ct == self.cin_real
-                and ct in (32, 64) and not _NO_CI1):
+                and ct in (32, 64)):
             # one output channel: its data gradient is a 1 -> C stencil (climsr_dgrad_single_output), not a GEMM
             hw = n * out_h * out_w
             nbytes = hw * 2 + hw * ct * 2 * (2 if res1 is not None else 1)
-            _run(f"dgrad_ci1_kernel<{self.ks}>", 2 * ct * self.ks * self.ks * hw, lambda: check(
+            kn = _lib.load().climsr_dgrad_single_output_kernel(self.ks, ct, act).decode() if PROFILER is not None else ""
+            _run(kn, 2 * ct * self.ks * self.ks * hw, lambda: check(
                 _lib.load().climsr_dgrad_single_output(n, out_h, out_w, self.ks, self.pad, ptr(dz), dz_cs, 0, ptr(self.weight), ct, act,
                                                        0.2, ptr(res1), res1_cs, res1_co, ptr(g), g_cs, g_co, _lib.stream_ptr()),
                 f"conv dgrad {self.name}"), "dgrad " + self.name, nbytes)
@@ -222,13 +210,13 @@ class ConvPlan:
         has_b = self.bias is not None and self.gb is not None
         flops = 2 * self.cin_real * self.cout * self.ks * self.ks * n * d.out_h * d.out_w
         nbytes = n * in_h * in_w * self.cin_real * 2 + n * d.out_h * d.out_w * self.cout * 2 + self.cout * self.cin_real * self.ks ** 2 * 4
-        _run(wgrad_kernel_name(self.cout, self.ks, self.cin_w == 4, self.cin_w, self.stride, self.pad, n * d.out_h * d.out_w), flops,
+        _run(lib.climsr_conv2d_wgrad_kernel(ctypes.byref(d)).decode() if PROFILER is not None else "", flops,
              lambda: check(
             lib.climsr_conv2d_wgrad(ctypes.byref(d), ptr(x), ptr(dz), dz_cs, ptr(part), ptr(bpart) if has_b else None, ns,
                                     _lib.stream_ptr()), f"conv wgrad {self.name}"), "wgrad " + self.name, nbytes)
-        check(lib.climsr_conv2d_wgrad_reduce(ptr(part), ptr(bpart) if has_b else None, ns, self.cout, self.cin_real, cw,
+        _launch(f"wgrad reduce {self.name}", lambda: lib.climsr_conv2d_wgrad_reduce(ptr(part), ptr(bpart) if has_b else None, ns, self.cout, self.cin_real, cw,
                                              self.ks, ptr(self.gw), ptr(self.gb) if has_b else None,
-                                             1 if accumulate else 0, s), f"wgrad reduce {self.name}")
+                                             1 if accumulate else 0, s))
 
 
 class GroupedWgrad:
@@ -272,13 +260,12 @@ class GroupedWgrad:
         s = _lib.stream_ptr()
         flops = sum(2 * p.cin_real * p.cout * 9 for p in self.plans) * n * in_h * in_w
         nbytes = n * in_h * in_w * (self.in_c + self.out_c) * 2 + sum(p.cout * p.cin_real * 9 * 4 for p in self.plans)
-        _run(f"conv_wgrad64_kernel<{2 if n * in_h * in_w >= (1 << 20) else 1}>", flops, lambda: check(
+        _run(lib.climsr_conv2d_wgrad_kernel(ctypes.byref(d)).decode() if PROFILER is not None else "", flops, lambda: check(
             lib.climsr_conv2d_wgrad(ctypes.byref(d), ptr(x), ptr(dz), dz_cs, ptr(part), ptr(bpart), ns, _lib.stream_ptr()),
             f"grouped wgrad {self.name}"), "wgrad " + self.name, nbytes)
         tab = self._table(x.device)
-        check(lib.climsr_conv2d_wgrad_reduce_rows(ptr(part), ptr(bpart), ns, self.out_c, self.in_c * 9, 3, ptr(tab),
-                                                  len(self.plans), self.max_elems, 1 if accumulate else 0, s),
-              f"grouped wgrad reduce {self.name}")
+        _launch(f"grouped wgrad reduce {self.name}", lambda: lib.climsr_conv2d_wgrad_reduce_rows(ptr(part), ptr(bpart), ns, self.out_c, self.in_c * 9, 3, ptr(tab),
+                                                  len(self.plans), self.max_elems, 1 if accumulate else 0, s))
 
 
 class Workspace:
@@ -295,31 +282,30 @@ class Workspace:
 
 def act_grad(npix: int, c_real: int, g: torch.Tensor, g_cs: int, g_co: int, y: Optional[torch.Tensor], y_cs: int, y_co: int,
              act: int, dz: torch.Tensor, dz_cs: int, scale: float = 1.0, slope: float = 0.2) -> None:
-    check(_lib.load().climsr_act_grad(npix, c_real, ptr(g), g_cs, g_co, ptr(y), y_cs, y_co, act, slope, scale, ptr(dz), dz_cs,
-                                      _lib.stream_ptr()), "act_grad")
+    _launch("act_grad", lambda: _lib.load().climsr_act_grad(npix, c_real, ptr(g), g_cs, g_co, ptr(y), y_cs, y_co, act, slope, scale, ptr(dz), dz_cs,
+                                      _lib.stream_ptr()))
 
 
 def axpby(npix: int, c: int, a: float, x: Optional[torch.Tensor], x_cs: int, x_co: int, b: float, y: torch.Tensor, y_cs: int,
           y_co: int) -> None:
-    check(_lib.load().climsr_axpby_f32(npix, c, a, ptr(x), x_cs, x_co, b, ptr(y), y_cs, y_co, _lib.stream_ptr()), "axpby")
+    _launch("axpby", lambda: _lib.load().climsr_axpby_f32(npix, c, a, ptr(x), x_cs, x_co, b, ptr(y), y_cs, y_co, _lib.stream_ptr()))
 
 
 def nchw_to_nhwc(src: torch.Tensor, dst: torch.Tensor, cs: int, co: int) -> None:
     n, c, h, w = src.shape
     assert src.dtype == torch.float32 and src.is_contiguous()
-    check(_lib.load().climsr_nchw_to_nhwc_bf16(ptr(src), n, c, h, w, ptr(dst), cs, co, _lib.stream_ptr()), "nchw_to_nhwc")
+    _launch("nchw_to_nhwc", lambda: _lib.load().climsr_nchw_to_nhwc_bf16(ptr(src), n, c, h, w, ptr(dst), cs, co, _lib.stream_ptr()))
 
 
 def nhwc_to_nchw(src: torch.Tensor, n: int, c: int, h: int, w: int, cs: int, co: int, dst: torch.Tensor) -> None:
     is_bf16 = 1 if src.dtype == torch.bfloat16 else 0
-    check(_lib.load().climsr_nhwc_to_nchw_f32(ptr(src), is_bf16, n, c, h, w, cs, co, ptr(dst), _lib.stream_ptr()),
-          "nhwc_to_nchw")
+    _launch("nhwc_to_nchw", lambda: _lib.load().climsr_nhwc_to_nchw_f32(ptr(src), is_bf16, n, c, h, w, cs, co, ptr(dst), _lib.stream_ptr()))
 
 
 def rdb_bwd_init(npix: int, nf: int, dc: int, gx: torch.Tensor, gy: torch.Tensor, gskip: torch.Tensor, dz: torch.Tensor, a_o: float,
                  save_skip: bool, add_skip: bool) -> None:
-    check(_lib.load().climsr_rdb_bwd_init(npix, nf, dc, ptr(gx), ptr(gy), ptr(gskip), ptr(dz), a_o, int(save_skip), int(add_skip),
-                                          _lib.stream_ptr()), "rdb_bwd_init")
+    _launch("rdb_bwd_init", lambda: _lib.load().climsr_rdb_bwd_init(npix, nf, dc, ptr(gx), ptr(gy), ptr(gskip), ptr(dz), a_o, int(save_skip), int(add_skip),
+                                          _lib.stream_ptr()))
 
 
 class BatchedPacker:
@@ -343,8 +329,7 @@ class BatchedPacker:
             self.max_elems = max(self.max_elems, 16 * 9 * d.cc)
 
     def run(self):
-        check(_lib.load().climsr_pack_conv_weights_batched(ptr(self.table), self.n, self.max_elems, _lib.stream_ptr()),
-              "pack batched")
+        _launch("pack batched", lambda: _lib.load().climsr_pack_conv_weights_batched(ptr(self.table), self.n, self.max_elems, _lib.stream_ptr()))
 
 
 class PullPlan(ConvPlan):
@@ -442,8 +427,7 @@ class PullPacker:
         self.max_elems = max([p.rows * p.kpk for p in pulls] + [16 * 9 * d.cc for d in extra])
 
     def run(self):
-        check(_lib.load().climsr_pack_pull_weights_batched(ptr(self.table), self.n, self.max_elems, _lib.stream_ptr()),
-              "pack pull batched")
+        _launch("pack pull batched", lambda: _lib.load().climsr_pack_pull_weights_batched(ptr(self.table), self.n, self.max_elems, _lib.stream_ptr()))
 
 
 # ------------------------------------------------------------------ discriminator / VGG / GAN-loss ops
@@ -451,37 +435,53 @@ def _L():
     return _lib.load()
 
 
+def bn_workspace(npix: int, c: int, cache: dict, dev) -> torch.Tensor:
+    """fp64 partial-sum scratch for bn_forward / bn_backward (grow-only, kept in ``cache``)."""
+    need = int(_L().climsr_bn_workspace_doubles(npix, c))
+    if need <= 0:
+        raise RuntimeError(f"bn: unsupported shape npix={npix} c={c}")
+    t = cache.get("bnws")
+    if t is None or t.numel() < need or t.device != dev:
+        t = torch.empty(max(need, 1 << 16), dtype=torch.float64, device=dev)
+        cache["bnws"] = t
+    return t
+
+
 def bn_forward(z, npix, c, gamma, beta, mean, rstd, y, ws, run_mean=None, run_var=None, act=ACT_LRELU, slope=0.2, eps=1e-5,
-               momentum=0.1):
-    check(_L().climsr_bn_forward(ptr(z), npix, c, ptr(gamma), ptr(beta), act, slope, eps, momentum, ptr(ws), ptr(mean), ptr(rstd),
-                                 ptr(run_mean), ptr(run_var), ptr(y), _lib.stream_ptr()), "bn_forward")
+               momentum=0.1, num_batches_tracked=None):
+    _run("bn_forward", 0, lambda: check(
+        _L().climsr_bn_forward(ptr(z), npix, c, ptr(gamma), ptr(beta), act, slope, eps, momentum, ptr(ws), ptr(mean), ptr(rstd),
+                               ptr(run_mean), ptr(run_var), ptr(num_batches_tracked), ptr(y), _lib.stream_ptr()), "bn_forward"),
+         "bn_forward", npix * c * 6)
 
 
 def bn_inference(z, npix, c, run_mean, run_var, gamma, beta, y, act=ACT_LRELU, slope=0.2, eps=1e-5):
-    check(_L().climsr_bn_inference(ptr(z), npix, c, ptr(run_mean), ptr(run_var), eps, ptr(gamma), ptr(beta), act, slope, ptr(y),
-                                   _lib.stream_ptr()), "bn_inference")
+    _run("bn_inference", 0, lambda: check(
+        _L().climsr_bn_inference(ptr(z), npix, c, ptr(run_mean), ptr(run_var), eps, ptr(gamma), ptr(beta), act, slope, ptr(y),
+                                 _lib.stream_ptr()), "bn_inference"), "bn_inference", npix * c * 4)
 
 
 def bn_backward(da, a, z, npix, c, mean, rstd, gamma, ws, coef, dgamma, dbeta, accumulate, dz, slope=0.2, out_slope=1.0):
-    check(_L().climsr_bn_backward(ptr(da), ptr(a), ptr(z), npix, c, ptr(mean), ptr(rstd), ptr(gamma), slope, out_slope, ptr(ws),
-                                  ptr(coef), ptr(dgamma), ptr(dbeta), int(accumulate), ptr(dz), _lib.stream_ptr()), "bn_backward")
+    _run("bn_backward", 0, lambda: check(
+        _L().climsr_bn_backward(ptr(da), ptr(a), ptr(z), npix, c, ptr(mean), ptr(rstd), ptr(gamma), slope, out_slope, ptr(ws),
+                                ptr(coef), ptr(dgamma), ptr(dbeta), int(accumulate), ptr(dz), _lib.stream_ptr()), "bn_backward"),
+         "bn_backward", npix * c * 18)
 
 
 def reflect_pad1(x, n, h, w, cs, y):
-    check(_L().climsr_reflect_pad1_bf16(ptr(x), n, h, w, cs, ptr(y), _lib.stream_ptr()), "reflect_pad1")
+    _launch("reflect_pad1", lambda: _L().climsr_reflect_pad1_bf16(ptr(x), n, h, w, cs, ptr(y), _lib.stream_ptr()))
 
 
 def reflect_pad1_bwd(gp, n, h, w, c, g):
-    check(_L().climsr_reflect_pad1_bwd_f32(ptr(gp), n, h, w, c, ptr(g), _lib.stream_ptr()), "reflect_pad1_bwd")
+    _launch("reflect_pad1_bwd", lambda: _L().climsr_reflect_pad1_bwd_f32(ptr(gp), n, h, w, c, ptr(g), _lib.stream_ptr()))
 
 
 def adaptive_pool_fwd(x, n, h, w, c, oh, ow, out, out_t=None, n_pad=0):
-    check(_L().climsr_adaptive_pool_fwd(ptr(x), n, h, w, c, oh, ow, ptr(out), ptr(out_t), n_pad, _lib.stream_ptr()),
-          "adaptive_pool_fwd")
+    _launch("adaptive_pool_fwd", lambda: _L().climsr_adaptive_pool_fwd(ptr(x), n, h, w, c, oh, ow, ptr(out), ptr(out_t), n_pad, _lib.stream_ptr()))
 
 
 def adaptive_pool_bwd(dp, n, h, w, c, oh, ow, dx):
-    check(_L().climsr_adaptive_pool_bwd(ptr(dp), n, h, w, c, oh, ow, ptr(dx), _lib.stream_ptr()), "adaptive_pool_bwd")
+    _launch("adaptive_pool_bwd", lambda: _L().climsr_adaptive_pool_bwd(ptr(dp), n, h, w, c, oh, ow, ptr(dx), _lib.stream_ptr()))
 
 
 def linear_fwd(x, w, bias, n, k, o, y, ws, act=ACT_NONE, slope=0.2):
@@ -503,30 +503,30 @@ def linear_wgrad(dy_t, x_t, n_pad, k, o, dw, accumulate):
 
 
 def d_head_fwd(h, w2, b2, n, o, s, sigmoid=True):
-    check(_L().climsr_d_head_fwd(ptr(h), ptr(w2), ptr(b2), n, o, int(sigmoid), ptr(s), _lib.stream_ptr()), "d_head_fwd")
+    _launch("d_head_fwd", lambda: _L().climsr_d_head_fwd(ptr(h), ptr(w2), ptr(b2), n, o, int(sigmoid), ptr(s), _lib.stream_ptr()))
 
 
 def d_head_bwd(h, s, ds, w2, n, o, n_pad, dw2, db2, db0, accumulate, du0, du0_t, slope=0.2, sigmoid=True):
-    check(_L().climsr_d_head_bwd(ptr(h), ptr(s), ptr(ds), ptr(w2), n, o, n_pad, slope, int(sigmoid), ptr(dw2), ptr(db2), ptr(db0),
-                                 int(accumulate), ptr(du0), ptr(du0_t), _lib.stream_ptr()), "d_head_bwd")
+    _launch("d_head_bwd", lambda: _L().climsr_d_head_bwd(ptr(h), ptr(s), ptr(ds), ptr(w2), n, o, n_pad, slope, int(sigmoid), ptr(dw2), ptr(db2), ptr(db0),
+                                 int(accumulate), ptr(du0), ptr(du0_t), _lib.stream_ptr()))
 
 
 def relativistic_bce(s_real, s_fake, n, t_rf, t_fr, loss=None, gscale=None, g_real=None, g_fake=None):
-    check(_L().climsr_relativistic_bce(ptr(s_real), ptr(s_fake), n, t_rf, t_fr, ptr(loss), ptr(gscale), ptr(g_real), ptr(g_fake),
-                                       _lib.stream_ptr()), "relativistic_bce")
+    _launch("relativistic_bce", lambda: _L().climsr_relativistic_bce(ptr(s_real), ptr(s_fake), n, t_rf, t_fr, ptr(loss), ptr(gscale), ptr(g_real), ptr(g_fake),
+                                       _lib.stream_ptr()))
 
 
 def maxpool2(x, n, h, w, c, y):
-    check(_L().climsr_maxpool2_bf16(ptr(x), n, h, w, c, ptr(y), _lib.stream_ptr()), "maxpool2")
+    _launch("maxpool2", lambda: _L().climsr_maxpool2_bf16(ptr(x), n, h, w, c, ptr(y), _lib.stream_ptr()))
 
 
 def l1_bf16(a, b, n, ws, out):
-    check(_L().climsr_l1_loss_bf16(ptr(a), ptr(b), n, ptr(ws), ptr(out), _lib.stream_ptr()), "l1_bf16")
+    _launch("l1_bf16", lambda: _L().climsr_l1_loss_bf16(ptr(a), ptr(b), n, ptr(ws), ptr(out), _lib.stream_ptr()))
 
 
 def f32_to_bf16(x, y):
-    check(_L().climsr_f32_to_bf16(ptr(x), x.numel(), ptr(y), _lib.stream_ptr()), "f32_to_bf16")
+    _launch("f32_to_bf16", lambda: _L().climsr_f32_to_bf16(ptr(x), x.numel(), ptr(y), _lib.stream_ptr()))
 
 
 def increment_i64(t):
-    check(_L().climsr_increment_i64(ptr(t), _lib.stream_ptr()), "increment_i64")
+    _launch("increment_i64", lambda: _L().climsr_increment_i64(ptr(t), _lib.stream_ptr()))

@@ -150,6 +150,11 @@ int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, const uint16_t
 /* Name of the kernel climsr_conv2d_fwd launches for these arguments (as rocprof reports it; "" if invalid).
  * Launches nothing; used to label per-kernel timings and PMC traffic. */
 const char* climsr_conv2d_fwd_kernel(const ClimsrConvDesc* d, const float* bias, const ClimsrEpilogue* ep);
+/* Dry-run kernel-name queries (profiler labels straight from the dispatch; nothing is launched): the weight-gradient
+ * kernel climsr_conv2d_wgrad would launch for d (with climsr_conv2d_wgrad_splits(d) splits), and the data-gradient
+ * stencil climsr_dgrad_single_output would launch for (ks, c, act).  "" if the arguments are unsupported. */
+const char* climsr_conv2d_wgrad_kernel(const ClimsrConvDesc* d);
+const char* climsr_dgrad_single_output_kernel(int ks, int c, int act);
 
 /* Weight (+ bias) gradient partials (d->in_c may be 4 = "at most 4 real input channels", which packs
  * 4 taps x 4 channels per MFMA fragment; the input buffer still has a multiple-of-8 channel stride): partial[split][out_c_pad16][in_c*ks*ks] (OIHW order) and
@@ -223,20 +228,23 @@ int climsr_adamw_step(int64_t n, float* p, const float* g, float* m, float* v, c
 
 /* ---------------- discriminator / perceptual loss / GAN loss (disc.hip) ---------------- */
 
-/* nn.BatchNorm2d in train mode over z [npix][c] (bf16 NHWC; c % 8 == 0, c <= 2048), fused with the
- * following activation: y = act(gamma*(z-mean)*rstd + beta).  Saves mean/rstd for the backward and
- * updates run_mean/run_var (momentum, unbiased var) when non-NULL (rfb_esrgan.py:32-50 BN + LeakyReLU).
- * workspace >= 256*2*c doubles. */
+/* nn.BatchNorm2d in train mode over z [npix][c] (bf16 NHWC; c % 8 == 0, c <= 2048, npix*c < 2^31), fused with
+ * the following activation: y = act(gamma*(z-mean)*rstd + beta).  Saves mean/rstd for the backward, updates
+ * run_mean/run_var (momentum, unbiased var) and increments *num_batches_tracked when non-NULL
+ * (rfb_esrgan.py:32-50 BN + LeakyReLU).  workspace >= climsr_bn_workspace_doubles(npix, c) doubles
+ * (per-block fp64 partial sums; the reduction order is fixed, so results are deterministic). */
+int64_t climsr_bn_workspace_doubles(int64_t npix, int c);
 int climsr_bn_forward(const uint16_t* z, int64_t npix, int c, const float* gamma, const float* beta, int act, float slope,
                       float eps, float momentum, double* workspace, float* mean, float* rstd, float* run_mean, float* run_var,
-                      uint16_t* y, void* stream);
+                      int64_t* num_batches_tracked, uint16_t* y, void* stream);
 /* Eval-mode BN (running statistics) + activation (nn.BatchNorm2d.eval()). */
 int climsr_bn_inference(const uint16_t* z, int64_t npix, int c, const float* run_mean, const float* run_var, float eps,
                         const float* gamma, const float* beta, int act, float slope, uint16_t* y, void* stream);
 /* *p += 1 on the device (BatchNorm num_batches_tracked). */
 int climsr_increment_i64(int64_t* p, void* stream);
 /* Backward of act(BN(z)): da = dL/d(act output) fp32, a = act output (bf16, sign gives lrelu'; slope 1 =
- * no activation), dz (bf16) = BN input gradient; dgamma/dbeta (+)= .  coef >= 3*c floats scratch.
+ * no activation), dz (bf16) = BN input gradient; dgamma/dbeta (+)= .  coef >= 3*c floats scratch;
+ * workspace as for climsr_bn_forward.
  * out_slope != 1: z itself is a LeakyReLU output (plain discriminator, discriminator.py:17-18) and dz is
  * carried through its derivative (z <= 0 -> * out_slope). */
 int climsr_bn_backward(const float* da, const uint16_t* a, const uint16_t* z, int64_t npix, int c, const float* mean,

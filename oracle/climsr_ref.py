@@ -362,8 +362,8 @@ def loss_g(d_fn, vgg_p: Params, hr, sr, factors=LOSS_FACTORS):
     """``GANLightningModule.loss_g`` (pl_gan.py:28-49).  ``d_fn`` is the discriminator callable; it is
     called separately on hr and sr (F8: per-call BN statistics)."""
     n = hr.shape[0]
-    real = torch.ones((n, 1), dtype=hr.dtype)
-    fake = torch.zeros((n, 1), dtype=hr.dtype)
+    real = torch.ones((n, 1), dtype=hr.dtype, device=hr.device)
+    fake = torch.zeros((n, 1), dtype=hr.dtype, device=hr.device)
     score_real = d_fn(hr)
     score_fake = d_fn(sr)
     rf = score_real - score_fake.mean()
@@ -379,8 +379,8 @@ def loss_g(d_fn, vgg_p: Params, hr, sr, factors=LOSS_FACTORS):
 def loss_d(d_fn, hr, sr):
     """``GANLightningModule.loss_d`` (pl_gan.py:51-61)."""
     n = hr.shape[0]
-    real = torch.ones((n, 1), dtype=hr.dtype)
-    fake = torch.zeros((n, 1), dtype=hr.dtype)
+    real = torch.ones((n, 1), dtype=hr.dtype, device=hr.device)
+    fake = torch.zeros((n, 1), dtype=hr.dtype, device=hr.device)
     score_real = d_fn(hr)
     score_fake = d_fn(sr.detach())
     rf = score_real - score_fake.mean()

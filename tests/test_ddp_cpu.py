@@ -120,3 +120,127 @@ def test_overlapped_reducer_gloo_world2():
         assert ok, f"rank {rank}: averaged gradient mismatch"
         assert buckets == [(14, 20), (5, 14), (0, 5)], buckets
         assert second == [(0, 20)], second
+
+
+# ------------------------------------------------------------------ the real modules' flat layouts
+def _real_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from climsr_amd.core.ddp import GradAllReducer, OverlappedGradAllReducer
+        from climsr_amd.models.esrgan import ESRGANGenerator
+        from climsr_amd.models.rfb_esrgan import RFBESRGANDiscriminator
+
+        g = ESRGANGenerator(in_channels=3, out_channels=1, nf=64, nb=11, gc=16, scale_factor=4)
+        d = RFBESRGANDiscriminator(in_channels=1)
+        out = {}
+        for name, net in (("G", g), ("D", d)):
+            net.grads_as_views()
+
+            def rank_grad(r, n=net._flat_grad.numel()):
+                return torch.randn(n, generator=torch.Generator().manual_seed(1000 * r + len(name)))
+
+            want = (rank_grad(0) + rank_grad(1)) / 2
+            # (1) reduce-after-backward: 256 MB buckets (D's 430 MB buffer is 2 buckets)
+            net._flat_grad.copy_(rank_grad(rank))
+            red = GradAllReducer(net)
+            nb_buckets = len(red.buckets)
+            red()
+            ok_bucketed = bool(torch.allclose(net._flat_grad, want, atol=1e-6))
+            # (2) overlapped: the slices the native backwards report (G: RRDB blocks 8/5/2, D: fc.0 + fc.2 first)
+            net._flat_grad.copy_(rank_grad(rank))
+            ov = OverlappedGradAllReducer(net)
+            if name == "G":
+                net.set_grad_ready_hook(ov.ready)
+                los = [net._block_flat_lo(b) for b in net._grad_ready_blocks]
+            else:
+                los = [net._fc_flat_lo()]
+            for lo in los:
+                ov.ready(lo)
+            ov.finish()
+            ok_overlap = bool(torch.allclose(net._flat_grad, want, atol=1e-6))
+            # per-parameter .grad views see the averaged values (fc.0 / conv_first)
+            p = net.fc[0].weight if name == "D" else net.conv_first.weight
+            lo = [off for q_, off, _n in net._flat_index if q_ is p][0]
+            ok_view = bool(torch.equal(p.grad.reshape(-1), net._flat_grad[lo:lo + p.numel()]))
+            out[name] = (ok_bucketed, ok_overlap, ok_view, nb_buckets, list(ov.launched))
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_real_module_layouts():
+    """DDP average on the real FlatParamsMixin layouts of ESRGANGenerator (nb 11, 4.28 M params) and
+    RFBESRGANDiscriminator (107.4 M params): bucketed AVG and the backward-overlapped slices both give the
+    average of the two ranks' gradient buffers, and every parameter's .grad view sees it."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_real_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, out in res:
+        for name, (ok_b, ok_o, ok_v, nbk, launched) in out.items():
+            assert ok_b and ok_o and ok_v, (rank, name)
+        assert out["D"][3] == 2  # 430 MB fp32 gradient in 256 MB buckets
+        g_slices = out["G"][4]
+        assert len(g_slices) == 4 and g_slices[-1][0] == 0 and all(a[0] == b[1] for a, b in zip(g_slices, g_slices[1:]))
+        d_slices = out["D"][4]
+        assert len(d_slices) == 2 and d_slices[0][1] - d_slices[0][0] == 1024 * 100352 + 1024 + 1024 + 1
+
+
+# ------------------------------------------------------------------ bench.py --gpus N launcher
+def test_bench_child_envs():
+    import bench
+
+    envs = bench.child_envs(4, 29555, base={"PATH": "/usr/bin"})
+    assert [e["RANK"] for e in envs] == ["0", "1", "2", "3"]
+    assert [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2", "3"]
+    assert all(e["WORLD_SIZE"] == "4" and e["MASTER_ADDR"] == "127.0.0.1" and e["MASTER_PORT"] == "29555" for e in envs)
+    assert all(e["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and e["PATH"] == "/usr/bin" for e in envs)
+
+
+def test_bench_launcher_fans_out(tmp_path):
+    """bench.launch starts one child per rank with torchrun's variables and returns 0 when all succeed."""
+    import sys
+
+    import bench
+
+    code = ("import os; p = os.path.join(%r, 'rank' + os.environ['RANK']); "
+            "open(p, 'w').write(' '.join(os.environ[k] for k in ('LOCAL_RANK', 'WORLD_SIZE', 'MASTER_ADDR', 'MASTER_PORT')))"
+            % str(tmp_path))
+    assert bench.launch(3, [sys.executable, "-c", code], timeout=60) == 0
+    got = sorted(os.listdir(tmp_path))
+    assert got == ["rank0", "rank1", "rank2"]
+    ports = set()
+    for r in range(3):
+        lr, ws, addr, port = open(tmp_path / f"rank{r}").read().split()
+        assert (lr, ws, addr) == (str(r), "3", "127.0.0.1")
+        ports.add(port)
+    assert len(ports) == 1
+
+
+def test_bench_launcher_propagates_failure():
+    import sys
+
+    import bench
+
+    code = "import os, sys, time; r = int(os.environ['RANK']); sys.exit(3) if r == 1 else time.sleep(30)"
+    t0 = __import__("time").time()
+    assert bench.launch(2, [sys.executable, "-c", code], timeout=60) == 3
+    assert __import__("time").time() - t0 < 20  # the surviving rank was killed, not waited for
+
+
+def test_bench_main_without_world_size_launches(monkeypatch):
+    """`python bench.py --gpus N` (no WORLD_SIZE in the environment) goes through the launcher with N ranks."""
+    import bench
+
+    seen = {}
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(bench, "launch", lambda n, cmd, timeout=None: seen.update(n=n, cmd=cmd) or 0)
+    assert bench.main(["--gpus", "8", "--steps", "3"]) == 0
+    assert seen["n"] == 8 and seen["cmd"][-4:] == ["--gpus", "8", "--steps", "3"]

@@ -1,0 +1,429 @@
+"""GPU parity at the benchmarked shapes (BASELINE configs 2/3: B=32, LR 64 -> HR 256).
+
+Several kernels dispatch only at bench-sized problems: ``conv_wgrad64_kernel<2>`` (8-wave tap split, >= 2^20 output
+pixels: HRconv / upconv2 weight gradients at 256^2, B=32), the 64-way split-K grouped weight gradient of a residual
+dense block at B=32, 64^2 (+ its row-sliced reduction), and ``conv_pw`` walking thousands of persistent XCD-ordered
+tiles at 256^2, B=32.  Each is compared here with a float64 GEMM on the GPU (unfold + matmul, test-only torch ops)
+over the same bf16-rounded operands: the only difference left is the kernels' fp32 accumulation order, bounded by
+``REL`` of the result scale.  The last tests run one whole config-2 step (nb 11, B=32, 64->256) and the config-3
+GAN passes (nb 1, B=32, 64->256) against the oracle (oracle/climsr_ref.py) evaluated in fp32 with torch ops on the
+GPU, within the same envelope as the reference's own AMP training (test_gpu_generator.py)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import climsr_ref as ref
+from tests.helpers import gen_params, rfb_d_params, vgg_params
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+REL = 5e-5  # fp32 accumulation over up to 2^21 products (split-K partials summed in a fixed order)
+
+
+def bf(t):
+    return t.to(torch.bfloat16).to(torch.float32)
+
+
+def nhwc(x, cs=None, co=0):
+    n, c, h, w = x.shape
+    cs = cs or ((c + 7) // 8 * 8)
+    buf = torch.zeros((n, h, w, cs), dtype=torch.bfloat16, device=DEV)
+    buf[..., co:co + c] = x.permute(0, 2, 3, 1).to(torch.bfloat16)
+    return buf
+
+
+def wgrad64(x, dz, ks=3, pad=1, chunk=4):
+    """dW[co][ci*k*k] = sum_px dz[px][co] * im2col(x)[px][ci*k*k] in float64 on the GPU, chunked over images."""
+    out = None
+    for i in range(0, x.shape[0], chunk):
+        cols = F.unfold(x[i:i + chunk].double(), ks, padding=pad)           # [b, ci*k*k, L]
+        d = dz[i:i + chunk].double().flatten(2)                              # [b, co, L]
+        part = torch.einsum("bkl,bcl->ck", cols, d)
+        out = part if out is None else out + part
+    return out
+
+
+def close(got, want, rel=REL, what=""):
+    scale = float(want.abs().max()) + 1e-30
+    err = float((got.double() - want.double()).abs().max())
+    assert err <= rel * scale, f"{what}: max err {err:.3e} vs scale {scale:.3e} (rel {err / scale:.2e})"
+
+
+def plan(cin, cout, ks=3, seed=0):
+    from climsr_amd.ops import ConvPlan
+
+    g = torch.Generator().manual_seed(seed)
+    w = ((torch.rand((cout, cin, ks, ks), generator=g) * 2 - 1) / (cin * ks * ks) ** 0.5).to(DEV)
+    b = ((torch.rand((cout,), generator=g) * 2 - 1) * 0.1).to(DEV)
+    p = ConvPlan(cin, cout, ks, 1, None, "bench-shape")
+    p.bind(w.contiguous(), b)
+    p.pack()
+    return p
+
+
+def test_wgrad64_tap_split_upsampled_at_1m_pixels():
+    """upconv2's weight gradient at the bench shape: x [32,64,128,128] nearest-x2 on load -> 256^2, 2^21 output
+    pixels (>= 2^20 selects conv_wgrad64_kernel<2>)."""
+    from climsr_amd import ops
+
+    n, h = 32, 128
+    p = plan(64, 64)
+    g = torch.Generator(device=DEV).manual_seed(1)
+    x = bf(torch.rand((n, 64, h, h), generator=g, device=DEV) * 2 - 1)
+    dz = bf(torch.rand((n, 64, 2 * h, 2 * h), generator=g, device=DEV) * 2 - 1)
+    p.gw = torch.zeros_like(p.weight)
+    p.gb = torch.zeros_like(p.bias)
+    names = []
+    ops.PROFILER = lambda name, flops, fn, tag="", nbytes=0: (names.append(name), fn())
+    try:
+        p.wgrad(nhwc(x), 64, 0, h, h, nhwc(dz), 64, n, ops.Workspace(), accumulate=False, up=2)
+    finally:
+        ops.PROFILER = None
+    torch.cuda.synchronize()
+    assert "conv_wgrad64_kernel<2>" in names, names
+    xu = F.interpolate(x, scale_factor=2, mode="nearest")
+    close(p.gw.reshape(64, -1), wgrad64(xu, dz), what="upconv2 wgrad")
+    close(p.gb, dz.double().sum((0, 2, 3)), what="upconv2 bias grad")
+
+
+def test_wgrad64_hrconv_accumulate_at_2m_pixels():
+    """HRconv-shaped (64->64 at 256^2, B=32) weight gradient accumulated onto an existing gradient."""
+    n, h = 32, 256
+    p = plan(64, 64, seed=2)
+    g = torch.Generator(device=DEV).manual_seed(2)
+    x = bf(torch.rand((n, 64, h, h), generator=g, device=DEV) * 2 - 1)
+    dz = bf(torch.rand((n, 64, h, h), generator=g, device=DEV) * 2 - 1)
+    p.gw = torch.full_like(p.weight, 3.0)
+    p.gb = torch.full_like(p.bias, -1.0)
+    from climsr_amd import ops
+
+    p.wgrad(nhwc(x), 64, 0, h, h, nhwc(dz), 64, n, ops.Workspace(), accumulate=True)
+    torch.cuda.synchronize()
+    close(p.gw.reshape(64, -1) - 3.0, wgrad64(x, dz), rel=1e-4, what="HRconv wgrad (+=)")
+    close(p.gb + 1.0, dz.double().sum((0, 2, 3)), rel=1e-4, what="HRconv bias grad (+=)")
+
+
+def test_rdb_grouped_wgrad_split_k_at_bench_shape():
+    """One residual dense block's five weight gradients as the grouped 128 x 1152 GEMM at B=32, 64^2 (the 64-way
+    split-K of conv_wgrad64_kernel<1> + wgrad_reduce_rows), vs per-conv float64 GEMMs."""
+    from climsr_amd import ops
+
+    n, h, nf, gc = 32, 64, 64, 16
+    cins = [nf + k * gc for k in range(5)]
+    couts = [gc] * 4 + [nf]
+    plans = []
+    for k in range(5):
+        p = plan(cins[k], couts[k], seed=10 + k)
+        p.gw = torch.full_like(p.weight, float("nan"))
+        p.gb = torch.full_like(p.bias, float("nan"))
+        plans.append(p)
+    gw = ops.GroupedWgrad(plans, 128, "rdb")
+    g = torch.Generator(device=DEV).manual_seed(3)
+    dense = bf(torch.rand((n, 128, h, h), generator=g, device=DEV) * 2 - 1)
+    dz = bf(torch.rand((n, 128, h, h), generator=g, device=DEV) * 2 - 1)
+    ws = ops.Workspace()
+    d_in, dz_in = nhwc(dense), nhwc(dz)
+    from climsr_amd import _lib
+    import ctypes
+
+    d = _lib.ConvDesc(n, h, h, 128, 128, 0, 1, 3, 1, 1, h, h, 128, 0, 0, 8)
+    assert _lib.load().climsr_conv2d_wgrad_splits(ctypes.byref(d)) >= 32  # the split-K path under test
+    gw.run(d_in, 128, 0, h, h, dz_in, 128, n, ws, accumulate=False)
+    torch.cuda.synchronize()
+    off = 0
+    for k, p in enumerate(plans):
+        want = wgrad64(dense[:, :cins[k]], dz[:, off:off + couts[k]])
+        close(p.gw.reshape(couts[k], -1), want, what=f"RDB conv{k + 1} wgrad")
+        close(p.gb, dz[:, off:off + couts[k]].double().sum((0, 2, 3)), what=f"RDB conv{k + 1} bias grad")
+        off += couts[k]
+
+
+@pytest.mark.parametrize("cin,cout,h", [(64, 64, 256), (128, 128, 128), (256, 256, 64), (512, 512, 32)])
+def test_wgrad64_stride2_discriminator_layers(cin, cout, h):
+    """The RFB discriminator's stride-2 convs (features.2/8/14/20, rfb_esrgan.py:29-49) at B=32 of 256^2 tiles: weight
+    gradient on conv_wgrad64_kernel<1, 2> (4 x 16 output tiles over a (2*4+1) x (2*16+1) input footprint)."""
+    from climsr_amd import ops
+
+    n = 32
+    p = plan(cin, cout, seed=cin)
+    p2 = ops.ConvPlan(cin, cout, 3, 2, 1, "s2")
+    p2.bind(p.weight, None)
+    p2.pack()
+    g = torch.Generator(device=DEV).manual_seed(cin)
+    x = bf(torch.rand((n, cin, h, h), generator=g, device=DEV) * 2 - 1)
+    dz = bf(torch.rand((n, cout, h // 2, h // 2), generator=g, device=DEV) * 2 - 1)
+    p2.gw = torch.zeros_like(p2.weight)
+    names = []
+    ops.PROFILER = lambda name, flops, fn, tag="", nbytes=0: (names.append(name), fn())
+    try:
+        p2.wgrad(nhwc(x), cin, 0, h, h, nhwc(dz), cout, n, ops.Workspace(), accumulate=False)
+    finally:
+        ops.PROFILER = None
+    torch.cuda.synchronize()
+    assert "conv_wgrad64_kernel<1, 2>" in names, names
+    want = None
+    for i in range(0, n, 4):
+        cols = F.unfold(x[i:i + 4].double(), 3, padding=1, stride=2)
+        part = torch.einsum("bkl,bcl->ck", cols, dz[i:i + 4].double().flatten(2))
+        want = part if want is None else want + part
+    close(p2.gw.reshape(cout, -1), want, what=f"stride-2 wgrad {cin}->{cout} @{h}")
+
+
+@pytest.mark.parametrize("act", [0, 1])
+def test_conv_pw_forward_at_256_b32(act):
+    """HRconv forward at 256^2, B=32 (conv_pw persistent XCD tile walk over 8192 tiles), bias (+ LeakyReLU)."""
+    from climsr_amd import ops
+
+    n, h = 32, 256
+    p = plan(64, 64, seed=4)
+    g = torch.Generator(device=DEV).manual_seed(4)
+    x = bf(torch.rand((n, 64, h, h), generator=g, device=DEV) * 2 - 1)
+    y = torch.empty((n, h, h, 64), dtype=torch.bfloat16, device=DEV)
+    names = []
+    ops.PROFILER = lambda name, flops, fn, tag="", nbytes=0: (names.append(name), fn())
+    try:
+        p.fwd(nhwc(x), 64, 0, h, h, y, 64, 0, n, act=act)
+    finally:
+        ops.PROFILER = None
+    torch.cuda.synchronize()
+    assert any(s.startswith("conv_pw_kernel") for s in names), names
+    for i in range(0, n, 8):  # float64 reference, 8 images at a time
+        want = F.conv2d(x[i:i + 8].double(), bf(p.weight).double(), p.bias.double(), padding=1)
+        if act == 1:
+            want = F.leaky_relu(want, 0.2)
+        got = y[i:i + 8].permute(0, 3, 1, 2).double()
+        err = float((got - want).abs().max())
+        assert err <= 2 ** -7 * float(want.abs().max()) + 1e-6, f"images {i}..: err {err:.3e}"  # one bf16 ulp of the output
+
+
+def test_conv_pw_dgrad_down2_at_256_b32():
+    """upconv2's data gradient at the bench shape: conv^T of dz [32,64,256,256], summed over 2x2 blocks (backward of
+    the nearest x2 feeding it), LeakyReLU' of upconv1's stored activation, bf16 out at 128^2."""
+    from climsr_amd import ops
+
+    n, h = 32, 128
+    p = plan(64, 64, seed=5)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    dz = bf(torch.rand((n, 64, 2 * h, 2 * h), generator=g, device=DEV) * 2 - 1)
+    act_out = bf(torch.rand((n, 64, h, h), generator=g, device=DEV) * 2 - 1)
+    gx = torch.empty((n, h, h, 64), dtype=torch.bfloat16, device=DEV)
+    p.dgrad(nhwc(dz), 64, 2 * h, 2 * h, gx, 64, 0, n, down2=True, act=ops.ACT_LRELU_BWD, res1=nhwc(act_out), res1_cs=64)
+    torch.cuda.synchronize()
+    for i in range(0, n, 8):
+        x = torch.zeros((8, 64, h, h), dtype=torch.float64, device=DEV, requires_grad=True)
+        y = F.conv2d(F.interpolate(x, scale_factor=2, mode="nearest"), bf(p.weight).double(), None, padding=1)
+        (want,) = torch.autograd.grad(y, x, dz[i:i + 8].double())
+        want = want * torch.where(act_out[i:i + 8] > 0, 1.0, 0.2).double()
+        got = gx[i:i + 8].permute(0, 3, 1, 2).double()
+        err = float((got - want).abs().max())
+        assert err <= 2 ** -7 * float(want.abs().max()) + 1e-6, f"images {i}..: err {err:.3e}"
+
+
+# ------------------------------------------------------------------ whole steps at the bench shape
+def _gemm_conv(p, name, x, stride=1, padding=None):
+    """The oracle's conv (oracle/climsr_ref.py _conv) as unfold + matmul: rocBLAS GEMMs instead of MIOpen, whose
+    per-shape kernel compilation on a fresh box takes minutes.  Same math, autocast-able."""
+    w = p[name + ".weight"]
+    b = p.get(name + ".bias")
+    ks = w.shape[-1]
+    pad = ks // 2 if padding is None else padding
+    n, _c, h, wd = x.shape
+    oh, ow = (h + 2 * pad - ks) // stride + 1, (wd + 2 * pad - ks) // stride + 1
+    cols = F.unfold(x, ks, padding=pad, stride=stride)
+    y = torch.matmul(w.reshape(w.shape[0], -1), cols)
+    if b is not None:
+        y = y + b.reshape(1, -1, 1).to(y.dtype)
+    return y.reshape(n, w.shape[0], oh, ow)
+
+
+@pytest.fixture
+def gemm_oracle(monkeypatch):
+    monkeypatch.setattr(ref, "_conv", _gemm_conv)
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
+
+
+def _log(*a):
+    print("[bench-shape]", *a, flush=True)
+
+
+def _cos(a, b):
+    return float((a * b).sum() / (a.norm() * b.norm() + 1e-30))
+
+
+def _envelope(native, ref32, amps, what):
+    """Per-tensor, against the fp32 reference: relative L2 error <= max(2x the AMP runs' own error, 2e-2), and
+    cosine >= min(0.97, 1 - 2 (1 - cos of the worse AMP run)) -- the reference's own fp16 training (and torch's bf16
+    autocast) is the yardstick for how far a reduced-precision forward moves a random-init gradient."""
+    bad = []
+    for k, want in ref32.items():
+        got = native[k]
+        rel = float((got - want).norm() / (want.norm() + 1e-30))
+        rel_amp = max(float((a[k] - want).norm() / (want.norm() + 1e-30)) for a in amps)
+        cos = _cos(got, want)
+        cos_amp = min(_cos(a[k], want) for a in amps)
+        if rel > max(2.0 * rel_amp, 2e-2) or cos < min(0.97, 1.0 - 2.0 * (1.0 - cos_amp)):
+            bad.append((k, round(rel, 4), round(rel_amp, 4), round(cos, 4), round(cos_amp, 4)))
+    assert not bad, f"{what}: {len(bad)} tensors outside the AMP envelope: {bad[:6]}"
+
+
+def _oracle_grads(p32, keys, loss_fn, dtype=None):
+    p = {k: v.detach().clone().requires_grad_(k in keys) for k, v in p32.items()}
+    if dtype is None:
+        loss = loss_fn(p)
+    else:
+        with torch.autocast("cuda", dtype=dtype):
+            loss = loss_fn(p)
+    grads = torch.autograd.grad(loss.float() * 65536.0, [p[k] for k in keys])
+    _log("oracle", dtype, "loss", float(loss))
+    return float(loss), {k: (g_.double() / 65536.0) for k, g_ in zip(keys, grads)}
+
+
+def test_config2_step_b32_nb11_vs_oracle_fp32(gemm_oracle):
+    """Config 2's whole L1-pretrain forward + backward at the bench shape (nb 11, B=32, 64->256): the loss and every
+    one of the 348 parameter gradients vs the oracle in fp32 on the GPU, in the AMP envelope."""
+    from climsr_amd.losses.l1 import l1_loss
+    from climsr_amd.models.esrgan import ESRGANGenerator
+
+    nb = 11
+    g = ESRGANGenerator(in_channels=3, out_channels=1, nf=64, nb=nb, gc=16, scale_factor=4)
+    p32 = gen_params(nb, torch.float32)
+    g.load_state_dict(p32)
+    g = g.to(DEV)
+    bt = {k: v.to(DEV) for k, v in ref.synthetic_batch(32, 256, seed=42).items()}
+    loss = l1_loss(g(bt["lr"], bt["elevation"], bt["mask"]), bt["hr"])
+    loss.backward()
+    torch.cuda.synchronize()
+    native = {k: p.grad.double() for k, p in g.named_parameters()}
+    _log("native config-2 loss", float(loss))
+    pd = {k: v.to(DEV) for k, v in p32.items()}
+    keys = list(pd.keys())
+
+    def fn(p):
+        return ref.l1_loss(ref.generator_forward(p, bt["lr"], bt["elevation"], bt["mask"], nb).float(), bt["hr"])
+
+    l32, g32 = _oracle_grads(pd, keys, fn)
+    _l16, g16 = _oracle_grads(pd, keys, fn, torch.float16)
+    _lbf, gbf = _oracle_grads(pd, keys, fn, torch.bfloat16)
+    assert abs(float(loss) - l32) <= 1e-3 * abs(l32), (float(loss), l32)
+    _envelope(native, g32, [g16, gbf], "config-2 step gradients")
+
+
+def test_config3_gan_passes_b32_vs_oracle_fp32(gemm_oracle):
+    """Config 3's two passes at the bench shape (nb 1, B=32, 64->256; RFB discriminator with train-mode BN over 32
+    tiles, VGG19 perceptual): the generator pass's loss_G + G gradients and the discriminator pass's loss_D + D
+    gradients vs the oracle in fp32 on the GPU (same weights, no optimizer step in between), in the AMP envelope."""
+    from climsr_amd.task.pl_gan import GANLightningModule
+
+    nb = 1
+    m = GANLightningModule(
+        generator={"_target_": "climsr_amd.models.esrgan.ESRGANGenerator", "in_channels": 3, "out_channels": 1, "nf": 64, "nb": nb,
+                   "gc": 16, "scale_factor": 4},
+        discriminator={"_target_": "climsr_amd.models.rfb_esrgan.RFBESRGANDiscriminator", "in_channels": 1})
+    gp, dp = gen_params(nb, torch.float32), rfb_d_params(torch.float32)
+    m.generator.load_state_dict(gp)
+    m.discriminator.load_state_dict(dp)
+    m = m.to(DEV)
+    vp = {k: v.float().to(DEV) for k, v in vgg_params().items()}
+    bt = {k: v.to(DEV) for k, v in ref.synthetic_batch(32, 256, seed=42).items()}
+    G, D = m.generator, m.discriminator
+    # ---- pass 0 (D frozen)
+    for p in D.parameters():
+        p.requires_grad_(False)
+    hr, sr = m.common_step(bt)
+    _perc, _adv, _pix, lg = m.loss_g(hr, sr)
+    lg.backward()
+    torch.cuda.synchronize()
+    g_native = {k: p.grad.double() for k, p in G.named_parameters()}
+    _log("native pass-0 loss_G", float(lg))
+    # ---- pass 1 (G frozen, fresh G forward with the same weights)
+    for p in D.parameters():
+        p.requires_grad_(True)
+    for p in G.parameters():
+        p.requires_grad_(False)
+    with torch.no_grad():
+        _hr, sr2 = m.common_step(bt)
+    ld = m.loss_d(hr, sr2)
+    ld.backward()
+    torch.cuda.synchronize()
+    d_native = {k: p.grad.double() for k, p in D.named_parameters()}
+    _log("native pass-1 loss_D", float(ld))
+
+    gpd = {k: v.to(DEV) for k, v in gp.items()}
+    dpd = {k: (v.to(DEV)) for k, v in dp.items()}
+
+    def d_fn(p):
+        return lambda t: ref.rfb_discriminator_forward(p, t, training=True, update_stats=False)
+
+    def pass0(p):
+        sr_ = ref.generator_forward(p, bt["lr"], bt["elevation"], bt["mask"], nb).float()
+        return ref.loss_g(d_fn(dpd), vp, bt["hr"], sr_)[3]
+
+    gkeys = list(gpd.keys())
+    l32, g32 = _oracle_grads(gpd, gkeys, pass0)
+    _a, g16 = _oracle_grads(gpd, gkeys, pass0, torch.float16)
+    _b, gbf = _oracle_grads(gpd, gkeys, pass0, torch.bfloat16)
+    assert abs(float(lg) - l32) <= 2e-2 * abs(l32), (float(lg), l32)
+    _envelope(g_native, g32, [g16, gbf], "GAN pass-0 generator gradients")
+
+    with torch.no_grad():
+        sr_ref = ref.generator_forward(gpd, bt["lr"], bt["elevation"], bt["mask"], nb).float()
+    dkeys = ref.trainable_keys(dpd)
+
+    def pass1(p):
+        return ref.loss_d(d_fn(p), bt["hr"], sr_ref)
+
+    l32d, d32 = _oracle_grads(dpd, dkeys, pass1)
+    _c, d16 = _oracle_grads(dpd, dkeys, pass1, torch.float16)
+    _d, dbf = _oracle_grads(dpd, dkeys, pass1, torch.bfloat16)
+    assert abs(float(ld) - l32d) <= 1e-2 * abs(l32d), (float(ld), l32d)
+    _envelope(d_native, d32, [d16, dbf], "GAN pass-1 discriminator gradients")
+
+
+@pytest.mark.parametrize("c,h", [(64, 128), (128, 128), (256, 32), (512, 16)])
+def test_batchnorm_train_at_bench_shapes(c, h):
+    """RFB discriminator BatchNorm2d + LeakyReLU(0.2) (rfb_esrgan.py:32-50) at B=32 bench sizes: batch statistics,
+    running-stat update, num_batches_tracked, the fused apply and the backward (dgamma, dbeta, dz) vs float64."""
+    from climsr_amd import ops
+
+    n = 32
+    npix = n * h * h
+    g = torch.Generator(device=DEV).manual_seed(c + h)
+    z = bf(torch.randn((npix, c), generator=g, device=DEV) * 1.7 + 0.4)  # off-centre: exercises the variance formula
+    zb = z.to(torch.bfloat16)
+    gamma = torch.rand(c, generator=g, device=DEV) + 0.5
+    beta = torch.rand(c, generator=g, device=DEV) - 0.5
+    rm, rv = torch.zeros(c, device=DEV), torch.ones(c, device=DEV)
+    nbt = torch.zeros((), dtype=torch.int64, device=DEV)
+    mean, rstd = torch.empty(c, device=DEV), torch.empty(c, device=DEV)
+    y = torch.empty((npix, c), dtype=torch.bfloat16, device=DEV)
+    cache = {}
+    ops.bn_forward(zb, npix, c, gamma, beta, mean, rstd, y, ops.bn_workspace(npix, c, cache, z.device), rm, rv,
+                   num_batches_tracked=nbt)
+    torch.cuda.synchronize()
+    zd = z.double()
+    m64 = zd.mean(0)
+    v64 = zd.var(0, unbiased=False)
+    close(mean, m64, rel=1e-6, what="mean")
+    close(rstd, 1 / torch.sqrt(v64 + 1e-5), rel=1e-5, what="rstd")
+    close(rm, 0.1 * m64, rel=1e-5, what="running_mean")
+    close(rv, 0.9 + 0.1 * zd.var(0, unbiased=True), rel=1e-5, what="running_var")
+    assert int(nbt) == 1
+    y64 = F.leaky_relu((zd - m64) / torch.sqrt(v64 + 1e-5) * gamma.double() + beta.double(), 0.2)
+    err = float((y.double() - y64).abs().max())
+    assert err <= 2 ** -7 * float(y64.abs().max()), f"bn apply err {err:.3e}"
+    # backward through lrelu(bn(z)), lrelu' from the stored bf16 activation (as the kernel does)
+    da = torch.randn((npix, c), generator=g, device=DEV)
+    dz = torch.empty((npix, c), dtype=torch.bfloat16, device=DEV)
+    coef = torch.empty(3 * c, device=DEV)
+    dgam, dbet = torch.full((c,), 2.0, device=DEV), torch.full((c,), -3.0, device=DEV)
+    ops.bn_backward(da, y, zb, npix, c, mean, rstd, gamma, ops.bn_workspace(npix, c, cache, z.device), coef, dgam, dbet, True, dz)
+    torch.cuda.synchronize()
+    d = da.double() * torch.where(y > 0, 1.0, 0.2).double()
+    xh = (zd - mean.double()) * rstd.double()
+    close(dgam - 2.0, (d * xh).sum(0), rel=1e-5, what="dgamma (+=)")
+    close(dbet + 3.0, d.sum(0), rel=1e-5, what="dbeta (+=)")
+    dz64 = gamma.double() * rstd.double() * (d - d.mean(0) - xh * (d * xh).mean(0))
+    err = float((dz.double() - dz64).abs().max())
+    assert err <= 2 ** -7 * float(dz64.abs().max()), f"bn backward dz err {err:.3e}"

@@ -143,10 +143,50 @@ def test_gan_step_vs_golden(golden_dir):
     got_d = float(out[1]["loss"])
     assert abs(got_d - want["loss_D"]) <= 1e-2 * abs(want["loss_D"]), (got_d, want["loss_D"])
     lr = 1e-4
+    # per tensor (not the mean over tensors): the fixture's [sum, norm] checksums of the updated parameters
+    worst = {}
     for net, before, key in ((m.generator, g_before, "g_params_after"), (m.discriminator, d_before, "d_params_after")):
-        diffs = []
         for k, p in net.named_parameters():
-            d_native = float(p.detach().double().cpu().sum() - before[k].sum())
-            d_ref = want[key][k][0] - float(before[k].sum())
-            diffs.append(abs(d_native - d_ref) / p.numel())
-        assert float(np.mean(diffs)) <= 0.1 * lr, (key, float(np.mean(diffs)))
+            n = p.numel()
+            pa = p.detach().double().cpu()
+            d_sum = abs(float(pa.sum() - before[k].sum()) - (want[key][k][0] - float(before[k].sum()))) / n
+            d_norm = abs(float(pa.norm()) - want[key][k][1]) / n ** 0.5
+            worst[key + ":" + k] = (d_sum / lr, d_norm / lr)
+    ws = max(worst.items(), key=lambda kv: kv[1][0])
+    wn = max(worst.items(), key=lambda kv: kv[1][1])
+    print("gan step worst per-tensor |dsum|/n/lr", ws, "|dnorm|/sqrt(n)/lr", wn)
+    assert ws[1][0] <= GAN_SUM_TOL, ("per-element mean update mismatch", ws)
+    assert wn[1][1] <= GAN_NORM_TOL, ("per-element norm mismatch", wn)
+    # and the full update vectors vs the fp64 oracle step from the same state (oracle.gan_step, CPU)
+    _update_vectors_vs_oracle(m, g_before, d_before, bt, lr)
+
+
+GAN_SUM_TOL = 0.25   # x lr, per tensor (Adam's first step moves every element by ~lr; a sign flip moves it by 2 lr)
+GAN_NORM_TOL = 0.25  # x lr, per tensor, on |norm| / sqrt(numel)
+# rel L2 of a tensor's update vector (native vs the fp64 oracle step).  Adam's first step is ~lr * sign(grad), so
+# elements whose gradient sits inside the bf16 noise flip sign (a 2 lr change each): at this perceptual-loss-dominated
+# golden step the reference's own AMP gradients are ~0.3-0.4 rel L2 off fp64, and ~4 % of the elements flip (measured
+# worst 0.71, median 0.42 on MI355X).  An uncorrelated update would be at sqrt(2) = 1.41, a sign-reversed one at 2.
+UPD_REL_TOL = 1.0
+UPD_REL_MEDIAN = 0.6
+
+
+def _update_vectors_vs_oracle(m, g_before, d_before, bt, lr):
+    gp = {k: v.clone() for k, v in g_before.items()}
+    dp = {k: (v.clone() if v.is_floating_point() else v) for k, v in rfb_d_params(torch.float64).items()}
+    dp.update({k: v.clone() for k, v in d_before.items()})
+    vp = vgg_params(torch.float64)
+    opt_g = ref.AdamWState(gp, list(gp.keys()), lr=lr, total_steps=10)
+    opt_d = ref.AdamWState(dp, ref.trainable_keys(dp), lr=lr, total_steps=10)
+    b64 = {k: v.double().cpu() for k, v in bt.items()}
+    ref.gan_step(gp, dp, vp, opt_g, opt_d, b64, 1)
+    rels = {}
+    for net, before, after in ((m.generator, g_before, gp), (m.discriminator, d_before, dp)):
+        for k, p in net.named_parameters():
+            dn = p.detach().double().cpu() - before[k]
+            dr = after[k] - before[k]
+            rels[k] = float((dn - dr).norm() / (dr.norm() + 1e-30))
+    worst = max(rels.items(), key=lambda kv: kv[1])
+    med = float(np.median(list(rels.values())))
+    print("gan step update-vector rel L2: worst", worst, "median", med)
+    assert worst[1] <= UPD_REL_TOL and med <= UPD_REL_MEDIAN, (worst, med)

@@ -148,13 +148,26 @@ def test_pretrain_steps_vs_golden(golden_dir):
         opt.step()
         sch.step()
     torch.cuda.synchronize()
-    # compare per-tensor sums of the parameter deltas with the reference (fp64 torch AdamW)
-    diffs = []
-    for k, p in g.named_parameters():
-        d_native = float(p.detach().double().cpu().sum() - before[k].sum())
-        d_ref = want["params_after"][k][0] - float(before[k].sum())
-        n = p.numel()
-        diffs.append(abs(d_native - d_ref) / n)
+    # per tensor: the fixture's [sum, norm] checksums of the updated parameters (reference modules, fp64 torch AdamW)
     lr = 1e-4
-    assert max(diffs) <= 0.25 * lr, f"max per-element mean delta diff {max(diffs):.3e}"
-    assert float(np.mean(diffs)) <= 0.05 * lr
+    sums, norms = {}, {}
+    for k, p in g.named_parameters():
+        n = p.numel()
+        pa = p.detach().double().cpu()
+        sums[k] = abs(float(pa.sum() - before[k].sum()) - (want["params_after"][k][0] - float(before[k].sum()))) / n / lr
+        norms[k] = abs(float(pa.norm()) - want["params_after"][k][1]) / n ** 0.5 / lr
+    ws, wn = max(sums.items(), key=lambda kv: kv[1]), max(norms.items(), key=lambda kv: kv[1])
+    print("pretrain 3 steps worst per-tensor |dsum|/n/lr", ws, "|dnorm|/sqrt(n)/lr", wn)
+    assert ws[1] <= 0.25, ws
+    assert wn[1] <= 0.25, wn
+    # the full update vectors vs the fp64 oracle's three steps from the same state
+    p64 = {k: v.clone() for k, v in before.items()}
+    opt64 = ref.AdamWState(p64, list(p64.keys()), lr=lr, total_steps=10)
+    for s in range(3):
+        ref.pretrain_step(p64, opt64, ref.synthetic_batch(2, 64, seed=100 + s, dtype=torch.float64), 1)
+    rels = {k: float((p.detach().double().cpu() - before[k] - (p64[k] - before[k])).norm() / ((p64[k] - before[k]).norm() + 1e-30))
+            for k, p in g.named_parameters()}
+    worst = max(rels.items(), key=lambda kv: kv[1])
+    med = float(np.median(list(rels.values())))
+    print("pretrain update-vector rel L2: worst", worst, "median", med)
+    assert worst[1] <= 0.75 and med <= 0.25, (worst, med)
