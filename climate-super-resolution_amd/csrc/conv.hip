@@ -106,18 +106,12 @@ extern "C" int climsr_version(void) { return 2; }
 // Convs with <= 16 outputs, 3x3 and <= 128 inputs (the residual dense block's conv1-4 and their pull data
 // gradients) run on conv_n16_kernel, whose packed K is tap-major with the channels padded to 32 per tap.
 static bool n16_shape(int in_c, int ks, int out_c) { return out_c <= 16 && ks == 3 && in_c <= 128; }
-static bool pw_disabled() {
-  static int v = getenv("CLIMSR_NO_PW") ? atoi(getenv("CLIMSR_NO_PW")) : 0;
-  return v != 0;
-}
 
 static bool pw_fits(int in_c, int ks, int out_c);
-static bool c64_fits(int in_c, int ks, int out_c, int stride);
 
 extern "C" int climsr_conv_chunk_ex(int in_c, int ks, int out_c, int stride) {
   if (stride == 1 && n16_shape(in_c, ks, out_c))  // conv_n16: one chunk, padded to 32/64/128
     return in_c <= 32 ? 32 : (in_c <= 64 ? 64 : 128);
-  if (c64_fits(in_c, ks, out_c, stride)) return in_c;  // conv_c64: the whole K in one chunk
   if (stride == 1 && pw_fits(in_c, ks, out_c)) return round_up(in_c, 8);  // conv_pw: the whole K in one chunk
   int cc = round_up(in_c, 8);
   FwdGeom g;
@@ -234,44 +228,12 @@ extern "C" int climsr_pack_conv_weights_batched(const ClimsrPackDesc* descs, int
   return check_launch("pack_conv_weights_batched");
 }
 
-// Pull data-gradient weights of a residual dense block (see climsr_hip.h): one launch packs all the
-// pull convs of a network (blockIdx.y = descriptor).
-__global__ void pack_pull_kernel(const ClimsrPullPackDesc* __restrict__ descs) {
-  const ClimsrPullPackDesc d = descs[blockIdx.y];
-  const int rows = climsr_rows_dev(d.out_c);
-  const int kcpad = (d.ks * d.ks * d.cc + 31) / 32 * 32;
-  const int kpk = (d.in_c + d.cc - 1) / d.cc * kcpad;
-  const int total8 = rows * kpk / 8, kpk8 = kpk / 8, kc8 = kcpad / 8;
-  const int kk2 = d.ks * d.ks;
-  for (int i8 = blockIdx.x * blockDim.x + threadIdx.x; i8 < total8; i8 += gridDim.x * blockDim.x) {
-    const int co = i8 / kpk8, kk8 = i8 - co * kpk8;
-    const int j = kk8 / kc8, kr = (kk8 - j * kc8) * 8;
-    const int tap = kr / d.cc;
-    float v[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = 0.f;
-    const int cabs = j * d.cc + kr - tap * d.cc;
-    int c = cabs;
-    if (co < d.out_c && tap < kk2 && c < d.in_c) {
-      // segments are multiples of 8 channels wide: the 8 elements share one
-      int s = 0;
-      while (s < d.nseg - 1 && c >= d.seg_oc[s]) c -= d.seg_oc[s++];
-      const int ky = tap / d.ks, kx = tap - ky * d.ks;
-      const float* src = d.seg_w[s] + ((c * d.seg_ic[s] + d.ci_off + co) * d.ks + (d.ks - 1 - ky)) * d.ks + (d.ks - 1 - kx);
-      const int cstr = d.seg_ic[s] * kk2;
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-        if (c + e < d.seg_oc[s] && cabs + e < d.in_c) v[e] = src[e * cstr];
-    }
-    *(uint4*)(d.out + (long)i8 * 8) = pack8(v);
-  }
-}
-
-// Row-per-workgroup packing (blockIdx.x strides over the packed rows co, blockIdx.y = descriptor): the
+// Pull data-gradient weights of a residual dense block (see climsr_hip.h), all the pull convs of a network in
+// one launch, row-per-workgroup (blockIdx.x strides over the packed rows co, blockIdx.y = descriptor): the
 // row's source weights W_s[c][ci_off + co][.][.] are 9 contiguous floats per input channel c, read in
 // those runs into an LDS [tap][channel] image (tap flipped), then the packed row is written as coalesced
-// 16 B vectors.  (The element-per-thread kernel above gathers 8 floats 36*seg_ic bytes apart per output
-// vector: 128 us per step for the generator's 165 pull convs.)
+// 16 B vectors.  (An element-per-thread gather of 8 floats 36*seg_ic bytes apart per output vector took
+// 128 us per step for the generator's 165 pull convs.)
 constexpr int PULL_ROW_MAX = 4096;  // in_c * ks^2 floats staged per row
 __global__ __launch_bounds__(256) void pack_pull_row_kernel(const ClimsrPullPackDesc* __restrict__ descs) {
   __shared__ float img[PULL_ROW_MAX];
@@ -321,15 +283,9 @@ extern "C" int climsr_pack_pull_weights_batched(const ClimsrPullPackDesc* descs,
     set_error("pack_pull_weights_batched: bad args");
     return CLIMSR_EINVAL;
   }
-  if (!getenv("CLIMSR_PULL_PACK_ELEM")) {
-    // rows per descriptor are on the device: 64 row slots (the RDB pulls have 16 or 64 rows), more rows loop
-    hipLaunchKernelGGL(pack_pull_row_kernel, dim3(64, ndesc), dim3(256), 0, (hipStream_t)stream, descs);
-    return check_launch("pack_pull_weights_batched");
-  }
-  int gx = ceil_div(max_elems / 8, 256);
-  if (gx > 64) gx = 64;
-  if (gx < 1) gx = 1;
-  hipLaunchKernelGGL(pack_pull_kernel, dim3(gx, ndesc), dim3(256), 0, (hipStream_t)stream, descs);
+  (void)max_elems;
+  // rows per descriptor are on the device: 64 row slots (the RDB pulls have 16 or 64 rows), more rows loop
+  hipLaunchKernelGGL(pack_pull_row_kernel, dim3(64, ndesc), dim3(256), 0, (hipStream_t)stream, descs);
   return check_launch("pack_pull_weights_batched");
 }
 
@@ -354,7 +310,6 @@ struct FwdArgs {
   int aux_cs, aux_co;
   float aux_scale;
   int lds_tab, lds_x;
-  int ablate;  // diagnostics only (CLIMSR_ABLATE): 1 skip global loads, 2 skip MFMA, 4 skip stores, 8 skip staging
 };
 
 // Epilogue residual operands: 4 consecutive channels, bf16 (8 B) or fp32 (16 B), kept raw until use so
@@ -648,7 +603,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
         if (i < nrx && ty_ < a.tph) {
           const int iy = iy0 + ty_, ix = ix0 + tx_;
           const int c = j * a.cc + cg * 8;
-          if (!(a.ablate & 1) && iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c && !((iy | ix) & dilmask))
+          if (iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c && !((iy | ix) & dilmask))
             px[i] = *(const uint4*)(a.x + (((long)nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + c);
         }
         cg += x_dc;
@@ -661,7 +616,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
 #pragma unroll
       for (int i = 0; i < PFW; ++i) {
         pw[i] = make_uint4(0, 0, 0, 0);
-        if (i < nrw && r < NT * 16 && !(a.ablate & 1))
+        if (i < nrw && r < NT * 16)
           pw[i] = *(const uint4*)(a.w + (long)(co_blk0 + r) * a.kpk + (long)j * a.kcpad + kv * 8);
         kv += w_dk;
         r += w_dr;
@@ -691,10 +646,10 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
     issue(0);
     for (int j = 0; j < a.nchunk; ++j) {
       __syncthreads();  // chunk j-1's fragment reads are done
-      if (!(a.ablate & 8)) stash();
+      stash();
       if (j + 1 < a.nchunk) issue(j + 1);  // lands while chunk j computes
       __syncthreads();
-      if (!(a.ablate & 2)) compute();
+      compute();
     }
   } else {
   // batched staging: every thread issues up to MV input + MV weight 16 B global loads before the first
@@ -704,7 +659,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
     __syncthreads();
     int ty_ = x_ty0, tx_ = x_tx0, cg = x_cg0;  // input tile (logical coordinates: upsampled / zero-inserted)
     int r = w_r0, kv = w_k0;                  // weight chunk rows [co_blk0, co_blk0 + 16*NT) x kcpad
-    for (int base = 0; base < ((a.ablate & 8) ? 0 : nbatch); base += MV) {
+    for (int base = 0; base < nbatch; base += MV) {
       uint4 bx[MV], bw[MV];
       int dx[MV], dw[MV];
 #pragma unroll
@@ -714,7 +669,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
           const int iy = iy0 + ty_, ix = ix0 + tx_;
           const int c = j * a.cc + cg * 8;
           uint4 val = make_uint4(0, 0, 0, 0);
-          if (!(a.ablate & 1) && iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c && !((iy | ix) & dilmask))
+          if (iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c && !((iy | ix) & dilmask))
             val = *(const uint4*)(a.x + (((long)nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + c);
           bx[i] = val;
           dx[i] = (ty_ * a.tpw + tx_) * a.ccp + cg * 8;
@@ -729,8 +684,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
       for (int i = 0; i < MV; ++i) {
         dw[i] = -1;
         if (base + i < nrw && r < NT * 16) {
-          bw[i] = (a.ablate & 1) ? make_uint4(0, 0, 0, 0)
-                                 : *(const uint4*)(a.w + (long)(co_blk0 + r) * a.kpk + (long)j * a.kcpad + kv * 8);
+          bw[i] = *(const uint4*)(a.w + (long)(co_blk0 + r) * a.kpk + (long)j * a.kcpad + kv * 8);
           dw[i] = r * wpitch + kv * 8;
         }
         kv += w_dk;
@@ -745,12 +699,8 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
         if (dw[i] >= 0) *(uint4*)(ws + dw[i]) = bw[i];
     }
     __syncthreads();
-    if (!(a.ablate & 2)) compute();
+    compute();
   }
-  }
-  if (a.ablate & 4) {
-    if (acc[0][0][0] == 123.f) ((float*)a.y)[0] = 0.f;  // keep the accumulators live
-    return;
   }
 
   // ---------------- epilogue ----------------
@@ -940,7 +890,7 @@ __global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs
       const int pix = v / CV, j = v % CV;
       const int py = pix / N16_TPW, px = pix - py * N16_TPW;
       const int iy = iy0 + py, ix = ix0 + px;
-      const bool ok = live && v < NPIX * CV && j < cvec && !(a.ablate & 1) && iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w;
+      const bool ok = live && v < NPIX * CV && j < cvec && iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w;
       const uint32_t off = (uint32_t)(((((nimg * a.in_h + iy) * a.in_w + ix) * a.in_cs) + a.in_co + j * 8) * 2);
       pre[i] = buf_load16(xr, ok ? off : BUF_OOB);
     }
@@ -966,7 +916,7 @@ __global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs
     const int nimg = tt / a.tiles_y;
     const int oy0 = ty * N16_TH, ox0 = tx * TW;
     lds_barrier();  // the previous tile's LDS reads (partials) are done
-    if (!(a.ablate & 8)) {
+    {
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
         const int v = tid + 256 * i;
@@ -980,7 +930,7 @@ __global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs
     f32x4 acc[MW];
 #pragma unroll
     for (int m = 0; m < MW; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    if (!(a.ablate & 2) && cb * 32 < a.in_c) {  // a wave whose 32-channel block is all padding adds zeros
+    if (cb * 32 < a.in_c) {  // a wave whose 32-channel block is all padding adds zeros
       const uint16_t* xb = xs + ((rg * MW) * N16_TPW + col) * P + cb * 32 + g * 8;
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
@@ -1001,7 +951,6 @@ __global__ __launch_bounds__(256, NCB == 4 ? 2 : 3) void conv_n16_kernel(FwdArgs
 #pragma unroll
     for (int m = 0; m < MW; ++m) *(f32x4*)(part + ((cb * N16_TH + rg * MW + m) * 64 + lane) * 4) = acc[m];
     lds_barrier();
-    if (a.ablate & 4) continue;
     // epilogue: wave w finishes output rows 2w, 2w+1; lane owns channels co..co+3 of column ox0 + col
     const int ox = ox0 + col;
     f32x4 sum[2];
@@ -1096,259 +1045,11 @@ static int launch_n16(const FwdArgs& a, hipStream_t s) {
   static int per_cu = 0;
   if (!per_cu) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, 256, lds) != hipSuccess || per_cu <= 0) per_cu = 2;
-    if (getenv("CLIMSR_N16_PER_CU")) per_cu = atoi(getenv("CLIMSR_N16_PER_CU"));  // tuning experiments
   }
   int ntiles = a.tiles_x * a.tiles_y * a.n;
   int grid = ntiles < per_cu * ncu ? ntiles : per_cu * ncu;
   hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, s, a);
   return check_launch("conv2d_fwd (n16)");
-}
-
-// ------------------------------------------------------------------------------------------
-// 3x3 stride-1 conv with 17..64 outputs and <= 128 inputs (RDB conv5 and its pull gradient, trunk_conv,
-// upconv1/2 with the nearest x2 upsample on load, HRconv, and their data gradients without a 2x2 sum).
-// One 8-wave workgroup per CU walks 8x16-pixel output tiles (persistent), next tile prefetched into
-// registers.  Wave w = (co block w%4, K half w/4) keeps its 16 x (9 taps x Cin/2) weight fragments in
-// VGPRs for the whole launch (no per-tile weight restaging), reads each input-row B fragment once for the
-// three output rows it feeds, and the two K halves meet through LDS (each finishes 4 of the 8 rows).
-// ------------------------------------------------------------------------------------------
-constexpr int C64_TH = 8;
-constexpr int C64_TPH = C64_TH + 2, C64_TPW = TW + 2;
-
-static bool co64_shape(int in_c, int ks, int out_c) { return ks == 3 && out_c > 16 && out_c <= 64 && in_c <= 128; }
-
-template <int NCB, bool RF>
-__global__ __launch_bounds__(512, 1) void conv_co64_kernel(FwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint16_t* xs = (uint16_t*)smem;
-  float* part = (float*)smem;  // [cob 4][kh 2][row 4][lane 64][4] (aliases the input tile after compute)
-  constexpr int CINP = NCB * 32, P = CINP + 16, CV = CINP / 8;  // P == 16 (mod 32): conflict-free fragment reads
-  constexpr int NCBH = (NCB + 1) / 2;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
-  const int cob = wave & 3, kh = wave >> 2;
-  const int cb0 = kh * NCBH;
-  const int cvec = a.in_c / 8;
-  const int upsh = a.up == 2 ? 1 : 0;
-  const int lh = a.in_h << upsh, lw = a.in_w << upsh;
-
-  // A fragments of this wave: rows co = 16 cob + col, k = tap * CINP + 32 cb + 8 g (packed with cc = CINP)
-  bf16x8 af[9][NCBH];
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int c = 0; c < NCBH; ++c) {
-      af[t][c] = (bf16x8){};
-      if (cb0 + c < NCB && !(a.ablate & 16))
-        af[t][c] = *(const bf16x8*)(a.w + (long)(cob * 16 + col) * a.kpk + t * CINP + (cb0 + c) * 32 + g * 8);
-    }
-  const int co = cob * 16 + g * 4;
-  float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (a.bias) {
-    bv.x = co < a.out_c ? a.bias[co] : 0.f;
-    bv.y = co + 1 < a.out_c ? a.bias[co + 1] : 0.f;
-    bv.z = co + 2 < a.out_c ? a.bias[co + 2] : 0.f;
-    bv.w = co + 3 < a.out_c ? a.bias[co + 3] : 0.f;
-  }
-  const int ntiles = a.tiles_x * a.tiles_y * a.n;
-  const bool f1 = RF && (a.res_f32 & 1), f2 = RF && ((a.res_f32 >> 1) & 1);
-  const bool valign = ((a.out_cs | a.out_co) & 3) == 0 && (!a.res1 || ((a.r1_cs | a.r1_co) & 3) == 0) &&
-                      (!a.res2 || ((a.r2_cs | a.r2_co) & 3) == 0) && co + 3 < a.out_c;
-
-  constexpr int NPIX = C64_TPH * C64_TPW, NV = (NPIX * CV + 511) / 512;
-  uint4 pre[NV];
-  auto issue = [&](int tile) {
-    int tt = tile;
-    const int tx = tt % a.tiles_x;
-    tt /= a.tiles_x;
-    const int ty = tt % a.tiles_y;
-    const int nimg = tt / a.tiles_y;
-    const int iy0 = ty * C64_TH - 1, ix0 = tx * TW - 1;
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int v = tid + 512 * i;
-      const int pix = v / CV, j = v % CV;
-      const int py = pix / C64_TPW, px = pix - py * C64_TPW;
-      const int iy = iy0 + py, ix = ix0 + px;
-      pre[i] = make_uint4(0, 0, 0, 0);
-      if (v < NPIX * CV && j < cvec && !(a.ablate & 1) && iy >= 0 && iy < lh && ix >= 0 && ix < lw)
-        pre[i] = *(const uint4*)(a.x + (((long)nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + j * 8);
-    }
-  };
-  if (blockIdx.x < ntiles) issue(blockIdx.x);
-
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    int tt = tile;
-    const int tx = tt % a.tiles_x;
-    tt /= a.tiles_x;
-    const int ty = tt % a.tiles_y;
-    const int nimg = tt / a.tiles_y;
-    const int oy0 = ty * C64_TH, ox0 = tx * TW;
-    __syncthreads();  // previous tile's partial reads are done
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int v = tid + 512 * i;
-      if (v < NPIX * CV) *(uint4*)(xs + (v / CV) * P + (v % CV) * 8) = pre[i];
-    }
-    if (tile + (int)gridDim.x < ntiles) issue(tile + gridDim.x);
-    __syncthreads();
-    f32x4 acc[C64_TH];
-#pragma unroll
-    for (int m = 0; m < C64_TH; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    if (!(a.ablate & 2)) {
-      const uint16_t* xb = xs + col * P + g * 8;
-#pragma unroll
-      for (int c = 0; c < NCBH; ++c) {
-        if (cb0 + c >= NCB) break;
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-          bf16x8 b[C64_TH + 2];  // all input rows of this (channel block, kx) in flight before the first MFMA
-#pragma unroll
-          for (int ir = 0; ir < C64_TH + 2; ++ir) b[ir] = *(const bf16x8*)(xb + (ir * C64_TPW + kx) * P + (cb0 + c) * 32);
-          __builtin_amdgcn_sched_barrier(0);  // keep the reads batched (the scheduler would re-serialise them)
-#pragma unroll
-          for (int ir = 0; ir < C64_TH + 2; ++ir)
-#pragma unroll
-            for (int ky = 0; ky < 3; ++ky) {
-              const int m = ir - ky;
-              if (m >= 0 && m < C64_TH) acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ky * 3 + kx][c], b[ir], acc[m], 0, 0, 0);
-            }
-        }
-      }
-    }
-    f32x4 sum[4];
-    if (!(a.ablate & 32)) {
-      __syncthreads();  // input tile reads done: partials overwrite it
-      // hand the partner K half the 4 rows it finishes; keep (and complete) my 4
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-        *(f32x4*)(part + (((cob * 2 + kh) * 4 + m) * 64 + lane) * 4) = acc[(1 - kh) * 4 + m];
-      __syncthreads();
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-        sum[m] = acc[kh * 4 + m] + *(const f32x4*)(part + (((cob * 2 + (1 - kh)) * 4 + m) * 64 + lane) * 4);
-    } else {
-#pragma unroll
-      for (int m = 0; m < 4; ++m) sum[m] = acc[kh * 4 + m];
-    }
-    if (a.ablate & 4) continue;
-    // epilogue: rows oy0 + 4 kh + m, column ox0 + col, channels co..co+3
-    const int ox = ox0 + col;
-    if (a.down2) {  // 2x2 sum (data gradient of a nearest x2 upsample): rows (m, m+1), columns via lane ^ 1
-      const int dh = a.out_h >> 1, dw = a.out_w >> 1;
-#pragma unroll
-      for (int m = 0; m < 4; m += 2) {
-        const int oy = oy0 + kh * 4 + m;
-        float v[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float sm = sum[m][i] + sum[m + 1][i];
-          sm += __shfl_xor(sm, 1);
-          v[i] = sm;
-        }
-        if ((col & 1) || oy >= a.out_h || ox >= a.out_w || co >= a.out_c) continue;
-        float* yp = (float*)a.y + (((long)nimg * dh + (oy >> 1)) * dw + (ox >> 1)) * a.out_cs + a.out_co + co;
-        if (valign) {
-          float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (a.out_mode == 2) o = *(const float4*)yp;
-          *(float4*)yp = make_float4(o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]);
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (co + i < a.out_c) yp[i] = (a.out_mode == 2 ? yp[i] : 0.f) + v[i];
-        }
-      }
-      continue;
-    }
-#pragma unroll
-    for (int mm = 0; mm < 4; mm += 2) {  // two rows per round: loads of both in flight, half the registers
-      uint4 r1v[2], r2v[2];
-      float4 old[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int oy = oy0 + kh * 4 + mm + h;
-        const long pidx = ((long)nimg * a.out_h + oy) * a.out_w + ox;
-        r1v[h] = r2v[h] = make_uint4(0, 0, 0, 0);
-        old[h] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (oy < a.out_h && ox < a.out_w && valign) {
-          if (a.res1) r1v[h] = load_res4(a.res1, f1, pidx * a.r1_cs + a.r1_co + co);
-          if (a.res2) r2v[h] = load_res4(a.res2, f2, pidx * a.r2_cs + a.r2_co + co);
-          if (a.out_mode == 2) old[h] = *(const float4*)((const float*)a.y + pidx * a.out_cs + a.out_co + co);
-        }
-      }
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int m = mm + h;
-        const int oy = oy0 + kh * 4 + m;
-        if (oy >= a.out_h || ox >= a.out_w || co >= a.out_c) continue;
-        const long pidx = ((long)nimg * a.out_h + oy) * a.out_w + ox;
-        const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
-        float v[4];
-        const long ob = pidx * a.out_cs + a.out_co + co;
-        if (valign) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            v[i] = ep_res(act_apply(sum[m][i] + bb[i], a.act, a.slope), a.act, a.slope, a.res1 != nullptr, res4_at(r1v[h], f1, i),
-                          a.alpha1, a.beta1, a.res2 != nullptr, res4_at(r2v[h], f2, i), a.alpha2, a.beta2);
-          if (a.out_mode == 0) {
-            uint2 pk;
-            pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-            pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-            *(uint2*)((uint16_t*)a.y + ob) = pk;
-          } else {
-            *(float4*)((float*)a.y + ob) = make_float4(old[h].x + v[0], old[h].y + v[1], old[h].z + v[2], old[h].w + v[3]);
-          }
-          if (a.aux) {
-            uint2 pk;
-            pk.x = (uint32_t)f2bf(a.aux_scale * v[0]) | ((uint32_t)f2bf(a.aux_scale * v[1]) << 16);
-            pk.y = (uint32_t)f2bf(a.aux_scale * v[2]) | ((uint32_t)f2bf(a.aux_scale * v[3]) << 16);
-            *(uint2*)(a.aux + pidx * a.aux_cs + a.aux_co + co) = pk;
-          }
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            if (co + i >= a.out_c) continue;
-            const float r1 = a.res1 ? res_at(a.res1, f1, pidx * a.r1_cs + a.r1_co + co + i) : 0.f;
-            const float r2 = a.res2 ? res_at(a.res2, f2, pidx * a.r2_cs + a.r2_co + co + i) : 0.f;
-            const float x = ep_res(act_apply(sum[m][i] + bb[i], a.act, a.slope), a.act, a.slope, a.res1 != nullptr, r1, a.alpha1,
-                                   a.beta1, a.res2 != nullptr, r2, a.alpha2, a.beta2);
-            if (a.out_mode == 0) ((uint16_t*)a.y)[ob + i] = f2bf(x);
-            else if (a.out_mode == 2) ((float*)a.y)[ob + i] += x;
-            else ((float*)a.y)[ob + i] = x;
-            if (a.aux) a.aux[pidx * a.aux_cs + a.aux_co + co + i] = f2bf(a.aux_scale * x);
-          }
-        }
-      }
-    }
-  }
-}
-
-template <int NCB, bool RF>
-static int launch_co64_t(const FwdArgs& a, hipStream_t s) {
-  auto k = conv_co64_kernel<NCB, RF>;
-  size_t lds = (size_t)C64_TPH * C64_TPW * (NCB * 32 + 16) * 2;
-  const size_t lds_p = (size_t)4 * 2 * 4 * 64 * 16;
-  if (lds_p > lds) lds = lds_p;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
-  }
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (ncu <= 0) ncu = 256;
-  }
-  const int ntiles = a.tiles_x * a.tiles_y * a.n;
-  const int grid = ntiles < ncu ? ntiles : ncu;
-  hipLaunchKernelGGL(k, dim3(grid), dim3(512), lds, s, a);
-  return check_launch("conv2d_fwd (co64)");
-}
-
-template <int NCB>
-static int launch_co64(const FwdArgs& a, hipStream_t s) {
-  return a.res_f32 ? launch_co64_t<NCB, true>(a, s) : launch_co64_t<NCB, false>(a, s);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1677,7 +1378,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
       {
         const int iy = iy0 + ty_, ix = ix0 + tx_;
         const int c = cg * 8;
-        const bool ok = live && tid + NTHR * i < nvec_x && !(a.ablate & 1) && iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c;
+        const bool ok = live && tid + NTHR * i < nvec_x && iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c;
         const uint32_t off = (uint32_t)((((nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + c) * 2);
         pre[i] = buf_load16(xr, ok ? off : BUF_OOB);
       }
@@ -1722,7 +1423,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
     for (int m = 0; m < MW; ++m)
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[m][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    if (!(a.ablate & 2)) {
+    {
       const int nks = a.kcpad / 32;
       for (int kstep = 0; kstep < nks; ++kstep) {
         const int off = tab[kstep * 4 + g];
@@ -1736,10 +1437,6 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
 #pragma unroll
           for (int t = 0; t < NT; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bfr[m], acc[m][t], 0, 0, 0);
       }
-    }
-    if (a.ablate & 4) {
-      if (acc[0][0][0] == 123.f) ((float*)a.y)[0] = 0.f;
-      continue;
     }
     const int ox = ox0 + col;
     if constexpr (EP == 5) {  // 2x2 sum + activation backward (act' of the bf16 low-res activation res1), bf16 out,
@@ -1861,179 +1558,6 @@ static int launch_pw(const FwdArgs& a0, const PwGeom& g, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------------------
-// 64-output 3x3 conv, stride 1, one channel chunk of 64 or 128 inputs (RDB conv5, the 128->64 pull gradient,
-// trunk_conv, HRconv and the 64->64 data gradients).  Built around the two rates that bound it:
-//  * A (weights) never touches LDS: wave w owns output channels 16w..16w+15 with ALL its 9 x Cin weight
-//    fragments in VGPRs for the whole launch (36 x Cin/32 registers);
-//  * every B fragment (16 pixels x 32 channels of one input row) read from LDS feeds the 3 output rows it
-//    touches (ky reuse): 0.42 LDS fragment reads per MFMA instead of 0.75-1 in the LDS-weight kernels;
-//  * the input tile is filled by global_load_lds (16 B per lane, no VGPR staging) into a lane-linear LDS image
-//    whose 16 B channel slots are XOR-swizzled by pixel (source address pre-swizzled, reads swizzled the same
-//    way: conflict-free ds_read_b128), double-buffered so tile t+1 lands while tile t computes; one barrier
-//    per tile.  Persistent XCD-aware tile walk, one workgroup per CU.
-// ------------------------------------------------------------------------------------------
-constexpr int C64_TH2 = 8;                       // output rows per tile
-constexpr int C64_IR = C64_TH2 + 2, C64_IC = TW + 2;  // input tile rows / columns
-__device__ __attribute__((aligned(16))) uint4 g_zero16[4];
-
-// Opt-in (CLIMSR_C64=1): measured 5-15 % slower than the generic kernel on conv5 / pull-x (one 4-wave workgroup per
-// CU cannot hide the LDS and epilogue latency) and mixed on the 256^2 64->64 convs (17 % faster than conv_pw in
-// isolation, slower inside the step).  Kept, parity-tested, as the starting point of a K-split 8-wave version.
-static bool c64_fits(int in_c, int ks, int out_c, int stride) {
-  static const bool on = getenv("CLIMSR_C64") != nullptr;
-  return on && ks == 3 && stride == 1 && out_c == 64 && (in_c == 64 || in_c == 128);
-}
-
-template <int NCH, bool SB>
-__global__ __launch_bounds__(256, NCH == 2 ? 2 : 1) void conv_c64_kernel(FwdArgs a) {
-  constexpr int CG = NCH * 4;                                   // 16 B channel slots per pixel
-  constexpr int NSLOT = C64_IR * C64_IC * CG;                   // slots of one input tile
-  constexpr int NINST = (NSLOT + 63) / 64;                      // glds instructions per tile (1 KiB each)
-  constexpr int BUF = NINST * 1024;                             // bytes of one LDS buffer
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
-
-  bf16x8 af[9][NCH];  // rows co = 16 wave + col, k = tap * cc + 32 c + 8 g
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) af[t][c] = *(const bf16x8*)(a.w + (long)(wave * 16 + col) * a.kpk + t * a.cc + c * 32 + g * 8);
-  const int co = wave * 16 + g * 4;
-  float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (a.bias) bv = make_float4(a.bias[co], a.bias[co + 1], a.bias[co + 2], a.bias[co + 3]);
-  const bool f1 = (a.res_f32 & 1) != 0, f2 = ((a.res_f32 >> 1) & 1) != 0;
-  const int ntiles = a.tiles_x * a.tiles_y * a.n;
-
-  // slot s -> (input row r, column px, stored channel group gs); the global source holds group gs ^ (px & 7)
-  auto issue = [&](int tile, int buf) {
-    int tt = tile;
-    const int tx = tt % a.tiles_x;
-    tt /= a.tiles_x;
-    const int ty = tt % a.tiles_y;
-    const int nimg = tt / a.tiles_y;
-    const int iy0 = ty * C64_TH2 - 1, ix0 = tx * TW - 1;
-    char* base = smem + buf * BUF;
-    for (int k = wave; k < NINST; k += 4) {
-      const int sl = k * 64 + lane;
-      const int pix = sl / CG, gs = sl - pix * CG;
-      const int r = pix / C64_IC, px = pix - r * C64_IC;
-      const int iy = iy0 + r, ix = ix0 + px;
-      const void* src = g_zero16;
-      if (sl < NSLOT && iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w)
-        src = a.x + (((long)nimg * a.in_h + iy) * a.in_w + ix) * a.in_cs + a.in_co + (gs ^ (px & 7)) * 8;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(base + k * 1024), 16, 0, 0);
-    }
-  };
-
-  const TileWalk walk(ntiles);
-  if (walk.first < walk.end) issue(walk.first, 0);
-  int buf = 0;
-  for (int tile = walk.first; tile < walk.end; tile += walk.step, buf ^= 1) {
-    __syncthreads();  // this tile's LDS image has landed (the barrier drains every wave's loads) and the
-                      // other buffer is no longer read (previous tile's compute is done)
-    if (tile + walk.step < walk.end) issue(tile + walk.step, buf ^ 1);
-    int tt = tile;
-    const int tx = tt % a.tiles_x;
-    tt /= a.tiles_x;
-    const int ty = tt % a.tiles_y;
-    const int nimg = tt / a.tiles_y;
-    const int oy0 = ty * C64_TH2, ox0 = tx * TW;
-
-    f32x4 acc[C64_TH2];
-#pragma unroll
-    for (int m = 0; m < C64_TH2; ++m) acc[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    const char* xb = smem + buf * BUF;
-#pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
-      const int px = col + kx;
-#pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        const int gsw = ((c * 4 + g) ^ (px & 7)) * 16;
-        bf16x8 b[C64_IR];
-#pragma unroll
-        for (int r = 0; r < C64_IR; ++r) b[r] = *(const bf16x8*)(xb + (r * C64_IC + px) * (CG * 16) + gsw);
-        if (SB) __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int r = 0; r < C64_IR; ++r)
-#pragma unroll
-          for (int ky = 0; ky < 3; ++ky) {
-            const int m = r - ky;
-            if (m >= 0 && m < C64_TH2) acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ky * 3 + kx][c], b[r], acc[m], 0, 0, 0);
-          }
-      }
-    }
-    // epilogue: lane owns channels co..co+3 of pixel (oy0 + m, ox0 + col)
-    const int ox = ox0 + col;
-    if (ox >= a.out_w) continue;
-#pragma unroll
-    for (int m = 0; m < C64_TH2; ++m) {
-      const int oy = oy0 + m;
-      if (oy >= a.out_h) break;
-      const long pidx = ((long)nimg * a.out_h + oy) * a.out_w + ox;
-      const uint4 r1 = a.res1 ? load_res4(a.res1, f1, pidx * a.r1_cs + a.r1_co + co) : make_uint4(0, 0, 0, 0);
-      const uint4 r2 = a.res2 ? load_res4(a.res2, f2, pidx * a.r2_cs + a.r2_co + co) : make_uint4(0, 0, 0, 0);
-      const long ob = pidx * a.out_cs + a.out_co + co;
-      float4 old = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (a.out_mode == 2) old = *(const float4*)((const float*)a.y + ob);
-      const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
-      float v[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        v[i] = ep_res(act_apply(acc[m][i] + bb[i], a.act, a.slope), a.act, a.slope, a.res1 != nullptr, res4_at(r1, f1, i), a.alpha1,
-                      a.beta1, a.res2 != nullptr, res4_at(r2, f2, i), a.alpha2, a.beta2);
-      if (a.out_mode == 0) {
-        uint2 pk;
-        pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-        pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-        *(uint2*)((uint16_t*)a.y + ob) = pk;
-      } else {
-        *(float4*)((float*)a.y + ob) = make_float4(old.x + v[0], old.y + v[1], old.z + v[2], old.w + v[3]);
-      }
-      if (a.aux) {
-        uint2 pk;
-        pk.x = (uint32_t)f2bf(a.aux_scale * v[0]) | ((uint32_t)f2bf(a.aux_scale * v[1]) << 16);
-        pk.y = (uint32_t)f2bf(a.aux_scale * v[2]) | ((uint32_t)f2bf(a.aux_scale * v[3]) << 16);
-        *(uint2*)(a.aux + pidx * a.aux_cs + a.aux_co + co) = pk;
-      }
-    }
-  }
-}
-
-template <int NCH>
-static int launch_c64(const FwdArgs& a0, hipStream_t s) {
-  static const bool sb = getenv("CLIMSR_C64_SB") != nullptr;
-  static const int wpc = getenv("CLIMSR_C64_WPC") ? atoi(getenv("CLIMSR_C64_WPC")) : (NCH == 2 ? 2 : 1);
-  if (g_dry) {
-    snprintf(g_dry_name, sizeof(g_dry_name), "conv_c64_kernel<%d, %s>", NCH, sb ? "true" : "false");
-    return CLIMSR_OK;
-  }
-  FwdArgs a = a0;
-  a.tiles_x = ceil_div(a.out_w, TW);
-  a.tiles_y = ceil_div(a.out_h, C64_TH2);
-  constexpr int NINST = (C64_IR * C64_IC * NCH * 4 + 63) / 64;
-  const size_t lds = (size_t)2 * NINST * 1024;
-  auto k = sb ? conv_c64_kernel<NCH, true> : conv_c64_kernel<NCH, false>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)conv_c64_kernel<NCH, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)conv_c64_kernel<NCH, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
-  }
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (ncu <= 0) ncu = 256;
-  }
-  const int ntiles = a.tiles_x * a.tiles_y * a.n;
-  const int grid = ntiles < wpc * ncu ? ntiles : wpc * ncu;
-  hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, s, a);
-  return check_launch("conv2d_fwd (c64)");
-}
-
-// ------------------------------------------------------------------------------------------
 // 1x1 conv as a streaming GEMM (srcnn.conv2 64->32 and its 32->64 data gradient with the ReLU mask):
 // out[p][co] = epilogue(sum_ci x[p][ci] w[co][ci]).  Nothing is reused across pixels except the weights, so
 // nothing goes through LDS: the weight fragments sit in VGPRs, each lane loads its 16 B channel slice of a
@@ -2046,7 +1570,7 @@ static bool pt_shape(const ClimsrConvDesc* d, const ClimsrEpilogue* ep) {
   return d->ks == 1 && d->stride == 1 && d->up == 1 && d->pad == 0 && !ep->down2 && d->in_c % 32 == 0 && d->in_c <= 128 &&
          d->cc == d->in_c && d->out_c % 16 == 0 && d->out_c <= 64 && d->out_h == d->in_h && d->out_w == d->in_w &&
          ((d->out_cstride | d->out_coff) & 3) == 0 && (!ep->res1 || ((ep->res1_cstride | ep->res1_coff) & 3) == 0) &&
-         (!ep->res2 || ((ep->res2_cstride | ep->res2_coff) & 3) == 0) && !getenv("CLIMSR_NO_PT");
+         (!ep->res2 || ((ep->res2_cstride | ep->res2_coff) & 3) == 0);
 }
 
 // EP: 0 generic (runtime flags); 3 activation forward (bias + leaky relu / relu, bf16 out); 4 activation backward
@@ -2398,10 +1922,6 @@ static int launch_fwd(const FwdArgs& a, int ncob, size_t lds, hipStream_t s) {
   return launch_fwd_ep<MW, NT, PFX, PFW, 0>(a, ncob, lds, s);
 }
 
-static bool fwd_pf_disabled() {
-  static const bool v = getenv("CLIMSR_NO_FWD_PF") != nullptr;
-  return v;
-}
 
 // Epilogue specialisations without residuals (store_tile_lds EP 3 / 6 / 7 / 8), or 0: activation forward with
 // (3) / without (6) bias, plain fp32 '=' output (7), plain bf16 output (8).  Needs 8-channel-aligned slices.
@@ -2467,12 +1987,10 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
   a.slope = ep->slope; a.alpha1 = ep->alpha1; a.alpha2 = ep->alpha2;
   a.r1_cs = ep->res1_cstride; a.r1_co = ep->res1_coff; a.r2_cs = ep->res2_cstride; a.r2_co = ep->res2_coff;
   a.lds_tab = (int)g.lds_tab; a.lds_x = (int)g.lds_x;
-  static int ablate = getenv("CLIMSR_ABLATE") ? atoi(getenv("CLIMSR_ABLATE")) : 0;
-  a.ablate = ablate;
   int rows = climsr_conv_packed_rows(d->out_c);
   int ncob = rows / (g.nt * 16);
   hipStream_t s = (hipStream_t)stream;
-  if (d->out_c == 1 && d->stride == 1 && d->up == 1 && !ep->down2 && !ep->res2 && co1m_shape(d) && !getenv("CLIMSR_NO_CO1M"))
+  if (d->out_c == 1 && d->stride == 1 && d->up == 1 && !ep->down2 && !ep->res2 && co1m_shape(d))
     return dispatch_co1m(d, a, s);
   if (d->out_c == 1 && d->stride == 1 && d->up == 1 && !ep->down2 && !ep->res2) {
     a.tiles_x = ceil_div(d->out_w, 16);
@@ -2509,30 +2027,14 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
       default: return launch_n16<4, 0>(a, s);
     }
   }
-  // conv_co64_kernel (A fragments register-resident, K halves per wave) measured slower than the generic
-  // kernel on every shape (register-capped at 8 waves/CU); kept for reference, not dispatched.
-  if (false && co64_shape(d->in_c, d->ks, d->out_c) && d->cc == 32 * n16_ncb(d->in_c) && d->stride == 1 && d->pad == 1 &&
-      (d->up == 1 || d->up == 2) && d->out_h == d->in_h * d->up && d->out_w == d->in_w * d->up) {
-    a.tiles_x = ceil_div(d->out_w, TW);
-    a.tiles_y = ceil_div(d->out_h, C64_TH);
-    switch (d->cc / 32) {
-      case 1: return launch_co64<1>(a, s);
-      case 2: return launch_co64<2>(a, s);
-      default: return launch_co64<4>(a, s);
-    }
-  }
   if (pt_shape(d, ep) && (d->out_c == 16 || d->out_c == 32 || d->out_c == 64) &&
       (d->in_c == 32 || d->in_c == 64 || d->in_c == 128))
     return dispatch_pt(d, a, s);
-  if (c64_fits(d->in_c, d->ks, d->out_c, d->stride) && d->cc == d->in_c && d->pad == 1 && d->up == 1 && !ep->down2 &&
-      d->out_h == d->in_h && d->out_w == d->in_w && ((d->out_cstride | d->out_coff) & 3) == 0 &&
-      (!ep->res1 || ((ep->res1_cstride | ep->res1_coff) & 3) == 0) && (!ep->res2 || ((ep->res2_cstride | ep->res2_coff) & 3) == 0))
-    return d->in_c == 128 ? launch_c64<4>(a, s) : launch_c64<2>(a, s);
   {  // weights-resident persistent kernel for one-chunk convs with 17..64 outputs (large-pixel-count layers)
     const int nt = fwd_nt(d->out_c);
     const long npx = (long)d->n * d->out_h * d->out_w;
     PwGeom pg;
-    if (ncob == 1 && (nt == 4 || nt == 2) && d->up != -2 && npx >= 4096 && !pw_disabled() &&
+    if (ncob == 1 && (nt == 4 || nt == 2) && d->up != -2 && npx >= 4096 &&
         (long)d->n * d->in_h * d->in_w * d->in_cstride * 2 < (1L << 31)) {  // 32-bit buffer offsets
       // 8 waves x 2 rows (two waves per SIMD) when the LDS allows, else 4 waves x 2 rows
       if (pw_geom(d, nt, 2, &pg, 8) && pg.nvx <= 512 * 7 && d->out_h >= 16) {
@@ -2567,7 +2069,7 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
   if (mw == 4) {
     // multi-chunk tiles whose per-thread staging fits 6 input + 9 weight vectors: chunk-pipelined variant
     const int nrx = ceil_div(g.tph * g.tpw * (d->cc / 8), 256), nrw = ceil_div(g.nt * 16 * (g.kcpad / 8), 256);
-    if (g.nchunk > 1 && nrx <= 6 && nrw <= 9 && !fwd_pf_disabled()) {
+    if (g.nchunk > 1 && nrx <= 6 && nrw <= 9) {
       // epilogue specialisations (store_tile_lds EP): residual forward (conv5, trunk_conv) / fp32 pull-x
       const bool v8 = (a.out_c & 7) == 0 && ((a.out_cs | a.out_co) & 7) == 0 && ((a.r1_cs | a.r1_co) & 7) == 0 &&
                       (!a.res2 || ((a.r2_cs | a.r2_co) & 7) == 0) && (!a.aux || ((a.aux_cs | a.aux_co) & 7) == 0) && !a.down2 &&
@@ -2585,7 +2087,7 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
     }
     // large input tiles (stride 2: 33x33 pixels per 16x16 outputs) with several chunks: the deeper-prefetch
     // variant (one workgroup per CU already, so the 18 staging vectors per thread cost no occupancy)
-    if (g.nchunk > 1 && nrx <= 18 && nrw <= 9 && !fwd_pf_disabled()) {
+    if (g.nchunk > 1 && nrx <= 18 && nrw <= 9) {
       if (plain_ep(a) == 8) return launch_fwd_ep<4, 4, 18, 9, 8>(a, ncob, g.lds_total, s);
       return launch_fwd<4, 4, 18, 9>(a, ncob, g.lds_total, s);
     }
@@ -2647,7 +2149,6 @@ struct WgArgs {
   int n, in_h, in_w, in_c, in_cs, in_co, up, ks, stride, pad, out_h, out_w, out_c, dz_cs;
   int tph, tpw, dzp, tiles_x, tiles_y, ntiles, nsplit, ntapb, ncib, co_rows, kw;
   int lds_x;
-  int ablate;
 };
 
 // CI4 = 1: inputs with <= 4 real channels (srcnn.conv1 / conv_first, 3 channels).  The x tile holds 4
@@ -2740,7 +2241,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs a) {
             const int iy = iy0 + ty_, ix = ix0 + tx_;
             const int c = ci0 + (CI4 ? 0 : h * 8);
             uint4 val = make_uint4(0, 0, 0, 0);
-            const bool ok = !(a.ablate & 1) && iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c;
+            const bool ok = iy >= 0 && iy < lh && ix >= 0 && ix < lw && c < a.in_c;
             const long src = (((long)nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + c;
             if (CI4) {
               if (ok) {
@@ -2777,7 +2278,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs a) {
             const int oy = oy0 + pix / TW, ox = ox0 + (pix % TW);
             const int c = co0 + cv * 8;
             uint4 val = make_uint4(0, 0, 0, 0);
-            if (!(a.ablate & 1) && oy < a.out_h && ox < a.out_w && c < a.dz_cs)
+            if (oy < a.out_h && ox < a.out_w && c < a.dz_cs)
               val = *(const uint4*)(a.dz + (((long)nimg * a.out_h + oy) * a.out_w + ox) * a.dz_cs + c);
             buf[i] = val;
           }
@@ -2795,7 +2296,6 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs a) {
     __syncthreads();
 #pragma unroll 2  // (a full unroll of the WS variant's 8 k-steps made hipcc copy the accumulators AGPR<->VGPR)
     for (int s = 0; s < (WS ? 8 : 2); ++s) {
-      if (a.ablate & 2) break;
       const int kk = WS ? s : wave * 2 + s;  // k-step: output pixel rows 2kk, 2kk+1 of the tile
       // pixel handled as row q (+4) of this lane's tr reads
       const int k0 = kk * 32 + 8 * g + q;
@@ -3031,7 +2531,7 @@ constexpr int WPT_CH = 128;
 
 static bool wpt_shape(const ClimsrConvDesc* d) {
   return d->ks == 1 && d->stride == 1 && d->up == 1 && d->pad == 0 && d->in_c == 64 && d->out_c % 16 == 0 && d->out_c <= 64 &&
-         d->out_h == d->in_h && d->out_w == d->in_w && !getenv("CLIMSR_NO_WPT");
+         d->out_h == d->in_h && d->out_w == d->in_w;
 }
 
 static int wpt_splits(const ClimsrConvDesc* d) {
@@ -3309,12 +2809,12 @@ static void wg_plan(const ClimsrConvDesc* d, WgPlan* w) {
 }
 
 static bool wg_ws(const ClimsrConvDesc* d, const WgPlan& w) {
-  return w.ci4 && d->ks == 9 && w.ncob == 1 && w.ntc == 4 && d->stride == 1 && !getenv("CLIMSR_NO_WGWS");
+  return w.ci4 && d->ks == 9 && w.ncob == 1 && w.ntc == 4 && d->stride == 1;
 }
 
 extern "C" int climsr_conv2d_wgrad_splits(const ClimsrConvDesc* d) {
   if (wpt_shape(d)) return wpt_splits(d);
-  if (wco1_shape(d) && !getenv("CLIMSR_NO_CO1M")) return wco1_splits(d);
+  if (wco1_shape(d)) return wco1_splits(d);
   if (w64_shape(d)) {  // one workgroup per CU: 256 / blocks splits
     int blocks = (d->out_c / 64) * (d->in_c / 64);
     int ntiles = d->n * ceil_div(d->out_w, TW) * ceil_div(d->out_h, w64_th(d));
@@ -3337,7 +2837,7 @@ extern "C" size_t climsr_conv2d_wgrad_workspace(const ClimsrConvDesc* d, int nsp
     const int co_rows = ceil_div(rows, ntc * 16) * ntc * 16;
     return (size_t)nsplit * co_rows * d->in_c + (size_t)nsplit * co_rows;
   }
-  if (wco1_shape(d) && !getenv("CLIMSR_NO_CO1M")) return (size_t)nsplit * 16 * d->in_c * d->ks * d->ks + (size_t)nsplit * 16;
+  if (wco1_shape(d)) return (size_t)nsplit * 16 * d->in_c * d->ks * d->ks + (size_t)nsplit * 16;
   if (w64_shape(d)) return (size_t)nsplit * d->out_c * d->in_c * 9 + (size_t)nsplit * d->out_c;
   WgPlan w;
   wg_plan(d, &w);
@@ -3382,7 +2882,7 @@ extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, c
     }
     return check_launch("conv2d_wgrad (1x1)");
   }
-  if (wco1_shape(d) && !getenv("CLIMSR_NO_CO1M")) {
+  if (wco1_shape(d)) {
     WgArgs a{};
     a.x = x; a.dz = dz; a.part = partial; a.bpart = bias_partial;
     a.n = d->n; a.in_h = d->in_h; a.in_w = d->in_w; a.in_c = d->in_c; a.in_cs = d->in_cstride; a.in_co = d->in_coff;
@@ -3412,7 +2912,7 @@ extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, c
     a.out_c = d->out_c; a.dz_cs = dz_cstride;
     a.tiles_x = ceil_div(d->out_w, TW); a.tiles_y = ceil_div(d->out_h, w64_th(d)); a.ntiles = d->n * a.tiles_x * a.tiles_y;
     a.nsplit = nsplit; a.ncib = d->in_c / 64; a.co_rows = d->out_c; a.kw = d->in_c * 9;
-    a.dzp = W64_P; a.ntapb = 1; a.lds_x = 0; a.ablate = 0;
+    a.dzp = W64_P; a.ntapb = 1; a.lds_x = 0;
     a.stride = d->stride;
     // 8 waves (tap-split) pay off on the large-pixel-count convs (HRconv / upconv at 256^2: +8 %) and lose on the
     // 64^2 dense-block GEMM (-19 %), measured with tests/perf_conv.py
@@ -3454,8 +2954,6 @@ extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, c
   a.tph = w.tph; a.tpw = w.tpw; a.dzp = w.dzp; a.tiles_x = w.tiles_x; a.tiles_y = w.tiles_y; a.ntiles = w.ntiles;
   a.nsplit = nsplit; a.ntapb = w.ntapb; a.ncib = w.ncib; a.co_rows = w.co_rows; a.kw = w.kw;
   a.lds_x = (int)w.lds_x;
-  static int ablate = getenv("CLIMSR_ABLATE") ? atoi(getenv("CLIMSR_ABLATE")) : 0;
-  a.ablate = ablate;
   int nblk = w.ntapb * w.ncib * w.ncob;
   hipStream_t s = (hipStream_t)stream;
   if (wg_ws(d, w)) {  // all 21 tap groups per workgroup, 6 per wave

@@ -1,254 +1,374 @@
-// Residual-dense-block chain: the four 16-output 3x3 convs of an RDB in ONE launch.
+// Residual-dense-block chain: the four 16-output 3x3 convs of an RDB in ONE launch (esrgan.py:22-37).
 //
-// Forward (esrgan.py:22-37):   x1 = lrelu(conv1(x)),  x2 = lrelu(conv2([x,x1])),  ...,  x4 = lrelu(conv4([x,x1,x2,x3]))
-// Pull backward (the data-gradient chain of the same block, see climsr_hip.h ClimsrPullPackDesc):
-//                              dZ4 = lrelu'(x4) * pull4(dZ5),  dZ3 = lrelu'(x3) * pull3([dZ5,dZ4]),  ...
-// Both are "level L reads a base tensor (64 ch) plus the outputs of levels < L (16 ch each)".  Run as four
-// separate convs, every level re-reads its whole input from HBM and pays a launch; here one workgroup owns a
-// 16-row x 32-column output strip and streams down it: wave L computes level L one row per step, lagging
-// level L-1 by two rows (so everything it reads was produced in earlier steps), with ring buffers of the
-// rows still needed in LDS, the base rows prefetched two steps ahead, and each wave's weights in VGPRs.
-// Halo rows / columns of levels 1-3 are recomputed by neighbouring strips; only owned pixels are stored.
-// MFMA v_mfma_f32_16x16x32_bf16: A = weights [16 co][32 k], B = 16 pixels of one row x 32 channels.
+// Forward:        x1 = lrelu(conv1(x)),  x2 = lrelu(conv2([x,x1])),  x3 = ...,  x4 = lrelu(conv4([x,x1,x2,x3]))
+// Pull backward:  dZ4 = lrelu'(x4) * pull4(dZ5),  dZ3 = lrelu'(x3) * pull3([dZ5,dZ4]),  ...  (climsr_hip.h)
+// Both are "level L reads a 64-channel base plus the 16-channel outputs of levels < L".  Run conv by conv, every
+// level re-reads its whole input from HBM (352 channel-reads per pixel for 64 read + 64 written here) and the
+// four launches are latency-bound (two 8x16 tiles per workgroup each).
+//
+// Here one workgroup owns R full-width image rows (width <= 64: 4 column fragments of 16 pixels, no horizontal
+// halo) and streams down them.  Step s: level 1 computes row y1 = r0 - 3 + s, level L row y1 - 2(L - 1) (every row
+// it reads from level L-1 was written in an earlier step: one barrier per step).  LDS holds a 10-row ring of the
+// base (64 ch) and an 8-row ring of the level outputs [out1|out2|out3] (48 ch); only the rows of the strip are
+// stored to HBM, the 3 + 2 + 1 halo rows above / below each strip are recomputed by the neighbouring strips.
+// Wave w (one per SIMD) owns column fragment w of EVERY level, so the four SIMDs carry equal work; its A
+// fragments (weights: 16 co x 32 k, 100 fragments over the four levels) sit in VGPRs/AGPRs for the whole launch
+// and each MFMA reads one B fragment (16 pixels x 32 channels of one tap) from LDS with ds_read_b128.
+// K blocking: the base part of a level is 9 taps x 2 blocks of 32 channels; the dense part is one block per tap for
+// 32 channels (out1|out2) and, for a 16-channel group (out1 of level 2, out3 of level 4), PAIRS of taps in one block
+// (lanes 0-31 read tap 2p, lanes 32-63 tap 2p+1): 5 blocks instead of 9 half-empty ones.
+// MFMA v_mfma_f32_16x16x32_bf16: A = weights [16 co][32 k], B = [32 k][16 pixels], C lane = 4 co of one pixel.
 #include "common.h"
 
 using namespace climsr;
 
 namespace {
 
-constexpr int CH_SW = 32;           // owned output columns per strip
-constexpr int CH_R = 16;            // owned output rows per strip
-constexpr int CH_COLS = 52;         // LDS columns (image column c0 - 5 + j)
-constexpr int CH_BP = 64 + 8;       // base pixel pitch (bf16)
-constexpr int CH_OP = 16 + 8;       // 16-channel ring pixel pitch
-constexpr int CH_RB = 10;           // base ring rows
-constexpr int CH_R1 = 8, CH_R2 = 6, CH_R3 = 4;  // ring rows of levels 1..3
-constexpr int CH_STEPS = CH_R + 9;
+constexpr int RC_W = 64;                         // widest image row (4 fragments)
+constexpr int RC_COLS = RC_W + 2;                // LDS pixel slots per row: image columns -1 .. 64
+constexpr int RC_XP = 64 + 16;                   // base pixel pitch (bf16): == 16 (mod 32), conflict-free b128 reads
+constexpr int RC_DP = 48;                        // dense pixel pitch: out1 | out2 | out3 (== 16 mod 32)
+constexpr int RC_XD = 10;                        // base ring rows (y1-7 .. y1+1 read, y1+2 staged)
+constexpr int RC_DD = 8;                         // dense ring rows (y1-7 .. y1-1 read, y1 written)
+constexpr int RC_XROW = RC_COLS * RC_XP;
+constexpr int RC_DROW = RC_COLS * RC_DP;
+constexpr int RC_OFF_D = RC_XD * RC_XROW;        // elements
+constexpr int RC_LDS = (RC_OFF_D + RC_DD * RC_DROW) * 2;  // 156,288 B
+constexpr int RC_XCH = RC_COLS * 8;              // 16 B chunks of one base row (528)
 
 struct ChainArgs {
-  const uint16_t* base;  // bf16 NHWC, 64 channels at boff
+  const uint16_t* base;
   int bcs, boff;
-  uint16_t* out;         // bf16 NHWC; level L writes 16 channels at ooff[L-1]
+  uint16_t* out;
   int ocs;
   int ooff[4];
-  const uint16_t* wt[4];  // packed [16][9*KP_L] (k = tap*KP_L + c), channel order base | out1 | out2 | out3
-  const float* bias[4];  // forward: conv biases; pull: null
-  const uint16_t* mask;  // pull: activation outputs x_j (act 3), level L uses channels moff[L-1]
+  const uint16_t* wt[4];  // packed [16][9*KP_L], k = tap*KP_L + channel (base | out1 | out2 | out3)
+  const float* bias[4];
+  const uint16_t* mask;
   int mcs;
   int moff[4];
-  int act;               // 1 = leaky relu (forward), 3 = leaky relu backward with mask
   float slope;
-  int n, h, w, strips_x, strips_y;
+  int n, h, w, rows, strips_y;
+  uint32_t base_bytes, mask_bytes;
 };
 
 __host__ __device__ constexpr int kp_blocks(int L) { return L == 1 ? 2 : (L == 4 ? 4 : 3); }
+__host__ __device__ constexpr int nd_blocks(int L) { return L == 1 ? 0 : (L == 2 ? 5 : (L == 3 ? 9 : 14)); }
+__host__ __device__ constexpr int n_blocks(int L) { return 18 + nd_blocks(L); }
 
-// LDS layout (bf16 elements)
-constexpr int OFF_BASE = 0;
-constexpr int OFF_R1 = OFF_BASE + CH_RB * CH_COLS * CH_BP;
-constexpr int OFF_R2 = OFF_R1 + CH_R1 * CH_COLS * CH_OP;
-constexpr int OFF_R3 = OFF_R2 + CH_R2 * CH_COLS * CH_OP;
-constexpr int OFF_ZERO = OFF_R3 + CH_R3 * CH_COLS * CH_OP;
-constexpr int LDS_ELEMS = OFF_ZERO + 40 * CH_OP;  // zero block covers every fragment offset
+// The (tap, channel offset in the dense pixel) of lane group g in dense block j of level L; tap < 0: padding
+// (zero weights; the B read goes to tap 8 of the same block so every value read is finite).
+__device__ __forceinline__ void dense_src(int L, int j, int g, int& tap, int& ch) {
+  if (L == 3 || (L == 4 && j < 9)) {
+    tap = j;
+    ch = 8 * g;
+  } else {
+    const int p = L == 2 ? j : j - 9;
+    tap = 2 * p + (g >> 1);
+    ch = (L == 2 ? 0 : 32) + 8 * (g & 1);
+    if (tap > 8) tap = -1;
+  }
+}
 
-__device__ __forceinline__ int wrap(int r, int m) { return ((r % m) + m) % m; }
+// Weight image in LDS during the prologue: level L's packed [16][9*KP] rows at element offset rc_woff(L), row pitch
+// 9*KP + 8 (the 16 B pad makes the 16 rows of a fragment read hit distinct banks).
+__host__ __device__ constexpr int rc_wpitch(int L) { return 9 * kp_blocks(L) * 32 + 8; }
+__host__ __device__ constexpr int rc_woff(int L) { return L <= 1 ? 0 : rc_woff(L - 1) + 16 * rc_wpitch(L - 1); }
+static_assert(rc_woff(5) * 2 <= RC_LDS, "weight image exceeds the LDS");
 
-// One level's row: acc over its K blocks, 3 frags of 16 columns (level 4: 2)
-// Fragments [F0, F0 + NF) of level L's row y (a level computes 3 fragments of 16 columns, level 4 two)
-template <int L, int F0, int NF>
-__device__ __forceinline__ void level_row(const ChainArgs& a, const uint16_t* lds, uint16_t* ldsw, const bf16x8 (&af)[9][4],
-                                          int lane, int nimg, int r0, int c0, int y, const uint2 (&mk)[2]) {
-  constexpr int NB = kp_blocks(L);
-  constexpr int col0 = (L == 4 ? 5 : L) + 16 * F0;  // first LDS column of this wave's fragments
-  const int g = lane >> 4, col = lane & 15;
-  f32x4 acc[NF];
+// All four levels' packed weights -> LDS, each byte once per workgroup, 16 B per lane, every load of the copy in
+// flight before the first store (two waves per level would otherwise each fetch it from L2 in 64 B pieces).
+template <int L>
+__device__ __forceinline__ void stage_issue(const ChainArgs& a, int tid, uint4 (&v)[5]) {
+  constexpr int CPR = 9 * kp_blocks(L) * 4, NI = (16 * CPR + 511) / 512;  // 16 B chunks per packed row
 #pragma unroll
-  for (int f = 0; f < NF; ++f) acc[f] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int ky = 0; ky < 3; ++ky) {
-    const int yy = y + ky - 1;
-    const int sb = wrap(yy, CH_RB), s1 = wrap(yy, CH_R1), s2 = wrap(yy, CH_R2), s3 = wrap(yy, CH_R3);
-    // per-lane row pointers of this ky; every (kx, fragment, block) read is then a compile-time offset
-    const int cc = col0 + col - 1;
-    const uint16_t* pb = lds + OFF_BASE + (sb * CH_COLS + cc) * CH_BP + g * 8;
-    const uint16_t* p2 = g < 2 ? lds + OFF_R1 + (s1 * CH_COLS + cc) * CH_OP + g * 8
-                               : (L >= 3 ? lds + OFF_R2 + (s2 * CH_COLS + cc) * CH_OP + (g - 2) * 8 : lds + OFF_ZERO);
-    const uint16_t* p3 = g < 2 ? lds + OFF_R3 + (s3 * CH_COLS + cc) * CH_OP + g * 8 : lds + OFF_ZERO;
-#pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
-      bf16x8 b[NB][NF];
-#pragma unroll
-      for (int f = 0; f < NF; ++f) {
-        const int dx = kx + 16 * f;
-#pragma unroll
-        for (int blk = 0; blk < NB; ++blk) {
-          if (blk < 2) b[blk][f] = *(const bf16x8*)(pb + dx * CH_BP + blk * 32);
-          else if (blk == 2) b[blk][f] = *(const bf16x8*)(p2 + dx * CH_OP);
-          else b[blk][f] = *(const bf16x8*)(p3 + dx * CH_OP);
-        }
-      }
-#pragma unroll
-      for (int blk = 0; blk < NB; ++blk)
-#pragma unroll
-        for (int f = 0; f < NF; ++f)
-          acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ky * 3 + kx][blk], b[blk][f], acc[f], 0, 0, 0);
-    }
+  for (int i = 0; i < NI; ++i) {
+    const int q = tid + 512 * i;
+    v[i] = *(const uint4*)(a.wt[L - 1] + (long)(q < 16 * CPR ? q : 0) * 8);  // (unconditional: no branch per load)
   }
-  // epilogue: lane holds channels 4g..4g+3 of column col0 + 16 f + col, row y
-  const int co = 4 * g;
-  float bb[4] = {0.f, 0.f, 0.f, 0.f};
-  if (a.bias[L - 1]) {
-    const float4 t = *(const float4*)(a.bias[L - 1] + co);
-    bb[0] = t.x; bb[1] = t.y; bb[2] = t.z; bb[3] = t.w;
-  }
-  const bool row_in = y >= 0 && y < a.h;
-  const bool own_row = y >= r0 && y < r0 + CH_R && row_in;
-  uint16_t* ring = L == 1 ? ldsw + OFF_R1 : (L == 2 ? ldsw + OFF_R2 : ldsw + OFF_R3);
-  const int rs = L == 1 ? CH_R1 : (L == 2 ? CH_R2 : CH_R3);
+}
+template <int L>
+__device__ __forceinline__ void stage_store(uint16_t* lds, int tid, const uint4 (&v)[5]) {
+  constexpr int CPR = 9 * kp_blocks(L) * 4, NI = (16 * CPR + 511) / 512;
 #pragma unroll
-  for (int f = 0; f < NF; ++f) {
-    const int cx = col0 + 16 * f + col;
-    const int ix = c0 - 5 + cx;
-    const bool in = row_in && ix >= 0 && ix < a.w;
-    float v[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float t = acc[f][i] + bb[i];
-      if (a.act == 1) t = t > 0.f ? t : t * a.slope;
-      else if (a.act == 3) {
-        const uint32_t mw = i < 2 ? mk[f].x : mk[f].y;
-        const float m = bf2f((uint16_t)((i & 1) ? (mw >> 16) : mw));
-        t = m > 0.f ? t : t * a.slope;
-      }
-      v[i] = in ? t : 0.f;  // outside the image: zero padding for the next levels
-    }
-    uint2 pk;
-    pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-    pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-    if (L < 4) *(uint2*)(ring + (wrap(y, rs) * CH_COLS + cx) * CH_OP + co) = pk;
-    if (own_row && in && cx >= 5 && cx < 5 + CH_SW)
-      *(uint2*)(a.out + (((long)nimg * a.h + y) * a.w + ix) * a.ocs + a.ooff[L - 1] + co) = pk;
+  for (int i = 0; i < NI; ++i) {
+    const int q = tid + 512 * i, row = q / CPR, c = q - row * CPR;
+    if (q < 16 * CPR) *(uint4*)(lds + rc_woff(L) + row * rc_wpitch(L) + c * 8) = v[i];
   }
+}
+__device__ __forceinline__ void stage_weights(const ChainArgs& a, uint16_t* lds, int tid) {
+  uint4 v1[5], v2[5], v3[5], v4[5];
+  stage_issue<1>(a, tid, v1);
+  stage_issue<2>(a, tid, v2);
+  stage_issue<3>(a, tid, v3);
+  stage_issue<4>(a, tid, v4);
+  stage_store<1>(lds, tid, v1);
+  stage_store<2>(lds, tid, v2);
+  stage_store<3>(lds, tid, v3);
+  stage_store<4>(lds, tid, v4);
 }
 
 template <int L>
-__device__ __forceinline__ void load_af(const ChainArgs& a, int lane, bf16x8 (&af)[9][4]) {
-  constexpr int NB = kp_blocks(L), KP = NB * 32;
+__device__ __forceinline__ void load_af(const uint16_t* lds, int lane, bf16x8 (&af)[n_blocks(L)]) {
+  constexpr int KP = kp_blocks(L) * 32;
   const int g = lane >> 4, col = lane & 15;
+  const uint16_t* wr = lds + rc_woff(L) + col * rc_wpitch(L);
 #pragma unroll
-  for (int t = 0; t < 9; ++t)
+  for (int j = 0; j < 18; ++j) af[j] = *(const bf16x8*)(wr + (j >> 1) * KP + (j & 1) * 32 + g * 8);
 #pragma unroll
-    for (int blk = 0; blk < 4; ++blk)
-      af[t][blk] = blk < NB ? *(const bf16x8*)(a.wt[L - 1] + (long)col * 9 * KP + t * KP + blk * 32 + g * 8) : (bf16x8){};
-}
-
-// mask (act 3) of level L's row y for this lane's 3 fragments, loaded before the MFMAs of the step
-template <int L, int F0, int NF>
-__device__ __forceinline__ void load_mask(const ChainArgs& a, int lane, int nimg, int c0, int y, uint2 (&mk)[2]) {
-  constexpr int col0 = (L == 4 ? 5 : L) + 16 * F0;
-  const int g = lane >> 4, col = lane & 15;
-#pragma unroll
-  for (int f = 0; f < 2; ++f) {
-    mk[f] = make_uint2(0, 0);
-    const int ix = c0 - 5 + col0 + 16 * f + col;
-    if (f < NF && a.act == 3 && y >= 0 && y < a.h && ix >= 0 && ix < a.w)
-      mk[f] = *(const uint2*)(a.mask + (((long)nimg * a.h + y) * a.w + ix) * a.mcs + a.moff[L - 1] + 4 * g);
+  for (int j = 0; j < nd_blocks(L); ++j) {
+    int tap, ch;
+    dense_src(L, j, g, tap, ch);
+    af[18 + j] = tap >= 0 ? *(const bf16x8*)(wr + tap * KP + 64 + ch) : (bf16x8){};
   }
 }
 
-// Wave w (8 per workgroup, two per SIMD) computes level (w & 3) + 1; w < 4 takes its first two fragments
-// (level 4: the first), w >= 4 the rest.
-template <int L, int HALF>
-__device__ __forceinline__ void wave_step(const ChainArgs& a, uint16_t* lds, const bf16x8 (&af)[9][4], int lane, int nimg, int r0,
-                                          int c0, int y) {
-  constexpr int F0 = HALF == 0 ? 0 : (L == 4 ? 1 : 2);
-  constexpr int NF = HALF == 0 ? (L == 4 ? 1 : 2) : 1;
-  uint2 mk[2];
-  load_mask<L, F0, NF>(a, lane, nimg, c0, y, mk);
-  level_row<L, F0, NF>(a, lds, lds, af, lane, nimg, r0, c0, y, mk);
+// One level row, two column fragments (16 pixels apart): acc0/acc1 = sum over the level's blocks.  xr[ky] / dr[ky]:
+// LDS element offsets of the base / dense ring rows y-1+ky; lx / ld / lp: this lane's pixel-column (+ channel
+// group) offsets within a row.  Every A fragment feeds two independent accumulators.
+template <int L>
+__device__ __forceinline__ const uint16_t* block_src(const uint16_t* lds, const int (&xr)[3], const int (&dr)[3], int lx,
+                                                     int ld, int lp, int g, int j) {
+  if (j < 18) {
+    const int t = j >> 1, ky = t / 3, kx = t % 3;
+    return lds + xr[ky] + lx + kx * RC_XP + (j & 1) * 32;
+  }
+  j -= 18;
+  int off;
+  if (L == 3 || (L == 4 && j < 9)) {
+    off = dr[j / 3] + ld + (j % 3) * RC_DP;
+  } else {
+    const int p = L == 2 ? j : j - 9;
+    const int ta = 2 * p, tb = 2 * p + 1 <= 8 ? 2 * p + 1 : 2 * p;
+    const int oa = dr[ta / 3] + (ta % 3) * RC_DP, ob = dr[tb / 3] + (tb % 3) * RC_DP;
+    off = (g >= 2 ? ob : oa) + lp + (L == 2 ? 0 : 32);
+  }
+  return lds + RC_OFF_D + off;
 }
 
+// Blocks run in groups of rc_group(L): the B fragments of group k+1 are read while group k is on the MFMA pipe, so
+// 2 x rc_group reads stay in flight (the group size is what each level's weight registers leave room for).
+__host__ __device__ constexpr int rc_group(int L) { return L <= 2 ? 6 : (L == 3 ? 5 : 4); }
+
+template <int L>
+__device__ __forceinline__ void level_acc(const uint16_t* lds, const bf16x8 (&af)[n_blocks(L)], const int (&xr)[3],
+                                          const int (&dr)[3], int lx, int ld, int lp, int g, f32x4& acc0, f32x4& acc1) {
+  constexpr int NB = n_blocks(L), G = rc_group(L), NG = (NB + G - 1) / G;
+  acc0 = (f32x4){0.f, 0.f, 0.f, 0.f};
+  acc1 = acc0;
+  bf16x8 b[2][G][2];
+  auto load = [&](int gi, bf16x8 (&bb)[G][2]) {
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const int j = gi * G + i;
+      if (j < NB) {
+        const uint16_t* p = block_src<L>(lds, xr, dr, lx, ld, lp, g, j);
+        bb[i][0] = *(const bf16x8*)p;
+        bb[i][1] = *(const bf16x8*)(p + (j < 18 ? 16 * RC_XP : 16 * RC_DP));  // the second fragment: 16 pixels on
+      }
+    }
+  };
+  load(0, b[0]);
+#pragma unroll
+  for (int gi = 0; gi < NG; ++gi) {
+    if (gi + 1 < NG) load(gi + 1, b[(gi + 1) & 1]);
+    __builtin_amdgcn_sched_barrier(0);  // the next group's reads go out before this group's MFMAs
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const int j = gi * G + i;
+      if (j < NB) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], b[gi & 1][i][0], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], b[gi & 1][i][1], acc1, 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+__device__ __forceinline__ int xslot(int y) { return (y + 4 * RC_XD) % RC_XD; }  // y >= -8
+__device__ __forceinline__ int dslot(int y) { return (y + 4 * RC_DD) & (RC_DD - 1); }
+
+__device__ __forceinline__ uint32_t pack2_bf16(float a, float b) {
+  const bf16x2 v = {(__bf16)a, (__bf16)b};  // v_cvt_pk_bf16_f32 (RNE)
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+// The whole strip walk of one wave: level L, column fragments 2h and 2h+1.  Every wave runs the same step loop
+// (base-row staging + one barrier per step); level L computes in steps 3(L-1) .. R+4+L.
+// MODE 0: forward (bias + leaky relu); 1: pull (leaky-relu derivative of the stored activation, no bias).
+// Address arithmetic is split into per-lane constants (computed once) and per-step wave-uniform row offsets.
+template <int MODE, int L>
+__device__ __forceinline__ void run_level(const ChainArgs& a, uint16_t* lds, int tid, int nimg, int r0) {
+  const int lane = tid & 63, g = lane >> 4, col = lane & 15, h = tid >> 8;
+  const int px0 = 32 * h + col;                  // this lane's image column in fragment 2h (fragment 2h+1: + 16)
+  const bool live0 = 32 * h < a.w, live1 = 32 * h + 16 < a.w;
+  const __amdgpu_buffer_rsrc_t br = buf_rsrc(a.base, a.base_bytes);
+  const __amdgpu_buffer_rsrc_t mr = buf_rsrc(a.mask, MODE == 1 ? a.mask_bytes : 0u);
+  const int R = a.rows, row0 = nimg * a.h;       // row0: this image's first row in the batch
+
+  // base row staging: chunk q = tid (+ 512) of a row is (slot q / 8 = image column + 1, 16 B channel group q % 8)
+  int xg[2], xl[2];  // byte offset within a base row in HBM (-1: zero chunk) / element offset within a ring row (-1: none)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = tid + 512 * i, p = q >> 3, c = q & 7, ix = p - 1;
+    xl[i] = q < RC_XCH ? p * RC_XP + c * 8 : -1;
+    xg[i] = q < RC_XCH && ix >= 0 && ix < a.w ? (ix * a.bcs + a.boff + c * 8) * 2 : -1;
+  }
+  const uint32_t xrow_bytes = (uint32_t)(a.w * a.bcs * 2);
+  auto issue_row = [&](int y, uint4 (&v)[2]) {
+    const bool rok = y >= 0 && y < a.h;
+    const uint32_t rb = (uint32_t)(row0 + y) * xrow_bytes;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) v[i] = buf_load16(br, rok && xg[i] >= 0 ? rb + (uint32_t)xg[i] : BUF_OOB);
+  };
+  auto store_row = [&](int y, const uint4 (&v)[2]) {
+    uint16_t* row = lds + xslot(y) * RC_XROW;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      if (xl[i] >= 0) *(uint4*)(row + xl[i]) = v[i];
+  };
+  // pull: the activation x_j of this level's row in step s for both fragments (zeros outside), one step ahead
+  int ml[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int px = px0 + 16 * k;
+    ml[k] = px < a.w ? (px * a.mcs + a.moff[L - 1] + 4 * g) * 2 : -1;
+  }
+  const uint32_t mrow_bytes = (uint32_t)(a.w * a.mcs * 2);
+  auto issue_mask = [&](int s, uint2 (&m)[2]) {
+    const int y = r0 - 3 + s - 2 * (L - 1);
+    const bool rok = y >= 0 && y < a.h;
+    const uint32_t rb = (uint32_t)(row0 + y) * mrow_bytes;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b64(mr, rok && ml[k] >= 0 ? rb + (uint32_t)ml[k] : BUF_OOB, 0, 0);
+      m[k] = make_uint2(v[0], v[1]);
+    }
+  };
+  // Prologue (the weight image is already in LDS, see the kernel): the first base rows are in flight while each wave
+  // copies its level's A fragments into registers; the image is then overwritten by the rings.
+  // Base rows are loaded one step before the step that stores them (two steps before their first use) and masks
+  // one step before their use; the loop is unrolled x2 with alternating register sets, so no register copy of a
+  // load still in flight (which would wait for it) is ever needed.
+  uint4 v0[2], v1[2], v2[2], ra[2], rb[2];
+  issue_row(r0 - 4, v0);
+  issue_row(r0 - 3, v1);
+  issue_row(r0 - 2, v2);
+  issue_row(r0 - 1, ra);
+  uint2 ma[2] = {}, mb[2] = {};
+  if constexpr (MODE == 1) issue_mask(0, ma);
+  const float4 bias = MODE == 0 ? *(const float4*)(a.bias[L - 1] + 4 * g) : make_float4(0.f, 0.f, 0.f, 0.f);
+  bf16x8 af[n_blocks(L)];
+  load_af<L>(lds, lane, af);
+  lds_barrier();  // every wave holds its fragments
+  // dense ring: the slots of image columns -1 and >= w are never written, they are the zero padding
+  for (int i = tid; i < RC_DD * (RC_COLS - a.w) * (RC_DP / 8); i += 512) {
+    const int c = i % (RC_DP / 8), k = (i / (RC_DP / 8)) % (RC_COLS - a.w), r = i / (RC_DP / 8) / (RC_COLS - a.w);
+    const int p = k == 0 ? 0 : a.w + k;
+    *(uint4*)(lds + RC_OFF_D + r * RC_DROW + p * RC_DP + c * 8) = make_uint4(0, 0, 0, 0);
+  }
+  store_row(r0 - 4, v0);
+  store_row(r0 - 3, v1);
+  store_row(r0 - 2, v2);
+  lds_barrier();
+  // retire the remaining loads here: with no VMEM result carried into the loop, hipcc's wait counting inside it
+  // stays exact (otherwise every step waits with a count that also drains the base-row prefetch)
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+
+  const int lx = px0 * RC_XP + 8 * g;  // + kx * RC_XP: input column px - 1 + kx sits in slot px + kx
+  const int ld = px0 * RC_DP + 8 * g;
+  const int lp = px0 * RC_DP + 8 * (g & 1);
+  const int dl = (px0 + 1) * RC_DP + 16 * (L - 1) + 4 * g;    // this lane's dense-ring store (fragment 2h)
+  const int ol = px0 * a.ocs + a.ooff[L - 1] + 4 * g;          // and HBM store, elements within an image row
+  const long orow = (long)a.w * a.ocs;
+  const float bb[4] = {bias.x, bias.y, bias.z, bias.w};
+  // step s: `cur` holds base row y1 + 2 (stored after the MFMAs), `nxt` receives row y1 + 3; `mcur` = this step's
+  // masks, `mnxt` receives the next step's
+  auto step = [&](int s, uint4 (&cur)[2], uint4 (&nxt)[2], const uint2 (&mcur)[2], uint2 (&mnxt)[2]) {
+    const int y1 = r0 - 3 + s;
+    issue_row(y1 + 3, nxt);
+    if constexpr (MODE == 1) issue_mask(s + 1, mnxt);
+    if (live0 && s >= 3 * (L - 1) && s <= R + 4 + L) {
+      const int y = y1 - 2 * (L - 1);
+      int xr[3], dr[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        xr[k] = xslot(y - 1 + k) * RC_XROW;
+        dr[k] = dslot(y - 1 + k) * RC_DROW;
+      }
+      f32x4 acc[2];
+      level_acc<L>(lds, af, xr, dr, lx, ld, lp, g, acc[0], acc[1]);
+      const bool in = y >= 0 && y < a.h;  // rows outside the image: zeros, the next level's padding
+      const bool own = in && y >= r0 && y < r0 + R;
+      uint16_t* drow = lds + RC_OFF_D + dslot(y) * RC_DROW + dl;
+      uint16_t* grow = a.out + (row0 + y) * orow + ol;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        if (k == 1 && !live1) break;
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float t = acc[k][i] + bb[i];
+          if (MODE == 0) {
+            v[i] = fmaxf(t, t * a.slope);  // leaky relu, 0 <= slope <= 1 (checked on the host)
+          } else {
+            const uint32_t mw = i < 2 ? mcur[k].x : mcur[k].y;
+            const float m = __uint_as_float((i & 1) ? (mw & 0xFFFF0000u) : (mw << 16));  // the stored activation
+            v[i] = m > 0.f ? t : t * a.slope;
+          }
+        }
+        uint2 pk = make_uint2(pack2_bf16(v[0], v[1]), pack2_bf16(v[2], v[3]));
+        if (!in) pk = make_uint2(0, 0);
+        if (L < 4) *(uint2*)(drow + 16 * k * RC_DP) = pk;
+        if (own) *(uint2*)(grow + 16 * k * a.ocs) = pk;
+      }
+    }
+    store_row(y1 + 2, cur);  // its slot held row y1 - 8, which no level reads in this step
+    lds_barrier();
+  };
+  for (int s = 0; s < R + 9; s += 2) {
+    step(s, ra, rb, ma, mb);
+    if (s + 1 < R + 9) step(s + 1, rb, ra, mb, ma);
+  }
+}
+
+// Wave w computes level (w & 3) + 1 (waves w and w + 4 share a SIMD: each SIMD carries one level), fragments
+// 2 (w >> 2) and 2 (w >> 2) + 1.
+template <int MODE>
 __global__ __launch_bounds__(512, 1) void rdb_chain_kernel(ChainArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint16_t* lds = (uint16_t*)smem;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  int bid = blockIdx.x;
-  const int sx = bid % a.strips_x;
-  bid /= a.strips_x;
-  const int sy = bid % a.strips_y;
-  const int nimg = bid / a.strips_y;
-  const int c0 = sx * CH_SW, r0 = sy * CH_R;
-  const int L = (wave & 3) + 1;
-
-  for (int i = tid; i < LDS_ELEMS / 8; i += 512) *(uint4*)(lds + i * 8) = make_uint4(0, 0, 0, 0);
-
-  bf16x8 af[9][4];
-  switch (L) {
-    case 1: load_af<1>(a, lane, af); break;
-    case 2: load_af<2>(a, lane, af); break;
-    case 3: load_af<3>(a, lane, af); break;
-    default: load_af<4>(a, lane, af); break;
-  }
-
-  // base staging: one LDS row = CH_COLS x 8 vectors (416), one per thread
-  auto load_base = [&](int yy, uint4& pre) {
-    const int cx = tid >> 3, cg = tid & 7;
-    const int ix = c0 - 5 + cx;
-    pre = make_uint4(0, 0, 0, 0);
-    if (tid < CH_COLS * 8 && yy >= 0 && yy < a.h && ix >= 0 && ix < a.w)
-      pre = *(const uint4*)(a.base + (((long)nimg * a.h + yy) * a.w + ix) * a.bcs + a.boff + cg * 8);
-  };
-  auto store_base = [&](int yy, const uint4& pre) {
-    if (tid < CH_COLS * 8) *(uint4*)(lds + OFF_BASE + (wrap(yy, CH_RB) * CH_COLS + (tid >> 3)) * CH_BP + (tid & 7) * 8) = pre;
-  };
-  __syncthreads();  // zero fill done
-  // prologue: base rows r0-4 .. r0-2 (level 1's first row r0-3 reads r0-4..r0-2)
-  for (int yy = r0 - 4; yy <= r0 - 2; ++yy) {
-    uint4 pre;
-    load_base(yy, pre);
-    store_base(yy, pre);
-  }
-  uint4 pa, pb;  // base rows for steps s+1 and s+2
-  load_base(r0 - 1, pa);
-  load_base(r0, pb);
-  __syncthreads();
-
-  for (int s = 0; s < CH_STEPS; ++s) {
-    // level L computes row y_L = r0 - 3 + s - 2(L-1) during steps 3L-3 .. R+L+4
-    const int y = r0 - 3 + s - 2 * (L - 1);
-    if (s >= 3 * L - 3 && s <= CH_R + L + 4) {
-      switch (wave) {
-        case 0: wave_step<1, 0>(a, lds, af, lane, nimg, r0, c0, y); break;
-        case 1: wave_step<2, 0>(a, lds, af, lane, nimg, r0, c0, y); break;
-        case 2: wave_step<3, 0>(a, lds, af, lane, nimg, r0, c0, y); break;
-        case 3: wave_step<4, 0>(a, lds, af, lane, nimg, r0, c0, y); break;
-        case 4: wave_step<1, 1>(a, lds, af, lane, nimg, r0, c0, y); break;
-        case 5: wave_step<2, 1>(a, lds, af, lane, nimg, r0, c0, y); break;
-        case 6: wave_step<3, 1>(a, lds, af, lane, nimg, r0, c0, y); break;
-        default: wave_step<4, 1>(a, lds, af, lane, nimg, r0, c0, y); break;
-      }
-    }
-    // base row needed from step s+1 on (level 1 at step s+1 reads up to row r0 - 1 + s)
-    store_base(r0 - 1 + s, pa);
-    pa = pb;
-    load_base(r0 + 1 + s, pb);
-    __syncthreads();
+  const int tid = threadIdx.x;
+  const int nimg = blockIdx.x / a.strips_y, r0 = (blockIdx.x % a.strips_y) * a.rows;
+  stage_weights(a, lds, tid);
+  lds_barrier();
+  switch ((tid >> 6) & 3) {
+    case 0: run_level<MODE, 1>(a, lds, tid, nimg, r0); break;
+    case 1: run_level<MODE, 2>(a, lds, tid, nimg, r0); break;
+    case 2: run_level<MODE, 3>(a, lds, tid, nimg, r0); break;
+    default: run_level<MODE, 4>(a, lds, tid, nimg, r0); break;
   }
 }
 
 }  // namespace
 
 extern "C" int climsr_rdb_chain(const ClimsrChainDesc* d, void* stream) {
-  if (!d || !d->base || !d->out || d->n <= 0 || d->h <= 0 || d->w <= 0 || d->bcs % 8 || d->boff % 8 || d->ocs % 4 ||
-      (d->act != 1 && d->act != 3) || (d->act == 3 && (!d->mask || d->mcs % 4))) {
-    set_error("rdb_chain: bad args");
+  if (!d || !d->base || !d->out || d->n <= 0 || d->h <= 0 || d->w <= 0 || d->w > RC_W || d->w % 16 || d->bcs % 8 ||
+      d->boff % 8 || d->ocs % 4 || (d->act != 1 && d->act != 3) || (d->act == 3 && (!d->mask || d->mcs % 4)) ||
+      !(d->slope >= 0.f && d->slope <= 1.f)) {
+    set_error("rdb_chain: bad args (width must be 16, 32, 48 or 64)");
     return CLIMSR_EINVAL;
   }
   for (int L = 0; L < 4; ++L) {
-    if (!d->wt[L] || d->ooff[L] % 4 || (d->act == 3 && d->moff[L] % 4)) {
+    if (!d->wt[L] || d->ooff[L] % 4 || (d->act == 1 && !d->bias[L]) || (d->act == 3 && d->moff[L] % 4)) {
       set_error("rdb_chain: bad level %d", L + 1);
       return CLIMSR_EINVAL;
     }
+  }
+  const long px = (long)d->n * d->h * d->w;
+  if (px * d->bcs * 2 >= (1L << 31) || (d->act == 3 && px * d->mcs * 2 >= (1L << 31))) {
+    set_error("rdb_chain: tensors over 2 GiB");
+    return CLIMSR_EINVAL;
   }
   ChainArgs a;
   a.base = d->base; a.bcs = d->bcs; a.boff = d->boff;
@@ -260,17 +380,40 @@ extern "C" int climsr_rdb_chain(const ClimsrChainDesc* d, void* stream) {
     a.bias[L] = d->bias[L];
     a.moff[L] = d->moff[L];
   }
-  a.act = d->act; a.slope = d->slope;
+  a.slope = d->slope;
   a.n = d->n; a.h = d->h; a.w = d->w;
-  a.strips_x = ceil_div(d->w, CH_SW);
-  a.strips_y = ceil_div(d->h, CH_R);
-  const size_t lds = (size_t)LDS_ELEMS * 2;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)rdb_chain_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
+  a.base_bytes = (uint32_t)(px * d->bcs * 2);
+  a.mask_bytes = d->act == 3 ? (uint32_t)(px * d->mcs * 2) : 0u;
+  // strip height: enough strips to give every CU one (a strip recomputes 3 + 2 + 1 halo rows per level chain)
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (ncu <= 0) ncu = 256;
   }
-  hipLaunchKernelGGL(rdb_chain_kernel, dim3(a.strips_x * a.strips_y * a.n), dim3(512), lds, (hipStream_t)stream, a);
+  int rows = ceil_div((long)d->n * d->h, ncu);
+  if (rows < 2) rows = 2;
+  if (rows > 32) rows = 32;
+  if (rows > d->h) rows = d->h;
+  a.rows = rows;
+  a.strips_y = ceil_div(d->h, rows);
+  const bool fwd = d->act == 1;
+  if (fwd) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)rdb_chain_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, RC_LDS);
+      attr = true;
+    }
+    hipLaunchKernelGGL(rdb_chain_kernel<0>, dim3(a.strips_y * a.n), dim3(512), RC_LDS, (hipStream_t)stream, a);
+  } else {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)rdb_chain_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, RC_LDS);
+      attr = true;
+    }
+    hipLaunchKernelGGL(rdb_chain_kernel<1>, dim3(a.strips_y * a.n), dim3(512), RC_LDS, (hipStream_t)stream, a);
+  }
   return check_launch("rdb_chain");
 }
 

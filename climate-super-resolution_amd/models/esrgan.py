@@ -17,7 +17,6 @@ node whose arithmetic is entirely HIP (libclimsr_hip.so):
 """
 from __future__ import annotations
 
-import os
 from typing import Dict, List, Optional
 
 import torch
@@ -114,11 +113,10 @@ class _Engine:
             # RDB convs need no transposed weights: their data gradients run as pull convs (below)
             p.bind(conv.weight, conv.bias, need_t=(name != "conv_first" and ".RDB" not in name))
         dev = gen.conv_first.weight.device
-        # conv1..conv4 of every RDB (and their pull gradients) as one fused row-streaming launch each (nf 64, gc 16).
-        # Measured slower than the four conv_n16 launches so far (barrier-bound: the four levels' work per step is
-        # unequal), so it is opt-in (CLIMSR_RDB_CHAIN=1) and parity-tested against the per-conv path.
+        # conv1..conv4 of every RDB (and their pull gradients) as one fused row-streaming launch each (nf 64, gc 16,
+        # image width 16/32/48/64: csrc/rdb_chain.hip); other widths run the four convs one by one (conv_n16)
         self.chains: List[RdbChain] = []
-        if nf == 64 and gc == 16 and os.environ.get("CLIMSR_RDB_CHAIN") == "1":
+        if nf == 64 and gc == 16:
             for i in range(3 * self.nb):
                 blk, r = divmod(i, 3)
                 self.chains.append(RdbChain([self.plans[self.rdb_name(blk, r + 1, k)] for k in range(1, 6)],
@@ -141,6 +139,9 @@ class _Engine:
             self.pulls.append(lst)
         self.pull_packer = PullPacker([p for lst in self.pulls for p in (lst[:1] if self.chains else lst)], dev,
                                       [d for ch in self.chains for d in ch.pull_descs()])
+        # the per-conv pulls 4..1 are packed only once a backward at a width the chain does not take needs them
+        self.pull_packer_rest = PullPacker([p for lst in self.pulls for p in lst[1:]], dev) if self.chains else None
+        self.pull_rest_on = False
         # the five weight gradients of an RDB: one GEMM over dZ (all dc channels) x the dense buffer (dc channels)
         self.rdb_wgrads: List[GroupedWgrad] = []
         for i in range(3 * self.nb if self.dc % 64 == 0 else 0):
@@ -160,12 +161,19 @@ class _Engine:
         if v != self.version:
             self.packer.run()
             self.pull_packer.run()
+            if self.pull_rest_on:
+                self.pull_packer_rest.run()
             self.version = v
 
     def repack(self):
         self.packer.run()
         self.pull_packer.run()
+        if self.pull_rest_on:
+            self.pull_packer_rest.run()
         self.version = self.gen._flat._version
+
+    def chain_ok(self, w: int) -> bool:
+        return bool(self.chains) and w % 16 == 0 and w <= 64
 
     def rdb_name(self, i, r, c):
         return f"RRDB_trunk.{i}.RDB{r}.conv{c}"
@@ -204,7 +212,7 @@ class _Engine:
             dst = dense[i + 1] if keep else dense[(i + 1) % 2]
             if r == 0 and not keep:  # remember the RRDB input for its residual
                 axpby_bf16_copy(src, rrdb_in, n * h * w, nf, dc)
-            if self.chains:
+            if self.chain_ok(w):
                 self.chains[i].forward(src, dc, n, h, w)
             else:
                 for c in range(1, 5):
@@ -312,9 +320,12 @@ class _Engine:
             g_out, g_in, g_skip = G[(i + 1) % 4], G[i % 4], G[(3 * blk + 3) % 4]
             dz, src, pulls = dZ[i % 2], dense[i], self.pulls[i]
             # dZ_j = lrelu'(x_j) * sum_{k>j} conv_k^T(dZ_k)   (x_j = channels nf+(j-1)gc.. of the dense buffer)
-            if self.chains:
+            if self.chain_ok(w):
                 self.chains[i].pull(dz, src, dc, n, h, w)
             else:
+                if self.chains and not self.pull_rest_on:
+                    self.pull_rest_on = True
+                    self.pull_packer_rest.run()
                 for j in (4, 3, 2, 1):
                     pulls[j].fwd(dz, dc, j * gc, h, w, dz, dc, (j - 1) * gc, n, act=ACT_LRELU_BWD, use_bias=False,
                                  res1=src, res1_cs=dc, res1_co=nf + (j - 1) * gc)

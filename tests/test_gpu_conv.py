@@ -340,15 +340,16 @@ def test_rdb_pull_backward_matches_torch():
     check_close(from_nhwc(aux, nf, 4 * gc).cpu(), 0.04 * want, 8e-3, "aux")
 
 
-@pytest.mark.parametrize("h,w", [(16, 32), (37, 45)])
-def test_rdb_chain_matches_per_conv(h, w):
+@pytest.mark.parametrize("n,h,w", [(2, 16, 32), (2, 37, 48), (3, 5, 16), (32, 64, 64)])
+def test_rdb_chain_matches_per_conv(n, h, w):
     """The fused RDB chain (csrc/rdb_chain.hip: conv1..conv4 forward and pull4..pull1 backward in one
-    row-streaming launch with recomputed halos) against the same math run conv by conv (n16 kernel).
+    row-streaming launch, full-width strips with recomputed row halos) against the same math run conv by conv
+    (n16 kernel), including the bench shape (32 x 64 x 64: 256 strips of 8 rows) and strips taller than the image.
     Both are bf16 MFMA with fp32 accumulation; outputs agree to bf16 rounding (1 ulp of the value), the
     chain's level inputs being the same bf16 values the per-conv path reads back from HBM."""
     from climsr_amd.ops import ACT_LRELU_BWD, BatchedPacker, PullPacker, PullPlan, RdbChain
 
-    nf, gc, n = 64, 16, 2
+    nf, gc = 64, 16
     dc = nf + 4 * gc
     gen = torch.Generator().manual_seed(9)
     plans = []
