@@ -25,7 +25,7 @@ def load(d, counter):
         for row in csv.DictReader(open(f)):
             if row.get("Counter_Name") != counter:
                 continue
-            name = row["Kernel_Name"].replace("void ", "").split("(")[0]
+            name = row["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
             tot[name] += float(row["Counter_Value"])
             disp[name].add(row.get("Dispatch_Id", len(disp[name])))
     return {k: (tot[k], len(disp[k])) for k in tot}
