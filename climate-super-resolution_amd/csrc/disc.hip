@@ -68,10 +68,21 @@ static inline BnGrid bn_grid(long npix, int c) {
   return BnGrid{(int)((npix + per - 1) / per), (int)per};
 }
 
-template <int MODE>
+// 8 consecutive channels of an output gradient held as fp32 (32 B) or bf16 (16 B)
+__device__ inline void load_da8(const float* da, size_t off, float* d) {
+  const float4* dp = (const float4*)(da + off);
+  const float4 d0 = dp[0], d1 = dp[1];
+  d[0] = d0.x; d[1] = d0.y; d[2] = d0.z; d[3] = d0.w; d[4] = d1.x; d[5] = d1.y; d[6] = d1.z; d[7] = d1.w;
+}
+__device__ inline void load_da8(const uint16_t* da, size_t off, float* d) { unpack8(*(const uint4*)(da + off), d); }
+
+// BN affine of the forward (bn_apply_kernel): y = z * sc + sh, sc = gamma*rstd, sh = beta - mean*sc, the same
+// fmaf, so sign(y) -- hence lrelu'(a) -- is recomputed bit-identically from z without reading a.
+template <int MODE, typename DA = float>
 __global__ __launch_bounds__(256) void bn_stats_kernel(int npix, int c, int per_blk, const uint16_t* __restrict__ z,
-                                                       const float* __restrict__ da, const uint16_t* __restrict__ a,
+                                                       const DA* __restrict__ da, const uint16_t* __restrict__ a,
                                                        const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
                                                        float slope, double* __restrict__ part) {
   __shared__ float ls[2][2048];  // [sum | sumsq][R][c] (R * c <= 2048)
   const int G = c >> 3;
@@ -81,13 +92,20 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(int npix, int c, int per_
   const int r = tid / G;
   const int p0 = blockIdx.x * per_blk;
   const int p1 = min(p0 + per_blk, npix);
-  float s[8], q[8], mu[8], rs[8];
+  float s[8], q[8], mu[8], rs[8], sc[8], sh[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) { s[i] = 0.f; q[i] = 0.f; mu[i] = 0.f; rs[i] = 0.f; }
+  for (int i = 0; i < 8; ++i) { s[i] = 0.f; q[i] = 0.f; mu[i] = 0.f; rs[i] = 0.f; sc[i] = 0.f; sh[i] = 0.f; }
   if (r < R) {
-    if (MODE == 1) {
+    if (MODE >= 1) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) { mu[i] = mean[cg * 8 + i]; rs[i] = rstd[cg * 8 + i]; }
+    }
+    if (MODE == 2) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        sc[i] = gamma[cg * 8 + i] * rs[i];
+        sh[i] = beta[cg * 8 + i] - mu[i] * sc[i];
+      }
     }
     auto accum = [&](int p) {
       float zf[8];
@@ -96,11 +114,14 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(int npix, int c, int per_
 #pragma unroll
         for (int i = 0; i < 8; ++i) { s[i] += zf[i]; q[i] = fmaf(zf[i], zf[i], q[i]); }
       } else {
-        float af[8];
-        unpack8(*(const uint4*)(a + (size_t)p * c + cg * 8), af);
-        const float4* dp = (const float4*)(da + (size_t)p * c + cg * 8);
-        const float4 d0 = dp[0], d1 = dp[1];
-        const float dd[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+        float af[8], dd[8];
+        if (MODE == 1) {
+          unpack8(*(const uint4*)(a + (size_t)p * c + cg * 8), af);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) af[i] = fmaf(zf[i], sc[i], sh[i]);
+        }
+        load_da8(da, (size_t)p * c + cg * 8, dd);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const float d = af[i] > 0.f ? dd[i] : dd[i] * slope;
@@ -249,9 +270,12 @@ __global__ __launch_bounds__(256) void bn_bwd_finish_kernel(const double* __rest
 
 // dz = gamma*rstd * (d - mean(d) - xhat * mean(d*xhat)), d = da * lrelu'(a); out_slope != 1: z is itself a
 // LeakyReLU output (plain discriminator) and dz carries its derivative too.
-__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(int npix, int c, int per_blk, const float* __restrict__ da,
+// FROM_Z: lrelu'(a) from the recomputed BN output (no read of a; MODE 2 of the statistics kernel).
+template <typename DA = float, bool FROM_Z = false>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(int npix, int c, int per_blk, const DA* __restrict__ da,
                                                            const uint16_t* __restrict__ a, const uint16_t* __restrict__ z,
                                                            const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                           const float* __restrict__ gamma, const float* __restrict__ beta,
                                                            const float* __restrict__ coef, float slope, float out_slope,
                                                            uint16_t* __restrict__ dz) {
   const int G = c >> 3;
@@ -259,7 +283,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(int npix, int c, int 
   const int cg = threadIdx.x % G;
   const int r = threadIdx.x / G;
   if (r >= R) return;
-  float k[8], m1[8], m2[8], mu[8], rs[8];
+  float k[8], m1[8], m2[8], mu[8], rs[8], sc[8], sh[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int ch = cg * 8 + i;
@@ -268,17 +292,22 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(int npix, int c, int 
     m2[i] = coef[2 * c + ch];
     mu[i] = mean[ch];
     rs[i] = rstd[ch];
+    sc[i] = FROM_Z ? gamma[ch] * rs[i] : 0.f;
+    sh[i] = FROM_Z ? beta[ch] - mu[i] * sc[i] : 0.f;
   }
   const int p0 = blockIdx.x * per_blk;
   const int p1 = min(p0 + per_blk, npix);
   auto one = [&](int p) {
     const size_t off = (size_t)p * c + cg * 8;
-    float zf[8], af[8], o[8];
+    float zf[8], af[8], o[8], dd[8];
     unpack8(*(const uint4*)(z + off), zf);
-    unpack8(*(const uint4*)(a + off), af);
-    const float4* dp = (const float4*)(da + off);
-    const float4 d0 = dp[0], d1 = dp[1];
-    const float dd[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+    if (FROM_Z) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) af[i] = fmaf(zf[i], sc[i], sh[i]);
+    } else {
+      unpack8(*(const uint4*)(a + off), af);
+    }
+    load_da8(da, off, dd);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float d = af[i] > 0.f ? dd[i] : dd[i] * slope;
@@ -322,8 +351,8 @@ extern "C" int climsr_bn_forward(const uint16_t* z, int64_t npix, int c, const f
   }
   hipStream_t s = (hipStream_t)stream;
   const BnGrid g = bn_grid(npix, c);
-  hipLaunchKernelGGL(bn_stats_kernel<0>, dim3(g.parts), dim3(256), 0, s, (int)npix, c, g.per_blk, z, nullptr, nullptr, nullptr,
-                     nullptr, 0.f, workspace);
+  hipLaunchKernelGGL(bn_stats_kernel<0>, dim3(g.parts), dim3(256), 0, s, (int)npix, c, g.per_blk, z, (const float*)nullptr, nullptr,
+                     nullptr, nullptr, nullptr, nullptr, 0.f, workspace);
   hipLaunchKernelGGL(bn_finish_stats_kernel, dim3(ceil_div(c, 8)), dim3(256), 0, s, workspace, g.parts, c, (int)npix, eps,
                      momentum, mean, rstd, run_mean, run_var, num_batches_tracked);
   int per;
@@ -355,15 +384,46 @@ extern "C" int climsr_bn_backward(const float* da, const uint16_t* a, const uint
   }
   hipStream_t s = (hipStream_t)stream;
   const BnGrid g = bn_grid(npix, c);
-  hipLaunchKernelGGL(bn_stats_kernel<1>, dim3(g.parts), dim3(256), 0, s, (int)npix, c, g.per_blk, z, da, a, mean, rstd, slope,
-                     workspace);
+  hipLaunchKernelGGL(bn_stats_kernel<1>, dim3(g.parts), dim3(256), 0, s, (int)npix, c, g.per_blk, z, da, a, mean, rstd, nullptr,
+                     nullptr, slope, workspace);
   hipLaunchKernelGGL(bn_bwd_finish_kernel, dim3(ceil_div(c, 8)), dim3(256), 0, s, workspace, g.parts, c, (int)npix, gamma, rstd,
                      dgamma, dbeta, accumulate, coef);
   int per;
   const int nb = bn_apply_grid(npix, c, &per);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(nb), dim3(256), 0, s, (int)npix, c, per, da, a, z, mean, rstd, coef, slope, out_slope,
-                     dz);
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<float, false>), dim3(nb), dim3(256), 0, s, (int)npix, c, per, da, a, z, mean, rstd, nullptr,
+                     nullptr, coef, slope, out_slope, dz);
   return check_launch("bn_backward");
+}
+
+// BatchNorm2d + LeakyReLU backward without the activation: lrelu'(a) comes from sign(z * gamma*rstd + beta -
+// mean*gamma*rstd), recomputed exactly as the forward applied it; da is bf16 (da_bf16 = 1: what the data gradient
+// of the next conv writes) or fp32.  Per element 4 B (bf16 da + z) read by each of the two passes, not 8.
+extern "C" int climsr_bn_backward_z(const void* da, int da_bf16, const uint16_t* z, int64_t npix, int c, const float* mean,
+                                    const float* rstd, const float* gamma, const float* beta, float slope, double* workspace,
+                                    float* coef, float* dgamma, float* dbeta, int accumulate, uint16_t* dz, void* stream) {
+  if (!da || !z || !mean || !rstd || !gamma || !beta || !workspace || !coef || !dz || !bn_shape_ok(npix, c)) {
+    set_error("bn_backward_z: bad args");
+    return CLIMSR_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const BnGrid g = bn_grid(npix, c);
+  if (da_bf16)
+    hipLaunchKernelGGL((bn_stats_kernel<2, uint16_t>), dim3(g.parts), dim3(256), 0, s, (int)npix, c, g.per_blk, z,
+                       (const uint16_t*)da, nullptr, mean, rstd, gamma, beta, slope, workspace);
+  else
+    hipLaunchKernelGGL((bn_stats_kernel<2, float>), dim3(g.parts), dim3(256), 0, s, (int)npix, c, g.per_blk, z, (const float*)da,
+                       nullptr, mean, rstd, gamma, beta, slope, workspace);
+  hipLaunchKernelGGL(bn_bwd_finish_kernel, dim3(ceil_div(c, 8)), dim3(256), 0, s, workspace, g.parts, c, (int)npix, gamma, rstd,
+                     dgamma, dbeta, accumulate, coef);
+  int per;
+  const int nb = bn_apply_grid(npix, c, &per);
+  if (da_bf16)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<uint16_t, true>), dim3(nb), dim3(256), 0, s, (int)npix, c, per, (const uint16_t*)da,
+                       nullptr, z, mean, rstd, gamma, beta, coef, slope, 1.f, dz);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<float, true>), dim3(nb), dim3(256), 0, s, (int)npix, c, per, (const float*)da, nullptr,
+                       z, mean, rstd, gamma, beta, coef, slope, 1.f, dz);
+  return check_launch("bn_backward_z");
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -190,6 +190,7 @@ class _RcanEngine:
         xb = bf(n, h, w, nf)
         P["head.0"].fwd(lr, self.cin_pad, 0, h, w, head, nf, 0, n, out_mode=OUT_F32, aux=xb, aux_cs=nf)
         xres = head.clone()
+        xb_alt = bf(n, h, w, nf)
         gin = f32(n, h, w, nf)
         t = bf(n, h, w, nf)
         u = f32(n, h, w, nf)
@@ -208,9 +209,11 @@ class _RcanEngine:
                 check(L.climsr_channel_attention(ptr(u), n, h * w, nf, nf, ptr(w1), ptr(b1), ptr(w2), ptr(b2), w1.shape[0],
                                                  ptr(self.ca_ws), ptr(s), st), f"channel attention {pre}")
                 check(L.climsr_ca_scale_add(ptr(u), nf, ptr(s), ptr(xres), ptr(xb), nf, n, h * w, nf, st), f"rcab residual {pre}")
-            # group tail conv + group skip (rcan.py:133-135), fp32 stream + bf16 shadow
+            # group tail conv + group skip (rcan.py:133-135), fp32 stream + bf16 shadow.  The shadow goes to the other
+            # buffer of a pair: written in place, a tile's aux store would race the halo reads of its neighbours.
             P[f"body.{g}.body.{m.n_resblocks}"].fwd(xb, nf, 0, h, w, xres, nf, 0, n, res1=gin, res1_cs=nf, out_mode=OUT_F32,
-                                                   aux=xb, aux_cs=nf)
+                                                   aux=xb_alt, aux_cs=nf)
+            xb, xb_alt = xb_alt, xb
         # body conv + global skip (rcan.py:185-186); only its bf16 form feeds the tail
         feat = bf(n, h, w, nf)
         P[f"body.{m.n_resgroups}"].fwd(xb, nf, 0, h, w, feat, nf, 0, n, res1=head, res1_cs=nf, out_mode=OUT_BF16)

@@ -22,7 +22,7 @@ from torch import Tensor
 
 from .. import ops
 from ..core.flat import FlatParamsMixin
-from ..ops import ACT_LRELU, BatchedPacker, ConvPlan, Workspace
+from ..ops import ACT_LRELU, ACT_LRELU_BWD, BatchedPacker, ConvPlan, Workspace
 
 POOL = 14
 
@@ -151,25 +151,44 @@ class _DEngine:
         ops.adaptive_pool_bwd(dp, n, hh, ww, c, POOL, POOL, da)
         coef = self._scr("bncoef", (3 * 512,), torch.float32, dev)
         dx = None
+        dz_next = None  # layer 0's output gradient, written directly by layer 1's data gradient
         for li in reversed(range(len(self.layers))):
             conv, bn, plan = self.layers[li]
             L = sv["layers"][li]
             oh, ow, c = L["oh"], L["ow"], plan.cout
             npix = n * oh * ow
             cz = (c + 7) // 8 * 8
-            dz = _bf16((n, oh, ow, cz), dev)
             if bn is not None:
-                ops.bn_backward(da, L["a"], L["z"], npix, c, L["mean"], L["rstd"], bn.weight, ops.bn_workspace(npix, c, self.scratch, dev), coef,
-                                bn.weight.grad if need_w else None, bn.bias.grad if need_w else None, acc, dz)
+                # lrelu'(a) recomputed from z: the activation is not read; da is the bf16 data gradient of the
+                # next conv (fp32 only for the last layer, from the pooling backward)
+                dz = _bf16((n, oh, ow, cz), dev)
+                ops.bn_backward_z(da, L["z"], npix, c, L["mean"], L["rstd"], bn.weight, bn.bias,
+                                  ops.bn_workspace(npix, c, self.scratch, dev), coef,
+                                  bn.weight.grad if need_w else None, bn.bias.grad if need_w else None, acc, dz)
+            elif dz_next is not None:
+                dz = dz_next
             else:
+                dz = _bf16((n, oh, ow, cz), dev)
                 ops.act_grad(npix, c, da, c, 0, L["a"], c, 0, ACT_LRELU, dz, cz)
             if need_w:
                 plan.gw = conv.weight.grad
                 plan.gb = None
                 plan.wgrad(L["a_in"], L["cs_in"], 0, L["h_in"], L["w_in"], dz, cz, n, self.ws, acc)
             if li > 0 or need_x:
-                g = _f32((n, L["h_in"], L["w_in"], plan.cin), dev)
-                plan.dgrad(dz, cz, oh, ow, g, plan.cin, 0, n)
+                prev_bn = self.layers[li - 1][1] if li > 0 else None
+                if li == 1 and prev_bn is None and plan.cin % 8 == 0:
+                    # layer 0 has no BN: its LeakyReLU' (from its stored bf16 activation) goes into this data
+                    # gradient's epilogue, which writes layer 0's bf16 output gradient
+                    P0 = sv["layers"][0]
+                    g = _bf16((n, L["h_in"], L["w_in"], plan.cin), dev)
+                    plan.dgrad(dz, cz, oh, ow, g, plan.cin, 0, n, act=ACT_LRELU_BWD, res1=P0["a"], res1_cs=plan.cin, res1_co=0)
+                    dz_next = g
+                elif li > 0:
+                    g = _bf16((n, L["h_in"], L["w_in"], plan.cin), dev)  # bf16: read by the previous layer's BN backward
+                    plan.dgrad(dz, cz, oh, ow, g, plan.cin, 0, n)
+                else:
+                    g = _f32((n, L["h_in"], L["w_in"], plan.cin), dev)
+                    plan.dgrad(dz, cz, oh, ow, g, plan.cin, 0, n)
                 da = g
             if li == 0 and need_x:
                 dx = torch.empty((n, 1, sv["h"], sv["w"]), dtype=torch.float32, device=dev)

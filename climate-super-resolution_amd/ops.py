@@ -475,6 +475,15 @@ def bn_backward(da, a, z, npix, c, mean, rstd, gamma, ws, coef, dgamma, dbeta, a
          "bn_backward", npix * c * 18)
 
 
+def bn_backward_z(da, z, npix, c, mean, rstd, gamma, beta, ws, coef, dgamma, dbeta, accumulate, dz, slope=0.2):
+    """Backward of LeakyReLU(BN(z)) from da (bf16 or fp32) and z alone (lrelu' recomputed from z)."""
+    bf = 1 if da.dtype == torch.bfloat16 else 0
+    _run("bn_backward", 0, lambda: check(
+        _L().climsr_bn_backward_z(ptr(da), bf, ptr(z), npix, c, ptr(mean), ptr(rstd), ptr(gamma), ptr(beta), slope, ptr(ws),
+                                  ptr(coef), ptr(dgamma), ptr(dbeta), int(accumulate), ptr(dz), _lib.stream_ptr()), "bn_backward_z"),
+         "bn_backward", npix * c * (3 * da.element_size() + 6))
+
+
 def reflect_pad1(x, n, h, w, cs, y):
     _launch("reflect_pad1", lambda: _L().climsr_reflect_pad1_bf16(ptr(x), n, h, w, cs, ptr(y), _lib.stream_ptr()))
 

@@ -250,6 +250,12 @@ int climsr_increment_i64(int64_t* p, void* stream);
 int climsr_bn_backward(const float* da, const uint16_t* a, const uint16_t* z, int64_t npix, int c, const float* mean,
                        const float* rstd, const float* gamma, float slope, float out_slope, double* workspace, float* coef,
                        float* dgamma, float* dbeta, int accumulate, uint16_t* dz, void* stream);
+/* Backward of LeakyReLU(BN(z)) without the activation tensor (rfb_esrgan.py:32-50): lrelu' is taken from the sign
+ * of gamma*(z-mean)*rstd + beta recomputed exactly as climsr_bn_forward applied it.  da = dL/d(act output), bf16
+ * (da_bf16 = 1, as the next conv's data gradient writes it) or fp32; other arguments as climsr_bn_backward. */
+int climsr_bn_backward_z(const void* da, int da_bf16, const uint16_t* z, int64_t npix, int c, const float* mean,
+                         const float* rstd, const float* gamma, const float* beta, float slope, double* workspace, float* coef,
+                         float* dgamma, float* dbeta, int accumulate, uint16_t* dz, void* stream);
 
 /* nn.AdaptiveAvgPool2d((oh,ow)) (rfb_esrgan.py:54) on NHWC bf16 x [n][h][w][c]; out = torch.flatten
  * order [n][c*oh*ow] bf16; out_t (optional) = its transpose [c*oh*ow][n_pad] for the fc.0 weight grad. */

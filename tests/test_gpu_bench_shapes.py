@@ -427,3 +427,20 @@ def test_batchnorm_train_at_bench_shapes(c, h):
     dz64 = gamma.double() * rstd.double() * (d - d.mean(0) - xh * (d * xh).mean(0))
     err = float((dz.double() - dz64).abs().max())
     assert err <= 2 ** -7 * float(dz64.abs().max()), f"bn backward dz err {err:.3e}"
+    # the activation-free form (rfb_esrgan.py's D backward): bf16 da, lrelu' recomputed from z -- the same
+    # decisions as the stored activation's sign, so the same float64 reference with the bf16-rounded da
+    beta = torch.rand(c, generator=g, device=DEV) - 0.5
+    ops.bn_forward(zb, npix, c, gamma, beta, mean, rstd, y, ops.bn_workspace(npix, c, cache, z.device))
+    dab = da.to(torch.bfloat16)
+    dz2 = torch.empty_like(dz)
+    dgam2, dbet2 = torch.zeros(c, device=DEV), torch.zeros(c, device=DEV)
+    ops.bn_backward_z(dab, zb, npix, c, mean, rstd, gamma, beta, ops.bn_workspace(npix, c, cache, z.device), coef, dgam2, dbet2,
+                      False, dz2)
+    torch.cuda.synchronize()
+    d = dab.double() * torch.where(y > 0, 1.0, 0.2).double()
+    xh = (zd - mean.double()) * rstd.double()
+    close(dgam2, (d * xh).sum(0), rel=1e-5, what="dgamma (from z)")
+    close(dbet2, d.sum(0), rel=1e-5, what="dbeta (from z)")
+    dz64 = gamma.double() * rstd.double() * (d - d.mean(0) - xh * (d * xh).mean(0))
+    err = float((dz2.double() - dz64).abs().max())
+    assert err <= 2 ** -7 * float(dz64.abs().max()), f"bn backward (from z) dz err {err:.3e}"

@@ -100,7 +100,7 @@ def _stats(got, want):
     return psnr(got, want), float((gc * wc).sum() / (gc.norm() * wc.norm())), float((got - want).norm() / want.norm())
 
 
-def _compare(got, want, amps, what, min_psnr=50.0):
+def _compare(got, want, amps_fn, what, min_psnr=50.0):
     """Native vs the fp32 oracle: PSNR >= min_psnr dB and centred correlation >= 0.999, OR inside the envelope of the
     reference's own reduced-precision inference (config 5 runs the reference in fp16: the oracle under torch
     autocast fp16 / bf16 on the same grid) -- relative L2 <= 2x the worse autocast run's and correlation no worse
@@ -108,13 +108,14 @@ def _compare(got, want, amps, what, min_psnr=50.0):
     assert got.shape == want.shape, (got.shape, want.shape)
     assert torch.isfinite(got).all(), what
     p, corr, rel = _stats(got, want)
-    amp = [_stats(a, want) for a in amps]
+    print(f"{what}: PSNR {p:.2f} dB, corr {corr:.6f}, rel L2 {rel:.2e}", flush=True)
+    if p >= min_psnr and corr >= 0.999:
+        return
+    amp = [_stats(a, want) for a in amps_fn()]  # only needed when the absolute bar is missed
     rel_amp, corr_amp = max(a[2] for a in amp), min(a[1] for a in amp)
-    print(f"{what}: PSNR {p:.2f} dB, corr {corr:.6f}, rel L2 {rel:.2e}; autocast fp16/bf16: "
-          + ", ".join(f"PSNR {a[0]:.2f} dB corr {a[1]:.6f} rel {a[2]:.2e}" for a in amp))
-    ok_abs = p >= min_psnr and corr >= 0.999
+    print(f"{what}: autocast fp16/bf16: " + ", ".join(f"PSNR {a[0]:.2f} dB corr {a[1]:.6f} rel {a[2]:.2e}" for a in amp), flush=True)
     ok_amp = rel <= 2.0 * rel_amp and corr >= 1.0 - 2.0 * (1.0 - corr_amp)
-    assert ok_abs or ok_amp, f"{what}: PSNR {p:.2f} dB, centred correlation {corr:.6f}, rel L2 {rel:.2e} (autocast {amp})"
+    assert ok_amp, f"{what}: PSNR {p:.2f} dB, centred correlation {corr:.6f}, rel L2 {rel:.2e} (autocast {amp})"
 
 
 def _autocast_runs(fn):
@@ -142,12 +143,15 @@ def test_config5_esrgan_whole_grid_vs_oracle_fp32(fp32_torch):
     lr, e, m = _grid(h, w)
     with torch.no_grad():
         sr = net(lr, e, m)
+        again = net(lr, e, m)
         torch.cuda.synchronize()
+        print("native done", flush=True)
+        assert torch.equal(sr, again), float((sr - again).abs().max())  # deterministic (fixed-order reductions)
         pd = {k: v.to(DEV) for k, v in p32.items()}
         want = ref.generator_forward(pd, lr, e, m, nb)
     assert sr.shape == (1, 1, 4 * h, 4 * w)
-    amps = _autocast_runs(lambda: ref.generator_forward(pd, lr, e, m, nb))
-    _compare(sr, want, amps, "config-5 ESRGAN nb11 720x360 -> 2880x1440")
+    _compare(sr, want, lambda: _autocast_runs(lambda: ref.generator_forward(pd, lr, e, m, nb)),
+             "config-5 ESRGAN nb11 720x360 -> 2880x1440")
 
 
 def test_config5_rcan_whole_grid_vs_oracle_fp32(fp32_torch):
@@ -163,8 +167,12 @@ def test_config5_rcan_whole_grid_vs_oracle_fp32(fp32_torch):
     lr, e, m = _grid(h, w, seed=43)
     with torch.no_grad():
         sr = net(lr, e, m)
+        again = net(lr, e, m)
         torch.cuda.synchronize()
+        print("native done", flush=True)
+        # every reduction runs in a fixed order and no launch reads what it writes: bit-identical reruns
+        assert torch.equal(sr, again), float((sr - again).abs().max())
         pd = {k: v.to(DEV) for k, v in p32.items()}
         want = ref.rcan_forward(pd, lr, e, m, 10, 20, 4)
-    amps = _autocast_runs(lambda: ref.rcan_forward(pd, lr, e, m, 10, 20, 4))
-    _compare(sr, want, amps, "config-5 RCAN 10x20 720x360 -> 2880x1440")
+    _compare(sr, want, lambda: _autocast_runs(lambda: ref.rcan_forward(pd, lr, e, m, 10, 20, 4)),
+             "config-5 RCAN 10x20 720x360 -> 2880x1440")

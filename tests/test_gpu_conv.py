@@ -387,3 +387,4 @@ def test_rdb_chain_matches_per_conv(n, h, w):
         err = ((a64 - b64).abs() - 2 ** -7 * b64.abs()).max().item()
         assert err <= 1e-3 * b64.abs().max().item(), f"{name}: excess error {err}"
     assert torch.equal(got[..., :nf], x[..., :nf]) and torch.equal(dgot[..., 4 * gc:], dz0[..., 4 * gc:])
+
