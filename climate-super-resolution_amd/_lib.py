@@ -98,6 +98,8 @@ SIGNATURES = {
     "climsr_conv2d_fwd_kernel": (ctypes.c_char_p, [P(ConvDesc), c_void_p, P(Epilogue)]),
     "climsr_conv2d_wgrad_kernel": (ctypes.c_char_p, [P(ConvDesc)]),
     "climsr_dgrad_single_output_kernel": (ctypes.c_char_p, [c_int, c_int, c_int]),
+    "climsr_conv_single_input": (c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int,
+                                         c_int, c_float, c_void_p, c_int, c_int, c_void_p]),
     "climsr_dgrad_single_output": (c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int,
                                            c_float, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p]),
     "climsr_conv2d_wgrad": (c_int, [P(ConvDesc), c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]),
@@ -119,6 +121,8 @@ SIGNATURES = {
     "climsr_adamw_hparams": (c_int, [c_void_p, c_int, c_double, c_double, c_double, c_double, c_double, c_double, c_double,
                                      c_void_p, c_void_p]),
     "climsr_adamw_step": (c_int, [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "climsr_adamw_step_mirror": (c_int, [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p,
+                                         c_void_p]),
     "climsr_bn_workspace_doubles": (c_int64, [c_int64, c_int]),
     "climsr_bn_forward": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_int, c_float, c_float, c_float, c_void_p,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -56,6 +56,7 @@ class AdamW(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         lib = _lib.load()
+        mirrored = False
         for group in self.param_groups:
             params = [p for p in group["params"] if p.grad is not None]
             if not params:
@@ -78,8 +79,8 @@ class AdamW(torch.optim.Optimizer):
                 if "m" not in st:
                     st["m"] = torch.zeros_like(flat)
                     st["v"] = torch.zeros_like(flat)
-                _launch("adamw", lambda: lib.climsr_adamw_step(flat.numel(), ptr(flat), ptr(gflat), ptr(st["m"]), ptr(st["v"]),
-                                                               ptr(hp), _lib.stream_ptr()), nbytes=28 * flat.numel())
+                _adamw_flat(lib, self.owner, flat, gflat, st["m"], st["v"], hp, _lib.stream_ptr())
+                mirrored = True
             else:
                 for p in params:
                     ps = self.state[p]
@@ -90,8 +91,30 @@ class AdamW(torch.optim.Optimizer):
                     _launch("adamw", lambda: lib.climsr_adamw_step(p.numel(), ptr(p), ptr(g), ptr(ps["m"]), ptr(ps["v"]), ptr(hp),
                                                                    _lib.stream_ptr()), nbytes=28 * p.numel())
         if self.owner is not None:
-            self.owner.repack_weights()
+            if mirrored and _mirror_of(self.owner) is not None:
+                self.owner.repack_weights(mirror_done=True)
+            else:
+                self.owner.repack_weights()
         return loss
+
+
+def _mirror_of(module):
+    """(offset, numel, bf16 buffer) of a weight the module reads as a bf16 copy of its flat buffer, or None."""
+    fn = getattr(module, "bf16_mirror", None)
+    return fn() if fn is not None else None
+
+
+def _adamw_flat(lib, module, flat, gflat, m, v, hp, stream):
+    """One fused AdamW launch over a flat buffer; when ``module`` mirrors part of it in bf16 (``bf16_mirror()``), the
+    same pass writes that copy."""
+    mir = _mirror_of(module) if module is not None else None
+    if mir is None:
+        _launch("adamw", lambda: lib.climsr_adamw_step(flat.numel(), ptr(flat), ptr(gflat), ptr(m), ptr(v), ptr(hp), stream),
+                nbytes=28 * flat.numel())
+    else:
+        lo, n, buf = mir
+        _launch("adamw", lambda: lib.climsr_adamw_step_mirror(flat.numel(), ptr(flat), ptr(gflat), ptr(m), ptr(v), ptr(hp), lo, n,
+                                                              ptr(buf), stream), nbytes=28 * flat.numel() + 2 * n)
 
 
 class GraphedAdamW:
@@ -120,6 +143,8 @@ class GraphedAdamW:
         _launch("adamw_hparams", lambda: lib.climsr_adamw_hparams(ptr(self.state), ts, lr, pct, div, fdiv, b2, eps, wd, ptr(self.hp),
                                                                   s))
         flat = self.module._flat
-        _launch("adamw", lambda: lib.climsr_adamw_step(flat.numel(), ptr(flat), ptr(self.module._flat_grad), ptr(self.m), ptr(self.v),
-                                                       ptr(self.hp), s), nbytes=28 * flat.numel())
-        self.module.engine().repack()
+        _adamw_flat(lib, self.module, flat, self.module._flat_grad, self.m, self.v, self.hp, s)
+        if _mirror_of(self.module) is not None:
+            self.module.engine().repack(mirror_done=True)
+        else:
+            self.module.engine().repack()

@@ -1770,11 +1770,15 @@ __global__ __launch_bounds__(256) void conv_pt_kernel(FwdArgs a, long npix) {
 constexpr int S1_T = 16;
 // LPP = C / 8 lanes share a pixel (8 channels each), so a wave's 16 B stores / residual loads cover whole
 // 128 B (C = 64) or 64 B (C = 32) pixel rows; weights in LDS as [tap][C] (two 16 B reads per tap).
-template <int KS, int LPP>
+// FWD: the same stencil as the FORWARD of a 1 -> C conv (the discriminator's features.0, rfb_esrgan.py:28: 1 -> 64,
+// 3x3, no bias, LeakyReLU): out[q][c] = act(sum W[c][0][ky][kx] * x[q + (ky,kx) - pad] + bias[c]), act 1 / 2 =
+// leaky relu / relu forward.  The implicit-GEMM path pads the single input channel to 8 (K = 72 of 96) and is
+// bound by its LDS-staged epilogue (156 us per B=32 256^2 launch for a 268 MB output).
+template <int KS, int LPP, bool FWD = false>
 __global__ __launch_bounds__(256) void dgrad_ci1_kernel(int n, int h, int w, int pad, const uint16_t* __restrict__ dz, int dz_cs,
                                                         int dz_co, const float* __restrict__ wt, int act, float slope,
                                                         const uint16_t* __restrict__ res1, int r1_cs, int r1_co, uint16_t* __restrict__ out,
-                                                        int out_cs, int out_co) {
+                                                        int out_cs, int out_co, const float* __restrict__ bias = nullptr) {
   constexpr int TP = S1_T + KS - 1, C = LPP * 8, PPS = 256 / LPP, NPASS = S1_T * S1_T / PPS;
   __shared__ float dzt[TP * TP];
   __shared__ __attribute__((aligned(16))) float wl[KS * KS * C];
@@ -1785,14 +1789,14 @@ __global__ __launch_bounds__(256) void dgrad_ci1_kernel(int n, int h, int w, int
   b /= tiles_x;
   const int by = b % tiles_y, img = b / tiles_y;
   const int x0 = bx * S1_T, y0 = by * S1_T;
-  // tile row r <-> dz row y0 - (KS - 1) + pad + r (same for columns)
-  const int ry0 = y0 - (KS - 1) + pad, rx0 = x0 - (KS - 1) + pad;
+  // tile row r <-> dz row y0 - (KS - 1) + pad + r (same for columns); forward: x row y0 - pad + r
+  const int ry0 = FWD ? y0 - pad : y0 - (KS - 1) + pad, rx0 = FWD ? x0 - pad : x0 - (KS - 1) + pad;
   // every residual load of this thread first (they land while the tile is staged and the sums computed)
   uint4 rv[NPASS];
 #pragma unroll
   for (int k = 0; k < NPASS; ++k) {
     const int pix = k * PPS + ps, qy = y0 + pix / S1_T, qx = x0 + pix % S1_T;
-    const bool ok = act && qy < h && qx < w;
+    const bool ok = !FWD && act && qy < h && qx < w;
     rv[k] = ok ? *(const uint4*)(res1 + (((long)img * h + qy) * w + qx) * r1_cs + r1_co + cg * 8) : make_uint4(0, 0, 0, 0);
   }
   for (int i = tid; i < TP * TP; i += 256) {
@@ -1813,14 +1817,20 @@ __global__ __launch_bounds__(256) void dgrad_ci1_kernel(int n, int h, int w, int
 #pragma unroll
     for (int ky = 0; ky < KS; ++ky)
 #pragma unroll
-      for (int kx = 0; kx < KS; ++kx) {  // out[q] += W[c][ky][kx] * dz[q - (ky, kx) + pad]
-        const float d = dzt[(ty + KS - 1 - ky) * TP + tx + KS - 1 - kx];
+      for (int kx = 0; kx < KS; ++kx) {  // out[q] += W[c][ky][kx] * dz[q - (ky, kx) + pad]  (FWD: x[q + (ky, kx) - pad])
+        const float d = FWD ? dzt[(ty + ky) * TP + tx + kx] : dzt[(ty + KS - 1 - ky) * TP + tx + KS - 1 - kx];
         const float4 w0 = *(const float4*)(wl + (ky * KS + kx) * C + cg * 8), w1 = *(const float4*)(wl + (ky * KS + kx) * C + cg * 8 + 4);
         v[0] += w0.x * d; v[1] += w0.y * d; v[2] += w0.z * d; v[3] += w0.w * d;
         v[4] += w1.x * d; v[5] += w1.y * d; v[6] += w1.z * d; v[7] += w1.w * d;
       }
     if (qy >= h || qx >= w) continue;
-    if (act) {
+    if (FWD) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (bias) v[i] += bias[cg * 8 + i];
+        v[i] = act_apply(v[i], act, slope);
+      }
+    } else if (act) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const uint32_t wd = i < 2 ? rv[k].x : i < 4 ? rv[k].y : i < 6 ? rv[k].z : rv[k].w;
@@ -1854,6 +1864,29 @@ extern "C" int climsr_dgrad_single_output(int n, int h, int w, int ks, int pad, 
   }
 #undef CLIMSR_CI1
   return check_launch("dgrad_single_output");
+}
+
+extern "C" int climsr_conv_single_input(int n, int h, int w, int ks, int pad, const uint16_t* x, int x_cstride, int x_coff,
+                                        const float* weight, const float* bias, int c, int act, float slope, uint16_t* out,
+                                        int out_cstride, int out_coff, void* stream) {
+  if (!x || !weight || !out || n <= 0 || h <= 0 || w <= 0 || (ks != 3 && ks != 5) || pad != ks / 2 || c % 8 || (c != 32 && c != 64) ||
+      (out_cstride | out_coff) % 8 || act < 0 || act > 2) {
+    set_error("conv_single_input: unsupported arguments (ks %d pad %d c %d act %d)", ks, pad, c, act);
+    return CLIMSR_EINVAL;
+  }
+  const long tiles = (long)n * ((h + S1_T - 1) / S1_T) * ((w + S1_T - 1) / S1_T);
+  if (dry_run("dgrad_ci1_kernel<%d, %d, true>", ks, c / 8)) return CLIMSR_OK;
+#define CLIMSR_CI1F(KS_, LPP_)                                                                                                   \
+  hipLaunchKernelGGL((dgrad_ci1_kernel<KS_, LPP_, true>), dim3((unsigned)tiles), dim3(256), 0, (hipStream_t)stream, n, h, w, pad, x, \
+                     x_cstride, x_coff, weight, act, slope, nullptr, 0, 0, out, out_cstride, out_coff, bias)
+  switch (ks * 100 + c / 8) {
+    case 308: CLIMSR_CI1F(3, 8); break;
+    case 304: CLIMSR_CI1F(3, 4); break;
+    case 508: CLIMSR_CI1F(5, 8); break;
+    default: CLIMSR_CI1F(5, 4); break;
+  }
+#undef CLIMSR_CI1F
+  return check_launch("conv_single_input");
 }
 
 template <int NCOF, int NKC>
@@ -2077,6 +2110,10 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
       if (v8 && a.bias && a.res_f32 == 0 && a.out_mode == 0 && !a.aux) return launch_fwd_ep<4, 4, 6, 9, 1>(a, ncob, g.lds_total, s);
       if (v8 && !a.bias && (a.res_f32 & 1) && (!a.res2 || (a.res_f32 & 2)) && a.out_mode == 1)
         return launch_fwd_ep<4, 4, 6, 9, 2>(a, ncob, g.lds_total, s);
+      // activation backward from a bf16 activation, bf16 out (the discriminator's layer-1 data gradient)
+      if (!a.bias && a.res1 && (a.act == 3 || a.act == 4) && a.res_f32 == 0 && !a.res2 && !a.aux && !a.down2 && a.out_mode == 0 &&
+          (a.out_c & 7) == 0 && ((a.out_cs | a.out_co | a.r1_cs | a.r1_co) & 7) == 0)
+        return launch_fwd_ep<4, 4, 6, 9, 4>(a, ncob, g.lds_total, s);
       switch (plain_ep(a)) {
         case 3: return launch_fwd_ep<4, 4, 6, 9, 3>(a, ncob, g.lds_total, s);
         case 6: return launch_fwd_ep<4, 4, 6, 9, 6>(a, ncob, g.lds_total, s);

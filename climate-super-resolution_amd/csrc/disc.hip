@@ -523,7 +523,27 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(const uint16_t* __restr
   for (int f = 0; f < NF; ++f) acc[f] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const uint16_t* wrow = w + (long)(o0 + col) * k + g * 8;
   const bool orow_ok = o0 + col < o;
-  for (int kk = kb; kk < ke; kk += 32) {
+  // LU k-steps per round, every load of a round issued before its MFMAs: 16 weight rows x LU*64 B contiguous per
+  // wave in flight (one k-step at a time kept a single 64 B segment per row outstanding: 2.4 TB/s)
+  constexpr int LU = 8;
+  int kk = kb;
+  for (; kk + 32 * LU <= ke; kk += 32 * LU) {
+    bf16x8 af[LU], bfr[LU][NF];
+#pragma unroll
+    for (int u = 0; u < LU; ++u) af[u] = orow_ok ? *(const bf16x8*)(wrow + kk + 32 * u) : (bf16x8){};
+#pragma unroll
+    for (int u = 0; u < LU; ++u)
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        const int nn = f * 16 + col;
+        bfr[u][f] = nn < n ? *(const bf16x8*)(x + (long)nn * k + kk + 32 * u + g * 8) : (bf16x8){};
+      }
+#pragma unroll
+    for (int u = 0; u < LU; ++u)
+#pragma unroll
+      for (int f = 0; f < NF; ++f) acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[u], bfr[u][f], acc[f], 0, 0, 0);
+  }
+  for (; kk < ke; kk += 32) {
     bf16x8 af = orow_ok ? *(const bf16x8*)(wrow + kk) : (bf16x8){};
     bf16x8 bfr[NF];
 #pragma unroll
@@ -567,8 +587,8 @@ extern "C" int climsr_linear_fwd(const uint16_t* x, const uint16_t* w, const flo
     return CLIMSR_EINVAL;
   }
   const int oblk = ceil_div(o, 64);
-  int nsplit = ceil_div(1024, oblk);
-  int ksplit = round_up(ceil_div(k, nsplit), 32);
+  int nsplit = ceil_div(1536, oblk);  // ~6 workgroups per CU, K slices of whole 256-element rounds where possible
+  int ksplit = round_up(ceil_div(k, nsplit), k >= 256 * nsplit ? 256 : 32);
   nsplit = ceil_div(k, ksplit);
   if ((int64_t)nsplit * n * o > ws_floats) {
     set_error("linear_fwd: workspace too small (%lld floats needed)", (long long)nsplit * n * o);
@@ -598,21 +618,26 @@ __global__ __launch_bounds__(256) void linear_dgrad_kernel(const uint16_t* __res
   f32x4 acc[NF];
 #pragma unroll
   for (int f = 0; f < NF; ++f) acc[f] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  for (int ob = 0; ob < o; ob += 128) {
-    __syncthreads();
-    // stage W[ob..ob+128][k0..k0+64]: 128 rows x 8 vectors
-    uint4 buf[4];
+  // W[ob..ob+128][k0..k0+64] tiles: 128 rows x 8 vectors; the next tile's loads are in flight (registers) while the
+  // current one is on the MFMA pipe
+  uint4 buf[4];
+  auto issue = [&](int ob) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int v = tid + i * 256;
       const int r = v >> 3, cv = v & 7;
       buf[i] = (ob + r < o && k0 + cv * 8 < k) ? *(const uint4*)(w + (long)(ob + r) * k + k0 + cv * 8) : make_uint4(0, 0, 0, 0);
     }
+  };
+  issue(0);
+  for (int ob = 0; ob < o; ob += 128) {
+    __syncthreads();
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int v = tid + i * 256;
       *(uint4*)(ws_ + (v >> 3) * 72 + (v & 7) * 8) = buf[i];
     }
+    if (ob + 128 < o) issue(ob + 128);
     __syncthreads();
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {  // 4 k-steps of 32 o

@@ -321,8 +321,15 @@ extern "C" int climsr_adamw_hparams(double* state, int total_steps, double max_l
 
 // torch.optim.AdamW (amsgrad=False) single-tensor semantics in fp32:
 //   p *= 1 - lr*wd; m = b1*m + (1-b1)*g; v = b2*v + (1-b2)*g*g; p -= (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps)
+// mirror (optional): bf16 copy of the updated p[lo, lo + mn) into mirror[0, mn) -- the MFMA operand of a layer whose
+// weights are read straight from the flat buffer (the discriminator's fc.0), written by this pass instead of a
+// separate fp32 -> bf16 sweep of the same 411 MB.
+__device__ __forceinline__ void adamw_mirror(long i, float v, uint16_t* mirror, long lo, long mn) {
+  if (mirror && i >= lo && i < lo + mn) mirror[i - lo] = f2bf(v);
+}
 __global__ void adamw_kernel(long n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                             float* __restrict__ v, const float* __restrict__ hp) {
+                             float* __restrict__ v, const float* __restrict__ hp, uint16_t* __restrict__ mirror = nullptr,
+                             long mlo = 0, long mn = 0) {
   const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4], step_size = hp[5], bc2s = hp[6];
   long i4 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i4 + 3 < n) {
@@ -336,6 +343,13 @@ __global__ void adamw_kernel(long n, float* __restrict__ p, const float* __restr
       P[k] -= step_size * (M[k] / (sqrtf(V[k]) / bc2s + eps));
     }
     *(float4*)(p + i4) = pp; *(float4*)(m + i4) = mm; *(float4*)(v + i4) = vv;
+    if (mirror && i4 >= mlo && i4 + 3 < mlo + mn && ((i4 - mlo) & 3) == 0) {  // 8 B store of 4 bf16
+      const uint2 pk = make_uint2((uint32_t)f2bf(P[0]) | ((uint32_t)f2bf(P[1]) << 16), (uint32_t)f2bf(P[2]) | ((uint32_t)f2bf(P[3]) << 16));
+      *(uint2*)(mirror + (i4 - mlo)) = pk;
+    } else if (mirror) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) adamw_mirror(i4 + k, P[k], mirror, mlo, mn);
+    }
   } else {
     for (long i = i4; i < n; ++i) {
       float pi = p[i] * (1.f - lr * wd);
@@ -343,6 +357,7 @@ __global__ void adamw_kernel(long n, float* __restrict__ p, const float* __restr
       float vi = v[i] * b2 + g[i] * g[i] * (1.f - b2);
       p[i] = pi - step_size * (mi / (sqrtf(vi) / bc2s + eps));
       m[i] = mi; v[i] = vi;
+      adamw_mirror(i, p[i], mirror, mlo, mn);
     }
   }
 }
@@ -353,6 +368,19 @@ extern "C" int climsr_adamw_step(int64_t n, float* p, const float* g, float* m, 
     return CLIMSR_EINVAL;
   }
   long threads = (n + 3) / 4;
-  hipLaunchKernelGGL(adamw_kernel, dim3(ceil_div(threads, 256)), dim3(256), 0, (hipStream_t)stream, (long)n, p, g, m, v, hp);
+  hipLaunchKernelGGL(adamw_kernel, dim3(ceil_div(threads, 256)), dim3(256), 0, (hipStream_t)stream, (long)n, p, g, m, v, hp,
+                     (uint16_t*)nullptr, 0L, 0L);
   return check_launch("adamw_step");
+}
+
+extern "C" int climsr_adamw_step_mirror(int64_t n, float* p, const float* g, float* m, float* v, const float* hp, int64_t mirror_lo,
+                                        int64_t mirror_n, uint16_t* mirror, void* stream) {
+  if (!p || !g || !m || !v || !hp || n <= 0 || !mirror || mirror_lo < 0 || mirror_n <= 0 || mirror_lo + mirror_n > n) {
+    set_error("adamw_step_mirror: bad args");
+    return CLIMSR_EINVAL;
+  }
+  long threads = (n + 3) / 4;
+  hipLaunchKernelGGL(adamw_kernel, dim3(ceil_div(threads, 256)), dim3(256), 0, (hipStream_t)stream, (long)n, p, g, m, v, hp, mirror,
+                     (long)mirror_lo, (long)mirror_n);
+  return check_launch("adamw_step_mirror");
 }

@@ -58,9 +58,11 @@ class _DEngine:
         if v != self.version:
             self.repack()
 
-    def repack(self):
+    def repack(self, mirror_done: bool = False):
+        """mirror_done: the optimizer's AdamW pass already wrote fc0_bf16 (climsr_adamw_step_mirror)."""
         self.packer.run()
-        ops.f32_to_bf16(self.d.fc[0].weight, self.fc0_bf16)
+        if not mirror_done:
+            ops.f32_to_bf16(self.d.fc[0].weight, self.fc0_bf16)
         self.version = self.d._flat._version
 
     def _scr(self, key, shape, dtype, dev):
@@ -112,7 +114,7 @@ class _DEngine:
         ops.adaptive_pool_fwd(a_prev, n, hh, ww, c, POOL, POOL, p, p_t, n_pad)
         fc0, fc2 = d.fc[0], d.fc[2]
         hid = _f32((n, fc0.out_features), dev)
-        nsplit_max = 1024 // ((fc0.out_features + 63) // 64) + 1
+        nsplit_max = 1536 // ((fc0.out_features + 63) // 64) + 1
         lin_ws = self._scr("linws", (nsplit_max * n * fc0.out_features,), torch.float32, dev)
         ops.linear_fwd(p, self.fc0_bf16, fc0.bias, n, feat, fc0.out_features, hid, lin_ws, act=ACT_LRELU, slope=0.2)
         s = _f32((n, 1), dev)
@@ -269,6 +271,11 @@ class RFBESRGANDiscriminator(FlatParamsMixin, nn.Module):
         object.__setattr__(self, "_ready_calls", 0)
         object.__setattr__(self, "_ready_need", max(1, int(calls_per_step)))
 
+    def bf16_mirror(self):
+        """(flat offset, numel, bf16 buffer) of fc.0's weight: its MFMA copy, written by the fused AdamW pass."""
+        eng = self.engine()
+        return self._fc_flat_lo(), self.fc[0].weight.numel(), eng.fc0_bf16
+
     def _fc_flat_lo(self) -> int:
         p = self.fc[0].weight
         for q, off, _n in self._flat_index:
@@ -290,8 +297,8 @@ class RFBESRGANDiscriminator(FlatParamsMixin, nn.Module):
             object.__setattr__(self, "_engine", _DEngine(self))
         return self._engine
 
-    def repack_weights(self) -> None:
-        self.engine().repack()
+    def repack_weights(self, mirror_done: bool = False) -> None:
+        self.engine().repack(mirror_done=mirror_done)
 
     def forward(self, input: Tensor) -> Tensor:
         if not input.is_cuda:

@@ -126,6 +126,18 @@ class ConvPlan:
         """y = epilogue(conv(x)); residuals res1/res2 may be bf16 or fp32 tensors (dtype decides), aux = optional
         second bf16 output aux_scale * y."""
         oh, ow = self.out_hw(in_h, in_w, up)
+        if (self.cin_real == 1 and self.ks in (3, 5) and self.stride == 1 and self.pad == self.ks // 2 and up == 1
+                and self.cout in (32, 64) and out_mode == OUT_BF16 and y.dtype == torch.bfloat16 and res1 is None and res2 is None
+                and aux is None and act in (ACT_NONE, ACT_LRELU, ACT_RELU) and (y_cs | y_co) % 8 == 0):
+            # one input channel: a 1 -> C stencil (climsr_conv_single_input), not a GEMM with K padded 9 -> 96
+            px = n * oh * ow
+            b = ptr(self.bias) if (use_bias and self.bias is not None) else None
+            kn = "dgrad_ci1_kernel<%d, %d, true>" % (self.ks, self.cout // 8) if PROFILER is not None else ""
+            _run(kn, 2 * self.cout * self.ks * self.ks * px, lambda: check(
+                _lib.load().climsr_conv_single_input(n, in_h, in_w, self.ks, self.pad, ptr(x), x_cs, x_co, ptr(self.weight), b,
+                                                     self.cout, act, slope, ptr(y), y_cs, y_co, _lib.stream_ptr()),
+                f"conv fwd {self.name}"), "fwd " + self.name, px * 2 + px * self.cout * 2)
+            return
         d = ConvDesc(n, in_h, in_w, self.cin, x_cs, x_co, up, self.ks, self.stride, self.pad, oh, ow, self.cout, y_cs, y_co,
                      self.cc)
         rf = (1 if res1 is not None and res1.dtype == torch.float32 else 0) | \

@@ -167,6 +167,13 @@ const char* climsr_dgrad_single_output_kernel(int ks, int c, int act);
 int climsr_dgrad_single_output(int n, int h, int w, int ks, int pad, const uint16_t* dz, int dz_cstride, int dz_coff,
                                const float* weight, int c, int act, float slope, const uint16_t* res1, int res1_cstride,
                                int res1_coff, uint16_t* out, int out_cstride, int out_coff, void* stream);
+/* Forward of a stride-1 'same' conv with ONE input channel (the RFB discriminator's features.0, rfb_esrgan.py:28:
+ * 1 -> 64, 3x3), replacing its nn.Conv2d forward: out[q][c] = act(sum_{ky,kx} w[c][0][ky][kx] * x[q + (ky,kx) - pad]
+ * + bias[c]); x = channel x_coff of a bf16 NHWC buffer, out bf16 NHWC; fp32 OIHW weight [c][1][ks][ks], bias
+ * optional; ks 3 or 5, c 32 or 64, act 0 / 1 (leaky relu, slope) / 2 (relu). */
+int climsr_conv_single_input(int n, int h, int w, int ks, int pad, const uint16_t* x, int x_cstride, int x_coff,
+                             const float* weight, const float* bias, int c, int act, float slope, uint16_t* out,
+                             int out_cstride, int out_coff, void* stream);
 int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, const uint16_t* dz, int dz_cstride,
                         float* partial, float* bias_partial, int nsplit, void* stream);
 /* Sum the split partials into OIHW fp32 grads (accumulate=1: +=).  bias_grad may be NULL. */
@@ -225,6 +232,10 @@ int climsr_adamw_hparams(double* state, int total_steps, double max_lr, double p
                          double final_div_factor, double beta2, double eps, double wd, float* hp, void* stream);
 /* Fused AdamW over flat fp32 buffers (conf/optimizers/adamw.yaml). */
 int climsr_adamw_step(int64_t n, float* p, const float* g, float* m, float* v, const float* hp, void* stream);
+/* The same update, also writing bf16(p[mirror_lo + i]) to mirror[i] for i < mirror_n (the bf16 MFMA copy of a
+ * weight inside the flat buffer: the RFB discriminator's fc.0, rfb_esrgan.py:56-61). */
+int climsr_adamw_step_mirror(int64_t n, float* p, const float* g, float* m, float* v, const float* hp, int64_t mirror_lo,
+                             int64_t mirror_n, uint16_t* mirror, void* stream);
 
 /* ---------------- discriminator / perceptual loss / GAN loss (disc.hip) ---------------- */
 
@@ -265,7 +276,7 @@ int climsr_adaptive_pool_fwd(const uint16_t* x, int n, int h, int w, int c, int 
 int climsr_adaptive_pool_bwd(const float* dp, int n, int h, int w, int c, int oh, int ow, float* dx, void* stream);
 
 /* nn.Linear forward on MFMA: y[n][o] = act(x[n][k] . w[o][k] + b[o]) (fp32 out); n <= 64, k % 32 == 0,
- * o % 16 == 0; split-K partials in workspace (ws_floats >= nsplit*n*o, nsplit <= 1024/ceil(o/64)). */
+ * o % 16 == 0; split-K partials in workspace (ws_floats >= nsplit*n*o, nsplit <= 1536/ceil(o/64) + 1). */
 int climsr_linear_fwd(const uint16_t* x, const uint16_t* w, const float* bias, int n, int k, int o, int act, float slope,
                       float* workspace, int64_t ws_floats, float* y, void* stream);
 /* dx[n][k] (+)= dy[n][o] . w[o][k] (bf16 in, fp32 out); k % 64 == 0, o % 32 == 0. */

@@ -388,3 +388,23 @@ def test_rdb_chain_matches_per_conv(n, h, w):
         assert err <= 1e-3 * b64.abs().max().item(), f"{name}: excess error {err}"
     assert torch.equal(got[..., :nf], x[..., :nf]) and torch.equal(dgot[..., 4 * gc:], dz0[..., 4 * gc:])
 
+
+
+@pytest.mark.parametrize("cout,ks,act,h,w", [(64, 3, 1, 40, 36), (64, 3, 0, 256, 256), (32, 5, 2, 20, 23)])
+def test_conv_single_input_channel_forward(cout, ks, act, h, w):
+    """1 -> C forward stencil (climsr_conv_single_input: the RFB discriminator's features.0, rfb_esrgan.py:28) vs fp64
+    torch on the same bf16 operands, with bias / leaky relu / relu variants."""
+    n = 2
+    p, wt, b = make_plan(1, cout, ks, bias=act != 1)
+    g = torch.Generator().manual_seed(9)
+    x = bf(torch.rand((n, 1, h, w), generator=g) * 2 - 1)
+    xb = to_nhwc(x)
+    y = torch.empty((n, h, w, cout), dtype=torch.bfloat16, device=DEV)
+    acts = {0: ACT_NONE, 1: ACT_LRELU, 2: ACT_RELU}
+    p.fwd(xb, xb.shape[-1], 0, h, w, y, cout, 0, n, act=acts[act])
+    torch.cuda.synchronize()
+    want = F.conv2d(x.double(), wt.double(), None if b is None else b.double(), padding=ks // 2)
+    want = F.leaky_relu(want, 0.2) if act == 1 else (F.relu(want) if act == 2 else want)
+    got = from_nhwc(y, cout).cpu().double()
+    err = (got - want).abs().max().item()
+    assert err <= 2 ** -8 * want.abs().max().item() + 1e-6, f"single-input fwd: max err {err:.3e}"
