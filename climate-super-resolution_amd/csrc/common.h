@@ -33,6 +33,15 @@ __device__ __forceinline__ s16x4 ds_read_tr16(const void* lds_ptr) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)(lds_ptr));
 }
 
+// Two transposed reads (rows k..k+3 and k+4..k+7 of one 16-lane column group) as ONE MFMA K-fragment of 8 bf16,
+// by vector shuffle: the halves land in adjacent VGPRs without per-element packing (a short[8] temporary made hipcc
+// emit v_bfi / v_perm per fragment).
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ bf16x8 cat_tr(s16x4 lo, s16x4 hi) {
+  const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
 // Buffer resource over [base, base + bytes): a raw buffer load whose byte offset is >= bytes returns zeros
 // (hardware range check), so halo / padding lanes get zeros without a branch around the load (a branch
 // around a load makes hipcc wait vmcnt(0) right there, which serialises a register prefetch).

@@ -2510,31 +2510,47 @@ __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
     }
     if (tile + a.nsplit < a.ntiles) issue(tile + a.nsplit);
     __syncthreads();
-#pragma unroll 2
-    for (int kk = 0; kk < TH * TW / 32; ++kk) {  // k-step: output pixel rows 2kk, 2kk+1
+    // k-step kk = output pixel rows 2kk, 2kk+1 of the tile; the fragments of k-step kk+1 are read from LDS while the
+    // MFMAs of kk run (one wave per SIMD cannot otherwise hide the read latency: ~14 waits per 36 MFMAs)
+    const bool last_short = TS == 2 && tg == 1;  // tap group 1 has 4 taps (5..8)
+    auto frags = [&](int kk, bf16x8 (&af)[4], bf16x8 (&bf)[NU]) {
       const int k0 = kk * 32 + 8 * g + q, k1 = k0 + 4;
-      bf16x8 af[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const s16x4 lo = ds_read_tr16(zs + k0 * W64_P + t * 16 + 4 * p);
-        const s16x4 hi = ds_read_tr16(zs + k1 * W64_P + t * 16 + 4 * p);
-        const short v8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        af[t] = __builtin_bit_cast(bf16x8, v8);
-      }
+      for (int t = 0; t < 4; ++t)
+        af[t] = cat_tr(ds_read_tr16(zs + k0 * W64_P + t * 16 + 4 * p), ds_read_tr16(zs + k1 * W64_P + t * 16 + 4 * p));
+      const int xb0 = (S * (k0 >> 4) * TPW + S * (k0 & 15)) * W64_P, xb1 = (S * (k1 >> 4) * TPW + S * (k1 & 15)) * W64_P;
+#pragma unroll
+      for (int u = 0; u < NU; ++u) bf[u] = cat_tr(ds_read_tr16(xs + xb0 + tapoff[u]), ds_read_tr16(xs + xb1 + tapoff[u]));
+    };
+    auto mma = [&](const bf16x8 (&af)[4], const bf16x8 (&bf)[NU]) {
       if (do_bias && wave == 0 && tg == 0) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) accb[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], ones, accb[t], 0, 0, 0);
       }
-      const int xb0 = (S * (k0 >> 4) * TPW + S * (k0 & 15)) * W64_P, xb1 = (S * (k1 >> 4) * TPW + S * (k1 & 15)) * W64_P;
 #pragma unroll
       for (int u = 0; u < NU; ++u) {
-        if (TS == 2 && u == NU - 1 && tg == 1) continue;  // tap group 1 has 4 taps (5..8)
-        const s16x4 lo = ds_read_tr16(xs + xb0 + tapoff[u]);
-        const s16x4 hi = ds_read_tr16(xs + xb1 + tapoff[u]);
-        const short v8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        const bf16x8 b = __builtin_bit_cast(bf16x8, v8);
+        if (u == NU - 1 && last_short) continue;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], b, acc[t][u], 0, 0, 0);
+        for (int t = 0; t < 4; ++t) acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bf[u], acc[t][u], 0, 0, 0);
+      }
+    };
+    constexpr int NK = TH * TW / 32;  // 4 (stride 1) or 2 (stride 2): even
+    if constexpr (TS == 1) {
+      bf16x8 afA[4], bfA[NU], afB[4], bfB[NU];
+      frags(0, afA, bfA);
+#pragma unroll 1
+      for (int kk = 0; kk < NK; kk += 2) {
+        frags(kk + 1, afB, bfB);
+        mma(afA, bfA);
+        if (kk + 2 < NK) frags(kk + 2, afA, bfA);
+        mma(afB, bfB);
+      }
+    } else {  // two waves per SIMD (256 VGPRs each): one fragment set, the partner wave hides the latency
+#pragma unroll 2
+      for (int kk = 0; kk < NK; ++kk) {
+        bf16x8 af[4], bf[NU];
+        frags(kk, af, bf);
+        mma(af, bf);
       }
     }
   }
