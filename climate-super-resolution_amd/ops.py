@@ -402,12 +402,12 @@ class RdbChain:
 
     def _launch(self, d, tag):
         """Forward = ``rdb_chain_kernel<0>`` (reads x: 64 ch, writes x1..x4: 64 ch); pull = ``rdb_chain_kernel<1>``
-        (reads dZ5: 16 ch and the stored activations x1..x4: 64 ch, writes dZ4..dZ1: 64 ch); bf16, every operand
+        (reads dZ5: 64 ch and the stored activations x1..x4: 64 ch, writes dZ4..dZ1: 64 ch); bf16, every operand
         once per pixel (the intermediate levels stay on chip)."""
         npx = d.n * d.h * d.w
         flops = sum(2 * self.convs[L].cin_real * 16 * 9 for L in range(4)) * npx
         pull = tag == "pull"
-        nbytes = npx * 2 * ((16 + 64 + 64) if pull else (64 + 64)) + sum(w.numel() * 2 for w in (self.w_pull if pull else self.w_fwd))
+        nbytes = npx * 2 * ((64 + 64 + 64) if pull else (64 + 64)) + sum(w.numel() * 2 for w in (self.w_pull if pull else self.w_fwd))
         _run(f"rdb_chain_kernel<{1 if pull else 0}>", flops, lambda: check(
             _lib.load().climsr_rdb_chain(ctypes.byref(d), _lib.stream_ptr()), f"rdb chain {self.name}"), tag + " " + self.name,
             nbytes)
