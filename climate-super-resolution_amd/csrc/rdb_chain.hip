@@ -70,49 +70,14 @@ __device__ __forceinline__ void dense_src(int L, int j, int g, int& tap, int& ch
   }
 }
 
-// Weight image in LDS during the prologue: level L's packed [16][9*KP] rows at element offset rc_woff(L), row pitch
-// 9*KP + 8 (the 16 B pad makes the 16 rows of a fragment read hit distinct banks).
-__host__ __device__ constexpr int rc_wpitch(int L) { return 9 * kp_blocks(L) * 32 + 8; }
-__host__ __device__ constexpr int rc_woff(int L) { return L <= 1 ? 0 : rc_woff(L - 1) + 16 * rc_wpitch(L - 1); }
-static_assert(rc_woff(5) * 2 <= RC_LDS, "weight image exceeds the LDS");
-
-// All four levels' packed weights -> LDS, each byte once per workgroup, 16 B per lane, every load of the copy in
-// flight before the first store (two waves per level would otherwise each fetch it from L2 in 64 B pieces).
+// A fragments of level L (16 co x 32 k per block) straight from the packed global weights ([16][9*KP], row pitch
+// 9*KP) into registers, kept for the whole launch: no LDS weight image, no workgroup barrier before the first base
+// rows are staged (the two waves of a level each fetch their 18-32 x 1 KB, L2-resident across the grid).
 template <int L>
-__device__ __forceinline__ void stage_issue(const ChainArgs& a, int tid, uint4 (&v)[5]) {
-  constexpr int CPR = 9 * kp_blocks(L) * 4, NI = (16 * CPR + 511) / 512;  // 16 B chunks per packed row
-#pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int q = tid + 512 * i;
-    v[i] = *(const uint4*)(a.wt[L - 1] + (long)(q < 16 * CPR ? q : 0) * 8);  // (unconditional: no branch per load)
-  }
-}
-template <int L>
-__device__ __forceinline__ void stage_store(uint16_t* lds, int tid, const uint4 (&v)[5]) {
-  constexpr int CPR = 9 * kp_blocks(L) * 4, NI = (16 * CPR + 511) / 512;
-#pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int q = tid + 512 * i, row = q / CPR, c = q - row * CPR;
-    if (q < 16 * CPR) *(uint4*)(lds + rc_woff(L) + row * rc_wpitch(L) + c * 8) = v[i];
-  }
-}
-__device__ __forceinline__ void stage_weights(const ChainArgs& a, uint16_t* lds, int tid) {
-  uint4 v1[5], v2[5], v3[5], v4[5];
-  stage_issue<1>(a, tid, v1);
-  stage_issue<2>(a, tid, v2);
-  stage_issue<3>(a, tid, v3);
-  stage_issue<4>(a, tid, v4);
-  stage_store<1>(lds, tid, v1);
-  stage_store<2>(lds, tid, v2);
-  stage_store<3>(lds, tid, v3);
-  stage_store<4>(lds, tid, v4);
-}
-
-template <int L>
-__device__ __forceinline__ void load_af(const uint16_t* lds, int lane, bf16x8 (&af)[n_blocks(L)]) {
+__device__ __forceinline__ void load_af_global(const uint16_t* __restrict__ wt, int lane, bf16x8 (&af)[n_blocks(L)]) {
   constexpr int KP = kp_blocks(L) * 32;
   const int g = lane >> 4, col = lane & 15;
-  const uint16_t* wr = lds + rc_woff(L) + col * rc_wpitch(L);
+  const uint16_t* wr = wt + col * 9 * KP;
 #pragma unroll
   for (int j = 0; j < 18; ++j) af[j] = *(const bf16x8*)(wr + (j >> 1) * KP + (j & 1) * 32 + g * 8);
 #pragma unroll
@@ -245,8 +210,7 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, uint16_t* lds, int
       m[k] = make_uint2(v[0], v[1]);
     }
   };
-  // Prologue (the weight image is already in LDS, see the kernel): the first base rows are in flight while each wave
-  // copies its level's A fragments into registers; the image is then overwritten by the rings.
+  // Prologue: the first base rows are in flight while each wave loads its level's A fragments.
   // Base rows are loaded one step before the step that stores them (two steps before their first use) and masks
   // one step before their use; the loop is unrolled x2 with alternating register sets, so no register copy of a
   // load still in flight (which would wait for it) is ever needed.
@@ -259,8 +223,7 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, uint16_t* lds, int
   if constexpr (MODE == 1) issue_mask(0, ma);
   const float4 bias = MODE == 0 ? *(const float4*)(a.bias[L - 1] + 4 * g) : make_float4(0.f, 0.f, 0.f, 0.f);
   bf16x8 af[n_blocks(L)];
-  load_af<L>(lds, lane, af);
-  lds_barrier();  // every wave holds its fragments
+  load_af_global<L>(a.wt[L - 1], lane, af);
   // dense ring: the slots of image columns -1 and >= w are never written, they are the zero padding
   for (int i = tid; i < RC_DD * (RC_COLS - a.w) * (RC_DP / 8); i += 512) {
     const int c = i % (RC_DP / 8), k = (i / (RC_DP / 8)) % (RC_COLS - a.w), r = i / (RC_DP / 8) / (RC_COLS - a.w);
@@ -332,17 +295,18 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, uint16_t* lds, int
   }
 }
 
-// Wave w computes level (w & 3) + 1 (waves w and w + 4 share a SIMD: each SIMD carries one level), fragments
-// 2 (w >> 2) and 2 (w >> 2) + 1.
+// Waves w and w + 4 share a SIMD (a workgroup's waves go round the 4 SIMDs in a fixed cyclic order).  Wave w < 4
+// computes level w + 1, wave w >= 4 level 8 - w, so each SIMD pairs a light and a heavy level (1+4, 2+3: 50 of the
+// 100 MFMA blocks per row each) instead of carrying one level: the per-step critical path is the slowest SIMD.
+// Wave w covers column fragments 2 (w >> 2) and 2 (w >> 2) + 1.
 template <int MODE>
 __global__ __launch_bounds__(512, 1) void rdb_chain_kernel(ChainArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint16_t* lds = (uint16_t*)smem;
   const int tid = threadIdx.x;
   const int nimg = blockIdx.x / a.strips_y, r0 = (blockIdx.x % a.strips_y) * a.rows;
-  stage_weights(a, lds, tid);
-  lds_barrier();
-  switch ((tid >> 6) & 3) {
+  const int w = tid >> 6;
+  switch (w < 4 ? w : 7 - w) {
     case 0: run_level<MODE, 1>(a, lds, tid, nimg, r0); break;
     case 1: run_level<MODE, 2>(a, lds, tid, nimg, r0); break;
     case 2: run_level<MODE, 3>(a, lds, tid, nimg, r0); break;
