@@ -1364,13 +1364,9 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
   // buffer loads (zeros out of range) and an unconditional call: the next tile's loads stay in flight
   // through this tile's compute (see conv_n16_kernel)
   const __amdgpu_buffer_rsrc_t xr = buf_rsrc(a.x, (uint32_t)((long)a.n * a.in_h * a.in_w * a.in_cs * 2));
-  auto issue = [&](int tile) {  // tile < 0: nothing to load
-    const bool live = tile >= 0;
-    int tt = live ? tile : 0;
-    const int tx = tt % a.tiles_x;
-    tt /= a.tiles_x;
-    const int ty = tt % a.tiles_y;
-    const int nimg = tt / a.tiles_y;
+  // tile coordinates advance incrementally by the walk's step (no per-tile integer divisions: wave-uniform
+  // divisions by runtime tile counts cost ~40 SALU each, 8 per tile, on the CU's shared scalar pipe)
+  auto issue = [&](bool live, int tx, int ty, int nimg) {  // !live: nothing to load
     const int iy0 = ty * (NW * MW) - a.pad, ix0 = tx * TW - a.pad;
     int ty_ = x_ty0, tx_ = x_tx0, cg = x_cg0;
 #pragma unroll
@@ -1390,18 +1386,26 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
     }
   };
   const TileWalk walk(ntiles);
-  if (walk.first < walk.end) issue(walk.first);
+  const int s_x = walk.step % a.tiles_x, s_y = (walk.step / a.tiles_x) % a.tiles_y, s_n = walk.step / (a.tiles_x * a.tiles_y);
+  auto advance = [&](int& tx, int& ty, int& n) {
+    tx += s_x;
+    int c = tx >= a.tiles_x;
+    tx -= c ? a.tiles_x : 0;
+    ty += s_y + c;
+    c = ty >= a.tiles_y;
+    ty -= c ? a.tiles_y : 0;
+    n += s_n + c;
+  };
+  int ctx = walk.first % a.tiles_x, cty = (walk.first / a.tiles_x) % a.tiles_y, cn = walk.first / (a.tiles_x * a.tiles_y);
+  if (walk.first < walk.end) issue(true, ctx, cty, cn);
 
   int pixbase[MW];
 #pragma unroll
   for (int m = 0; m < MW; ++m) pixbase[m] = ((wave * MW + m) * a.tpw + col) * a.ccp;
 
   for (int tile = walk.first; tile < walk.end; tile += walk.step) {
-    int tt = tile;
-    const int tx = tt % a.tiles_x;
-    tt /= a.tiles_x;
-    const int ty = tt % a.tiles_y;
-    const int nimg = tt / a.tiles_y;
+    const int tx = ctx, ty = cty, nimg = cn;
+    advance(ctx, cty, cn);  // the next tile of this workgroup
     const int ox0 = tx * TW, oy0 = ty * (NW * MW);
     lds_barrier();  // previous tile's epilogue reads of the aliased region are done
     {
@@ -1416,7 +1420,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
         if (tx_ >= a.tpw) { tx_ -= a.tpw; ++ty_; }
       }
     }
-    issue(tile + walk.step < walk.end ? tile + walk.step : -1);  // lands while this tile computes
+    issue(tile + walk.step < walk.end, ctx, cty, cn);  // lands while this tile computes
     lds_barrier();
     f32x4 acc[MW][NT];
 #pragma unroll
@@ -1424,19 +1428,32 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[m][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
     {
+      // k-steps two deep: k-step s+1's tap offset and fragments are read while s is on the MFMA pipe (one k-step at
+      // a time serialised tab read -> B read -> MFMAs, 3 lgkmcnt waits per 8 MFMAs)
       const int nks = a.kcpad / 32;
-      for (int kstep = 0; kstep < nks; ++kstep) {
-        const int off = tab[kstep * 4 + g];
-        bf16x8 af[NT], bfr[MW];
+      bf16x8 afA[NT], bfA[MW], afB[NT], bfB[MW];
+      auto ld = [&](int ks, bf16x8 (&af)[NT], bf16x8 (&bf)[MW]) {
+        const int off = tab[ks * 4 + g];
 #pragma unroll
-        for (int t = 0; t < NT; ++t) af[t] = *(const bf16x8*)(ws + (t * 16 + col) * wpitch + kstep * 32 + g * 8);
+        for (int t = 0; t < NT; ++t) af[t] = *(const bf16x8*)(ws + (t * 16 + col) * wpitch + ks * 32 + g * 8);
 #pragma unroll
-        for (int m = 0; m < MW; ++m) bfr[m] = *(const bf16x8*)(xs + pixbase[m] + off);
+        for (int m = 0; m < MW; ++m) bf[m] = *(const bf16x8*)(xs + pixbase[m] + off);
+      };
+      auto mm = [&](const bf16x8 (&af)[NT], const bf16x8 (&bf)[MW]) {
 #pragma unroll
         for (int m = 0; m < MW; ++m)
 #pragma unroll
-          for (int t = 0; t < NT; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bfr[m], acc[m][t], 0, 0, 0);
+          for (int t = 0; t < NT; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bf[m], acc[m][t], 0, 0, 0);
+      };
+      ld(0, afA, bfA);
+      int ks = 0;
+      for (; ks + 2 <= nks; ks += 2) {
+        ld(ks + 1, afB, bfB);
+        mm(afA, bfA);
+        ld(ks + 2 < nks ? ks + 2 : nks - 1, afA, bfA);  // clamped: no branch around the reads
+        mm(afB, bfB);
       }
+      if (ks < nks) mm(afA, bfA);
     }
     const int ox = ox0 + col;
     if constexpr (EP == 5) {  // 2x2 sum + activation backward (act' of the bf16 low-res activation res1), bf16 out,
@@ -2466,12 +2483,18 @@ __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
 
   constexpr int VZ = NZ / NTHR, VX = (NX + NTHR - 1) / NTHR;
   uint4 pz[VZ], px[VX];
-  auto issue = [&](int tile) {
-    int tt = tile;
-    const int tx = tt % a.tiles_x;
-    tt /= a.tiles_x;
-    const int ty = tt % a.tiles_y;
-    const int nimg = tt / a.tiles_y;
+  // split-strided tile walk with incremental coordinates (no per-tile integer divisions on the scalar pipe)
+  const int s_x = a.nsplit % a.tiles_x, s_y = (a.nsplit / a.tiles_x) % a.tiles_y, s_n = a.nsplit / (a.tiles_x * a.tiles_y);
+  int ntx = split % a.tiles_x, nty = (split / a.tiles_x) % a.tiles_y, nn = split / (a.tiles_x * a.tiles_y);
+  auto issue = [&]() {  // the tile at (ntx, nty, nn), then advance them by nsplit tiles
+    const int tx = ntx, ty = nty, nimg = nn;
+    ntx += s_x;
+    int c = ntx >= a.tiles_x;
+    ntx -= c ? a.tiles_x : 0;
+    nty += s_y + c;
+    c = nty >= a.tiles_y;
+    nty -= c ? a.tiles_y : 0;
+    nn += s_n + c;
     const int oy0 = ty * TH, ox0 = tx * TW;
 #pragma unroll
     for (int i = 0; i < VZ; ++i) {  // dz: pixel v/8, channel group v%8
@@ -2495,7 +2518,7 @@ __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
     }
   };
   int tile = split;
-  if (tile < a.ntiles) issue(tile);
+  if (tile < a.ntiles) issue();
   for (; tile < a.ntiles; tile += a.nsplit) {
     __syncthreads();  // previous tile's fragment reads done
 #pragma unroll
@@ -2508,7 +2531,7 @@ __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
       const int v = tid + NTHR * i;
       if (v < NX) *(uint4*)(xs + (v >> 3) * W64_P + (v & 7) * 8) = px[i];
     }
-    if (tile + a.nsplit < a.ntiles) issue(tile + a.nsplit);
+    if (tile + a.nsplit < a.ntiles) issue();
     __syncthreads();
     // k-step kk = output pixel rows 2kk, 2kk+1 of the tile; the fragments of k-step kk+1 are read from LDS while the
     // MFMAs of kk run (one wave per SIMD cannot otherwise hide the read latency: ~14 waits per 36 MFMAs)
