@@ -482,15 +482,133 @@ __global__ void adaptive_pool_bwd_kernel(const float* __restrict__ dp, int n, in
   dx[idx] = s;
 }
 
+// Tiled forms (the discriminator's 16x16 -> 14x14 over 512 channels, 32 images): one workgroup per (image, AP_CB
+// channels).  The element-per-thread kernels above gather / scatter with a 196-element stride between neighbouring
+// lanes (NCHW flatten vs NHWC), 33 / 72 us per launch for 16 MB.
+constexpr int AP_CB = 64;
+constexpr size_t AP_LDS = 64 * 1024;
+
+// Window tables (integer divisions once per workgroup, not per element): output row / column windows [y0, y1) /
+// [x0, x1); for the backward, the (at most AP_MAXC) output rows / columns whose windows contain each input row /
+// column, with the window extents.  Element loops read them with independent lookups (no per-element division
+// chains: a dependent LDS lookup chain per element kept these kernels latency-bound at 4 waves per CU).
+constexpr int AP_MAXD = 64, AP_MAXC = 3, AP_SPLIT = 4;
+__device__ __forceinline__ void ap_win_tables(int h, int w, int oh, int ow, int* y0, int* y1, int* x0, int* x1) {
+  for (int i = threadIdx.x; i < oh; i += blockDim.x) { y0[i] = (i * h) / oh; y1[i] = ((i + 1) * h + oh - 1) / oh; }
+  for (int j = threadIdx.x; j < ow; j += blockDim.x) { x0[j] = (j * w) / ow; x1[j] = ((j + 1) * w + ow - 1) / ow; }
+}
+// cand[p][k] = k-th output index whose window [lo, hi) contains input p (or -1), ext[p][k] = hi - lo
+__device__ __forceinline__ void ap_cand_tables(int in, int out, int (*cand)[AP_MAXC], int (*ext)[AP_MAXC]) {
+  for (int p = threadIdx.x; p < in; p += blockDim.x) {
+    int k = 0;
+    const int lo = max(0, (p * out) / in - 1), hi = min(out - 1, ((p + 1) * out + in - 1) / in);
+    for (int o = lo; o <= hi && k < AP_MAXC; ++o) {
+      const int s0 = (o * in) / out, s1 = ((o + 1) * in + out - 1) / out;
+      if (p >= s0 && p < s1) { cand[p][k] = o; ext[p][k] = s1 - s0; ++k; }
+    }
+    for (; k < AP_MAXC; ++k) { cand[p][k] = -1; ext[p][k] = 1; }
+  }
+}
+
+// grid (c / AP_CB, n, AP_SPLIT): workgroup z computes output positions [z*no/S, (z+1)*no/S) of 64 channels
+__global__ __launch_bounds__(256) void adaptive_pool_fwd_tile_kernel(const uint16_t* __restrict__ x, int h, int w, int c, int oh, int ow,
+                                                                    uint16_t* __restrict__ out) {
+  __shared__ uint16_t xs[AP_LDS / 2];  // [channel][h*w] bf16, channel pitch h*w + 1
+  __shared__ int ty0[AP_MAXD], ty1[AP_MAXD], tx0[AP_MAXD], tx1[AP_MAXD];
+  const int b = blockIdx.y, c0 = blockIdx.x * AP_CB, hw = h * w, pitch = hw + 1, no = oh * ow;
+  ap_win_tables(h, w, oh, ow, ty0, ty1, tx0, tx1);
+  const uint16_t* xb = x + (long)b * hw * c + c0;
+  for (int i = threadIdx.x; i < hw * AP_CB; i += 256) {  // coalesced NHWC read (64 channels = 128 B per pixel)
+    const int px = i / AP_CB, ch = i - px * AP_CB;
+    xs[ch * pitch + px] = xb[(long)px * c + ch];
+  }
+  __syncthreads();
+  const int r0 = no * blockIdx.z / AP_SPLIT, r1 = no * (blockIdx.z + 1) / AP_SPLIT, nr = r1 - r0;
+  uint16_t* ob = out + (long)b * c * no + (long)c0 * no;
+  for (int i = threadIdx.x; i < AP_CB * nr; i += 256) {  // (channel, position) with position fastest: contiguous runs
+    const int ch = i / nr, r = r0 + i - ch * nr, oi = r / ow, oj = r - oi * ow;
+    const int y0 = ty0[oi], y1 = ty1[oi], x0 = tx0[oj], x1 = tx1[oj];
+    float sm = 0.f;
+    for (int yy = y0; yy < y1; ++yy)
+      for (int xx = x0; xx < x1; ++xx) sm += bf2f(xs[ch * pitch + yy * w + xx]);
+    ob[(long)ch * no + r] = f2bf(sm / (float)((y1 - y0) * (x1 - x0)));
+  }
+}
+
+// out_t[f][b] = out[b][f] for b < n, 0 for n <= b < n_pad: 64 x 64 tiles through LDS
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const uint16_t* __restrict__ in, int n, long feat, int n_pad,
+                                                             uint16_t* __restrict__ out) {
+  __shared__ uint16_t t[64][66];
+  const long f0 = (long)blockIdx.x * 64;
+  const int b0 = blockIdx.y * 64;
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int bb = i / 64, ff = i % 64;
+    const long f = f0 + ff;
+    t[bb][ff] = (b0 + bb < n && f < feat) ? in[(long)(b0 + bb) * feat + f] : (uint16_t)0;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int ff = i / 64, bb = i % 64;
+    const long f = f0 + ff;
+    if (f < feat && b0 + bb < n_pad) out[f * n_pad + b0 + bb] = t[bb][ff];
+  }
+}
+
+// grid (c / AP_CB, n, AP_SPLIT): workgroup z writes input rows [z*h/S, (z+1)*h/S) of 64 channels
+__global__ __launch_bounds__(256) void adaptive_pool_bwd_tile_kernel(const float* __restrict__ dp, int h, int w, int c, int oh, int ow,
+                                                                    float* __restrict__ dx) {
+  __shared__ float ds[AP_LDS / 4];  // [channel][oh*ow], channel pitch oh*ow + 1 (conflict-free column reads)
+  __shared__ int rc[AP_MAXD][AP_MAXC], re[AP_MAXD][AP_MAXC], cc_[AP_MAXD][AP_MAXC], ce[AP_MAXD][AP_MAXC];
+  const int b = blockIdx.y, c0 = blockIdx.x * AP_CB, no = oh * ow, pitch = no + 1;
+  ap_cand_tables(h, oh, rc, re);
+  ap_cand_tables(w, ow, cc_, ce);
+  const float* db = dp + (long)b * c * no + (long)c0 * no;
+  for (int i = threadIdx.x; i < AP_CB * no; i += 256) {  // contiguous read of the 64 channels' pooled gradients
+    const int ch = i / no;
+    ds[ch * pitch + (i - ch * no)] = db[i];
+  }
+  __syncthreads();
+  const int y0 = h * blockIdx.z / AP_SPLIT, y1 = h * (blockIdx.z + 1) / AP_SPLIT;
+  float* xb = dx + (long)b * h * w * c + c0;
+  const int ch = threadIdx.x % AP_CB;
+  for (int q = threadIdx.x / AP_CB; q < (y1 - y0) * w; q += 256 / AP_CB) {  // (pixel, channel), channel fastest
+    const int yy = y0 + q / w, xx = q - (q / w) * w;
+    float sm = 0.f;
+#pragma unroll
+    for (int u = 0; u < AP_MAXC; ++u) {
+      const int oi = rc[yy][u];
+      if (oi < 0) break;
+#pragma unroll
+      for (int v = 0; v < AP_MAXC; ++v) {
+        const int oj = cc_[xx][v];
+        if (oj < 0) break;
+        sm += ds[ch * pitch + oi * ow + oj] / (float)(re[yy][u] * ce[xx][v]);
+      }
+    }
+    xb[((long)yy * w + xx) * c + ch] = sm;
+  }
+}
+
 extern "C" int climsr_adaptive_pool_fwd(const uint16_t* x, int n, int h, int w, int c, int oh, int ow, uint16_t* out,
                                         uint16_t* out_t, int n_pad, void* stream) {
   if (!x || !out || oh <= 0 || ow <= 0 || (out_t && n_pad < n)) {
     set_error("adaptive_pool_fwd: bad args");
     return CLIMSR_EINVAL;
   }
+  hipStream_t st = (hipStream_t)stream;
+  if (c % AP_CB == 0 && ((size_t)h * w + 1) * AP_CB * 2 <= AP_LDS && oh <= AP_MAXD && ow <= AP_MAXD) {
+    // one workgroup per (image, 64 channels): NHWC tile staged once, NCHW-flattened output written contiguously;
+    // the [feat][n_pad] copy by a tiled transpose (both sides coalesced)
+    hipLaunchKernelGGL(adaptive_pool_fwd_tile_kernel, dim3(c / AP_CB, n, AP_SPLIT), dim3(256), 0, st, x, h, w, c, oh, ow, out);
+    if (out_t) {
+      const long feat = (long)c * oh * ow;
+      hipLaunchKernelGGL(transpose_bf16_kernel, dim3(ceil_div(feat, 64), ceil_div(n_pad, 64)), dim3(256), 0, st, out, n, feat, n_pad,
+                         out_t);
+    }
+    return check_launch("adaptive_pool_fwd");
+  }
   long total = (long)n * oh * ow * c;
-  hipLaunchKernelGGL(adaptive_pool_fwd_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, x, n, h, w, c, oh, ow,
-                     out, out_t, n_pad);
+  hipLaunchKernelGGL(adaptive_pool_fwd_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, st, x, n, h, w, c, oh, ow, out, out_t, n_pad);
   return check_launch("adaptive_pool_fwd");
 }
 
@@ -498,6 +616,12 @@ extern "C" int climsr_adaptive_pool_bwd(const float* dp, int n, int h, int w, in
   if (!dp || !dx || oh <= 0 || ow <= 0) {
     set_error("adaptive_pool_bwd: bad args");
     return CLIMSR_EINVAL;
+  }
+  if (c % AP_CB == 0 && ((size_t)oh * ow + 1) * AP_CB * 4 <= AP_LDS && h <= AP_MAXD && w <= AP_MAXD && oh <= AP_MAXD &&
+      ow <= AP_MAXD && oh <= 2 * h && ow <= 2 * w && h >= AP_SPLIT) {
+    hipLaunchKernelGGL(adaptive_pool_bwd_tile_kernel, dim3(c / AP_CB, n, AP_SPLIT), dim3(256), 0, (hipStream_t)stream, dp, h, w, c, oh,
+                       ow, dx);
+    return check_launch("adaptive_pool_bwd");
   }
   long total = (long)n * h * w * c;
   hipLaunchKernelGGL(adaptive_pool_bwd_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, dp, n, h, w, c, oh,
@@ -572,8 +696,16 @@ __global__ void linear_reduce_kernel(const float* __restrict__ part, int nsplit,
                                      float slope, float* __restrict__ y, uint16_t* __restrict__ ybf) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (long)n * o) return;
-  float s = 0.f;
-  for (int sp = 0; sp < nsplit; ++sp) s += part[(long)sp * n * o + idx];
+  // 8 independent partial sums (loads in flight together), combined in a fixed order: deterministic
+  const long stride = (long)n * o;
+  float a8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int sp = 0;
+  for (; sp + 8 <= nsplit; sp += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a8[u] += part[(long)(sp + u) * stride + idx];
+  }
+  for (; sp < nsplit; ++sp) a8[0] += part[(long)sp * stride + idx];
+  float s = ((a8[0] + a8[1]) + (a8[2] + a8[3])) + ((a8[4] + a8[5]) + (a8[6] + a8[7]));
   if (bias) s += bias[idx % o];
   s = act_apply(s, act, slope);
   y[idx] = s;
@@ -735,23 +867,22 @@ extern "C" int climsr_linear_wgrad(const uint16_t* dy_t, const uint16_t* x_t, in
 // db0 += sum_n du0; du0 written as bf16 [n][o] and transposed [o][n_pad] for the fc.0 grads.
 // One workgroup, n <= 64, fixed reduction order.
 // ---------------------------------------------------------------------------------------------
+// one workgroup per image (blockIdx.x = b), fixed-order tree reduction
 __global__ __launch_bounds__(256) void d_head_fwd_kernel(const float* __restrict__ h, const float* __restrict__ w2,
                                                          const float* __restrict__ b2, int n, int o, int sigmoid, float* __restrict__ s) {
   __shared__ float red[256];
-  for (int b = 0; b < n; ++b) {
-    float t = 0.f;
-    for (int j = threadIdx.x; j < o; j += 256) t += h[(long)b * o + j] * w2[j];
-    red[threadIdx.x] = t;
+  const int b = blockIdx.x;
+  float t = 0.f;
+  for (int j = threadIdx.x; j < o; j += 256) t += h[(long)b * o + j] * w2[j];
+  red[threadIdx.x] = t;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
     __syncthreads();
-    for (int st = 128; st > 0; st >>= 1) {
-      if (threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-      float u = red[0] + b2[0];
-      s[b] = sigmoid ? 1.f / (1.f + expf(-u)) : u;
-    }
-    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float u = red[0] + b2[0];
+    s[b] = sigmoid ? 1.f / (1.f + expf(-u)) : u;
   }
 }
 
@@ -759,24 +890,33 @@ __global__ __launch_bounds__(256) void d_head_bwd_kernel(const float* __restrict
                                                          const float* __restrict__ w2, int n, int o, int n_pad, float slope, int sigmoid,
                                                          float* dw2, float* db2, float* db0, int accumulate, uint16_t* __restrict__ du0,
                                                          uint16_t* __restrict__ du0_t) {
-  for (int j = threadIdx.x; j < o; j += 256) {
+  const int j = blockIdx.x * 256 + threadIdx.x;  // one hidden unit per thread over the grid
+  if (j < o) {
     float a_w2 = 0.f, a_b0 = 0.f;
-    for (int b = 0; b < n_pad; ++b) {
-      float v = 0.f;
-      if (b < n) {
-        const float du = sigmoid ? ds[b] * s[b] * (1.f - s[b]) : ds[b];
-        const float hv = h[(long)b * o + j];
-        a_w2 += du * hv;
-        v = du * w2[j] * (hv > 0.f ? 1.f : slope);
-        a_b0 += v;
-        du0[(long)b * o + j] = f2bf(v);
+    uint4* trow = (uint4*)(du0_t + (long)j * n_pad);  // n_pad % 32 == 0: whole 16 B vectors per row
+    for (int b8 = 0; b8 < n_pad; b8 += 8) {
+      uint32_t pk[4];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int b = b8 + q;
+        float v = 0.f;
+        if (b < n) {
+          const float du = sigmoid ? ds[b] * s[b] * (1.f - s[b]) : ds[b];
+          const float hv = h[(long)b * o + j];
+          a_w2 += du * hv;
+          v = du * w2[j] * (hv > 0.f ? 1.f : slope);
+          a_b0 += v;
+          du0[(long)b * o + j] = f2bf(v);
+        }
+        if (q & 1) pk[q >> 1] |= (uint32_t)f2bf(v) << 16;
+        else pk[q >> 1] = f2bf(v);
       }
-      du0_t[(long)j * n_pad + b] = f2bf(v);
+      trow[b8 / 8] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
     }
     if (dw2) dw2[j] = (accumulate ? dw2[j] : 0.f) + a_w2;
     if (db0) db0[j] = (accumulate ? db0[j] : 0.f) + a_b0;
   }
-  if (threadIdx.x == 0 && db2) {
+  if (blockIdx.x == 0 && threadIdx.x == 0 && db2) {
     float t = 0.f;
     for (int b = 0; b < n; ++b) t += sigmoid ? ds[b] * s[b] * (1.f - s[b]) : ds[b];
     db2[0] = (accumulate ? db2[0] : 0.f) + t;
@@ -789,19 +929,19 @@ extern "C" int climsr_d_head_fwd(const float* h, const float* w2, const float* b
     set_error("d_head_fwd: bad args");
     return CLIMSR_EINVAL;
   }
-  hipLaunchKernelGGL(d_head_fwd_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, h, w2, b2, n, o, sigmoid, s);
+  hipLaunchKernelGGL(d_head_fwd_kernel, dim3(n), dim3(256), 0, (hipStream_t)stream, h, w2, b2, n, o, sigmoid, s);
   return check_launch("d_head_fwd");
 }
 
 extern "C" int climsr_d_head_bwd(const float* h, const float* s, const float* ds, const float* w2, int n, int o, int n_pad, float slope,
                                  int sigmoid, float* dw2, float* db2, float* db0, int accumulate, uint16_t* du0, uint16_t* du0_t,
                                  void* stream) {
-  if (!h || !s || !ds || !w2 || !du0 || !du0_t || n_pad < n) {
+  if (!h || !s || !ds || !w2 || !du0 || !du0_t || n_pad < n || n_pad % 32) {
     set_error("d_head_bwd: bad args");
     return CLIMSR_EINVAL;
   }
-  hipLaunchKernelGGL(d_head_bwd_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, h, s, ds, w2, n, o, n_pad, slope, sigmoid, dw2, db2,
-                     db0, accumulate, du0, du0_t);
+  hipLaunchKernelGGL(d_head_bwd_kernel, dim3(ceil_div(o, 256)), dim3(256), 0, (hipStream_t)stream, h, s, ds, w2, n, o, n_pad, slope, sigmoid,
+                     dw2, db2, db0, accumulate, du0, du0_t);
   return check_launch("d_head_bwd");
 }
 
@@ -817,23 +957,31 @@ __device__ inline double bcewl(double x, double t) { return fmax(x, 0.0) - x * t
 __global__ void rel_bce_kernel(const float* __restrict__ sr, const float* __restrict__ sf, int n, float t_rf, float t_fr,
                                float* __restrict__ loss, const float* __restrict__ gscale, float* __restrict__ gr,
                                float* __restrict__ gf) {
-  if (threadIdx.x != 0) return;
-  double mr = 0.0, mf = 0.0;
-  for (int i = 0; i < n; ++i) { mr += sr[i]; mf += sf[i]; }
-  mr /= n;
-  mf /= n;
-  double l_rf = 0.0, l_fr = 0.0, sum_drf = 0.0, sum_dfr = 0.0;
-  for (int i = 0; i < n; ++i) {
+  // one wave; lane l owns samples l, l+64, ... (summed in that order), then a fixed butterfly: deterministic
+  const int l = threadIdx.x;
+  auto wsum = [](double v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+    return v;
+  };
+  double pr = 0.0, pf = 0.0;
+  for (int i = l; i < n; i += 64) { pr += sr[i]; pf += sf[i]; }
+  const double mr = wsum(pr) / n, mf = wsum(pf) / n;
+  double l_rf = 0.0, l_fr = 0.0, s_drf = 0.0, s_dfr = 0.0;
+  for (int i = l; i < n; i += 64) {
     const double rf = sr[i] - mf, fr = sf[i] - mr;
     l_rf += bcewl(rf, t_rf);
     l_fr += bcewl(fr, t_fr);
-    sum_drf += 0.5 / n * (1.0 / (1.0 + exp(-rf)) - t_rf);
-    sum_dfr += 0.5 / n * (1.0 / (1.0 + exp(-fr)) - t_fr);
+    s_drf += 0.5 / n * (1.0 / (1.0 + exp(-rf)) - t_rf);
+    s_dfr += 0.5 / n * (1.0 / (1.0 + exp(-fr)) - t_fr);
   }
-  if (loss) loss[0] = (float)((l_rf / n + l_fr / n) / 2.0);
+  l_rf = wsum(l_rf);
+  l_fr = wsum(l_fr);
+  const double sum_drf = wsum(s_drf), sum_dfr = wsum(s_dfr);
+  if (loss && l == 0) loss[0] = (float)((l_rf / n + l_fr / n) / 2.0);
   if (gscale) {
     const double gs = gscale[0];
-    for (int i = 0; i < n; ++i) {
+    for (int i = l; i < n; i += 64) {
       const double rf = sr[i] - mf, fr = sf[i] - mr;
       const double drf = 0.5 / n * (1.0 / (1.0 + exp(-rf)) - t_rf);
       const double dfr = 0.5 / n * (1.0 / (1.0 + exp(-fr)) - t_fr);
