@@ -41,6 +41,10 @@ class Epilogue(ctypes.Structure):
         super().__init__(*args, **kw)
 
 
+class Planes8(ctypes.Structure):
+    _fields_ = [("p", c_void_p * 8), ("img_stride", ctypes.c_int64 * 8)]
+
+
 class PackDesc(ctypes.Structure):
     _fields_ = [("w", c_void_p), ("out", c_void_p)] + [(n, ctypes.c_int32) for n in (
         "out_c", "in_c", "in_c_real", "out_c_real", "ks", "cc", "tflip", "reserved")]
@@ -112,6 +116,7 @@ SIGNATURES = {
     "climsr_act_grad": (c_int, [c_int64, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int, c_float, c_float,
                                 c_void_p, c_int, c_void_p]),
     "climsr_nchw_to_nhwc_bf16": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p]),
+    "climsr_pack_planes_nhwc8_bf16": (c_int, [ctypes.POINTER(Planes8), c_int, c_int, c_int, c_void_p, c_void_p]),
     "climsr_nhwc_to_nchw_f32": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "climsr_axpby_f32": (c_int, [c_int64, c_int, c_float, c_void_p, c_int, c_int, c_float, c_void_p, c_int, c_int, c_void_p]),
     "climsr_rdb_bwd_init": (c_int, [c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_int,

@@ -3068,6 +3068,19 @@ extern "C" const char* climsr_conv2d_wgrad_kernel(const ClimsrConvDesc* d) {
 
 // 256 threads = 32 consecutive outputs x 8 split groups (8 independent load chains per output,
 // coalesced 128 B rows), combined in a fixed order through LDS: deterministic.
+// Split group sg's share of the nsplit partials (sg, sg+8, ...): 4 independent chains so the loads are in flight
+// together (one chain waited for each load in turn), combined in a fixed order.
+__device__ __forceinline__ float sum_splits(const float* src, long sstride, int sg, int nsplit) {
+  float a4[4] = {0.f, 0.f, 0.f, 0.f};
+  int sp = sg;
+  for (; sp + 24 < nsplit; sp += 32) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a4[u] += src[(long)(sp + 8 * u) * sstride];
+  }
+  for (; sp < nsplit; sp += 8) a4[0] += src[(long)sp * sstride];
+  return (a4[0] + a4[1]) + (a4[2] + a4[3]);
+}
+
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, const float* __restrict__ bpart,
                                                           int nsplit, int out_c, int in_c_real, int in_c, int ks2, int co_rows,
                                                           int kw, float* __restrict__ wg, float* __restrict__ bg, int accumulate) {
@@ -3088,11 +3101,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
     src = bpart + (idx - nw);
     sstride = co_rows;
   }
-  float acc = 0.f;
-  if (src) {
-    for (int sp = sg; sp < nsplit; sp += 8) acc += src[(long)sp * sstride];
-  }
-  red[sg][lane] = acc;
+  red[sg][lane] = src ? sum_splits(src, sstride, sg, nsplit) : 0.f;
   __syncthreads();
   if (sg == 0 && idx < total) {
     float t = 0.f;
@@ -3129,10 +3138,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_rows_kernel(const float* __r
     src = bpart + d.row0 + (idx - nw);
     sstride = co_rows;
   }
-  float acc = 0.f;
-  if (src)
-    for (int sp = sg; sp < nsplit; sp += 8) acc += src[(long)sp * sstride];
-  red[sg][lane] = acc;
+  red[sg][lane] = src ? sum_splits(src, sstride, sg, nsplit) : 0.f;
   __syncthreads();
   if (sg == 0 && idx < total) {
     float t = 0.f;

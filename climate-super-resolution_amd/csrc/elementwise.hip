@@ -101,6 +101,34 @@ extern "C" int climsr_nchw_to_nhwc_bf16(const float* src, int n, int c, int h, i
   return check_launch("nchw_to_nhwc_bf16");
 }
 
+// Up to 8 fp32 planes ([n] images of h*w, image stride per plane) -> one bf16 NHWC pixel of 8 channels per thread, a
+// single 16 B store (channel k = plane k, zero where the plane is absent): the padded network inputs (G's lr /
+// elevation / mask, D's input, the perceptual loss's 3-channel repeat) in one pass, no zero fill beforehand and no
+// 2-byte strided stores.
+__global__ void pack_planes8_kernel(ClimsrPlanes8 pl, int n, long hw, uint16_t* __restrict__ dst) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)n * hw) return;
+  const long b = idx / hw, r = idx - b * hw;
+  uint32_t v[4];
+#pragma unroll
+  for (int k = 0; k < 8; k += 2) {
+    const uint16_t lo = pl.p[k] ? f2bf(pl.p[k][b * pl.img_stride[k] + r]) : (uint16_t)0;
+    const uint16_t hi = pl.p[k + 1] ? f2bf(pl.p[k + 1][b * pl.img_stride[k + 1] + r]) : (uint16_t)0;
+    v[k >> 1] = (uint32_t)lo | ((uint32_t)hi << 16);
+  }
+  *(uint4*)(dst + idx * 8) = make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+extern "C" int climsr_pack_planes_nhwc8_bf16(const ClimsrPlanes8* planes, int n, int h, int w, uint16_t* dst, void* stream) {
+  if (!planes || !dst || n <= 0 || h <= 0 || w <= 0) {
+    set_error("pack_planes_nhwc8_bf16: bad args");
+    return CLIMSR_EINVAL;
+  }
+  const long total = (long)n * h * w;
+  hipLaunchKernelGGL(pack_planes8_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, *planes, n, (long)h * w, dst);
+  return check_launch("pack_planes_nhwc8_bf16");
+}
+
 __global__ void nhwc_to_nchw_kernel(const void* __restrict__ src, int is_bf16, int n, int c, int h, int w, int cs, int co,
                                     float* __restrict__ dst) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;

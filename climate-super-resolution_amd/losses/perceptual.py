@@ -91,10 +91,11 @@ class PerceptualLoss(nn.Module):
             self.loss_network.to(a.device)
             self._build(a.device)
         n, _c, h, w = a.shape
-        x3 = torch.zeros((2 * n, h, w, 8), dtype=torch.bfloat16, device=a.device)
-        for ch in range(3):  # torch.cat([x, x, x], dim=1)  (perceptual.py:26-31)
-            ops.nchw_to_nhwc(a.contiguous().float(), x3[:n], 8, ch)
-            ops.nchw_to_nhwc(b.contiguous().float(), x3[n:], 8, ch)
+        x3 = torch.empty((2 * n, h, w, 8), dtype=torch.bfloat16, device=a.device)
+        a32, b32 = a.contiguous().float(), b.contiguous().float()
+        # torch.cat([x, x, x], dim=1) (perceptual.py:26-31) as channels 0..2 of the padded NHWC input, one pass each
+        ops.pack_planes8([(a32, 0)] * 3, n, h, w, x3[:n])
+        ops.pack_planes8([(b32, 0)] * 3, n, h, w, x3[n:])
         f = self.features(x3, 2 * n, h, w)
         half = f.numel() // 2
         ws = torch.empty(512, dtype=torch.float64, device=a.device)

@@ -25,7 +25,7 @@ from torch import Tensor
 
 from ..core.flat import FlatParamsMixin
 from ..ops import (ACT_LRELU, ACT_LRELU_BWD, ACT_NONE, ACT_RELU, ACT_RELU_BWD, OUT_F32, BatchedPacker, ConvPlan, GroupedWgrad, PullPacker, PullPlan,
-                   RdbChain, Workspace, act_grad, axpby, nchw_to_nhwc)
+                   RdbChain, Workspace, act_grad, axpby, nchw_to_nhwc, pack_planes8)
 from .srcnn import SRCNN
 
 
@@ -197,8 +197,12 @@ class _Engine:
         P = self.plans
         self.ensure_packed()
         x = x.contiguous().float()
-        lr = torch.zeros((n, h, w, self.cin_pad), dtype=torch.bfloat16, device=dev)
-        nchw_to_nhwc(x, lr, self.cin_pad, 0)
+        if self.cin_pad == 8:  # lr channels + zero padding in one full-pixel pass
+            lr = torch.empty((n, h, w, 8), dtype=torch.bfloat16, device=dev)
+            pack_planes8([(x, k) for k in range(x.shape[1])], n, h, w, lr)
+        else:
+            lr = torch.zeros((n, h, w, self.cin_pad), dtype=torch.bfloat16, device=dev)
+            nchw_to_nhwc(x, lr, self.cin_pad, 0)
         ndense = 3 * nb + 1 if keep else 2
         dense = [_bf16((n, h, w, dc), dev) for _ in range(ndense)]
         rrdb_in = _bf16((n, h, w, nf), dev) if not keep else None

@@ -79,8 +79,13 @@ class _DEngine:
         dev = x.device
         self.ensure_packed()
         cpad = (cin + 7) // 8 * 8
-        x8 = torch.zeros((n, h, w, cpad), dtype=torch.bfloat16, device=dev)
-        ops.nchw_to_nhwc(x.contiguous().float(), x8, cpad, 0)
+        xc = x.contiguous().float()
+        if cpad == 8:  # channels 0..cin-1 + zero padding in one full-pixel pass
+            x8 = torch.empty((n, h, w, 8), dtype=torch.bfloat16, device=dev)
+            ops.pack_planes8([(xc, k) for k in range(cin)], n, h, w, x8)
+        else:
+            x8 = torch.zeros((n, h, w, cpad), dtype=torch.bfloat16, device=dev)
+            ops.nchw_to_nhwc(xc, x8, cpad, 0)
         a_prev, cs_prev, hh, ww = x8, cpad, h, w
         saved = []
         training = d.training

@@ -309,6 +309,23 @@ def nchw_to_nhwc(src: torch.Tensor, dst: torch.Tensor, cs: int, co: int) -> None
     _launch("nchw_to_nhwc", lambda: _lib.load().climsr_nchw_to_nhwc_bf16(ptr(src), n, c, h, w, ptr(dst), cs, co, _lib.stream_ptr()))
 
 
+def pack_planes8(planes, n: int, h: int, w: int, dst: torch.Tensor) -> None:
+    """dst [n,h,w,8] bf16 (all 8 channels written): channel k = planes[k] (an fp32 [n,c,h,w] tensor and its channel
+    index, or None -> zeros)."""
+    assert dst.dtype == torch.bfloat16 and dst.is_contiguous() and dst.shape[-1] == 8 and len(planes) <= 8
+    pl = _lib.Planes8()
+    for k, spec in enumerate(planes):
+        if spec is None:
+            continue
+        t, ch = spec
+        assert t.dtype == torch.float32 and t.is_contiguous() and t.shape[0] == n and t.shape[2:] == (h, w)
+        pl.p[k] = t.data_ptr() + ch * h * w * 4
+        pl.img_stride[k] = t.shape[1] * h * w
+    keep = [spec[0] for spec in planes if spec is not None]  # keep the sources alive until the launch is queued
+    _launch("pack_planes8", lambda: _lib.load().climsr_pack_planes_nhwc8_bf16(ctypes.byref(pl), n, h, w, ptr(dst), _lib.stream_ptr()),
+            nbytes=n * h * w * (16 + 4 * len(keep)))
+
+
 def nhwc_to_nchw(src: torch.Tensor, n: int, c: int, h: int, w: int, cs: int, co: int, dst: torch.Tensor) -> None:
     is_bf16 = 1 if src.dtype == torch.bfloat16 else 0
     _launch("nhwc_to_nchw", lambda: _lib.load().climsr_nhwc_to_nchw_f32(ptr(src), is_bf16, n, c, h, w, cs, co, ptr(dst), _lib.stream_ptr()))

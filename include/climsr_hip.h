@@ -203,6 +203,15 @@ int climsr_act_grad(int64_t npix, int c_real, const float* g, int g_cstride, int
                     int y_cstride, int y_coff, int act, float slope, float scale, uint16_t* dz, int dz_cstride,
                     void* stream);
 
+/* Up to 8 fp32 image planes -> a bf16 NHWC buffer of exactly 8 channels per pixel (channel k = plane k, zeros where
+ * p[k] is NULL), one 16 B store per pixel: the padded inputs of the networks (esrgan.py:89 lr + srcnn.py:13 elevation /
+ * mask concatenation, rfb_esrgan.py:28 input, perceptual.py:26-31 torch.cat([x, x, x])).  Plane k of image b is
+ * p[k] + b * img_stride[k] (elements), h*w contiguous fp32 values. */
+typedef struct ClimsrPlanes8 {
+  const float* p[8];
+  int64_t img_stride[8];
+} ClimsrPlanes8;
+int climsr_pack_planes_nhwc8_bf16(const ClimsrPlanes8* planes, int n, int h, int w, uint16_t* dst, void* stream);
 /* NCHW fp32 -> NHWC bf16 (pad channels with 0): dst[n][h][w][coff+c] = src[n][c][h][w]. */
 int climsr_nchw_to_nhwc_bf16(const float* src, int n, int c, int h, int w, uint16_t* dst, int cstride, int coff,
                              void* stream);

@@ -62,7 +62,7 @@ def test_struct_layouts_match_header(lib):
 
 STRUCTS = {"ConvDesc": "ClimsrConvDesc", "Epilogue": "ClimsrEpilogue", "PackDesc": "ClimsrPackDesc",
            "ReduceDesc": "ClimsrReduceDesc", "ChainDesc": "ClimsrChainDesc", "PullPackDesc": "ClimsrPullPackDesc",
-           "TileDesc": "ClimsrTileDesc", "MetricsDesc": "ClimsrMetricsDesc"}
+           "TileDesc": "ClimsrTileDesc", "MetricsDesc": "ClimsrMetricsDesc", "Planes8": "ClimsrPlanes8"}
 
 
 def test_struct_offsets_match_gcc(lib, tmp_path):
