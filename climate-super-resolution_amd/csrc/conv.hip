@@ -1826,6 +1826,16 @@ __global__ __launch_bounds__(256) void dgrad_ci1_kernel(int n, int h, int w, int
     wl[t * C + c] = wt[i];
   }
   __syncthreads();
+  // 3x3: this thread's 8 channels x 9 taps of weights held in registers across the passes (72 VGPRs); 5x5 re-reads LDS
+  constexpr bool WREG = KS == 3;
+  float4 wr0[WREG ? KS * KS : 1], wr1[WREG ? KS * KS : 1];
+  if constexpr (WREG) {
+#pragma unroll
+    for (int t = 0; t < KS * KS; ++t) {
+      wr0[t] = *(const float4*)(wl + t * C + cg * 8);
+      wr1[t] = *(const float4*)(wl + t * C + cg * 8 + 4);
+    }
+  }
 #pragma unroll
   for (int k = 0; k < NPASS; ++k) {
     const int pix = k * PPS + ps, ty = pix / S1_T, tx = pix % S1_T;
@@ -1836,7 +1846,9 @@ __global__ __launch_bounds__(256) void dgrad_ci1_kernel(int n, int h, int w, int
 #pragma unroll
       for (int kx = 0; kx < KS; ++kx) {  // out[q] += W[c][ky][kx] * dz[q - (ky, kx) + pad]  (FWD: x[q + (ky, kx) - pad])
         const float d = FWD ? dzt[(ty + ky) * TP + tx + kx] : dzt[(ty + KS - 1 - ky) * TP + tx + KS - 1 - kx];
-        const float4 w0 = *(const float4*)(wl + (ky * KS + kx) * C + cg * 8), w1 = *(const float4*)(wl + (ky * KS + kx) * C + cg * 8 + 4);
+        const int t = ky * KS + kx;
+        const float4 w0 = WREG ? wr0[WREG ? t : 0] : *(const float4*)(wl + t * C + cg * 8);
+        const float4 w1 = WREG ? wr1[WREG ? t : 0] : *(const float4*)(wl + t * C + cg * 8 + 4);
         v[0] += w0.x * d; v[1] += w0.y * d; v[2] += w0.z * d; v[3] += w0.w * d;
         v[4] += w1.x * d; v[5] += w1.y * d; v[6] += w1.z * d; v[7] += w1.w * d;
       }
