@@ -58,6 +58,9 @@ constexpr int TW = 16;            // output tile width (one MFMA N-fragment of p
 // is 16 (mod 32) bf16 elements, and 2-way conflicted at 8 (mod 32) (measured SQ_LDS_BANK_CONFLICT 43 % of
 // the LDS cycles of conv5 with the old +8 pads).
 static inline int xpitch(int cc) { return cc + ((16 - cc % 32) + 32) % 32; }  // >= cc, == 16 (mod 32)
+// Stride 2: a fragment's 16 pixels sit 2 pixels apart in the tile, so the lane pitch is 2 * ccp and ccp == 8 (mod 16)
+// keeps it at 16 (mod 32) (the stride-1 pitch left every stride-2 read 4-way conflicted: SQ_LDS_BANK_CONFLICT 35 %).
+static inline int xpitch_s2(int cc) { return cc + ((8 - cc % 16) + 16) % 16; }
 constexpr int WPAD = 16;          // k padding of the LDS weight tile rows (kcpad is a multiple of 32)
 constexpr int FWD_LDS_BUDGET = 80 * 1024;  // two workgroups per CU
 constexpr int FWD_MAXV = 8;             // 16 B staging vectors per thread held in registers (prefetch)
@@ -83,7 +86,7 @@ static void fwd_geom(int in_c, int ks, int stride, int out_c, int cc, int mw, Fw
   g->th = 4 * mw;
   g->tph = (g->th - 1) * stride + ks;
   g->tpw = (TW - 1) * stride + ks;
-  g->ccp = xpitch(cc);
+  g->ccp = stride == 2 ? xpitch_s2(cc) : xpitch(cc);
   g->kc = ks * ks * cc;
   g->kcpad = round_up(g->kc, 32);
   g->nchunk = ceil_div(in_c, cc);

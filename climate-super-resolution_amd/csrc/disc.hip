@@ -692,6 +692,72 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(const uint16_t* __restr
   }
 }
 
+// Wide-row form (o % 256 == 0): a wave owns 64 weight rows (4 A fragments), so each B fragment (the 32 x rows) read
+// per k-step feeds 4 MFMAs instead of one -- the x operand (re-read by every workgroup of a K slice) was 2/3 of the
+// load instructions of the form above.  Workgroup = 256 rows, grid = (o / 256) x nsplit.  Measured at fc.0 (n 32,
+// k 100352, o 1024): 65 us = 3.2 TB/s of weights with 3 workgroups per CU; 8 or 16 waves per workgroup splitting K
+// inside it (partials met in LDS) were slower (68-110 us), as were 1.5 or 6 workgroups per CU.
+template <int NF>
+__global__ __launch_bounds__(256) void linear_fwd_wide_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, int n,
+                                                              int k, int o, int ksplit, float* __restrict__ part) {
+  constexpr int NA = 4, LU = 4;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
+  const int o0 = blockIdx.x * 256 + wave * 64;
+  const int split = blockIdx.y;
+  const int kb = split * ksplit, ke = min(k, kb + ksplit);
+  f32x4 acc[NA][NF];
+#pragma unroll
+  for (int t = 0; t < NA; ++t)
+#pragma unroll
+    for (int f = 0; f < NF; ++f) acc[t][f] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const uint16_t* wrow = w + (long)(o0 + col) * k + g * 8;
+  int kk = kb;
+  for (; kk + 32 * LU <= ke; kk += 32 * LU) {
+    bf16x8 af[LU][NA], bfr[LU][NF];
+#pragma unroll
+    for (int u = 0; u < LU; ++u)
+#pragma unroll
+      for (int t = 0; t < NA; ++t) af[u][t] = *(const bf16x8*)(wrow + (long)t * 16 * k + kk + 32 * u);
+#pragma unroll
+    for (int u = 0; u < LU; ++u)
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        const int nn = f * 16 + col;
+        bfr[u][f] = nn < n ? *(const bf16x8*)(x + (long)nn * k + kk + 32 * u + g * 8) : (bf16x8){};
+      }
+#pragma unroll
+    for (int u = 0; u < LU; ++u)
+#pragma unroll
+      for (int t = 0; t < NA; ++t)
+#pragma unroll
+        for (int f = 0; f < NF; ++f) acc[t][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[u][t], bfr[u][f], acc[t][f], 0, 0, 0);
+  }
+  for (; kk < ke; kk += 32) {
+    bf16x8 af[NA], bfr[NF];
+#pragma unroll
+    for (int t = 0; t < NA; ++t) af[t] = *(const bf16x8*)(wrow + (long)t * 16 * k + kk);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const int nn = f * 16 + col;
+      bfr[f] = nn < n ? *(const bf16x8*)(x + (long)nn * k + kk + g * 8) : (bf16x8){};
+    }
+#pragma unroll
+    for (int t = 0; t < NA; ++t)
+#pragma unroll
+      for (int f = 0; f < NF; ++f) acc[t][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bfr[f], acc[t][f], 0, 0, 0);
+  }
+  float* dst = part + (long)split * n * o;
+#pragma unroll
+  for (int t = 0; t < NA; ++t)
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const int nn = f * 16 + col;
+      if (nn >= n) continue;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dst[(long)nn * o + o0 + t * 16 + g * 4 + i] = acc[t][f][i];
+    }
+}
+
 __global__ void linear_reduce_kernel(const float* __restrict__ part, int nsplit, int n, int o, const float* __restrict__ bias, int act,
                                      float slope, float* __restrict__ y, uint16_t* __restrict__ ybf) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -718,9 +784,12 @@ extern "C" int climsr_linear_fwd(const uint16_t* x, const uint16_t* w, const flo
     set_error("linear_fwd: bad args (n=%d k=%d o=%d; need n<=64, k%%32==0, o%%16==0)", n, k, o);
     return CLIMSR_EINVAL;
   }
-  const int oblk = ceil_div(o, 64);
-  int nsplit = ceil_div(1536, oblk);  // ~6 workgroups per CU, K slices of whole 256-element rounds where possible
-  int ksplit = round_up(ceil_div(k, nsplit), k >= 256 * nsplit ? 256 : 32);
+  const bool wide = o % 256 == 0;
+  const int oblk = wide ? o / 256 : ceil_div(o, 64);
+  // ~6 (narrow) / 3 (wide: 4x the rows per workgroup) workgroups per CU, K slices of whole rounds where possible
+  const int rnd = wide ? 128 : 256;
+  int nsplit = wide ? ceil_div(768, oblk) : ceil_div(1536, oblk);
+  int ksplit = round_up(ceil_div(k, nsplit), k >= rnd * nsplit ? rnd : 32);
   nsplit = ceil_div(k, ksplit);
   if ((int64_t)nsplit * n * o > ws_floats) {
     set_error("linear_fwd: workspace too small (%lld floats needed)", (long long)nsplit * n * o);
@@ -729,7 +798,11 @@ extern "C" int climsr_linear_fwd(const uint16_t* x, const uint16_t* w, const flo
   hipStream_t s = (hipStream_t)stream;
   const int nf = (n + 15) / 16;
   dim3 grid(oblk, nsplit);
-  if (nf == 1) hipLaunchKernelGGL(linear_fwd_kernel<1>, grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
+  if (wide) {
+    if (nf == 1) hipLaunchKernelGGL(linear_fwd_wide_kernel<1>, grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
+    else if (nf == 2) hipLaunchKernelGGL(linear_fwd_wide_kernel<2>, grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
+    else hipLaunchKernelGGL(linear_fwd_wide_kernel<4>, grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
+  } else if (nf == 1) hipLaunchKernelGGL(linear_fwd_kernel<1>, grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
   else if (nf == 2) hipLaunchKernelGGL(linear_fwd_kernel<2>, grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
   else hipLaunchKernelGGL(linear_fwd_kernel<4>, grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
   hipLaunchKernelGGL(linear_reduce_kernel, dim3(ceil_div((long)n * o, 256)), dim3(256), 0, s, workspace, nsplit, n, o, bias, act, slope,

@@ -119,7 +119,7 @@ class _DEngine:
         ops.adaptive_pool_fwd(a_prev, n, hh, ww, c, POOL, POOL, p, p_t, n_pad)
         fc0, fc2 = d.fc[0], d.fc[2]
         hid = _f32((n, fc0.out_features), dev)
-        nsplit_max = 1536 // ((fc0.out_features + 63) // 64) + 1
+        nsplit_max = 3072 // ((fc0.out_features + 63) // 64) + 1
         lin_ws = self._scr("linws", (nsplit_max * n * fc0.out_features,), torch.float32, dev)
         ops.linear_fwd(p, self.fc0_bf16, fc0.bias, n, feat, fc0.out_features, hid, lin_ws, act=ACT_LRELU, slope=0.2)
         s = _f32((n, 1), dev)

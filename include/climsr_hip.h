@@ -285,7 +285,7 @@ int climsr_adaptive_pool_fwd(const uint16_t* x, int n, int h, int w, int c, int 
 int climsr_adaptive_pool_bwd(const float* dp, int n, int h, int w, int c, int oh, int ow, float* dx, void* stream);
 
 /* nn.Linear forward on MFMA: y[n][o] = act(x[n][k] . w[o][k] + b[o]) (fp32 out); n <= 64, k % 32 == 0,
- * o % 16 == 0; split-K partials in workspace (ws_floats >= nsplit*n*o, nsplit <= 1536/ceil(o/64) + 1). */
+ * o % 16 == 0; split-K partials in workspace (ws_floats >= nsplit*n*o, nsplit <= 3072/ceil(o/64) + 1). */
 int climsr_linear_fwd(const uint16_t* x, const uint16_t* w, const float* bias, int n, int k, int o, int act, float slope,
                       float* workspace, int64_t ws_floats, float* y, void* stream);
 /* dx[n][k] (+)= dy[n][o] . w[o][k] (bf16 in, fp32 out); k % 64 == 0, o % 32 == 0. */

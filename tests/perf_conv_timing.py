@@ -1,0 +1,25 @@
+"""hipGraph-replay launch timing shared by the perf_* micro-benchmarks (GPU box only)."""
+import torch
+
+
+def timeit(fn, reps):
+    """Average GPU time per launch: `reps` launches captured in one hipGraph and replayed (no host overhead)."""
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(gr, stream=side):
+            for _ in range(reps):
+                fn()
+    torch.cuda.synchronize()
+    gr.replay()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    gr.replay()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps * 1e3  # us

@@ -444,3 +444,37 @@ def test_batchnorm_train_at_bench_shapes(c, h):
     dz64 = gamma.double() * rstd.double() * (d - d.mean(0) - xh * (d * xh).mean(0))
     err = float((dz2.double() - dz64).abs().max())
     assert err <= 2 ** -7 * float(dz64.abs().max()), f"bn backward (from z) dz err {err:.3e}"
+
+
+@pytest.mark.parametrize("n,k,o", [(32, 100352, 1024), (2, 8192, 96), (20, 4096, 256)])
+def test_linear_fwd_dgrad_wgrad_vs_float64(n, k, o):
+    """fc.0 of the RFB discriminator (rfb_esrgan.py:57: Linear(100352, 1024) + LeakyReLU, B=32) and the plain
+    discriminator's padded head: forward (wide / narrow split-K + reduce), data gradient and weight gradient (+=)
+    vs float64 matmuls of the same bf16 operands."""
+    from climsr_amd import ops
+
+    g = torch.Generator(device=DEV).manual_seed(n + o)
+    x = (torch.randn((n, k), generator=g, device=DEV) * 0.5).to(torch.bfloat16)
+    w = (torch.randn((o, k), generator=g, device=DEV) / k ** 0.5).to(torch.bfloat16)
+    b = torch.randn(o, generator=g, device=DEV) * 0.1
+    y = torch.empty((n, o), device=DEV)
+    ws = torch.empty((3072 // max(1, o // 64) + 2) * n * o, device=DEV)
+    ops.linear_fwd(x, w, b, n, k, o, y, ws, act=ops.ACT_LRELU, slope=0.2)
+    torch.cuda.synchronize()
+    want = F.leaky_relu(x.double() @ w.double().t() + b.double(), 0.2)
+    close(y, want, rel=1e-5, what="linear fwd")
+    dy = (torch.randn((n, o), generator=g, device=DEV)).to(torch.bfloat16)
+    dx = torch.full((n, k), 1.5, device=DEV)
+    ops.linear_dgrad(dy, w, n, k, o, dx, accumulate=True)
+    torch.cuda.synchronize()
+    close(dx - 1.5, dy.double() @ w.double(), rel=1e-5, what="linear dgrad (+=)")
+    n_pad = (n + 31) // 32 * 32
+    dy_t = torch.zeros((o, n_pad), dtype=torch.bfloat16, device=DEV)
+    dy_t[:, :n] = dy.t()
+    x_t = torch.zeros((k, n_pad), dtype=torch.bfloat16, device=DEV)
+    x_t[:, :n] = x.t()
+    if o % 64 == 0:
+        dw = torch.zeros((o, k), device=DEV)
+        ops.linear_wgrad(dy_t, x_t, n_pad, k, o, dw, accumulate=False)
+        torch.cuda.synchronize()
+        close(dw, dy.double().t() @ x.double(), rel=1e-5, what="linear wgrad")
