@@ -501,8 +501,16 @@ __device__ __forceinline__ void store_tile_lds(const FwdArgs& a, const float* eb
 // PF > 0: software-pipelined chunks.  Chunk j+1's input and weight vectors (at most PFX + PFW per thread) are
 // loaded into registers while chunk j is on the MFMA pipe, so a multi-chunk tile (RDB conv5 / pull-x: four
 // 32-channel chunks) pays one staging latency instead of one per chunk.
-template <int MW, int NT, bool RF, int MV, int PFX = 0, int PFW = 0, int EP = 0>
-__global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
+#ifndef CLIMSR_DIAG_MODE
+#define CLIMSR_DIAG_MODE 0  // diagnostic builds only: 1 = every chunk computed twice, 2 = one staging, compute only
+#endif
+// GEO (host-checked geometry specialisation, 0 = runtime geometry): 1 / 2 = 3x3 taps over 32-channel chunks at
+// stride 1 / 2 with 16x16 output tiles (MW 4): every tap / row / fragment LDS offset is a compile-time immediate,
+// so the unrolled k-steps read their fragments with no address arithmetic and no tap-table lookup (the runtime
+// form waited on a dependent ds_read of the table each k-step, and the compiler then issued the fragment reads
+// just before their MFMAs: the compute phase alone ran at ~55 % of the MFMA rate).
+template <int MW, int NT, bool RF, int MV, int PFX, int PFW, int EP, int GEO>
+__device__ __forceinline__ void conv_fwd_body(const FwdArgs& a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int* tab = (int*)smem;
   uint16_t* xs = (uint16_t*)(smem + a.lds_tab);
@@ -526,7 +534,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
   const int ks2 = a.ks * a.ks;
 
   // tap table: LDS element offset of k-group (8 channels) within a chunk
-  for (int i = tid; i < a.kcpad / 8; i += 256) {
+  for (int i = tid; i < (GEO > 0 ? 0 : a.kcpad / 8); i += 256) {
     int kr = i * 8;
     int tap = kr / a.cc;
     int c = kr - tap * a.cc;
@@ -570,6 +578,30 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
   // k-steps software-pipelined two deep: the fragments of k-step s+1 are read from LDS while the MFMAs of
   // k-step s run (one wave per SIMD pair cannot hide the ds_read latency otherwise)
   auto compute = [&]() {
+    if constexpr (GEO > 0) {
+      static_assert(MW == 4, "GEO tiles are 16 x 16");
+      constexpr int S = GEO, TPW = (TW - 1) * S + 3, CCP = S == 1 ? 48 : 40, WP = 9 * 32 + WPAD;
+      const uint16_t* xb = xs + ((wave * MW * TPW + col) * S) * CCP + g * 8;
+      const uint16_t* wb = ws + col * WP + g * 8;
+      bf16x8 af[2][NT], bf[2][MW];
+      auto ld = [&](int k, int b) {
+        const int off = ((k / 3) * TPW + (k % 3)) * CCP;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) af[b][t] = *(const bf16x8*)(wb + t * 16 * WP + k * 32);
+#pragma unroll
+        for (int m = 0; m < MW; ++m) bf[b][m] = *(const bf16x8*)(xb + m * S * TPW * CCP + off);
+      };
+      ld(0, 0);
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        if (k + 1 < 9) ld(k + 1, (k + 1) & 1);
+#pragma unroll
+        for (int m = 0; m < MW; ++m)
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k & 1][t], bf[k & 1][m], acc[m][t], 0, 0, 0);
+      }
+      return;
+    }
     const int nks = a.kcpad / 32;
     bf16x8 afA[NT], bfA[MW], afB[NT], bfB[MW];
     auto ld = [&](int ks, bf16x8(&af)[NT], bf16x8(&bf)[MW]) {
@@ -647,13 +679,23 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
       }
     };
     issue(0);
+#if CLIMSR_DIAG_MODE == 2
+    __syncthreads();
+    stash();
+    __syncthreads();
+    for (int j = 0; j < a.nchunk; ++j) compute();
+#else
     for (int j = 0; j < a.nchunk; ++j) {
       __syncthreads();  // chunk j-1's fragment reads are done
       stash();
       if (j + 1 < a.nchunk) issue(j + 1);  // lands while chunk j computes
       __syncthreads();
       compute();
+#if CLIMSR_DIAG_MODE == 1
+      compute();
+#endif
     }
+#endif
   } else {
   // batched staging: every thread issues up to MV input + MV weight 16 B global loads before the first
   // LDS store, so a chunk pays ~one memory latency instead of one per vector
@@ -798,6 +840,17 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(FwdArgs a) {
     for (int t = 0; t < NT; ++t) *(f32x4*)(eb + (m * 16 + col) * EPP + t * 16 + g * 4) = acc[m][t];
   __syncthreads();  // orders the staging writes before the transposed reads (they use another vector type)
   store_tile_lds<RF, MW * 16, NT * 16, 64, EP>(a, eb, EPP, lane, nimg, oy0 + wave * MW, ox0, co_blk0);
+}
+
+// two workgroups per CU (<= 80 KiB LDS each): at most 256 registers so that two waves share each SIMD
+template <int MW, int NT, bool RF, int MV, int PFX = 0, int PFW = 0, int EP = 0, int GEO = 0>
+__global__ __launch_bounds__(256, 2) void conv_fwd_kernel(FwdArgs a) {
+  conv_fwd_body<MW, NT, RF, MV, PFX, PFW, EP, GEO>(a);
+}
+// large stride-2 input tiles (one workgroup per CU): the deep prefetch may use the whole register file
+template <int MW, int NT, bool RF, int MV, int PFX = 0, int PFW = 0, int EP = 0, int GEO = 0>
+__global__ __launch_bounds__(256) void conv_fwd_wide_kernel(FwdArgs a) {
+  conv_fwd_body<MW, NT, RF, MV, PFX, PFW, EP, GEO>(a);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1957,29 +2010,49 @@ static int dispatch_pt(const ClimsrConvDesc* d, const FwdArgs& a, hipStream_t s)
   }
 }
 
-template <int MW, int NT, int PFX = 0, int PFW = 0, int EP = 0>
-static int launch_fwd_ep(const FwdArgs& a, int ncob, size_t lds, hipStream_t s) {
+template <int MW, int NT, int PFX, int PFW, int EP, int GEO>
+static int launch_fwd_geo(const FwdArgs& a, int ncob, size_t lds, hipStream_t s) {
   dim3 grid(a.tiles_x * a.tiles_y * a.n, ncob);
   const size_t lds_ep = (size_t)4 * MW * 16 * (NT * 16 + 4) * 4;  // epilogue staging (aliases the operands)
   if (lds_ep > lds) lds = lds_ep;
   constexpr int MV = NT == 1 ? 6 : (NT == 2 ? 8 : 4);
+  constexpr bool WIDE = PFX == 18;
   if (g_dry) {
-    if (PFX) snprintf(g_dry_name, sizeof(g_dry_name), "conv_fwd_kernel<%d, %d, %s, %d, %d, %d, %d>", MW, NT, a.res_f32 ? "true" : "false", MV, PFX, PFW, EP);
-    else if (EP) snprintf(g_dry_name, sizeof(g_dry_name), "conv_fwd_kernel<%d, %d, %s, %d, 0, 0, %d>", MW, NT, a.res_f32 ? "true" : "false", MV, EP);
-    else snprintf(g_dry_name, sizeof(g_dry_name), "conv_fwd_kernel<%d, %d, %s, %d>", MW, NT, a.res_f32 ? "true" : "false", MV);
+    snprintf(g_dry_name, sizeof(g_dry_name), "%s<%d, %d, %s, %d, %d, %d, %d, %d>", WIDE ? "conv_fwd_wide_kernel" : "conv_fwd_kernel", MW, NT,
+             a.res_f32 ? "true" : "false", MV, PFX, PFW, EP, GEO);
     return CLIMSR_OK;
   }
-  auto k = a.res_f32 ? conv_fwd_kernel<MW, NT, true, MV, PFX, PFW, EP> : conv_fwd_kernel<MW, NT, false, MV, PFX, PFW, EP>;
+  void (*kt)(FwdArgs);
+  void (*kf)(FwdArgs);
+  if constexpr (WIDE) {
+    kt = conv_fwd_wide_kernel<MW, NT, true, MV, PFX, PFW, EP, GEO>;
+    kf = conv_fwd_wide_kernel<MW, NT, false, MV, PFX, PFW, EP, GEO>;
+  } else {
+    kt = conv_fwd_kernel<MW, NT, true, MV, PFX, PFW, EP, GEO>;
+    kf = conv_fwd_kernel<MW, NT, false, MV, PFX, PFW, EP, GEO>;
+  }
+  auto k = a.res_f32 ? kt : kf;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)conv_fwd_kernel<MW, NT, true, MV, PFX, PFW, EP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    (void)hipFuncSetAttribute((const void*)conv_fwd_kernel<MW, NT, false, MV, PFX, PFW, EP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+    (void)hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)kf, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a);
   return check_launch("conv2d_fwd");
+}
+
+// the GEO specialisation matching a's geometry (conv_fwd_kernel): 16x16 tiles of 3x3 taps over 32-channel chunks
+template <int MW, int NT, int PFX = 0, int PFW = 0, int EP = 0>
+static int launch_fwd_ep(const FwdArgs& a, int ncob, size_t lds, hipStream_t s) {
+  const bool base = MW == 4 && a.cc == 32 && a.ks == 3 && a.kcpad == 9 * 32;
+  if constexpr (MW == 4 && PFX != 18) {
+    if (base && a.stride == 1 && a.tpw == TW + 2 && a.ccp == 48) return launch_fwd_geo<MW, NT, PFX, PFW, EP, 1>(a, ncob, lds, s);
+  }
+  if constexpr (MW == 4 && PFX == 18) {
+    if (base && a.stride == 2 && a.tpw == 2 * TW + 1 && a.ccp == 40) return launch_fwd_geo<MW, NT, PFX, PFW, EP, 2>(a, ncob, lds, s);
+  }
+  return launch_fwd_geo<MW, NT, PFX, PFW, EP, 0>(a, ncob, lds, s);
 }
 
 template <int MW, int NT, int PFX = 0, int PFW = 0>
