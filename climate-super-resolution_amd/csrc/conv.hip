@@ -2010,6 +2010,209 @@ static int dispatch_pt(const ClimsrConvDesc* d, const FwdArgs& a, hipStream_t s)
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Data gradient of a 3x3 / stride-2 / pad-1 conv (the discriminator's downsampling convs, rfb_esrgan.py:30-48),
+// phase-decomposed.  The zero-inserted form (a stride-1 conv over the 2x-upsampled dz, up = -2) spends 3 of every
+// 4 MFMAs on inserted zeros; here a dx pixel (2i+a, 2j+b) sums only its own taps: with the transposed, flipped
+// weights of wpk_t (tap (ky, kx) = forward tap (2-ky, 2-kx)), tap (ky, kx) feeds phase (ky != 1, kx != 1) from dz
+// pixel (i + (ky == 2), j + (kx == 2)).  Every tap is one k-step (32-channel chunks), 9 k-steps per chunk in all.
+// Workgroup: 16 x 16 dz positions (32 x 32 dx pixels) x 32 dx channels; wave w owns dz rows 4w..4w+3 and keeps
+// 4 phases x 4 rows x 2 channel blocks of accumulators.  The taps are walked grouped by dz offset, so a B fragment
+// (16 dz pixels x 32 channels) is read once per offset (4 per chunk, not 9).  dz tile 17 x 17 pixels (+ right /
+// bottom halo) and the weight chunk are staged in LDS, the next chunk prefetched into registers during the
+// MFMAs.  Epilogue per phase through LDS (fp32), 16 B bf16 stores, optional LeakyReLU/ReLU backward from the
+// bf16 activation res1 at the dx pixel (EP 4: the layer-1 data gradient writing layer 0's output gradient).
+// ------------------------------------------------------------------------------------------
+constexpr int S2D_TPW = 17, S2D_CCP = 48, S2D_WP = 9 * 32 + WPAD;
+template <int MW>
+constexpr int s2d_lds(int nt) { return (4 * MW + 1) * S2D_TPW * S2D_CCP * 2 + nt * 16 * S2D_WP * 2; }
+
+// MW dz rows per wave x NT 16-channel blocks (MW * NT = 8: 4 x 2 for >= 128 dx channels, 2 x 4 -- whole 128 B
+// pixel lines per workgroup -- for 64)
+template <int EP, int MW, int NT>
+__global__ __launch_bounds__(256, 2) void conv_dgrad_s2_kernel(FwdArgs a) {
+  constexpr int TPH = 4 * MW + 1, CO = NT * 16, EPP = CO + 4;
+  constexpr int NRX = (TPH * S2D_TPW * 4 + 255) / 256, NRW = (CO * 36 + 255) / 256;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* xs = (uint16_t*)smem;
+  uint16_t* ws = (uint16_t*)(smem + TPH * S2D_TPW * S2D_CCP * 2);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
+  // XCD-paired order: the channel blocks of one tile are 8 workgroups apart, i.e. on the same XCD (round-robin
+  // dispatch) at about the same time, so they share the dz tile in that L2 and complete each other's partial
+  // dx lines there (a block writes 64 of a pixel's 128 B at 64 channels)
+  const int ncob = a.out_c / CO, grp = blockIdx.x / (8 * ncob), r8 = blockIdx.x % (8 * ncob);
+  int bid = grp * 8 + (r8 & 7);
+  if (bid >= a.tiles_x * a.tiles_y * a.n) return;
+  const int tx = bid % a.tiles_x;
+  bid /= a.tiles_x;
+  const int ty = bid % a.tiles_y;
+  const int nimg = bid / a.tiles_y;
+  const int j0 = tx * 16, i0 = ty * 4 * MW, co0 = (r8 >> 3) * CO;
+
+  f32x4 acc[4][MW][NT];
+#pragma unroll
+  for (int p = 0; p < 4; ++p)
+#pragma unroll
+    for (int m = 0; m < MW; ++m)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[p][m][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  uint4 px[NRX], pw[NRW];
+  auto issue = [&](int j) {
+#pragma unroll
+    for (int r = 0; r < NRX; ++r) {
+      const int v = tid + 256 * r, pix = v >> 2, cg = v & 3;
+      const int yy = i0 + pix / S2D_TPW, xx = j0 + pix % S2D_TPW;
+      px[r] = make_uint4(0, 0, 0, 0);
+      if (pix < TPH * S2D_TPW && yy < a.in_h && xx < a.in_w)
+        px[r] = *(const uint4*)(a.x + (((long)nimg * a.in_h + yy) * a.in_w + xx) * a.in_cs + a.in_co + j * 32 + cg * 8);
+    }
+#pragma unroll
+    for (int r = 0; r < NRW; ++r) {
+      const int v = tid + 256 * r, row = v / 36, kv = v % 36;
+      pw[r] = make_uint4(0, 0, 0, 0);
+      if (row < CO) pw[r] = *(const uint4*)(a.w + (long)(co0 + row) * a.kpk + (long)j * 288 + kv * 8);
+    }
+  };
+  auto stash = [&]() {
+#pragma unroll
+    for (int r = 0; r < NRX; ++r) {
+      const int v = tid + 256 * r, pix = v >> 2, cg = v & 3;
+      if (pix < TPH * S2D_TPW) *(uint4*)(xs + pix * S2D_CCP + cg * 8) = px[r];
+    }
+#pragma unroll
+    for (int r = 0; r < NRW; ++r) {
+      const int v = tid + 256 * r, row = v / 36, kv = v % 36;
+      if (row < CO) *(uint4*)(ws + row * S2D_WP + kv * 8) = pw[r];
+    }
+  };
+  // taps grouped by dz offset (dy, dx): (0,0): ky,kx in {0,1}; (0,1): kx = 2; (1,0): ky = 2; (1,1): (2,2)
+  constexpr int TKY[9] = {0, 0, 1, 1, 0, 1, 2, 2, 2}, TKX[9] = {0, 1, 0, 1, 2, 2, 0, 1, 2};
+  const uint16_t* xb = xs + (wave * MW * S2D_TPW + col) * S2D_CCP + g * 8;
+  const uint16_t* wb = ws + col * S2D_WP + g * 8;
+  auto compute = [&]() {
+    bf16x8 af[2][NT], bf[2][MW];
+    auto lda = [&](int st, int b) {
+      const int tap = TKY[st] * 3 + TKX[st];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) af[b][t] = *(const bf16x8*)(wb + t * 16 * S2D_WP + tap * 32);
+    };
+    auto ldb = [&](int st, int b) {
+      const int off = ((TKY[st] == 2) * S2D_TPW + (TKX[st] == 2)) * S2D_CCP;
+#pragma unroll
+      for (int m = 0; m < MW; ++m) bf[b][m] = *(const bf16x8*)(xb + m * S2D_TPW * S2D_CCP + off);
+    };
+    lda(0, 0);
+    ldb(0, 0);
+    int bb = 0;
+#pragma unroll
+    for (int st = 0; st < 9; ++st) {
+      const bool newb = st + 1 < 9 && (st + 1 == 4 || st + 1 == 6 || st + 1 == 8);
+      if (st + 1 < 9) lda(st + 1, (st + 1) & 1);
+      if (newb) ldb(st + 1, bb ^ 1);
+      const int ph = (TKY[st] != 1) * 2 + (TKX[st] != 1);
+#pragma unroll
+      for (int m = 0; m < MW; ++m)
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          acc[ph][m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[st & 1][t], bf[bb][m], acc[ph][m][t], 0, 0, 0);
+      if (newb) bb ^= 1;
+    }
+  };
+  issue(0);
+  for (int j = 0; j < a.nchunk; ++j) {
+    __syncthreads();  // chunk j-1's fragment reads are done
+    stash();
+    if (j + 1 < a.nchunk) issue(j + 1);  // lands while chunk j computes
+    __syncthreads();
+    compute();
+  }
+
+  // epilogue, one phase at a time: fp32 [64 px][32 ch] per wave in LDS, then 8 channels (16 B bf16) per item
+  float* eb = (float*)smem + wave * (MW * 16 * EPP);
+  constexpr int NG = CO / 8;  // 16 B channel groups per pixel
+  const __amdgpu_buffer_rsrc_t rr1 = opt_rsrc(EP == 4 ? a.res1 : nullptr);
+  // item (phase ph, k): pixel it / NG of the wave's MW x 16 dz positions, channels (it % NG) * 8, it = lane + 64 k;
+  // the activation operand of all 4 phases is loaded up front (one HBM latency, not four)
+  auto item_pidx = [&](int ph, int k, bool& ok) -> long {
+    const int it = lane + 64 * k, pl = it / NG;
+    const int py = 2 * (i0 + wave * MW + (pl >> 4)) + (ph >> 1), pxx = 2 * (j0 + (pl & 15)) + (ph & 1);
+    ok = py < a.out_h && pxx < a.out_w;
+    return ok ? ((long)nimg * a.out_h + py) * a.out_w + pxx : 0;
+  };
+  uint4 r1[4][4];
+#pragma unroll
+  for (int ph = 0; ph < 4; ++ph)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      r1[ph][k] = make_uint4(0, 0, 0, 0);
+      if (EP == 4) {
+        bool ok;
+        const long pidx = item_pidx(ph, k, ok);
+        r1[ph][k] = buf_load16(rr1, (uint32_t)((pidx * a.r1_cs + (ok ? a.r1_co + co0 + ((lane + 64 * k) % NG) * 8 : 0)) * 2));
+      }
+    }
+#pragma unroll
+  for (int ph = 0; ph < 4; ++ph) {
+    __syncthreads();  // operands (first phase) / the previous phase's reads are done
+#pragma unroll
+    for (int m = 0; m < MW; ++m)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) *(f32x4*)(eb + (m * 16 + col) * EPP + t * 16 + g * 4) = acc[ph][m][t];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int it = lane + 64 * k, pl = it / NG, cg = it % NG;
+      bool ok;
+      const long oidx = item_pidx(ph, k, ok) * a.out_cs + a.out_co + co0 + cg * 8;
+      const float4 s0 = *(const float4*)(eb + pl * EPP + cg * 8), s1 = *(const float4*)(eb + pl * EPP + cg * 8 + 4);
+      float v[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+      if (EP == 4) {
+        Raw8 rr;
+        rr.lo = r1[ph][k];
+        rr.hi = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float r = raw8_at(rr, false, i);
+          v[i] = a.act == 3 ? (r > 0.f ? v[i] : v[i] * a.slope) : (r > 0.f ? v[i] : 0.f);
+        }
+      }
+      if (ok) *(uint4*)((uint16_t*)a.y + oidx) = pack8_bf16(v, 1.f);
+    }
+  }
+}
+
+static bool dgrad_s2_shape(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const float* bias) {
+  const bool act_ok = ep->act == 0 ? !ep->res1 : ((ep->act == 3 || ep->act == 4) && ep->res1 && !(ep->res_f32 & 1) &&
+                                                   ((ep->res1_cstride | ep->res1_coff) & 7) == 0);
+  return d->up == -2 && d->stride == 1 && d->ks == 3 && d->pad == 1 && d->cc == 32 && d->in_c % 32 == 0 && d->out_c % 32 == 0 &&
+         d->in_coff % 8 == 0 && d->in_cstride % 8 == 0 && ((d->out_cstride | d->out_coff) & 7) == 0 && d->out_h == 2 * d->in_h &&
+         d->out_w == 2 * d->in_w && ep->out_mode == 0 && !bias && !ep->res2 && !ep->aux && !ep->down2 && act_ok;
+}
+
+template <int MW, int NT>
+static int launch_dgrad_s2_t(const ClimsrConvDesc* d, FwdArgs a, hipStream_t s) {
+  a.tiles_x = ceil_div(d->in_w, 16);
+  a.tiles_y = ceil_div(d->in_h, 4 * MW);
+  const bool ep4 = a.act == 3 || a.act == 4;
+  if (g_dry) {
+    snprintf(g_dry_name, sizeof(g_dry_name), "conv_dgrad_s2_kernel<%d, %d, %d>", ep4 ? 4 : 0, MW, NT);
+    return CLIMSR_OK;
+  }
+  dim3 grid(ceil_div(a.tiles_x * a.tiles_y * a.n, 8) * 8 * (d->out_c / (NT * 16)));
+  const int lds = s2d_lds<MW>(NT);
+  if (ep4) hipLaunchKernelGGL((conv_dgrad_s2_kernel<4, MW, NT>), grid, dim3(256), lds, s, a);
+  else hipLaunchKernelGGL((conv_dgrad_s2_kernel<0, MW, NT>), grid, dim3(256), lds, s, a);
+  return check_launch("conv2d_fwd (dgrad s2)");
+}
+
+static int launch_dgrad_s2(const ClimsrConvDesc* d, const FwdArgs& a, hipStream_t s) {
+  // 64 dx channels: one workgroup per 128 B pixel line (layer 1 with LeakyReLU': 158 -> 150 us at B=32; for wider
+  // layers the 4 x 2 form is 2-8 % faster)
+  if (d->out_c == 64) return launch_dgrad_s2_t<2, 4>(d, a, s);
+  return launch_dgrad_s2_t<4, 2>(d, a, s);
+}
+
 template <int MW, int NT, int PFX, int PFW, int EP, int GEO>
 static int launch_fwd_geo(const FwdArgs& a, int ncob, size_t lds, hipStream_t s) {
   dim3 grid(a.tiles_x * a.tiles_y * a.n, ncob);
@@ -2165,6 +2368,8 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
       default: return launch_n16<4, 0>(a, s);
     }
   }
+  if (dgrad_s2_shape(d, ep, bias) && (long)d->n * d->out_h * d->out_w * ep->res1_cstride * 2 < (1L << 32) - 64)
+    return launch_dgrad_s2(d, a, s);
   if (pt_shape(d, ep) && (d->out_c == 16 || d->out_c == 32 || d->out_c == 64) &&
       (d->in_c == 32 || d->in_c == 64 || d->in_c == 128))
     return dispatch_pt(d, a, s);

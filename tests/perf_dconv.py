@@ -10,7 +10,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 import climsr_amd  # noqa: E402,F401
-from climsr_amd.ops import ACT_RELU, ConvPlan, Workspace  # noqa: E402
+from climsr_amd.ops import ACT_LRELU_BWD, ACT_RELU, ConvPlan, Workspace  # noqa: E402
 from tests.perf_conv_timing import timeit  # noqa: E402
 
 ap = argparse.ArgumentParser()
@@ -48,6 +48,10 @@ if args.only in ("", "d"):
         g = torch.empty(n, h, h, cin, device=dev, dtype=torch.bfloat16)
         td = timeit(lambda: p.dgrad(dz, cout, oh, oh, g, cin, 0, n), args.reps)
         tw = timeit(lambda: p.wgrad(x, cin, 0, h, h, dz, cout, n, ws, accumulate=False), args.reps)
+        if stride == 2 and cin == 64:  # layer 1: the data gradient also applies layer 0's LeakyReLU' (rfb_esrgan.py:29)
+            ta = timeit(lambda: p.dgrad(dz, cout, oh, oh, g, cin, 0, n, act=ACT_LRELU_BWD, res1=x, res1_cs=cin, res1_co=0),
+                        args.reps)
+            print(f"{p.name:14s} @{h:3d}  dgrad + LeakyReLU' {ta:7.1f} us {(dz.numel() + 2 * g.numel()) * 2 / ta / 1e6:5.2f} TB/s")
         tot["fwd"] += t
         tot["dgrad"] += td
         tot["wgrad"] += tw

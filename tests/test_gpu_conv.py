@@ -408,3 +408,36 @@ def test_conv_single_input_channel_forward(cout, ks, act, h, w):
     got = from_nhwc(y, cout).cpu().double()
     err = (got - want).abs().max().item()
     assert err <= 2 ** -8 * want.abs().max().item() + 1e-6, f"single-input fwd: max err {err:.3e}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,h,w,act", [(64, 64, 32, 48, 0), (64, 128, 34, 20, 3), (96, 64, 16, 16, 4), (40, 64, 18, 22, 3),
+                                              (128, 128, 64, 64, 0)])
+def test_conv_dgrad_stride2_bf16(cin, cout, h, w, act):
+    """Data gradient of the discriminator's 3x3 stride-2 convs (rfb_esrgan.py:30-48) as the D backward runs it: bf16
+    output, optionally with the previous LeakyReLU/ReLU derivative from its bf16 activation (conv_dgrad_s2_kernel when
+    the channels are multiples of 32 -- ragged 17-row / 10-column dz tiles included -- else the zero-inserted generic
+    conv) vs autograd of F.conv2d in float64 on the same bf16 weights.  Tolerance: bf16 rounding of the result."""
+    from climsr_amd.ops import ACT_LRELU_BWD, ACT_NONE, ACT_RELU_BWD
+
+    n = 2
+    p, wt, _b = make_plan(cin, cout, 3, stride=2, bias=False)
+    oh, ow = (h + 1) // 2, (w + 1) // 2
+    g = torch.Generator().manual_seed(11)
+    dz = bf(torch.rand((n, cout, oh, ow), generator=g) * 2 - 1)
+    a = bf(torch.rand((n, cin, h, w), generator=g) * 2 - 1)
+    out = torch.zeros((n, h, w, p.cin), dtype=torch.bfloat16, device=DEV)
+    act_code = {0: ACT_NONE, 3: ACT_LRELU_BWD, 4: ACT_RELU_BWD}[act]
+    p.dgrad(to_nhwc(dz), p.cin_t, oh, ow, out, p.cin, 0, n, act=act_code, res1=to_nhwc(a) if act else None, res1_cs=p.cin,
+            res1_co=0)
+    torch.cuda.synchronize()
+    x = torch.zeros((n, cin, h, w), dtype=torch.float64, requires_grad=True)
+    y = F.conv2d(x, bf(wt).double(), None, stride=2, padding=1)
+    (gref,) = torch.autograd.grad(y, x, dz.double())
+    if act == 3:
+        gref = torch.where(a.double() > 0, gref, gref * 0.2)
+    elif act == 4:
+        gref = torch.where(a.double() > 0, gref, torch.zeros_like(gref))
+    got = from_nhwc(out, cin).cpu().double()
+    err = (got - gref).abs().max().item()
+    assert err <= 8e-3 * gref.abs().max().item() + 1e-6, f"stride-2 dgrad max err {err} (scale {gref.abs().max().item()})"
