@@ -1368,7 +1368,9 @@ static bool pw_fits(int in_c, int ks, int out_c) {
   return pw_geom(&d, nt, 2, &g, 4);
 }
 
-template <int NW, int MW, int NT, bool RF, int PV, int EP = 0>
+// GEO = 1: 3x3 taps over one 64-channel chunk with 8 waves x 2 rows (the 64 -> 64 HR-resolution / VGG conv1_2
+// shapes): the 18 k-steps unrolled with compile-time LDS offsets (no tap table; see conv_fwd_kernel's GEO)
+template <int NW, int MW, int NT, bool RF, int PV, int EP = 0, int GEO = 0>
 __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
   constexpr int NTHR = 64 * NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1380,7 +1382,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
   const int wpitch = a.kcpad + WPAD;
   const int ks2 = a.ks * a.ks;
-  for (int i = tid; i < a.kcpad / 8; i += NTHR) {  // tap table (one chunk)
+  for (int i = tid; i < (GEO ? 0 : a.kcpad / 8); i += NTHR) {  // tap table (one chunk)
     const int kr = i * 8;
     int tap = kr / a.cc, c = kr - tap * a.cc;
     if (tap >= ks2) { tap = 0; c = 0; }
@@ -1486,6 +1488,29 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
     {
       // k-steps two deep: k-step s+1's tap offset and fragments are read while s is on the MFMA pipe (one k-step at
       // a time serialised tab read -> B read -> MFMAs, 3 lgkmcnt waits per 8 MFMAs)
+      if constexpr (GEO == 1) {
+        static_assert(NW * MW == 16, "GEO 1: 16-row tiles");
+        constexpr int TPW = TW + 2, CCP = 80, WP = 9 * 64 + WPAD;
+        const uint16_t* xb = xs + ((wave * MW) * TPW + col) * CCP + g * 8;
+        const uint16_t* wb = ws + col * WP + g * 8;
+        bf16x8 af[2][NT], bf[2][MW];
+        auto ldk = [&](int k, int b) {  // k-step k: tap k / 2, channels (k & 1) * 32 + 8 g
+          const int tap = k >> 1, off = ((tap / 3) * TPW + tap % 3) * CCP + (k & 1) * 32;
+#pragma unroll
+          for (int t = 0; t < NT; ++t) af[b][t] = *(const bf16x8*)(wb + t * 16 * WP + k * 32);
+#pragma unroll
+          for (int m = 0; m < MW; ++m) bf[b][m] = *(const bf16x8*)(xb + m * TPW * CCP + off);
+        };
+        ldk(0, 0);
+#pragma unroll
+        for (int k = 0; k < 18; ++k) {
+          if (k + 1 < 18) ldk(k + 1, (k + 1) & 1);
+#pragma unroll
+          for (int m = 0; m < MW; ++m)
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k & 1][t], bf[k & 1][m], acc[m][t], 0, 0, 0);
+        }
+      } else {
       const int nks = a.kcpad / 32;
       bf16x8 afA[NT], bfA[MW], afB[NT], bfB[MW];
       auto ld = [&](int ks, bf16x8 (&af)[NT], bf16x8 (&bf)[MW]) {
@@ -1510,6 +1535,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
         mm(afB, bfB);
       }
       if (ks < nks) mm(afA, bfA);
+      }
     }
     const int ox = ox0 + col;
     if constexpr (EP == 5) {  // 2x2 sum + activation backward (act' of the bf16 low-res activation res1), bf16 out,
@@ -1596,10 +1622,11 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
   }
 }
 
-template <int NW, int MW, int NT, int PV, int EP = 0>
-static int launch_pw(const FwdArgs& a0, const PwGeom& g, hipStream_t s) {
+template <int NW, int MW, int NT, int PV, int EP, int GEO>
+static int launch_pw_geo(const FwdArgs& a0, const PwGeom& g, hipStream_t s) {
   if (g_dry) {
-    snprintf(g_dry_name, sizeof(g_dry_name), "conv_pw_kernel<%d, %d, %d, %s, %d, %d>", NW, MW, NT, a0.res_f32 ? "true" : "false", PV, EP);
+    snprintf(g_dry_name, sizeof(g_dry_name), "conv_pw_kernel<%d, %d, %d, %s, %d, %d, %d>", NW, MW, NT, a0.res_f32 ? "true" : "false", PV, EP,
+             GEO);
     return CLIMSR_OK;
   }
   FwdArgs a = a0;
@@ -1608,12 +1635,12 @@ static int launch_pw(const FwdArgs& a0, const PwGeom& g, hipStream_t s) {
   a.tiles_y = ceil_div(a.out_h, NW * MW);
   a.lds_tab = (int)g.lds_tab;
   a.lds_x = (int)g.lds_w;  // offset of the input tile = tab + weights
-  auto k = a.res_f32 ? conv_pw_kernel<NW, MW, NT, true, PV, EP> : conv_pw_kernel<NW, MW, NT, false, PV, EP>;
+  auto k = a.res_f32 ? conv_pw_kernel<NW, MW, NT, true, PV, EP, GEO> : conv_pw_kernel<NW, MW, NT, false, PV, EP, GEO>;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)conv_pw_kernel<NW, MW, NT, true, PV, EP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)conv_pw_kernel<NW, MW, NT, true, PV, EP, GEO>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
-    (void)hipFuncSetAttribute((const void*)conv_pw_kernel<NW, MW, NT, false, PV, EP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)conv_pw_kernel<NW, MW, NT, false, PV, EP, GEO>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     attr_set = true;
   }
@@ -1628,6 +1655,15 @@ static int launch_pw(const FwdArgs& a0, const PwGeom& g, hipStream_t s) {
   const int grid = ntiles < ncu ? ntiles : ncu;
   hipLaunchKernelGGL(k, dim3(grid), dim3(64 * NW), g.lds_total, s, a);
   return check_launch("conv2d_fwd (pw)");
+}
+
+template <int NW, int MW, int NT, int PV, int EP = 0>
+static int launch_pw(const FwdArgs& a, const PwGeom& g, hipStream_t s) {
+  if constexpr (NW * MW == 16) {
+    if (a.ks == 3 && a.cc == 64 && g.kcpad == 9 * 64 && g.ccp == 80 && g.tpw == TW + 2 && g.tph == 18)
+      return launch_pw_geo<NW, MW, NT, PV, EP, 1>(a, g, s);
+  }
+  return launch_pw_geo<NW, MW, NT, PV, EP, 0>(a, g, s);
 }
 
 // ------------------------------------------------------------------------------------------
