@@ -9,6 +9,7 @@
 // (MFMA B = input pixels staged in LDS, im2col done by LDS addressing), K = taps x channels.
 // MFMA: v_mfma_f32_16x16x32_bf16.  Lane l: A[row l&15][k 8(l>>4)+j], B[k 8(l>>4)+j][col l&15],
 // C[row 4(l>>4)+i][col l&15].
+#include <algorithm>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -2759,14 +2760,21 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgArgs a) {
 // registers while the current one is on the MFMA pipe.  Partials: [split][co_rows][in_c*9] (as above).
 // Stride 2 (the discriminator's features.2/8/14/20): 4 x 16 output tiles whose (2*4+1) x (2*16+1) input
 // footprint is staged whole; tap (r, s) of output pixel k reads tile pixel (2*row(k) + r, 2*col(k) + s).
-constexpr int W64_P = 64 + 8;  // LDS pixel pitch (channels) of both tiles
+// LDS pixel pitches (channels).  A transposed fragment read (ds_read_b64_tr_b16) is served 32 lanes at a time:
+// with the k-step's pixel rows taken as 4g + q (+16), those 32 lanes read 8 consecutive tile pixels, 32 B each,
+// which land in 8 disjoint 8-bank groups when one pixel step is 8 x odd banks: pitch 80 (dz tile; x tile at
+// stride 1) or 72 (x tile at stride 2, where a pixel step is two tile pixels).  The old 72 / rows 8g + q left
+// SQ_LDS_BANK_CONFLICT at 42 % of the LDS cycles.
+constexpr int W64_P = 64 + 8;  // (dzp of the generic wgrad path's descriptor)
+constexpr int W64_ZP = 80;
 template <int S>
 struct W64 {
   static constexpr int TH = S == 1 ? 8 : 4;                    // output tile rows (x TW = 16 columns)
   static constexpr int TPH = S * (TH - 1) + 3, TPW = S * (TW - 1) + 3;  // staged input footprint
+  static constexpr int XP = S == 1 ? 80 : 72;                 // x tile pixel pitch
   static constexpr int NZ = TH * TW * 8;                      // 16 B vectors of a dz tile (TH*16 px x 64 ch)
   static constexpr int NX = TPH * TPW * 8;                    // of an x tile
-  static constexpr size_t LDS = (size_t)(TH * TW + TPH * TPW) * W64_P * 2;
+  static constexpr size_t LDS = (size_t)TH * TW * W64_ZP * 2 + (size_t)TPH * TPW * XP * 2;
 };
 
 // TS = 2: 8 waves, wave w owns ci block w & 3 and taps [0,5) or [5,9) (w >> 2): 20 accumulators instead of 36, so
@@ -2774,10 +2782,8 @@ struct W64 {
 template <int TS, int S = 1>
 __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
   constexpr int NTHR = 256 * TS, NU = TS == 1 ? 9 : 5;
-  constexpr int TH = W64<S>::TH, TPW = W64<S>::TPW, NZ = W64<S>::NZ, NX = W64<S>::NX;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint16_t* zs = (uint16_t*)smem;                       // [TH*16 px][W64_P]
-  uint16_t* xs = zs + TH * TW * W64_P;                  // [TPH*TPW px][W64_P]
+  constexpr int TH = W64<S>::TH, TPW = W64<S>::TPW, NZ = W64<S>::NZ, NX = W64<S>::NX, XP = W64<S>::XP;
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // TS 1: two buffers of W64<S>::LDS
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
   const int wave = (tid >> 6) & 3, tg = TS == 1 ? 0 : tid >> 8;  // ci block, tap group
   const int u0 = tg * 5;
@@ -2803,10 +2809,10 @@ __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
     if constexpr (TS == 1) {
-      tapoff[u] = ((u / 3) * TPW + (u % 3)) * W64_P + wave * 16 + 4 * p;
+      tapoff[u] = ((u / 3) * TPW + (u % 3)) * XP + wave * 16 + 4 * p;
     } else {
       const int tp = u0 + u < 9 ? u0 + u : 8;
-      tapoff[u] = ((tp / 3) * TPW + (tp % 3)) * W64_P + wave * 16 + 4 * p;
+      tapoff[u] = ((tp / 3) * TPW + (tp % 3)) * XP + wave * 16 + 4 * p;
     }
   }
 
@@ -2846,84 +2852,121 @@ __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
                                 cg * 8);
     }
   };
-  int tile = split;
-  if (tile < a.ntiles) issue();
-  for (; tile < a.ntiles; tile += a.nsplit) {
-    __syncthreads();  // previous tile's fragment reads done
+  // buffer b of the staged tiles: dz [TH*16 px][W64_ZP], x [TPH*TPW px][XP]
+  auto zbuf = [&](int b) { return (uint16_t*)(smem + b * W64<S>::LDS); };
+  auto xbuf = [&](int b) { return (uint16_t*)(smem + b * W64<S>::LDS) + TH * TW * W64_ZP; };
+  auto stash = [&](int b) {
+    uint16_t* zs = zbuf(b);
+    uint16_t* xs = xbuf(b);
 #pragma unroll
     for (int i = 0; i < VZ; ++i) {
       const int v = tid + NTHR * i;
-      *(uint4*)(zs + (v >> 3) * W64_P + (v & 7) * 8) = pz[i];
+      *(uint4*)(zs + (v >> 3) * W64_ZP + (v & 7) * 8) = pz[i];
     }
 #pragma unroll
     for (int i = 0; i < VX; ++i) {
       const int v = tid + NTHR * i;
-      if (v < NX) *(uint4*)(xs + (v >> 3) * W64_P + (v & 7) * 8) = px[i];
+      if (v < NX) *(uint4*)(xs + (v >> 3) * XP + (v & 7) * 8) = px[i];
     }
-    if (tile + a.nsplit < a.ntiles) issue();
+  };
+  // k-step kk = 32 output pixels of the tile; lane group g's 8 k values = pixel rows 4g + q and 16 + 4g + q (a
+  // permutation of the k-step's pixels, the same for both operands)
+  const bool last_short = TS == 2 && tg == 1;  // tap group 1 has 4 taps (5..8)
+  auto frags = [&](int b, int kk, bf16x8 (&af)[4], bf16x8 (&bf)[NU]) {
+    const uint16_t* zs = zbuf(b);
+    const uint16_t* xs = xbuf(b);
+    const int k0 = kk * 32 + 4 * g + q, k1 = k0 + 16;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      af[t] = cat_tr(ds_read_tr16(zs + k0 * W64_ZP + t * 16 + 4 * p), ds_read_tr16(zs + k1 * W64_ZP + t * 16 + 4 * p));
+    const int xb0 = (S * (k0 >> 4) * TPW + S * (k0 & 15)) * XP, xb1 = (S * (k1 >> 4) * TPW + S * (k1 & 15)) * XP;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) bf[u] = cat_tr(ds_read_tr16(xs + xb0 + tapoff[u]), ds_read_tr16(xs + xb1 + tapoff[u]));
+  };
+  auto mma = [&](const bf16x8 (&af)[4], const bf16x8 (&bf)[NU]) {
+    if (do_bias && wave == 0 && tg == 0) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) accb[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], ones, accb[t], 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      if (u == NU - 1 && last_short) continue;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bf[u], acc[t][u], 0, 0, 0);
+    }
+  };
+  constexpr int NK = TH * TW / 32;  // 4 (stride 1) or 2 (stride 2): even
+  int tile = split;
+  if (tile < a.ntiles) issue();
+  if constexpr (TS == 1) {
+    // double-buffered LDS, one barrier per tile: tile t+1 (in registers since tile t-1) is written to the other
+    // buffer after the first k-step pair of tile t is on the MFMA pipe, then tile t+2 is requested -- the stash
+    // no longer runs between two barriers with the MFMAs idle (one workgroup per CU: nothing else hid it)
+    if (tile < a.ntiles) {
+      stash(0);
+      if (tile + a.nsplit < a.ntiles) issue();
+    }
     __syncthreads();
-    // k-step kk = output pixel rows 2kk, 2kk+1 of the tile; the fragments of k-step kk+1 are read from LDS while the
-    // MFMAs of kk run (one wave per SIMD cannot otherwise hide the read latency: ~14 waits per 36 MFMAs)
-    const bool last_short = TS == 2 && tg == 1;  // tap group 1 has 4 taps (5..8)
-    auto frags = [&](int kk, bf16x8 (&af)[4], bf16x8 (&bf)[NU]) {
-      const int k0 = kk * 32 + 8 * g + q, k1 = k0 + 4;
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-        af[t] = cat_tr(ds_read_tr16(zs + k0 * W64_P + t * 16 + 4 * p), ds_read_tr16(zs + k1 * W64_P + t * 16 + 4 * p));
-      const int xb0 = (S * (k0 >> 4) * TPW + S * (k0 & 15)) * W64_P, xb1 = (S * (k1 >> 4) * TPW + S * (k1 & 15)) * W64_P;
-#pragma unroll
-      for (int u = 0; u < NU; ++u) bf[u] = cat_tr(ds_read_tr16(xs + xb0 + tapoff[u]), ds_read_tr16(xs + xb1 + tapoff[u]));
-    };
-    auto mma = [&](const bf16x8 (&af)[4], const bf16x8 (&bf)[NU]) {
-      if (do_bias && wave == 0 && tg == 0) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) accb[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], ones, accb[t], 0, 0, 0);
-      }
-#pragma unroll
-      for (int u = 0; u < NU; ++u) {
-        if (u == NU - 1 && last_short) continue;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bf[u], acc[t][u], 0, 0, 0);
-      }
-    };
-    constexpr int NK = TH * TW / 32;  // 4 (stride 1) or 2 (stride 2): even
-    if constexpr (TS == 1) {
+    int cur = 0;
+    for (; tile < a.ntiles; tile += a.nsplit) {
+      const bool more = tile + a.nsplit < a.ntiles;
       bf16x8 afA[4], bfA[NU], afB[4], bfB[NU];
-      frags(0, afA, bfA);
-#pragma unroll 1
+      frags(cur, 0, afA, bfA);
+#pragma unroll
       for (int kk = 0; kk < NK; kk += 2) {
-        frags(kk + 1, afB, bfB);
+        frags(cur, kk + 1, afB, bfB);
         mma(afA, bfA);
-        if (kk + 2 < NK) frags(kk + 2, afA, bfA);
+        if (kk == 0 && more) {
+          stash(cur ^ 1);
+          if (tile + 2 * a.nsplit < a.ntiles) issue();
+        }
+        if (kk + 2 < NK) frags(cur, kk + 2, afA, bfA);
         mma(afB, bfB);
       }
-    } else {  // two waves per SIMD (256 VGPRs each): one fragment set, the partner wave hides the latency
+      __syncthreads();  // this tile's reads of buffer cur and the stash of buffer cur ^ 1 are done
+      cur ^= 1;
+    }
+  } else {
+    for (; tile < a.ntiles; tile += a.nsplit) {
+      __syncthreads();  // previous tile's fragment reads done
+      stash(0);
+      if (tile + a.nsplit < a.ntiles) issue();
+      __syncthreads();
+      // two waves per SIMD (256 VGPRs each): one fragment set, the partner wave hides the latency
 #pragma unroll 2
       for (int kk = 0; kk < NK; ++kk) {
         bf16x8 af[4], bf[NU];
-        frags(kk, af, bf);
+        frags(0, kk, af, bf);
         mma(af, bf);
       }
     }
   }
-  // C[row = co][col = ci]: lane holds co = co0 + 16t + 4g + i, ci = ci0 + 16 wave + col
-  float* slab = a.part + (long)split * a.co_rows * a.kw;
-  const int ci = ci0 + wave * 16 + col;
+  // C[row = co][col = ci]: lane holds co = co0 + 16t + 4g + i, ci = ci0 + 16 wave + col.  The workgroup's slab block
+  // (64 co rows x 576 contiguous floats each) is assembled in LDS and written with coalesced 16 B stores (the direct
+  // form issued 144 scattered 4 B stores per lane, 36 B apart)
+  constexpr int EPW = 9 * 64 + 4;  // staged row pitch (floats)
+  float* st = (float*)smem;
+  __syncthreads();  // every wave's fragment reads are done (the staging aliases the tiles)
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
+  for (int t = 0; t < 4; ++t)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int co = co0 + t * 16 + g * 4 + i;
-      float* row = slab + (long)co * a.kw + ci * 9;
+      float* row = st + (t * 16 + g * 4 + i) * EPW + (wave * 16 + col) * 9;
 #pragma unroll
       for (int u = 0; u < NU; ++u) {
         if constexpr (TS == 1) row[u] = acc[t][u][i];
         else if (u0 + u < 9) row[u0 + u] = acc[t][u][i];
       }
-      if (do_bias && wave == 0 && tg == 0 && col == 0) a.bpart[(long)split * a.co_rows + co] = accb[t][i];
+      if (do_bias && wave == 0 && tg == 0 && col == 0) a.bpart[(long)split * a.co_rows + co0 + t * 16 + g * 4 + i] = accb[t][i];
     }
+  __syncthreads();
+  float* slab = a.part + (long)split * a.co_rows * a.kw + (long)co0 * a.kw + ci0 * 9;
+  for (int f = tid; f < 64 * 144; f += NTHR) {
+    const int row = f / 144, c4 = f - row * 144;
+    *(float4*)(slab + (long)row * a.kw + c4 * 4) = *(const float4*)(st + row * EPW + c4 * 4);
   }
 }
+constexpr size_t W64_EP_LDS = (size_t)64 * (9 * 64 + 4) * 4;  // the slab staging of conv_wgrad64_kernel
 
 // ------------------------------------------------------------------------------------------
 // Weight gradient of a 1x1 conv with 64 inputs and <= 64 outputs (srcnn.conv2): dW[co][ci] = sum_p dz[p][co]
@@ -3333,15 +3376,15 @@ extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, c
     if (d->stride == 2) {
       a.tph = W64<2>::TPH; a.tpw = W64<2>::TPW;
       if (dry_run("conv_wgrad64_kernel<1, 2>")) return CLIMSR_OK;
-      hipLaunchKernelGGL((conv_wgrad64_kernel<1, 2>), grid, dim3(256), W64<2>::LDS, (hipStream_t)stream, a);
+      hipLaunchKernelGGL((conv_wgrad64_kernel<1, 2>), grid, dim3(256), std::max(2 * W64<2>::LDS, W64_EP_LDS), (hipStream_t)stream, a);
     } else if (ts2) {
       a.tph = W64<1>::TPH; a.tpw = W64<1>::TPW;
       if (dry_run("conv_wgrad64_kernel<2, 1>")) return CLIMSR_OK;
-      hipLaunchKernelGGL((conv_wgrad64_kernel<2, 1>), grid, dim3(512), W64<1>::LDS, (hipStream_t)stream, a);
+      hipLaunchKernelGGL((conv_wgrad64_kernel<2, 1>), grid, dim3(512), std::max(W64<1>::LDS, W64_EP_LDS), (hipStream_t)stream, a);
     } else {
       a.tph = W64<1>::TPH; a.tpw = W64<1>::TPW;
       if (dry_run("conv_wgrad64_kernel<1, 1>")) return CLIMSR_OK;
-      hipLaunchKernelGGL((conv_wgrad64_kernel<1, 1>), grid, dim3(256), W64<1>::LDS, (hipStream_t)stream, a);
+      hipLaunchKernelGGL((conv_wgrad64_kernel<1, 1>), grid, dim3(256), std::max(2 * W64<1>::LDS, W64_EP_LDS), (hipStream_t)stream, a);
     }
     return check_launch("conv2d_wgrad (64x64 block)");
   }
