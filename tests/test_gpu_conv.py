@@ -441,3 +441,23 @@ def test_conv_dgrad_stride2_bf16(cin, cout, h, w, act):
     got = from_nhwc(out, cin).cpu().double()
     err = (got - gref).abs().max().item()
     assert err <= 8e-3 * gref.abs().max().item() + 1e-6, f"stride-2 dgrad max err {err} (scale {gref.abs().max().item()})"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,h,w", [(64, 64, 64, 48), (64, 128, 34, 20), (128, 64, 16, 16), (96, 64, 40, 66)])
+def test_conv_fwd_stride2_plain_bf16(cin, cout, h, w):
+    """The discriminator's stride-2 convs as its forward runs them (rfb_esrgan.py:30-48): no bias, no activation,
+    bf16 out for the BatchNorm (conv_fwd_s2_kernel: 8 waves over two tap groups; ragged 17-row / 10- and 33-column
+    output tiles included) vs F.conv2d in float64 on the same bf16 operands.  Tolerance: bf16 rounding."""
+    n = 2
+    p, wt, _b = make_plan(cin, cout, 3, stride=2, bias=False)
+    g = torch.Generator().manual_seed(12)
+    x = bf(torch.rand((n, cin, h, w), generator=g) * 2 - 1)
+    oh, ow = (h + 1) // 2, (w + 1) // 2
+    y = torch.zeros((n, oh, ow, cout), dtype=torch.bfloat16, device=DEV)
+    p.fwd(to_nhwc(x), p.cin, 0, h, w, y, cout, 0, n, use_bias=False)
+    torch.cuda.synchronize()
+    want = F.conv2d(x.double(), bf(wt).double(), None, stride=2, padding=1)
+    got = from_nhwc(y, cout).cpu().double()
+    err = (got - want).abs().max().item()
+    assert err <= 8e-3 * want.abs().max().item() + 1e-6, f"stride-2 fwd max err {err}"
