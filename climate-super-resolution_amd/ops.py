@@ -188,7 +188,8 @@ class ConvPlan:
         mode = OUT_BF16 if g.dtype == torch.bfloat16 else (OUT_F32_ADD if accumulate else OUT_F32)
         ep = Epilogue(act, 0.2 if act == ACT_LRELU_BWD else 0.0, 1.0, ptr(res1), res1_cs, res1_co, 1.0, None, 0, 0, mode,
                       1 if down2 else 0, 0, 1.0, 1.0, aux_cs, ptr(aux), aux_co, aux_scale)
-        flops = 2 * self.cout * ct * self.ks * self.ks * n * out_h * out_w
+        # algorithmic: the forward's FLOPs (stride 2: the zero-inserted taps are not work)
+        flops = 2 * self.cout * ct * self.ks * self.ks * n * out_h * out_w // (self.stride * self.stride)
         gpx = n * out_h * out_w // (4 if down2 else 1)  # result pixels (after the 2x2 sum)
         nbytes = (n * d.in_h * d.in_w * self.cout * 2 + self.rows_t * self.kpk_t * 2 +
                   gpx * ct * (g.element_size() * (2 if mode == OUT_F32_ADD else 1) + _esize(res1) + _esize(aux)))
