@@ -114,6 +114,9 @@ static bool n16_shape(int in_c, int ks, int out_c) { return out_c <= 16 && ks ==
 static bool pw_fits(int in_c, int ks, int out_c);
 
 extern "C" int climsr_conv_chunk_ex(int in_c, int ks, int out_c, int stride) {
+  // <= 4 real input channels (conv_first, srcnn.conv1, VGG conv1_1, RCAN head): taps packed 4 channels apart
+  // (conv_pw GEO 2) -- K = ks^2 * 4 instead of ks^2 * 8 (9x9: 11 k-steps instead of 21)
+  if (in_c == 4 && stride == 1 && out_c == 64 && (ks == 3 || ks == 9)) return 4;
   if (stride == 1 && n16_shape(in_c, ks, out_c))  // conv_n16: one chunk, padded to 32/64/128
     return in_c <= 32 ? 32 : (in_c <= 64 ? 64 : 128);
   if (stride == 1 && pw_fits(in_c, ks, out_c)) return round_up(in_c, 8);  // conv_pw: the whole K in one chunk
@@ -169,7 +172,7 @@ __global__ void pack_kernel(const float* __restrict__ w, int rows, int kpk, int 
 
 extern "C" int climsr_pack_conv_weight(const float* w, int out_c, int in_c, int in_c_real, int out_c_real, int ks, int cc,
                                        int transpose_flip, uint16_t* wpk, void* stream) {
-  if (!w || !wpk || in_c % 8 || cc % 8 || cc <= 0 || ks <= 0) {
+  if (!w || !wpk || (in_c % 8 && !(in_c == 4 && cc == 4)) || (cc % 8 && cc != 4) || cc <= 0 || ks <= 0) {
     set_error("pack_conv_weight: bad args (in_c=%d cc=%d ks=%d)", in_c, cc, ks);
     return CLIMSR_EINVAL;
   }
@@ -203,13 +206,12 @@ __global__ void pack_batched_kernel(const ClimsrPackDesc* __restrict__ descs) {
   for (int i8 = blockIdx.x * blockDim.x + threadIdx.x; i8 < total8; i8 += gridDim.x * blockDim.x) {
     const int co = i8 / kpk8, kk8 = i8 - co * kpk8;
     const int j = kk8 / kc8, kr = (kk8 - j * kc8) * 8;
-    const int tap = kr / d.cc, c0 = j * d.cc + kr - tap * d.cc;
     float v[8];
-    const bool ok = co < d.out_c_real && tap < kk2;
-    const int ky = tap / d.ks, kx = tap - (tap / d.ks) * d.ks;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int c = c0 + e;
+    for (int e = 0; e < 8; ++e) {  // (cc = 4: the 8 elements span two taps)
+      const int tap = (kr + e) / d.cc, c = j * d.cc + (kr + e) - tap * d.cc;
+      const bool ok = co < d.out_c_real && tap < kk2;
+      const int ky = tap / d.ks, kx = tap - (tap / d.ks) * d.ks;
       v[e] = 0.f;
       if (ok && c < d.in_c_real) {
         if (!d.tflip) v[e] = d.w[((co * d.in_c_real + c) * d.ks + ky) * d.ks + kx];
@@ -1346,10 +1348,11 @@ static bool pw_geom(const ClimsrConvDesc* d, int nt, int mw, PwGeom* g, int nw =
   g->mw = mw;
   g->tph = nw * mw + d->ks - 1;
   g->tpw = TW + d->ks - 1;
-  g->ccp = xpitch(d->cc);
+  const int ccs = d->cc < 8 ? 8 : d->cc;  // staged channels per pixel (cc 4: 16 B loads, 4 of 8 channels used)
+  g->ccp = xpitch(ccs);
   g->kcpad = round_up(d->ks * d->ks * d->cc, 32);
-  g->nvx = g->tph * g->tpw * (d->cc / 8);
-  g->lds_tab = ((size_t)(g->kcpad / 8) * 4 + 15) / 16 * 16;
+  g->nvx = g->tph * g->tpw * (ccs / 8);
+  g->lds_tab = ((size_t)(g->kcpad / (d->cc < 8 ? 4 : 8)) * 4 + 15) / 16 * 16;
   g->lds_w = (size_t)nt * 16 * (g->kcpad + WPAD) * 2;
   g->lds_x = (size_t)g->tph * g->tpw * g->ccp * 2;
   g->lds_ep = (size_t)nw * mw * 16 * (nt * 16 + 4) * 4;
@@ -1383,6 +1386,12 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
   const int wpitch = a.kcpad + WPAD;
   const int ks2 = a.ks * a.ks;
+  if constexpr (GEO == 2) {  // 4-channel taps: table of tap offsets, one per 4 k values
+    for (int i = tid; i < a.kcpad / 4; i += NTHR) {
+      const int tap = i < ks2 ? i : 0, ky = tap / a.ks, kx = tap - ky * a.ks;
+      tab[i] = (ky * a.tpw + kx) * a.ccp;
+    }
+  }
   for (int i = tid; i < (GEO ? 0 : a.kcpad / 8); i += NTHR) {  // tap table (one chunk)
     const int kr = i * 8;
     int tap = kr / a.cc, c = kr - tap * a.cc;
@@ -1515,11 +1524,18 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
       const int nks = a.kcpad / 32;
       bf16x8 afA[NT], bfA[MW], afB[NT], bfB[MW];
       auto ld = [&](int ks, bf16x8 (&af)[NT], bf16x8 (&bf)[MW]) {
-        const int off = tab[ks * 4 + g];
 #pragma unroll
         for (int t = 0; t < NT; ++t) af[t] = *(const bf16x8*)(ws + (t * 16 + col) * wpitch + ks * 32 + g * 8);
+        if constexpr (GEO == 2) {  // k values 8g..8g+7 of the step = taps 8 ks + 2g, +1, 4 channels each
+          const int off0 = tab[ks * 8 + 2 * g], off1 = tab[ks * 8 + 2 * g + 1];
 #pragma unroll
-        for (int m = 0; m < MW; ++m) bf[m] = *(const bf16x8*)(xs + pixbase[m] + off);
+          for (int m = 0; m < MW; ++m)
+            bf[m] = cat_tr(*(const s16x4*)(xs + pixbase[m] + off0), *(const s16x4*)(xs + pixbase[m] + off1));
+        } else {
+          const int off = tab[ks * 4 + g];
+#pragma unroll
+          for (int m = 0; m < MW; ++m) bf[m] = *(const bf16x8*)(xs + pixbase[m] + off);
+        }
       };
       auto mm = [&](const bf16x8 (&af)[NT], const bf16x8 (&bf)[MW]) {
 #pragma unroll
@@ -1660,6 +1676,12 @@ static int launch_pw_geo(const FwdArgs& a0, const PwGeom& g, hipStream_t s) {
 
 template <int NW, int MW, int NT, int PV, int EP = 0>
 static int launch_pw(const FwdArgs& a, const PwGeom& g, hipStream_t s) {
+  if (a.cc == 4) {  // 4-channel taps: staged as 8-channel pixels (16 B loads)
+    FwdArgs b = a;
+    b.cc = 8;
+    b.in_c = 8;
+    return launch_pw_geo<NW, MW, NT, PV, EP, 2>(b, g, s);
+  }
   if constexpr (NW * MW == 16) {
     if (a.ks == 3 && a.cc == 64 && g.kcpad == 9 * 64 && g.ccp == 80 && g.tpw == TW + 2 && g.tph == 18)
       return launch_pw_geo<NW, MW, NT, PV, EP, 1>(a, g, s);
@@ -2474,7 +2496,8 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
     set_error("conv2d_fwd: null argument");
     return CLIMSR_EINVAL;
   }
-  if (d->in_c % 8 || d->in_cstride % 8 || d->in_coff % 8 || d->cc % 8 || d->cc <= 0 ||
+  const bool cc4 = d->cc == 4 && d->in_c == 4;  // conv_pw GEO 2 (climsr_conv_chunk_ex)
+  if ((d->in_c % 8 && !cc4) || d->in_cstride % 8 || d->in_coff % 8 || (d->cc % 8 && !cc4) || d->cc <= 0 ||
       (d->up != 1 && d->up != 2 && d->up != -2) ||
       (d->stride != 1 && d->stride != 2) || d->ks < 1 || d->n <= 0 || d->out_c <= 0 || d->in_coff + d->in_c > d->in_cstride) {
     set_error("conv2d_fwd: unsupported geometry (in_c=%d cs=%d coff=%d cc=%d up=%d stride=%d ks=%d)", d->in_c, d->in_cstride,
@@ -2573,10 +2596,10 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
     const int nt = fwd_nt(d->out_c);
     const long npx = (long)d->n * d->out_h * d->out_w;
     PwGeom pg;
-    if (ncob == 1 && (nt == 4 || nt == 2) && d->up != -2 && npx >= 4096 &&
+    if (ncob == 1 && (nt == 4 || nt == 2) && d->up != -2 && (npx >= 4096 || cc4) &&
         (long)d->n * d->in_h * d->in_w * d->in_cstride * 2 < (1L << 31)) {  // 32-bit buffer offsets
       // 8 waves x 2 rows (two waves per SIMD) when the LDS allows, else 4 waves x 2 rows
-      if (pw_geom(d, nt, 2, &pg, 8) && pg.nvx <= 512 * 7 && d->out_h >= 16) {
+      if (pw_geom(d, nt, 2, &pg, 8) && pg.nvx <= 512 * 7 && (d->out_h >= 16 || cc4)) {
         // epilogue specialisations (store_tile_lds EP 3 / 4): activation forward / activation backward
         const bool v8 = (a.out_c & 7) == 0 && ((a.out_cs | a.out_co) & 7) == 0 && !a.down2 && !a.res2 && !a.aux &&
                         a.out_mode == 0 && a.res_f32 == 0;
@@ -2600,6 +2623,10 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
       }
       if (pw_geom(d, nt, 2, &pg, 4)) return nt == 4 ? launch_pw<4, 2, 4, 12>(a, pg, s) : launch_pw<4, 2, 2, 12>(a, pg, s);
     }
+  }
+  if (cc4) {
+    set_error("conv2d_fwd: 4-channel chunks need the conv_pw path (stride 1, up 1/2, 64 outputs, 32-bit offsets)");
+    return CLIMSR_EINVAL;
   }
   if (g.lds_total > 160 * 1024) {
     set_error("conv2d_fwd: LDS %zu exceeds 160 KiB (cc=%d)", g.lds_total, d->cc);

@@ -66,8 +66,13 @@ class ConvPlan:
         self.cin_real, self.cout, self.ks, self.stride = cin_real, cout, ks, stride
         self.pad = ks // 2 if pad is None else pad
         self.cin = round_up(cin_real, 8)
-        self.cc = lib.climsr_conv_chunk_ex(self.cin, ks, cout, stride)
-        self.kpk = lib.climsr_conv_packed_k(self.cin, ks, self.cc)
+        # <= 4 real input channels: taps packed 4 channels apart (climsr_conv_chunk_ex returns 4 for the shapes it
+        # has a kernel for); cin_k = the channel count of the packed K layout
+        self.cc = lib.climsr_conv_chunk_ex(4 if cin_real <= 4 else self.cin, ks, cout, stride)
+        if self.cc == 4 and self.pad != ks // 2:
+            self.cc = lib.climsr_conv_chunk_ex(self.cin, ks, cout, stride)
+        self.cin_k = 4 if self.cc == 4 else self.cin
+        self.kpk = lib.climsr_conv_packed_k(self.cin_k, ks, self.cc)
         self.rows = lib.climsr_conv_packed_rows(cout)
         # transposed conv (data gradient): in = cout (padded to 8), out = cin_real
         self.cin_t = round_up(cout, 8)
@@ -98,14 +103,14 @@ class ConvPlan:
         s = _lib.stream_ptr() if stream is None else stream
         w = self.weight
         assert w is not None and w.dtype == torch.float32 and w.is_contiguous()
-        _launch(f"pack {self.name}", lambda: lib.climsr_pack_conv_weight(ptr(w), self.cout, self.cin, self.cin_real, self.cout, self.ks, self.cc, 0,
-                                          ptr(self.wpk), s))
+        _launch(f"pack {self.name}", lambda: lib.climsr_pack_conv_weight(ptr(w), self.cout, self.cin_k, self.cin_real, self.cout, self.ks, self.cc,
+                                          0, ptr(self.wpk), s))
         if self.wpk_t is not None:
             _launch(f"pack_t {self.name}", lambda: lib.climsr_pack_conv_weight(ptr(w), self.cout_t, self.cin_t, self.cout, self.cout_t, self.ks, self.cc_t, 1,
                                               ptr(self.wpk_t), s))
 
     def pack_descs(self):
-        out = [PackDesc(ptr(self.weight), ptr(self.wpk), self.cout, self.cin, self.cin_real, self.cout, self.ks, self.cc, 0, 0)]
+        out = [PackDesc(ptr(self.weight), ptr(self.wpk), self.cout, self.cin_k, self.cin_real, self.cout, self.ks, self.cc, 0, 0)]
         if self.wpk_t is not None:
             out.append(PackDesc(ptr(self.weight), ptr(self.wpk_t), self.cout_t, self.cin_t, self.cout, self.cout_t, self.ks,
                                 self.cc_t, 1, 0))
@@ -138,7 +143,7 @@ class ConvPlan:
                                                      self.cout, act, slope, ptr(y), y_cs, y_co, _lib.stream_ptr()),
                 f"conv fwd {self.name}"), "fwd " + self.name, px * 2 + px * self.cout * 2)
             return
-        d = ConvDesc(n, in_h, in_w, self.cin, x_cs, x_co, up, self.ks, self.stride, self.pad, oh, ow, self.cout, y_cs, y_co,
+        d = ConvDesc(n, in_h, in_w, self.cin_k, x_cs, x_co, up, self.ks, self.stride, self.pad, oh, ow, self.cout, y_cs, y_co,
                      self.cc)
         rf = (1 if res1 is not None and res1.dtype == torch.float32 else 0) | \
              (2 if res2 is not None and res2.dtype == torch.float32 else 0)
