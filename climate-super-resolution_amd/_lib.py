@@ -30,7 +30,8 @@ class Epilogue(ctypes.Structure):
                 ("res1_cstride", ctypes.c_int32), ("res1_coff", ctypes.c_int32), ("alpha2", c_float), ("res2", c_void_p),
                 ("res2_cstride", ctypes.c_int32), ("res2_coff", ctypes.c_int32), ("out_mode", ctypes.c_int32),
                 ("down2", ctypes.c_int32), ("res_f32", ctypes.c_int32), ("beta1", c_float), ("beta2", c_float),
-                ("aux_cstride", ctypes.c_int32), ("aux", c_void_p), ("aux_coff", ctypes.c_int32), ("aux_scale", c_float)]
+                ("aux_cstride", ctypes.c_int32), ("aux", c_void_p), ("aux_coff", ctypes.c_int32), ("aux_scale", c_float),
+                ("bn_part", c_void_p)]
 
     def __init__(self, *args, **kw):
         # plain residual adds unless a caller scales them (beta1 / beta2 are positional fields 13 / 14)
@@ -99,6 +100,9 @@ SIGNATURES = {
     "climsr_rdb_chain": (c_int, [P(ChainDesc), c_void_p]),
     "climsr_rdb_chain_kp": (c_int, [c_int]),
     "climsr_conv2d_fwd": (c_int, [P(ConvDesc), c_void_p, c_void_p, c_void_p, P(Epilogue), c_void_p, c_void_p]),
+    "climsr_conv2d_fwd_bn_parts": (ctypes.c_int64, [P(ConvDesc), P(Epilogue)]),
+    "climsr_bn_forward_parts": (c_int, [c_void_p, ctypes.c_int64, c_void_p, ctypes.c_int64, c_int, c_void_p, c_void_p, c_int, c_float,
+                                        c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "climsr_conv2d_fwd_kernel": (ctypes.c_char_p, [P(ConvDesc), c_void_p, P(Epilogue)]),
     "climsr_conv2d_wgrad_kernel": (ctypes.c_char_p, [P(ConvDesc)]),
     "climsr_dgrad_single_output_kernel": (ctypes.c_char_p, [c_int, c_int, c_int]),

@@ -316,6 +316,7 @@ struct FwdArgs {
   int aux_cs, aux_co;
   float aux_scale;
   int lds_tab, lds_x;
+  double* bn_part;  // EP 9: per-tile BatchNorm partial sums [tile][2][out_c] of the bf16 outputs (climsr_conv2d_fwd_bn_parts)
 };
 
 // Epilogue residual operands: 4 consecutive channels, bf16 (8 B) or fp32 (16 B), kept raw until use so
@@ -409,7 +410,7 @@ __device__ __forceinline__ uint4 pack8_bf16(const float* v, float scale) {
 // 2 = fp32 data gradient (no bias / activation, fp32 residual(s), fp32 '=' output, optional bf16 aux: pull-x).
 template <bool RF, int NPX, int NCH, int NLANE, int EP = 0>
 __device__ __forceinline__ void store_tile_lds(const FwdArgs& a, const float* eb, int ep, int lane, int nimg, int oy0, int ox0,
-                                               int co0) {
+                                               int co0, float* ssum = nullptr, float* ssq = nullptr) {
   constexpr int NG = NCH / 8, NIT = NPX * NG;
   // EP 3 = activation forward (bias + leaky relu / relu, bf16 out); 4 = activation backward (act' read from
   // the bf16 activation res1, no bias, bf16 out): the HR-resolution layers (conv_pw_kernel); 6 = activation
@@ -418,7 +419,9 @@ __device__ __forceinline__ void store_tile_lds(const FwdArgs& a, const float* eb
   const bool f1 = EP == 2 ? true : EP != 0 ? false : RF && (a.res_f32 & 1);
   const bool f2 = EP == 2 ? true : EP != 0 ? false : RF && ((a.res_f32 >> 1) & 1);
   const bool has_bias = (EP == 1 || EP == 3) ? true : EP != 0 ? false : a.bias != nullptr;
-  const int act = (EP == 1 || EP == 2 || EP == 7 || EP == 8) ? 0 : a.act;
+  // EP 9 = EP 8 + sums / sums of squares of the stored (bf16-rounded) values per lane (ssum / ssq [8]: the lane's
+  // 8 channels, the same for all of its items when NCH / 8 divides NLANE)
+  const int act = (EP == 1 || EP == 2 || EP == 7 || EP == 8 || EP == 9) ? 0 : a.act;
   const bool has1 = (EP == 1 || EP == 2 || EP == 4) ? true : EP != 0 ? false : a.res1 != nullptr;
   const bool has2 = (EP == 0 || EP == 1 || EP == 2) ? a.res2 != nullptr : false;
   const int out_mode = (EP == 2 || EP == 7) ? 1 : EP != 0 ? 0 : a.out_mode;
@@ -474,7 +477,19 @@ __device__ __forceinline__ void store_tile_lds(const FwdArgs& a, const float* eb
           v[i] = ep_res(act_apply(v[i] + bb[i], act, a.slope), act, a.slope, has1, raw8_at(r1[j], f1, i), a.alpha1, a.beta1, has2,
                         raw8_at(r2[j], f2, i), a.alpha2, a.beta2);
         if (out_mode == 0) {
-          *(uint4*)((uint16_t*)a.y + ob) = pack8_bf16(v, 1.f);
+          const uint4 pk = pack8_bf16(v, 1.f);
+          *(uint4*)((uint16_t*)a.y + ob) = pk;
+          if constexpr (EP == 9) {
+            Raw8 rr;
+            rr.lo = pk;
+            rr.hi = make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              const float r = raw8_at(rr, false, i);
+              ssum[i] += r;
+              ssq[i] = fmaf(r, r, ssq[i]);
+            }
+          }
         } else {
           float o[8];
 #pragma unroll
@@ -498,6 +513,45 @@ __device__ __forceinline__ void store_tile_lds(const FwdArgs& a, const float* eb
         }
       }
     }
+  }
+}
+
+// BatchNorm partials of one 16x16-pixel x 64-channel output tile (EP 9): the lanes with equal lane % 8 own the same
+// 8 channels (store_tile_lds items), so three xor-shuffles (8, 16, 32) give each wave's sums in lanes 0..7; the 4
+// row waves meet in LDS and wave 0 writes fp64 part[tile][0 / 1][co0 + ch] -- fixed order, deterministic.  Every
+// wave of the workgroup calls it (`live` = the wave stored rows); red = 2 KB of LDS no wave reads any more.
+__device__ __forceinline__ void bn_tile_partials(const FwdArgs& a, float* ssum, float* ssq, bool live, int wave4, int lane, long tile,
+                                                 int co0, float* red) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (!live) { ssum[i] = 0.f; ssq[i] = 0.f; }
+#pragma unroll
+    for (int m = 8; m < 64; m <<= 1) {
+      ssum[i] += __shfl_xor(ssum[i], m);
+      ssq[i] += __shfl_xor(ssq[i], m);
+    }
+  }
+  // LDS-only barriers: __syncthreads()' release fence would also wait for this wave's output stores
+  lds_barrier();  // every wave's epilogue reads of the staging region are done
+  if (live && lane < 8) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      red[wave4 * 128 + lane * 8 + i] = ssum[i];
+      red[wave4 * 128 + 64 + lane * 8 + i] = ssq[i];
+    }
+  }
+  lds_barrier();
+  if (threadIdx.x < 64) {
+    const int ch = threadIdx.x;
+    float ts = 0.f, tq = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      ts += red[w * 128 + ch];
+      tq += red[w * 128 + 64 + ch];
+    }
+    double* out = a.bn_part + tile * 2 * a.out_c;
+    out[co0 + ch] = (double)ts;
+    out[a.out_c + co0 + ch] = (double)tq;
   }
 }
 
@@ -842,7 +896,14 @@ __device__ __forceinline__ void conv_fwd_body(const FwdArgs& a) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) *(f32x4*)(eb + (m * 16 + col) * EPP + t * 16 + g * 4) = acc[m][t];
   __syncthreads();  // orders the staging writes before the transposed reads (they use another vector type)
-  store_tile_lds<RF, MW * 16, NT * 16, 64, EP>(a, eb, EPP, lane, nimg, oy0 + wave * MW, ox0, co_blk0);
+  if constexpr (EP == 9) {
+    static_assert(MW == 4 && NT == 4, "BatchNorm partials: 16x16 x 64-channel tiles");
+    float ssum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, ssq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    store_tile_lds<RF, MW * 16, NT * 16, 64, EP>(a, eb, EPP, lane, nimg, oy0 + wave * MW, ox0, co_blk0, ssum, ssq);
+    bn_tile_partials(a, ssum, ssq, true, wave, lane, blockIdx.x, co_blk0, (float*)smem);
+  } else {
+    store_tile_lds<RF, MW * 16, NT * 16, 64, EP>(a, eb, EPP, lane, nimg, oy0 + wave * MW, ox0, co_blk0);
+  }
 }
 
 // two workgroups per CU (<= 80 KiB LDS each): at most 256 registers so that two waves share each SIMD
@@ -2256,6 +2317,7 @@ constexpr int S2F_EPP = 64 + 4;
 constexpr int S2F_LDS_RED = 4 * 16 * 64 * 16, S2F_LDS_EP = 4 * 64 * S2F_EPP * 4;
 constexpr int S2F_LDS = S2F_LDS_OP > S2F_LDS_RED + S2F_LDS_EP ? S2F_LDS_OP : S2F_LDS_RED + S2F_LDS_EP;
 
+template <bool STATS>
 __global__ __launch_bounds__(512) void conv_fwd_s2_kernel(FwdArgs a) {
   constexpr int MW = 4, NT = 4, NRX = (S2F_TP * S2F_TP * 4 + 511) / 512, NRW = (64 * 36 + 511) / 512;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -2359,22 +2421,25 @@ __global__ __launch_bounds__(512) void conv_fwd_s2_kernel(FwdArgs a) {
       for (int t = 0; t < NT; ++t) red[(m * NT + t) * 64 + lane] = make_float4(acc[m][t][0], acc[m][t][1], acc[m][t][2], acc[m][t][3]);
   }
   __syncthreads();
-  if (h == 1) return;
+  float ssum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, ssq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (h == 0) {
 #pragma unroll
-  for (int m = 0; m < MW; ++m)
+    for (int m = 0; m < MW; ++m)
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const float4 o = red[(m * NT + t) * 64 + lane];
-      acc[m][t][0] += o.x;
-      acc[m][t][1] += o.y;
-      acc[m][t][2] += o.z;
-      acc[m][t][3] += o.w;
-      *(f32x4*)(eb + (m * 16 + col) * S2F_EPP + t * 16 + g * 4) = acc[m][t];
-    }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-  store_tile_lds<false, MW * 16, NT * 16, 64, 8>(a, eb, S2F_EPP, lane, nimg, oy0 + r * MW, ox0, co0);
+      for (int t = 0; t < NT; ++t) {
+        const float4 o = red[(m * NT + t) * 64 + lane];
+        acc[m][t][0] += o.x;
+        acc[m][t][1] += o.y;
+        acc[m][t][2] += o.z;
+        acc[m][t][3] += o.w;
+        *(f32x4*)(eb + (m * 16 + col) * S2F_EPP + t * 16 + g * 4) = acc[m][t];
+      }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    store_tile_lds<false, MW * 16, NT * 16, 64, STATS ? 9 : 8>(a, eb, S2F_EPP, lane, nimg, oy0 + r * MW, ox0, co0, ssum, ssq);
+  }
+  if constexpr (STATS) bn_tile_partials(a, ssum, ssq, h == 0, r, lane, blockIdx.x, co0, (float*)smem);
 }
 
 static int plain_ep(const FwdArgs& a);
@@ -2387,15 +2452,18 @@ static int launch_fwd_s2(const ClimsrConvDesc* d, FwdArgs a, hipStream_t s) {
   a.tiles_x = ceil_div(d->out_w, 16);
   a.tiles_y = ceil_div(d->out_h, 16);
   if (g_dry) {
-    snprintf(g_dry_name, sizeof(g_dry_name), "conv_fwd_s2_kernel");
+    snprintf(g_dry_name, sizeof(g_dry_name), "conv_fwd_s2_kernel<%s>", a.bn_part ? "true" : "false");
     return CLIMSR_OK;
   }
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)conv_fwd_s2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)conv_fwd_s2_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)conv_fwd_s2_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  hipLaunchKernelGGL(conv_fwd_s2_kernel, dim3(a.tiles_x * a.tiles_y * a.n, d->out_c / 64), dim3(512), S2F_LDS, s, a);
+  const dim3 grid(a.tiles_x * a.tiles_y * a.n, d->out_c / 64);
+  if (a.bn_part) hipLaunchKernelGGL(conv_fwd_s2_kernel<true>, grid, dim3(512), S2F_LDS, s, a);
+  else hipLaunchKernelGGL(conv_fwd_s2_kernel<false>, grid, dim3(512), S2F_LDS, s, a);
   return check_launch("conv2d_fwd (s2)");
 }
 
@@ -2490,6 +2558,32 @@ static int plain_ep(const FwdArgs& a) {
   return 0;
 }
 
+// The convs whose epilogue can emit BatchNorm partials (EP 9 / conv_fwd_s2_kernel<true>): plain bf16 out over 16x16
+// tiles of 64-channel blocks -- the stride-2 kernel, or the chunk-pipelined generic kernel with >= 2 channel blocks
+// (so neither conv_pw nor conv_n16 takes it).  Mirrors the dispatch below.
+static bool bn_parts_ok(const ClimsrConvDesc* d, const FwdArgs& a, const FwdGeom& g) {
+  if (plain_ep(a) != 8 || d->out_c % 64) return false;
+  if (d->stride == 2) return fwd_s2_shape(d, a);
+  const int nrx = ceil_div(g.tph * g.tpw * (d->cc / 8), 256), nrw = ceil_div(g.nt * 16 * (g.kcpad / 8), 256);
+  return d->stride == 1 && d->up == 1 && d->ks == 3 && g.mw == 4 && g.nt == 4 && d->out_c >= 128 && g.nchunk > 1 && nrx <= 6 &&
+         nrw <= 9 && g.lds_total <= 160 * 1024;
+}
+
+extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, const uint16_t* wpk, const float* bias,
+                                 const ClimsrEpilogue* ep, void* y, void* stream);
+
+extern "C" int64_t climsr_conv2d_fwd_bn_parts(const ClimsrConvDesc* d, const ClimsrEpilogue* ep) {
+  if (!d || !ep || d->cc % 8 || d->cc <= 0 || d->stride < 1) return 0;
+  const int mw = (d->out_h >= 12 && fwd_nt(d->out_c) == 4) ? 4 : 2;
+  FwdGeom g;
+  fwd_geom(d->in_c, d->ks, d->stride, d->out_c, d->cc, mw, &g);
+  FwdArgs a{};
+  a.act = ep->act; a.out_mode = ep->out_mode; a.down2 = ep->down2; a.res1 = ep->res1; a.res2 = ep->res2; a.aux = (uint16_t*)ep->aux;
+  a.res_f32 = ep->res_f32; a.out_c = d->out_c; a.out_cs = d->out_cstride; a.out_co = d->out_coff; a.kcpad = g.kcpad;
+  if (!bn_parts_ok(d, a, g)) return 0;
+  return (int64_t)ceil_div(d->out_w, TW) * ceil_div(d->out_h, 16) * d->n;
+}
+
 extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, const uint16_t* wpk, const float* bias,
                                  const ClimsrEpilogue* ep, void* y, void* stream) {
   if (!d || !x || !wpk || !ep || !y) {
@@ -2546,9 +2640,14 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
   a.slope = ep->slope; a.alpha1 = ep->alpha1; a.alpha2 = ep->alpha2;
   a.r1_cs = ep->res1_cstride; a.r1_co = ep->res1_coff; a.r2_cs = ep->res2_cstride; a.r2_co = ep->res2_coff;
   a.lds_tab = (int)g.lds_tab; a.lds_x = (int)g.lds_x;
+  a.bn_part = ep->bn_part;
   int rows = climsr_conv_packed_rows(d->out_c);
   int ncob = rows / (g.nt * 16);
   hipStream_t s = (hipStream_t)stream;
+  if (ep->bn_part && !bn_parts_ok(d, a, g)) {
+    set_error("conv2d_fwd: BatchNorm partials only for the 16x16-tile bf16 paths (climsr_conv2d_fwd_bn_parts)");
+    return CLIMSR_EINVAL;
+  }
   if (d->out_c == 1 && d->stride == 1 && d->up == 1 && !ep->down2 && !ep->res2 && co1m_shape(d))
     return dispatch_co1m(d, a, s);
   if (d->out_c == 1 && d->stride == 1 && d->up == 1 && !ep->down2 && !ep->res2) {
@@ -2651,7 +2750,7 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
         case 3: return launch_fwd_ep<4, 4, 6, 9, 3>(a, ncob, g.lds_total, s);
         case 6: return launch_fwd_ep<4, 4, 6, 9, 6>(a, ncob, g.lds_total, s);
         case 7: return launch_fwd_ep<4, 4, 6, 9, 7>(a, ncob, g.lds_total, s);
-        case 8: return launch_fwd_ep<4, 4, 6, 9, 8>(a, ncob, g.lds_total, s);
+        case 8: return a.bn_part ? launch_fwd_ep<4, 4, 6, 9, 9>(a, ncob, g.lds_total, s) : launch_fwd_ep<4, 4, 6, 9, 8>(a, ncob, g.lds_total, s);
         default: return launch_fwd<4, 4, 6, 9>(a, ncob, g.lds_total, s);
       }
     }

@@ -362,6 +362,23 @@ extern "C" int climsr_bn_forward(const uint16_t* z, int64_t npix, int c, const f
   return check_launch("bn_forward");
 }
 
+extern "C" int climsr_bn_forward_parts(const double* parts, int64_t nparts, const uint16_t* z, int64_t npix, int c, const float* gamma,
+                                       const float* beta, int act, float slope, float eps, float momentum, float* mean, float* rstd,
+                                       float* run_mean, float* run_var, int64_t* num_batches_tracked, uint16_t* y, void* stream) {
+  if (!parts || nparts <= 0 || nparts > (1L << 30) || !z || !gamma || !beta || !mean || !rstd || !y || !bn_shape_ok(npix, c)) {
+    set_error("bn_forward_parts: bad args (c=%d, npix=%lld, parts=%lld)", c, (long long)npix, (long long)nparts);
+    return CLIMSR_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(bn_finish_stats_kernel, dim3(ceil_div(c, 8)), dim3(256), 0, s, parts, (int)nparts, c, (int)npix, eps, momentum,
+                     mean, rstd, run_mean, run_var, num_batches_tracked);
+  int per;
+  const int nb = bn_apply_grid(npix, c, &per);
+  hipLaunchKernelGGL(bn_apply_kernel<0>, dim3(nb), dim3(256), 0, s, (int)npix, c, per, z, mean, rstd, 0.f, gamma, beta, act, slope,
+                     y);
+  return check_launch("bn_forward_parts");
+}
+
 extern "C" int climsr_bn_inference(const uint16_t* z, int64_t npix, int c, const float* run_mean, const float* run_var, float eps,
                                    const float* gamma, const float* beta, int act, float slope, uint16_t* y, void* stream) {
   if (!z || !run_mean || !run_var || !gamma || !beta || !y || !bn_shape_ok(npix, c)) {

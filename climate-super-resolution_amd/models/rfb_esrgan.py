@@ -98,14 +98,22 @@ class _DEngine:
                 saved.append(dict(a_in=a_prev, cs_in=cs_prev, h_in=hh, w_in=ww, z=None, a=a, mean=None, rstd=None, oh=oh, ow=ow))
             else:
                 z = _bf16((n, oh, ow, c), dev)
-                plan.fwd(a_prev, cs_prev, 0, hh, ww, z, c, 0, n, use_bias=False)
                 a = _bf16((n, oh, ow, c), dev)
                 npix = n * oh * ow
+                # train mode: the conv epilogue emits the batch statistics' partial sums (no pass over z for them)
+                nparts = plan.bn_parts(cs_prev, hh, ww, n, c) if training else 0
+                part = self._scr(f"bnpart{len(saved)}", (max(nparts, 1) * 2 * c,), torch.float64, dev) if nparts else None
+                plan.fwd(a_prev, cs_prev, 0, hh, ww, z, c, 0, n, use_bias=False, bn_part=part)
                 if training:
                     mean, rstd = _f32((c,), dev), _f32((c,), dev)
-                    ops.bn_forward(z, npix, c, bn.weight, bn.bias, mean, rstd, a, ops.bn_workspace(npix, c, self.scratch, dev),
-                                   bn.running_mean, bn.running_var, eps=bn.eps, momentum=bn.momentum,
-                                   num_batches_tracked=bn.num_batches_tracked)
+                    if nparts:
+                        ops.bn_forward_parts(part, nparts, z, npix, c, bn.weight, bn.bias, mean, rstd, a, bn.running_mean,
+                                             bn.running_var, eps=bn.eps, momentum=bn.momentum,
+                                             num_batches_tracked=bn.num_batches_tracked)
+                    else:
+                        ops.bn_forward(z, npix, c, bn.weight, bn.bias, mean, rstd, a, ops.bn_workspace(npix, c, self.scratch, dev),
+                                       bn.running_mean, bn.running_var, eps=bn.eps, momentum=bn.momentum,
+                                       num_batches_tracked=bn.num_batches_tracked)
                 else:
                     mean = rstd = None
                     ops.bn_inference(z, npix, c, bn.running_mean, bn.running_var, bn.weight, bn.bias, a, eps=bn.eps)

@@ -127,9 +127,10 @@ class ConvPlan:
             res1: Optional[torch.Tensor] = None, alpha1: float = 1.0, res1_cs: int = 0, res1_co: int = 0,
             res2: Optional[torch.Tensor] = None, alpha2: float = 1.0, res2_cs: int = 0, res2_co: int = 0,
             out_mode: int = OUT_BF16, beta1: float = 1.0, beta2: float = 1.0, aux: Optional[torch.Tensor] = None,
-            aux_cs: int = 0, aux_co: int = 0, aux_scale: float = 1.0) -> None:
+            aux_cs: int = 0, aux_co: int = 0, aux_scale: float = 1.0, bn_part: Optional[torch.Tensor] = None) -> None:
         """y = epilogue(conv(x)); residuals res1/res2 may be bf16 or fp32 tensors (dtype decides), aux = optional
-        second bf16 output aux_scale * y."""
+        second bf16 output aux_scale * y; bn_part (fp64, bn_parts() rows x 2 x cout) = BatchNorm partial sums of y
+        for bn_forward_parts."""
         oh, ow = self.out_hw(in_h, in_w, up)
         if (self.cin_real == 1 and self.ks in (3, 5) and self.stride == 1 and self.pad == self.ks // 2 and up == 1
                 and self.cout in (32, 64) and out_mode == OUT_BF16 and y.dtype == torch.bfloat16 and res1 is None and res2 is None
@@ -148,7 +149,7 @@ class ConvPlan:
         rf = (1 if res1 is not None and res1.dtype == torch.float32 else 0) | \
              (2 if res2 is not None and res2.dtype == torch.float32 else 0)
         ep = Epilogue(act, slope, alpha1, ptr(res1), res1_cs, res1_co, alpha2, ptr(res2), res2_cs, res2_co, out_mode, 0,
-                      rf, beta1, beta2, aux_cs, ptr(aux), aux_co, aux_scale)
+                      rf, beta1, beta2, aux_cs, ptr(aux), aux_co, aux_scale, ptr(bn_part))
         b = ptr(self.bias) if (use_bias and self.bias is not None) else None
         flops = 2 * self.cin_real * self.cout * self.ks * self.ks * n * oh * ow
         opx = n * oh * ow
@@ -158,6 +159,14 @@ class ConvPlan:
         _run(_kname(d, b, ep), flops, lambda: check(
             _lib.load().climsr_conv2d_fwd(ctypes.byref(d), ptr(x), ptr(self.wpk), b, ctypes.byref(ep), ptr(y), _lib.stream_ptr()),
             f"conv fwd {self.name}"), "fwd " + self.name, nbytes)
+
+    def bn_parts(self, x_cs: int, in_h: int, in_w: int, n: int, y_cs: int) -> int:
+        """Rows of BatchNorm partials fwd(..., use_bias=False, bn_part=...) writes (plain bf16 output), 0 if its kernel
+        cannot (climsr_conv2d_fwd_bn_parts)."""
+        oh, ow = self.out_hw(in_h, in_w)
+        d = ConvDesc(n, in_h, in_w, self.cin_k, x_cs, 0, 1, self.ks, self.stride, self.pad, oh, ow, self.cout, y_cs, 0, self.cc)
+        ep = Epilogue(ACT_NONE, 0.0, 1.0, None, 0, 0, 1.0, None, 0, 0, OUT_BF16, 0, 0, 1.0, 1.0, 0, None, 0, 1.0, 1)
+        return int(_lib.load().climsr_conv2d_fwd_bn_parts(ctypes.byref(d), ctypes.byref(ep)))
 
     def dgrad(self, dz: torch.Tensor, dz_cs: int, out_h: int, out_w: int, g: torch.Tensor, g_cs: int, g_co: int, n: int,
               accumulate: bool = False, down2: bool = False, cout_t: Optional[int] = None, aux: Optional[torch.Tensor] = None,
@@ -495,6 +504,15 @@ def bn_forward(z, npix, c, gamma, beta, mean, rstd, y, ws, run_mean=None, run_va
         _L().climsr_bn_forward(ptr(z), npix, c, ptr(gamma), ptr(beta), act, slope, eps, momentum, ptr(ws), ptr(mean), ptr(rstd),
                                ptr(run_mean), ptr(run_var), ptr(num_batches_tracked), ptr(y), _lib.stream_ptr()), "bn_forward"),
          "bn_forward", npix * c * 6)
+
+
+def bn_forward_parts(parts, nparts, z, npix, c, gamma, beta, mean, rstd, y, run_mean=None, run_var=None, act=ACT_LRELU, slope=0.2,
+                     eps=1e-5, momentum=0.1, num_batches_tracked=None):
+    """bn_forward with the batch statistics from the producing conv's epilogue partials (ConvPlan.fwd bn_part)."""
+    _run("bn_forward", 0, lambda: check(
+        _L().climsr_bn_forward_parts(ptr(parts), nparts, ptr(z), npix, c, ptr(gamma), ptr(beta), act, slope, eps, momentum, ptr(mean),
+                                     ptr(rstd), ptr(run_mean), ptr(run_var), ptr(num_batches_tracked), ptr(y), _lib.stream_ptr()),
+        "bn_forward_parts"), "bn_forward", npix * c * 4)
 
 
 def bn_inference(z, npix, c, run_mean, run_var, gamma, beta, y, act=ACT_LRELU, slope=0.2, eps=1e-5):

@@ -71,6 +71,9 @@ typedef struct ClimsrEpilogue {
   void* aux;                    /* optional second output, bf16 NHWC, same pixels */
   int32_t aux_coff;
   float aux_scale;
+  double* bn_part;              /* optional (plain bf16 output only): per-tile BatchNorm partials [tiles][2][out_c] (sum, sum of
+                                   squares of the stored bf16 values) for climsr_bn_forward_parts; tiles and support from
+                                   climsr_conv2d_fwd_bn_parts */
 } ClimsrEpilogue;
 
 const char* climsr_last_error(void);
@@ -147,6 +150,9 @@ int climsr_rdb_chain_kp(int level);
  * transpose_flip weights, its data gradient (stride 1). */
 int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, const uint16_t* wpk, const float* bias,
                       const ClimsrEpilogue* ep, void* y, void* stream);
+/* Number of BatchNorm partial rows (tiles) climsr_conv2d_fwd writes to ep->bn_part for this conv (no bias), or 0 when
+ * its dispatch cannot produce them (then bn_part must be NULL). */
+int64_t climsr_conv2d_fwd_bn_parts(const ClimsrConvDesc* d, const ClimsrEpilogue* ep);
 /* Name of the kernel climsr_conv2d_fwd launches for these arguments (as rocprof reports it; "" if invalid).
  * Launches nothing; used to label per-kernel timings and PMC traffic. */
 const char* climsr_conv2d_fwd_kernel(const ClimsrConvDesc* d, const float* bias, const ClimsrEpilogue* ep);
@@ -257,6 +263,11 @@ int64_t climsr_bn_workspace_doubles(int64_t npix, int c);
 int climsr_bn_forward(const uint16_t* z, int64_t npix, int c, const float* gamma, const float* beta, int act, float slope,
                       float eps, float momentum, double* workspace, float* mean, float* rstd, float* run_mean, float* run_var,
                       int64_t* num_batches_tracked, uint16_t* y, void* stream);
+/* climsr_bn_forward with the batch statistics taken from the producing conv's epilogue partials (ClimsrEpilogue.bn_part,
+ * nparts = climsr_conv2d_fwd_bn_parts) instead of a pass over z. */
+int climsr_bn_forward_parts(const double* parts, int64_t nparts, const uint16_t* z, int64_t npix, int c, const float* gamma,
+                            const float* beta, int act, float slope, float eps, float momentum, float* mean, float* rstd,
+                            float* run_mean, float* run_var, int64_t* num_batches_tracked, uint16_t* y, void* stream);
 /* Eval-mode BN (running statistics) + activation (nn.BatchNorm2d.eval()). */
 int climsr_bn_inference(const uint16_t* z, int64_t npix, int c, const float* run_mean, const float* run_var, float eps,
                         const float* gamma, const float* beta, int act, float slope, uint16_t* y, void* stream);

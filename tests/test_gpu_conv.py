@@ -461,3 +461,50 @@ def test_conv_fwd_stride2_plain_bf16(cin, cout, h, w):
     got = from_nhwc(y, cout).cpu().double()
     err = (got - want).abs().max().item()
     assert err <= 8e-3 * want.abs().max().item() + 1e-6, f"stride-2 fwd max err {err}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,stride,h,w", [(64, 128, 1, 32, 48), (128, 128, 2, 34, 40), (64, 64, 2, 64, 64), (64, 64, 1, 32, 32)])
+def test_conv_bn_partials_match_bn_forward(cin, cout, stride, h, w):
+    """BatchNorm statistics from the conv epilogue (ClimsrEpilogue.bn_part -> climsr_bn_forward_parts; the discriminator's
+    train-mode conv + BatchNorm2d + LeakyReLU, rfb_esrgan.py:30-50) vs climsr_bn_forward's own pass over the same z:
+    batch mean / rstd / running stats within fp32 summation-order noise, the activation within one bf16 ulp.  A conv
+    whose kernel cannot emit partials (64 -> 64 stride 1: conv_pw) reports 0 rows."""
+    from climsr_amd import ops
+
+    n = 2
+    p, _wt, _b = make_plan(cin, cout, 3, stride=stride, bias=False)
+    g = torch.Generator().manual_seed(21)
+    x = to_nhwc(bf(torch.rand((n, cin, h, w), generator=g) * 2 - 1))
+    oh, ow = p.out_hw(h, w)
+    nparts = p.bn_parts(p.cin, h, w, n, cout)
+    if cin == 64 and cout == 64 and stride == 1:
+        assert nparts == 0
+        return
+    assert nparts == n * ((oh + 15) // 16) * ((ow + 15) // 16)
+    part = torch.full((nparts * 2 * cout,), float("nan"), dtype=torch.float64, device=DEV)
+    z = torch.empty((n, oh, ow, cout), dtype=torch.bfloat16, device=DEV)
+    z2 = torch.empty_like(z)
+    p.fwd(x, p.cin, 0, h, w, z, cout, 0, n, use_bias=False, bn_part=part)
+    p.fwd(x, p.cin, 0, h, w, z2, cout, 0, n, use_bias=False)
+    gamma = torch.rand(cout, generator=g).to(DEV) + 0.5
+    beta = (torch.rand(cout, generator=g) - 0.5).to(DEV)
+    npix = n * oh * ow
+    outs = []
+    for fused in (True, False):
+        mean, rstd = torch.empty(cout, device=DEV), torch.empty(cout, device=DEV)
+        rm, rv = torch.zeros(cout, device=DEV), torch.ones(cout, device=DEV)
+        a = torch.empty_like(z)
+        if fused:
+            ops.bn_forward_parts(part, nparts, z, npix, cout, gamma, beta, mean, rstd, a, rm, rv)
+        else:
+            ops.bn_forward(z, npix, cout, gamma, beta, mean, rstd, a, ops.bn_workspace(npix, cout, {}, torch.device(DEV)), rm, rv)
+        outs.append((mean, rstd, rm, rv, a))
+    torch.cuda.synchronize()
+    assert torch.equal(z, z2), "bn_part must not change the conv output"
+    assert not torch.isnan(part).any(), "every partial row written"
+    for got, want, what in zip(outs[0][:4], outs[1][:4], ("mean", "rstd", "running_mean", "running_var")):
+        err = (got.double() - want.double()).abs().max().item()
+        assert err <= 1e-5 * (want.abs().max().item() + 1e-3), f"{what}: {err}"
+    da = (outs[0][4].float() - outs[1][4].float()).abs()
+    assert da.max().item() <= 1e-2 * outs[1][4].float().abs().max().item(), f"activation max diff {da.max().item()}"
