@@ -893,6 +893,84 @@ __global__ __launch_bounds__(256) void linear_dgrad_kernel(const uint16_t* __res
   }
 }
 
+// Wide form (k % 128 == 0, the fc.0 case): a workgroup owns 128 k columns (two 16-column fragments per wave), so a W
+// tile row is 256 contiguous bytes, and the dy fragments of the next 128-row o tile are loaded into registers together
+// with the next W tile (the form above reads them from global memory right before each MFMA).
+template <int NF>
+__global__ __launch_bounds__(256) void linear_dgrad_wide_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ w, int n,
+                                                                int k, int o, float* __restrict__ dx, int accumulate) {
+  constexpr int WP = 128 + 8;  // LDS row pitch (bf16)
+  __shared__ __attribute__((aligned(16))) uint16_t ws_[128 * WP];  // 128 o rows x 128 k
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
+  const int q = (lane & 15) >> 2, p = lane & 3;
+  const int k0 = blockIdx.x * 128;
+  f32x4 acc[2][NF];
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int f = 0; f < NF; ++f) acc[b][f] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  uint4 buf[8];
+  bf16x8 dyf[4][NF];
+  auto issue = [&](int ob) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int v = tid + i * 256;
+      const int r = v >> 4, cv = v & 15;
+      buf[i] = ob + r < o ? *(const uint4*)(w + (long)(ob + r) * k + k0 + cv * 8) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        const int nn = f * 16 + col, oo = ob + ks * 32 + g * 8;
+        dyf[ks][f] = (nn < n && oo < o) ? *(const bf16x8*)(dy + (long)nn * o + oo) : (bf16x8){};
+      }
+  };
+  issue(0);
+  for (int ob = 0; ob < o; ob += 128) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int v = tid + i * 256;
+      *(uint4*)(ws_ + (v >> 4) * WP + (v & 15) * 8) = buf[i];
+    }
+    bf16x8 af[4][NF];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int f = 0; f < NF; ++f) af[ks][f] = dyf[ks][f];
+    if (ob + 128 < o) issue(ob + 128);
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {  // 4 k-steps of 32 o
+      const int orow = ks * 32 + 8 * g + q;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int c0 = wave * 32 + b * 16 + 4 * p;
+        const bf16x8 bfr = cat_tr(ds_read_tr16(ws_ + orow * WP + c0), ds_read_tr16(ws_ + (orow + 4) * WP + c0));
+#pragma unroll
+        for (int f = 0; f < NF; ++f) acc[b][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][f], bfr, acc[b][f], 0, 0, 0);
+      }
+    }
+  }
+  // C: row = n (4g+i within frag f), col = k
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int kk = k0 + wave * 32 + b * 16 + col;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int nn = f * 16 + g * 4 + i;
+        if (nn < n) {
+          float* d = dx + (long)nn * k + kk;
+          *d = (accumulate ? *d : 0.f) + acc[b][f][i];
+        }
+      }
+    }
+  }
+}
+
 extern "C" int climsr_linear_dgrad(const uint16_t* dy, const uint16_t* w, int n, int k, int o, float* dx, int accumulate,
                                    void* stream) {
   if (!dy || !w || !dx || n <= 0 || n > 64 || k % 64 || o % 32) {
@@ -901,6 +979,13 @@ extern "C" int climsr_linear_dgrad(const uint16_t* dy, const uint16_t* w, int n,
   }
   hipStream_t s = (hipStream_t)stream;
   const int nf = (n + 15) / 16;
+  if (k % 128 == 0) {
+    dim3 gw(k / 128);
+    if (nf == 1) hipLaunchKernelGGL(linear_dgrad_wide_kernel<1>, gw, dim3(256), 0, s, dy, w, n, k, o, dx, accumulate);
+    else if (nf == 2) hipLaunchKernelGGL(linear_dgrad_wide_kernel<2>, gw, dim3(256), 0, s, dy, w, n, k, o, dx, accumulate);
+    else hipLaunchKernelGGL(linear_dgrad_wide_kernel<4>, gw, dim3(256), 0, s, dy, w, n, k, o, dx, accumulate);
+    return check_launch("linear_dgrad");
+  }
   dim3 grid(k / 64);
   if (nf == 1) hipLaunchKernelGGL(linear_dgrad_kernel<1>, grid, dim3(256), 0, s, dy, w, n, k, o, dx, accumulate);
   else if (nf == 2) hipLaunchKernelGGL(linear_dgrad_kernel<2>, grid, dim3(256), 0, s, dy, w, n, k, o, dx, accumulate);
