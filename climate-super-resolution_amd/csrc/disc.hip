@@ -1003,26 +1003,23 @@ __global__ __launch_bounds__(256) void linear_wgrad_kernel(const uint16_t* __res
   f32x4 acc[4];
 #pragma unroll
   for (int f = 0; f < 4; ++f) acc[f] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // A = x^T rows (k), B = dy^T columns (o): C[row = k (4g+i)][col = o], so a lane holds 4 consecutive k of one dW row
+  // and stores (and, accumulating, loads) them as one 16 B vector (the dy-as-A form wrote 4 B per lane, k floats apart)
   for (int nb = 0; nb < n_pad; nb += 32) {
-    bf16x8 af = *(const bf16x8*)(dyt + (long)(o0 + col) * n_pad + nb + g * 8);
+    const bf16x8 bo = *(const bf16x8*)(dyt + (long)(o0 + col) * n_pad + nb + g * 8);
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
-      bf16x8 bfr = *(const bf16x8*)(xt + (long)(k0 + f * 16 + col) * n_pad + nb + g * 8);
-      acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[f], 0, 0, 0);
+      const bf16x8 ak = *(const bf16x8*)(xt + (long)(k0 + f * 16 + col) * n_pad + nb + g * 8);
+      acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, bo, acc[f], 0, 0, 0);
     }
   }
-  // C: row = o (4g+i), col = k
-  float4 old[4][1];
-  (void)old;
+  float* row = dw + (long)(o0 + col) * k + k0 + g * 4;
+  float4 old[4];
 #pragma unroll
-  for (int f = 0; f < 4; ++f) {
-    const int kk = k0 + f * 16 + col;
+  for (int f = 0; f < 4; ++f) old[f] = accumulate ? *(const float4*)(row + f * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float* d = dw + (long)(o0 + g * 4 + i) * k + kk;
-      *d = (accumulate ? *d : 0.f) + acc[f][i];
-    }
-  }
+  for (int f = 0; f < 4; ++f)
+    *(float4*)(row + f * 16) = make_float4(old[f].x + acc[f][0], old[f].y + acc[f][1], old[f].z + acc[f][2], old[f].w + acc[f][3]);
 }
 
 extern "C" int climsr_linear_wgrad(const uint16_t* dy_t, const uint16_t* x_t, int n_pad, int k, int o, float* dw, int accumulate,
