@@ -140,7 +140,13 @@ def pmc_traffic(kernel, mode):
     FETCH_SIZE x2 gfx950 correction, MI355X_MICROARCH.md).  None if no summary covers it."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{mode}_pmc_traffic.json")))
+    import re
+
+    def build_key(path):  # r02_v11 after r02_v9: (round, version) as numbers, not as text
+        m = re.match(r"r(\d+)_v(\d+)_", os.path.basename(path))
+        return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{mode}_pmc_traffic.json")), key=build_key)
     if not files:
         return None, None
     f = files[-1]  # only the newest build's counters: an older build's bytes would describe other code
