@@ -554,13 +554,14 @@ def adaptive_pool_bwd(dp, n, h, w, c, oh, ow, dx):
 
 
 def linear_fwd(x, w, bias, n, k, o, y, ws, act=ACT_NONE, slope=0.2):
-    _run("linear_fwd_kernel", 2 * n * k * o, lambda: check(
+    # label = the kernel climsr_linear_fwd dispatches (o % 256 == 0: 64 weight rows per wave) + its split-K reduce
+    _run("linear_fwd_wide_kernel" if o % 256 == 0 else "linear_fwd_kernel", 2 * n * k * o, lambda: check(
         _L().climsr_linear_fwd(ptr(x), ptr(w), ptr(bias), n, k, o, act, slope, ptr(ws), ws.numel(), ptr(y), _lib.stream_ptr()),
         "linear_fwd"), "fwd fc.0")
 
 
 def linear_dgrad(dy, w, n, k, o, dx, accumulate=False):
-    _run("linear_dgrad_kernel", 2 * n * k * o, lambda: check(
+    _run("linear_dgrad_wide_kernel" if k % 128 == 0 else "linear_dgrad_kernel", 2 * n * k * o, lambda: check(
         _L().climsr_linear_dgrad(ptr(dy), ptr(w), n, k, o, ptr(dx), int(accumulate), _lib.stream_ptr()), "linear_dgrad"),
         "dgrad fc.0")
 
