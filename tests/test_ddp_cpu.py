@@ -244,3 +244,71 @@ def test_bench_main_without_world_size_launches(monkeypatch):
     monkeypatch.setattr(bench, "launch", lambda n, cmd, timeout=None: seen.update(n=n, cmd=cmd) or 0)
     assert bench.main(["--gpus", "8", "--steps", "3"]) == 0
     assert seen["n"] == 8 and seen["cmd"][-4:] == ["--gpus", "8", "--steps", "3"]
+
+
+# ------------------------------------------------------------------ world-2 step == single-process step
+def _dp_step_worker(rank, world, port, q):
+    """One data-parallel L1-pretrain step (config 4's algorithm, pl_generator_pre_training.py:18-33): each rank
+    takes its shard of the batch, its gradient goes through the real ESRGANGenerator flat layout and the
+    product's GradAllReducer, then AdamW.  The per-shard arithmetic is the fp64 oracle (the HIP kernels need a
+    GPU; their parity is the -m gpu suite) — what this checks is the data-parallel decomposition itself."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from climsr_amd.core.ddp import GradAllReducer, shard_indices
+        from climsr_amd.models.esrgan import ESRGANGenerator
+        from oracle import climsr_ref as ref
+        from tests.helpers import gen_params
+
+        nb, batch, hr = 1, 4, 32
+        p_ref = gen_params(nb, torch.float64)
+        g = ESRGANGenerator(in_channels=3, out_channels=1, nf=64, nb=nb, gc=16, scale_factor=4)
+        g.load_state_dict({k: v.float() for k, v in p_ref.items()})
+        g.grads_as_views()
+        keys = ref.trainable_keys(p_ref)
+        data = ref.synthetic_batch(batch, hr, dtype=torch.float64)
+
+        def grads_on(idx):
+            p = {k: v.clone().requires_grad_(k in keys) for k, v in p_ref.items()}
+            sr = ref.generator_forward(p, data["lr"][idx], data["elevation"][idx], data["mask"][idx], nb)
+            return ref._grads(ref.l1_loss(sr, data["hr"][idx]), p, keys)
+
+        shard = shard_indices(batch, rank, world)
+        local = grads_on(shard)
+        for name, prm in g.named_parameters():
+            prm.grad.copy_(local[name])
+        GradAllReducer(g)()
+        avg = {name: prm.grad.double().clone() for name, prm in g.named_parameters()}
+        full = grads_on(list(range(batch)))
+        num = sum(float((avg[k] - full[k]).norm() ** 2) for k in keys) ** 0.5
+        den = sum(float(full[k].norm() ** 2) for k in keys) ** 0.5
+        # one optimizer step from the averaged gradient vs the single-process step on the whole batch
+        p_dp = {k: v.clone() for k, v in p_ref.items()}
+        ref.AdamWState(p_dp, keys, 2e-4, 100).step(p_dp, avg)
+        p_sp = {k: v.clone() for k, v in p_ref.items()}
+        ref.pretrain_step(p_sp, ref.AdamWState(p_sp, keys, 2e-4, 100), data, nb)
+        dp_max = max(float((p_dp[k] - p_sp[k]).abs().max()) for k in keys)
+        q.put((rank, shard, num / den, dp_max, float(sum(avg[k].sum() for k in keys))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_step_equals_concatenated_batch():
+    """World-2 DP gradient (each rank's shard, averaged over gloo through the product reducer and the
+    generator's flat layout) equals the single-process gradient of the concatenated batch, and one AdamW step
+    from it lands on the single-process step's parameters (within fp32 rounding of the flat buffer)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_step_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, s0, rel0, dmax0, sum0), (_, s1, rel1, dmax1, sum1) = res
+    assert sorted(s0 + s1) == [0, 1, 2, 3] and not set(s0) & set(s1)
+    assert rel0 < 1e-6 and rel1 < 1e-6, (rel0, rel1)
+    assert dmax0 < 2e-4 * 1e-3 and dmax1 < 2e-4 * 1e-3, (dmax0, dmax1)  # << lr: same update direction
+    assert sum0 == sum1  # both ranks hold the identical averaged gradient
