@@ -8,10 +8,22 @@ whole buffer in one launch, and the data-parallel all-reduce sends it in a few l
 """
 from __future__ import annotations
 
-from typing import List, Tuple
+from typing import List, Optional, Tuple
 
 import torch
 import torch.nn as nn
+
+
+def ddp_forward_active() -> bool:
+    """True while a ``torch.nn.parallel.DistributedDataParallel`` forward runs (torch marks the wrapping module for the
+    duration of its ``_run_ddp_forward``): the native modules then hand their parameter gradients to autograd, whose
+    AccumulateGrad nodes fire DDP's reducer hooks (Lightning ``accelerator: ddp``, conf/trainer/benchmark.yaml:4)."""
+    try:
+        from torch.nn.parallel import DistributedDataParallel as DDP
+    except ImportError:  # pragma: no cover
+        return False
+    fn = getattr(DDP, "_get_active_ddp_module", None)
+    return (fn() if fn is not None else getattr(DDP, "_active_ddp_module", None)) is not None
 
 
 class FlatParamsMixin:
@@ -20,6 +32,12 @@ class FlatParamsMixin:
     _flat: torch.Tensor
     _flat_grad: torch.Tensor
     _flat_index: List[Tuple[nn.Parameter, int, int]]
+    # How a native backward delivers parameter gradients.  False: written in place into the flat gradient buffer that
+    # every ``param.grad`` views (one buffer for the fused AdamW / bucketed all-reduce; autograd sees no parameter
+    # gradient, so no AccumulateGrad node runs).  True: written into a fresh flat buffer whose views are returned to
+    # autograd (AccumulateGrad steals them when ``param.grad`` is None, adds them otherwise, and runs its hooks — what
+    # torch DDP's reducer needs).  None (default): True only inside a DistributedDataParallel forward.
+    grads_through_autograd: Optional[bool] = None
 
     def _flatten(self) -> None:
         params = [p for p in self.parameters()]
@@ -71,6 +89,27 @@ class FlatParamsMixin:
         if getattr(self, "_flat_index", None):
             self._ensure_flat()
         return ret
+
+    def _route_grads_through_autograd(self) -> bool:
+        """Decided at forward time (the node remembers it): see ``grads_through_autograd``."""
+        v = self.grads_through_autograd
+        return ddp_forward_active() if v is None else bool(v)
+
+    def _begin_autograd_grads(self):
+        """Point every ``param.grad`` at a fresh flat buffer for one native backward (overwrite semantics); returns
+        (buffer, the previous grads) for ``_end_autograd_grads``."""
+        buf = torch.empty_like(self._flat_grad)
+        saved = [p.grad for p, _o, _n in self._flat_index]
+        for p, off, n in self._flat_index:
+            p.grad = buf[off:off + n].view(p.shape)
+        return buf, saved
+
+    def _end_autograd_grads(self, buf, saved, needs) -> tuple:
+        """Restore the previous ``param.grad`` objects and return the fresh buffer's views (None where the parameter
+        needs no gradient), in flat order = the order the native Functions receive the parameters."""
+        for (p, _o, _n), g in zip(self._flat_index, saved):
+            p.grad = g
+        return tuple(buf[off:off + n].view(p.shape) if need else None for (p, off, n), need in zip(self._flat_index, needs))
 
     def grads_as_views(self) -> bool:
         """Point every param.grad at its slice of the flat grad buffer.  Returns True if they

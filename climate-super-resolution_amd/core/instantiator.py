@@ -53,7 +53,10 @@ class HydraInstantiator:
             from .optim import AdamW
 
             params = {k: v for k, v in cfg.items() if not k.startswith("_")}
-            return AdamW(model.parameters(), owner=model, **params)
+            odd = {k: v for k, v in params.items() if k in AdamW._UNSUPPORTED and v != AdamW._UNSUPPORTED[k]}
+            if not odd:
+                return AdamW(model.parameters(), owner=model, **params)
+            # options the fused update does not implement (maximize, foreach, fused, ...): torch's own AdamW + repack
         opt = self.instantiate(cfg, model.parameters())
         if native:
             step = opt.step

@@ -41,10 +41,18 @@ class AdamW(torch.optim.Optimizer):
     bf16 weight layouts are refreshed through ``owner.repack_weights()`` when given.
     """
 
+    # torch.optim.AdamW options this fused update does not implement: accepted only at their default value
+    _UNSUPPORTED = {"maximize": False, "foreach": None, "fused": None, "capturable": False, "differentiable": False}
+
     def __init__(self, params: Iterable, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 1e-2,
                  amsgrad: bool = False, owner=None, **kwargs):
         if amsgrad:
             raise ValueError("amsgrad is not supported")
+        for k, v in kwargs.items():
+            if k not in self._UNSUPPORTED:
+                raise TypeError(f"AdamW got an unexpected keyword argument {k!r}")
+            if v != self._UNSUPPORTED[k]:
+                raise ValueError(f"AdamW option {k}={v!r} is not supported by the fused update (only {self._UNSUPPORTED[k]!r})")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self.owner = owner
         self._hp = None

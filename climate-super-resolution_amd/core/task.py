@@ -108,10 +108,14 @@ class TaskSuperResolutionModule(_Base):
         ltb = t.limit_train_batches
         if isinstance(ltb, int) and ltb != 0:
             dataset_size = ltb
-        elif isinstance(ltb, float):  # a fraction of the batches
-            dataset_size = int(len(t.datamodule.train_dataloader()) * ltb)
         else:
-            dataset_size = len(t.datamodule.train_dataloader())
+            if getattr(t, "datamodule", None) is None:
+                raise ValueError("cannot infer the number of training steps: the trainer has no datamodule and "
+                                 f"limit_train_batches={ltb!r} is not a batch count; pass Trainer(num_training_steps=N), "
+                                 "Trainer(datamodule=...), an int limit_train_batches, or set the scheduler cfg's "
+                                 "num_training_steps")
+            n_batches = len(t.datamodule.train_dataloader())
+            dataset_size = int(n_batches * ltb) if isinstance(ltb, float) else n_batches  # float: a fraction
         num_devices = max(1, getattr(t, "num_gpus", 0) or 0, getattr(t, "num_processes", 0) or 0)
         if getattr(t, "tpu_cores", None):
             num_devices = max(num_devices, t.tpu_cores)

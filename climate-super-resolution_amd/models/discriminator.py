@@ -218,9 +218,9 @@ class _PlainDEngine:
 class _PlainDFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, box, *params):
-        engine, keep, need_pt = box
+        engine, keep, need_pt, via_autograd = box
         s, sv = engine.forward(x, keep, need_pt)
-        ctx.engine, ctx.sv = engine, sv
+        ctx.engine, ctx.sv, ctx.via_autograd = engine, sv, via_autograd
         return s
 
     @staticmethod
@@ -230,6 +230,11 @@ class _PlainDFn(torch.autograd.Function):
             raise RuntimeError("discriminator forward ran without saving activations")
         need_w = any(ctx.needs_input_grad[2:])
         need_x = ctx.needs_input_grad[0]
+        if need_w and ctx.via_autograd:  # torch DDP: the gradients go through AccumulateGrad (and the reducer's hooks)
+            buf, prev = engine.d._begin_autograd_grads()
+            dx = engine.backward(ds, sv, need_w, need_x, False)
+            ctx.sv = None
+            return (dx, None) + engine.d._end_autograd_grads(buf, prev, ctx.needs_input_grad[2:])
         acc = engine.d.grads_as_views() if need_w else True
         dx = engine.backward(ds, sv, need_w, need_x, acc)
         ctx.sv = None
@@ -281,4 +286,4 @@ class Discriminator(FlatParamsMixin, nn.Module):
         grad_on = torch.is_grad_enabled()
         need_w = grad_on and any(p.requires_grad for p in params)
         keep = grad_on and (need_w or x.requires_grad)
-        return _PlainDFn.apply(x, (eng, keep, need_w), *params)
+        return _PlainDFn.apply(x, (eng, keep, need_w, need_w and self._route_grads_through_autograd()), *params)

@@ -172,8 +172,11 @@ class _Engine:
             self.pull_packer_rest.run()
         self.version = self.gen._flat._version
 
-    def chain_ok(self, w: int) -> bool:
-        return bool(self.chains) and w % 16 == 0 and w <= 64
+    def chain_ok(self, w: int, n: int = 1, h: int = 1) -> bool:
+        """The fused conv1-4 launch takes widths 16/32/48/64 and buffers under 2 GiB (its 32-bit buffer offsets:
+        climsr_rdb_chain rejects larger ones; the pull reads the dense buffer as its activation mask, same size);
+        anything else runs conv by conv."""
+        return bool(self.chains) and w % 16 == 0 and w <= 64 and n * h * w * self.dc * 2 < (1 << 31)
 
     def rdb_name(self, i, r, c):
         return f"RRDB_trunk.{i}.RDB{r}.conv{c}"
@@ -216,7 +219,7 @@ class _Engine:
             dst = dense[i + 1] if keep else dense[(i + 1) % 2]
             if r == 0 and not keep:  # remember the RRDB input for its residual
                 axpby_bf16_copy(src, rrdb_in, n * h * w, nf, dc)
-            if self.chain_ok(w):
+            if self.chain_ok(w, n, h):
                 self.chains[i].forward(src, dc, n, h, w)
             else:
                 for c in range(1, 5):
@@ -324,7 +327,7 @@ class _Engine:
             g_out, g_in, g_skip = G[(i + 1) % 4], G[i % 4], G[(3 * blk + 3) % 4]
             dz, src, pulls = dZ[i % 2], dense[i], self.pulls[i]
             # dZ_j = lrelu'(x_j) * sum_{k>j} conv_k^T(dZ_k)   (x_j = channels nf+(j-1)gc.. of the dense buffer)
-            if self.chain_ok(w):
+            if self.chain_ok(w, n, h):
                 self.chains[i].pull(dz, src, dc, n, h, w)
             else:
                 if self.chains and not self.pull_rest_on:
@@ -364,10 +367,11 @@ def axpby_bf16_copy(src, dst, npix, c, src_cs):
 class _GeneratorFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, elev, mask, engine_box, *params):
-        engine, keep = engine_box  # grad mode is off inside Function.forward: decided by the caller
+        engine, keep, via_autograd = engine_box  # grad mode is off inside Function.forward: decided by the caller
         out, saved = engine.forward(x, elev, mask, keep=keep)
         ctx.engine = engine
         ctx.saved = saved
+        ctx.via_autograd = via_autograd
         return out
 
     @staticmethod
@@ -378,6 +382,12 @@ class _GeneratorFn(torch.autograd.Function):
         if ctx.saved is None:
             raise RuntimeError("generator forward ran without saving activations")
         gen = engine.gen
+        if ctx.via_autograd:  # torch DDP: the gradients go through AccumulateGrad (and the reducer's hooks)
+            buf, prev = gen._begin_autograd_grads()
+            engine.bind_grads()
+            engine.backward(gout, ctx.saved, accumulate=False)
+            ctx.saved = None
+            return (None, None, None, None) + gen._end_autograd_grads(buf, prev, ctx.needs_input_grad[4:])
         acc = gen.grads_as_views()
         engine.bind_grads()
         engine.backward(gout, ctx.saved, accumulate=acc)
@@ -441,7 +451,7 @@ class ESRGANGenerator(FlatParamsMixin, nn.Module):
         eng = self.engine()
         params = self._flat_params()
         keep = torch.is_grad_enabled() and any(p.requires_grad for p in params)
-        return _GeneratorFn.apply(x, elev, mask, (eng, keep), *params)
+        return _GeneratorFn.apply(x, elev, mask, (eng, keep, keep and self._route_grads_through_autograd()), *params)
 
     def _flat_params(self) -> List[nn.Parameter]:
         return [p for p, _o, _n in self._flat_index]

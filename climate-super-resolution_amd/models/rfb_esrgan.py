@@ -191,10 +191,10 @@ class _DEngine:
                 plan.wgrad(L["a_in"], L["cs_in"], 0, L["h_in"], L["w_in"], dz, cz, n, self.ws, acc)
             if li > 0 or need_x:
                 prev_bn = self.layers[li - 1][1] if li > 0 else None
-                if li == 1 and prev_bn is None and plan.cin % 8 == 0:
-                    # layer 0 has no BN: its LeakyReLU' (from its stored bf16 activation) goes into this data
-                    # gradient's epilogue, which writes layer 0's bf16 output gradient
-                    P0 = sv["layers"][0]
+                if prev_bn is None and li > 0:
+                    # the previous layer has no BN (layer 0): its LeakyReLU' (from its stored bf16 activation) goes
+                    # into this data gradient's epilogue, which writes that layer's bf16 output gradient
+                    P0 = sv["layers"][li - 1]
                     g = _bf16((n, L["h_in"], L["w_in"], plan.cin), dev)
                     plan.dgrad(dz, cz, oh, ow, g, plan.cin, 0, n, act=ACT_LRELU_BWD, res1=P0["a"], res1_cs=plan.cin, res1_co=0)
                     dz_next = g
@@ -214,9 +214,9 @@ class _DEngine:
 class _DFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, box, *params):
-        engine, keep, need_pt = box
+        engine, keep, need_pt, via_autograd = box
         s, sv = engine.forward(x, keep, need_pt)
-        ctx.engine, ctx.sv = engine, sv
+        ctx.engine, ctx.sv, ctx.via_autograd = engine, sv, via_autograd
         return s
 
     @staticmethod
@@ -226,6 +226,11 @@ class _DFn(torch.autograd.Function):
             raise RuntimeError("discriminator forward ran without saving activations")
         need_w = any(ctx.needs_input_grad[2:])
         need_x = ctx.needs_input_grad[0]
+        if need_w and ctx.via_autograd:  # torch DDP: the gradients go through AccumulateGrad (and the reducer's hooks)
+            buf, prev = engine.d._begin_autograd_grads()
+            dx = engine.backward(ds, sv, need_w, need_x, False)
+            ctx.sv = None
+            return (dx, None) + engine.d._end_autograd_grads(buf, prev, ctx.needs_input_grad[2:])
         acc = engine.d.grads_as_views() if need_w else True
         dx = engine.backward(ds, sv, need_w, need_x, acc)
         ctx.sv = None
@@ -321,4 +326,4 @@ class RFBESRGANDiscriminator(FlatParamsMixin, nn.Module):
         grad_on = torch.is_grad_enabled()
         need_w = grad_on and any(p.requires_grad for p in params)
         keep = grad_on and (need_w or input.requires_grad)
-        return _DFn.apply(input, (eng, keep, need_w), *params)
+        return _DFn.apply(input, (eng, keep, need_w, need_w and self._route_grads_through_autograd()), *params)

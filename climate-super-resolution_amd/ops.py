@@ -309,6 +309,8 @@ class Workspace:
 
 def act_grad(npix: int, c_real: int, g: torch.Tensor, g_cs: int, g_co: int, y: Optional[torch.Tensor], y_cs: int, y_co: int,
              act: int, dz: torch.Tensor, dz_cs: int, scale: float = 1.0, slope: float = 0.2) -> None:
+    if g.dtype != torch.float32:  # the C ABI reads `const float* g`
+        raise TypeError(f"act_grad: the incoming gradient must be float32, got {g.dtype}")
     _launch("act_grad", lambda: _lib.load().climsr_act_grad(npix, c_real, ptr(g), g_cs, g_co, ptr(y), y_cs, y_co, act, slope, scale, ptr(dz), dz_cs,
                                       _lib.stream_ptr()))
 

@@ -65,3 +65,40 @@ def ssim(a, b, data_range=None, kernel=11, sigma=1.5):
     sab = f(a * b) - mu_a * mu_b
     m = ((2 * mu_a * mu_b + c1) * (2 * sab + c2)) / ((mu_a ** 2 + mu_b ** 2 + c1) * (saa + sbb + c2))
     return float(m.mean())
+
+
+def gemm_conv(p, name, x, stride=1, padding=None):
+    """The oracle's conv (oracle/climsr_ref.py _conv) as unfold + matmul: rocBLAS GEMMs instead of MIOpen (whose per-shape
+    kernel compilation on a fresh box takes minutes).  Same math, autocast-able.  Test-only (monkeypatched in)."""
+    import torch.nn.functional as F
+
+    w = p[name + ".weight"]
+    b = p.get(name + ".bias")
+    ks = w.shape[-1]
+    pad = ks // 2 if padding is None else padding
+    n, _c, h, wd = x.shape
+    oh, ow = (h + 2 * pad - ks) // stride + 1, (wd + 2 * pad - ks) // stride + 1
+    cols = F.unfold(x, ks, padding=pad, stride=stride)
+    y = torch.matmul(w.reshape(w.shape[0], -1), cols)
+    if b is not None:
+        y = y + b.reshape(1, -1, 1).to(y.dtype)
+    return y.reshape(n, w.shape[0], oh, ow)
+
+
+def rel_l2(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / (b.norm() + 1e-30))
+
+
+def update_envelope(native, ref64, amps, floor=2e-2):
+    """Per tensor: the relative L2 distance of the native update (or gradient) from the fp64 oracle's must stay within
+    2x the larger distance of the oracle's own torch-autocast fp16 / bf16 runs from the same state (the reference
+    trains with precision 16), or ``floor``.  Returns (offenders, worst ratio, per-tensor table)."""
+    rows = {}
+    for k, want in ref64.items():
+        rel = rel_l2(native[k], want)
+        rel_amp = max(rel_l2(a[k], want) for a in amps)
+        rows[k] = (rel, rel_amp)
+    bad = [(k, round(r, 4), round(ra, 4)) for k, (r, ra) in rows.items() if r > max(2.0 * ra, floor)]
+    worst = max(rows.items(), key=lambda kv: kv[1][0] / max(2.0 * kv[1][1], floor))
+    return bad, worst, rows

@@ -312,3 +312,92 @@ def test_gloo_world2_step_equals_concatenated_batch():
     assert rel0 < 1e-6 and rel1 < 1e-6, (rel0, rel1)
     assert dmax0 < 2e-4 * 1e-3 and dmax1 < 2e-4 * 1e-3, (dmax0, dmax1)  # << lr: same update direction
     assert sum0 == sum1  # both ranks hold the identical averaged gradient
+
+
+def test_bench_launcher_times_out_hung_rank():
+    """A rank that never exits is killed at the launcher's limit (exit 124) instead of hanging the run."""
+    import sys
+    import time
+
+    import bench
+
+    assert bench.launch.__defaults__[0] == bench.LAUNCH_TIMEOUT_S and bench.LAUNCH_TIMEOUT_S > 0  # on by default
+    code = "import time; time.sleep(120)"
+    t0 = time.time()
+    assert bench.launch(2, [sys.executable, "-c", code], timeout=3) == 124
+    assert time.time() - t0 < 30
+
+
+# ------------------------------------------------------------------ world-2 GAN discriminator pass
+def _gan_d_worker(rank, world, port, q):
+    """The D pass of one GAN step (pl_gan.py:51-61 loss_d, then AdamW_D) as Lightning DDP runs it: each rank takes
+    its shard, D's BatchNorms use the shard's batch statistics (no SyncBN, conf/trainer/default.yaml:31) and the
+    relativistic means are over the shard; the per-rank D gradients (fp64 oracle arithmetic; the HIP kernels need a
+    GPU) are written into the real RFBESRGANDiscriminator flat gradient buffer and averaged by the product's
+    overlapped reducer with the slices D's backward reports (fc first, then the rest)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from climsr_amd.core.ddp import OverlappedGradAllReducer, shard_indices
+        from climsr_amd.models.rfb_esrgan import RFBESRGANDiscriminator
+        from oracle import climsr_ref as ref
+        from tests.helpers import rfb_d_params
+
+        torch.set_num_threads(2)
+        batch, hr = 4, 32
+        p0 = rfb_d_params(torch.float64)
+        keys = ref.trainable_keys(p0)
+        data = ref.synthetic_batch(batch, hr, seed=9, dtype=torch.float64)
+        sr_all = torch.tanh(torch.randn((batch, 1, hr, hr), generator=torch.Generator().manual_seed(11), dtype=torch.float64))
+
+        def d_pass(idx):
+            p = {k: (v.clone().requires_grad_(k in keys) if v.is_floating_point() else v.clone()) for k, v in p0.items()}
+            ld = ref.loss_d(lambda t: ref.rfb_discriminator_forward(p, t, training=True), data["hr"][idx], sr_all[idx])
+            grads = ref._grads(ld, p, keys)
+            stats = torch.cat([p[pre + ".running_mean"] for pre in ref.rfb_bn_prefixes()]).detach()
+            return float(ld), grads, stats
+
+        shard = shard_indices(batch, rank, world)
+        loss, local, stats = d_pass(shard)
+        d = RFBESRGANDiscriminator(in_channels=1)
+        d.grads_as_views()
+        for k, prm in d.named_parameters():
+            prm.grad.copy_(local[k])
+        ov = OverlappedGradAllReducer(d)
+        ov.ready(d._fc_flat_lo())
+        ov.finish()
+        avg = {k: prm.grad.double().clone() for k, prm in d.named_parameters()}
+        # expected: the mean of the two shards' gradients, each with its own BN statistics (computed here in one process)
+        shards = [shard_indices(batch, r, world) for r in range(world)]
+        per = [d_pass(s) for s in shards]
+        want = {k: sum(pp[1][k] for pp in per) / world for k in keys}
+        whole = d_pass(list(range(batch)))[1]
+
+        def rel(a, b):
+            num = sum(float((a[k] - b[k]).norm() ** 2) for k in keys) ** 0.5
+            return num / (sum(float(b[k].norm() ** 2) for k in keys) ** 0.5)
+
+        q.put((rank, shard, loss, rel(avg, want), rel(want, whole), stats, per[rank][2], list(ov.launched)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_gan_discriminator_pass():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gan_d_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=600) for _ in procs), key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, shard, loss, rel_avg, rel_whole, stats, stats_check, launched in res:
+        assert rel_avg < 1e-6, (rank, rel_avg)  # product reducer + D flat layout: the average of the per-shard gradients
+        assert rel_whole > 1e-3, (rank, rel_whole)  # per-rank BN statistics: not the whole-batch (SyncBN) gradient
+        assert torch.equal(stats, stats_check)
+        assert len(launched) == 2 and launched[0][1] - launched[0][0] == 1024 * 100352 + 1024 + 1024 + 1
+    assert res[0][1] == [0, 2] and res[1][1] == [1, 3]
+    assert not torch.allclose(res[0][5], res[1][5])  # each rank's running statistics follow its own shard
+    assert res[0][2] != res[1][2]  # and so do the per-rank losses

@@ -20,7 +20,7 @@ import pytest
 import torch
 
 from oracle import climsr_ref as ref
-from tests.helpers import gen_params, psnr
+from tests.helpers import gemm_conv, gen_params, psnr, update_envelope
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -30,7 +30,7 @@ ONE_CYCLE_YAML = {"_target_": "torch.optim.lr_scheduler.OneCycleLR", "max_lr": 1
                   "pct_start": 0.05, "div_factor": 2, "final_div_factor": 100}
 
 
-def test_config1_trainer_steps_vs_golden(golden_dir):
+def test_config1_trainer_steps_vs_golden(golden_dir, monkeypatch):
     from climsr_amd.core.trainer import Trainer
     from climsr_amd.task.pl_generator_pre_training import SuperResolutionLightningModule
 
@@ -71,18 +71,31 @@ def test_config1_trainer_steps_vs_golden(golden_dir):
     print("config-1 worst per-tensor |dsum|/n/lr", ws, "|dnorm|/sqrt(n)/lr", wn)
     assert ws[1] <= 0.25, ws
     assert wn[1] <= 0.25, wn
-    # full update vectors vs the fp64 oracle's three steps from the same state (CPU, test-only)
+    # full update vectors vs the fp64 oracle's three steps from the same state (CPU, test-only), per tensor within 2x the
+    # deviation of the oracle's own autocast fp16 / bf16 three steps (the reference trains with precision 16)
     torch.set_num_threads(min(16, os.cpu_count() or 1))
-    q = {k: v.clone() for k, v in before.items()}
-    opt64 = ref.AdamWState(q, list(q.keys()), lr=lr, total_steps=want["total_steps"])
-    for s in want["seeds"]:
-        ref.pretrain_step(q, opt64, ref.synthetic_batch(b, hr, seed=s, dtype=torch.float64), nb)
-    rels = {k: float((p.detach().double().cpu() - before[k] - (q[k] - before[k])).norm() / ((q[k] - before[k]).norm() + 1e-30))
-            for k, p in m.generator.named_parameters()}
-    worst = max(rels.items(), key=lambda kv: kv[1])
-    med = float(np.median(list(rels.values())))
-    print("config-1 update-vector rel L2: worst", worst, "median", med)
-    assert worst[1] <= 0.75 and med <= 0.25, (worst, med)
+
+    def oracle_update(dev, dtype, autocast=None):
+        q = {k: v.clone().to(dev, dtype) for k, v in before.items()}
+        opt64 = ref.AdamWState(q, list(q.keys()), lr=lr, total_steps=want["total_steps"])
+        for s in want["seeds"]:
+            bt = {k: v.to(dev, dtype) for k, v in ref.synthetic_batch(b, hr, seed=s, dtype=torch.float64).items()}
+            if autocast is None:
+                ref.pretrain_step(q, opt64, bt, nb)
+            else:
+                with torch.autocast("cuda", dtype=autocast):
+                    ref.pretrain_step(q, opt64, bt, nb)
+        return {k: q[k].double().cpu() - before[k] for k in before}
+
+    upd64 = oracle_update("cpu", torch.float64)
+    monkeypatch.setattr(ref, "_conv", gemm_conv)  # rocBLAS GEMMs on the GPU (no MIOpen per-shape compiles)
+    torch.backends.cuda.matmul.allow_tf32 = False
+    amps = [oracle_update(DEV, torch.float32, dt) for dt in (torch.float16, torch.bfloat16)]
+    native = {k: p.detach().double().cpu() - before[k] for k, p in m.generator.named_parameters()}
+    bad, worst, rows = update_envelope(native, upd64, amps)
+    rels = sorted(r for r, _ra in rows.values())
+    print("config-1 update-vector rel L2 vs fp64: worst", worst, "median", rels[len(rels) // 2], flush=True)
+    assert not bad, f"{len(bad)} tensors outside 2x the autocast deviation: {bad[:8]}"
 
 
 def _grid(h, w, seed=42):

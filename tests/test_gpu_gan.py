@@ -11,7 +11,7 @@ import pytest
 import torch
 
 from oracle import climsr_ref as ref
-from tests.helpers import gen_params, rfb_d_params, vgg_params
+from tests.helpers import gemm_conv, gen_params, rfb_d_params, update_envelope, vgg_params
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -115,7 +115,7 @@ def test_perceptual_loss_vs_oracle_and_properties():
     assert abs(got - want) <= 2e-2 * abs(want), (got, want)
 
 
-def test_gan_step_vs_golden(golden_dir):
+def test_gan_step_vs_golden(golden_dir, monkeypatch):
     """One full GAN training step (G pass + AdamW_G, D pass with a fresh G forward + AdamW_D,
     both OneCycleLR steps) through the native task vs the reference-module fixture."""
     want = json.load(open(os.path.join(golden_dir, "gan_step.json")))
@@ -158,35 +158,48 @@ def test_gan_step_vs_golden(golden_dir):
     assert ws[1][0] <= GAN_SUM_TOL, ("per-element mean update mismatch", ws)
     assert wn[1][1] <= GAN_NORM_TOL, ("per-element norm mismatch", wn)
     # and the full update vectors vs the fp64 oracle step from the same state (oracle.gan_step, CPU)
-    _update_vectors_vs_oracle(m, g_before, d_before, bt, lr)
+    _update_vectors_vs_oracle(m, g_before, d_before, bt, lr, monkeypatch)
 
 
 GAN_SUM_TOL = 0.25   # x lr, per tensor (Adam's first step moves every element by ~lr; a sign flip moves it by 2 lr)
 GAN_NORM_TOL = 0.25  # x lr, per tensor, on |norm| / sqrt(numel)
-# rel L2 of a tensor's update vector (native vs the fp64 oracle step).  Adam's first step is ~lr * sign(grad), so
-# elements whose gradient sits inside the bf16 noise flip sign (a 2 lr change each): at this perceptual-loss-dominated
-# golden step the reference's own AMP gradients are ~0.3-0.4 rel L2 off fp64, and ~4 % of the elements flip (measured
-# worst 0.71, median 0.42 on MI355X).  An uncorrelated update would be at sqrt(2) = 1.41, a sign-reversed one at 2.
-UPD_REL_TOL = 1.0
-UPD_REL_MEDIAN = 0.6
 
 
-def _update_vectors_vs_oracle(m, g_before, d_before, bt, lr):
-    gp = {k: v.clone() for k, v in g_before.items()}
-    dp = {k: (v.clone() if v.is_floating_point() else v) for k, v in rfb_d_params(torch.float64).items()}
-    dp.update({k: v.clone() for k, v in d_before.items()})
-    vp = vgg_params(torch.float64)
+def _oracle_gan_update(g_before, d_before, bt, lr, dev, dtype, autocast=None):
+    """The oracle's GAN step (oracle.gan_step: G pass + AdamW_G, D pass + AdamW_D, both schedulers) from the same state:
+    fp64 on the CPU, or fp32 on the GPU under torch.autocast(dtype) -- the reference's precision-16 training and
+    torch's bf16 autocast, the yardstick for how far reduced precision moves this step.  Returns the update vectors."""
+    gp = {k: v.clone().to(dev, dtype) for k, v in g_before.items()}
+    dp = {k: (v.clone().to(dev, dtype) if v.is_floating_point() else v.clone().to(dev)) for k, v in rfb_d_params(torch.float64).items()}
+    dp.update({k: v.clone().to(dev, dtype) for k, v in d_before.items()})
+    vp = {k: v.to(dev, dtype) for k, v in vgg_params(torch.float64).items()}
     opt_g = ref.AdamWState(gp, list(gp.keys()), lr=lr, total_steps=10)
     opt_d = ref.AdamWState(dp, ref.trainable_keys(dp), lr=lr, total_steps=10)
-    b64 = {k: v.double().cpu() for k, v in bt.items()}
-    ref.gan_step(gp, dp, vp, opt_g, opt_d, b64, 1)
-    rels = {}
-    for net, before, after in ((m.generator, g_before, gp), (m.discriminator, d_before, dp)):
+    b = {k: v.to(dev, dtype) for k, v in bt.items()}
+    if autocast is None:
+        ref.gan_step(gp, dp, vp, opt_g, opt_d, b, 1)
+    else:
+        with torch.autocast("cuda", dtype=autocast):
+            ref.gan_step(gp, dp, vp, opt_g, opt_d, b, 1)
+    upd = {k: gp[k].double().cpu() - g_before[k] for k in g_before}
+    upd.update({k: dp[k].double().cpu() - d_before[k] for k in d_before})
+    return upd
+
+
+def _update_vectors_vs_oracle(m, g_before, d_before, bt, lr, monkeypatch=None):
+    """Per tensor, the native update vector vs the fp64 oracle step from the same state, bounded by 2x the deviation of
+    the oracle's own autocast fp16 / bf16 steps (floor 2e-2).  Adam's first step is ~lr * sign(grad), so elements whose
+    gradient sits inside the reduced-precision noise flip sign in the AMP runs as in ours."""
+    upd64 = _oracle_gan_update(g_before, d_before, bt, lr, "cpu", torch.float64)
+    if monkeypatch is not None:
+        monkeypatch.setattr(ref, "_conv", gemm_conv)  # rocBLAS GEMMs on the GPU (no MIOpen per-shape compiles)
+    torch.backends.cuda.matmul.allow_tf32 = False
+    amps = [_oracle_gan_update(g_before, d_before, bt, lr, DEV, torch.float32, dt) for dt in (torch.float16, torch.bfloat16)]
+    native = {}
+    for net, before in ((m.generator, g_before), (m.discriminator, d_before)):
         for k, p in net.named_parameters():
-            dn = p.detach().double().cpu() - before[k]
-            dr = after[k] - before[k]
-            rels[k] = float((dn - dr).norm() / (dr.norm() + 1e-30))
-    worst = max(rels.items(), key=lambda kv: kv[1])
-    med = float(np.median(list(rels.values())))
-    print("gan step update-vector rel L2: worst", worst, "median", med)
-    assert worst[1] <= UPD_REL_TOL and med <= UPD_REL_MEDIAN, (worst, med)
+            native[k] = p.detach().double().cpu() - before[k]
+    bad, worst, rows = update_envelope(native, upd64, amps)
+    rels = sorted(r for r, _ra in rows.values())
+    print("gan step update-vector rel L2 vs fp64: worst", worst, "median", rels[len(rels) // 2], flush=True)
+    assert not bad, f"{len(bad)} tensors outside 2x the autocast deviation: {bad[:8]}"

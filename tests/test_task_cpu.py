@@ -121,3 +121,29 @@ def test_scheduler_rejects_other_libraries():
     opt = torch.optim.SGD([torch.nn.Parameter(torch.ones(1))], lr=0.1)
     with pytest.raises(ValueError):
         HydraInstantiator().scheduler({"_target_": "mylib.Sched", "num_training_steps": 1, "num_warmup_steps": 0}, opt)
+
+
+def test_builtin_trainer_without_steps_or_datamodule_explains():
+    """Trainer(module) with neither num_training_steps, a datamodule nor an int limit_train_batches: a clear error
+    naming the missing configuration (not an AttributeError on None)."""
+    from climsr_amd.core.trainer import Trainer
+
+    with pytest.raises(ValueError, match="num_training_steps"):
+        Trainer(_gan())
+
+
+def test_adamw_rejects_options_it_does_not_implement():
+    from climsr_amd.core.instantiator import HydraInstantiator
+    from climsr_amd.core.optim import AdamW
+    from climsr_amd.models.esrgan import ESRGANGenerator
+
+    g = ESRGANGenerator(in_channels=3, out_channels=1, nf=64, nb=1, gc=16)
+    with pytest.raises(ValueError, match="maximize"):
+        AdamW(g.parameters(), lr=1e-4, maximize=True)
+    with pytest.raises(TypeError, match="bogus"):
+        AdamW(g.parameters(), lr=1e-4, bogus=1)
+    assert isinstance(AdamW(g.parameters(), lr=1e-4, maximize=False, foreach=None), AdamW)  # defaults are fine
+    # through the instantiator a torch.optim.AdamW cfg with such an option falls back to torch's AdamW (+ repack)
+    opt = HydraInstantiator().optimizer(g, dict(ADAMW_YAML, maximize=True))
+    assert type(opt) is torch.optim.AdamW and opt.param_groups[0]["maximize"] is True
+    assert isinstance(HydraInstantiator().optimizer(g, dict(ADAMW_YAML)), AdamW)
