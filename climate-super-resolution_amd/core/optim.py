@@ -81,6 +81,15 @@ class AdamW(torch.optim.Optimizer):
             flat = _flat_owner(group["params"]) if len(params) == len(group["params"]) else None
             if flat is not None:
                 gflat = _flat_owner([p.grad for p in group["params"]])
+                own = self.owner
+                if gflat is None and own is not None and getattr(own, "_flat", None) is not None and \
+                        own._flat.data_ptr() == flat.data_ptr() and own._flat.numel() == flat.numel():
+                    # gradients delivered through autograd as separate tensors (torch DDP; a module called twice sums
+                    # its nodes' gradients out of place): gather them into the module's flat gradient buffer (one
+                    # multi-tensor copy) and keep the one-launch update
+                    views = [own._flat_grad[off:off + n].view(p.shape) for p, off, n in own._flat_index]
+                    torch._foreach_copy_(views, [p.grad for p in group["params"]])
+                    gflat = own._flat_grad
                 if gflat is None:
                     flat = None
             if flat is not None:

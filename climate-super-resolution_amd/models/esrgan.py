@@ -206,19 +206,22 @@ class _Engine:
         else:
             lr = torch.zeros((n, h, w, self.cin_pad), dtype=torch.bfloat16, device=dev)
             nchw_to_nhwc(x, lr, self.cin_pad, 0)
-        ndense = 3 * nb + 1 if keep else 2
+        # keep (training): every RDB's dense buffer is saved for the backward.  No-grad: a ring of three -- RDB i
+        # reads ring[i % 3] and writes ring[(i + 1) % 3], so an RRDB's input ring[3 blk % 3] is still intact when its
+        # third RDB's conv5 adds it (esrgan.py:54) and writes the result over it in place (the epilogue reads each
+        # residual element before the same lane stores that element; conv5's conv input is another buffer)
+        ndense = 3 * nb + 1 if keep else 3
         dense = [_bf16((n, h, w, dc), dev) for _ in range(ndense)]
-        rrdb_in = _bf16((n, h, w, nf), dev) if not keep else None
-        P["conv_first"].fwd(lr, self.cin_pad, 0, h, w, dense[0], dc, 0, n)
-        fea = dense[0] if keep else _bf16((n, h, w, nf), dev)
-        if not keep:  # keep a copy of fea for the global skip (dense[0] is recycled)
-            P["conv_first"].fwd(lr, self.cin_pad, 0, h, w, fea, nf, 0, n)
+        if keep:
+            P["conv_first"].fwd(lr, self.cin_pad, 0, h, w, dense[0], dc, 0, n)
+            fea = dense[0]
+        else:  # fea (kept for the global skip, esrgan.py:91) and the first RDB's input in one launch (aux output)
+            fea = _bf16((n, h, w, nf), dev)
+            P["conv_first"].fwd(lr, self.cin_pad, 0, h, w, fea, nf, 0, n, aux=dense[0], aux_cs=dc, aux_co=0)
         for i in range(3 * nb):
             blk, r = divmod(i, 3)
-            src = dense[i] if keep else dense[i % 2]
-            dst = dense[i + 1] if keep else dense[(i + 1) % 2]
-            if r == 0 and not keep:  # remember the RRDB input for its residual
-                axpby_bf16_copy(src, rrdb_in, n * h * w, nf, dc)
+            src = dense[i] if keep else dense[i % 3]
+            dst = dense[i + 1] if keep else dense[(i + 1) % 3]
             if self.chain_ok(w, n, h):
                 self.chains[i].forward(src, dc, n, h, w)
             else:
@@ -226,10 +229,10 @@ class _Engine:
                     P[self.rdb_name(blk, r + 1, c)].fwd(src, dc, 0, h, w, src, dc, nf + (c - 1) * gc, n, act=ACT_LRELU)
             res2 = None
             if r == 2:
-                res2 = dense[3 * blk] if keep else rrdb_in
+                res2 = dense[3 * blk] if keep else dense[(3 * blk) % 3]  # no-grad: == dst (in place)
             P[self.rdb_name(blk, r + 1, 5)].fwd(src, dc, 0, h, w, dst, dc, 0, n, res1=src, alpha1=0.2, res1_cs=dc, res1_co=0,
-                                                 res2=res2, alpha2=0.2, res2_cs=(dc if keep else nf), res2_co=0)
-        last = dense[3 * nb] if keep else dense[(3 * nb) % 2]
+                                                 res2=res2, alpha2=0.2, res2_cs=dc, res2_co=0)
+        last = dense[3 * nb] if keep else dense[(3 * nb) % 3]
         fea2 = _bf16((n, h, w, nf), dev)
         P["trunk_conv"].fwd(last, dc, 0, h, w, fea2, nf, 0, n, res1=fea, alpha1=1.0, res1_cs=(dc if keep else nf), res1_co=0)
         u1 = _bf16((n, h2, w2, nf), dev)
@@ -357,11 +360,6 @@ class _Engine:
         axpby(npx_lr, nf, 1.0, g_fea2, nf, 0, 1.0, G[0], nf, 0)
         act_grad(npx_lr, nf, G[0], nf, 0, None, 0, 0, ACT_NONE, dz64, nf)
         P["conv_first"].wgrad(sv["lr"], self.cin_pad, 0, h, w, dz64, nf, n, ws, acc)
-
-
-def axpby_bf16_copy(src, dst, npix, c, src_cs):
-    """Copy channels [0, c) of an NHWC bf16 buffer (inference path only)."""
-    dst.copy_(src.view(-1, src_cs)[:, :c].reshape(dst.shape))
 
 
 class _GeneratorFn(torch.autograd.Function):
