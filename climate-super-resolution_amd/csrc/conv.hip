@@ -652,10 +652,15 @@ __device__ __forceinline__ void conv_fwd_body(const FwdArgs& a) {
 #pragma unroll
       for (int k = 0; k < 9; ++k) {
         if (k + 1 < 9) ld(k + 1, (k + 1) & 1);
+        // the next k-step's NT + MW fragment reads go out as one burst ahead of this k-step's MW x NT MFMAs (the
+        // compiler otherwise sinks each read next to its first MFMA and waits lgkmcnt(0) there: the LDS latency was
+        // exposed at nearly every k-step of the unrolled loop)
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int m = 0; m < MW; ++m)
 #pragma unroll
           for (int t = 0; t < NT; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k & 1][t], bf[k & 1][m], acc[m][t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
       }
       return;
     }

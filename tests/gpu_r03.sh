@@ -13,7 +13,7 @@ has() { [[ " $STEPS " == *" $1 "* ]]; }
 run() {  # name, limit, command...
   local name=$1 lim=$2
   shift 2
-  echo "[gpu_r03] $name ($(date +%T))"
+  echo "[gpu_r03] $name ($(date +%T))" >&2
   timeout -k 10 "$lim" "$@"
 }
 set -o pipefail
