@@ -1581,10 +1581,12 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_pw_kernel(FwdArgs a) {
 #pragma unroll
         for (int k = 0; k < 18; ++k) {
           if (k + 1 < 18) ldk(k + 1, (k + 1) & 1);
+          __builtin_amdgcn_sched_barrier(0);  // the next k-step's reads as one burst ahead of this k-step's MFMAs
 #pragma unroll
           for (int m = 0; m < MW; ++m)
 #pragma unroll
             for (int t = 0; t < NT; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k & 1][t], bf[k & 1][m], acc[m][t], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
         }
       } else {
       const int nks = a.kcpad / 32;
@@ -2391,19 +2393,25 @@ __global__ __launch_bounds__(512) void conv_fwd_s2_kernel(FwdArgs a) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[b][t], bf[b][m], acc[m][t], 0, 0, 0);
     };
+    // each tap's fragment reads go out as one burst ahead of the previous tap's MFMAs (sched_barrier: the compiler
+    // otherwise sinks every read next to its first use and waits for it there)
     if (h == 0) {
       ld(0, 0);
 #pragma unroll
       for (int k = 0; k < 5; ++k) {
         if (k + 1 < 5) ld(k + 1, (k + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
         mm(k & 1);
+        __builtin_amdgcn_sched_barrier(0);
       }
     } else {
       ld(5, 0);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         if (k + 1 < 4) ld(6 + k, (k + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
         mm(k & 1);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
   };
