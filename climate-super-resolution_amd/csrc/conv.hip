@@ -3072,7 +3072,8 @@ struct W64 {
   static constexpr int XP = S == 1 ? 80 : 72;                 // x tile pixel pitch
   static constexpr int NZ = TH * TW * 8;                      // 16 B vectors of a dz tile (TH*16 px x 64 ch)
   static constexpr int NX = TPH * TPW * 8;                    // of an x tile
-  static constexpr size_t LDS = (size_t)TH * TW * W64_ZP * 2 + (size_t)TPH * TPW * XP * 2;
+  // + one spare x pixel: the stash's lanes past the tile write there (no branch in the tile loop)
+  static constexpr size_t LDS = (size_t)TH * TW * W64_ZP * 2 + (size_t)(TPH * TPW + 1) * XP * 2;
 };
 
 // TS = 2: 8 waves, wave w owns ci block w & 3 and taps [0,5) or [5,9) (w >> 2): 20 accumulators instead of 36, so
@@ -3116,10 +3117,30 @@ __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
 
   constexpr int VZ = NZ / NTHR, VX = (NX + NTHR - 1) / NTHR;
   uint4 pz[VZ], px[VX];
+  // Branch-free tile loads: buffer loads whose byte offset is pushed out of range for halo / ragged lanes return
+  // zeros (no branch around a load: hipcc waits vmcnt(0) at each one under a condition, and the per-vector 64-bit
+  // address arithmetic of the branchy form was ~20 VALU a vector -- VALU-issue-bound at one wave per SIMD).  Every
+  // per-vector term that does not depend on the tile is a per-thread constant.
+  // dz vector i: pixel row zr + (NTHR / 128) i, column zc of the tile, channels co0 + 8 (tid & 7)
+  const int zr = tid >> 7, zc = (tid >> 3) & 15, cg8 = (tid & 7) * 8;
+  const uint32_t zrow_b = (uint32_t)a.out_w * a.dz_cs * 2;
+  const uint32_t z_lane = (uint32_t)((zc * a.dz_cs + co0 + cg8) * 2) + (uint32_t)zr * zrow_b;
+  const __amdgpu_buffer_rsrc_t zrs = buf_rsrc(a.dz, (uint32_t)((long)a.n * a.out_h * a.out_w * a.dz_cs * 2));
+  // x vector i: tile pixel (xpy[i], xpx[i]), channels ci0 + 8 (tid & 7) (the upsample-on-load source: pixel >> 1)
+  int xpy[VX], xpx[VX];
+#pragma unroll
+  for (int i = 0; i < VX; ++i) {
+    const int pix = (tid + NTHR * i) >> 3;
+    xpy[i] = tid + NTHR * i < NX ? pix / TPW : 1 << 20;  // past the tile: never in range
+    xpx[i] = pix % TPW;
+  }
+  const uint32_t ximg_b = (uint32_t)a.in_h * a.in_w * a.in_cs * 2;
+  const uint32_t x_lane = (uint32_t)((a.in_co + ci0 + cg8) * 2);
+  const __amdgpu_buffer_rsrc_t xrs = buf_rsrc(a.x, (uint32_t)((long)a.n * a.in_h * a.in_w * a.in_cs * 2));
   // split-strided tile walk with incremental coordinates (no per-tile integer divisions on the scalar pipe)
   const int s_x = a.nsplit % a.tiles_x, s_y = (a.nsplit / a.tiles_x) % a.tiles_y, s_n = a.nsplit / (a.tiles_x * a.tiles_y);
   int ntx = split % a.tiles_x, nty = (split / a.tiles_x) % a.tiles_y, nn = split / (a.tiles_x * a.tiles_y);
-  auto issue = [&]() {  // the tile at (ntx, nty, nn), then advance them by nsplit tiles
+  auto issue = [&](bool live) {  // the tile at (ntx, nty, nn) (zeros if !live), then advance them by nsplit tiles
     const int tx = ntx, ty = nty, nimg = nn;
     ntx += s_x;
     int c = ntx >= a.tiles_x;
@@ -3129,25 +3150,21 @@ __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
     nty -= c ? a.tiles_y : 0;
     nn += s_n + c;
     const int oy0 = ty * TH, ox0 = tx * TW;
+    const uint32_t zt = (uint32_t)(((nimg * a.out_h + oy0) * a.out_w + ox0) * a.dz_cs * 2) + z_lane;
+    const bool zok = live && ox0 + zc < a.out_w;
 #pragma unroll
-    for (int i = 0; i < VZ; ++i) {  // dz: pixel v/8, channel group v%8
-      const int v = tid + NTHR * i;
-      const int pix = v >> 3, cg = v & 7;
-      const int oy = oy0 + (pix >> 4), ox = ox0 + (pix & 15);
-      pz[i] = make_uint4(0, 0, 0, 0);
-      if (oy < a.out_h && ox < a.out_w)
-        pz[i] = *(const uint4*)(a.dz + (((long)nimg * a.out_h + oy) * a.out_w + ox) * a.dz_cs + co0 + cg * 8);
+    for (int i = 0; i < VZ; ++i) {
+      const bool ok = zok && oy0 + zr + (NTHR / 128) * i < a.out_h;
+      pz[i] = buf_load16(zrs, ok ? zt + (uint32_t)((NTHR / 128) * i) * zrow_b : BUF_OOB);
     }
+    const int iy0 = S * oy0 - a.pad, ix0 = S * ox0 - a.pad;
+    const uint32_t xt = (uint32_t)nimg * ximg_b + x_lane;
 #pragma unroll
     for (int i = 0; i < VX; ++i) {
-      const int v = tid + NTHR * i;
-      const int pix = v >> 3, cg = v & 7;
-      const int py = pix / TPW, pxx = pix - py * TPW;
-      const int iy = S * oy0 - a.pad + py, ix = S * ox0 - a.pad + pxx;
-      px[i] = make_uint4(0, 0, 0, 0);
-      if (v < NX && iy >= 0 && iy < lh && ix >= 0 && ix < lw)
-        px[i] = *(const uint4*)(a.x + (((long)nimg * a.in_h + (iy >> upsh)) * a.in_w + (ix >> upsh)) * a.in_cs + a.in_co + ci0 +
-                                cg * 8);
+      const int iy = iy0 + xpy[i], ix = ix0 + xpx[i];
+      const bool ok = live && iy >= 0 && iy < lh && ix >= 0 && ix < lw;
+      const uint32_t off = xt + (uint32_t)((((iy >> upsh) * a.in_w) + (ix >> upsh)) * a.in_cs * 2);
+      px[i] = buf_load16(xrs, ok ? off : BUF_OOB);
     }
   };
   // buffer b of the staged tiles: dz [TH*16 px][W64_ZP], x [TPH*TPW px][XP]
@@ -3164,7 +3181,7 @@ __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
 #pragma unroll
     for (int i = 0; i < VX; ++i) {
       const int v = tid + NTHR * i;
-      if (v < NX) *(uint4*)(xs + (v >> 3) * XP + (v & 7) * 8) = px[i];
+      *(uint4*)(xs + (v < NX ? v >> 3 : W64<S>::TPH * TPW) * XP + (v & 7) * 8) = px[i];  // past the tile: the spare pixel
     }
   };
   // k-step kk = 32 output pixels of the tile; lane group g's 8 k values = pixel rows 4g + q and 16 + 4g + q (a
@@ -3182,10 +3199,11 @@ __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
     for (int u = 0; u < NU; ++u) bf[u] = cat_tr(ds_read_tr16(xs + xb0 + tapoff[u]), ds_read_tr16(xs + xb1 + tapoff[u]));
   };
   auto mma = [&](const bf16x8 (&af)[4], const bf16x8 (&bf)[NU]) {
-    if (do_bias && wave == 0 && tg == 0) {
+    // the bias gradient (sum of dz over the pixels) on every wave: 4 more MFMAs per k-step, but no branch in the tile
+    // loop (a wave-uniform branch here made hipcc copy the 144 accumulators between AGPRs and VGPRs every tile);
+    // wave 0 of a bias-owning workgroup stores it
 #pragma unroll
-      for (int t = 0; t < 4; ++t) accb[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], ones, accb[t], 0, 0, 0);
-    }
+    for (int t = 0; t < 4; ++t) accb[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], ones, accb[t], 0, 0, 0);
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
       if (u == NU - 1 && last_short) continue;
@@ -3195,41 +3213,41 @@ __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
   };
   constexpr int NK = TH * TW / 32;  // 4 (stride 1) or 2 (stride 2): even
   int tile = split;
-  if (tile < a.ntiles) issue();
+  issue(tile < a.ntiles);
   if constexpr (TS == 1) {
     // double-buffered LDS, one barrier per tile: tile t+1 (in registers since tile t-1) is written to the other
     // buffer after the first k-step pair of tile t is on the MFMA pipe, then tile t+2 is requested -- the stash
-    // no longer runs between two barriers with the MFMAs idle (one workgroup per CU: nothing else hid it)
-    if (tile < a.ntiles) {
-      stash(0);
-      if (tile + a.nsplit < a.ntiles) issue();
-    }
-    __syncthreads();
+    // no longer runs between two barriers with the MFMAs idle (one workgroup per CU: nothing else hid it).  The
+    // stash and the request are unconditional (past the last tile they move zeros into the idle buffer): no branch
+    // inside the tile loop, so the accumulators stay in place (the conditional form made hipcc copy all 144 of
+    // them out of and back into the AGPRs every tile).  LDS-only barriers keep the register prefetch in flight.
+    stash(0);
+    issue(tile + a.nsplit < a.ntiles);
+    lds_barrier();
     int cur = 0;
     for (; tile < a.ntiles; tile += a.nsplit) {
-      const bool more = tile + a.nsplit < a.ntiles;
       bf16x8 afA[4], bfA[NU], afB[4], bfB[NU];
       frags(cur, 0, afA, bfA);
 #pragma unroll
       for (int kk = 0; kk < NK; kk += 2) {
         frags(cur, kk + 1, afB, bfB);
         mma(afA, bfA);
-        if (kk == 0 && more) {
+        if (kk == 0) {
           stash(cur ^ 1);
-          if (tile + 2 * a.nsplit < a.ntiles) issue();
+          issue(tile + 2 * a.nsplit < a.ntiles);
         }
         if (kk + 2 < NK) frags(cur, kk + 2, afA, bfA);
         mma(afB, bfB);
       }
-      __syncthreads();  // this tile's reads of buffer cur and the stash of buffer cur ^ 1 are done
+      lds_barrier();  // this tile's reads of buffer cur and the stash of buffer cur ^ 1 are done
       cur ^= 1;
     }
   } else {
     for (; tile < a.ntiles; tile += a.nsplit) {
-      __syncthreads();  // previous tile's fragment reads done
+      lds_barrier();  // previous tile's fragment reads done
       stash(0);
-      if (tile + a.nsplit < a.ntiles) issue();
-      __syncthreads();
+      issue(tile + a.nsplit < a.ntiles);
+      lds_barrier();
       // two waves per SIMD (256 VGPRs each): one fragment set, the partner wave hides the latency
 #pragma unroll 2
       for (int kk = 0; kk < NK; ++kk) {
@@ -3651,6 +3669,11 @@ extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, c
     }
   }
   if (w64_shape(d)) {
+    if ((long)d->n * d->in_h * d->in_w * d->in_cstride * 2 >= (1L << 31) ||
+        (long)d->n * d->out_h * d->out_w * dz_cstride * 2 >= (1L << 31)) {  // 32-bit buffer offsets (BUF_OOB)
+      set_error("conv2d_wgrad: operands over 2 GiB (split the batch)");
+      return CLIMSR_EINVAL;
+    }
     WgArgs a;
     a.x = x; a.dz = dz; a.part = partial; a.bpart = bias_partial;
     a.n = d->n; a.in_h = d->in_h; a.in_w = d->in_w; a.in_c = d->in_c; a.in_cs = d->in_cstride; a.in_co = d->in_coff;
