@@ -690,7 +690,63 @@ __device__ __forceinline__ void conv_fwd_body(const FwdArgs& a) {
     if (ks < nks) mm(afA, bfA);  // odd k-step count: the last one is already loaded
   };
 
-  if constexpr (PFX > 0) {
+  if constexpr (PFX > 0 && GEO == 1) {
+    // Compile-time staging geometry (18 x 18-pixel x tile of 4 x 16 B channel vectors, 64 x 36 weight vectors per
+    // chunk): each thread's vector i is (tid + 256 i), so its pixel / channel group / weight row are per-thread
+    // constants; the chunk-0 byte offset of every vector is computed once (out-of-image vectors get BUF_OOB, which
+    // stays out of range at every chunk), and a chunk's loads are buffer loads at offset + j * chunk bytes -- one add
+    // per vector.  The runtime-geometry walk below spent ~570 VALU per chunk on index carries, bounds checks and
+    // 64-bit addresses (4 VALU per MFMA: the chunk loop was VALU-issue bound, conv5 / pull-x most of all).
+    // The host takes GEO 1 only for up == 1, in_c % 32 == 0 and tensors under 2 GiB.
+    constexpr int CV = 4, TPWc = TW + 2, CCPc = 48, NXV = (TW + 2) * (TW + 2) * CV, WV = 36, WPc = 9 * 32 + WPAD, NWV = NT * 16 * WV;
+    static_assert(PFX * 256 >= NXV && PFW * 256 >= NWV, "GEO 1 staging: not enough prefetch vectors");
+    uint4 px[PFX], pw[PFW];
+    const int cg8 = (tid & 3) * 8;  // 256 % CV == 0: every vector of a thread has the same channel group
+    const __amdgpu_buffer_rsrc_t xr = buf_rsrc(a.x, (uint32_t)((long)a.n * a.in_h * a.in_w * a.in_cs * 2));
+    const __amdgpu_buffer_rsrc_t wr = buf_rsrc(a.w, (uint32_t)((long)(blockIdx.y + 1) * NT * 16 * a.kpk * 2));
+    uint32_t xo[PFX], wo[PFW];
+#pragma unroll
+    for (int i = 0; i < PFX; ++i) {
+      const int v = tid + 256 * i, pix = v >> 2, ty_ = pix / TPWc, tx_ = pix - ty_ * TPWc;
+      const int iy = iy0 + ty_, ix = ix0 + tx_;
+      const bool ok = v < NXV && iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w;
+      xo[i] = ok ? (uint32_t)((((nimg * a.in_h + iy) * a.in_w + ix) * a.in_cs + a.in_co + cg8) * 2) : BUF_OOB;
+    }
+#pragma unroll
+    for (int i = 0; i < PFW; ++i) {
+      const int v = tid + 256 * i, r = v / WV, kv = v - r * WV;
+      wo[i] = v < NWV ? (uint32_t)(((co_blk0 + r) * a.kpk + kv * 8) * 2) : BUF_OOB;
+    }
+    auto issue = [&](int j) {
+#pragma unroll
+      for (int i = 0; i < PFX; ++i) px[i] = buf_load16(xr, xo[i] + (uint32_t)j * 64u);
+#pragma unroll
+      for (int i = 0; i < PFW; ++i) pw[i] = buf_load16(wr, wo[i] + (uint32_t)j * (uint32_t)(a.kcpad * 2));
+    };
+    auto stash = [&]() {
+      // pixel (v >> 2) = (tid >> 2) + 64 i: compile-time steps; lanes past the tile dump into the pad channels 32..39
+      // of pixel 0, which no fragment reads
+      const int xl0 = (tid >> 2) * CCPc + cg8;
+#pragma unroll
+      for (int i = 0; i < PFX; ++i) {
+        const int v = tid + 256 * i;
+        *(uint4*)(xs + ((NXV % 256 == 0 || v < NXV) ? xl0 + 64 * CCPc * i : 32)) = px[i];
+      }
+#pragma unroll
+      for (int i = 0; i < PFW; ++i) {
+        const int v = tid + 256 * i, r = v / WV, kv = v - r * WV;
+        if (NWV % 256 == 0 || v < NWV) *(uint4*)(ws + r * WPc + kv * 8) = pw[i];
+      }
+    };
+    issue(0);
+    for (int j = 0; j < a.nchunk; ++j) {
+      lds_barrier();  // chunk j-1's fragment reads are done
+      stash();
+      if (j + 1 < a.nchunk) issue(j + 1);  // lands while chunk j computes
+      lds_barrier();
+      compute();
+    }
+  } else if constexpr (PFX > 0) {
     uint4 px[PFX], pw[PFW];
     auto issue = [&](int j) {
       int ty_ = x_ty0, tx_ = x_tx0, cg = x_cg0;
@@ -2548,7 +2604,9 @@ template <int MW, int NT, int PFX = 0, int PFW = 0, int EP = 0>
 static int launch_fwd_ep(const FwdArgs& a, int ncob, size_t lds, hipStream_t s) {
   const bool base = MW == 4 && a.cc == 32 && a.ks == 3 && a.kcpad == 9 * 32;
   if constexpr (MW == 4 && PFX != 18) {
-    if (base && a.stride == 1 && a.tpw == TW + 2 && a.ccp == 48) return launch_fwd_geo<MW, NT, PFX, PFW, EP, 1>(a, ncob, lds, s);
+    if (base && a.stride == 1 && a.tpw == TW + 2 && a.ccp == 48 && a.up == 1 && a.in_c % 32 == 0 && a.nchunk * 32 == a.in_c &&
+        (long)a.n * a.in_h * a.in_w * a.in_cs * 2 < (1L << 31) && (long)ncob * NT * 16 * a.kpk * 2 < (1L << 31))
+      return launch_fwd_geo<MW, NT, PFX, PFW, EP, 1>(a, ncob, lds, s);
   }
   if constexpr (MW == 4 && PFX == 18) {
     if (base && a.stride == 2 && a.tpw == 2 * TW + 1 && a.ccp == 40) return launch_fwd_geo<MW, NT, PFX, PFW, EP, 2>(a, ncob, lds, s);
