@@ -559,7 +559,8 @@ __device__ __forceinline__ void bn_tile_partials(const FwdArgs& a, float* ssum, 
 // loaded into registers while chunk j is on the MFMA pipe, so a multi-chunk tile (RDB conv5 / pull-x: four
 // 32-channel chunks) pays one staging latency instead of one per chunk.
 #ifndef CLIMSR_DIAG_MODE
-#define CLIMSR_DIAG_MODE 0  // diagnostic builds only: 1 = every chunk computed twice, 2 = one staging, compute only
+#define CLIMSR_DIAG_MODE 0  // diagnostic builds only: 1 = every chunk computed twice, 2 = one staging, compute only,
+                            // 3 = staging only (GEO 1)
 #endif
 // GEO (host-checked geometry specialisation, 0 = runtime geometry): 1 / 2 = 3x3 taps over 32-channel chunks at
 // stride 1 / 2 with 16x16 output tiles (MW 4): every tap / row / fragment LDS offset is a compile-time immediate,
@@ -739,13 +740,22 @@ __device__ __forceinline__ void conv_fwd_body(const FwdArgs& a) {
       }
     };
     issue(0);
+#if CLIMSR_DIAG_MODE == 2
+    lds_barrier();
+    stash();
+    lds_barrier();
+    for (int j = 0; j < a.nchunk; ++j) compute();
+#else
     for (int j = 0; j < a.nchunk; ++j) {
       lds_barrier();  // chunk j-1's fragment reads are done
       stash();
       if (j + 1 < a.nchunk) issue(j + 1);  // lands while chunk j computes
       lds_barrier();
+#if CLIMSR_DIAG_MODE != 3  // diagnostic build 3: staging only, no k-loop
       compute();
+#endif
     }
+#endif
   } else if constexpr (PFX > 0) {
     uint4 px[PFX], pw[PFW];
     auto issue = [&](int j) {

@@ -22,6 +22,10 @@
 
 using namespace climsr;
 
+#ifndef CLIMSR_CHAIN_DIAG
+#define CLIMSR_CHAIN_DIAG 0  // diagnostic builds only (tests/diag_build.sh): 1 = no MFMAs, 2 = no output stores, 3 = no row loads
+#endif
+
 namespace {
 
 constexpr int RC_W = 64;                         // widest image row (4 fragments)
@@ -49,8 +53,9 @@ struct ChainArgs {
   int moff[4];
   float slope;
   int n, h, w, rows, strips_y;
-  uint32_t base_bytes, mask_bytes;
+  uint32_t base_bytes, mask_bytes, out_bytes;
 };
+typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
 
 __host__ __device__ constexpr int kp_blocks(int L) { return L == 1 ? 2 : (L == 4 ? 4 : 3); }
 __host__ __device__ constexpr int nd_blocks(int L) { return L == 1 ? 0 : (L == 2 ? 5 : (L == 3 ? 9 : 14)); }
@@ -142,8 +147,13 @@ __device__ __forceinline__ void level_acc(const uint16_t* lds, const bf16x8 (&af
     for (int i = 0; i < G; ++i) {
       const int j = gi * G + i;
       if (j < NB) {
+#if CLIMSR_CHAIN_DIAG == 1  // diagnostic build only: no MFMAs (the fragments are still read and consumed)
+        acc0[0] += (float)b[gi & 1][i][0][0] + (float)af[j][0];
+        acc1[0] += (float)b[gi & 1][i][1][0];
+#else
         acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], b[gi & 1][i][0], acc0, 0, 0, 0);
         acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], b[gi & 1][i][1], acc1, 0, 0, 0);
+#endif
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -184,7 +194,7 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, uint16_t* lds, int
     const bool rok = y >= 0 && y < a.h;
     const uint32_t rb = (uint32_t)(row0 + y) * xrow_bytes;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) v[i] = buf_load16(br, rok && xg[i] >= 0 ? rb + (uint32_t)xg[i] : BUF_OOB);
+    for (int i = 0; i < 2; ++i) v[i] = buf_load16(br, CLIMSR_CHAIN_DIAG != 3 && rok && xg[i] >= 0 ? rb + (uint32_t)xg[i] : BUF_OOB);
   };
   auto store_row = [&](int y, const uint4 (&v)[2]) {
     uint16_t* row = lds + xslot(y) * RC_XROW;
@@ -247,12 +257,19 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, uint16_t* lds, int
   const float bb[4] = {bias.x, bias.y, bias.z, bias.w};
   // step s: `cur` holds base row y1 + 2 (stored after the MFMAs), `nxt` receives row y1 + 3; `mcur` = this step's
   // masks, `mnxt` receives the next step's
+  // output stores are raw buffer stores issued unconditionally every step (an out-of-range offset drops them): a store
+  // under the step's level-active / own-row branches made the compiler's vmcnt for the next base-row wait count it as
+  // maybe-not-issued, so that wait also drained this step's stores (measured: 7 of 31 us per forward launch)
+  const __amdgpu_buffer_rsrc_t orr = buf_rsrc(a.out, a.out_bytes);
   auto step = [&](int s, uint4 (&cur)[2], uint4 (&nxt)[2], const uint2 (&mcur)[2], uint2 (&mnxt)[2]) {
     const int y1 = r0 - 3 + s;
     issue_row(y1 + 3, nxt);
     if constexpr (MODE == 1) issue_mask(s + 1, mnxt);
-    if (live0 && s >= 3 * (L - 1) && s <= R + 4 + L) {
-      const int y = y1 - 2 * (L - 1);
+    const bool active = live0 && s >= 3 * (L - 1) && s <= R + 4 + L;
+    const int y = y1 - 2 * (L - 1);
+    const bool own = active && y >= 0 && y < a.h && y >= r0 && y < r0 + R;
+    uint2 pko[2] = {make_uint2(0, 0), make_uint2(0, 0)};
+    if (active) {
       int xr[3], dr[3];
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
@@ -262,12 +279,9 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, uint16_t* lds, int
       f32x4 acc[2];
       level_acc<L>(lds, af, xr, dr, lx, ld, lp, g, acc[0], acc[1]);
       const bool in = y >= 0 && y < a.h;  // rows outside the image: zeros, the next level's padding
-      const bool own = in && y >= r0 && y < r0 + R;
       uint16_t* drow = lds + RC_OFF_D + dslot(y) * RC_DROW + dl;
-      uint16_t* grow = a.out + (row0 + y) * orow + ol;
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
-        if (k == 1 && !live1) break;
         float v[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -282,10 +296,18 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, uint16_t* lds, int
         }
         uint2 pk = make_uint2(pack2_bf16(v[0], v[1]), pack2_bf16(v[2], v[3]));
         if (!in) pk = make_uint2(0, 0);
-        if (L < 4) *(uint2*)(drow + 16 * k * RC_DP) = pk;
-        if (own) *(uint2*)(grow + 16 * k * a.ocs) = pk;
+        if (L < 4 && (k == 0 || live1)) *(uint2*)(drow + 16 * k * RC_DP) = pk;
+        pko[k] = pk;
       }
     }
+#if CLIMSR_CHAIN_DIAG != 2  // diagnostic build 2: no output stores
+    const uint32_t ob = (uint32_t)((row0 + y) * orow + ol) * 2u;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const bool ok = own && (k == 0 || live1);
+      __builtin_amdgcn_raw_buffer_store_b64((v2u32){pko[k].x, pko[k].y}, orr, ok ? ob + (uint32_t)(16 * k * a.ocs * 2) : BUF_OOB, 0, 0);
+    }
+#endif
     store_row(y1 + 2, cur);  // its slot held row y1 - 8, which no level reads in this step
     lds_barrier();
   };
@@ -330,7 +352,7 @@ extern "C" int climsr_rdb_chain(const ClimsrChainDesc* d, void* stream) {
     }
   }
   const long px = (long)d->n * d->h * d->w;
-  if (px * d->bcs * 2 >= (1L << 31) || (d->act == 3 && px * d->mcs * 2 >= (1L << 31))) {
+  if (px * d->bcs * 2 >= (1L << 31) || px * d->ocs * 2 >= (1L << 31) || (d->act == 3 && px * d->mcs * 2 >= (1L << 31))) {
     set_error("rdb_chain: tensors over 2 GiB");
     return CLIMSR_EINVAL;
   }
@@ -347,6 +369,7 @@ extern "C" int climsr_rdb_chain(const ClimsrChainDesc* d, void* stream) {
   a.slope = d->slope;
   a.n = d->n; a.h = d->h; a.w = d->w;
   a.base_bytes = (uint32_t)(px * d->bcs * 2);
+  a.out_bytes = (uint32_t)(px * d->ocs * 2);
   a.mask_bytes = d->act == 3 ? (uint32_t)(px * d->mcs * 2) : 0u;
   // strip height: enough strips to give every CU one (a strip recomputes 3 + 2 + 1 halo rows per level chain)
   static int ncu = 0;
