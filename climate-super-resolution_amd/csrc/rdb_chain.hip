@@ -37,9 +37,7 @@ constexpr int RC_DD = 8;                         // dense ring rows (y1-7 .. y1-
 constexpr int RC_XROW = RC_COLS * RC_XP;
 constexpr int RC_DROW = RC_COLS * RC_DP;
 constexpr int RC_OFF_D = RC_XD * RC_XROW;        // elements
-constexpr int RC_L4P = 16;                       // level-4 row buffer pixel pitch (its 16 channels)
-constexpr int RC_OFF_4 = RC_OFF_D + RC_DD * RC_DROW;  // two level-4 row buffers (steps alternate)
-constexpr int RC_LDS = (RC_OFF_4 + 2 * RC_W * RC_L4P) * 2;  // 160,384 B
+constexpr int RC_LDS = (RC_OFF_D + RC_DD * RC_DROW) * 2;  // 156,288 B
 constexpr int RC_XCH = RC_COLS * 8;              // 16 B chunks of one base row (528)
 
 struct ChainArgs {
@@ -57,7 +55,7 @@ struct ChainArgs {
   int n, h, w, rows, strips_y;
   uint32_t base_bytes, mask_bytes, out_bytes;
 };
-typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
 
 __host__ __device__ constexpr int kp_blocks(int L) { return L == 1 ? 2 : (L == 4 ? 4 : 3); }
 __host__ __device__ constexpr int nd_blocks(int L) { return L == 1 ? 0 : (L == 2 ? 5 : (L == 3 ? 9 : 14)); }
@@ -254,39 +252,23 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, uint16_t* lds, int
   const int ld = px0 * RC_DP + 8 * g;
   const int lp = px0 * RC_DP + 8 * (g & 1);
   const int dl = (px0 + 1) * RC_DP + 16 * (L - 1) + 4 * g;    // this lane's dense-ring store (fragment 2h)
-  const int d4 = px0 * RC_L4P + 4 * g;                         // level 4: its row buffer
+  const int ol = px0 * a.ocs + a.ooff[L - 1] + 4 * g;          // and HBM store, elements within an image row
   const long orow = (long)a.w * a.ocs;
   const float bb[4] = {bias.x, bias.y, bias.z, bias.w};
-  // Output rows leave as whole 64-channel pixel rows: the four levels' 16-channel outputs of one row are contiguous in
-  // the HBM buffer (ooff ascending or descending by 16, host-checked), so one step after level 4 finishes row y every
-  // thread stores one 16 B piece of it (pixel t / 8, channels 8 (t % 8)) from the dense ring (levels 1-3, still there:
-  // row y is 6 / 4 / 2 rows behind the rows levels 1-3 write this step) and the level-4 row buffer.  Per-level 8 B
-  // stores of 32 B pixel pieces 256 B apart ran at ~2.4 TB/s (7 of 31 us per forward launch).
-  const __amdgpu_buffer_rsrc_t orr = buf_rsrc(a.out, a.out_bytes);
-  const bool asc = a.ooff[1] > a.ooff[0];
-  const int wp = tid >> 3, wc = tid & 7;                       // write-out: pixel, 8-channel piece of x1..x4
-  const int wl = asc ? (wc >> 1) : 3 - (wc >> 1);              // the level that produced piece wc
-  const int wsrc = wl < 3 ? RC_OFF_D + (wp + 1) * RC_DP + 16 * wl + 8 * (wc & 1) : RC_OFF_4 + wp * RC_L4P + 8 * (wc & 1);
-  const uint32_t wdst = (uint32_t)((wp * a.ocs + (asc ? a.ooff[0] : a.ooff[3]) + 8 * wc) * 2);
-  auto write_out = [&](int s) {  // level 4's row of step s
-    const int y = r0 - 3 + s - 6;
-    const bool ok = s >= 9 && y >= r0 && y < r0 + R && y < a.h && wp < a.w;
-    const uint16_t* src = lds + wsrc + (wl < 3 ? dslot(y) * RC_DROW : (s & 1) * RC_W * RC_L4P);
-    const uint4 v = *(const uint4*)src;
-    __builtin_amdgcn_raw_buffer_store_b128((v4u32){v.x, v.y, v.z, v.w}, orr,
-                                           ok ? (uint32_t)((row0 + y) * orow) * 2u + wdst : BUF_OOB, 0, 0);
-  };
   // step s: `cur` holds base row y1 + 2 (stored after the MFMAs), `nxt` receives row y1 + 3; `mcur` = this step's
   // masks, `mnxt` receives the next step's
+  // output stores are raw buffer stores issued unconditionally every step (an out-of-range offset drops them): a store
+  // under the step's level-active / own-row branches made the compiler's vmcnt for the next base-row wait count it as
+  // maybe-not-issued, so that wait also drained this step's stores (measured: 7 of 31 us per forward launch)
+  const __amdgpu_buffer_rsrc_t orr = buf_rsrc(a.out, a.out_bytes);
   auto step = [&](int s, uint4 (&cur)[2], uint4 (&nxt)[2], const uint2 (&mcur)[2], uint2 (&mnxt)[2]) {
     const int y1 = r0 - 3 + s;
     issue_row(y1 + 3, nxt);
     if constexpr (MODE == 1) issue_mask(s + 1, mnxt);
-#if CLIMSR_CHAIN_DIAG != 2  // diagnostic build 2: no output stores
-    write_out(s - 1);
-#endif
     const bool active = live0 && s >= 3 * (L - 1) && s <= R + 4 + L;
     const int y = y1 - 2 * (L - 1);
+    const bool own = active && y >= 0 && y < a.h && y >= r0 && y < r0 + R;
+    uint2 pko[2] = {make_uint2(0, 0), make_uint2(0, 0)};
     if (active) {
       int xr[3], dr[3];
 #pragma unroll
@@ -314,12 +296,18 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, uint16_t* lds, int
         }
         uint2 pk = make_uint2(pack2_bf16(v[0], v[1]), pack2_bf16(v[2], v[3]));
         if (!in) pk = make_uint2(0, 0);
-        if (k == 0 || live1) {
-          if (L < 4) *(uint2*)(drow + 16 * k * RC_DP) = pk;
-          else *(uint2*)(lds + RC_OFF_4 + (s & 1) * RC_W * RC_L4P + d4 + 16 * k * RC_L4P) = pk;
-        }
+        if (L < 4 && (k == 0 || live1)) *(uint2*)(drow + 16 * k * RC_DP) = pk;
+        pko[k] = pk;
       }
     }
+#if CLIMSR_CHAIN_DIAG != 2  // diagnostic build 2: no output stores
+    const uint32_t ob = (uint32_t)((row0 + y) * orow + ol) * 2u;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const bool ok = own && (k == 0 || live1);
+      __builtin_amdgcn_raw_buffer_store_b64((v2u32){pko[k].x, pko[k].y}, orr, ok ? ob + (uint32_t)(16 * k * a.ocs * 2) : BUF_OOB, 0, 0);
+    }
+#endif
     store_row(y1 + 2, cur);  // its slot held row y1 - 8, which no level reads in this step
     lds_barrier();
   };
@@ -327,9 +315,6 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, uint16_t* lds, int
     step(s, ra, rb, ma, mb);
     if (s + 1 < R + 9) step(s + 1, rb, ra, mb, ma);
   }
-#if CLIMSR_CHAIN_DIAG != 2
-  write_out(R + 8);  // the last row (the final step's barrier ordered its LDS writes)
-#endif
 }
 
 // Waves w and w + 4 share a SIMD (a workgroup's waves go round the 4 SIMDs in a fixed cyclic order).  Wave w < 4
@@ -358,12 +343,6 @@ extern "C" int climsr_rdb_chain(const ClimsrChainDesc* d, void* stream) {
       d->boff % 8 || d->ocs % 4 || (d->act != 1 && d->act != 3) || (d->act == 3 && (!d->mask || d->mcs % 4)) ||
       !(d->slope >= 0.f && d->slope <= 1.f)) {
     set_error("rdb_chain: bad args (width must be 16, 32, 48 or 64)");
-    return CLIMSR_EINVAL;
-  }
-  const int ostep = d->ooff[1] - d->ooff[0];
-  if ((ostep != 16 && ostep != -16) || d->ooff[2] - d->ooff[1] != ostep || d->ooff[3] - d->ooff[2] != ostep ||
-      (ostep > 0 ? d->ooff[0] : d->ooff[3]) % 8 || d->ocs % 8) {
-    set_error("rdb_chain: the four level outputs must be contiguous 16-channel slices (8-aligned)");
     return CLIMSR_EINVAL;
   }
   for (int L = 0; L < 4; ++L) {
