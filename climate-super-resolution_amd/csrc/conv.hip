@@ -317,7 +317,17 @@ struct FwdArgs {
   float aux_scale;
   int lds_tab, lds_x;
   double* bn_part;  // EP 9: per-tile BatchNorm partial sums [tile][2][out_c] of the bf16 outputs (climsr_conv2d_fwd_bn_parts)
+  int xgrp;         // > 0: 1-D grid in XCD-major (channel-block group, tile, channel block) order, xgrp blocks a group
 };
+
+// Blocks are dealt round-robin over the 8 XCDs (blocks b and b + 8 share one, MI355X_MICROARCH.md 'Workgroup
+// dispatch'; for speed only, nothing depends on it).  xcd_major(b, n) renumbers a grid of n so that each XCD's
+// blocks form one contiguous index range (bijective for any n): blocks that read the same operand tiles and sit
+// next to each other in that order share an L2 instead of fetching the tiles once per XCD.
+__device__ __forceinline__ int xcd_major(int b, int n) {
+  const int x = b & 7, j = b >> 3, q = n >> 3, r = n & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + j;
+}
 
 // Epilogue residual operands: 4 consecutive channels, bf16 (8 B) or fp32 (16 B), kept raw until use so
 // that all loads of a round are in flight together.
@@ -580,14 +590,23 @@ __device__ __forceinline__ void conv_fwd_body(const FwdArgs& a) {
   const int g = lane >> 4;
   const int col = lane & 15;
 
-  int bid = blockIdx.x;
+  // (tile, output-channel block): blockIdx, or with xgrp the XCD-major order in which the xgrp channel blocks of a
+  // tile are consecutive on one XCD (the x tile is fetched into that L2 once for all of them, not once per XCD)
+  int tile_id = blockIdx.x, cob = blockIdx.y;
+  if (a.xgrp > 0) {
+    const int ntile = a.tiles_x * a.tiles_y * a.n, idx = xcd_major(blockIdx.x, gridDim.x);
+    const int grp = idx / (ntile * a.xgrp), rem = idx - grp * (ntile * a.xgrp);
+    tile_id = rem / a.xgrp;
+    cob = grp * a.xgrp + (rem - tile_id * a.xgrp);
+  }
+  int bid = tile_id;
   const int tx = bid % a.tiles_x;
   bid /= a.tiles_x;
   const int ty = bid % a.tiles_y;
   const int nimg = bid / a.tiles_y;
   const int ox0 = tx * TW;
   const int oy0 = ty * (4 * MW);
-  const int co_blk0 = blockIdx.y * NT * 16;
+  const int co_blk0 = cob * NT * 16;
   const int wpitch = a.kcpad + WPAD;
   const int ks2 = a.ks * a.ks;
 
@@ -704,7 +723,7 @@ __device__ __forceinline__ void conv_fwd_body(const FwdArgs& a) {
     uint4 px[PFX], pw[PFW];
     const int cg8 = (tid & 3) * 8;  // 256 % CV == 0: every vector of a thread has the same channel group
     const __amdgpu_buffer_rsrc_t xr = buf_rsrc(a.x, (uint32_t)((long)a.n * a.in_h * a.in_w * a.in_cs * 2));
-    const __amdgpu_buffer_rsrc_t wr = buf_rsrc(a.w, (uint32_t)((long)(blockIdx.y + 1) * NT * 16 * a.kpk * 2));
+    const __amdgpu_buffer_rsrc_t wr = buf_rsrc(a.w, (uint32_t)((long)(cob + 1) * NT * 16 * a.kpk * 2));
     uint32_t xo[PFX], wo[PFW];
 #pragma unroll
     for (int i = 0; i < PFX; ++i) {
@@ -971,7 +990,7 @@ __device__ __forceinline__ void conv_fwd_body(const FwdArgs& a) {
     static_assert(MW == 4 && NT == 4, "BatchNorm partials: 16x16 x 64-channel tiles");
     float ssum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, ssq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     store_tile_lds<RF, MW * 16, NT * 16, 64, EP>(a, eb, EPP, lane, nimg, oy0 + wave * MW, ox0, co_blk0, ssum, ssq);
-    bn_tile_partials(a, ssum, ssq, true, wave, lane, blockIdx.x, co_blk0, (float*)smem);
+    bn_tile_partials(a, ssum, ssq, true, wave, lane, tile_id, co_blk0, (float*)smem);
   } else {
     store_tile_lds<RF, MW * 16, NT * 16, 64, EP>(a, eb, EPP, lane, nimg, oy0 + wave * MW, ox0, co_blk0);
   }
@@ -2577,9 +2596,25 @@ static int launch_dgrad_s2(const ClimsrConvDesc* d, const FwdArgs& a, hipStream_
   return launch_dgrad_s2_t<4, 2>(d, a, s);
 }
 
+static int env_flag(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
+// channel blocks grouped per tile in the XCD-major order: the largest divisor of ncob (>= 2) whose weight blocks
+// together stay within ~2.5 MB of the XCD's 4 MB L2 (they are re-read by every tile of the group), else 0
+static int conv_xcd_group(int ncob, long wblk_bytes) {
+  static const int mode = env_flag("CLIMSR_CONV_XCD", 1);
+  if (!mode || ncob < 2) return 0;
+  for (int gsz = ncob; gsz >= 2; --gsz)
+    if (ncob % gsz == 0 && gsz * wblk_bytes <= (5L << 19)) return gsz;
+  return 0;
+}
+
 template <int MW, int NT, int PFX, int PFW, int EP, int GEO>
-static int launch_fwd_geo(const FwdArgs& a, int ncob, size_t lds, hipStream_t s) {
-  dim3 grid(a.tiles_x * a.tiles_y * a.n, ncob);
+static int launch_fwd_geo(const FwdArgs& a0, int ncob, size_t lds, hipStream_t s) {
+  FwdArgs a = a0;
+  a.xgrp = GEO == 1 ? conv_xcd_group(ncob, (long)NT * 16 * a.kpk * 2) : 0;
+  const dim3 grid = a.xgrp ? dim3(a.tiles_x * a.tiles_y * a.n * ncob) : dim3(a.tiles_x * a.tiles_y * a.n, ncob);
   const size_t lds_ep = (size_t)4 * MW * 16 * (NT * 16 + 4) * 4;  // epilogue staging (aliases the operands)
   if (lds_ep > lds) lds = lds_ep;
   constexpr int MV = NT == 1 ? 6 : (NT == 2 ? 8 : 4);
@@ -2899,6 +2934,7 @@ struct WgArgs {
   int n, in_h, in_w, in_c, in_cs, in_co, up, ks, stride, pad, out_h, out_w, out_c, dz_cs;
   int tph, tpw, dzp, tiles_x, tiles_y, ntiles, nsplit, ntapb, ncib, co_rows, kw;
   int lds_x;
+  int xcd;  // conv_wgrad64_kernel: 1-D grid in XCD-major (split, channel block) order (else blockIdx.y = split)
 };
 
 // CI4 = 1: inputs with <= 4 real channels (srcnn.conv1 / conv_first, 3 channels).  The x tile holds 4
@@ -3155,8 +3191,12 @@ __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
   const int wave = (tid >> 6) & 3, tg = TS == 1 ? 0 : tid >> 8;  // ci block, tap group
   const int u0 = tg * 5;
   const int q = (lane & 15) >> 2, p = lane & 3, col = lane & 15;
-  const int cib = blockIdx.x % a.ncib, cob = blockIdx.x / a.ncib;
-  const int split = blockIdx.y;
+  // (split, 64x64 block): with a.xcd the XCD-major order in which a split's blocks are consecutive on one XCD -- they
+  // walk the same pixel tiles at the same time, so each x / dz tile is fetched into that L2 once for all of them
+  const int nblk = a.ncib * (a.out_c / 64);
+  const int bidx = a.xcd ? xcd_major(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int blk = a.xcd ? bidx % nblk : bidx, split = a.xcd ? bidx / nblk : blockIdx.y;
+  const int cib = blk % a.ncib, cob = blk / a.ncib;
   const int ci0 = cib * 64, co0 = cob * 64;
   const bool do_bias = cib == 0 && a.bpart != nullptr;
   const int lh = a.in_h * a.up, lw = a.in_w * a.up;
@@ -3293,6 +3333,23 @@ __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
     issue(tile + a.nsplit < a.ntiles);
     lds_barrier();
     int cur = 0;
+        if (u == 0) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) accb[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk & 1][t], ones, accb[t], 0, 0, 0);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk & 1][t], bq[gi % RING], acc[t][u], 0, 0, 0);
+#endif
+        if (gi == 2) {
+          stash(cur ^ 1);
+          issue(tile + 2 * a.nsplit < a.ntiles);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      lds_barrier();  // this tile's reads of buffer cur and the stash of buffer cur ^ 1 are done
+      cur ^= 1;
+    }
+#else
     for (; tile < a.ntiles; tile += a.nsplit) {
       bf16x8 afA[4], bfA[NU], afB[4], bfB[NU];
       frags(cur, 0, afA, bfA);
@@ -3761,7 +3818,8 @@ extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, c
       (void)hipFuncSetAttribute((const void*)conv_wgrad64_kernel<1, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       attr_set = true;
     }
-    const dim3 grid((d->out_c / 64) * (d->in_c / 64), nsplit);
+    a.xcd = env_flag("CLIMSR_W64_XCD", 1);
+    const dim3 grid = a.xcd ? dim3((d->out_c / 64) * (d->in_c / 64) * nsplit) : dim3((d->out_c / 64) * (d->in_c / 64), nsplit);
     if (d->stride == 2) {
       a.tph = W64<2>::TPH; a.tpw = W64<2>::TPW;
       if (dry_run("conv_wgrad64_kernel<1, 2>")) return CLIMSR_OK;

@@ -10,7 +10,7 @@ import torch  # noqa: E402
 
 import climsr_amd  # noqa: E402,F401
 from climsr_amd import _lib  # noqa: E402
-from climsr_amd.ops import ACT_LRELU, OUT_F32, BatchedPacker, ConvPlan, RdbChain  # noqa: E402
+from climsr_amd.ops import ACT_LRELU, OUT_F32, BatchedPacker, ConvPlan, RdbChain, Workspace  # noqa: E402
 from tests.perf_conv_timing import timeit  # noqa: E402
 
 dev, n, dc = "cuda", 32, 128
@@ -43,6 +43,16 @@ g_in = torch.empty(n, 64, 64, 64, device=dev)
 g_out = torch.randn(n, 64, 64, 64, device=dev)
 res["pullx_us"] = timeit(lambda: px.fwd(dzb, dc, 0, 64, 64, g_in, 64, 0, n, use_bias=False, out_mode=OUT_F32, res1=g_out, res1_cs=64,
                                         res1_co=0), 20)
+# weight gradients: the residual dense block's grouped GEMM shape (128 input x 128 output-gradient channels at 64^2)
+# and the trunk's 64 -> 64 (both conv_wgrad64_kernel<1, 1>); the wgrad includes its split-K reduce launch
+wsp = Workspace()
+for cin, cout in ((128, 128), (64, 64)):
+    pw = plan(cin, cout)
+    pw.gw = torch.zeros_like(pw.weight)
+    pw.gb = torch.zeros(cout, device=dev)
+    xw = torch.randn(n, 64, 64, cin, device=dev).to(torch.bfloat16)
+    dzw = torch.randn(n, 64, 64, cout, device=dev).to(torch.bfloat16)
+    res[f"wgrad_{cin}_us"] = timeit(lambda: pw.wgrad(xw, cin, 0, 64, 64, dzw, cout, n, wsp, accumulate=False), 20)
 for cin, cout, hw in ((256, 256, 64), (512, 512, 32)):
     p = plan(cin, cout)
     x = torch.randn(64, hw, hw, cin, device=dev).to(torch.bfloat16)
