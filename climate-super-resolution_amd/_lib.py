@@ -31,7 +31,8 @@ class Epilogue(ctypes.Structure):
                 ("res2_cstride", ctypes.c_int32), ("res2_coff", ctypes.c_int32), ("out_mode", ctypes.c_int32),
                 ("down2", ctypes.c_int32), ("res_f32", ctypes.c_int32), ("beta1", c_float), ("beta2", c_float),
                 ("aux_cstride", ctypes.c_int32), ("aux", c_void_p), ("aux_coff", ctypes.c_int32), ("aux_scale", c_float),
-                ("bn_part", c_void_p)]
+                ("bn_part", c_void_p), ("bn_z", c_void_p), ("bn_z_cstride", ctypes.c_int32), ("bn_slope", c_float),
+                ("bn_mean", c_void_p), ("bn_rstd", c_void_p), ("bn_gamma", c_void_p), ("bn_beta", c_void_p)]
 
     def __init__(self, *args, **kw):
         # plain residual adds unless a caller scales them (beta1 / beta2 are positional fields 13 / 14)
@@ -139,6 +140,8 @@ SIGNATURES = {
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "climsr_bn_backward_z": (c_int, [c_void_p, c_int, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
                                      c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "climsr_bn_backward_parts": (c_int, [c_void_p, ctypes.c_int64, c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p,
+                                         c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "climsr_reflect_pad1_bf16": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "climsr_reflect_pad1_bwd_f32": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "climsr_adaptive_pool_fwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,

@@ -318,6 +318,11 @@ struct FwdArgs {
   int lds_tab, lds_x;
   double* bn_part;  // EP 9: per-tile BatchNorm partial sums [tile][2][out_c] of the bf16 outputs (climsr_conv2d_fwd_bn_parts)
   int xgrp;         // > 0: 1-D grid in XCD-major (channel-block group, tile, channel block) order, xgrp blocks a group
+  // EP 10: BatchNorm-backward partials of the stored data gradient (ClimsrEpilogue.bn_z ...) into bn_part
+  const uint16_t* bz;
+  int bz_cs;
+  float bslope;
+  const float *bmean, *brstd, *bgamma, *bbeta;
 };
 
 // Blocks are dealt round-robin over the 8 XCDs (blocks b and b + 8 share one, MI355X_MICROARCH.md 'Workgroup
@@ -431,7 +436,9 @@ __device__ __forceinline__ void store_tile_lds(const FwdArgs& a, const float* eb
   const bool has_bias = (EP == 1 || EP == 3) ? true : EP != 0 ? false : a.bias != nullptr;
   // EP 9 = EP 8 + sums / sums of squares of the stored (bf16-rounded) values per lane (ssum / ssq [8]: the lane's
   // 8 channels, the same for all of its items when NCH / 8 divides NLANE)
-  const int act = (EP == 1 || EP == 2 || EP == 7 || EP == 8 || EP == 9) ? 0 : a.act;
+  // EP 10 = EP 8 + BatchNorm-backward partials (ssum += d, ssq += d * xhat; d = stored value * lrelu'(BN(z)), z read
+  // from a.bz at the output pixel: the layer's affine is recomputed as bn_stats_kernel MODE 2 does, bit for bit)
+  const int act = (EP == 1 || EP == 2 || EP == 7 || EP == 8 || EP == 9 || EP == 10) ? 0 : a.act;
   const bool has1 = (EP == 1 || EP == 2 || EP == 4) ? true : EP != 0 ? false : a.res1 != nullptr;
   const bool has2 = (EP == 0 || EP == 1 || EP == 2) ? a.res2 != nullptr : false;
   const int out_mode = (EP == 2 || EP == 7) ? 1 : EP != 0 ? 0 : a.out_mode;
@@ -439,8 +446,20 @@ __device__ __forceinline__ void store_tile_lds(const FwdArgs& a, const float* eb
   const bool vec = EP != 0 || ((a.out_c & 7) == 0 && ((a.out_cs | a.out_co) & 7) == 0 && (!a.res1 || ((a.r1_cs | a.r1_co) & 7) == 0) &&
                                (!a.res2 || ((a.r2_cs | a.r2_co) & 7) == 0) && (!a.aux || ((a.aux_cs | a.aux_co) & 7) == 0));
   constexpr int IB = RF ? 2 : 4;  // items per round: their global loads are in flight together
-  const __amdgpu_buffer_rsrc_t rr1 = opt_rsrc(has1 ? a.res1 : nullptr), rr2 = opt_rsrc(has2 ? a.res2 : nullptr),
-                               rry = opt_rsrc(out_mode == 2 ? a.y : nullptr);
+  const __amdgpu_buffer_rsrc_t rr1 = opt_rsrc(EP == 10 ? (const void*)a.bz : has1 ? a.res1 : nullptr),
+                               rr2 = opt_rsrc(has2 ? a.res2 : nullptr), rry = opt_rsrc(out_mode == 2 ? a.y : nullptr);
+  float bmu[8], brs[8], bsc[8], bsh[8];  // EP 10: the lane's 8 channels (the same for all of its items, as for EP 9)
+  if constexpr (EP == 10) {
+    static_assert(NLANE % NG == 0, "EP 10: one channel group per lane");
+    const int c = co0 + (lane % NG) * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      bmu[i] = a.bmean[c + i];
+      brs[i] = a.brstd[c + i];
+      bsc[i] = a.bgamma[c + i] * brs[i];
+      bsh[i] = a.bbeta[c + i] - bmu[i] * bsc[i];
+    }
+  }
 #pragma unroll
   for (int base = 0; base < (NIT + NLANE - 1) / NLANE; base += IB) {
     Raw8 r1[IB], r2[IB], old[IB];
@@ -458,7 +477,8 @@ __device__ __forceinline__ void store_tile_lds(const FwdArgs& a, const float* eb
       const long pidx = ld ? pidxs[j] : 0;
       const int c = ld ? co : 0;
       // (EP 0: unconditional, a null operand reads zeros; EP > 0: compile-time known)
-      if (EP == 0 || has1) r1[j] = load8b(rr1, f1, pidx * a.r1_cs + (ld ? a.r1_co : 0) + c);
+      if (EP == 10) r1[j] = load8b(rr1, false, pidx * a.bz_cs + c);  // the layer's z
+      else if (EP == 0 || has1) r1[j] = load8b(rr1, f1, pidx * a.r1_cs + (ld ? a.r1_co : 0) + c);
       else r1[j].lo = r1[j].hi = make_uint4(0, 0, 0, 0);
       if (EP == 0 || has2) r2[j] = load8b(rr2, f2, pidx * a.r2_cs + (ld ? a.r2_co : 0) + c);
       else r2[j].lo = r2[j].hi = make_uint4(0, 0, 0, 0);
@@ -498,6 +518,18 @@ __device__ __forceinline__ void store_tile_lds(const FwdArgs& a, const float* eb
               const float r = raw8_at(rr, false, i);
               ssum[i] += r;
               ssq[i] = fmaf(r, r, ssq[i]);
+            }
+          }
+          if constexpr (EP == 10) {
+            Raw8 rr;
+            rr.lo = pk;
+            rr.hi = make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              const float r = raw8_at(rr, false, i), z = raw8_at(r1[j], false, i);
+              const float d = fmaf(z, bsc[i], bsh[i]) > 0.f ? r : r * a.bslope;
+              ssum[i] += d;
+              ssq[i] = fmaf(d, (z - bmu[i]) * brs[i], ssq[i]);
             }
           }
         } else {
@@ -986,7 +1018,7 @@ __device__ __forceinline__ void conv_fwd_body(const FwdArgs& a) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) *(f32x4*)(eb + (m * 16 + col) * EPP + t * 16 + g * 4) = acc[m][t];
   __syncthreads();  // orders the staging writes before the transposed reads (they use another vector type)
-  if constexpr (EP == 9) {
+  if constexpr (EP == 9 || EP == 10) {
     static_assert(MW == 4 && NT == 4, "BatchNorm partials: 16x16 x 64-channel tiles");
     float ssum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, ssq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     store_tile_lds<RF, MW * 16, NT * 16, 64, EP>(a, eb, EPP, lane, nimg, oy0 + wave * MW, ox0, co_blk0, ssum, ssq);
@@ -1833,6 +1865,9 @@ static int launch_pw(const FwdArgs& a, const PwGeom& g, hipStream_t s) {
     FwdArgs b = a;
     b.cc = 8;
     b.in_c = 8;
+    // one 16 B vector per pixel: the 24 x 24 (9x9) / 18 x 18 (3x3) input tile is <= 2 vectors per thread, and the
+    // staging loops run PV iterations of address math whether or not their vectors exist
+    if (g.nvx <= 2 * 64 * NW) return launch_pw_geo<NW, MW, NT, 2, EP, 2>(b, g, s);
     return launch_pw_geo<NW, MW, NT, PV, EP, 2>(b, g, s);
   }
   if constexpr (NW * MW == 16) {
@@ -2353,6 +2388,23 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_s2_kernel(FwdArgs a) {
     return ok ? ((long)nimg * a.out_h + py) * a.out_w + pxx : 0;
   };
   uint4 r1[4][4];
+  // EP 10: the BatchNorm-backward partials of the stored dx (store_tile_lds EP 10): z is loaded up front like the
+  // activation operand; the lane's 8 channels are the same for all of its items (64 % NG == 0)
+  const __amdgpu_buffer_rsrc_t rrz = opt_rsrc(EP == 10 ? (const void*)a.bz : nullptr);
+  const int cgl = lane % NG;
+  float bmu[8], brs[8], bsc[8], bsh[8], ssum[8], ssq[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    ssum[i] = 0.f;
+    ssq[i] = 0.f;
+    if constexpr (EP == 10) {
+      const int c = co0 + cgl * 8 + i;
+      bmu[i] = a.bmean[c];
+      brs[i] = a.brstd[c];
+      bsc[i] = a.bgamma[c] * brs[i];
+      bsh[i] = a.bbeta[c] - bmu[i] * bsc[i];
+    }
+  }
 #pragma unroll
   for (int ph = 0; ph < 4; ++ph)
 #pragma unroll
@@ -2362,6 +2414,11 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_s2_kernel(FwdArgs a) {
         bool ok;
         const long pidx = item_pidx(ph, k, ok);
         r1[ph][k] = buf_load16(rr1, (uint32_t)((pidx * a.r1_cs + (ok ? a.r1_co + co0 + ((lane + 64 * k) % NG) * 8 : 0)) * 2));
+      } else if (EP == 10) {
+        bool ok;
+        const long pidx = item_pidx(ph, k, ok);
+        // (opt_rsrc has no range limit: a pixel outside the image reads pixel 0, whose d is 0)
+        r1[ph][k] = buf_load16(rrz, (uint32_t)((pidx * a.bz_cs + co0 + cgl * 8) * 2));
       }
     }
 #pragma unroll
@@ -2389,7 +2446,54 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_s2_kernel(FwdArgs a) {
           v[i] = a.act == 3 ? (r > 0.f ? v[i] : v[i] * a.slope) : (r > 0.f ? v[i] : 0.f);
         }
       }
-      if (ok) *(uint4*)((uint16_t*)a.y + oidx) = pack8_bf16(v, 1.f);
+      const uint4 pk = pack8_bf16(v, 1.f);
+      if (ok) *(uint4*)((uint16_t*)a.y + oidx) = pk;
+      if constexpr (EP == 10) {
+        Raw8 rr, rz;
+        rr.lo = pk;
+        rz.lo = r1[ph][k];
+        rr.hi = rz.hi = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float r = ok ? raw8_at(rr, false, i) : 0.f, z = raw8_at(rz, false, i);
+          const float d = fmaf(z, bsc[i], bsh[i]) > 0.f ? r : r * a.bslope;
+          ssum[i] += d;
+          ssq[i] = fmaf(d, (z - bmu[i]) * brs[i], ssq[i]);
+        }
+      }
+    }
+  }
+  if constexpr (EP == 10) {
+    // lanes with equal lane % NG hold the same 8 channels: xor-shuffles over the other lane bits, then the 4 waves
+    // meet in LDS (the staging is free after a barrier) and part[tile][0 / 1][co0 + ch] gets fixed-order fp64 sums
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int m = NG; m < 64; m <<= 1) {
+        ssum[i] += __shfl_xor(ssum[i], m);
+        ssq[i] += __shfl_xor(ssq[i], m);
+      }
+    float* red = (float*)smem;
+    lds_barrier();  // every wave's reads of the last phase's staging are done
+    if (lane < NG) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        red[wave * 2 * CO + lane * 8 + i] = ssum[i];
+        red[wave * 2 * CO + CO + lane * 8 + i] = ssq[i];
+      }
+    }
+    lds_barrier();
+    if (tid < CO) {
+      float ts = 0.f, tq = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        ts += red[w * 2 * CO + tid];
+        tq += red[w * 2 * CO + CO + tid];
+      }
+      const long tile = ((long)nimg * a.tiles_y + ty) * a.tiles_x + tx;
+      double* out = a.bn_part + tile * 2 * a.out_c;
+      out[co0 + tid] = (double)ts;
+      out[a.out_c + co0 + tid] = (double)tq;
     }
   }
 }
@@ -2579,12 +2683,13 @@ static int launch_dgrad_s2_t(const ClimsrConvDesc* d, FwdArgs a, hipStream_t s) 
   a.tiles_y = ceil_div(d->in_h, 4 * MW);
   const bool ep4 = a.act == 3 || a.act == 4;
   if (g_dry) {
-    snprintf(g_dry_name, sizeof(g_dry_name), "conv_dgrad_s2_kernel<%d, %d, %d>", ep4 ? 4 : 0, MW, NT);
+    snprintf(g_dry_name, sizeof(g_dry_name), "conv_dgrad_s2_kernel<%d, %d, %d>", ep4 ? 4 : a.bz ? 10 : 0, MW, NT);
     return CLIMSR_OK;
   }
   dim3 grid(ceil_div(a.tiles_x * a.tiles_y * a.n, 8) * 8 * (d->out_c / (NT * 16)));
   const int lds = s2d_lds<MW>(NT);
   if (ep4) hipLaunchKernelGGL((conv_dgrad_s2_kernel<4, MW, NT>), grid, dim3(256), lds, s, a);
+  else if (a.bz) hipLaunchKernelGGL((conv_dgrad_s2_kernel<10, MW, NT>), grid, dim3(256), lds, s, a);
   else hipLaunchKernelGGL((conv_dgrad_s2_kernel<0, MW, NT>), grid, dim3(256), lds, s, a);
   return check_launch("conv2d_fwd (dgrad s2)");
 }
@@ -2685,6 +2790,13 @@ static bool bn_parts_ok(const ClimsrConvDesc* d, const FwdArgs& a, const FwdGeom
          nrw <= 9 && g.lds_total <= 160 * 1024;
 }
 
+// Backward partials (ep->bn_z): the stride-1 16x16-tile path (EP 10) or the phase-decomposed stride-2 data gradient
+static bool bn_bwd_parts_ok(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const FwdArgs& a, const FwdGeom& g) {
+  if (plain_ep(a) != 8) return false;
+  if (d->up == -2) return dgrad_s2_shape(d, ep, nullptr);
+  return d->stride == 1 && bn_parts_ok(d, a, g);
+}
+
 extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, const uint16_t* wpk, const float* bias,
                                  const ClimsrEpilogue* ep, void* y, void* stream);
 
@@ -2696,6 +2808,11 @@ extern "C" int64_t climsr_conv2d_fwd_bn_parts(const ClimsrConvDesc* d, const Cli
   FwdArgs a{};
   a.act = ep->act; a.out_mode = ep->out_mode; a.down2 = ep->down2; a.res1 = ep->res1; a.res2 = ep->res2; a.aux = (uint16_t*)ep->aux;
   a.res_f32 = ep->res_f32; a.out_c = d->out_c; a.out_cs = d->out_cstride; a.out_co = d->out_coff; a.kcpad = g.kcpad;
+  if (ep->bn_z) {
+    if (!bn_bwd_parts_ok(d, ep, a, g)) return 0;
+    if (d->up == -2) return (int64_t)ceil_div(d->in_w, 16) * ceil_div(d->in_h, 4 * (d->out_c == 64 ? 2 : 4)) * d->n;  // dz tiles
+    return (int64_t)ceil_div(d->out_w, TW) * ceil_div(d->out_h, 16) * d->n;
+  }
   if (!bn_parts_ok(d, a, g)) return 0;
   return (int64_t)ceil_div(d->out_w, TW) * ceil_div(d->out_h, 16) * d->n;
 }
@@ -2742,7 +2859,7 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
   // 16x16 output tiles (64 px per wave) for the 64-channel layers; 8x16 otherwise
   const int mw = (d->out_h >= 12 && fwd_nt(d->out_c) == 4) ? 4 : 2;
   fwd_geom(d->in_c, d->ks, d->stride, d->out_c, d->cc, mw, &g);
-  FwdArgs a;
+  FwdArgs a{};  // zero: the optional operands (bz, bn_part, xgrp, ...) default to absent
   a.x = x; a.w = wpk; a.bias = bias; a.y = y;
   a.res1 = ep->res1; a.res2 = ep->res2; a.aux = (uint16_t*)ep->aux;
   a.res_f32 = ep->res_f32; a.beta1 = ep->beta1; a.beta2 = ep->beta2;
@@ -2757,10 +2874,19 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
   a.r1_cs = ep->res1_cstride; a.r1_co = ep->res1_coff; a.r2_cs = ep->res2_cstride; a.r2_co = ep->res2_coff;
   a.lds_tab = (int)g.lds_tab; a.lds_x = (int)g.lds_x;
   a.bn_part = ep->bn_part;
+  if (ep->bn_part && ep->bn_z) {
+    if (!ep->bn_mean || !ep->bn_rstd || !ep->bn_gamma || !ep->bn_beta || ep->bn_z_cstride < d->out_c || ep->bn_z_cstride % 8 ||
+        (long)d->n * d->out_h * d->out_w * ep->bn_z_cstride * 2 >= (1L << 31)) {
+      set_error("conv2d_fwd: BatchNorm-backward partials need z (channel stride >= out_c, 8-aligned, < 2 GiB) and its statistics");
+      return CLIMSR_EINVAL;
+    }
+    a.bz = ep->bn_z; a.bz_cs = ep->bn_z_cstride; a.bslope = ep->bn_slope;
+    a.bmean = ep->bn_mean; a.brstd = ep->bn_rstd; a.bgamma = ep->bn_gamma; a.bbeta = ep->bn_beta;
+  }
   int rows = climsr_conv_packed_rows(d->out_c);
   int ncob = rows / (g.nt * 16);
   hipStream_t s = (hipStream_t)stream;
-  if (ep->bn_part && !bn_parts_ok(d, a, g)) {
+  if (ep->bn_part && !(ep->bn_z ? bn_bwd_parts_ok(d, ep, a, g) : bn_parts_ok(d, a, g))) {
     set_error("conv2d_fwd: BatchNorm partials only for the 16x16-tile bf16 paths (climsr_conv2d_fwd_bn_parts)");
     return CLIMSR_EINVAL;
   }
@@ -2866,7 +2992,8 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
         case 3: return launch_fwd_ep<4, 4, 6, 9, 3>(a, ncob, g.lds_total, s);
         case 6: return launch_fwd_ep<4, 4, 6, 9, 6>(a, ncob, g.lds_total, s);
         case 7: return launch_fwd_ep<4, 4, 6, 9, 7>(a, ncob, g.lds_total, s);
-        case 8: return a.bn_part ? launch_fwd_ep<4, 4, 6, 9, 9>(a, ncob, g.lds_total, s) : launch_fwd_ep<4, 4, 6, 9, 8>(a, ncob, g.lds_total, s);
+        case 8: return a.bz ? launch_fwd_ep<4, 4, 6, 9, 10>(a, ncob, g.lds_total, s)
+                       : a.bn_part ? launch_fwd_ep<4, 4, 6, 9, 9>(a, ncob, g.lds_total, s) : launch_fwd_ep<4, 4, 6, 9, 8>(a, ncob, g.lds_total, s);
         default: return launch_fwd<4, 4, 6, 9>(a, ncob, g.lds_total, s);
       }
     }
@@ -3182,8 +3309,10 @@ struct W64 {
 
 // TS = 2: 8 waves, wave w owns ci block w & 3 and taps [0,5) or [5,9) (w >> 2): 20 accumulators instead of 36, so
 // two waves share each SIMD (latency hiding) at the price of each wave re-reading the shared dz fragments.
-template <int TS, int S = 1>
-__global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
+// G (TS 1, S 1): the LDS-DMA form -- see conv_wgrad64_glds_kernel below.
+template <int TS, int S, bool G>
+__device__ __forceinline__ void wgrad64_body(const WgArgs& a) {
+  static_assert(!G || (TS == 1 && S == 1), "LDS-DMA form: 256 threads, stride 1");
   constexpr int NTHR = 256 * TS, NU = TS == 1 ? 9 : 5;
   constexpr int TH = W64<S>::TH, TPW = W64<S>::TPW, NZ = W64<S>::NZ, NX = W64<S>::NX, XP = W64<S>::XP;
   extern __shared__ __attribute__((aligned(16))) char smem[];  // TS 1: two buffers of W64<S>::LDS
@@ -3321,6 +3450,124 @@ __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
   };
   constexpr int NK = TH * TW / 32;  // 4 (stride 1) or 2 (stride 2): even
   int tile = split;
+  if constexpr (G) {
+    // LDS-DMA staging: buffer_load ... lds writes each wave-instruction's 64 x 16 B straight into LDS at
+    // (wave-uniform base + 16 lane), so the tiles need no registers, no ds_write pass and no VALU to move them,
+    // and three buffers keep two tiles in flight (the register path held one tile in 40 VGPRs, and with two whole
+    // fragment sets its 160 accumulators overflowed into AGPR copies: 4.5 VALU per MFMA).  Images are lane-linear:
+    // lane l of an instruction fills pixel slot 8 i + (l >> 3), 16 B position l & 7, with that pixel's channel chunk
+    // (l & 7) ^ (column & 7) -- an XOR swizzle chosen on the global (source) side that spreads the 8 pixels of a
+    // transposed fragment read over all 64 banks, as the register path's 80-element pitch did.
+    constexpr int ZB = TH * TW * 128, XB = 24 * 1024, BUF = ZB + XB, NXP = W64<1>::TPH * TPW;
+    const int l8 = lane >> 3, c8 = lane & 7, wv = tid >> 6;
+    // dz: wave w issues instructions w + 4 j (j < 4): tile row (w >> 1) + 2 j, column 8 (w & 1) + l8
+    const int zcol = 8 * (wv & 1) + l8, zrow0 = wv >> 1;
+    const uint32_t zrow_b = (uint32_t)a.out_w * a.dz_cs * 2;
+    const uint32_t z_lane = (uint32_t)((zcol * a.dz_cs + co0 + 8 * (c8 ^ (zcol & 7))) * 2) + (uint32_t)zrow0 * zrow_b;
+    const __amdgpu_buffer_rsrc_t zrs = buf_rsrc(a.dz, (uint32_t)((long)a.n * a.out_h * a.out_w * a.dz_cs * 2));
+    // x: instructions w + 4 j (j < 6): footprint pixel 8 (w + 4 j) + l8 of the 10 x 18 footprint (180 pixels; the
+    // slots past it get zeros): (row << 16) | (column << 8) | source chunk
+    int xrc[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int P = 8 * (wv + 4 * j) + l8, row = P < NXP ? P / TPW : 1023, cx = P % TPW;
+      xrc[j] = (row << 16) | (cx << 8) | (c8 ^ (cx & 7));
+    }
+    const uint32_t ximg_b = (uint32_t)a.in_h * a.in_w * a.in_cs * 2, pxb = (uint32_t)a.in_cs * 2;
+    const uint32_t x_ch = (uint32_t)((a.in_co + ci0) * 2);
+    const __amdgpu_buffer_rsrc_t xrs = buf_rsrc(a.x, (uint32_t)((long)a.n * a.in_h * a.in_w * a.in_cs * 2));
+    const int s_x = a.nsplit % a.tiles_x, s_y = (a.nsplit / a.tiles_x) % a.tiles_y, s_n = a.nsplit / (a.tiles_x * a.tiles_y);
+    int ntx = split % a.tiles_x, nty = (split / a.tiles_x) % a.tiles_y, nn = split / (a.tiles_x * a.tiles_y);
+    // in asm, not __builtin_amdgcn_raw_ptr_buffer_load_lds: hipcc treats the builtin as an LDS write of unknown
+    // extent and waits vmcnt(0) before the next ds_read, i.e. for the tile just requested; hidden from it, the DMAs
+    // are counted by hand (vmcnt(10) below) and drained before the epilogue.  M0 (the wave's LDS destination) is set
+    // and restored inside the statement.
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
+    const int wvu = __builtin_amdgcn_readfirstlane(wv);  // provably wave-uniform: the LDS destination is an "s" operand
+    auto glds = [&](__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t lds) {
+      uint32_t keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(off), "s"(r), "s"(lds) : "memory");
+    };
+    auto issue = [&](bool live, int b) {  // the tile at (ntx, nty, nn) into buffer b (zeros if !live), then advance
+      const int tx = ntx, ty = nty, nimg = nn;
+      ntx += s_x;
+      int c = ntx >= a.tiles_x;
+      ntx -= c ? a.tiles_x : 0;
+      nty += s_y + c;
+      c = nty >= a.tiles_y;
+      nty -= c ? a.tiles_y : 0;
+      nn += s_n + c;
+      const int oy0 = ty * TH, ox0 = tx * TW;
+      const uint32_t zb = lds0 + (uint32_t)(b * BUF);
+      const uint32_t zt = (uint32_t)(((nimg * a.out_h + oy0) * a.out_w + ox0) * a.dz_cs * 2) + z_lane;
+      const bool zok = live & (ox0 + zcol < a.out_w);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool ok = zok & (oy0 + zrow0 + 2 * j < a.out_h);
+        glds(zrs, ok ? zt + (uint32_t)(2 * j) * zrow_b : BUF_OOB, zb + (uint32_t)((wvu + 4 * j) * 1024));
+      }
+      const uint32_t iy0 = (uint32_t)(oy0 - a.pad), ix0 = (uint32_t)(ox0 - a.pad), xt = (uint32_t)nimg * ximg_b + x_ch;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        const uint32_t iy = iy0 + (uint32_t)(xrc[j] >> 16), ix = ix0 + (uint32_t)((xrc[j] >> 8) & 255);
+        const bool ok = live & (iy < (uint32_t)lh) & (ix < (uint32_t)lw);
+        const uint32_t off = xt + ((iy >> upsh) * (uint32_t)a.in_w + (ix >> upsh)) * pxb + (uint32_t)((xrc[j] & 7) * 16);
+        glds(xrs, ok ? off : BUF_OOB, zb + (uint32_t)(ZB + (wvu + 4 * j) * 1024));
+      }
+    };
+    // fragment reads: k-step kk, lane (g, q, p) = output pixel c0 = 4 g + q of rows 2 kk (k0) and 2 kk + 1 (k1),
+    // channels 4 p.. of the 16-channel group: dz group t (chunk 2 t + (p >> 1)), x group wave (chunk 2 wave + (p >> 1))
+    const int c0 = 4 * g + q;
+    int zoff[4], xoff[3];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) zoff[t] = c0 * 128 + (((2 * t + (p >> 1)) ^ (c0 & 7)) << 4) + 8 * (p & 1);
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) xoff[dx] = (c0 + dx) * 128 + (((2 * wave + (p >> 1)) ^ ((c0 + dx) & 7)) << 4) + 8 * (p & 1);
+    auto ld_af = [&](const char* zb, int kk, bf16x8 (&af)[4]) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) af[t] = cat_tr(ds_read_tr16(zb + kk * 32 * 128 + zoff[t]), ds_read_tr16(zb + (kk * 32 + 16) * 128 + zoff[t]));
+    };
+    auto ld_bf = [&](const char* xb, int kk, int u) {
+      const int dy = u / 3, dx = u % 3;
+      return cat_tr(ds_read_tr16(xb + (2 * kk + dy) * TPW * 128 + xoff[dx]), ds_read_tr16(xb + (2 * kk + 1 + dy) * TPW * 128 + xoff[dx]));
+    };
+    issue(tile < a.ntiles, 0);
+    issue(tile + a.nsplit < a.ntiles, 1);
+    int cur = 0;
+    for (; tile < a.ntiles; tile += a.nsplit) {
+      // this tile's 10 DMAs (per wave) have landed once at most the next tile's 10 are outstanding; the barrier makes
+      // that true for every wave, and every wave is past its reads of the tile before last (buffer (cur + 2) % 3)
+      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      issue(tile + 2 * a.nsplit < a.ntiles, cur == 0 ? 2 : cur - 1);
+      const char* zb = smem + cur * BUF;
+      const char* xb = zb + ZB;
+      // the 36 (k-step, tap) groups of 4 MFMAs read their x fragment from a 3-register ring loaded 2 groups ahead,
+      // the next k-step's dz fragments half-way through the current one (one whole fragment set: 56 registers)
+      bf16x8 af[2][4], bq[3];
+      ld_af(zb, 0, af[0]);
+      bq[0] = ld_bf(xb, 0, 0);
+      bq[1] = ld_bf(xb, 0, 1);
+#pragma unroll
+      for (int gi = 0; gi < NK * 9; ++gi) {
+        const int kk = gi / 9, u = gi % 9, gn = gi + 2;
+        if (gn < NK * 9) bq[gn % 3] = ld_bf(xb, gn / 9, gn % 9);
+        if (u == 4 && kk + 1 < NK) ld_af(zb, kk + 1, af[(kk + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (u == 0) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) accb[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk & 1][t], ones, accb[t], 0, 0, 0);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk & 1][t], bq[gi % 3], acc[t][u], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      cur = cur == 2 ? 0 : cur + 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the two DMAs past the last tile (zeros) land before the
+                                                        // epilogue staging reuses the buffers
+  } else {
   issue(tile < a.ntiles);
   if constexpr (TS == 1) {
     // double-buffered LDS, one barrier per tile: tile t+1 (in registers since tile t-1) is written to the other
@@ -3333,23 +3580,6 @@ __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
     issue(tile + a.nsplit < a.ntiles);
     lds_barrier();
     int cur = 0;
-        if (u == 0) {
-#pragma unroll
-          for (int t = 0; t < 4; ++t) accb[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk & 1][t], ones, accb[t], 0, 0, 0);
-        }
-#pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk & 1][t], bq[gi % RING], acc[t][u], 0, 0, 0);
-#endif
-        if (gi == 2) {
-          stash(cur ^ 1);
-          issue(tile + 2 * a.nsplit < a.ntiles);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      lds_barrier();  // this tile's reads of buffer cur and the stash of buffer cur ^ 1 are done
-      cur ^= 1;
-    }
-#else
     for (; tile < a.ntiles; tile += a.nsplit) {
       bf16x8 afA[4], bfA[NU], afB[4], bfB[NU];
       frags(cur, 0, afA, bfA);
@@ -3382,6 +3612,7 @@ __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
       }
     }
   }
+  }
   // C[row = co][col = ci]: lane holds co = co0 + 16t + 4g + i, ci = ci0 + 16 wave + col.  The workgroup's slab block
   // (64 co rows x 576 contiguous floats each) is assembled in LDS and written with coalesced 16 B stores (the direct
   // form issued 144 scattered 4 B stores per lane, 36 B apart)
@@ -3408,6 +3639,15 @@ __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
   }
 }
 constexpr size_t W64_EP_LDS = (size_t)64 * (9 * 64 + 4) * 4;  // the slab staging of conv_wgrad64_kernel
+constexpr size_t W64G_LDS = (size_t)3 * (8 * 16 * 128 + 24 * 1024);  // three LDS-DMA tile buffers (G form)
+
+template <int TS, int S = 1>
+__global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
+  wgrad64_body<TS, S, false>(a);
+}
+// at most 256 registers (one workgroup per CU either way: 148 KB of LDS): the accumulators stay in VGPRs -- the
+// 512-register form kept some of them in AGPRs and shuffled them every tile
+__global__ __launch_bounds__(256, 2) void conv_wgrad64_glds_kernel(WgArgs a) { wgrad64_body<1, 1, true>(a); }
 
 // ------------------------------------------------------------------------------------------
 // Weight gradient of a 1x1 conv with 64 inputs and <= 64 outputs (srcnn.conv2): dW[co][ci] = sum_p dz[p][co]
@@ -3799,7 +4039,7 @@ extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, c
       set_error("conv2d_wgrad: operands over 2 GiB (split the batch)");
       return CLIMSR_EINVAL;
     }
-    WgArgs a;
+    WgArgs a{};
     a.x = x; a.dz = dz; a.part = partial; a.bpart = bias_partial;
     a.n = d->n; a.in_h = d->in_h; a.in_w = d->in_w; a.in_c = d->in_c; a.in_cs = d->in_cstride; a.in_co = d->in_coff;
     a.up = d->up; a.ks = 3; a.stride = 1; a.pad = 1; a.out_h = d->out_h; a.out_w = d->out_w;
@@ -3816,6 +4056,7 @@ extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, c
       (void)hipFuncSetAttribute((const void*)conv_wgrad64_kernel<1, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       (void)hipFuncSetAttribute((const void*)conv_wgrad64_kernel<2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       (void)hipFuncSetAttribute((const void*)conv_wgrad64_kernel<1, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)conv_wgrad64_glds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       attr_set = true;
     }
     a.xcd = env_flag("CLIMSR_W64_XCD", 1);
@@ -3828,6 +4069,10 @@ extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, c
       a.tph = W64<1>::TPH; a.tpw = W64<1>::TPW;
       if (dry_run("conv_wgrad64_kernel<2, 1>")) return CLIMSR_OK;
       hipLaunchKernelGGL((conv_wgrad64_kernel<2, 1>), grid, dim3(512), std::max(W64<1>::LDS, W64_EP_LDS), (hipStream_t)stream, a);
+    } else if (env_flag("CLIMSR_W64_GLDS", 1)) {
+      a.tph = W64<1>::TPH; a.tpw = W64<1>::TPW;
+      if (dry_run("conv_wgrad64_glds_kernel")) return CLIMSR_OK;
+      hipLaunchKernelGGL(conv_wgrad64_glds_kernel, grid, dim3(256), std::max(W64G_LDS, W64_EP_LDS), (hipStream_t)stream, a);
     } else {
       a.tph = W64<1>::TPH; a.tpw = W64<1>::TPW;
       if (dry_run("conv_wgrad64_kernel<1, 1>")) return CLIMSR_OK;
@@ -3841,7 +4086,7 @@ extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, c
     set_error("conv2d_wgrad: LDS %zu too large", w.lds_total);
     return CLIMSR_EINVAL;
   }
-  WgArgs a;
+  WgArgs a{};
   a.x = x; a.dz = dz; a.part = partial; a.bpart = bias_partial;
   a.n = d->n; a.in_h = d->in_h; a.in_w = d->in_w; a.in_c = d->in_c; a.in_cs = d->in_cstride; a.in_co = d->in_coff;
   a.up = d->up; a.ks = d->ks; a.stride = d->stride; a.pad = d->pad; a.out_h = d->out_h; a.out_w = d->out_w;

@@ -443,6 +443,27 @@ extern "C" int climsr_bn_backward_z(const void* da, int da_bf16, const uint16_t*
   return check_launch("bn_backward_z");
 }
 
+// climsr_bn_backward_z with the statistics pass replaced by the producing data gradient's epilogue partials
+// (ClimsrEpilogue.bn_z / bn_part, nparts = climsr_conv2d_fwd_bn_parts): finish + apply only.
+extern "C" int climsr_bn_backward_parts(const double* parts, int64_t nparts, const uint16_t* da, const uint16_t* z, int64_t npix,
+                                        int c, const float* mean, const float* rstd, const float* gamma, const float* beta,
+                                        float slope, float* coef, float* dgamma, float* dbeta, int accumulate, uint16_t* dz,
+                                        void* stream) {
+  if (!parts || nparts <= 0 || nparts > (1L << 30) || !da || !z || !mean || !rstd || !gamma || !beta || !coef || !dz ||
+      !bn_shape_ok(npix, c)) {
+    set_error("bn_backward_parts: bad args (c=%d, npix=%lld, parts=%lld)", c, (long long)npix, (long long)nparts);
+    return CLIMSR_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(bn_bwd_finish_kernel, dim3(ceil_div(c, 8)), dim3(256), 0, s, parts, (int)nparts, c, (int)npix, gamma, rstd,
+                     dgamma, dbeta, accumulate, coef);
+  int per;
+  const int nb = bn_apply_grid(npix, c, &per);
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<uint16_t, true>), dim3(nb), dim3(256), 0, s, (int)npix, c, per, da, nullptr, z, mean, rstd,
+                     gamma, beta, coef, slope, 1.f, dz);
+  return check_launch("bn_backward_parts");
+}
+
 // ---------------------------------------------------------------------------------------------
 // nn.AdaptiveAvgPool2d((oh, ow)) on NHWC bf16, output flattened in torch's NCHW order
 // (torch.flatten(out, 1), rfb_esrgan.py:65-66): out[n][(c*oh + i)*ow + j]; optional transposed

@@ -167,6 +167,7 @@ class _DEngine:
         coef = self._scr("bncoef", (3 * 512,), torch.float32, dev)
         dx = None
         dz_next = None  # layer 0's output gradient, written directly by layer 1's data gradient
+        fused = {}  # layer -> (part, nparts): its BN backward statistics, from the next layer's data-gradient epilogue
         for li in reversed(range(len(self.layers))):
             conv, bn, plan = self.layers[li]
             L = sv["layers"][li]
@@ -177,9 +178,14 @@ class _DEngine:
                 # lrelu'(a) recomputed from z: the activation is not read; da is the bf16 data gradient of the
                 # next conv (fp32 only for the last layer, from the pooling backward)
                 dz = _bf16((n, oh, ow, cz), dev)
-                ops.bn_backward_z(da, L["z"], npix, c, L["mean"], L["rstd"], bn.weight, bn.bias,
-                                  ops.bn_workspace(npix, c, self.scratch, dev), coef,
-                                  bn.weight.grad if need_w else None, bn.bias.grad if need_w else None, acc, dz)
+                if li in fused:
+                    part, nparts = fused.pop(li)
+                    ops.bn_backward_parts(part, nparts, da, L["z"], npix, c, L["mean"], L["rstd"], bn.weight, bn.bias, coef,
+                                          bn.weight.grad if need_w else None, bn.bias.grad if need_w else None, acc, dz)
+                else:
+                    ops.bn_backward_z(da, L["z"], npix, c, L["mean"], L["rstd"], bn.weight, bn.bias,
+                                      ops.bn_workspace(npix, c, self.scratch, dev), coef,
+                                      bn.weight.grad if need_w else None, bn.bias.grad if need_w else None, acc, dz)
             elif dz_next is not None:
                 dz = dz_next
             else:
@@ -200,7 +206,17 @@ class _DEngine:
                     dz_next = g
                 elif li > 0:
                     g = _bf16((n, L["h_in"], L["w_in"], plan.cin), dev)  # bf16: read by the previous layer's BN backward
-                    plan.dgrad(dz, cz, oh, ow, g, plan.cin, 0, n)
+                    P = sv["layers"][li - 1]
+                    # that BN's backward statistics (sum d, sum d * xhat) come from this data gradient's epilogue
+                    # where its kernel supports them: the separate statistics pass over g and z is skipped
+                    nparts = plan.dgrad_bn_parts(cz, oh, ow, plan.cin, n, plan.cin) if P["mean"] is not None else 0
+                    if nparts:
+                        part = self._scr(f"bnbwd{li - 1}", (nparts * 2 * plan.cin,), torch.float64, dev)
+                        plan.dgrad(dz, cz, oh, ow, g, plan.cin, 0, n,
+                                   bn_bwd=(part, P["z"], plan.cin, P["mean"], P["rstd"], prev_bn.weight, prev_bn.bias))
+                        fused[li - 1] = (part, nparts)
+                    else:
+                        plan.dgrad(dz, cz, oh, ow, g, plan.cin, 0, n)
                 else:
                     g = _f32((n, L["h_in"], L["w_in"], plan.cin), dev)
                     plan.dgrad(dz, cz, oh, ow, g, plan.cin, 0, n)

@@ -171,12 +171,15 @@ class ConvPlan:
     def dgrad(self, dz: torch.Tensor, dz_cs: int, out_h: int, out_w: int, g: torch.Tensor, g_cs: int, g_co: int, n: int,
               accumulate: bool = False, down2: bool = False, cout_t: Optional[int] = None, aux: Optional[torch.Tensor] = None,
               aux_cs: int = 0, aux_co: int = 0, aux_scale: float = 1.0, act: int = ACT_NONE, res1: Optional[torch.Tensor] = None,
-              res1_cs: int = 0, res1_co: int = 0) -> None:
+              res1_cs: int = 0, res1_co: int = 0, bn_bwd: Optional[tuple] = None) -> None:
         """Data gradient: g[:, :, :, g_co:g_co+cin_real] (+)= conv^T(dz); (out_h, out_w) are dz's dims.  g is fp32
         (= or += with accumulate), or bf16: then it is the NEXT layer's conv output gradient directly, with
         act = ACT_LRELU_BWD / ACT_RELU_BWD applied from that layer's stored activation res1.  With down2 the
         result is summed over 2x2 pixel blocks (backward of the nearest x2 upsample feeding this conv).
-        Stride-2 convs (pad 1, even input) run as a stride-1 conv over the zero-inserted dz."""
+        Stride-2 convs (pad 1, even input) run as a stride-1 conv over the zero-inserted dz.
+        bn_bwd = (part, z, z_cs, mean, rstd, gamma, beta): g (bf16) is dL/da of the previous BatchNorm + LeakyReLU(0.2)
+        layer and the epilogue writes that layer's backward statistics partials into part (fp64, dgrad_bn_parts() rows x 2
+        x cin) for bn_backward_parts."""
         ct = self.cout_t if cout_t is None else cout_t
         if (self.cout == 1 and self.stride == 1 and self.ks in (3, 5) and self.pad == self.ks // 2 and g.dtype == torch.bfloat16
                 and not down2 and aux is None and act in (ACT_NONE, ACT_LRELU_BWD, ACT_RELU_BWD) and ct == self.cin_real
@@ -190,18 +193,16 @@ class ConvPlan:
                                                        0.2, ptr(res1), res1_cs, res1_co, ptr(g), g_cs, g_co, _lib.stream_ptr()),
                 f"conv dgrad {self.name}"), "dgrad " + self.name, nbytes)
             return
-        pad_t = self.ks - 1 - self.pad
-        if self.stride == 1:  # input size = out + ks - 1 - 2 pad (== out for 'same' convs)
-            ih, iw = out_h + 2 * pad_t - self.ks + 1, out_w + 2 * pad_t - self.ks + 1
-            d = ConvDesc(n, out_h, out_w, self.cin_t, dz_cs, 0, 1, self.ks, 1, pad_t, ih, iw, ct, g_cs, g_co, self.cc_t)
-        else:  # stride 2: stride-1 conv over the zero-inserted gradient (logical size 2*out)
-            assert self.stride == 2 and not down2
-            ih, iw = 2 * out_h + 2 * pad_t - self.ks + 1, 2 * out_w + 2 * pad_t - self.ks + 1
-            d = ConvDesc(n, out_h, out_w, self.cin_t, dz_cs, 0, -2, self.ks, 1, pad_t, ih, iw, ct, g_cs, g_co, self.cc_t)
-        out_h, out_w = ih, iw
+        assert self.stride == 1 or not down2
+        d = self._dgrad_desc(dz_cs, out_h, out_w, g_cs, g_co, n, ct)
+        out_h, out_w = d.out_h, d.out_w
         mode = OUT_BF16 if g.dtype == torch.bfloat16 else (OUT_F32_ADD if accumulate else OUT_F32)
         ep = Epilogue(act, 0.2 if act == ACT_LRELU_BWD else 0.0, 1.0, ptr(res1), res1_cs, res1_co, 1.0, None, 0, 0, mode,
                       1 if down2 else 0, 0, 1.0, 1.0, aux_cs, ptr(aux), aux_co, aux_scale)
+        if bn_bwd is not None:
+            part, z, z_cs, mean, rstd, gamma, beta = bn_bwd
+            ep.bn_part, ep.bn_z, ep.bn_z_cstride, ep.bn_slope = ptr(part), ptr(z), z_cs, 0.2
+            ep.bn_mean, ep.bn_rstd, ep.bn_gamma, ep.bn_beta = ptr(mean), ptr(rstd), ptr(gamma), ptr(beta)
         # algorithmic: the forward's FLOPs (stride 2: the zero-inserted taps are not work)
         flops = 2 * self.cout * ct * self.ks * self.ks * n * out_h * out_w // (self.stride * self.stride)
         gpx = n * out_h * out_w // (4 if down2 else 1)  # result pixels (after the 2x2 sum)
@@ -210,6 +211,23 @@ class ConvPlan:
         _run(_kname(d, None, ep), flops, lambda: check(
             _lib.load().climsr_conv2d_fwd(ctypes.byref(d), ptr(dz), ptr(self.wpk_t), None, ctypes.byref(ep), ptr(g),
                                           _lib.stream_ptr()), f"conv dgrad {self.name}"), "dgrad " + self.name, nbytes)
+
+    def _dgrad_desc(self, dz_cs, out_h, out_w, g_cs, g_co, n, ct):
+        pad_t = self.ks - 1 - self.pad
+        if self.stride == 1:  # input size = out + ks - 1 - 2 pad (== out for 'same' convs)
+            ih, iw = out_h + 2 * pad_t - self.ks + 1, out_w + 2 * pad_t - self.ks + 1
+            return ConvDesc(n, out_h, out_w, self.cin_t, dz_cs, 0, 1, self.ks, 1, pad_t, ih, iw, ct, g_cs, g_co, self.cc_t)
+        # stride 2: stride-1 conv over the zero-inserted gradient (logical size 2*out)
+        assert self.stride == 2
+        ih, iw = 2 * out_h + 2 * pad_t - self.ks + 1, 2 * out_w + 2 * pad_t - self.ks + 1
+        return ConvDesc(n, out_h, out_w, self.cin_t, dz_cs, 0, -2, self.ks, 1, pad_t, ih, iw, ct, g_cs, g_co, self.cc_t)
+
+    def dgrad_bn_parts(self, dz_cs: int, out_h: int, out_w: int, g_cs: int, n: int, z_cs: int) -> int:
+        """Rows of BatchNorm-backward partials dgrad(..., bn_bwd=...) writes for a bf16 g, 0 if its kernel cannot."""
+        d = self._dgrad_desc(dz_cs, out_h, out_w, g_cs, 0, n, self.cout_t)
+        ep = Epilogue(ACT_NONE, 0.0, 1.0, None, 0, 0, 1.0, None, 0, 0, OUT_BF16, 0, 0, 1.0, 1.0, 0, None, 0, 1.0, 1)
+        ep.bn_z, ep.bn_z_cstride = 1, z_cs
+        return int(_lib.load().climsr_conv2d_fwd_bn_parts(ctypes.byref(d), ctypes.byref(ep)))
 
     @property
     def cin_w(self) -> int:
@@ -528,6 +546,14 @@ def bn_backward(da, a, z, npix, c, mean, rstd, gamma, ws, coef, dgamma, dbeta, a
         _L().climsr_bn_backward(ptr(da), ptr(a), ptr(z), npix, c, ptr(mean), ptr(rstd), ptr(gamma), slope, out_slope, ptr(ws),
                                 ptr(coef), ptr(dgamma), ptr(dbeta), int(accumulate), ptr(dz), _lib.stream_ptr()), "bn_backward"),
          "bn_backward", npix * c * 18)
+
+
+def bn_backward_parts(parts, nparts, da, z, npix, c, mean, rstd, gamma, beta, coef, dgamma, dbeta, accumulate, dz, slope=0.2):
+    """bn_backward_z (bf16 da) with the statistics from the producing data gradient's epilogue (ConvPlan.dgrad bn_bwd)."""
+    _run("bn_backward", 0, lambda: check(
+        _L().climsr_bn_backward_parts(ptr(parts), nparts, ptr(da), ptr(z), npix, c, ptr(mean), ptr(rstd), ptr(gamma), ptr(beta), slope,
+                                      ptr(coef), ptr(dgamma), ptr(dbeta), int(accumulate), ptr(dz), _lib.stream_ptr()),
+        "bn_backward_parts"), "bn_backward", npix * c * 6)
 
 
 def bn_backward_z(da, z, npix, c, mean, rstd, gamma, beta, ws, coef, dgamma, dbeta, accumulate, dz, slope=0.2):

@@ -74,6 +74,18 @@ typedef struct ClimsrEpilogue {
   double* bn_part;              /* optional (plain bf16 output only): per-tile BatchNorm partials [tiles][2][out_c] (sum, sum of
                                    squares of the stored bf16 values) for climsr_bn_forward_parts; tiles and support from
                                    climsr_conv2d_fwd_bn_parts */
+  /* BatchNorm-backward partials instead (bn_part and bn_z set; a data gradient whose output is dL/da of a BatchNorm +
+     LeakyReLU(bn_slope) layer a = lrelu(BN(z))): bn_part[tile][0][c] = sum of d, [tile][1][c] = sum of d * xhat over the
+     tile, d = out * lrelu'(z * gamma*rstd + (beta - mean*gamma*rstd)) with out bf16-rounded as stored, xhat = (z - mean) *
+     rstd -- the statistics climsr_bn_backward's own pass would compute (rfb_esrgan.py:32-50's BatchNorm2d backward);
+     finish with climsr_bn_backward_parts.  z: bf16 NHWC over the output's pixels, channel stride bn_z_cstride. */
+  const uint16_t* bn_z;
+  int32_t bn_z_cstride;
+  float bn_slope;
+  const float* bn_mean;
+  const float* bn_rstd;
+  const float* bn_gamma;
+  const float* bn_beta;
 } ClimsrEpilogue;
 
 const char* climsr_last_error(void);
@@ -268,6 +280,13 @@ int climsr_bn_forward(const uint16_t* z, int64_t npix, int c, const float* gamma
 int climsr_bn_forward_parts(const double* parts, int64_t nparts, const uint16_t* z, int64_t npix, int c, const float* gamma,
                             const float* beta, int act, float slope, float eps, float momentum, float* mean, float* rstd,
                             float* run_mean, float* run_var, int64_t* num_batches_tracked, uint16_t* y, void* stream);
+
+/* climsr_bn_backward_z (bf16 da) with the statistics pass replaced by the producing data gradient's epilogue partials
+ * (ClimsrEpilogue.bn_z + bn_part, nparts = climsr_conv2d_fwd_bn_parts with bn_z set): dgamma / dbeta and
+ * dz = gamma*rstd * (d - mean(d) - xhat * mean(d*xhat)).  Replaces the BatchNorm2d backward of rfb_esrgan.py:32-50. */
+int climsr_bn_backward_parts(const double* parts, int64_t nparts, const uint16_t* da, const uint16_t* z, int64_t npix, int c,
+                             const float* mean, const float* rstd, const float* gamma, const float* beta, float slope, float* coef,
+                             float* dgamma, float* dbeta, int accumulate, uint16_t* dz, void* stream);
 /* Eval-mode BN (running statistics) + activation (nn.BatchNorm2d.eval()). */
 int climsr_bn_inference(const uint16_t* z, int64_t npix, int c, const float* run_mean, const float* run_var, float eps,
                         const float* gamma, const float* beta, int act, float slope, uint16_t* y, void* stream);

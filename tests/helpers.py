@@ -90,12 +90,25 @@ def rel_l2(a, b):
     return float((a - b).norm() / (b.norm() + 1e-30))
 
 
-def update_envelope(native, ref64, amps, floor=2e-2):
+def pool_small(tensors, below):
+    """The dict with every tensor of fewer than `below` elements replaced by one concatenated entry (key order): a
+    16-element bias gradient's relative error is a handful of sign-random terms, pooled it is a statistic."""
+    big = {k: v for k, v in tensors.items() if v.numel() >= below}
+    small = [v.reshape(-1).double() for k, v in tensors.items() if v.numel() < below]
+    if small:
+        big[f"<{len(small)} tensors under {below} elements>"] = torch.cat(small)
+    return big
+
+
+def update_envelope(native, ref64, amps, floor=2e-2, pool_below=0):
     """Per tensor: the relative L2 distance of the native update (or gradient) from the fp64 oracle's must stay within
     2x the reduced-precision spread of the same quantity -- the larger of the oracle's own torch-autocast fp16 / bf16
     runs' distances from it (the reference trains with precision 16) and of those two runs' distance from each other
     (two equally valid reduced-precision runs: the noise level of the statistic itself, which for a small tensor is a
-    few sign flips of Adam's ~lr*sign(grad) first steps) -- or ``floor``.  Returns (offenders, worst, per-tensor table)."""
+    few sign flips of Adam's ~lr*sign(grad) first steps) -- or ``floor``.  pool_below: tensors under that many elements
+    are compared as one pooled vector (pool_small).  Returns (offenders, worst, per-tensor table)."""
+    if pool_below:
+        native, ref64, amps = pool_small(native, pool_below), pool_small(ref64, pool_below), [pool_small(a, pool_below) for a in amps]
     rows = {}
     for k, want in ref64.items():
         rel = rel_l2(native[k], want)
