@@ -318,6 +318,7 @@ struct FwdArgs {
   int lds_tab, lds_x;
   double* bn_part;  // EP 9: per-tile BatchNorm partial sums [tile][2][out_c] of the bf16 outputs (climsr_conv2d_fwd_bn_parts)
   int xgrp;         // > 0: 1-D grid in XCD-major (channel-block group, tile, channel block) order, xgrp blocks a group
+  int stag_lo, stag_hi, stag_n;  // blocks [stag_lo, stag_hi) start stag_n x 2048 cycles late (see conv_fwd_body)
   // EP 10: BatchNorm-backward partials of the stored data gradient (ClimsrEpilogue.bn_z ...) into bn_part
   const uint16_t* bz;
   int bz_cs;
@@ -601,7 +602,7 @@ __device__ __forceinline__ void bn_tile_partials(const FwdArgs& a, float* ssum, 
 // loaded into registers while chunk j is on the MFMA pipe, so a multi-chunk tile (RDB conv5 / pull-x: four
 // 32-channel chunks) pays one staging latency instead of one per chunk.
 #ifndef CLIMSR_DIAG_MODE
-#define CLIMSR_DIAG_MODE 0  // diagnostic builds only: 1 = every chunk computed twice, 2 = one staging, compute only,
+#define CLIMSR_DIAG_MODE 0  // diagnostic builds only: 4 = GEO k-loop MFMAs without per-k-step fragment reads, 1 = every chunk computed twice, 2 = one staging, compute only,
                             // 3 = staging only (GEO 1)
 #endif
 // GEO (host-checked geometry specialisation, 0 = runtime geometry): 1 / 2 = 3x3 taps over 32-channel chunks at
@@ -624,6 +625,13 @@ __device__ __forceinline__ void conv_fwd_body(const FwdArgs& a) {
 
   // (tile, output-channel block): blockIdx, or with xgrp the XCD-major order in which the xgrp channel blocks of a
   // tile are consecutive on one XCD (the x tile is fetched into that L2 once for all of them, not once per XCD)
+  // Stagger: the two workgroups that share a CU run the same program and start together, so they stage (global
+  // loads, LDS stores, barriers) and compute (MFMA) in lockstep -- diagnostic builds measured staging + MFMA-only
+  // times that simply add (VGG 256 @64^2: 141 + 147 us = 288 us).  The second workgroup of each CU (the second
+  // dispatch round, [stag_lo, stag_hi)) starts about half a chunk late; the blocks that replace them inherit the
+  // offset.  Speed only: nothing depends on which workgroups share a CU.
+  if (a.stag_n && (int)blockIdx.x >= a.stag_lo && (int)blockIdx.x < a.stag_hi)
+    for (int i = 0; i < a.stag_n; ++i) __builtin_amdgcn_s_sleep(32);
   int tile_id = blockIdx.x, cob = blockIdx.y;
   if (a.xgrp > 0) {
     const int ntile = a.tiles_x * a.tiles_y * a.n, idx = xcd_major(blockIdx.x, gridDim.x);
@@ -703,7 +711,11 @@ __device__ __forceinline__ void conv_fwd_body(const FwdArgs& a) {
       ld(0, 0);
 #pragma unroll
       for (int k = 0; k < 9; ++k) {
+#if CLIMSR_DIAG_MODE == 4  // diagnostic build 4: the k-step fragments read once per chunk, MFMAs only
+        if (k == 0) ld(1, 1);
+#else
         if (k + 1 < 9) ld(k + 1, (k + 1) & 1);
+#endif
         // the next k-step's NT + MW fragment reads go out as one burst ahead of this k-step's MW x NT MFMAs (the
         // compiler otherwise sinks each read next to its first MFMA and waits lgkmcnt(0) there: the LDS latency was
         // exposed at nearly every k-step of the unrolled loop)
@@ -2388,8 +2400,9 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_s2_kernel(FwdArgs a) {
     return ok ? ((long)nimg * a.out_h + py) * a.out_w + pxx : 0;
   };
   uint4 r1[4][4];
-  // EP 10: the BatchNorm-backward partials of the stored dx (store_tile_lds EP 10): z is loaded up front like the
-  // activation operand; the lane's 8 channels are the same for all of its items (64 % NG == 0)
+  // EP 10: the BatchNorm-backward partials of the stored dx (store_tile_lds EP 10): z is loaded per phase (not up
+  // front like the activation operand: 64 more registers beside the 128 accumulators spilled); the lane's 8
+  // channels are the same for all of its items (64 % NG == 0)
   const __amdgpu_buffer_rsrc_t rrz = opt_rsrc(EP == 10 ? (const void*)a.bz : nullptr);
   const int cgl = lane % NG;
   float bmu[8], brs[8], bsc[8], bsh[8], ssum[8], ssq[8];
@@ -2414,15 +2427,20 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_s2_kernel(FwdArgs a) {
         bool ok;
         const long pidx = item_pidx(ph, k, ok);
         r1[ph][k] = buf_load16(rr1, (uint32_t)((pidx * a.r1_cs + (ok ? a.r1_co + co0 + ((lane + 64 * k) % NG) * 8 : 0)) * 2));
-      } else if (EP == 10) {
-        bool ok;
-        const long pidx = item_pidx(ph, k, ok);
-        // (opt_rsrc has no range limit: a pixel outside the image reads pixel 0, whose d is 0)
-        r1[ph][k] = buf_load16(rrz, (uint32_t)((pidx * a.bz_cs + co0 + cgl * 8) * 2));
       }
     }
 #pragma unroll
   for (int ph = 0; ph < 4; ++ph) {
+    uint4 zv[4];
+    if constexpr (EP == 10) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        bool ok;
+        const long pidx = item_pidx(ph, k, ok);
+        // (opt_rsrc has no range limit: a pixel outside the image reads pixel 0, whose d is 0)
+        zv[k] = buf_load16(rrz, (uint32_t)((pidx * a.bz_cs + co0 + cgl * 8) * 2));
+      }
+    }
     __syncthreads();  // operands (first phase) / the previous phase's reads are done
 #pragma unroll
     for (int m = 0; m < MW; ++m)
@@ -2451,7 +2469,7 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_s2_kernel(FwdArgs a) {
       if constexpr (EP == 10) {
         Raw8 rr, rz;
         rr.lo = pk;
-        rz.lo = r1[ph][k];
+        rz.lo = zv[k];
         rr.hi = rz.hi = make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -2715,10 +2733,22 @@ static int conv_xcd_group(int ncob, long wblk_bytes) {
   return 0;
 }
 
+#define WIDE_GEO(pfx) ((pfx) == 18)
 template <int MW, int NT, int PFX, int PFW, int EP, int GEO>
 static int launch_fwd_geo(const FwdArgs& a0, int ncob, size_t lds, hipStream_t s) {
   FwdArgs a = a0;
   a.xgrp = GEO == 1 ? conv_xcd_group(ncob, (long)NT * 16 * a.kpk * 2) : 0;
+  {
+    static int ncu = 0, stag = -1;
+    if (!ncu) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+      if (ncu <= 0) ncu = 256;
+      stag = env_flag("CLIMSR_CONV_STAGGER", 0);
+    }
+    a.stag_lo = ncu; a.stag_hi = 2 * ncu; a.stag_n = GEO == 1 && !WIDE_GEO(PFX) ? stag : 0;
+  }
   const dim3 grid = a.xgrp ? dim3(a.tiles_x * a.tiles_y * a.n * ncob) : dim3(a.tiles_x * a.tiles_y * a.n, ncob);
   const size_t lds_ep = (size_t)4 * MW * 16 * (NT * 16 + 4) * 4;  // epilogue staging (aliases the operands)
   if (lds_ep > lds) lds = lds_ep;

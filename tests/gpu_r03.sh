@@ -17,10 +17,11 @@ run() {  # name, limit, command...
   timeout -k 10 "$lim" "$@"
 }
 set -o pipefail
-ok1() { local rc=$?; [ $rc -eq 0 ] || [ $rc -eq 1 ]; }  # pytest: 1 = tests failed (read the log), anything else = stop
+# pytest: 1 = tests failed (read the log) and the run goes on, unless the log shows a GPU fault; anything else = stop
+ok1() { local rc=$?; [ $rc -eq 0 ] || { [ $rc -eq 1 ] && ! grep -q -E "illegal memory access|HIP error|hipError|Memory access fault" "$1"; }; }
 { ! has new || { run new 900 $PYT ${NEW_TESTS:-tests/test_gpu_timed_step.py tests/test_gpu_ddp.py tests/test_gpu_gan.py::test_gan_step_vs_golden tests/test_gpu_configs.py::test_config1_trainer_steps_vs_golden} \
-    > gpurun_out/${T}_pytest_new.log 2>&1; ok1; }; } &&
-{ ! has suite || { run suite 1100 $PYT -m gpu tests > gpurun_out/${T}_pytest_gpu.log 2>&1; ok1; }; } &&
+    > gpurun_out/${T}_pytest_new.log 2>&1; ok1 gpurun_out/${T}_pytest_new.log; }; } &&
+{ ! has suite || { run suite 1100 $PYT -rP -m gpu tests > gpurun_out/${T}_pytest_gpu.log 2>&1; ok1 gpurun_out/${T}_pytest_gpu.log; }; } &&
 { ! has smoke || run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${T}_smoke.log 2>&1; } &&
 { ! has bench || run bench 600 python -u bench.py > gpurun_out/${T}_gan_bench.json 2> gpurun_out/${T}_gan_bench.err; } &&
 { ! has infer || run infer_esrgan 400 python -u bench.py --mode infer --model esrgan --steps 10 --warmup 3 --cpu-seconds 10 \
