@@ -10,7 +10,6 @@
 // MFMA: v_mfma_f32_16x16x32_bf16.  Lane l: A[row l&15][k 8(l>>4)+j], B[k 8(l>>4)+j][col l&15],
 // C[row 4(l>>4)+i][col l&15].
 #include <algorithm>
-#include <type_traits>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -1038,197 +1037,6 @@ __device__ __forceinline__ void conv_fwd_body(const FwdArgs& a) {
     bn_tile_partials(a, ssum, ssq, true, wave, lane, tile_id, co_blk0, (float*)smem);
   } else {
     store_tile_lds<RF, MW * 16, NT * 16, 64, EP>(a, eb, EPP, lane, nimg, oy0 + wave * MW, ox0, co_blk0);
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// K-split, persistent form of the GEO 1 conv (3x3, stride 1, 32-channel chunks, 16 x 16-pixel x 64-channel tiles).
-// The one-round kernel runs two 4-wave workgroups per CU, and diagnostic builds showed them in lockstep: staging
-// (global loads, LDS stores, barriers) and MFMA phases simply added up (VGG 256 @64^2: 141 + 147 us of 288).  Here
-// ONE 8-wave workgroup per CU owns each tile: waves w and w + 4 share SIMD w & 3 and the same 64 x 64 output
-// block, and split every chunk's 9 k-steps 5 / 4.  Both LDS buffers hold a chunk each (2 x 70 KB): chunk q is
-// computed from buffer q & 1 while chunk q + 1 (in registers since chunk q - 1) is stored into the other and chunk
-// q + 2 is requested -- the first half computes then stages, the second stages then computes, so each SIMD's
-// matrix pipe has one computing wave while its partner stages.  One barrier per chunk.  The workgroup walks
-// (tile, channel block) items persistently and the chunk sequence runs across items (the next item's first chunks
-// load during this one's last chunk and epilogue).  Per item: the second half's accumulators are added to the
-// first's through LDS, then the first half runs the usual epilogue.
-// ------------------------------------------------------------------------------------------
-constexpr int CKS_XB = 18 * 18 * 48 * 2;            // x tile of one chunk (bytes)
-constexpr int CKS_WB = 64 * (9 * 32 + WPAD) * 2;    // weight chunk
-constexpr int CKS_BUF = CKS_XB + CKS_WB;              // 70,912 B >= the 4-wave epilogue staging (69,632 B)
-constexpr int CKS_LDS = 2 * CKS_BUF;
-
-template <bool RF, int EP>
-__global__ __launch_bounds__(512, 1) void conv_fwd_ks_kernel(FwdArgs a, int nitems) {
-  constexpr int MW = 4, NT = 4, PFX = 3, PFW = 5;
-  constexpr int CV = 4, TPWc = TW + 2, CCPc = 48, NXV = (TW + 2) * (TW + 2) * CV, WV = 36, WPc = 9 * 32 + WPAD, NWV = NT * 16 * WV;
-  constexpr int EPP = NT * 16 + 4;
-  static_assert(PFX * 512 >= NXV && PFW * 512 >= NWV && 4 * MW * 16 * EPP * 4 <= CKS_BUF && 4 * 16 * 64 * 16 <= CKS_BUF,
-                "K-split geometry");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
-  // pixel-row group, k-step half (a readfirstlane'd h, i.e. scalar branches between the two programs, made hipcc
-  // spill 188 B per lane; the exec-masked form allocates 208 registers)
-  const int rw = wave & 3, h = wave >> 2;
-  const int ncob = a.out_c / 64, nch = a.nchunk;
-
-  // staging: thread vector i = (tid + 512 i); x vector = pixel (v >> 2) of the 18 x 18 tile, channel group
-  // (tid & 3) * 8; weight vector = row v / 36, 16 B column v % 36 of the 64 x 288 chunk.  Vectors past either image
-  // load zeros (out-of-range offsets) and are stored into pad channels no fragment reads.
-  const int cg8 = (tid & 3) * 8;
-  int xty[PFX], xtx[PFX], xl[PFX];
-#pragma unroll
-  for (int i = 0; i < PFX; ++i) {
-    const int v = tid + 512 * i, pix = v >> 2;
-    const bool in = v < NXV;
-    xty[i] = in ? pix / TPWc : 1 << 20;  // never in range
-    xtx[i] = pix % TPWc;
-    xl[i] = in ? pix * CCPc + cg8 : 32;  // past the tile: pad channels 32..39 of pixel 0
-  }
-  uint32_t wrel[PFW];
-  int wl[PFW];
-#pragma unroll
-  for (int i = 0; i < PFW; ++i) {
-    const int v = tid + 512 * i, r = v / WV, kv = v - r * WV;
-    const bool in = v < NWV;
-    wrel[i] = in ? (uint32_t)((r * a.kpk + kv * 8) * 2) : BUF_OOB;
-    wl[i] = in ? r * WPc + kv * 8 : 9 * 32;  // past the chunk: the pad of weight row 0
-  }
-  const __amdgpu_buffer_rsrc_t xr = buf_rsrc(a.x, (uint32_t)((long)a.n * a.in_h * a.in_w * a.in_cs * 2));
-  const __amdgpu_buffer_rsrc_t wr = buf_rsrc(a.w, (uint32_t)((long)ncob * NT * 16 * a.kpk * 2));
-  const uint32_t xrow_b = (uint32_t)a.in_w * a.in_cs * 2, ximg_b = (uint32_t)a.in_h * xrow_b, pxb = (uint32_t)a.in_cs * 2;
-
-  auto tile_xy = [&](int tile, int& nimg, int& oy0, int& ox0) {
-    const int tx = tile % a.tiles_x, r = tile / a.tiles_x, ty = r % a.tiles_y;
-    nimg = r / a.tiles_y;
-    oy0 = ty * 16;
-    ox0 = tx * TW;
-  };
-  uint4 px[PFX], pw[PFW];
-  auto issue = [&](int q) {  // chunk q of this workgroup's sequence (zeros past it)
-    const int k = q / nch, j = q - k * nch, it = blockIdx.x + k * gridDim.x;
-    const bool live = it < nitems;
-    const int tile = it / ncob, cob = it - tile * ncob;
-    int nimg, oy0, ox0;
-    tile_xy(live ? tile : 0, nimg, oy0, ox0);
-    // bounds as unsigned compares combined with & (no short-circuit branches in the chunk loop)
-    const uint32_t iy0 = live ? (uint32_t)(oy0 - a.pad) : 1u << 24, ix0 = (uint32_t)(ox0 - a.pad);  // pad 1, or 0
-                                                                                                     // (reflect-padded input)
-    const uint32_t xb = (uint32_t)nimg * ximg_b + (uint32_t)((a.in_co + j * 32 + cg8) * 2);
-#pragma unroll
-    for (int i = 0; i < PFX; ++i) {
-      const uint32_t iy = iy0 + (uint32_t)xty[i], ix = ix0 + (uint32_t)xtx[i];
-      const bool ok = (iy < (uint32_t)a.in_h) & (ix < (uint32_t)a.in_w);
-      px[i] = buf_load16(xr, ok ? xb + iy * xrow_b + ix * pxb : BUF_OOB);
-    }
-    const uint32_t wb = (uint32_t)((cob * NT * 16 * a.kpk + j * a.kcpad) * 2);
-#pragma unroll
-    for (int i = 0; i < PFW; ++i) pw[i] = buf_load16(wr, live ? wb + wrel[i] : BUF_OOB);  // (BUF_OOB + wb: still out)
-  };
-  auto stash = [&](int b) {
-    uint16_t* xs = (uint16_t*)(smem + b * CKS_BUF);
-    uint16_t* ws = (uint16_t*)(smem + b * CKS_BUF + CKS_XB);
-#pragma unroll
-    for (int i = 0; i < PFX; ++i) *(uint4*)(xs + xl[i]) = px[i];
-#pragma unroll
-    for (int i = 0; i < PFW; ++i) *(uint4*)(ws + wl[i]) = pw[i];
-  };
-
-  f32x4 acc[MW][NT];
-  auto compute = [&](int b) {  // this wave's k-steps of the chunk in buffer b: [0, 5) or [5, 9)
-    const uint16_t* xb = (const uint16_t*)(smem + b * CKS_BUF) + (rw * MW * TPWc + col) * CCPc + g * 8;
-    const uint16_t* wb = (const uint16_t*)(smem + b * CKS_BUF + CKS_XB) + col * WPc + g * 8;
-    bf16x8 af[2][NT], bf[2][MW];
-    auto ld = [&](int k, int bb) {
-      const int off = ((k / 3) * TPWc + (k % 3)) * CCPc;
-#pragma unroll
-      for (int t = 0; t < NT; ++t) af[bb][t] = *(const bf16x8*)(wb + t * 16 * WPc + k * 32);
-#pragma unroll
-      for (int m = 0; m < MW; ++m) bf[bb][m] = *(const bf16x8*)(xb + m * TPWc * CCPc + off);
-    };
-    auto run = [&](auto K0c, auto K1c) {
-      constexpr int K0 = decltype(K0c)::value, K1 = decltype(K1c)::value;
-      ld(K0, 0);
-#pragma unroll
-      for (int k = K0; k < K1; ++k) {
-        if (k + 1 < K1) ld(k + 1, (k + 1 - K0) & 1);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int m = 0; m < MW; ++m)
-#pragma unroll
-          for (int t = 0; t < NT; ++t)
-            acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[(k - K0) & 1][t], bf[(k - K0) & 1][m], acc[m][t], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    };
-    if (h == 0) run(std::integral_constant<int, 0>{}, std::integral_constant<int, 5>{});
-    else run(std::integral_constant<int, 5>{}, std::integral_constant<int, 9>{});
-  };
-
-  const int nmine = nitems > (int)blockIdx.x ? (nitems - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
-  if (nmine == 0) return;
-  issue(0);
-  stash(0);
-  issue(1);
-  lds_barrier();
-  int q = 0;
-  for (int k = 0; k < nmine; ++k) {
-    const int it = blockIdx.x + k * gridDim.x;
-#pragma unroll
-    for (int m = 0; m < MW; ++m)
-#pragma unroll
-      for (int t = 0; t < NT; ++t) acc[m][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    for (int j = 0; j < nch; ++j, ++q) {
-      // buffer q & 1 holds chunk q (stored before the last barrier); buffer (q + 1) & 1 is free (chunk q - 1 is done)
-      if (h == 0) {
-        compute(q & 1);
-        stash((q + 1) & 1);
-        issue(q + 2);
-      } else {
-        stash((q + 1) & 1);
-        issue(q + 2);
-        compute(q & 1);
-      }
-      lds_barrier();
-    }
-    // the item's reduction and epilogue in buffer (q - 1) & 1 (its last chunk's; free since the barrier above)
-    const int tile = it / ncob, cob = it - tile * ncob;
-    int nimg, oy0, ox0;
-    tile_xy(tile, nimg, oy0, ox0);
-    char* stg = smem + ((q - 1) & 1) * CKS_BUF;
-    f32x4* red = (f32x4*)stg + rw * (MW * NT * 64);
-    if (h == 1) {
-#pragma unroll
-      for (int m = 0; m < MW; ++m)
-#pragma unroll
-        for (int t = 0; t < NT; ++t) red[(m * NT + t) * 64 + lane] = acc[m][t];
-    }
-    lds_barrier();
-    if (h == 0) {
-#pragma unroll
-      for (int m = 0; m < MW; ++m)
-#pragma unroll
-        for (int t = 0; t < NT; ++t) acc[m][t] += red[(m * NT + t) * 64 + lane];
-    }
-    lds_barrier();  // the partial sums are read: the staging below overwrites them
-    float* eb = (float*)stg + rw * (MW * 16 * EPP);
-    if (h == 0) {
-#pragma unroll
-      for (int m = 0; m < MW; ++m)
-#pragma unroll
-        for (int t = 0; t < NT; ++t) *(f32x4*)(eb + (m * 16 + col) * EPP + t * 16 + g * 4) = acc[m][t];
-    }
-    lds_barrier();  // the transposed reads use another vector type
-    if constexpr (EP == 9 || EP == 10) {
-      float ssum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, ssq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (h == 0) store_tile_lds<RF, MW * 16, NT * 16, 64, EP>(a, eb, EPP, lane, nimg, oy0 + rw * MW, ox0, cob * 64, ssum, ssq);
-      // (every wave takes part in its barriers; the second half adds nothing; scratch aliases the staging)
-      bn_tile_partials(a, ssum, ssq, h == 0, rw, lane, tile, cob * 64, (float*)stg);
-    } else {
-      if (h == 0) store_tile_lds<RF, MW * 16, NT * 16, 64, EP>(a, eb, EPP, lane, nimg, oy0 + rw * MW, ox0, cob * 64);
-    }
-    lds_barrier();  // the staging reads are done: the buffer takes the next item's second chunk
   }
 }
 
@@ -2887,6 +2695,27 @@ static bool dgrad_s2_shape(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, co
          d->out_w == 2 * d->in_w && ep->out_mode == 0 && !bias && !ep->res2 && !ep->aux && !ep->down2 && act_ok;
 }
 
+static int env_flag(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
+// channel blocks grouped per tile in the XCD-major order: the largest divisor of ncob (>= 2) whose weight blocks
+// together stay within ~2.5 MB of the XCD's 4 MB L2 (they are re-read by every tile of the group), else 0
+// the second dispatch round of a two-workgroups-per-CU launch starts late (conv_fwd_body 'Stagger')
+static void set_stagger(FwdArgs& a) {
+  static int ncu = 0, stag = -1;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (ncu <= 0) ncu = 256;
+    stag = env_flag("CLIMSR_CONV_STAGGER", 2);  // 2 x 2048 cycles: GAN step 25.25 -> 24.98 ms (same box, 2 + 6 runs)
+  }
+  a.stag_lo = ncu;
+  a.stag_hi = 2 * ncu;
+  a.stag_n = stag;
+}
+
 template <int MW, int NT>
 static int launch_dgrad_s2_t(const ClimsrConvDesc* d, FwdArgs a, hipStream_t s) {
   a.tiles_x = ceil_div(d->in_w, 16);
@@ -2898,6 +2727,7 @@ static int launch_dgrad_s2_t(const ClimsrConvDesc* d, FwdArgs a, hipStream_t s) 
   }
   dim3 grid(ceil_div(a.tiles_x * a.tiles_y * a.n, 8) * 8 * (d->out_c / (NT * 16)));
   const int lds = s2d_lds<MW>(NT);
+
   if (ep4) hipLaunchKernelGGL((conv_dgrad_s2_kernel<4, MW, NT>), grid, dim3(256), lds, s, a);
   else if (a.bz) hipLaunchKernelGGL((conv_dgrad_s2_kernel<10, MW, NT>), grid, dim3(256), lds, s, a);
   else hipLaunchKernelGGL((conv_dgrad_s2_kernel<0, MW, NT>), grid, dim3(256), lds, s, a);
@@ -2911,12 +2741,6 @@ static int launch_dgrad_s2(const ClimsrConvDesc* d, const FwdArgs& a, hipStream_
   return launch_dgrad_s2_t<4, 2>(d, a, s);
 }
 
-static int env_flag(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v && *v ? atoi(v) : dflt;
-}
-// channel blocks grouped per tile in the XCD-major order: the largest divisor of ncob (>= 2) whose weight blocks
-// together stay within ~2.5 MB of the XCD's 4 MB L2 (they are re-read by every tile of the group), else 0
 static int conv_xcd_group(int ncob, long wblk_bytes) {
   static const int mode = env_flag("CLIMSR_CONV_XCD", 1);
   if (!mode || ncob < 2) return 0;
@@ -2925,52 +2749,13 @@ static int conv_xcd_group(int ncob, long wblk_bytes) {
   return 0;
 }
 
-template <int EP>
-static int launch_fwd_ks(const FwdArgs& a, int ncob, hipStream_t s) {
-  if (g_dry) {
-    snprintf(g_dry_name, sizeof(g_dry_name), "conv_fwd_ks_kernel<%s, %d>", a.res_f32 ? "true" : "false", EP);
-    return CLIMSR_OK;
-  }
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (ncu <= 0) ncu = 256;
-  }
-  const int nitems = a.tiles_x * a.tiles_y * a.n * ncob;
-  auto kt = conv_fwd_ks_kernel<true, EP>;
-  auto kf = conv_fwd_ks_kernel<false, EP>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, CKS_LDS);
-    (void)hipFuncSetAttribute((const void*)kf, hipFuncAttributeMaxDynamicSharedMemorySize, CKS_LDS);
-    attr_set = true;
-  }
-  hipLaunchKernelGGL(a.res_f32 ? kt : kf, dim3(nitems < ncu ? nitems : ncu), dim3(512), CKS_LDS, s, a, nitems);
-  return check_launch("conv2d_fwd (K-split)");
-}
-
 #define WIDE_GEO(pfx) ((pfx) == 18)
 template <int MW, int NT, int PFX, int PFW, int EP, int GEO>
 static int launch_fwd_geo(const FwdArgs& a0, int ncob, size_t lds, hipStream_t s) {
-  if constexpr (GEO == 1 && MW == 4 && NT == 4 && PFX == 6 && PFW == 9) {
-    static const int ks = env_flag("CLIMSR_CONV_KS", 0);
-    if (ks) return launch_fwd_ks<EP>(a0, ncob, s);
-  }
   FwdArgs a = a0;
   a.xgrp = GEO == 1 ? conv_xcd_group(ncob, (long)NT * 16 * a.kpk * 2) : 0;
-  {
-    static int ncu = 0, stag = -1;
-    if (!ncu) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-      if (ncu <= 0) ncu = 256;
-      stag = env_flag("CLIMSR_CONV_STAGGER", 2);  // 2 x 2048 cycles: GAN step 25.25 -> 24.98 ms (same box, 2 + 6 runs)
-    }
-    a.stag_lo = ncu; a.stag_hi = 2 * ncu; a.stag_n = GEO == 1 && !WIDE_GEO(PFX) ? stag : 0;
-  }
+  set_stagger(a);
+  if (GEO != 1 || WIDE_GEO(PFX)) a.stag_n = 0;
   const dim3 grid = a.xgrp ? dim3(a.tiles_x * a.tiles_y * a.n * ncob) : dim3(a.tiles_x * a.tiles_y * a.n, ncob);
   const size_t lds_ep = (size_t)4 * MW * 16 * (NT * 16 + 4) * 4;  // epilogue staging (aliases the operands)
   if (lds_ep > lds) lds = lds_ep;
