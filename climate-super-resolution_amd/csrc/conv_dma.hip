@@ -1,0 +1,223 @@
+// LDS-DMA implicit-GEMM conv for CDNA4 (gfx950): the 3x3 / stride-1 / 32-channel-chunk shapes of conv.hip's GEO 1
+// path (VGG19 perceptual-loss convs climsr/losses/perceptual.py:22-36, RDB conv5 / its data gradient
+// climsr/models/esrgan.py:26,32-38, the discriminator's stride-1 layers climsr/models/rfb_esrgan.py:28-52).
+#include <algorithm>
+
+#include "conv_ep.h"
+
+// ------------------------------------------------------------------------------------------
+// LDS-DMA form of the GEO 1 conv (3x3, stride 1, 32-channel chunks: VGG19 2_1..4_4, RDB conv5 / pull-x, the
+// discriminator's stride-1 layers): ONE 8-wave workgroup per CU over a 32 x 16-pixel x 64-channel output tile (wave
+// w: rows 4w..4w+3, the 4 x 4 MFMA fragments of conv_fwd_body GEO 1).  Chunk operands move global -> LDS by
+// `buffer_load ... lds` (no staging registers, no ds_write, no VALU) into two buffers: chunk q + 1 is requested right
+// after the barrier that opens chunk q and lands under its 144 MFMAs per wave, and the two waves of each SIMD hide
+// each other's fragment-read latency.  (conv_fwd_kernel's two 4-wave workgroups per CU ran in lockstep, so their
+// staging and MFMA phases added up: DESIGN §3.3.)  The weights of a chunk are staged once per 512 output pixels
+// instead of per 256.
+// LDS images are lane-linear (one DMA instruction = 64 lanes x 16 B, contiguous): x = [34 x 18 px][4 x 16 B],
+// weights = [64 rows][9 taps][4 x 16 B].  The 16 B slot s of x-tile column c / weight row r holds channel group
+// s ^ 2((c >> 2) & 1) / s ^ 2((r >> 2) & 1) (the XOR is applied on the global side): every 16-lane bank group of a
+// ds_read_b128 fragment read then covers the 64 banks once, and the k-steps' fragment offsets stay compile-time
+// immediates on top of three per-lane x bases (one per tap column) and one weight base.
+// ------------------------------------------------------------------------------------------
+constexpr int DMA_TPW = TW + 2, DMA_XROW = DMA_TPW * 64;  // x-image bytes per tile row
+constexpr int DMA_XU = (DMA_TH + 2) * DMA_TPW * 4;                    // 16 B units of the x image (2448)
+constexpr int DMA_XI = (DMA_XU + 63) / 64;                            // its DMA instructions (39)
+constexpr int DMA_WI = 64 * 36 / 64;                                  // weight DMA instructions (36)
+constexpr int DMA_XB = DMA_XI * 1024, DMA_WB = DMA_WI * 1024, DMA_BUF = DMA_XB + DMA_WB;
+constexpr int DMA_EPP = 64 + 4;                                       // epilogue staging pitch (floats)
+constexpr size_t DMA_LDS = std::max((size_t)2 * DMA_BUF, (size_t)8 * 64 * DMA_EPP * 4);
+static_assert(DMA_LDS <= 160 * 1024, "LDS-DMA conv: two chunk buffers");
+
+template <int EP, bool RF>
+__global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
+  const int wvu = __builtin_amdgcn_readfirstlane(wave);
+  int tile_id = blockIdx.x, cob = blockIdx.y;
+  if (a.xgrp > 0) {  // XCD-major (channel-block group, tile, channel block) order, as conv_fwd_body
+    const int ntile = a.tiles_x * a.tiles_y * a.n, idx = xcd_major(blockIdx.x, gridDim.x);
+    const int grp = idx / (ntile * a.xgrp), rem = idx - grp * (ntile * a.xgrp);
+    tile_id = rem / a.xgrp;
+    cob = grp * a.xgrp + (rem - tile_id * a.xgrp);
+  }
+  const int tx = tile_id % a.tiles_x, ty = (tile_id / a.tiles_x) % a.tiles_y, nimg = tile_id / (a.tiles_x * a.tiles_y);
+  const int ox0 = tx * TW, oy0 = ty * DMA_TH, co_blk0 = cob * 64;
+  const int iy0 = oy0 - 1, ix0 = ox0 - 1;
+
+  // per-lane DMA source offsets of chunk 0 (wave w issues x / weight instructions w + 8 i); out-of-image and
+  // past-the-image lanes get BUF_OOB, which stays out of range at every chunk (zeros land in LDS)
+  const __amdgpu_buffer_rsrc_t xr = buf_rsrc(a.x, (uint32_t)((long)a.n * a.in_h * a.in_w * a.in_cs * 2));
+  const __amdgpu_buffer_rsrc_t wr = buf_rsrc(a.w, (uint32_t)((long)(co_blk0 + 64) * a.kpk * 2));
+  uint32_t xo[5], wo[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const int L = (wave + 8 * i) * 64 + lane, P = L >> 2, r = P / DMA_TPW, c = P - r * DMA_TPW;
+    const int iy = iy0 + r, ix = ix0 + c, ch = (L & 3) ^ (((c >> 2) & 1) << 1);
+    const bool ok = L < DMA_XU && iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w;
+    xo[i] = ok ? (uint32_t)((((nimg * a.in_h + iy) * a.in_w + ix) * a.in_cs + a.in_co + ch * 8) * 2) : BUF_OOB;
+    const int row = L / 36, slot = L - row * 36, wch = (slot & 3) ^ (((row >> 2) & 1) << 1);
+    wo[i] = L < 64 * 36 ? (uint32_t)(((co_blk0 + row) * a.kpk + (slot >> 2) * 32 + wch * 8) * 2) : BUF_OOB;
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
+  // in asm (not the builtin): hipcc would wait vmcnt(0) before the next ds_read for an LDS write of unknown extent;
+  // the DMAs are drained by hand (vmcnt(0) at each chunk barrier).  M0 = the instruction's LDS destination.
+  auto glds = [&](__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(off), "s"(rs), "s"(lds) : "memory");
+  };
+  const uint32_t wstep = (uint32_t)a.kcpad * 2;
+  // DMA piece p (0..9) of chunk j into buffer b: x instruction wave + 8 p (p < 5), weight instruction wave + 8 (p - 5)
+  auto piece = [&](int p, uint32_t j, int b) {
+    const uint32_t base = lds0 + (uint32_t)(b * DMA_BUF);
+    if (p < 5) {
+      if (wvu + 8 * p < DMA_XI) glds(xr, xo[p] + j * 64u, base + (uint32_t)((wvu + 8 * p) * 1024));
+    } else if (wvu + 8 * (p - 5) < DMA_WI) {
+      glds(wr, wo[p - 5] + j * wstep, base + (uint32_t)(DMA_XB + (wvu + 8 * (p - 5)) * 1024));
+    }
+  };
+#ifndef CLIMSR_DMA_SPREAD
+#define CLIMSR_DMA_SPREAD 1  // DMA pieces per k-step: 1 (k-steps 0..8, two at the last) or 2 (k-steps 0..4)
+#endif
+#ifndef CLIMSR_DMA_DIAG
+#define CLIMSR_DMA_DIAG 0  // diagnostic builds only: >= 1 = chunk 0 DMA'd, later chunks computed on stale buffers (3 / 5: no
+                           // epilogue stores, 4 / 5: no per-k-step fragment reads)
+#endif
+  // fragment offsets: weights row 16 t + col, tap k, group g at woff + 16 t * 576 + 64 k; x pixel (4 wave + m + dy,
+  // col + dx), group g at xoff[dx] + (m + dy) * DMA_XROW
+  int xoff[3];
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx) {
+    const int c = col + dx;
+    xoff[dx] = wave * 4 * DMA_XROW + c * 64 + ((g ^ (((c >> 2) & 1) << 1)) << 4);
+  }
+  const int woff = col * 576 + ((g ^ (((col >> 2) & 1) << 1)) << 4);
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[m][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int p = 0; p < 10; ++p) piece(p, 0, 0);
+  for (int j = 0; j < a.nchunk; ++j) {
+    // chunk j's DMAs (this wave's) have landed; after the barrier every wave's have, and every wave is past its
+    // fragment reads of chunk j - 1, whose buffer chunk j + 1 now overwrites
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    // chunk j + 1's 10 DMA pieces go out between this chunk's k-steps, behind their MFMAs (issued back to back
+    // before the first MFMA they held the SIMD's issue for ~1k cycles per chunk)
+    const bool more = CLIMSR_DMA_DIAG == 0 && j + 1 < a.nchunk;
+    const char* xb = smem + (j & 1) * DMA_BUF;
+    const char* wb = xb + DMA_XB;
+    bf16x8 af[2][4], bf[2][4];
+    auto ld = [&](int k, int s) {
+      const int dy = k / 3, dx = k % 3;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) af[s][t] = *(const bf16x8*)(wb + woff + t * 16 * 576 + k * 64);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) bf[s][m] = *(const bf16x8*)(xb + xoff[dx] + (m + dy) * DMA_XROW);
+    };
+    ld(0, 0);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+#if CLIMSR_DMA_DIAG >= 4  // diagnostic 4: k-step fragments read once per chunk (MFMAs without LDS traffic)
+      if (k == 0) ld(1, 1);
+#else
+      if (k + 1 < 9) ld(k + 1, (k + 1) & 1);
+#endif
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k & 1][t], bf[k & 1][m], acc[m][t], 0, 0, 0);
+      if (more) {
+        if (CLIMSR_DMA_SPREAD == 2) {
+          if (k < 5) {
+            piece(2 * k, (uint32_t)(j + 1), (j + 1) & 1);
+            piece(2 * k + 1, (uint32_t)(j + 1), (j + 1) & 1);
+          }
+        } else {
+          piece(k, (uint32_t)(j + 1), (j + 1) & 1);
+          if (k == 8) piece(9, (uint32_t)(j + 1), (j + 1) & 1);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  // epilogue: each wave's 64 pixels x 64 channels through its own LDS region (aliasing the chunk buffers)
+  float* eb = (float*)smem + wave * (64 * DMA_EPP);
+  __syncthreads();  // every wave is done with the chunk buffers
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) *(f32x4*)(eb + (m * 16 + col) * DMA_EPP + t * 16 + g * 4) = acc[m][t];
+  __syncthreads();
+  if constexpr (EP == 9 || EP == 10) {
+    // BatchNorm partials per 16 x 16 tile (the rows of waves 4h..4h+3 are 16-row tile 2 ty + h; the host takes EP 9 /
+    // 10 only for out_h % 32 == 0): the sums of conv_fwd_body's bn_tile_partials in the same fixed order, bit for bit
+    float ssum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, ssq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    store_tile_lds<RF, 64, 64, 64, EP>(a, eb, DMA_EPP, lane, nimg, oy0 + wave * 4, ox0, co_blk0, ssum, ssq);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int m = 8; m < 64; m <<= 1) {
+        ssum[i] += __shfl_xor(ssum[i], m);
+        ssq[i] += __shfl_xor(ssq[i], m);
+      }
+    lds_barrier();  // every wave's epilogue reads of the staging region are done
+    float* red = (float*)smem + (wave >> 2) * 512;
+    if (lane < 8) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        red[(wave & 3) * 128 + lane * 8 + i] = ssum[i];
+        red[(wave & 3) * 128 + 64 + lane * 8 + i] = ssq[i];
+      }
+    }
+    lds_barrier();
+    if ((wave & 3) == 0) {
+      float ts = 0.f, tq = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        ts += red[w * 128 + lane];
+        tq += red[w * 128 + 64 + lane];
+      }
+      const long tile16 = ((long)nimg * (2 * a.tiles_y) + 2 * ty + (wave >> 2)) * a.tiles_x + tx;
+      double* out = a.bn_part + tile16 * 2 * a.out_c;
+      out[co_blk0 + lane] = (double)ts;
+      out[a.out_c + co_blk0 + lane] = (double)tq;
+    }
+  } else {
+#if CLIMSR_DMA_DIAG == 3 || CLIMSR_DMA_DIAG == 5  // diagnostics 3 / 5: no epilogue
+    if (a.n < 0)
+#endif
+    store_tile_lds<RF, 64, 64, 64, EP>(a, eb, DMA_EPP, lane, nimg, oy0 + wave * 4, ox0, co_blk0);
+  }
+}
+
+
+namespace climsr {
+int fwd_dma_launch(int ep, const FwdArgs& a, int ncob, hipStream_t s) {
+  void (*k)(FwdArgs) = nullptr;
+  const bool rf = a.res_f32 != 0;
+#define DMA_EP(E) \
+  case E: k = rf ? conv_fwd_dma_kernel<E, true> : conv_fwd_dma_kernel<E, false>; break;
+  switch (ep) {
+    DMA_EP(0) DMA_EP(1) DMA_EP(2) DMA_EP(3) DMA_EP(4) DMA_EP(6) DMA_EP(7) DMA_EP(8) DMA_EP(9) DMA_EP(10)
+    default: set_error("conv2d_fwd: no LDS-DMA kernel for epilogue %d", ep); return CLIMSR_EINVAL;
+  }
+#undef DMA_EP
+  static bool attr_set[16][2] = {};
+  if (!attr_set[ep][rf]) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set[ep][rf] = true;
+  }
+  const int ntile = a.tiles_x * a.tiles_y * a.n;
+  const dim3 grid = a.xgrp ? dim3(ntile * ncob) : dim3(ntile, ncob);
+  hipLaunchKernelGGL(k, grid, dim3(512), DMA_LDS, s, a);
+  return CLIMSR_OK;
+}
+}  // namespace climsr

@@ -88,6 +88,59 @@ def test_conv_fwd_matches_torch(cin, cout, ks, stride, up, n, h, w):
     check_close(from_nhwc(y, cout).cpu(), want, what=f"fwd {cin}->{cout} k{ks} s{stride} up{up}")
 
 
+# LDS-DMA form of the 3x3 / 32-channel-chunk conv (conv_fwd_dma_kernel: 32 x 16 tiles, 8 waves, two DMA chunk
+# buffers) under each epilogue it takes: activation forward (EP 3), RDB conv5 residual (EP 1), fp32 pull-x data
+# gradient with an fp32 residual (EP 2), generic fp32 out with bias (EP 0), plain bf16 (EP 8); ragged rows / columns
+DMA_CASES = [
+    (64, 128, 2, 64, 64, "act"),
+    (128, 64, 2, 96, 40, "conv5"),
+    (128, 64, 1, 100, 33, "pullx"),
+    (256, 256, 1, 32, 32, "plain"),
+    (64, 128, 1, 64, 48, "bf16"),
+]
+
+
+@pytest.mark.parametrize("cin,cout,n,h,w,mode", DMA_CASES)
+def test_conv_fwd_lds_dma_matches_torch(cin, cout, n, h, w, mode):
+    import climsr_amd.ops as ops
+    p, wt, b = make_plan(cin, cout, 3, seed=11, bias=mode in ("act", "conv5", "plain"))
+    g = torch.Generator().manual_seed(12)
+    x = torch.rand((n, cin, h, w), generator=g) * 2 - 1
+    xin = to_nhwc(bf(x))
+    r = torch.rand((n, cout, h, w), generator=g) * 2 - 1
+    f32 = mode in ("pullx", "plain")
+    y = torch.zeros((n, h, w, cout), dtype=torch.float32 if f32 else torch.bfloat16, device=DEV)
+    kw = dict(out_mode=OUT_F32 if f32 else OUT_BF16)
+    if mode == "act":
+        kw["act"] = ACT_RELU
+    elif mode == "conv5":
+        kw.update(res1=xin, res1_cs=cin, res1_co=0, alpha1=0.2)
+    elif mode == "pullx":
+        kw.update(use_bias=False, res1=to_nhwc(r, dtype=torch.float32), res1_cs=cout, res1_co=0)
+    names = []
+    ops.PROFILER = lambda name, flops, fn, tag="", nbytes=0: (names.append(name), fn())
+    try:
+        p.fwd(xin, cin, 0, h, w, y, cout, 0, n, **kw)
+    finally:
+        ops.PROFILER = None
+    torch.cuda.synchronize()
+    assert names and names[-1].startswith("conv_fwd_dma_kernel"), names
+    want = F.conv2d(bf(x).double(), bf(wt).double(), None if b is None else b.double(), padding=1)
+    if mode == "act":
+        want = F.relu(want)
+    elif mode == "conv5":
+        want = want * 0.2 + bf(x)[:, :cout].double()
+    elif mode == "pullx":
+        want = want + r.double()
+    got = from_nhwc(y, cout).cpu().double()
+    if f32:
+        check_close(got, want, what=f"dma {mode}")
+    else:  # bf16 store: one rounding of the fp32 result
+        scale = want.abs().max().item()
+        err = ((got - want).abs() - want.abs() * 2.0 ** -8).max().item()
+        assert err <= 1e-5 * scale, f"dma {mode}: bf16 err {err:.3e} vs scale {scale:.3e}"
+
+
 def test_conv_fwd_epilogue_slices_and_residuals():
     """Dense-buffer slices (read [0,80), write at channel 80) + lrelu, and the RRDB double residual."""
     n, h, w = 2, 16, 16
