@@ -2467,9 +2467,12 @@ static int launch_fwd_geo(const FwdArgs& a0, int ncob, size_t lds, hipStream_t s
   if constexpr (GEO == 1 && !WIDE_GEO(PFX) && MW == 4 && NT == 4) {
     // the LDS-DMA form for the tiles it fills (32-row tiles: not the 16^2 VGG conv5 layers); with BatchNorm partials
     // (per 16 x 16 tile) only when every 32-row tile holds two whole 16-row tiles
+    // RDB conv5 / pull-x (EP 1 / 2: 256 items at B=32 64^2, one round of one workgroup per CU) measured 7 % slower in
+    // the GAN step than the two-workgroups-per-CU form (its chunk-0 latency and epilogue are not hidden in a single
+    // round); CLIMSR_CONV_DMA=2 takes them too, 0 none
     static const int dma = env_flag("CLIMSR_CONV_DMA", 1);
     const bool fits = (EP == 9 || EP == 10) ? a0.out_h % DMA_TH == 0 : (a0.out_h % DMA_TH == 0 || a0.out_h >= 3 * DMA_TH);
-    if (dma && !a0.down2 && fits) return launch_fwd_dma<EP>(a0, ncob, s);
+    if ((dma == 2 || (dma == 1 && EP != 1 && EP != 2)) && !a0.down2 && fits) return launch_fwd_dma<EP>(a0, ncob, s);
   }
   FwdArgs a = a0;
   a.xgrp = GEO == 1 ? conv_xcd_group(ncob, (long)NT * 16 * a.kpk * 2) : 0;

@@ -2,6 +2,7 @@
 // path (VGG19 perceptual-loss convs climsr/losses/perceptual.py:22-36, RDB conv5 / its data gradient
 // climsr/models/esrgan.py:26,32-38, the discriminator's stride-1 layers climsr/models/rfb_esrgan.py:28-52).
 #include <algorithm>
+#include <stdlib.h>
 
 #include "conv_ep.h"
 
@@ -29,36 +30,130 @@ constexpr int DMA_EPP = 64 + 4;                                       // epilogu
 constexpr size_t DMA_LDS = std::max((size_t)2 * DMA_BUF, (size_t)8 * 64 * DMA_EPP * 4);
 static_assert(DMA_LDS <= 160 * 1024, "LDS-DMA conv: two chunk buffers");
 
+
+// Epilogue of one wave's 64 pixels x 32 channels (staged fp32 at eb, pitch EPH) for the persistent EPs: the math of
+// store_tile_lds (same helpers, same order: bit-identical results), but every lane issues the same number of buffer
+// stores whatever its pixels (invalid ones get an out-of-range offset, which the hardware drops), so the next chunk's
+// DMA wait can count them: NSTORE per call.
+constexpr uint32_t ST_OOB = 0xFFFFFFC0u;
+typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
+template <int EP>
+struct DmaEp {
+  static constexpr bool F32 = EP == 2 || EP == 7;                          // fp32 '=' output
+  static constexpr int NSTORE = 4 * (F32 ? 2 : 1) + (EP == 2 ? 4 : 0);     // per call (EP 2: + the bf16 aux)
+};
+template <int EP>
+__device__ __forceinline__ void dma_store_half(const FwdArgs& a, const float* eb, int ehp, int lane, int nimg, int oyw, int ox0, int co0) {
+  static_assert(EP == 1 || EP == 2 || EP == 3 || EP == 6 || EP == 7 || EP == 8, "persistent epilogues");
+  constexpr bool F32 = DmaEp<EP>::F32;
+  const bool has_bias = EP == 1 || EP == 3;
+  const int act = (EP == 3 || EP == 6) ? a.act : 0;
+  const bool has1 = EP == 1 || EP == 2, has2 = (EP == 1 || EP == 2) && a.res2 != nullptr;
+  const long opx = (long)a.n * a.out_h * a.out_w;
+  const __amdgpu_buffer_rsrc_t ry = buf_rsrc(a.y, (uint32_t)(opx * a.out_cs * (F32 ? 4 : 2)));
+  const __amdgpu_buffer_rsrc_t rr1 = opt_rsrc(has1 ? a.res1 : nullptr), rr2 = opt_rsrc(has2 ? a.res2 : nullptr);
+  const __amdgpu_buffer_rsrc_t rax = buf_rsrc(a.aux, EP == 2 && a.aux ? (uint32_t)(opx * a.aux_cs * 2) : 0u);
+  Raw8 r1[4], r2[4];
+  uint32_t off[4], aoff[4];
+  long pidx[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int it = j * 64 + lane, pl = it >> 2, cg = it & 3;
+    const int oy = oyw + (pl >> 4), ox = ox0 + (pl & 15), co = co0 + cg * 8;
+    const bool ok = oy < a.out_h && ox < a.out_w && co < a.out_c;
+    pidx[j] = ok ? ((long)(nimg * a.out_h + oy) * a.out_w + ox) : 0;
+    const int c = ok ? co : 0;
+    off[j] = ok ? (uint32_t)((pidx[j] * a.out_cs + a.out_co + co) * (F32 ? 4 : 2)) : ST_OOB;
+    aoff[j] = ok ? (uint32_t)((pidx[j] * a.aux_cs + a.aux_co + co) * 2) : ST_OOB;
+    if (has1) r1[j] = load8b(rr1, EP == 2, pidx[j] * a.r1_cs + (ok ? a.r1_co : 0) + c);
+    else r1[j].lo = r1[j].hi = make_uint4(0, 0, 0, 0);
+    if (EP == 1 || EP == 2) r2[j] = load8b(rr2, EP == 2, pidx[j] * a.r2_cs + (ok ? a.r2_co : 0) + c);
+    else r2[j].lo = r2[j].hi = make_uint4(0, 0, 0, 0);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int it = j * 64 + lane, pl = it >> 2, cg = it & 3;
+    const int co = co0 + cg * 8;
+    const float4 s0 = *(const float4*)(eb + pl * ehp + cg * 8), s1 = *(const float4*)(eb + pl * ehp + cg * 8 + 4);
+    float v[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    float bb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (has_bias && off[j] != ST_OOB) {
+      const float4 b0 = *(const float4*)(a.bias + co), b1 = *(const float4*)(a.bias + co + 4);
+      bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w; bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      v[i] = ep_res(act_apply(v[i] + bb[i], act, a.slope), act, a.slope, has1, raw8_at(r1[j], EP == 2, i), a.alpha1, a.beta1, has2,
+                    raw8_at(r2[j], EP == 2, i), a.alpha2, a.beta2);
+    if constexpr (F32) {
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, make_float4(v[0], v[1], v[2], v[3])), ry, off[j], 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, make_float4(v[4], v[5], v[6], v[7])), ry, off[j] + 16u, 0, 0);
+    } else {
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, pack8_bf16(v, 1.f)), ry, off[j], 0, 0);
+    }
+    if constexpr (EP == 2) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, pack8_bf16(v, a.aux_scale)), rax, aoff[j], 0, 0);
+  }
+}
+
+#ifndef CLIMSR_DMA_SPREAD
+#define CLIMSR_DMA_SPREAD 1  // DMA pieces per k-step: 1 (k-steps 0..8, two at the last) or 2 (k-steps 0..4)
+#endif
+#ifndef CLIMSR_DMA_DIAG
+#define CLIMSR_DMA_DIAG 0  // diagnostic builds only: >= 1 = chunk 0 DMA'd, later chunks computed on stale buffers (3 / 5: no
+                           // epilogue stores, 4 / 5: no per-k-step fragment reads)
+#endif
+
+// Persistent over (tile, channel block) items v = blockIdx.x + k gridDim.x (host: gridDim.x <= #CUs, a multiple of 8,
+// so v's XCD is blockIdx.x's and xcd_major keeps a tile's channel blocks on one L2): the chunks of consecutive items
+// form one stream, so the next item's chunk 0 lands under the current item's last chunk, and the epilogue's stores
+// drain under the next item's MFMAs.  The epilogue stages each wave's 64 pixels x 32 channels at a time through the
+// chunk buffer just computed (the other one is receiving the next chunk).  EP 9 / 10 (BatchNorm partials of a whole
+// 64-channel tile): one item per workgroup, the whole tile staged at once.
 template <int EP, bool RF>
 __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr bool BN = EP == 9 || EP == 10;
+  // epilogues with a fixed store count per lane (dma_store_half), so the wait for the next item's chunk 0 skips them
+  constexpr bool CNT = EP == 1 || EP == 2 || EP == 3 || EP == 6 || EP == 7 || EP == 8;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
   const int wvu = __builtin_amdgcn_readfirstlane(wave);
-  int tile_id = blockIdx.x, cob = blockIdx.y;
-  if (a.xgrp > 0) {  // XCD-major (channel-block group, tile, channel block) order, as conv_fwd_body
-    const int ntile = a.tiles_x * a.tiles_y * a.n, idx = xcd_major(blockIdx.x, gridDim.x);
-    const int grp = idx / (ntile * a.xgrp), rem = idx - grp * (ntile * a.xgrp);
-    tile_id = rem / a.xgrp;
-    cob = grp * a.xgrp + (rem - tile_id * a.xgrp);
-  }
-  const int tx = tile_id % a.tiles_x, ty = (tile_id / a.tiles_x) % a.tiles_y, nimg = tile_id / (a.tiles_x * a.tiles_y);
-  const int ox0 = tx * TW, oy0 = ty * DMA_TH, co_blk0 = cob * 64;
-  const int iy0 = oy0 - 1, ix0 = ox0 - 1;
+  const int ntile = a.tiles_x * a.tiles_y * a.n, ncob = (a.out_c + 63) / 64;  // = the host's packed-row blocks
+  const int nitem = ntile * ncob;
+  // item v -> tile, channel block (XCD-major (channel-block group, tile, channel block) order with xgrp, as conv_fwd_body)
+  auto decode = [&](int v, int& nimg, int& oy0, int& ox0, int& co0, int& tyo) {
+    int tile_id, cob;
+    if (a.xgrp > 0) {
+      const int idx = xcd_major(v, nitem), grp = idx / (ntile * a.xgrp), rem = idx - grp * (ntile * a.xgrp);
+      tile_id = rem / a.xgrp;
+      cob = grp * a.xgrp + (rem - tile_id * a.xgrp);
+    } else {
+      cob = v / ntile;
+      tile_id = v - cob * ntile;
+    }
+    const int tx = tile_id % a.tiles_x, ty = (tile_id / a.tiles_x) % a.tiles_y;
+    nimg = tile_id / (a.tiles_x * a.tiles_y);
+    ox0 = tx * TW;
+    oy0 = ty * DMA_TH;
+    co0 = cob * 64;
+    tyo = ty;
+  };
 
-  // per-lane DMA source offsets of chunk 0 (wave w issues x / weight instructions w + 8 i); out-of-image and
-  // past-the-image lanes get BUF_OOB, which stays out of range at every chunk (zeros land in LDS)
   const __amdgpu_buffer_rsrc_t xr = buf_rsrc(a.x, (uint32_t)((long)a.n * a.in_h * a.in_w * a.in_cs * 2));
-  const __amdgpu_buffer_rsrc_t wr = buf_rsrc(a.w, (uint32_t)((long)(co_blk0 + 64) * a.kpk * 2));
+  const __amdgpu_buffer_rsrc_t wr = buf_rsrc(a.w, (uint32_t)((long)ncob * 64 * a.kpk * 2));
+  // per-lane DMA source offsets of an item's chunk 0 (wave w issues x / weight instructions w + 8 i); out-of-image and
+  // past-the-image lanes get BUF_OOB, which stays out of range at every chunk (zeros land in LDS)
   uint32_t xo[5], wo[5];
+  auto offsets = [&](int nimg, int oy0, int ox0, int co0) {
 #pragma unroll
-  for (int i = 0; i < 5; ++i) {
-    const int L = (wave + 8 * i) * 64 + lane, P = L >> 2, r = P / DMA_TPW, c = P - r * DMA_TPW;
-    const int iy = iy0 + r, ix = ix0 + c, ch = (L & 3) ^ (((c >> 2) & 1) << 1);
-    const bool ok = L < DMA_XU && iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w;
-    xo[i] = ok ? (uint32_t)((((nimg * a.in_h + iy) * a.in_w + ix) * a.in_cs + a.in_co + ch * 8) * 2) : BUF_OOB;
-    const int row = L / 36, slot = L - row * 36, wch = (slot & 3) ^ (((row >> 2) & 1) << 1);
-    wo[i] = L < 64 * 36 ? (uint32_t)(((co_blk0 + row) * a.kpk + (slot >> 2) * 32 + wch * 8) * 2) : BUF_OOB;
-  }
+    for (int i = 0; i < 5; ++i) {
+      const int L = (wave + 8 * i) * 64 + lane, P = L >> 2, r = P / DMA_TPW, c = P - r * DMA_TPW;
+      const int iy = oy0 - 1 + r, ix = ox0 - 1 + c, ch = (L & 3) ^ (((c >> 2) & 1) << 1);
+      const bool ok = L < DMA_XU && iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w;
+      xo[i] = ok ? (uint32_t)((((nimg * a.in_h + iy) * a.in_w + ix) * a.in_cs + a.in_co + ch * 8) * 2) : BUF_OOB;
+      const int row = L / 36, slot = L - row * 36, wch = (slot & 3) ^ (((row >> 2) & 1) << 1);
+      wo[i] = L < 64 * 36 ? (uint32_t)(((co0 + row) * a.kpk + (slot >> 2) * 32 + wch * 8) * 2) : BUF_OOB;
+    }
+  };
   const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
   // in asm (not the builtin): hipcc would wait vmcnt(0) before the next ds_read for an LDS write of unknown extent;
   // the DMAs are drained by hand (vmcnt(0) at each chunk barrier).  M0 = the instruction's LDS destination.
@@ -77,13 +172,6 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
       glds(wr, wo[p - 5] + j * wstep, base + (uint32_t)(DMA_XB + (wvu + 8 * (p - 5)) * 1024));
     }
   };
-#ifndef CLIMSR_DMA_SPREAD
-#define CLIMSR_DMA_SPREAD 1  // DMA pieces per k-step: 1 (k-steps 0..8, two at the last) or 2 (k-steps 0..4)
-#endif
-#ifndef CLIMSR_DMA_DIAG
-#define CLIMSR_DMA_DIAG 0  // diagnostic builds only: >= 1 = chunk 0 DMA'd, later chunks computed on stale buffers (3 / 5: no
-                           // epilogue stores, 4 / 5: no per-k-step fragment reads)
-#endif
   // fragment offsets: weights row 16 t + col, tap k, group g at woff + 16 t * 576 + 64 k; x pixel (4 wave + m + dy,
   // col + dx), group g at xoff[dx] + (m + dy) * DMA_XROW
   int xoff[3];
@@ -94,112 +182,155 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
   }
   const int woff = col * 576 + ((g ^ (((col >> 2) & 1) << 1)) << 4);
 
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[m][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
+  int v = blockIdx.x;
+  if (v >= nitem) return;
+  int nimg, oy0, ox0, co0, ty;
+  decode(v, nimg, oy0, ox0, co0, ty);
+  offsets(nimg, oy0, ox0, co0);
 #pragma unroll
   for (int p = 0; p < 10; ++p) piece(p, 0, 0);
-  for (int j = 0; j < a.nchunk; ++j) {
-    // chunk j's DMAs (this wave's) have landed; after the barrier every wave's have, and every wave is past its
-    // fragment reads of chunk j - 1, whose buffer chunk j + 1 now overwrites
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();
-    // chunk j + 1's 10 DMA pieces go out between this chunk's k-steps, behind their MFMAs (issued back to back
-    // before the first MFMA they held the SIMD's issue for ~1k cycles per chunk)
-    const bool more = CLIMSR_DMA_DIAG == 0 && j + 1 < a.nchunk;
-    const char* xb = smem + (j & 1) * DMA_BUF;
-    const char* wb = xb + DMA_XB;
-    bf16x8 af[2][4], bf[2][4];
-    auto ld = [&](int k, int s) {
-      const int dy = k / 3, dx = k % 3;
+  int buf = 0;  // the buffer chunk j of the current item is in
+  for (;;) {
+    const int vn = BN ? nitem : v + (int)gridDim.x;  // the next item (none with BatchNorm partials)
+    int nimg_n = 0, oy0_n = 0, ox0_n = 0, co0_n = 0, ty_n = 0;
+    f32x4 acc[4][4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) af[s][t] = *(const bf16x8*)(wb + woff + t * 16 * 576 + k * 64);
+    for (int m = 0; m < 4; ++m)
 #pragma unroll
-      for (int m = 0; m < 4; ++m) bf[s][m] = *(const bf16x8*)(xb + xoff[dx] + (m + dy) * DMA_XROW);
-    };
-    ld(0, 0);
+      for (int t = 0; t < 4; ++t) acc[m][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < a.nchunk; ++j, buf ^= 1) {
+      // chunk j's DMAs (this wave's) have landed; after the barrier every wave's have, and every wave is past its
+      // fragment reads of the other buffer (and of its epilogue staging), which the next chunk now overwrites.  The
+      // wait also drains the previous item's epilogue stores (issued after the DMAs of this chunk)
+      if (CNT && j == 0 && v != (int)blockIdx.x) {
+        // chunk 0 of a later item: only its DMAs, not the previous item's epilogue stores issued after them
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DmaEp<CNT ? EP : 8>::NSTORE) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      lds_barrier();
+      // the next chunk: chunk j + 1 of this item, or chunk 0 of the next one (its offsets replace this item's: every
+      // DMA of this item has been issued); its 10 DMA pieces go out between this chunk's k-steps, behind their MFMAs
+      const bool last = j + 1 == a.nchunk;
+      if (last && vn < nitem) {
+        decode(vn, nimg_n, oy0_n, ox0_n, co0_n, ty_n);
+        offsets(nimg_n, oy0_n, ox0_n, co0_n);
+      }
+      const bool more = CLIMSR_DMA_DIAG == 0 && (!last || vn < nitem);
+      const uint32_t jn = last ? 0u : (uint32_t)(j + 1);
+      const char* xb = smem + buf * DMA_BUF;
+      const char* wb = xb + DMA_XB;
+      bf16x8 af[2][4], bf[2][4];
+      auto ld = [&](int k, int s) {
+        const int dy = k / 3, dx = k % 3;
 #pragma unroll
-    for (int k = 0; k < 9; ++k) {
+        for (int t = 0; t < 4; ++t) af[s][t] = *(const bf16x8*)(wb + woff + t * 16 * 576 + k * 64);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) bf[s][m] = *(const bf16x8*)(xb + xoff[dx] + (m + dy) * DMA_XROW);
+      };
+      ld(0, 0);
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
 #if CLIMSR_DMA_DIAG >= 4  // diagnostic 4: k-step fragments read once per chunk (MFMAs without LDS traffic)
-      if (k == 0) ld(1, 1);
+        if (k == 0) ld(1, 1);
 #else
-      if (k + 1 < 9) ld(k + 1, (k + 1) & 1);
+        if (k + 1 < 9) ld(k + 1, (k + 1) & 1);
 #endif
-      __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k & 1][t], bf[k & 1][m], acc[m][t], 0, 0, 0);
+        if (more) {
+          if (CLIMSR_DMA_SPREAD == 2) {
+            if (k < 5) {
+              piece(2 * k, jn, buf ^ 1);
+              piece(2 * k + 1, jn, buf ^ 1);
+            }
+          } else {
+            piece(k, jn, buf ^ 1);
+            if (k == 8) piece(9, jn, buf ^ 1);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // epilogue through the buffer just computed (buf ^ 1 after the loop's last flip); LDS-only barriers, so the
+    // stores stay in flight
+    lds_barrier();  // every wave's fragment reads of it are done
+    if constexpr (BN) {
+      float* eb = (float*)smem + wave * (64 * DMA_EPP);  // the whole tile (aliases both buffers: no DMA in flight)
 #pragma unroll
       for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k & 1][t], bf[k & 1][m], acc[m][t], 0, 0, 0);
-      if (more) {
-        if (CLIMSR_DMA_SPREAD == 2) {
-          if (k < 5) {
-            piece(2 * k, (uint32_t)(j + 1), (j + 1) & 1);
-            piece(2 * k + 1, (uint32_t)(j + 1), (j + 1) & 1);
-          }
-        } else {
-          piece(k, (uint32_t)(j + 1), (j + 1) & 1);
-          if (k == 8) piece(9, (uint32_t)(j + 1), (j + 1) & 1);
+        for (int t = 0; t < 4; ++t) *(f32x4*)(eb + (m * 16 + col) * DMA_EPP + t * 16 + g * 4) = acc[m][t];
+      lds_barrier();
+      // BatchNorm partials per 16 x 16 tile (the rows of waves 4h..4h+3 are 16-row tile 2 ty + h; the host takes EP 9 /
+      // 10 only for out_h % 32 == 0): the sums of conv_fwd_body's bn_tile_partials in the same fixed order, bit for bit
+      float ssum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, ssq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      store_tile_lds<RF, 64, 64, 64, EP>(a, eb, DMA_EPP, lane, nimg, oy0 + wave * 4, ox0, co0, ssum, ssq);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int m = 8; m < 64; m <<= 1) {
+          ssum[i] += __shfl_xor(ssum[i], m);
+          ssq[i] += __shfl_xor(ssq[i], m);
+        }
+      lds_barrier();  // every wave's epilogue reads of the staging region are done
+      float* red = (float*)smem + (wave >> 2) * 512;
+      if (lane < 8) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          red[(wave & 3) * 128 + lane * 8 + i] = ssum[i];
+          red[(wave & 3) * 128 + 64 + lane * 8 + i] = ssq[i];
         }
       }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-
-  // epilogue: each wave's 64 pixels x 64 channels through its own LDS region (aliasing the chunk buffers)
-  float* eb = (float*)smem + wave * (64 * DMA_EPP);
-  __syncthreads();  // every wave is done with the chunk buffers
+      lds_barrier();
+      if ((wave & 3) == 0) {
+        float ts = 0.f, tq = 0.f;
 #pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) *(f32x4*)(eb + (m * 16 + col) * DMA_EPP + t * 16 + g * 4) = acc[m][t];
-  __syncthreads();
-  if constexpr (EP == 9 || EP == 10) {
-    // BatchNorm partials per 16 x 16 tile (the rows of waves 4h..4h+3 are 16-row tile 2 ty + h; the host takes EP 9 /
-    // 10 only for out_h % 32 == 0): the sums of conv_fwd_body's bn_tile_partials in the same fixed order, bit for bit
-    float ssum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, ssq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    store_tile_lds<RF, 64, 64, 64, EP>(a, eb, DMA_EPP, lane, nimg, oy0 + wave * 4, ox0, co_blk0, ssum, ssq);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int m = 8; m < 64; m <<= 1) {
-        ssum[i] += __shfl_xor(ssum[i], m);
-        ssq[i] += __shfl_xor(ssq[i], m);
+        for (int w = 0; w < 4; ++w) {
+          ts += red[w * 128 + lane];
+          tq += red[w * 128 + 64 + lane];
+        }
+        const long tile16 = ((long)nimg * (2 * a.tiles_y) + 2 * ty + (wave >> 2)) * a.tiles_x + ox0 / TW;
+        double* out = a.bn_part + tile16 * 2 * a.out_c;
+        out[co0 + lane] = (double)ts;
+        out[a.out_c + co0 + lane] = (double)tq;
       }
-    lds_barrier();  // every wave's epilogue reads of the staging region are done
-    float* red = (float*)smem + (wave >> 2) * 512;
-    if (lane < 8) {
+      return;
+    } else {
+      constexpr int EPH = 32 + 4;  // staged pitch (floats) of one 32-channel half
+      float* eb = (float*)(smem + (buf ^ 1) * DMA_BUF) + wave * (64 * EPH);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        red[(wave & 3) * 128 + lane * 8 + i] = ssum[i];
-        red[(wave & 3) * 128 + 64 + lane * 8 + i] = ssq[i];
-      }
-    }
-    lds_barrier();
-    if ((wave & 3) == 0) {
-      float ts = 0.f, tq = 0.f;
+      for (int h = 0; h < 2; ++h) {
+        if (h) lds_barrier();  // the first half's reads are done
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        ts += red[w * 128 + lane];
-        tq += red[w * 128 + 64 + lane];
-      }
-      const long tile16 = ((long)nimg * (2 * a.tiles_y) + 2 * ty + (wave >> 2)) * a.tiles_x + tx;
-      double* out = a.bn_part + tile16 * 2 * a.out_c;
-      out[co_blk0 + lane] = (double)ts;
-      out[a.out_c + co_blk0 + lane] = (double)tq;
-    }
-  } else {
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int t = 0; t < 2; ++t) *(f32x4*)(eb + (m * 16 + col) * EPH + t * 16 + g * 4) = acc[m][2 * h + t];
+        lds_barrier();  // (orders the staging writes before the reads: another vector type)
 #if CLIMSR_DMA_DIAG == 3 || CLIMSR_DMA_DIAG == 5  // diagnostics 3 / 5: no epilogue
-    if (a.n < 0)
+        if (a.n < 0)
 #endif
-    store_tile_lds<RF, 64, 64, 64, EP>(a, eb, DMA_EPP, lane, nimg, oy0 + wave * 4, ox0, co_blk0);
+        {
+          if constexpr (CNT) dma_store_half<CNT ? EP : 8>(a, eb, EPH, lane, nimg, oy0 + wave * 4, ox0, co0 + 32 * h);
+          else store_tile_lds<RF, 64, 32, 64, EP>(a, eb, EPH, lane, nimg, oy0 + wave * 4, ox0, co0 + 32 * h);
+        }
+      }
+    }
+    if (vn >= nitem) break;
+    v = vn;
+    nimg = nimg_n; oy0 = oy0_n; ox0 = ox0_n; co0 = co0_n; ty = ty_n;
   }
 }
 
-
 namespace climsr {
+static int env_flag_dma(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
+
 int fwd_dma_launch(int ep, const FwdArgs& a, int ncob, hipStream_t s) {
   void (*k)(FwdArgs) = nullptr;
   const bool rf = a.res_f32 != 0;
@@ -211,13 +342,22 @@ int fwd_dma_launch(int ep, const FwdArgs& a, int ncob, hipStream_t s) {
   }
 #undef DMA_EP
   static bool attr_set[16][2] = {};
+  static int ncu = 0;
   if (!attr_set[ep][rf]) {
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set[ep][rf] = true;
   }
-  const int ntile = a.tiles_x * a.tiles_y * a.n;
-  const dim3 grid = a.xgrp ? dim3(ntile * ncob) : dim3(ntile, ncob);
-  hipLaunchKernelGGL(k, grid, dim3(512), DMA_LDS, s, a);
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    ncu = ncu >= 8 ? ncu / 8 * 8 : 256;
+  }
+  // one workgroup per item with BatchNorm partials, else persistent: at most one workgroup per CU
+  const int nitem = a.tiles_x * a.tiles_y * a.n * ncob;
+  static const int persist = env_flag_dma("CLIMSR_CONV_DMA_PERSIST", 1);
+  const int grid = (ep == 9 || ep == 10 || !persist) ? nitem : std::min(nitem, ncu);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(512), DMA_LDS, s, a);
   return CLIMSR_OK;
 }
 }  // namespace climsr

@@ -2,6 +2,8 @@
 plain PyTorch fp64 reference of the same op on the same bf16-rounded operands.  The only
 difference left is fp32 MFMA accumulation order, so the bound is tight (rel 1e-5 of the scale
 plus one bf16 ulp where the output is stored in bf16)."""
+import os
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -93,7 +95,7 @@ def test_conv_fwd_matches_torch(cin, cout, ks, stride, up, n, h, w):
 # gradient with an fp32 residual (EP 2), generic fp32 out with bias (EP 0), plain bf16 (EP 8); ragged rows / columns
 DMA_CASES = [
     (64, 128, 2, 64, 64, "act"),
-    (128, 64, 2, 96, 40, "conv5"),
+    (128, 64, 2, 96, 40, "conv5"),  # (EP 1 / 2 take the DMA kernel only with CLIMSR_CONV_DMA=2)
     (128, 64, 1, 100, 33, "pullx"),
     (256, 256, 1, 32, 32, "plain"),
     (64, 128, 1, 64, 48, "bf16"),
@@ -124,7 +126,8 @@ def test_conv_fwd_lds_dma_matches_torch(cin, cout, n, h, w, mode):
     finally:
         ops.PROFILER = None
     torch.cuda.synchronize()
-    assert names and names[-1].startswith("conv_fwd_dma_kernel"), names
+    dma_all = os.environ.get("CLIMSR_CONV_DMA") == "2"
+    assert names and (names[-1].startswith("conv_fwd_dma_kernel") or (mode in ("conv5", "pullx") and not dma_all)), names
     want = F.conv2d(bf(x).double(), bf(wt).double(), None if b is None else b.double(), padding=1)
     if mode == "act":
         want = F.relu(want)
