@@ -2451,6 +2451,7 @@ template <int EP>
 static int launch_fwd_dma(const FwdArgs& a0, int ncob, hipStream_t s) {
   FwdArgs a = a0;
   a.tiles_y = ceil_div(a.out_h, DMA_TH);
+  a.nchunk = a.in_c / 32;  // 32-channel chunks (of a 32- or 64-channel packing)
   a.xgrp = conv_xcd_group(ncob, (long)64 * a.kpk * 2);
   a.stag_n = 0;
   if (g_dry) {
@@ -2692,6 +2693,27 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
   if (pt_shape(d, ep) && (d->out_c == 16 || d->out_c == 32 || d->out_c == 64) &&
       (d->in_c == 32 || d->in_c == 64 || d->in_c == 128))
     return dispatch_pt(d, a, s);
+  {  // the one-chunk 3x3 HR convs (HRconv, upconv1/2 with upsample-on-load, VGG conv1_2 and their data gradients: the
+     // conv_pw shapes below) on the LDS-DMA conv, over 32-channel halves of the 64-channel packing
+    static const int pwdma = env_flag("CLIMSR_CONV_DMA_PW", 0);  // (off until measured in the step)
+    const bool v8 = (a.out_c & 7) == 0 && ((a.out_cs | a.out_co) & 7) == 0 && !a.down2 && !a.res2 && !a.aux && a.out_mode == 0 &&
+                    a.res_f32 == 0;
+    int epx = plain_ep(a);
+    if (epx == 0 && v8 && !a.bias && a.res1 && ((a.r1_cs | a.r1_co) & 7) == 0 && (a.act == 3 || a.act == 4)) epx = 4;
+    if (pwdma && env_flag("CLIMSR_CONV_DMA", 1) && epx && d->ks == 3 && d->stride == 1 && d->pad == 1 && (d->up == 1 || d->up == 2) &&
+        (d->cc == 32 || d->cc == 64) && g.kcpad == 9 * d->cc && d->in_c % 32 == 0 && d->out_c == 64 && !cc4 && !ep->down2 &&
+        (d->out_h % DMA_TH == 0 || d->out_h >= 3 * DMA_TH) && (long)d->n * d->in_h * d->in_w * d->in_cstride * 2 < (1L << 31) &&
+        (long)64 * g.kpk * 2 < (1L << 31)) {
+      switch (epx) {
+        case 3: return launch_fwd_dma<3>(a, 1, s);
+        case 4: return launch_fwd_dma<4>(a, 1, s);
+        case 6: return launch_fwd_dma<6>(a, 1, s);
+        case 7: return launch_fwd_dma<7>(a, 1, s);
+        case 8: return launch_fwd_dma<8>(a, 1, s);
+        default: break;
+      }
+    }
+  }
   {  // weights-resident persistent kernel for one-chunk convs with 17..64 outputs (large-pixel-count layers)
     const int nt = fwd_nt(d->out_c);
     const long npx = (long)d->n * d->out_h * d->out_w;

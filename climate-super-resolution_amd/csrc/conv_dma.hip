@@ -142,16 +142,21 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
   const __amdgpu_buffer_rsrc_t wr = buf_rsrc(a.w, (uint32_t)((long)ncob * 64 * a.kpk * 2));
   // per-lane DMA source offsets of an item's chunk 0 (wave w issues x / weight instructions w + 8 i); out-of-image and
   // past-the-image lanes get BUF_OOB, which stays out of range at every chunk (zeros land in LDS)
+  // 32-channel chunk j of the packed weights (packing chunks of a.cc = 32 or 64 channels, tap-major within one):
+  // packing chunk j / (cc / 32) at kcpad elements each, its channels 32 (j % (cc / 32)) ..
+  const int ups = a.up == 2 ? 1 : 0, cpc = a.cc >> 5;
+  auto wchunk = [&](uint32_t j) { return ((j / cpc) * (uint32_t)a.kcpad + (j % cpc) * 32u) * 2u; };
   uint32_t xo[5], wo[5];
   auto offsets = [&](int nimg, int oy0, int ox0, int co0) {
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
       const int L = (wave + 8 * i) * 64 + lane, P = L >> 2, r = P / DMA_TPW, c = P - r * DMA_TPW;
+      // (up 2: nearest x2 upsample on load, source pixel = logical >> 1)
       const int iy = oy0 - 1 + r, ix = ox0 - 1 + c, ch = (L & 3) ^ (((c >> 2) & 1) << 1);
-      const bool ok = L < DMA_XU && iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w;
-      xo[i] = ok ? (uint32_t)((((nimg * a.in_h + iy) * a.in_w + ix) * a.in_cs + a.in_co + ch * 8) * 2) : BUF_OOB;
+      const bool ok = L < DMA_XU && iy >= 0 && iy < (a.in_h << ups) && ix >= 0 && ix < (a.in_w << ups);
+      xo[i] = ok ? (uint32_t)((((nimg * a.in_h + (iy >> ups)) * a.in_w + (ix >> ups)) * a.in_cs + a.in_co + ch * 8) * 2) : BUF_OOB;
       const int row = L / 36, slot = L - row * 36, wch = (slot & 3) ^ (((row >> 2) & 1) << 1);
-      wo[i] = L < 64 * 36 ? (uint32_t)(((co0 + row) * a.kpk + (slot >> 2) * 32 + wch * 8) * 2) : BUF_OOB;
+      wo[i] = L < 64 * 36 ? (uint32_t)(((co0 + row) * a.kpk + (slot >> 2) * a.cc + wch * 8) * 2) : BUF_OOB;
     }
   };
   const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
@@ -162,14 +167,13 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(off), "s"(rs), "s"(lds) : "memory");
   };
-  const uint32_t wstep = (uint32_t)a.kcpad * 2;
   // DMA piece p (0..9) of chunk j into buffer b: x instruction wave + 8 p (p < 5), weight instruction wave + 8 (p - 5)
   auto piece = [&](int p, uint32_t j, int b) {
     const uint32_t base = lds0 + (uint32_t)(b * DMA_BUF);
     if (p < 5) {
       if (wvu + 8 * p < DMA_XI) glds(xr, xo[p] + j * 64u, base + (uint32_t)((wvu + 8 * p) * 1024));
     } else if (wvu + 8 * (p - 5) < DMA_WI) {
-      glds(wr, wo[p - 5] + j * wstep, base + (uint32_t)(DMA_XB + (wvu + 8 * (p - 5)) * 1024));
+      glds(wr, wo[p - 5] + wchunk(j), base + (uint32_t)(DMA_XB + (wvu + 8 * (p - 5)) * 1024));
     }
   };
   // fragment offsets: weights row 16 t + col, tap k, group g at woff + 16 t * 576 + 64 k; x pixel (4 wave + m + dy,

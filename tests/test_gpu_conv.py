@@ -99,19 +99,26 @@ DMA_CASES = [
     (128, 64, 1, 100, 33, "pullx"),
     (256, 256, 1, 32, 32, "plain"),
     (64, 128, 1, 64, 48, "bf16"),
+    # the one-chunk HR shapes (64 -> 64 packed in one 64-channel chunk; upconv's nearest x2 upsample on load)
+    (64, 64, 2, 64, 40, "act"),
+    (64, 64, 1, 48, 24, "act", 2),
+    (64, 64, 1, 64, 32, "bf16"),
 ]
 
 
-@pytest.mark.parametrize("cin,cout,n,h,w,mode", DMA_CASES)
-def test_conv_fwd_lds_dma_matches_torch(cin, cout, n, h, w, mode):
+@pytest.mark.parametrize("case", DMA_CASES)
+def test_conv_fwd_lds_dma_matches_torch(case):
+    cin, cout, n, h, w, mode = case[:6]
+    up = case[6] if len(case) > 6 else 1
     import climsr_amd.ops as ops
     p, wt, b = make_plan(cin, cout, 3, seed=11, bias=mode in ("act", "conv5", "plain"))
     g = torch.Generator().manual_seed(12)
     x = torch.rand((n, cin, h, w), generator=g) * 2 - 1
     xin = to_nhwc(bf(x))
-    r = torch.rand((n, cout, h, w), generator=g) * 2 - 1
+    oh, ow = h * up, w * up
+    r = torch.rand((n, cout, oh, ow), generator=g) * 2 - 1
     f32 = mode in ("pullx", "plain")
-    y = torch.zeros((n, h, w, cout), dtype=torch.float32 if f32 else torch.bfloat16, device=DEV)
+    y = torch.zeros((n, oh, ow, cout), dtype=torch.float32 if f32 else torch.bfloat16, device=DEV)
     kw = dict(out_mode=OUT_F32 if f32 else OUT_BF16)
     if mode == "act":
         kw["act"] = ACT_RELU
@@ -122,13 +129,16 @@ def test_conv_fwd_lds_dma_matches_torch(cin, cout, n, h, w, mode):
     names = []
     ops.PROFILER = lambda name, flops, fn, tag="", nbytes=0: (names.append(name), fn())
     try:
-        p.fwd(xin, cin, 0, h, w, y, cout, 0, n, **kw)
+        p.fwd(xin, cin, 0, h, w, y, cout, 0, n, up=up, **kw)
     finally:
         ops.PROFILER = None
     torch.cuda.synchronize()
     dma_all = os.environ.get("CLIMSR_CONV_DMA") == "2"
     assert names and (names[-1].startswith("conv_fwd_dma_kernel") or (mode in ("conv5", "pullx") and not dma_all)), names
-    want = F.conv2d(bf(x).double(), bf(wt).double(), None if b is None else b.double(), padding=1)
+    xr = bf(x).double()
+    if up == 2:
+        xr = F.interpolate(xr, scale_factor=2, mode="nearest")
+    want = F.conv2d(xr, bf(wt).double(), None if b is None else b.double(), padding=1)
     if mode == "act":
         want = F.relu(want)
     elif mode == "conv5":
