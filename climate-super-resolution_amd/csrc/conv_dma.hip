@@ -152,7 +152,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
     for (int i = 0; i < 5; ++i) {
       const int L = (wave + 8 * i) * 64 + lane, P = L >> 2, r = P / DMA_TPW, c = P - r * DMA_TPW;
       // (up 2: nearest x2 upsample on load, source pixel = logical >> 1)
-      const int iy = oy0 - 1 + r, ix = ox0 - 1 + c, ch = (L & 3) ^ (((c >> 2) & 1) << 1);
+      const int iy = oy0 - a.pad + r, ix = ox0 - a.pad + c, ch = (L & 3) ^ (((c >> 2) & 1) << 1);
       const bool ok = L < DMA_XU && iy >= 0 && iy < (a.in_h << ups) && ix >= 0 && ix < (a.in_w << ups);
       xo[i] = ok ? (uint32_t)((((nimg * a.in_h + (iy >> ups)) * a.in_w + (ix >> ups)) * a.in_cs + a.in_co + ch * 8) * 2) : BUF_OOB;
       const int row = L / 36, slot = L - row * 36, wch = (slot & 3) ^ (((row >> 2) & 1) << 1);
