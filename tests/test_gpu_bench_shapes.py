@@ -8,6 +8,7 @@ over the same bf16-rounded operands: the only difference left is the kernels' fp
 ``REL`` of the result scale.  The last tests run one whole config-2 step (nb 11, B=32, 64->256) and the config-3
 GAN passes (nb 1, B=32, 64->256) against the oracle (oracle/climsr_ref.py) evaluated in fp32 with torch ops on the
 GPU, within the same envelope as the reference's own AMP training (test_gpu_generator.py)."""
+import os
 import pytest
 import torch
 import torch.nn.functional as F
@@ -187,7 +188,9 @@ def test_conv_pw_forward_at_256_b32(act):
     finally:
         ops.PROFILER = None
     torch.cuda.synchronize()
-    assert any(s.startswith("conv_pw_kernel") for s in names), names
+    # CLIMSR_CONV_DMA_PW=1 routes this one-chunk HR shape to the LDS-DMA conv instead
+    kern = "conv_fwd_dma_kernel" if os.environ.get("CLIMSR_CONV_DMA_PW", "0") == "1" else "conv_pw_kernel"
+    assert any(s.startswith(kern) for s in names), names
     for i in range(0, n, 8):  # float64 reference, 8 images at a time
         want = F.conv2d(x[i:i + 8].double(), bf(p.weight).double(), p.bias.double(), padding=1)
         if act == 1:
