@@ -97,7 +97,12 @@ class FlatParamsMixin:
 
     def _begin_autograd_grads(self):
         """Point every ``param.grad`` at a fresh flat buffer for one native backward (overwrite semantics); returns
-        (buffer, the previous grads) for ``_end_autograd_grads``."""
+        (buffer, the previous grads) for ``_end_autograd_grads``.  The overlapped flat-buffer reducer
+        (core/ddp.OverlappedGradAllReducer) reads ``_flat_grad`` through the grad-ready hook, which this route does not
+        fill: the two gradient routes are exclusive."""
+        if getattr(self, "_grad_ready_hook", None) is not None:
+            raise RuntimeError("a grad-ready hook (the flat-buffer DDP reducer) is installed, but this backward hands its "
+                               "gradients to autograd (torch DDP): use one data-parallel route, not both")
         buf = torch.empty_like(self._flat_grad)
         saved = [p.grad for p, _o, _n in self._flat_index]
         for p, off, n in self._flat_index:

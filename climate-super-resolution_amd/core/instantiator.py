@@ -53,11 +53,14 @@ class HydraInstantiator:
             from .optim import AdamW
 
             params = {k: v for k, v in cfg.items() if not k.startswith("_")}
-            odd = {k: v for k, v in params.items() if k in AdamW._UNSUPPORTED and v != AdamW._UNSUPPORTED[k]}
+            unsupported = dict(AdamW._UNSUPPORTED, amsgrad=False)
+            odd = {k: v for k, v in params.items() if k in unsupported and v != unsupported[k]}
             if not odd:
                 return AdamW(model.parameters(), owner=model, **params)
-            # options the fused update does not implement (maximize, foreach, fused, ...): torch's own AdamW + repack
-        opt = self.instantiate(cfg, model.parameters())
+            # options the fused update does not implement (amsgrad, maximize, foreach, ...): torch's own AdamW + repack
+            opt = torch.optim.AdamW(model.parameters(), **params)
+        else:
+            opt = self.instantiate(cfg, model.parameters())
         if native:
             step = opt.step
 

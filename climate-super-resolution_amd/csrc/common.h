@@ -14,6 +14,10 @@ namespace climsr {
 
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
+// CU count of the current device (cached per device, thread-safe)
+int device_cus();
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device), thread-safe, error checked
+int lds_opt_in(const void* fn, int bytes);
 
 __device__ __forceinline__ uint16_t f2bf(float f) {
   __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32: RNE, NaN-preserving

@@ -10,6 +10,8 @@
 // MFMA: v_mfma_f32_16x16x32_bf16.  Lane l: A[row l&15][k 8(l>>4)+j], B[k 8(l>>4)+j][col l&15],
 // C[row 4(l>>4)+i][col l&15].
 #include <algorithm>
+#include <atomic>
+#include <mutex>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -47,6 +49,57 @@ int check_launch(const char* what) {
   if (e != hipSuccess) {
     set_error("%s: %s", what, hipGetErrorString(e));
     return CLIMSR_EHIP;
+  }
+  return CLIMSR_OK;
+}
+
+// Per-device launch facts, shared by every dispatcher (one process may drive several devices from several threads):
+// the CU count of the CURRENT device and the dynamic-LDS opt-in of a kernel on it, each settled once per device
+// under a mutex; readers of a settled entry take no lock.
+static constexpr int MAX_DEV = 64;
+static std::mutex g_rt_mu;
+static std::atomic<int> g_ncu[MAX_DEV];
+
+static int current_device() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEV) dev = 0;
+  return dev;
+}
+
+int device_cus() {
+  const int dev = current_device();
+  int n = g_ncu[dev].load(std::memory_order_acquire);
+  if (n > 0) return n;
+  std::lock_guard<std::mutex> lk(g_rt_mu);
+  n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  g_ncu[dev].store(n, std::memory_order_release);
+  return n;
+}
+
+int lds_opt_in(const void* fn, int bytes) {
+  struct Key {
+    const void* fn;
+    int dev;
+  };
+  static Key done[1024];
+  static std::atomic<int> ndone{0};
+  const int dev = current_device();
+  const int seen = ndone.load(std::memory_order_acquire);
+  for (int i = 0; i < seen; ++i)
+    if (done[i].fn == fn && done[i].dev == dev) return CLIMSR_OK;
+  std::lock_guard<std::mutex> lk(g_rt_mu);
+  const int m = ndone.load(std::memory_order_relaxed);
+  for (int i = 0; i < m; ++i)
+    if (done[i].fn == fn && done[i].dev == dev) return CLIMSR_OK;
+  const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e != hipSuccess) {
+    set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize=%d): %s", bytes, hipGetErrorString(e));
+    return CLIMSR_EHIP;
+  }
+  if (m < 1024) {
+    done[m] = Key{fn, dev};
+    ndone.store(m + 1, std::memory_order_release);
   }
   return CLIMSR_OK;
 }
@@ -981,21 +1034,13 @@ static int launch_n16(const FwdArgs& a, hipStream_t s) {
   size_t lds = (size_t)N16_TPH * N16_TPW * (NCB * 32 + 16) * 2;
   const size_t lds_p = (size_t)NCB * N16_TH * 64 * 16;             // partial sums (aliased)
   if (lds_p > lds) lds = lds_p;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
-  }
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (ncu <= 0) ncu = 256;
-  }
-  static int per_cu = 0;
+  if (int e = lds_opt_in((const void*)k, 160 * 1024)) return e;
+  const int ncu = device_cus();
+  static std::atomic<int> occ{0};  // workgroups per CU: a property of the kernel and the architecture
+  int per_cu = occ.load(std::memory_order_relaxed);
   if (!per_cu) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, 256, lds) != hipSuccess || per_cu <= 0) per_cu = 2;
+    occ.store(per_cu, std::memory_order_relaxed);
   }
   int ntiles = a.tiles_x * a.tiles_y * a.n;
   int grid = ntiles < per_cu * ncu ? ntiles : per_cu * ncu;
@@ -1547,21 +1592,8 @@ static int launch_pw_geo(const FwdArgs& a0, const PwGeom& g, hipStream_t s) {
   a.lds_tab = (int)g.lds_tab;
   a.lds_x = (int)g.lds_w;  // offset of the input tile = tab + weights
   auto k = a.res_f32 ? conv_pw_kernel<NW, MW, NT, true, PV, EP, GEO> : conv_pw_kernel<NW, MW, NT, false, PV, EP, GEO>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)conv_pw_kernel<NW, MW, NT, true, PV, EP, GEO>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    (void)hipFuncSetAttribute((const void*)conv_pw_kernel<NW, MW, NT, false, PV, EP, GEO>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    attr_set = true;
-  }
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (ncu <= 0) ncu = 256;
-  }
+  if (int e = lds_opt_in((const void*)k, 160 * 1024)) return e;
+  const int ncu = device_cus();
   const int ntiles = a.tiles_x * a.tiles_y * a.n;
   const int grid = ntiles < ncu ? ntiles : ncu;
   hipLaunchKernelGGL(k, dim3(grid), dim3(64 * NW), g.lds_total, s, a);
@@ -2372,12 +2404,8 @@ static int launch_fwd_s2(const ClimsrConvDesc* d, FwdArgs a, hipStream_t s) {
     snprintf(g_dry_name, sizeof(g_dry_name), "conv_fwd_s2_kernel<%s>", a.bn_part ? "true" : "false");
     return CLIMSR_OK;
   }
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)conv_fwd_s2_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)conv_fwd_s2_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
-  }
+  if (int e = lds_opt_in(a.bn_part ? (const void*)conv_fwd_s2_kernel<true> : (const void*)conv_fwd_s2_kernel<false>, 160 * 1024))
+    return e;
   const dim3 grid(a.tiles_x * a.tiles_y * a.n, d->out_c / 64);
   if (a.bn_part) hipLaunchKernelGGL(conv_fwd_s2_kernel<true>, grid, dim3(512), S2F_LDS, s, a);
   else hipLaunchKernelGGL(conv_fwd_s2_kernel<false>, grid, dim3(512), S2F_LDS, s, a);
@@ -2392,25 +2420,14 @@ static bool dgrad_s2_shape(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, co
          d->out_w == 2 * d->in_w && ep->out_mode == 0 && !bias && !ep->res2 && !ep->aux && !ep->down2 && act_ok;
 }
 
-static int env_flag(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v && *v ? atoi(v) : dflt;
-}
 // channel blocks grouped per tile in the XCD-major order: the largest divisor of ncob (>= 2) whose weight blocks
 // together stay within ~2.5 MB of the XCD's 4 MB L2 (they are re-read by every tile of the group), else 0
 // the second dispatch round of a two-workgroups-per-CU launch starts late (conv_fwd_body 'Stagger')
 static void set_stagger(FwdArgs& a) {
-  static int ncu = 0, stag = -1;
-  if (!ncu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (ncu <= 0) ncu = 256;
-    stag = env_flag("CLIMSR_CONV_STAGGER", 2);  // 2 x 2048 cycles: GAN step 25.25 -> 24.98 ms (same box, 2 + 6 runs)
-  }
+  const int ncu = device_cus();
   a.stag_lo = ncu;
   a.stag_hi = 2 * ncu;
-  a.stag_n = stag;
+  a.stag_n = 2;  // 2 x 2048 cycles: GAN step 25.25 -> 24.98 ms (same box, 2 + 6 runs)
 }
 
 template <int MW, int NT>
@@ -2439,8 +2456,7 @@ static int launch_dgrad_s2(const ClimsrConvDesc* d, const FwdArgs& a, hipStream_
 }
 
 static int conv_xcd_group(int ncob, long wblk_bytes) {
-  static const int mode = env_flag("CLIMSR_CONV_XCD", 1);
-  if (!mode || ncob < 2) return 0;
+  if (ncob < 2) return 0;
   for (int gsz = ncob; gsz >= 2; --gsz)
     if (ncob % gsz == 0 && gsz * wblk_bytes <= (5L << 19)) return gsz;
   return 0;
@@ -2470,10 +2486,9 @@ static int launch_fwd_geo(const FwdArgs& a0, int ncob, size_t lds, hipStream_t s
     // (per 16 x 16 tile) only when every 32-row tile holds two whole 16-row tiles
     // RDB conv5 / pull-x (EP 1 / 2: 256 items at B=32 64^2, one round of one workgroup per CU) measured 7 % slower in
     // the GAN step than the two-workgroups-per-CU form (its chunk-0 latency and epilogue are not hidden in a single
-    // round); CLIMSR_CONV_DMA=2 takes them too, 0 none
-    static const int dma = env_flag("CLIMSR_CONV_DMA", 1);
+    // round)
     const bool fits = (EP == 9 || EP == 10) ? a0.out_h % DMA_TH == 0 : (a0.out_h % DMA_TH == 0 || a0.out_h >= 3 * DMA_TH);
-    if ((dma == 2 || (dma == 1 && EP != 1 && EP != 2)) && !a0.down2 && fits) return launch_fwd_dma<EP>(a0, ncob, s);
+    if (EP != 1 && EP != 2 && !a0.down2 && fits) return launch_fwd_dma<EP>(a0, ncob, s);
   }
   FwdArgs a = a0;
   a.xgrp = GEO == 1 ? conv_xcd_group(ncob, (long)NT * 16 * a.kpk * 2) : 0;
@@ -2499,12 +2514,7 @@ static int launch_fwd_geo(const FwdArgs& a0, int ncob, size_t lds, hipStream_t s
     kf = conv_fwd_kernel<MW, NT, false, MV, PFX, PFW, EP, GEO>;
   }
   auto k = a.res_f32 ? kt : kf;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)kf, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
-  }
+  if (int e = lds_opt_in((const void*)k, 160 * 1024)) return e;
   hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a);
   return check_launch("conv2d_fwd");
 }
@@ -2559,6 +2569,10 @@ static bool bn_bwd_parts_ok(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, c
 
 extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, const uint16_t* wpk, const float* bias,
                                  const ClimsrEpilogue* ep, void* y, void* stream);
+namespace climsr {
+int conv_wr_launch(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const uint16_t* x, const uint16_t* wpk, int kpk,
+                   const float* bias, void* y, hipStream_t s, bool dry, char* name, int name_len);
+}
 
 extern "C" int64_t climsr_conv2d_fwd_bn_parts(const ClimsrConvDesc* d, const ClimsrEpilogue* ep) {
   if (!d || !ep || d->cc % 8 || d->cc <= 0 || d->stride < 1) return 0;
@@ -2693,26 +2707,9 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
   if (pt_shape(d, ep) && (d->out_c == 16 || d->out_c == 32 || d->out_c == 64) &&
       (d->in_c == 32 || d->in_c == 64 || d->in_c == 128))
     return dispatch_pt(d, a, s);
-  {  // the one-chunk 3x3 HR convs (HRconv, upconv1/2 with upsample-on-load, VGG conv1_2 and their data gradients: the
-     // conv_pw shapes below) on the LDS-DMA conv, over 32-channel halves of the 64-channel packing
-    static const int pwdma = env_flag("CLIMSR_CONV_DMA_PW", 0);  // (off until measured in the step)
-    const bool v8 = (a.out_c & 7) == 0 && ((a.out_cs | a.out_co) & 7) == 0 && !a.down2 && !a.res2 && !a.aux && a.out_mode == 0 &&
-                    a.res_f32 == 0;
-    int epx = plain_ep(a);
-    if (epx == 0 && v8 && !a.bias && a.res1 && ((a.r1_cs | a.r1_co) & 7) == 0 && (a.act == 3 || a.act == 4)) epx = 4;
-    if (pwdma && env_flag("CLIMSR_CONV_DMA", 1) && epx && d->ks == 3 && d->stride == 1 && d->pad == 1 && (d->up == 1 || d->up == 2) &&
-        (d->cc == 32 || d->cc == 64) && g.kcpad == 9 * d->cc && d->in_c % 32 == 0 && d->out_c == 64 && !cc4 && !ep->down2 &&
-        (d->out_h % DMA_TH == 0 || d->out_h >= 3 * DMA_TH) && (long)d->n * d->in_h * d->in_w * d->in_cstride * 2 < (1L << 31) &&
-        (long)64 * g.kpk * 2 < (1L << 31)) {
-      switch (epx) {
-        case 3: return launch_fwd_dma<3>(a, 1, s);
-        case 4: return launch_fwd_dma<4>(a, 1, s);
-        case 6: return launch_fwd_dma<6>(a, 1, s);
-        case 7: return launch_fwd_dma<7>(a, 1, s);
-        case 8: return launch_fwd_dma<8>(a, 1, s);
-        default: break;
-      }
-    }
+  {  // 64 -> 64 3x3: the weights resident in registers, wave-independent tiles (conv_wr.hip)
+    const int rc = conv_wr_launch(d, ep, x, wpk, g.kpk, bias, y, s, g_dry, g_dry_name, (int)sizeof(g_dry_name));
+    if (rc != -1) return rc;
   }
   {  // weights-resident persistent kernel for one-chunk convs with 17..64 outputs (large-pixel-count layers)
     const int nt = fwd_nt(d->out_c);
@@ -3665,11 +3662,7 @@ static int launch_wco1(const WgArgs& a, hipStream_t s) {
   const size_t lds_x = (size_t)4 * WCO1_XT * (NCF * 16 + 8) * 2 + (size_t)4 * KS * 8 * WCO1_DZL * 2;
   const size_t lds_r = (size_t)4 * KS * NCF * 64 * 16;
   const size_t lds = lds_x > lds_r ? lds_x : lds_r;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
-    attr_set = true;
-  }
+  if (int e = lds_opt_in((const void*)k, 159 * 1024)) return e;
   hipLaunchKernelGGL(k, dim3(a.nsplit), dim3(256), lds, s, a);
   return check_launch("conv2d_wgrad (co1m)");
 }
@@ -3758,11 +3751,7 @@ template <int NTC, int TB, int CI4>
 static int launch_wg(const WgArgs& a, int nblk, size_t lds, hipStream_t s) {
   if (dry_run("conv_wgrad_kernel<%d, %d, %d, false>", NTC, TB, CI4)) return CLIMSR_OK;
   auto k = conv_wgrad_kernel<NTC, TB, CI4>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
-  }
+  if (int e = lds_opt_in((const void*)k, 160 * 1024)) return e;
   hipLaunchKernelGGL(k, dim3(nblk, a.nsplit), dim3(256), lds, s, a);
   return check_launch("conv2d_wgrad");
 }
@@ -3830,34 +3819,25 @@ extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, c
     a.dzp = W64_P; a.ntapb = 1; a.lds_x = 0;
     a.stride = d->stride;
     // 8 waves (tap-split) pay off on the large-pixel-count convs (HRconv / upconv at 256^2: +8 %) and lose on the
-    // 64^2 dense-block GEMM (-19 %), measured with tests/perf_conv.py
+    // 64^2 dense-block GEMM (-19 %), measured with tools/perf_conv.py
     const bool ts2 = d->stride == 1 && (long)d->n * d->out_h * d->out_w >= (1L << 20);
-    static bool attr_set = false;
-    if (!attr_set) {
-      (void)hipFuncSetAttribute((const void*)conv_wgrad64_kernel<1, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      (void)hipFuncSetAttribute((const void*)conv_wgrad64_kernel<2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      (void)hipFuncSetAttribute((const void*)conv_wgrad64_kernel<1, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      (void)hipFuncSetAttribute((const void*)conv_wgrad64_glds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      attr_set = true;
-    }
-    a.xcd = env_flag("CLIMSR_W64_XCD", 1);
-    const dim3 grid = a.xcd ? dim3((d->out_c / 64) * (d->in_c / 64) * nsplit) : dim3((d->out_c / 64) * (d->in_c / 64), nsplit);
+    a.xcd = 1;
+    const dim3 grid = dim3((d->out_c / 64) * (d->in_c / 64) * nsplit);
     if (d->stride == 2) {
       a.tph = W64<2>::TPH; a.tpw = W64<2>::TPW;
       if (dry_run("conv_wgrad64_kernel<1, 2>")) return CLIMSR_OK;
+      if (int e = lds_opt_in((const void*)conv_wgrad64_kernel<1, 2>, 160 * 1024)) return e;
       hipLaunchKernelGGL((conv_wgrad64_kernel<1, 2>), grid, dim3(256), std::max(2 * W64<2>::LDS, W64_EP_LDS), (hipStream_t)stream, a);
     } else if (ts2) {
       a.tph = W64<1>::TPH; a.tpw = W64<1>::TPW;
       if (dry_run("conv_wgrad64_kernel<2, 1>")) return CLIMSR_OK;
+      if (int e = lds_opt_in((const void*)conv_wgrad64_kernel<2, 1>, 160 * 1024)) return e;
       hipLaunchKernelGGL((conv_wgrad64_kernel<2, 1>), grid, dim3(512), std::max(W64<1>::LDS, W64_EP_LDS), (hipStream_t)stream, a);
-    } else if (env_flag("CLIMSR_W64_GLDS", 1)) {
-      a.tph = W64<1>::TPH; a.tpw = W64<1>::TPW;
-      if (dry_run("conv_wgrad64_glds_kernel")) return CLIMSR_OK;
-      hipLaunchKernelGGL(conv_wgrad64_glds_kernel, grid, dim3(256), std::max(W64G_LDS, W64_EP_LDS), (hipStream_t)stream, a);
     } else {
       a.tph = W64<1>::TPH; a.tpw = W64<1>::TPW;
-      if (dry_run("conv_wgrad64_kernel<1, 1>")) return CLIMSR_OK;
-      hipLaunchKernelGGL((conv_wgrad64_kernel<1, 1>), grid, dim3(256), std::max(2 * W64<1>::LDS, W64_EP_LDS), (hipStream_t)stream, a);
+      if (dry_run("conv_wgrad64_glds_kernel")) return CLIMSR_OK;
+      if (int e = lds_opt_in((const void*)conv_wgrad64_glds_kernel, 160 * 1024)) return e;
+      hipLaunchKernelGGL(conv_wgrad64_glds_kernel, grid, dim3(256), std::max(W64G_LDS, W64_EP_LDS), (hipStream_t)stream, a);
     }
     return check_launch("conv2d_wgrad (64x64 block)");
   }
@@ -3881,11 +3861,7 @@ extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, c
     a.ntapb = 1;
     if (dry_run("conv_wgrad_kernel<4, 6, 1, true>")) return CLIMSR_OK;
     auto k = conv_wgrad_kernel<4, 6, 1, true>;
-    static bool attr_set = false;
-    if (!attr_set) {
-      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      attr_set = true;
-    }
+    if (int e = lds_opt_in((const void*)k, 160 * 1024)) return e;
     hipLaunchKernelGGL(k, dim3(1, nsplit), dim3(256), w.lds_total, s, a);
     return check_launch("conv2d_wgrad (ci4, wave-split taps)");
   }

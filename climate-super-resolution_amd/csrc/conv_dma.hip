@@ -2,7 +2,6 @@
 // path (VGG19 perceptual-loss convs climsr/losses/perceptual.py:22-36, RDB conv5 / its data gradient
 // climsr/models/esrgan.py:26,32-38, the discriminator's stride-1 layers climsr/models/rfb_esrgan.py:28-52).
 #include <algorithm>
-#include <stdlib.h>
 
 #include "conv_ep.h"
 
@@ -330,11 +329,6 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
 }
 
 namespace climsr {
-static int env_flag_dma(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v && *v ? atoi(v) : dflt;
-}
-
 int fwd_dma_launch(int ep, const FwdArgs& a, int ncob, hipStream_t s) {
   void (*k)(FwdArgs) = nullptr;
   const bool rf = a.res_f32 != 0;
@@ -345,22 +339,12 @@ int fwd_dma_launch(int ep, const FwdArgs& a, int ncob, hipStream_t s) {
     default: set_error("conv2d_fwd: no LDS-DMA kernel for epilogue %d", ep); return CLIMSR_EINVAL;
   }
 #undef DMA_EP
-  static bool attr_set[16][2] = {};
-  static int ncu = 0;
-  if (!attr_set[ep][rf]) {
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set[ep][rf] = true;
-  }
-  if (!ncu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    ncu = ncu >= 8 ? ncu / 8 * 8 : 256;
-  }
+  if (int e = lds_opt_in((const void*)k, 160 * 1024)) return e;
+  int ncu = device_cus();
+  ncu = ncu >= 8 ? ncu / 8 * 8 : 8;  // a multiple of 8: an item's XCD is its workgroup's (kernel comment)
   // one workgroup per item with BatchNorm partials, else persistent: at most one workgroup per CU
   const int nitem = a.tiles_x * a.tiles_y * a.n * ncob;
-  static const int persist = env_flag_dma("CLIMSR_CONV_DMA_PERSIST", 1);
-  const int grid = (ep == 9 || ep == 10 || !persist) ? nitem : std::min(nitem, ncu);
+  const int grid = (ep == 9 || ep == 10) ? nitem : std::min(nitem, ncu);
   hipLaunchKernelGGL(k, dim3(grid), dim3(512), DMA_LDS, s, a);
   return CLIMSR_OK;
 }

@@ -1,0 +1,244 @@
+// 64 -> 64-channel 3x3 stride-1 convolution with the weights resident in registers (CDNA4, gfx950).
+//
+// Replaces nn.Conv2d on the HR-resolution / large-grid 64-channel layers: HRconv and upconv1/2 with the nearest x2
+// upsample on load (climsr/models/esrgan.py:82-83,94-99), VGG19 conv1_2 (climsr/losses/perceptual.py:16), RCAN's
+// residual-block convs (climsr/models/rcan.py:50-69) and their activation-backward data gradients.
+//
+// The 72 A fragments of the whole weight matrix (64 co x 576 k: 4 co blocks x 18 k blocks of 16 x 32 bf16) stay in
+// registers for the launch -- 60 in AGPRs, read by the MFMAs from there (mfma_agpr.h), the last 12 in VGPRs -- so the
+// LDS holds pixels only and every 1 KB B fragment read feeds 4 MFMAs (one per co block): 0.25 KB of LDS reads per
+// MFMA, against 0.75 for conv_pw's 8-wave form that re-reads the weights from LDS.
+// Waves are independent: each owns a 4 x 16-pixel output tile at a time, brings its 6 x 18-pixel input footprint
+// (64 channels, pitch 80 bf16 = conflict-free b128 reads) into its own pair of LDS buffers with LDS-DMA
+// (buffer_load ... lds: no staging registers, no ds_write), the next tile's footprint landing while the current one
+// computes, and stores its epilogue straight from the accumulators.  No workgroup barrier anywhere: the four waves of
+// a CU drift apart, so one wave's epilogue and DMA waits overlap the others' MFMAs (the lockstep of identical
+// workgroups is what held conv_pw and the generic conv).
+// Tiles: wave w of workgroup b (XCD-major renumbered) takes tiles 4 (b + k G) + w: the four waves of a CU work on four
+// horizontally adjacent tiles (shared halo columns) and consecutive workgroups of an XCD on the next ones.
+#include <algorithm>
+#include <stdio.h>
+
+#include "conv_ep.h"
+#include "mfma_agpr.h"
+
+namespace {
+
+constexpr int WR_TR = 4, WR_TC = 16;                    // output rows x columns of a wave tile
+constexpr int WR_PR = WR_TR + 2, WR_PC = WR_TC + 2;     // input footprint (3x3, pad 1)
+constexpr int WR_XP = 80;                               // footprint pixel pitch (bf16): 64 channels + 16 pad
+constexpr int WR_SPP = WR_XP / 8;                       // 16 B slots per pixel (8 data + 2 pad)
+constexpr int WR_SLOTS = WR_PR * WR_PC * WR_SPP;        // 1080
+constexpr int WR_NI = (WR_SLOTS + 63) / 64;             // LDS-DMA instructions per footprint (17)
+constexpr int WR_BUF = WR_NI * 1024;                    // bytes per footprint buffer
+constexpr int WR_LDS = 4 * 2 * WR_BUF;                  // 4 waves x 2 buffers: 139,264 B
+static_assert(WR_LDS <= 160 * 1024, "conv_wr LDS");
+
+struct WrArgs {
+  const uint16_t* x;
+  const uint16_t* w;     // packed [64 co][kpk], k = tap * 64 + channel
+  const float* bias;     // may be null
+  uint16_t* y;
+  const uint16_t* res1;  // EP 1: residual (v = alpha1 v + beta1 r); EP 2: the activation output (act 3 / 4)
+  int n, in_h, in_w, in_cs, in_co, up, out_h, out_w, out_cs, out_co, kpk;
+  int act;  // forward: 0 none, 1 leaky relu, 2 relu; EP 2: 3 / 4 = backward of leaky relu / relu
+  float slope, alpha1, beta1;
+  int r1_cs, r1_co;
+  int tiles_x, tiles_y, ntiles;
+  uint32_t x_bytes, y_bytes, r1_bytes;
+};
+typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
+
+template <int EP>
+__global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NEPI = EP == 0 ? 16 : 32;  // vector-memory operations of one epilogue (loads + stores), fixed per lane
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, col = lane & 15;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int G4 = (int)gridDim.x * 4;
+  int T = xcd_major(blockIdx.x, gridDim.x) * 4 + wv;
+  if (T >= a.ntiles) return;
+
+  // ---- the weight matrix: A fragment (co block t, k block j) = rows 16 t + col, k = 32 j + 8 g ..
+  bf16x8 afb[4][18];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int j = 0; j < 18; ++j) afb[t][j] = *(const bf16x8*)(a.w + (long)(t * 16 + col) * a.kpk + j * 32 + g * 8);
+  float bias[4][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const float4 b4 = a.bias ? *(const float4*)(a.bias + t * 16 + 4 * g) : make_float4(0.f, 0.f, 0.f, 0.f);
+    bias[t][0] = b4.x; bias[t][1] = b4.y; bias[t][2] = b4.z; bias[t][3] = b4.w;
+  }
+
+  // ---- footprint DMA: instruction i, lane l fills 16 B slot q = 64 i + l = (pixel q / 10, slot q % 10); slots 8, 9
+  // of a pixel (the pitch padding) and slots past the footprint get zeros (out-of-range source offset)
+  int dg[WR_NI];
+#pragma unroll
+  for (int i = 0; i < WR_NI; ++i) {
+    const int q = i * 64 + lane, p = q / WR_SPP, c = q - p * WR_SPP;
+    dg[i] = (p < WR_PR * WR_PC && c < 8) ? ((p / WR_PC) << 16) | ((p % WR_PC) << 8) | c : -1;
+  }
+  const __amdgpu_buffer_rsrc_t xr = buf_rsrc(a.x, a.x_bytes);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
+  const uint32_t mybuf = lds0 + (uint32_t)(wv * 2 * WR_BUF);
+  const int ups = a.up == 2 ? 1 : 0, lh = a.in_h << ups, lw = a.in_w << ups;
+  // in asm (not the builtin): hipcc would wait vmcnt(0) before the next ds_read for an LDS write of unknown extent;
+  // the DMAs are counted by hand.  M0 = the instruction's LDS destination (wave-uniform).
+  auto glds = [&](uint32_t off, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(off), "s"(xr), "s"(lds) : "memory");
+  };
+  auto decode = [&](int tile, int& nimg, int& oy0, int& ox0) {
+    const int tx = tile % a.tiles_x, r = tile / a.tiles_x, ty = r % a.tiles_y;
+    nimg = r / a.tiles_y;
+    oy0 = ty * WR_TR;
+    ox0 = tx * WR_TC;
+  };
+  auto issue = [&](int tile, int b) {  // tile < 0: zeros (keeps the per-iteration DMA count fixed)
+    int nimg = 0, oy0 = -1 << 20, ox0 = 0;
+    if (tile >= 0) decode(tile, nimg, oy0, ox0);
+    const uint32_t dst = mybuf + (uint32_t)(b * WR_BUF);
+#pragma unroll
+    for (int i = 0; i < WR_NI; ++i) {
+      const int iy = oy0 - 1 + (dg[i] >> 16), ix = ox0 - 1 + ((dg[i] >> 8) & 255), c = dg[i] & 255;
+      const bool ok = dg[i] >= 0 && iy >= 0 && iy < lh && ix >= 0 && ix < lw;
+      const uint32_t off = (uint32_t)((((long)(nimg * a.in_h + (iy >> ups)) * a.in_w + (ix >> ups)) * a.in_cs + a.in_co + c * 8) * 2);
+      glds(ok ? off : BUF_OOB, dst + (uint32_t)(i * 1024));
+    }
+  };
+
+  const __amdgpu_buffer_rsrc_t yr = buf_rsrc(a.y, a.y_bytes);
+  const __amdgpu_buffer_rsrc_t rr = buf_rsrc(a.res1, EP ? a.r1_bytes : 0u);
+  const int lb = col * WR_XP * 2 + g * 16;  // this lane's byte offset in a footprint row: pixel col, channels 8 g ..
+  issue(T, 0);
+  for (int it = 0;; ++it) {
+    const int Tn = T + G4;
+    issue(Tn < a.ntiles ? Tn : -1, (it + 1) & 1);
+    // tile T's footprint has landed once at most the younger operations are outstanding: the last epilogue's and
+    // the DMA just issued
+    if (it == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WR_NI) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WR_NI + NEPI) : "memory");
+    const char* xb = smem + (wv * 2 + (it & 1)) * WR_BUF + lb;
+    f32x4 acc[4][4];  // [output row m][co block t]
+    bf16x8 bq[2][4];
+    auto ldb = [&](int j, int s) {  // k block j = tap j / 2, channels 32 (j % 2) ..: the 4 rows' B fragments
+      const int tap = j >> 1, ky = tap / 3, kx = tap % 3;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) bq[s][m] = *(const bf16x8*)(xb + ((m + ky) * WR_PC + kx) * WR_XP * 2 + (j & 1) * 64);
+    };
+    ldb(0, 0);
+#pragma unroll
+    for (int j = 0; j < 18; ++j) {
+      if (j + 1 < 18) ldb(j + 1, (j + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        if (j == 0) mfma4x_agpr<true, false>(acc[m][0], acc[m][1], acc[m][2], acc[m][3], afb[0][j], afb[1][j], afb[2][j], afb[3][j], bq[0][m]);
+        else if (j < 6) mfma4x_agpr<false, false>(acc[m][0], acc[m][1], acc[m][2], acc[m][3], afb[0][j], afb[1][j], afb[2][j], afb[3][j], bq[j & 1][m]);
+        else mfma4x_agpr<false, true>(acc[m][0], acc[m][1], acc[m][2], acc[m][3], afb[0][j], afb[1][j], afb[2][j], afb[3][j], bq[j & 1][m]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    pad_mfma16(acc);
+    // ---- epilogue straight from the accumulators: lane (col, g) holds co 16 t + 4 g .. + 3 of pixel (m, col);
+    // every lane issues the same number of loads / stores (out-of-range offsets are dropped)
+    int nimg, oy0, ox0;
+    decode(T, nimg, oy0, ox0);
+    const int ox = ox0 + col;
+    uint32_t off[4];
+    uint2 rv[4][4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int oy = oy0 + m;
+      const bool ok = oy < a.out_h && ox < a.out_w;
+      const long pix = ((long)nimg * a.out_h + oy) * a.out_w + ox;
+      off[m] = ok ? (uint32_t)((pix * a.out_cs + a.out_co + 4 * g) * 2) : BUF_OOB;
+      if constexpr (EP != 0) {
+        const uint32_t ro = ok ? (uint32_t)((pix * a.r1_cs + a.r1_co + 4 * g) * 2) : BUF_OOB;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const auto v = __builtin_amdgcn_raw_buffer_load_b64(rr, ro == BUF_OOB ? BUF_OOB : ro + (uint32_t)(t * 32), 0, 0);
+          rv[m][t] = make_uint2(v[0], v[1]);
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float x = acc[m][t][i] + bias[t][i];
+          if constexpr (EP == 2) {
+            const uint32_t w = i < 2 ? rv[m][t].x : rv[m][t].y;
+            const float r = __uint_as_float((i & 1) ? (w & 0xFFFF0000u) : (w << 16));
+            x = r > 0.f ? x : (a.act == 3 ? x * a.slope : 0.f);
+          } else {
+            if (a.act == 1) x = x > 0.f ? x : x * a.slope;
+            else if (a.act == 2) x = x > 0.f ? x : 0.f;
+            if constexpr (EP == 1) {
+              const uint32_t w = i < 2 ? rv[m][t].x : rv[m][t].y;
+              const float r = __uint_as_float((i & 1) ? (w & 0xFFFF0000u) : (w << 16));
+              x = x * a.alpha1 + a.beta1 * r;
+            }
+          }
+          v[i] = x;
+        }
+        const bf16x2 p0 = {(__bf16)v[0], (__bf16)v[1]}, p1 = {(__bf16)v[2], (__bf16)v[3]};
+        const v2u32 pk = {__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1)};
+        __builtin_amdgcn_raw_buffer_store_b64(pk, yr, off[m] == BUF_OOB ? BUF_OOB : off[m] + (uint32_t)(t * 32), 0, 0);
+      }
+    if (Tn >= a.ntiles) break;
+    T = Tn;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the zero-filling DMA past the last tile lands before the wave ends
+}
+
+}  // namespace
+
+namespace climsr {
+
+// shape check + launch (called from climsr_conv2d_fwd's dispatcher); returns -1 when the shape is not this kernel's
+int conv_wr_launch(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const uint16_t* x, const uint16_t* wpk, int kpk,
+                   const float* bias, void* y, hipStream_t s, bool dry, char* name, int name_len) {
+  const bool res = ep->res1 != nullptr;
+  int epk = -1;
+  if (!res && ep->act >= 0 && ep->act <= 2) epk = 0;
+  else if (res && ep->act == 0 && !(ep->res_f32 & 1)) epk = 1;
+  else if (res && (ep->act == 3 || ep->act == 4) && !bias && !(ep->res_f32 & 1)) epk = 2;
+  const long opx = (long)d->n * d->out_h * d->out_w;
+  if (epk < 0 || d->in_c != 64 || d->out_c != 64 || d->cc != 64 || d->ks != 3 || d->stride != 1 || d->pad != 1 ||
+      (d->up != 1 && d->up != 2) || d->out_h != d->in_h * d->up || d->out_w != d->in_w * d->up || d->in_cstride % 8 ||
+      d->in_coff % 8 || (d->out_cstride | d->out_coff) & 3 || ep->down2 || ep->res2 || ep->aux || ep->out_mode != 0 ||
+      ep->bn_part || kpk < 576 || (res && ((ep->res1_cstride | ep->res1_coff) & 3)) ||
+      (long)d->n * d->in_h * d->in_w * d->in_cstride * 2 >= (1L << 31) || opx * d->out_cstride * 2 >= (1L << 31) ||
+      (res && opx * ep->res1_cstride * 2 >= (1L << 31)))
+    return -1;
+  if (dry) {
+    snprintf(name, name_len, "conv_wr_kernel<%d>", epk);
+    return CLIMSR_OK;
+  }
+  WrArgs a;
+  a.x = x; a.w = wpk; a.bias = bias; a.y = (uint16_t*)y; a.res1 = (const uint16_t*)ep->res1;
+  a.n = d->n; a.in_h = d->in_h; a.in_w = d->in_w; a.in_cs = d->in_cstride; a.in_co = d->in_coff; a.up = d->up;
+  a.out_h = d->out_h; a.out_w = d->out_w; a.out_cs = d->out_cstride; a.out_co = d->out_coff; a.kpk = kpk;
+  a.act = ep->act; a.slope = ep->slope; a.alpha1 = ep->alpha1; a.beta1 = ep->beta1;
+  a.r1_cs = ep->res1_cstride; a.r1_co = ep->res1_coff;
+  a.tiles_x = ceil_div(d->out_w, WR_TC); a.tiles_y = ceil_div(d->out_h, WR_TR);
+  a.ntiles = a.tiles_x * a.tiles_y * d->n;
+  a.x_bytes = (uint32_t)((long)d->n * d->in_h * d->in_w * d->in_cstride * 2);
+  a.y_bytes = (uint32_t)(opx * d->out_cstride * 2);
+  a.r1_bytes = res ? (uint32_t)(opx * ep->res1_cstride * 2) : 0u;
+  const int ncu = device_cus();
+  const int grid = std::min(ceil_div(a.ntiles, 4), ncu);
+  void (*k)(WrArgs) = epk == 0 ? conv_wr_kernel<0> : epk == 1 ? conv_wr_kernel<1> : conv_wr_kernel<2>;
+  if (int e = lds_opt_in((const void*)k, WR_LDS)) return e;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), WR_LDS, s, a);
+  return check_launch("conv2d_fwd (wr)");
+}
+
+}  // namespace climsr

@@ -2,43 +2,51 @@
 //
 // Forward:        x1 = lrelu(conv1(x)),  x2 = lrelu(conv2([x,x1])),  x3 = ...,  x4 = lrelu(conv4([x,x1,x2,x3]))
 // Pull backward:  dZ4 = lrelu'(x4) * pull4(dZ5),  dZ3 = lrelu'(x3) * pull3([dZ5,dZ4]),  ...  (climsr_hip.h)
-// Both are "level L reads a 64-channel base plus the 16-channel outputs of levels < L".  Run conv by conv, every
-// level re-reads its whole input from HBM (352 channel-reads per pixel for 64 read + 64 written here) and the
-// four launches are latency-bound (two 8x16 tiles per workgroup each).
+// Both are "level L reads a 64-channel base plus the 16-channel outputs of levels < L".
 //
-// Here one workgroup owns R full-width image rows (width <= 64: 4 column fragments of 16 pixels, no horizontal
-// halo) and streams down them.  Step s: level 1 computes row y1 = r0 - 3 + s, level L row y1 - 2(L - 1) (every row
-// it reads from level L-1 was written in an earlier step: one barrier per step).  LDS holds a 10-row ring of the
-// base (64 ch) and an 8-row ring of the level outputs [out1|out2|out3] (48 ch); only the rows of the strip are
-// stored to HBM, the 3 + 2 + 1 halo rows above / below each strip are recomputed by the neighbouring strips.
-// Wave w (one per SIMD) owns column fragment w of EVERY level, so the four SIMDs carry equal work; its A
-// fragments (weights: 16 co x 32 k, 100 fragments over the four levels) sit in VGPRs/AGPRs for the whole launch
-// and each MFMA reads one B fragment (16 pixels x 32 channels of one tap) from LDS with ds_read_b128.
-// K blocking: the base part of a level is 9 taps x 2 blocks of 32 channels; the dense part is one block per tap for
-// 32 channels (out1|out2) and, for a 16-channel group (out1 of level 2, out3 of level 4), PAIRS of taps in one block
-// (lanes 0-31 read tap 2p, lanes 32-63 tap 2p+1): 5 blocks instead of 9 half-empty ones.
+// A level is a skinny GEMM (16 output channels): every MFMA needs a fresh 1 KB B fragment of pixels (16 px x 32 k)
+// while its A fragment (weights) can stay in registers, so computed level by level the LDS read rate, not the matrix
+// core, bounds it (1 KB per 16-cycle MFMA per SIMD = the whole 256 B/clk of the CU).  But the base part of the four
+// levels (K = 9 x 64 of K = 9 x (64 + 16(L-1))) does not depend on the chain: it is ONE 64 -> 64-channel conv.  So
+// here a wave owns a 16-pixel column fragment for ALL four levels: when base row y arrives it computes the base part
+// of row y for all four levels at once (each B fragment feeds four MFMAs), keeps the partial sums of the levels that
+// finish row y later in registers, and each level adds its dense part (the outputs of the earlier levels, from an LDS
+// ring) when that row's inputs exist: level L finishes row y1 - 2(L-1) in step y1 (one barrier per step).
+//
+// A workgroup (4 waves, one per SIMD) streams down R rows of a 64-column window (4 fragments).  Images up to 64
+// columns wide are one window (zero padding at the image edges); wider ones are cut into strips of 48 own columns,
+// whose window adds 8 columns each side (the halo of 3 + 2 + 1 columns the chain consumes; the window's edge values
+// are wrong and never stored).  The 3 + 2 + 1 halo rows above / below a strip are recomputed by its neighbours.
+// LDS: a 4-row ring of the base (64 ch), an 8-row ring of the level outputs [out1|out2|out3] (48 ch), the dense-part
+// A fragments of levels 3 and 4 (23 KB) and per wave the fp32 partial sums of levels 3 / 4 in flight (4 / 6 rows, one
+// 1 KB lane-linear slot each); registers: the base-part A fragments of all four levels (72 x 16 B per lane), level 2's
+// dense A fragments and its partial sums (two rows: the step loop runs two steps per iteration, so they never move).
 // MFMA v_mfma_f32_16x16x32_bf16: A = weights [16 co][32 k], B = [32 k][16 pixels], C lane = 4 co of one pixel.
 #include "common.h"
+#include "mfma_agpr.h"
 
 using namespace climsr;
 
-#ifndef CLIMSR_CHAIN_DIAG
-#define CLIMSR_CHAIN_DIAG 0  // diagnostic builds only (tests/diag_build.sh): 1 = no MFMAs, 2 = no output stores, 3 = no row loads
-#endif
-
 namespace {
 
-constexpr int RC_W = 64;                         // widest image row (4 fragments)
-constexpr int RC_COLS = RC_W + 2;                // LDS pixel slots per row: image columns -1 .. 64
-constexpr int RC_XP = 64 + 16;                   // base pixel pitch (bf16): == 16 (mod 32), conflict-free b128 reads
-constexpr int RC_DP = 48;                        // dense pixel pitch: out1 | out2 | out3 (== 16 mod 32)
-constexpr int RC_XD = 10;                        // base ring rows (y1-7 .. y1+1 read, y1+2 staged)
-constexpr int RC_DD = 8;                         // dense ring rows (y1-7 .. y1-1 read, y1 written)
-constexpr int RC_XROW = RC_COLS * RC_XP;
-constexpr int RC_DROW = RC_COLS * RC_DP;
-constexpr int RC_OFF_D = RC_XD * RC_XROW;        // elements
-constexpr int RC_LDS = (RC_OFF_D + RC_DD * RC_DROW) * 2;  // 156,288 B
-constexpr int RC_XCH = RC_COLS * 8;              // 16 B chunks of one base row (528)
+constexpr int NFR = 4;                          // 16-pixel column fragments per window = waves per workgroup
+constexpr int WIN = 16 * NFR;                   // window columns
+constexpr int HALO_X = 8;                       // window columns on each side of a strip's own columns (wide images)
+constexpr int COLS = WIN + 2;                   // LDS pixel slots per ring row: window columns -1 .. WIN
+constexpr int XP = 64 + 16;                     // base pixel pitch (bf16): == 16 (mod 32), conflict-free b128 reads
+constexpr int DP = 48;                          // dense pixel pitch: out1 | out2 | out3 (== 16 mod 32)
+constexpr int XD = 4;                           // base ring rows (y1-1 .. y1+1 read, y1+2 staged)
+constexpr int DD = 8;                           // dense ring rows (y1-7 .. y1-1 read, y1 written)
+constexpr int XROW = COLS * XP, DROW = COLS * DP;
+constexpr int OFF_D = XD * XROW;                // elements
+constexpr int OFF_A = OFF_D + DD * DROW;        // dense-part A fragments of levels 3, 4 [block][lane][8 bf16]
+constexpr int NDA = 9 + 14;                     // their dense blocks
+constexpr int OFF_P = OFF_A + NDA * 512;        // partial sums: per wave 4 (level 3) + 6 (level 4) slots of 64 x f32x4
+constexpr int NPS = 4 + 6;
+constexpr int LDS_BYTES = OFF_P * 2 + NFR * NPS * 1024;  // 157,440 B
+constexpr int XCH = COLS * 8;                   // 16 B chunks of one base row
+constexpr int XIT = (XCH + 255) / 256;          // of them per thread
+static_assert(LDS_BYTES <= 160 * 1024, "rdb chain LDS");
 
 struct ChainArgs {
   const uint16_t* base;
@@ -52,17 +60,19 @@ struct ChainArgs {
   int mcs;
   int moff[4];
   float slope;
-  int n, h, w, rows, strips_y;
+  int n, h, w, rows, strips_y, strips_x, own_w, x_halo;
   uint32_t base_bytes, mask_bytes, out_bytes;
 };
 typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
 
 __host__ __device__ constexpr int kp_blocks(int L) { return L == 1 ? 2 : (L == 4 ? 4 : 3); }
 __host__ __device__ constexpr int nd_blocks(int L) { return L == 1 ? 0 : (L == 2 ? 5 : (L == 3 ? 9 : 14)); }
-__host__ __device__ constexpr int n_blocks(int L) { return 18 + nd_blocks(L); }
+__host__ __device__ constexpr int da_base(int L) { return L == 3 ? 0 : 9; }
 
 // The (tap, channel offset in the dense pixel) of lane group g in dense block j of level L; tap < 0: padding
-// (zero weights; the B read goes to tap 8 of the same block so every value read is finite).
+// (zero weights; the B read goes to tap 8 of the same block so every value read is finite).  A block is 32 k: one
+// tap of 32 channels (out1|out2), or for a 16-channel group (out1 of level 2, out3 of level 4) PAIRS of taps (lanes
+// 0-31 read tap 2p, lanes 32-63 tap 2p+1): 5 blocks instead of 9 half-empty ones.
 __device__ __forceinline__ void dense_src(int L, int j, int g, int& tap, int& ch) {
   if (L == 3 || (L == 4 && j < 9)) {
     tap = j;
@@ -75,274 +85,296 @@ __device__ __forceinline__ void dense_src(int L, int j, int g, int& tap, int& ch
   }
 }
 
-// A fragments of level L (16 co x 32 k per block) straight from the packed global weights ([16][9*KP], row pitch
-// 9*KP) into registers, kept for the whole launch: no LDS weight image, no workgroup barrier before the first base
-// rows are staged (the two waves of a level each fetch their 18-32 x 1 KB, L2-resident across the grid).
+// element offset (from the dense ring) of dense block j of level L for this lane: dr[ky] = ring row y-1+ky, ld / lp
+// = this lane's pixel (+ channel group) offsets within a row
 template <int L>
-__device__ __forceinline__ void load_af_global(const uint16_t* __restrict__ wt, int lane, bf16x8 (&af)[n_blocks(L)]) {
-  constexpr int KP = kp_blocks(L) * 32;
-  const int g = lane >> 4, col = lane & 15;
-  const uint16_t* wr = wt + col * 9 * KP;
-#pragma unroll
-  for (int j = 0; j < 18; ++j) af[j] = *(const bf16x8*)(wr + (j >> 1) * KP + (j & 1) * 32 + g * 8);
-#pragma unroll
-  for (int j = 0; j < nd_blocks(L); ++j) {
-    int tap, ch;
-    dense_src(L, j, g, tap, ch);
-    af[18 + j] = tap >= 0 ? *(const bf16x8*)(wr + tap * KP + 64 + ch) : (bf16x8){};
-  }
+__device__ __forceinline__ int dense_off(const int (&dr)[3], int ld, int lp, int g, int j) {
+  if (L == 3 || (L == 4 && j < 9)) return dr[j / 3] + ld + (j % 3) * DP;
+  const int p = L == 2 ? j : j - 9;
+  const int ta = 2 * p, tb = 2 * p + 1 <= 8 ? 2 * p + 1 : 2 * p;
+  const int oa = dr[ta / 3] + (ta % 3) * DP, ob = dr[tb / 3] + (tb % 3) * DP;
+  return (g >= 2 ? ob : oa) + lp + (L == 2 ? 0 : 32);
 }
 
-// One level row, two column fragments (16 pixels apart): acc0/acc1 = sum over the level's blocks.  xr[ky] / dr[ky]:
-// LDS element offsets of the base / dense ring rows y-1+ky; lx / ld / lp: this lane's pixel-column (+ channel
-// group) offsets within a row.  Every A fragment feeds two independent accumulators.
-template <int L>
-__device__ __forceinline__ const uint16_t* block_src(const uint16_t* lds, const int (&xr)[3], const int (&dr)[3], int lx,
-                                                     int ld, int lp, int g, int j) {
-  if (j < 18) {
-    const int t = j >> 1, ky = t / 3, kx = t % 3;
-    return lds + xr[ky] + lx + kx * RC_XP + (j & 1) * 32;
-  }
-  j -= 18;
-  int off;
-  if (L == 3 || (L == 4 && j < 9)) {
-    off = dr[j / 3] + ld + (j % 3) * RC_DP;
-  } else {
-    const int p = L == 2 ? j : j - 9;
-    const int ta = 2 * p, tb = 2 * p + 1 <= 8 ? 2 * p + 1 : 2 * p;
-    const int oa = dr[ta / 3] + (ta % 3) * RC_DP, ob = dr[tb / 3] + (tb % 3) * RC_DP;
-    off = (g >= 2 ? ob : oa) + lp + (L == 2 ? 0 : 32);
-  }
-  return lds + RC_OFF_D + off;
-}
-
-// Blocks run in groups of rc_group(L): the B fragments of group k+1 are read while group k is on the MFMA pipe, so
-// 2 x rc_group reads stay in flight (the group size is what each level's weight registers leave room for).
-__host__ __device__ constexpr int rc_group(int L) { return L <= 2 ? 6 : (L == 3 ? 5 : 4); }
-
-template <int L>
-__device__ __forceinline__ void level_acc(const uint16_t* lds, const bf16x8 (&af)[n_blocks(L)], const int (&xr)[3],
-                                          const int (&dr)[3], int lx, int ld, int lp, int g, f32x4& acc0, f32x4& acc1) {
-  constexpr int NB = n_blocks(L), G = rc_group(L), NG = (NB + G - 1) / G;
-  acc0 = (f32x4){0.f, 0.f, 0.f, 0.f};
-  acc1 = acc0;
-  bf16x8 b[2][G][2];
-  auto load = [&](int gi, bf16x8 (&bb)[G][2]) {
-#pragma unroll
-    for (int i = 0; i < G; ++i) {
-      const int j = gi * G + i;
-      if (j < NB) {
-        const uint16_t* p = block_src<L>(lds, xr, dr, lx, ld, lp, g, j);
-        bb[i][0] = *(const bf16x8*)p;
-        bb[i][1] = *(const bf16x8*)(p + (j < 18 ? 16 * RC_XP : 16 * RC_DP));  // the second fragment: 16 pixels on
-      }
-    }
-  };
-  load(0, b[0]);
-#pragma unroll
-  for (int gi = 0; gi < NG; ++gi) {
-    if (gi + 1 < NG) load(gi + 1, b[(gi + 1) & 1]);
-    __builtin_amdgcn_sched_barrier(0);  // the next group's reads go out before this group's MFMAs
-#pragma unroll
-    for (int i = 0; i < G; ++i) {
-      const int j = gi * G + i;
-      if (j < NB) {
-#if CLIMSR_CHAIN_DIAG == 1  // diagnostic build only: no MFMAs (the fragments are still read and consumed)
-        acc0[0] += (float)b[gi & 1][i][0][0] + (float)af[j][0];
-        acc1[0] += (float)b[gi & 1][i][1][0];
-#else
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], b[gi & 1][i][0], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], b[gi & 1][i][1], acc1, 0, 0, 0);
-#endif
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
-__device__ __forceinline__ int xslot(int y) { return (y + 4 * RC_XD) % RC_XD; }  // y >= -8
-__device__ __forceinline__ int dslot(int y) { return (y + 4 * RC_DD) & (RC_DD - 1); }
+__device__ __forceinline__ int xslot(int y) { return (y + 64) & (XD - 1); }  // y >= -64
+__device__ __forceinline__ int dslot(int y) { return (y + 64) & (DD - 1); }
 
 __device__ __forceinline__ uint32_t pack2_bf16(float a, float b) {
   const bf16x2 v = {(__bf16)a, (__bf16)b};  // v_cvt_pk_bf16_f32 (RNE)
   return __builtin_bit_cast(uint32_t, v);
 }
 
-// The whole strip walk of one wave: level L, column fragments 2h and 2h+1.  Every wave runs the same step loop
-// (base-row staging + one barrier per step); level L computes in steps 3(L-1) .. R+4+L.
-// MODE 0: forward (bias + leaky relu); 1: pull (leaky-relu derivative of the stored activation, no bias).
-// Address arithmetic is split into per-lane constants (computed once) and per-step wave-uniform row offsets.
-template <int MODE, int L>
-__device__ __forceinline__ void run_level(const ChainArgs& a, uint16_t* lds, int tid, int nimg, int r0) {
-  const int lane = tid & 63, g = lane >> 4, col = lane & 15, h = tid >> 8;
-  const int px0 = 32 * h + col;                  // this lane's image column in fragment 2h (fragment 2h+1: + 16)
-  const bool live0 = 32 * h < a.w, live1 = 32 * h + 16 < a.w;
-  const __amdgpu_buffer_rsrc_t br = buf_rsrc(a.base, a.base_bytes);
-  const __amdgpu_buffer_rsrc_t mr = buf_rsrc(a.mask, MODE == 1 ? a.mask_bytes : 0u);
-  const int R = a.rows, row0 = nimg * a.h;       // row0: this image's first row in the batch
-
-  // base row staging: chunk q = tid (+ 512) of a row is (slot q / 8 = image column + 1, 16 B channel group q % 8)
-  int xg[2], xl[2];  // byte offset within a base row in HBM (-1: zero chunk) / element offset within a ring row (-1: none)
+// The dense part of level L added to acc: B from the ring, A from registers (level 2: ar) or LDS (levels 3, 4).
+// Blocks go in groups of 3: the next group's fragments are read while this group is on the MFMA pipe.
+template <int L>
+__device__ __forceinline__ void dense_acc(const uint16_t* lds, const bf16x8 (&ar)[5], int y, int ld, int lp, int g, int lane,
+                                          f32x4& acc) {
+  constexpr int NB = nd_blocks(L), G = 3, NG = (NB + G - 1) / G;
+  int dr[3];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int q = tid + 512 * i, p = q >> 3, c = q & 7, ix = p - 1;
-    xl[i] = q < RC_XCH ? p * RC_XP + c * 8 : -1;
-    xg[i] = q < RC_XCH && ix >= 0 && ix < a.w ? (ix * a.bcs + a.boff + c * 8) * 2 : -1;
-  }
-  const uint32_t xrow_bytes = (uint32_t)(a.w * a.bcs * 2);
-  auto issue_row = [&](int y, uint4 (&v)[2]) {
-    const bool rok = y >= 0 && y < a.h;
-    const uint32_t rb = (uint32_t)(row0 + y) * xrow_bytes;
+  for (int k = 0; k < 3; ++k) dr[k] = OFF_D + dslot(y - 1 + k) * DROW;
+  const uint16_t* ab = lds + OFF_A + da_base(L) * 512 + lane * 8;
+  bf16x8 fa[2][G], fb[2][G];
+  auto load = [&](int gi, int s) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) v[i] = buf_load16(br, CLIMSR_CHAIN_DIAG != 3 && rok && xg[i] >= 0 ? rb + (uint32_t)xg[i] : BUF_OOB);
-  };
-  auto store_row = [&](int y, const uint4 (&v)[2]) {
-    uint16_t* row = lds + xslot(y) * RC_XROW;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      if (xl[i] >= 0) *(uint4*)(row + xl[i]) = v[i];
-  };
-  // pull: the activation x_j of this level's row in step s for both fragments (zeros outside), one step ahead
-  int ml[2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int px = px0 + 16 * k;
-    ml[k] = px < a.w ? (px * a.mcs + a.moff[L - 1] + 4 * g) * 2 : -1;
-  }
-  const uint32_t mrow_bytes = (uint32_t)(a.w * a.mcs * 2);
-  auto issue_mask = [&](int s, uint2 (&m)[2]) {
-    const int y = r0 - 3 + s - 2 * (L - 1);
-    const bool rok = y >= 0 && y < a.h;
-    const uint32_t rb = (uint32_t)(row0 + y) * mrow_bytes;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const auto v = __builtin_amdgcn_raw_buffer_load_b64(mr, rok && ml[k] >= 0 ? rb + (uint32_t)ml[k] : BUF_OOB, 0, 0);
-      m[k] = make_uint2(v[0], v[1]);
-    }
-  };
-  // Prologue: the first base rows are in flight while each wave loads its level's A fragments.
-  // Base rows are loaded one step before the step that stores them (two steps before their first use) and masks
-  // one step before their use; the loop is unrolled x2 with alternating register sets, so no register copy of a
-  // load still in flight (which would wait for it) is ever needed.
-  uint4 v0[2], v1[2], v2[2], ra[2], rb[2];
-  issue_row(r0 - 4, v0);
-  issue_row(r0 - 3, v1);
-  issue_row(r0 - 2, v2);
-  issue_row(r0 - 1, ra);
-  uint2 ma[2] = {}, mb[2] = {};
-  if constexpr (MODE == 1) issue_mask(0, ma);
-  const float4 bias = MODE == 0 ? *(const float4*)(a.bias[L - 1] + 4 * g) : make_float4(0.f, 0.f, 0.f, 0.f);
-  bf16x8 af[n_blocks(L)];
-  load_af_global<L>(a.wt[L - 1], lane, af);
-  // dense ring: the slots of image columns -1 and >= w are never written, they are the zero padding
-  for (int i = tid; i < RC_DD * (RC_COLS - a.w) * (RC_DP / 8); i += 512) {
-    const int c = i % (RC_DP / 8), k = (i / (RC_DP / 8)) % (RC_COLS - a.w), r = i / (RC_DP / 8) / (RC_COLS - a.w);
-    const int p = k == 0 ? 0 : a.w + k;
-    *(uint4*)(lds + RC_OFF_D + r * RC_DROW + p * RC_DP + c * 8) = make_uint4(0, 0, 0, 0);
-  }
-  store_row(r0 - 4, v0);
-  store_row(r0 - 3, v1);
-  store_row(r0 - 2, v2);
-  lds_barrier();
-  // retire the remaining loads here: with no VMEM result carried into the loop, hipcc's wait counting inside it
-  // stays exact (otherwise every step waits with a count that also drains the base-row prefetch)
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-
-  const int lx = px0 * RC_XP + 8 * g;  // + kx * RC_XP: input column px - 1 + kx sits in slot px + kx
-  const int ld = px0 * RC_DP + 8 * g;
-  const int lp = px0 * RC_DP + 8 * (g & 1);
-  const int dl = (px0 + 1) * RC_DP + 16 * (L - 1) + 4 * g;    // this lane's dense-ring store (fragment 2h)
-  const int ol = px0 * a.ocs + a.ooff[L - 1] + 4 * g;          // and HBM store, elements within an image row
-  const long orow = (long)a.w * a.ocs;
-  const float bb[4] = {bias.x, bias.y, bias.z, bias.w};
-  // step s: `cur` holds base row y1 + 2 (stored after the MFMAs), `nxt` receives row y1 + 3; `mcur` = this step's
-  // masks, `mnxt` receives the next step's
-  // output stores are raw buffer stores issued unconditionally every step (an out-of-range offset drops them): a store
-  // under the step's level-active / own-row branches made the compiler's vmcnt for the next base-row wait count it as
-  // maybe-not-issued, so that wait also drained this step's stores (measured: 7 of 31 us per forward launch)
-  const __amdgpu_buffer_rsrc_t orr = buf_rsrc(a.out, a.out_bytes);
-  auto step = [&](int s, uint4 (&cur)[2], uint4 (&nxt)[2], const uint2 (&mcur)[2], uint2 (&mnxt)[2]) {
-    const int y1 = r0 - 3 + s;
-    issue_row(y1 + 3, nxt);
-    if constexpr (MODE == 1) issue_mask(s + 1, mnxt);
-    const bool active = live0 && s >= 3 * (L - 1) && s <= R + 4 + L;
-    const int y = y1 - 2 * (L - 1);
-    const bool own = active && y >= 0 && y < a.h && y >= r0 && y < r0 + R;
-    uint2 pko[2] = {make_uint2(0, 0), make_uint2(0, 0)};
-    if (active) {
-      int xr[3], dr[3];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        xr[k] = xslot(y - 1 + k) * RC_XROW;
-        dr[k] = dslot(y - 1 + k) * RC_DROW;
-      }
-      f32x4 acc[2];
-      level_acc<L>(lds, af, xr, dr, lx, ld, lp, g, acc[0], acc[1]);
-      const bool in = y >= 0 && y < a.h;  // rows outside the image: zeros, the next level's padding
-      uint16_t* drow = lds + RC_OFF_D + dslot(y) * RC_DROW + dl;
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        float v[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float t = acc[k][i] + bb[i];
-          if (MODE == 0) {
-            v[i] = fmaxf(t, t * a.slope);  // leaky relu, 0 <= slope <= 1 (checked on the host)
-          } else {
-            const uint32_t mw = i < 2 ? mcur[k].x : mcur[k].y;
-            const float m = __uint_as_float((i & 1) ? (mw & 0xFFFF0000u) : (mw << 16));  // the stored activation
-            v[i] = m > 0.f ? t : t * a.slope;
-          }
-        }
-        uint2 pk = make_uint2(pack2_bf16(v[0], v[1]), pack2_bf16(v[2], v[3]));
-        if (!in) pk = make_uint2(0, 0);
-        if (L < 4 && (k == 0 || live1)) *(uint2*)(drow + 16 * k * RC_DP) = pk;
-        pko[k] = pk;
+    for (int i = 0; i < G; ++i) {
+      const int j = gi * G + i;
+      if (j < NB) {
+        fa[s][i] = L == 2 ? ar[j < 5 ? j : 0] : *(const bf16x8*)(ab + j * 512);
+        fb[s][i] = *(const bf16x8*)(lds + dense_off<L>(dr, ld, lp, g, j));
       }
     }
-#if CLIMSR_CHAIN_DIAG != 2  // diagnostic build 2: no output stores
-    const uint32_t ob = (uint32_t)((row0 + y) * orow + ol) * 2u;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const bool ok = own && (k == 0 || live1);
-      __builtin_amdgcn_raw_buffer_store_b64((v2u32){pko[k].x, pko[k].y}, orr, ok ? ob + (uint32_t)(16 * k * a.ocs * 2) : BUF_OOB, 0, 0);
-    }
-#endif
-    store_row(y1 + 2, cur);  // its slot held row y1 - 8, which no level reads in this step
-    lds_barrier();
   };
-  for (int s = 0; s < R + 9; s += 2) {
-    step(s, ra, rb, ma, mb);
-    if (s + 1 < R + 9) step(s + 1, rb, ra, mb, ma);
+  load(0, 0);
+#pragma unroll
+  for (int gi = 0; gi < NG; ++gi) {
+    if (gi + 1 < NG) load(gi + 1, (gi + 1) & 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < G; ++i)
+      if (gi * G + i < NB) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[gi & 1][i], fb[gi & 1][i], acc, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
-// Waves w and w + 4 share a SIMD (a workgroup's waves go round the 4 SIMDs in a fixed cyclic order).  Wave w < 4
-// computes level w + 1, wave w >= 4 level 8 - w, so each SIMD pairs a light and a heavy level (1+4, 2+3: 50 of the
-// 100 MFMA blocks per row each) instead of carrying one level: the per-step critical path is the slowest SIMD.
-// Wave w covers column fragments 2 (w >> 2) and 2 (w >> 2) + 1.
+// Base part of one row for levels 1..M (pn[L-1] += conv_L restricted to the 64 base channels): 18 blocks (tap t = j / 2,
+// 32-channel half j % 2), in groups of 3 whose B fragments are read under the previous group's MFMAs; every fragment
+// feeds M MFMAs.  The A fragments of levels 1..3 and blocks 0..5 of level 4 come from AGPRs (mfma3_agpr), level 4's
+// blocks 6..17 from VGPRs (mfma3_vgpr; the 256 AGPRs hold 60 of the 72).  Every MFMA of the loop is in asm: hipcc must
+// never see an MFMA that could make it move an accumulator between the register halves mid-chain.
+template <int M>
+__device__ __forceinline__ void base_part(const uint16_t* lds, const bf16x8 (&afb)[4][18], const int (&xr)[3], int lx, f32x4 (&pn)[4]) {
+  constexpr int G = 3, NG = 18 / G;
+  bf16x8 b[2][G];
+  auto load = [&](int gi, int st) {
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const int j = gi * G + i, t = j >> 1, ky = t / 3, kx = t % 3;
+      b[st][i] = *(const bf16x8*)(lds + xr[ky] + lx + kx * XP + (j & 1) * 32);
+    }
+  };
+  load(0, 0);
+#pragma unroll
+  for (int gi = 0; gi < NG; ++gi) {
+    if (gi + 1 < NG) load(gi + 1, (gi + 1) & 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int L = 0; L < M; ++L) {
+      if (gi == 0) {
+        mfma3_agpr<true>(pn[L], afb[L][0], afb[L][1], afb[L][2], b[0][0], b[0][1], b[0][2]);
+      } else if (L < 3 || gi < 2) {
+        mfma3_agpr<false>(pn[L], afb[L][gi * G], afb[L][gi * G + 1], afb[L][gi * G + 2], b[gi & 1][0], b[gi & 1][1], b[gi & 1][2]);
+      } else {
+        mfma3_vgpr(pn[L], afb[L][gi * G], afb[L][gi * G + 1], afb[L][gi * G + 2], b[gi & 1][0], b[gi & 1][1], b[gi & 1][2]);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// MODE 0: forward (bias + leaky relu); 1: pull (leaky-relu derivative of the stored activation, no bias).
 template <int MODE>
-__global__ __launch_bounds__(512, 1) void rdb_chain_kernel(ChainArgs a) {
+__global__ __launch_bounds__(256, 1) void rdb_chain_kernel(ChainArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint16_t* lds = (uint16_t*)smem;
-  const int tid = threadIdx.x;
-  const int nimg = blockIdx.x / a.strips_y, r0 = (blockIdx.x % a.strips_y) * a.rows;
-  const int w = tid >> 6;
-  switch (w < 4 ? w : 7 - w) {
-    case 0: run_level<MODE, 1>(a, lds, tid, nimg, r0); break;
-    case 1: run_level<MODE, 2>(a, lds, tid, nimg, r0); break;
-    case 2: run_level<MODE, 3>(a, lds, tid, nimg, r0); break;
-    default: run_level<MODE, 4>(a, lds, tid, nimg, r0); break;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, col = lane & 15;
+  const int f = __builtin_amdgcn_readfirstlane(tid >> 6);  // this wave's column fragment
+  int bi = blockIdx.x;
+  const int sx = bi % a.strips_x;
+  bi /= a.strips_x;
+  const int sy = bi % a.strips_y, nimg = bi / a.strips_y;
+  const int r0 = sy * a.rows, R = min(a.rows, a.h - r0);
+  const int c0 = sx * a.own_w, x0 = c0 - a.x_halo;  // window column 0 = image column x0
+  const int row0 = nimg * a.h;                       // this image's first row in the batch
+  const __amdgpu_buffer_rsrc_t br = buf_rsrc(a.base, a.base_bytes);
+
+  // ---- dense-part A fragments of levels 3, 4 into LDS, lane-linear per block; the dense ring zeroed (its edge slots
+  // and the columns of fragments outside the image are the zero padding of the level convs)
+  for (int i = tid; i < NDA * 64; i += 256) {
+    const int blk = i >> 6, l = i & 63, gg = l >> 4, cc = l & 15;
+    const int L = blk < 9 ? 3 : 4, j = blk - (L == 3 ? 0 : 9);
+    const int KP = kp_blocks(L) * 32;
+    const uint16_t* wp = L == 3 ? a.wt[2] : a.wt[3];
+    int tap, ch;
+    dense_src(L, j, gg, tap, ch);
+    *(bf16x8*)(lds + OFF_A + i * 8) = tap >= 0 ? *(const bf16x8*)(wp + cc * 9 * KP + tap * KP + 64 + ch) : (bf16x8){};
+  }
+  for (int i = tid; i < DD * DROW / 8; i += 256) *(uint4*)(lds + OFF_D + i * 8) = make_uint4(0, 0, 0, 0);
+
+  // ---- base row staging: chunk q = tid + 256 i of a row is (slot q / 8 = window column + 1, 16 B channel group q % 8)
+  int xg[XIT], xl[XIT];
+#pragma unroll
+  for (int i = 0; i < XIT; ++i) {
+    const int q = tid + 256 * i, p = q >> 3, c = q & 7, ix = x0 + p - 1;
+    xl[i] = q < XCH ? p * XP + c * 8 : -1;
+    xg[i] = q < XCH && ix >= 0 && ix < a.w ? (ix * a.bcs + a.boff + c * 8) * 2 : -1;
+  }
+  const uint32_t xrow_bytes = (uint32_t)(a.w * a.bcs * 2);
+  auto issue_row = [&](int y, uint4 (&v)[XIT]) {
+    const bool rok = y >= 0 && y < a.h;
+    const uint32_t rb = (uint32_t)(row0 + y) * xrow_bytes;
+#pragma unroll
+    for (int i = 0; i < XIT; ++i) v[i] = buf_load16(br, rok && xg[i] >= 0 ? rb + (uint32_t)xg[i] : BUF_OOB);
+  };
+  auto store_row = [&](int y, const uint4 (&v)[XIT]) {
+    uint16_t* row = lds + xslot(y) * XROW;
+#pragma unroll
+    for (int i = 0; i < XIT; ++i)
+      if (xl[i] >= 0) *(uint4*)(row + xl[i]) = v[i];
+  };
+  {
+    uint4 v0[XIT], v1[XIT], v2[XIT];
+    issue_row(r0 - 4, v0);
+    issue_row(r0 - 3, v1);
+    issue_row(r0 - 2, v2);
+    store_row(r0 - 4, v0);
+    store_row(r0 - 3, v1);
+    store_row(r0 - 2, v2);
+  }
+
+  // ---- base-part A fragments of the four levels, kept in registers for the whole launch
+  bf16x8 afb[4][18];
+#pragma unroll
+  for (int L = 0; L < 4; ++L) {
+    const int KP = kp_blocks(L + 1) * 32;
+    const uint16_t* wr = a.wt[L] + col * 9 * KP;
+#pragma unroll
+    for (int j = 0; j < 18; ++j) afb[L][j] = *(const bf16x8*)(wr + (j >> 1) * KP + (j & 1) * 32 + g * 8);
+  }
+  bf16x8 ad2[5];  // level 2's dense A fragments
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    int tap, ch;
+    dense_src(2, j, g, tap, ch);
+    ad2[j] = tap >= 0 ? *(const bf16x8*)(a.wt[1] + col * 9 * 96 + tap * 96 + 64 + ch) : (bf16x8){};
+  }
+  float bias[4][4];
+#pragma unroll
+  for (int L = 0; L < 4; ++L) {
+    const float4 b4 = MODE == 0 ? *(const float4*)(a.bias[L] + 4 * g) : make_float4(0.f, 0.f, 0.f, 0.f);
+    bias[L][0] = b4.x; bias[L][1] = b4.y; bias[L][2] = b4.z; bias[L][3] = b4.w;
+  }
+  lds_barrier();
+
+  // this lane's pixel: window column px = 16 f + col = image column x
+  const int px = 16 * f + col, x = x0 + px;
+  const bool fact = x0 + 16 * f < a.w && x0 + 16 * f + 16 > 0;  // wave-uniform: the fragment touches the image
+  const bool xin = x >= 0 && x < a.w, xown = xin && x >= c0 && x < c0 + a.own_w;
+  const int lx = px * XP + 8 * g;                      // + kx * XP: window column px - 1 + kx sits in slot px + kx
+  const int ld = px * DP + 8 * g, lp = px * DP + 8 * (g & 1);
+  const int dl = (px + 1) * DP + 4 * g;                // dense-ring store (+ 16 (L-1))
+  const __amdgpu_buffer_rsrc_t orr = buf_rsrc(a.out, a.out_bytes);
+  const __amdgpu_buffer_rsrc_t mr = buf_rsrc(a.mask, MODE == 1 ? a.mask_bytes : 0u);
+
+  // partial sums (base part) of rows still to finish: level 2 in registers (P2e / P2o: the row of the last even / odd
+  // step), levels 3 / 4 in this wave's LDS slots (row of step s in slot s % 4 / s % 6)
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  f32x4 P2e = z4, P2o = z4;
+  f32x4* ps = (f32x4*)(smem + OFF_P * 2 + f * (NPS * 1024)) + lane;  // slot k: ps[64 k]
+
+  // level L's epilogue for row y: leaky relu (forward, + bias) or its derivative from the stored activation (pull);
+  // zeros outside the image (the next level's padding); the dense-ring store (levels 1..3) and the HBM store of the
+  // strip's own pixels, a raw buffer store issued unconditionally (an out-of-range offset drops it)
+  auto finish = [&](int L, int y, bool act, const f32x4& acc, uint2 m) {
+    const bool in = act && xin && y >= 0 && y < a.h;
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float t = acc[i] + bias[L - 1][i];
+      if (MODE == 0) {
+        v[i] = fmaxf(t, t * a.slope);  // leaky relu, 0 <= slope <= 1 (checked on the host)
+      } else {
+        const uint32_t mw = i < 2 ? m.x : m.y;
+        const float mv = __uint_as_float((i & 1) ? (mw & 0xFFFF0000u) : (mw << 16));  // the stored activation
+        v[i] = mv > 0.f ? t : t * a.slope;
+      }
+    }
+    uint2 pk = make_uint2(pack2_bf16(v[0], v[1]), pack2_bf16(v[2], v[3]));
+    if (!in) pk = make_uint2(0, 0);
+    if (L < 4 && act && fact) *(uint2*)(lds + OFF_D + dslot(y) * DROW + dl + 16 * (L - 1)) = pk;
+    const bool own = in && xown && y >= r0 && y < r0 + R;
+    const uint32_t ob = (uint32_t)(((long)(row0 + y) * a.w + x) * a.ocs + a.ooff[L - 1] + 4 * g) * 2u;
+    __builtin_amdgcn_raw_buffer_store_b64((v2u32){pk.x, pk.y}, orr, own ? ob : BUF_OOB, 0, 0);
+  };
+
+  auto step = [&](int s, f32x4& P2) {
+    const int y1 = r0 - 3 + s;
+    uint4 nxt[XIT];
+    issue_row(y1 + 2, nxt);  // stored at the end of this step
+    // pull: the stored activations of the four levels' rows in this step
+    uint2 mk[4] = {};
+    if constexpr (MODE == 1) {
+#pragma unroll
+      for (int L = 1; L <= 4; ++L) {
+        const int y = y1 - 2 * (L - 1);
+        const bool ok = xin && y >= 0 && y < a.h;
+        const uint32_t mo = (uint32_t)(((long)(row0 + y) * a.w + x) * a.mcs + a.moff[L - 1] + 4 * g) * 2u;
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(mr, ok ? mo : BUF_OOB, 0, 0);
+        mk[L - 1] = make_uint2(v[0], v[1]);
+      }
+    }
+    // levels whose base part is computed in this step: level L's rows are computed 2(L-1) steps before it finishes
+    // them, for s in [L-1, R + 6 - L] -- always the prefix 1..m of the levels (none for rows outside the image)
+    const bool yin = fact && y1 >= 0 && y1 < a.h;
+    const int m = yin ? min(4, min(s + 1, R + 6 - s)) : 0;
+    // ---- base part of row y1 for levels 1..m: 18 blocks (9 taps x 2 x 32 channels), each B fragment feeding the
+    // MFMAs of every such level; one branch-free copy of the loop per m
+    f32x4 pn[4];
+    if (m > 0) {
+      int xr[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) xr[k] = xslot(y1 - 1 + k) * XROW;
+      switch (m) {
+        case 4: base_part<4>(lds, afb, xr, lx, pn); break;
+        case 3: base_part<3>(lds, afb, xr, lx, pn); break;
+        case 2: base_part<2>(lds, afb, xr, lx, pn); break;
+        default: base_part<1>(lds, afb, xr, lx, pn); break;
+      }
+      pad_mfma(pn);
+    }
+    // levels past m: zero partials
+#pragma unroll
+    for (int L = 0; L < 4; ++L)
+      if (L >= m) pn[L] = z4;
+    // ---- level 1 (row y1): base part only
+    finish(1, y1, s <= R + 5, pn[0], mk[0]);
+    // ---- level 2 (row y1 - 2), 3 (y1 - 4), 4 (y1 - 6): + the dense part from the ring (rows of earlier steps)
+    const bool a2 = s >= 3 && s <= R + 6, a3 = s >= 6 && s <= R + 7, a4 = s >= 9 && s <= R + 8;
+    f32x4* p3 = ps + 64 * (s & 3);        // level 3: the row of step s - 4 (read), then this step's row (written)
+    f32x4* p4 = ps + 64 * (4 + s % 6);    // level 4: the row of step s - 6, then this step's
+    {
+      f32x4 acc = P2;  // the row of step s - 2 (same parity)
+      if (a2 && fact) dense_acc<2>(lds, ad2, y1 - 2, ld, lp, g, lane, acc);
+      finish(2, y1 - 2, a2, acc, mk[1]);
+    }
+    {
+      f32x4 acc = a3 ? *p3 : z4;
+      if (a3 && fact) dense_acc<3>(lds, ad2, y1 - 4, ld, lp, g, lane, acc);
+      finish(3, y1 - 4, a3, acc, mk[2]);
+    }
+    {
+      f32x4 acc = a4 ? *p4 : z4;
+      if (a4 && fact) dense_acc<4>(lds, ad2, y1 - 6, ld, lp, g, lane, acc);
+      finish(4, y1 - 6, a4, acc, mk[3]);
+    }
+    P2 = pn[1];
+    *p3 = pn[2];  // (this wave's own slots: no barrier between its read and its write)
+    *p4 = pn[3];
+    store_row(y1 + 2, nxt);  // its slot held row y1 - 2, which no level reads in this step
+    lds_barrier();
+  };
+  for (int s = 0; s < R + 9; s += 2) {
+    step(s, P2e);
+    if (s + 1 < R + 9) step(s + 1, P2o);
   }
 }
 
 }  // namespace
 
 extern "C" int climsr_rdb_chain(const ClimsrChainDesc* d, void* stream) {
-  if (!d || !d->base || !d->out || d->n <= 0 || d->h <= 0 || d->w <= 0 || d->w > RC_W || d->w % 16 || d->bcs % 8 ||
-      d->boff % 8 || d->ocs % 4 || (d->act != 1 && d->act != 3) || (d->act == 3 && (!d->mask || d->mcs % 4)) ||
-      !(d->slope >= 0.f && d->slope <= 1.f)) {
-    set_error("rdb_chain: bad args (width must be 16, 32, 48 or 64)");
+  if (!d || !d->base || !d->out || d->n <= 0 || d->h <= 0 || d->w <= 0 || d->bcs % 8 || d->boff % 8 || d->ocs % 4 ||
+      (d->act != 1 && d->act != 3) || (d->act == 3 && (!d->mask || d->mcs % 4)) || !(d->slope >= 0.f && d->slope <= 1.f)) {
+    set_error("rdb_chain: bad args");
     return CLIMSR_EINVAL;
   }
   for (int L = 0; L < 4; ++L) {
@@ -371,35 +403,32 @@ extern "C" int climsr_rdb_chain(const ClimsrChainDesc* d, void* stream) {
   a.base_bytes = (uint32_t)(px * d->bcs * 2);
   a.out_bytes = (uint32_t)(px * d->ocs * 2);
   a.mask_bytes = d->act == 3 ? (uint32_t)(px * d->mcs * 2) : 0u;
-  // strip height: enough strips to give every CU one (a strip recomputes 3 + 2 + 1 halo rows per level chain)
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (ncu <= 0) ncu = 256;
+  // columns: one window when the image fits it, else strips of WIN - 2 HALO_X own columns
+  if (d->w <= WIN) {
+    a.strips_x = 1; a.own_w = d->w; a.x_halo = 0;
+  } else {
+    a.own_w = WIN - 2 * HALO_X; a.x_halo = HALO_X; a.strips_x = ceil_div(d->w, a.own_w);
   }
-  int rows = ceil_div((long)d->n * d->h, ncu);
+  // rows: about one strip per CU (a strip recomputes 3 + 2 + 1 halo rows per level chain)
+  const int ncu = device_cus();
+  const long bands = (long)d->n * a.strips_x;
+  int rows = ceil_div(bands * d->h, ncu);
   if (rows < 2) rows = 2;
-  if (rows > 32) rows = 32;
+  if (rows > 64) rows = 64;
   if (rows > d->h) rows = d->h;
   a.rows = rows;
   a.strips_y = ceil_div(d->h, rows);
-  const bool fwd = d->act == 1;
-  if (fwd) {
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void*)rdb_chain_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, RC_LDS);
-      attr = true;
-    }
-    hipLaunchKernelGGL(rdb_chain_kernel<0>, dim3(a.strips_y * a.n), dim3(512), RC_LDS, (hipStream_t)stream, a);
+  const long grid = bands * a.strips_y;
+  if (grid >= (1L << 31)) {
+    set_error("rdb_chain: grid too large");
+    return CLIMSR_EINVAL;
+  }
+  if (d->act == 1) {
+    if (int e = lds_opt_in((const void*)rdb_chain_kernel<0>, LDS_BYTES)) return e;
+    hipLaunchKernelGGL(rdb_chain_kernel<0>, dim3((unsigned)grid), dim3(256), LDS_BYTES, (hipStream_t)stream, a);
   } else {
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void*)rdb_chain_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, RC_LDS);
-      attr = true;
-    }
-    hipLaunchKernelGGL(rdb_chain_kernel<1>, dim3(a.strips_y * a.n), dim3(512), RC_LDS, (hipStream_t)stream, a);
+    if (int e = lds_opt_in((const void*)rdb_chain_kernel<1>, LDS_BYTES)) return e;
+    hipLaunchKernelGGL(rdb_chain_kernel<1>, dim3((unsigned)grid), dim3(256), LDS_BYTES, (hipStream_t)stream, a);
   }
   return check_launch("rdb_chain");
 }

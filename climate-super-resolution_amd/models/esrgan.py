@@ -113,8 +113,8 @@ class _Engine:
             # RDB convs need no transposed weights: their data gradients run as pull convs (below)
             p.bind(conv.weight, conv.bias, need_t=(name != "conv_first" and ".RDB" not in name))
         dev = gen.conv_first.weight.device
-        # conv1..conv4 of every RDB (and their pull gradients) as one fused row-streaming launch each (nf 64, gc 16,
-        # image width 16/32/48/64: csrc/rdb_chain.hip); other widths run the four convs one by one (conv_n16)
+        # conv1..conv4 of every RDB (and their pull gradients) as one fused row-streaming launch each (nf 64, gc 16:
+        # csrc/rdb_chain.hip); other configurations run the four convs one by one (conv_n16)
         self.chains: List[RdbChain] = []
         if nf == 64 and gc == 16:
             for i in range(3 * self.nb):
@@ -173,10 +173,10 @@ class _Engine:
         self.version = self.gen._flat._version
 
     def chain_ok(self, w: int, n: int = 1, h: int = 1) -> bool:
-        """The fused conv1-4 launch takes widths 16/32/48/64 and buffers under 2 GiB (its 32-bit buffer offsets:
+        """The fused conv1-4 launch takes any image size whose buffers stay under 2 GiB (its 32-bit buffer offsets:
         climsr_rdb_chain rejects larger ones; the pull reads the dense buffer as its activation mask, same size);
         anything else runs conv by conv."""
-        return bool(self.chains) and w % 16 == 0 and w <= 64 and n * h * w * self.dc * 2 < (1 << 31)
+        return bool(self.chains) and n * h * w * self.dc * 2 < (1 << 31)
 
     def rdb_name(self, i, r, c):
         return f"RRDB_trunk.{i}.RDB{r}.conv{c}"

@@ -401,3 +401,81 @@ def test_gloo_world2_gan_discriminator_pass():
     assert res[0][1] == [0, 2] and res[1][1] == [1, 3]
     assert not torch.allclose(res[0][5], res[1][5])  # each rank's running statistics follow its own shard
     assert res[0][2] != res[1][2]  # and so do the per-rank losses
+
+
+# ------------------------------------------------------------------ world-2 GAN generator pass
+def _gan_g_worker(rank, world, port, q):
+    """The G pass of one GAN step (pl_gan.py:28-49 loss_g, then AdamW_G) as Lightning DDP runs it: each rank takes its
+    shard, D (frozen, train mode) is called separately on hr and sr with the shard's BatchNorm statistics (no SyncBN,
+    conf/trainer/default.yaml:31), the relativistic means are over the shard, and G's gradient flows through D(sr) and
+    the pixel loss (the perceptual loss carries none, F7).  The per-rank G gradients (fp64 oracle arithmetic; the HIP
+    kernels need a GPU) go into the real ESRGANGenerator flat gradient buffer and are averaged by the product's
+    overlapped reducer at the slice the generator's backward reports (after RRDB block 1 of 2), then at finish."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from climsr_amd.core.ddp import OverlappedGradAllReducer, shard_indices
+        from climsr_amd.models.esrgan import ESRGANGenerator
+        from oracle import climsr_ref as ref
+        from tests.helpers import gen_params, rfb_d_params, vgg_params
+
+        torch.set_num_threads(2)
+        nb, batch, hr = 2, 4, 32
+        g0 = gen_params(nb, torch.float64)
+        d0 = rfb_d_params(torch.float64)
+        vp = vgg_params(torch.float64)
+        keys = ref.trainable_keys(g0)
+        data = ref.synthetic_batch(batch, hr, seed=5, dtype=torch.float64)
+
+        def g_pass(idx):
+            p = {k: v.clone().requires_grad_(True) for k, v in g0.items()}
+            dp = {k: v.clone() for k, v in d0.items()}  # D frozen in the G pass (Lightning toggles requires_grad)
+            sr = ref.generator_forward(p, data["lr"][idx], data["elevation"][idx], data["mask"][idx], nb)
+            _perc, _adv, _pix, total = ref.loss_g(lambda t: ref.rfb_discriminator_forward(dp, t, training=True), vp,
+                                                  data["hr"][idx], sr)
+            return float(total), ref._grads(total, p, keys)
+
+        shard = shard_indices(batch, rank, world)
+        loss, local = g_pass(shard)
+        g = ESRGANGenerator(in_channels=3, out_channels=1, nf=64, nb=nb, gc=16, scale_factor=4)
+        g.grads_as_views()
+        for k, prm in g.named_parameters():
+            prm.grad.copy_(local[k])
+        ov = OverlappedGradAllReducer(g)
+        g.set_grad_ready_hook(ov.ready)
+        for b in g._grad_ready_blocks:  # the slices the native backward reports, in its order
+            ov.ready(g._block_flat_lo(b))
+        ov.finish()
+        avg = {k: prm.grad.double().clone() for k, prm in g.named_parameters()}
+        shards = [shard_indices(batch, r, world) for r in range(world)]
+        per = [g_pass(s) for s in shards]
+        want = {k: sum(pp[1][k] for pp in per) / world for k in keys}
+        whole = g_pass(list(range(batch)))[1]
+
+        def rel(a, b):
+            num = sum(float((a[k] - b[k]).norm() ** 2) for k in keys) ** 0.5
+            return num / (sum(float(b[k].norm() ** 2) for k in keys) ** 0.5)
+
+        q.put((rank, shard, loss, rel(avg, want), rel(want, whole), list(ov.launched)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_gan_generator_pass():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gan_g_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=600) for _ in procs), key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, shard, loss, rel_avg, rel_whole, launched in res:
+        assert rel_avg < 1e-6, (rank, rel_avg)  # product reducer + G flat layout: the average of the per-shard gradients
+        # per-rank relativistic means and BN statistics in loss_g: not the gradient of the whole batch
+        assert rel_whole > 1e-4, (rank, rel_whole)
+        assert len(launched) == 2 and launched[-1][0] == 0 and launched[0][0] == launched[1][1]
+    assert res[0][1] == [0, 2] and res[1][1] == [1, 3]
+    assert res[0][2] != res[1][2]  # per-rank losses

@@ -8,7 +8,6 @@ over the same bf16-rounded operands: the only difference left is the kernels' fp
 ``REL`` of the result scale.  The last tests run one whole config-2 step (nb 11, B=32, 64->256) and the config-3
 GAN passes (nb 1, B=32, 64->256) against the oracle (oracle/climsr_ref.py) evaluated in fp32 with torch ops on the
 GPU, within the same envelope as the reference's own AMP training (test_gpu_generator.py)."""
-import os
 import pytest
 import torch
 import torch.nn.functional as F
@@ -173,7 +172,8 @@ def test_wgrad64_stride2_discriminator_layers(cin, cout, h):
 
 @pytest.mark.parametrize("act", [0, 1])
 def test_conv_pw_forward_at_256_b32(act):
-    """HRconv forward at 256^2, B=32 (conv_pw persistent XCD tile walk over 8192 tiles), bias (+ LeakyReLU)."""
+    """HRconv forward at 256^2, B=32 (conv_wr: weights in registers, 32768 wave tiles walked by a persistent
+    XCD-ordered grid), bias (+ LeakyReLU)."""
     from climsr_amd import ops
 
     n, h = 32, 256
@@ -188,9 +188,7 @@ def test_conv_pw_forward_at_256_b32(act):
     finally:
         ops.PROFILER = None
     torch.cuda.synchronize()
-    # CLIMSR_CONV_DMA_PW=1 routes this one-chunk HR shape to the LDS-DMA conv instead
-    kern = "conv_fwd_dma_kernel" if os.environ.get("CLIMSR_CONV_DMA_PW", "0") == "1" else "conv_pw_kernel"
-    assert any(s.startswith(kern) for s in names), names
+    assert any(s.startswith("conv_wr_kernel") for s in names), names
     for i in range(0, n, 8):  # float64 reference, 8 images at a time
         want = F.conv2d(x[i:i + 8].double(), bf(p.weight).double(), p.bias.double(), padding=1)
         if act == 1:

@@ -1,0 +1,43 @@
+"""Build-time check of the kernels that issue MFMAs from inline asm (csrc/mfma_agpr.h): hipcc inserts no wait states
+around them, so the compiled gfx950 ISA is linted (tests/isa_mfma_lint.py) for any instruction that touches an asm
+MFMA's destination registers before the kernel's hazard pad, on every control-flow path.  Compiles for gfx950 on the
+CPU (no GPU needed)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+from tests.isa_mfma_lint import lint
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "climate-super-resolution_amd", "csrc")
+HIPCC = "/opt/rocm/bin/hipcc"
+
+
+def _kernels(asm_text):
+    lines = asm_text.split("\n")
+    out = {}
+    for i, l in enumerate(lines):
+        m = re.match(r"^(_Z\w*kernel\w*):", l)
+        if m:
+            end = next((j for j in range(i + 1, len(lines)) if lines[j].startswith(".Lfunc_end")), len(lines))
+            out[m.group(1)] = lines[i:end + 1]
+    return out
+
+
+@pytest.mark.parametrize("src", ["rdb_chain.hip", "conv_wr.hip"])
+def test_asm_mfma_results_are_padded(src, tmp_path):
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not available")
+    if not os.path.exists(os.path.join(CSRC, src)):
+        pytest.skip(f"{src} not in this build")
+    subprocess.run([HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", f"-I{ROOT}/include", "--save-temps", "-c",
+                    os.path.join(CSRC, src), "-o", str(tmp_path / "k.o")], cwd=tmp_path, check=True, capture_output=True)
+    asm = [f for f in os.listdir(tmp_path) if f.endswith("gfx950.s")]
+    assert asm, os.listdir(tmp_path)
+    kern = _kernels(open(tmp_path / asm[0]).read())
+    assert kern, "no kernels found in the ISA"
+    bad = {name: lint(lines)[:5] for name, lines in kern.items()}
+    bad = {k: v for k, v in bad.items() if v}
+    assert not bad, bad

@@ -147,3 +147,17 @@ def test_adamw_rejects_options_it_does_not_implement():
     opt = HydraInstantiator().optimizer(g, dict(ADAMW_YAML, maximize=True))
     assert type(opt) is torch.optim.AdamW and opt.param_groups[0]["maximize"] is True
     assert isinstance(HydraInstantiator().optimizer(g, dict(ADAMW_YAML)), AdamW)
+    # amsgrad too, also when _target_ names the fused class itself
+    for target in ("torch.optim.AdamW", "climsr_amd.core.optim.AdamW"):
+        opt = HydraInstantiator().optimizer(g, dict(ADAMW_YAML, _target_=target, amsgrad=True))
+        assert type(opt) is torch.optim.AdamW and opt.param_groups[0]["amsgrad"] is True
+
+
+def test_autograd_grad_route_refuses_a_flat_reducer_hook():
+    from climsr_amd.models.esrgan import ESRGANGenerator
+
+    g = ESRGANGenerator(in_channels=3, out_channels=1, nf=64, nb=2, gc=16)
+    g._begin_autograd_grads()  # no hook: fine
+    g.set_grad_ready_hook(lambda lo: None)
+    with pytest.raises(RuntimeError, match="grad-ready hook"):
+        g._begin_autograd_grads()

@@ -1,0 +1,56 @@
+"""Summarise two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) into per-launch HBM bytes per kernel.
+
+    python tools/pmc_traffic.py <fetch_dir> <write_dir> <out_prefix> "<title>"
+
+Each dir holds the `--output-format csv` output of one pass, e.g.
+    rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/f -o run -- python3 bench.py --steps 2 --warmup 1 ...
+Per /opt/skills/guides/MI355X_MICROARCH.md: the counters are in KB (x1024) and gfx950's FETCH_SIZE reports half of
+a wide streaming read (x2).  Writes <out_prefix>.json (read by bench.py for `roofline.traffic`) and <out_prefix>.md.
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def load(d, counter):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {d}")
+    tot = collections.defaultdict(float)
+    disp = collections.defaultdict(set)
+    for f in files:
+        for row in csv.DictReader(open(f)):
+            if row.get("Counter_Name") != counter:
+                continue
+            name = row["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+            tot[name] += float(row["Counter_Value"])
+            disp[name].add(row.get("Dispatch_Id", len(disp[name])))
+    return {k: (tot[k], len(disp[k])) for k in tot}
+
+
+def main():
+    fdir, wdir, out, title = sys.argv[1:5]
+    fetch, write = load(fdir, "FETCH_SIZE"), load(wdir, "WRITE_SIZE")
+    rows = {}
+    for k, (ft, n) in fetch.items():
+        wt, nw = write.get(k, (0.0, 1))
+        fb = ft / n * 1024 * 2
+        wb = wt / max(nw, 1) * 1024
+        rows[k] = {"launches": n, "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb, "hbm_bytes_per_launch": fb + wb}
+    rows = dict(sorted(rows.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"] * kv[1]["launches"]))
+    src = (f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes): {title}; values per launch, averaged over all "
+           "launches of the kernel in the run; FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 reports half of a wide "
+           "streaming read); KB->bytes x1024")
+    json.dump({"source": src, "kernels": rows}, open(out + ".json", "w"), indent=1)
+    with open(out + ".md", "w") as f:
+        f.write(f"# {title}\n\n| kernel | launches | fetch MB/launch (x2 corrected) | write MB/launch |\n|---|---|---|---|\n")
+        for k, v in list(rows.items())[:25]:
+            f.write(f"| {k} | {v['launches']} | {v['fetch_bytes_per_launch'] / 1e6:.1f} | {v['write_bytes_per_launch'] / 1e6:.1f} |\n")
+    print(open(out + ".md").read())
+
+
+if __name__ == "__main__":
+    main()
