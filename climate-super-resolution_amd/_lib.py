@@ -32,7 +32,8 @@ class Epilogue(ctypes.Structure):
                 ("down2", ctypes.c_int32), ("res_f32", ctypes.c_int32), ("beta1", c_float), ("beta2", c_float),
                 ("aux_cstride", ctypes.c_int32), ("aux", c_void_p), ("aux_coff", ctypes.c_int32), ("aux_scale", c_float),
                 ("bn_part", c_void_p), ("bn_z", c_void_p), ("bn_z_cstride", ctypes.c_int32), ("bn_slope", c_float),
-                ("bn_mean", c_void_p), ("bn_rstd", c_void_p), ("bn_gamma", c_void_p), ("bn_beta", c_void_p)]
+                ("bn_mean", c_void_p), ("bn_rstd", c_void_p), ("bn_gamma", c_void_p), ("bn_beta", c_void_p),
+                ("ch_part", c_void_p)]
 
     def __init__(self, *args, **kw):
         # plain residual adds unless a caller scales them (beta1 / beta2 are positional fields 13 / 14)
@@ -69,6 +70,12 @@ class PullPackDesc(ctypes.Structure):
         (n, ctypes.c_int32) for n in ("nseg", "out_c", "in_c", "ks", "cc", "ci_off")]
 
 
+class SrcnnDesc(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("x_cs", ctypes.c_int32), ("x_co", ctypes.c_int32), ("wpk", c_void_p), ("b1", c_void_p),
+                ("b2", c_void_p), ("b3", c_void_p), ("out", c_void_p), ("s1", c_void_p), ("s2", c_void_p),
+                ("n", ctypes.c_int32), ("h", ctypes.c_int32), ("w", ctypes.c_int32)]
+
+
 class TileDesc(ctypes.Structure):
     _fields_ = [(n, c_void_p) for n in ("hr_raw", "elev_raw", "hr_min", "hr_max", "elev_minmax", "xform", "lr", "hr", "elev",
                                         "mask", "nearest", "elev_lr", "hr_lr")] + [
@@ -100,6 +107,10 @@ SIGNATURES = {
     "climsr_pack_pull_weights_batched": (c_int, [c_void_p, c_int, c_int64, c_void_p]),
     "climsr_rdb_chain": (c_int, [P(ChainDesc), c_void_p]),
     "climsr_rdb_chain_kp": (c_int, [c_int]),
+    "climsr_srcnn_fwd": (c_int, [P(SrcnnDesc), c_void_p]),
+    "climsr_srcnn_fwd_kernel": (ctypes.c_char_p, [P(SrcnnDesc)]),
+    "climsr_srcnn_pack": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "climsr_srcnn_packed_elems": (c_int64, []),
     "climsr_conv2d_fwd": (c_int, [P(ConvDesc), c_void_p, c_void_p, c_void_p, P(Epilogue), c_void_p, c_void_p]),
     "climsr_conv2d_fwd_bn_parts": (ctypes.c_int64, [P(ConvDesc), P(Epilogue)]),
     "climsr_bn_forward_parts": (c_int, [c_void_p, ctypes.c_int64, c_void_p, ctypes.c_int64, c_int, c_void_p, c_void_p, c_int, c_float,
@@ -173,6 +184,9 @@ SIGNATURES = {
     "climsr_channel_attention_workspace": (c_size_t, [c_int, c_int]),
     "climsr_channel_attention": (c_int, [c_void_p, c_int, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                          c_void_p, c_void_p, c_void_p]),
+    "climsr_channel_attention_parts": (c_int, [c_void_p, c_int, c_int, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                               c_int, c_void_p, c_void_p, c_void_p]),
+    "climsr_conv2d_fwd_ch_parts": (ctypes.c_int64, [P(ConvDesc), P(Epilogue), c_void_p]),
     "climsr_ca_scale_add": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int64, c_int, c_void_p]),
     "climsr_pixel_shuffle_bf16": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
 }

@@ -2572,6 +2572,13 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
 namespace climsr {
 int conv_wr_launch(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const uint16_t* x, const uint16_t* wpk, int kpk,
                    const float* bias, void* y, hipStream_t s, bool dry, char* name, int name_len);
+long conv_wr_ch_parts(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, int* tiles_per_image);
+int conv_wr_ep(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const float* bias);
+}
+
+extern "C" int64_t climsr_conv2d_fwd_ch_parts(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, int32_t* tiles_per_image) {
+  if (!d || !ep) return 0;
+  return conv_wr_ch_parts(d, ep, tiles_per_image);
 }
 
 extern "C" int64_t climsr_conv2d_fwd_bn_parts(const ClimsrConvDesc* d, const ClimsrEpilogue* ep) {
@@ -2612,6 +2619,11 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
   }
   if (ep->act < 0 || ep->act > 4 || ((ep->act == 3 || ep->act == 4) && !ep->res1)) {
     set_error("conv2d_fwd: act %d invalid (3/4 need res1 = the activation output)", ep->act);
+    return CLIMSR_EINVAL;
+  }
+  if (ep->ch_part && conv_wr_ep(d, ep, bias) != 3) {
+    set_error("conv2d_fwd: per-tile channel sums only from the 64 -> 64 3x3 fp32-output register-resident conv "
+              "(climsr_conv2d_fwd_ch_parts)");
     return CLIMSR_EINVAL;
   }
   if (ep->aux && ((ep->aux_cstride | ep->aux_coff) & 3)) {

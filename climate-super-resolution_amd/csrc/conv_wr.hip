@@ -40,6 +40,7 @@ struct WrArgs {
   const float* bias;     // may be null
   uint16_t* y;
   const uint16_t* res1;  // EP 1: residual (v = alpha1 v + beta1 r); EP 2: the activation output (act 3 / 4)
+  float* ch_part;        // EP 3 (fp32 output): per-tile channel sums [tile][64] (null: none)
   int n, in_h, in_w, in_cs, in_co, up, out_h, out_w, out_cs, out_co, kpk;
   int act;  // forward: 0 none, 1 leaky relu, 2 relu; EP 2: 3 / 4 = backward of leaky relu / relu
   float slope, alpha1, beta1;
@@ -48,11 +49,13 @@ struct WrArgs {
   uint32_t x_bytes, y_bytes, r1_bytes;
 };
 typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 
 template <int EP>
 __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int NEPI = EP == 0 ? 16 : 32;  // vector-memory operations of one epilogue (loads + stores), fixed per lane
+  // vector-memory operations of one epilogue (loads + stores), fixed per lane
+  constexpr int NEPI = EP == 0 ? 16 : (EP == 3 ? 20 : 32);
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, col = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int G4 = (int)gridDim.x * 4;
@@ -111,6 +114,7 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
   };
 
   const __amdgpu_buffer_rsrc_t yr = buf_rsrc(a.y, a.y_bytes);
+  const __amdgpu_buffer_rsrc_t pr = buf_rsrc(a.ch_part, EP == 3 && a.ch_part ? (uint32_t)a.ntiles * 256u : 0u);
   const __amdgpu_buffer_rsrc_t rr = buf_rsrc(a.res1, EP ? a.r1_bytes : 0u);
   const int lb = col * WR_XP * 2 + g * 16;  // this lane's byte offset in a footprint row: pixel col, channels 8 g ..
   issue(T, 0);
@@ -155,7 +159,7 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
       const int oy = oy0 + m;
       const bool ok = oy < a.out_h && ox < a.out_w;
       const long pix = ((long)nimg * a.out_h + oy) * a.out_w + ox;
-      off[m] = ok ? (uint32_t)((pix * a.out_cs + a.out_co + 4 * g) * 2) : BUF_OOB;
+      off[m] = ok ? (uint32_t)((pix * a.out_cs + a.out_co + 4 * g) * (EP == 3 ? 4 : 2)) : BUF_OOB;
       if constexpr (EP != 0) {
         const uint32_t ro = ok ? (uint32_t)((pix * a.r1_cs + a.r1_co + 4 * g) * 2) : BUF_OOB;
 #pragma unroll
@@ -165,6 +169,7 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
         }
       }
     }
+    float csum[4][4] = {};  // EP 3: this lane's channel sums over its 4 pixels (rows)
 #pragma unroll
     for (int m = 0; m < 4; ++m)
 #pragma unroll
@@ -188,10 +193,31 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
           }
           v[i] = x;
         }
-        const bf16x2 p0 = {(__bf16)v[0], (__bf16)v[1]}, p1 = {(__bf16)v[2], (__bf16)v[3]};
-        const v2u32 pk = {__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1)};
-        __builtin_amdgcn_raw_buffer_store_b64(pk, yr, off[m] == BUF_OOB ? BUF_OOB : off[m] + (uint32_t)(t * 32), 0, 0);
+        if constexpr (EP == 3) {
+          const v4u32 pk = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+          __builtin_amdgcn_raw_buffer_store_b128(pk, yr, off[m] == BUF_OOB ? BUF_OOB : off[m] + (uint32_t)(t * 64), 0, 0);
+          if (off[m] != BUF_OOB) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) csum[t][i] += v[i];
+          }
+        } else {
+          const bf16x2 p0 = {(__bf16)v[0], (__bf16)v[1]}, p1 = {(__bf16)v[2], (__bf16)v[3]};
+          const v2u32 pk = {__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1)};
+          __builtin_amdgcn_raw_buffer_store_b64(pk, yr, off[m] == BUF_OOB ? BUF_OOB : off[m] + (uint32_t)(t * 32), 0, 0);
+        }
       }
+    if constexpr (EP == 3) {  // per-tile channel sums: the 16 pixel columns by a fixed xor tree, lane col 0 stores
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int k = 1; k < 16; k <<= 1) csum[t][i] += __shfl_xor(csum[t][i], k);
+        const v4u32 pk = {__float_as_uint(csum[t][0]), __float_as_uint(csum[t][1]), __float_as_uint(csum[t][2]),
+                          __float_as_uint(csum[t][3])};
+        __builtin_amdgcn_raw_buffer_store_b128(pk, pr, col == 0 ? (uint32_t)((T * 64 + t * 16 + 4 * g) * 4) : BUF_OOB, 0, 0);
+      }
+    }
     if (Tn >= a.ntiles) break;
     T = Tn;
   }
@@ -202,28 +228,50 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
 
 namespace climsr {
 
-// shape check + launch (called from climsr_conv2d_fwd's dispatcher); returns -1 when the shape is not this kernel's
-int conv_wr_launch(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const uint16_t* x, const uint16_t* wpk, int kpk,
-                   const float* bias, void* y, hipStream_t s, bool dry, char* name, int name_len) {
+// the conv_wr epilogue for (d, ep), or -1 when the conv is not this kernel's: 0 bias / activation, bf16 out; 1 + bf16
+// residual; 2 activation backward from the stored activation (no bias); 3 bias / activation, fp32 out (+ per-tile
+// channel sums).  ch_part only with 3.
+int conv_wr_ep(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const float* bias) {
   const bool res = ep->res1 != nullptr;
   int epk = -1;
-  if (!res && ep->act >= 0 && ep->act <= 2) epk = 0;
-  else if (res && ep->act == 0 && !(ep->res_f32 & 1)) epk = 1;
-  else if (res && (ep->act == 3 || ep->act == 4) && !bias && !(ep->res_f32 & 1)) epk = 2;
+  if (ep->out_mode == 0 && !res && ep->act >= 0 && ep->act <= 2) epk = 0;
+  else if (ep->out_mode == 0 && res && ep->act == 0 && !(ep->res_f32 & 1)) epk = 1;
+  else if (ep->out_mode == 0 && res && (ep->act == 3 || ep->act == 4) && !bias && !(ep->res_f32 & 1)) epk = 2;
+  else if (ep->out_mode == 1 && !res && ep->act >= 0 && ep->act <= 2) epk = 3;
   const long opx = (long)d->n * d->out_h * d->out_w;
-  if (epk < 0 || d->in_c != 64 || d->out_c != 64 || d->cc != 64 || d->ks != 3 || d->stride != 1 || d->pad != 1 ||
-      (d->up != 1 && d->up != 2) || d->out_h != d->in_h * d->up || d->out_w != d->in_w * d->up || d->in_cstride % 8 ||
-      d->in_coff % 8 || (d->out_cstride | d->out_coff) & 3 || ep->down2 || ep->res2 || ep->aux || ep->out_mode != 0 ||
-      ep->bn_part || kpk < 576 || (res && ((ep->res1_cstride | ep->res1_coff) & 3)) ||
-      (long)d->n * d->in_h * d->in_w * d->in_cstride * 2 >= (1L << 31) || opx * d->out_cstride * 2 >= (1L << 31) ||
-      (res && opx * ep->res1_cstride * 2 >= (1L << 31)))
+  if (epk < 0 || (ep->ch_part && epk != 3) || d->in_c != 64 || d->out_c != 64 || d->cc != 64 || d->ks != 3 || d->stride != 1 ||
+      d->pad != 1 || (d->up != 1 && d->up != 2) || d->out_h != d->in_h * d->up || d->out_w != d->in_w * d->up ||
+      d->in_cstride % 8 || d->in_coff % 8 || (d->out_cstride | d->out_coff) & 3 || ep->down2 || ep->res2 || ep->aux ||
+      ep->bn_part || (res && ((ep->res1_cstride | ep->res1_coff) & 3)) ||
+      (long)d->n * d->in_h * d->in_w * d->in_cstride * 2 >= (1L << 31) ||
+      opx * d->out_cstride * (epk == 3 ? 4 : 2) >= (1L << 31) || (res && opx * ep->res1_cstride * 2 >= (1L << 31)) ||
+      (long)ceil_div(d->out_w, WR_TC) * ceil_div(d->out_h, WR_TR) * d->n * 256 >= (1L << 31))
     return -1;
+  return epk;
+}
+
+// tiles (rows of ch_part) of the conv, and per image; 0 when conv_wr does not take (d, ep)
+long conv_wr_ch_parts(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, int* tiles_per_image) {
+  ClimsrEpilogue e = *ep;
+  e.out_mode = 1;
+  if (conv_wr_ep(d, &e, nullptr) != 3) return 0;
+  const int tpi = ceil_div(d->out_w, WR_TC) * ceil_div(d->out_h, WR_TR);
+  if (tiles_per_image) *tiles_per_image = tpi;
+  return (long)tpi * d->n;
+}
+
+int conv_wr_launch(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const uint16_t* x, const uint16_t* wpk, int kpk,
+                   const float* bias, void* y, hipStream_t s, bool dry, char* name, int name_len) {
+  const int epk = conv_wr_ep(d, ep, bias);
+  const bool res = ep->res1 != nullptr;
+  const long opx = (long)d->n * d->out_h * d->out_w;
+  if (epk < 0 || kpk < 576) return -1;
   if (dry) {
     snprintf(name, name_len, "conv_wr_kernel<%d>", epk);
     return CLIMSR_OK;
   }
   WrArgs a;
-  a.x = x; a.w = wpk; a.bias = bias; a.y = (uint16_t*)y; a.res1 = (const uint16_t*)ep->res1;
+  a.x = x; a.w = wpk; a.bias = bias; a.y = (uint16_t*)y; a.res1 = (const uint16_t*)ep->res1; a.ch_part = ep->ch_part;
   a.n = d->n; a.in_h = d->in_h; a.in_w = d->in_w; a.in_cs = d->in_cstride; a.in_co = d->in_coff; a.up = d->up;
   a.out_h = d->out_h; a.out_w = d->out_w; a.out_cs = d->out_cstride; a.out_co = d->out_coff; a.kpk = kpk;
   a.act = ep->act; a.slope = ep->slope; a.alpha1 = ep->alpha1; a.beta1 = ep->beta1;
@@ -231,11 +279,11 @@ int conv_wr_launch(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const uint
   a.tiles_x = ceil_div(d->out_w, WR_TC); a.tiles_y = ceil_div(d->out_h, WR_TR);
   a.ntiles = a.tiles_x * a.tiles_y * d->n;
   a.x_bytes = (uint32_t)((long)d->n * d->in_h * d->in_w * d->in_cstride * 2);
-  a.y_bytes = (uint32_t)(opx * d->out_cstride * 2);
+  a.y_bytes = (uint32_t)(opx * d->out_cstride * (epk == 3 ? 4 : 2));
   a.r1_bytes = res ? (uint32_t)(opx * ep->res1_cstride * 2) : 0u;
   const int ncu = device_cus();
   const int grid = std::min(ceil_div(a.ntiles, 4), ncu);
-  void (*k)(WrArgs) = epk == 0 ? conv_wr_kernel<0> : epk == 1 ? conv_wr_kernel<1> : conv_wr_kernel<2>;
+  void (*k)(WrArgs) = epk == 0 ? conv_wr_kernel<0> : epk == 1 ? conv_wr_kernel<1> : epk == 2 ? conv_wr_kernel<2> : conv_wr_kernel<3>;
   if (int e = lds_opt_in((const void*)k, WR_LDS)) return e;
   hipLaunchKernelGGL(k, dim3(grid), dim3(256), WR_LDS, s, a);
   return check_launch("conv2d_fwd (wr)");

@@ -99,6 +99,34 @@ __device__ __forceinline__ void mfma4x_agpr(f32x4& c0, f32x4& c1, f32x4& c2, f32
   }
 }
 
+// c[t] (+)= A[t] B for t = 0, 1 (two co blocks sharing a B fragment); A1V: the second A fragment is in a VGPR
+template <bool FIRST, bool A1V>
+__device__ __forceinline__ void mfma2x_agpr(f32x4& c0, f32x4& c1, const bf16x8& a0, const bf16x8& a1, const bf16x8& b) {
+  if constexpr (FIRST) {
+    if constexpr (A1V) {
+      asm volatile("s_nop 3\n\tv_mfma_f32_16x16x32_bf16 %0, %2, %4, 0\n\tv_mfma_f32_16x16x32_bf16 %1, %3, %4, 0"
+                   : "=&v"(c0), "=&v"(c1) : "a"(a0), "v"(a1), "v"(b));
+    } else {
+      asm volatile("s_nop 3\n\tv_mfma_f32_16x16x32_bf16 %0, %2, %4, 0\n\tv_mfma_f32_16x16x32_bf16 %1, %3, %4, 0"
+                   : "=&v"(c0), "=&v"(c1) : "a"(a0), "a"(a1), "v"(b));
+    }
+  } else {
+    if constexpr (A1V) {
+      asm volatile("s_nop 3\n\tv_mfma_f32_16x16x32_bf16 %0, %2, %4, %0\n\tv_mfma_f32_16x16x32_bf16 %1, %3, %4, %1"
+                   : "+v"(c0), "+v"(c1) : "a"(a0), "v"(a1), "v"(b));
+    } else {
+      asm volatile("s_nop 3\n\tv_mfma_f32_16x16x32_bf16 %0, %2, %4, %0\n\tv_mfma_f32_16x16x32_bf16 %1, %3, %4, %1"
+                   : "+v"(c0), "+v"(c1) : "a"(a0), "a"(a1), "v"(b));
+    }
+  }
+}
+
+__device__ __forceinline__ void pad_mfma8(f32x4 (&c)[4][2]) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3"
+               : "+v"(c[0][0]), "+v"(c[0][1]), "+v"(c[1][0]), "+v"(c[1][1]), "+v"(c[2][0]), "+v"(c[2][1]), "+v"(c[3][0]),
+                 "+v"(c[3][1]));
+}
+
 __device__ __forceinline__ void pad_mfma(f32x4 (&pn)[4]) {
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+v"(pn[0]), "+v"(pn[1]), "+v"(pn[2]), "+v"(pn[3]));
 }

@@ -97,6 +97,40 @@ extern "C" int climsr_channel_attention(const float* u, int n, int64_t hw, int c
 
 extern "C" size_t climsr_channel_attention_workspace(int n, int c) { return (size_t)n * POOL_SPLIT * c * sizeof(double); }
 
+// channel_attention from per-tile channel sums: the image's tile rows folded into POOL_SPLIT fp64 slices (slice sp =
+// tiles [tpi sp / POOL_SPLIT, tpi (sp + 1) / POOL_SPLIT), summed in order), then ca_mlp_kernel over the slices -- the
+// same fixed order every run.  One workgroup per (slice, image): 256 threads = 4 tile lanes x 64 channels per round.
+__global__ __launch_bounds__(256) void tile_parts_fold_kernel(const float* __restrict__ part, int tpi, int c, double* __restrict__ out) {
+  const int nimg = blockIdx.y, sp = blockIdx.x;
+  const long t0 = (long)tpi * sp / POOL_SPLIT, t1 = (long)tpi * (sp + 1) / POOL_SPLIT;
+  __shared__ double sh[256];
+  for (int c0 = 0; c0 < c; c0 += 64) {
+    const int ch = c0 + (threadIdx.x & 63), tl = threadIdx.x >> 6;
+    double t = 0.0;
+    if (ch < c)
+      for (long k = t0 + tl; k < t1; k += 4) t += (double)part[((long)nimg * tpi + k) * c + ch];
+    sh[threadIdx.x] = t;
+    __syncthreads();
+    if (threadIdx.x < 64 && ch < c)
+      out[((long)nimg * POOL_SPLIT + sp) * c + ch] = ((sh[threadIdx.x] + sh[64 + threadIdx.x]) + sh[128 + threadIdx.x]) + sh[192 + threadIdx.x];
+    __syncthreads();
+  }
+}
+
+extern "C" int climsr_channel_attention_parts(const float* part, int n, int tiles_per_image, int64_t hw, int c, const float* w1,
+                                              const float* b1, const float* w2, const float* b2, int cr, double* workspace, float* s,
+                                              void* stream) {
+  if (!part || !w1 || !w2 || !s || !workspace || n <= 0 || tiles_per_image <= 0 || hw <= 0 || c <= 0 || c > 1024 || cr <= 0) {
+    set_error("channel_attention_parts: bad args");
+    return CLIMSR_EINVAL;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(tile_parts_fold_kernel, dim3(POOL_SPLIT, n), dim3(256), 0, st, part, tiles_per_image, c, workspace);
+  hipLaunchKernelGGL(ca_mlp_kernel, dim3(n), dim3(1024), (size_t)(c + cr) * sizeof(float), st, workspace, (long)hw, c, cr, w1, b1,
+                     w2, b2, s);
+  return check_launch("channel_attention_parts");
+}
+
 // xres[p][c] = u[p][c] * s[n][c] + xres[p][c];  xb[p][c] = bf16(xres[p][c])   (RCAB: body(x) + x)
 __global__ __launch_bounds__(256) void ca_scale_add_kernel(const float* __restrict__ u, int u_cs, const float* __restrict__ s,
                                                            float* __restrict__ xres, uint16_t* __restrict__ xb, int xb_cs, long hw,

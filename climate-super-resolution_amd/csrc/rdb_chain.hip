@@ -297,13 +297,10 @@ __global__ __launch_bounds__(256, 1) void rdb_chain_kernel(ChainArgs a) {
     __builtin_amdgcn_raw_buffer_store_b64((v2u32){pk.x, pk.y}, orr, own ? ob : BUF_OOB, 0, 0);
   };
 
-  auto step = [&](int s, f32x4& P2) {
-    const int y1 = r0 - 3 + s;
-    uint4 nxt[XIT];
-    issue_row(y1 + 2, nxt);  // stored at the end of this step
-    // pull: the stored activations of the four levels' rows in this step
-    uint2 mk[4] = {};
+  // pull: the stored activations of the four levels' rows in step s (issued a step ahead)
+  auto issue_mask = [&](int s, uint2 (&mk)[4]) {
     if constexpr (MODE == 1) {
+      const int y1 = r0 - 3 + s;
 #pragma unroll
       for (int L = 1; L <= 4; ++L) {
         const int y = y1 - 2 * (L - 1);
@@ -313,6 +310,15 @@ __global__ __launch_bounds__(256, 1) void rdb_chain_kernel(ChainArgs a) {
         mk[L - 1] = make_uint2(v[0], v[1]);
       }
     }
+  };
+
+  // step s: base rows are loaded two steps before they are staged (row y1 + 2, stored at the end of step s, was issued
+  // in step s - 1 into cur; row y1 + 3 goes into nxt now) and the pull's activation rows one step before their use,
+  // so the HBM latency hides under a step's MFMAs
+  auto step = [&](int s, f32x4& P2, uint4 (&cur)[XIT], uint4 (&nxt)[XIT], const uint2 (&mk)[4], uint2 (&mkn)[4]) {
+    const int y1 = r0 - 3 + s;
+    issue_row(y1 + 3, nxt);
+    issue_mask(s + 1, mkn);
     // levels whose base part is computed in this step: level L's rows are computed 2(L-1) steps before it finishes
     // them, for s in [L-1, R + 6 - L] -- always the prefix 1..m of the levels (none for rows outside the image)
     const bool yin = fact && y1 >= 0 && y1 < a.h;
@@ -360,12 +366,16 @@ __global__ __launch_bounds__(256, 1) void rdb_chain_kernel(ChainArgs a) {
     P2 = pn[1];
     *p3 = pn[2];  // (this wave's own slots: no barrier between its read and its write)
     *p4 = pn[3];
-    store_row(y1 + 2, nxt);  // its slot held row y1 - 2, which no level reads in this step
+    store_row(y1 + 2, cur);  // its slot held row y1 - 2, which no level reads in this step
     lds_barrier();
   };
+  uint4 ra[XIT], rb[XIT];
+  uint2 ma[4] = {}, mb[4] = {};
+  issue_row(r0 - 1, ra);
+  issue_mask(0, ma);
   for (int s = 0; s < R + 9; s += 2) {
-    step(s, P2e);
-    if (s + 1 < R + 9) step(s + 1, P2o);
+    step(s, P2e, ra, rb, ma, mb);
+    if (s + 1 < R + 9) step(s + 1, P2o, rb, ra, mb, ma);
   }
 }
 

@@ -25,7 +25,7 @@ from torch import Tensor
 
 from ..core.flat import FlatParamsMixin
 from ..ops import (ACT_LRELU, ACT_LRELU_BWD, ACT_NONE, ACT_RELU, ACT_RELU_BWD, OUT_F32, BatchedPacker, ConvPlan, GroupedWgrad, PullPacker, PullPlan,
-                   RdbChain, Workspace, act_grad, axpby, nchw_to_nhwc, pack_planes8)
+                   RdbChain, SrcnnTail, Workspace, act_grad, axpby, nchw_to_nhwc, pack_planes8)
 from .srcnn import SRCNN
 
 
@@ -148,6 +148,9 @@ class _Engine:
             blk, r = divmod(i, 3)
             convs = [self.plans[self.rdb_name(blk, r + 1, k)] for k in range(1, 6)]
             self.rdb_wgrads.append(GroupedWgrad(convs, self.dc, f"RRDB_trunk.{blk}.RDB{r + 1}"))
+        # the SRCNN tail as one launch (csrc/srcnn.hip) when its input is the climate cat[out, elev, mask] (<= 4 channels)
+        tail = [self.plans[f"srcnn.conv{k}"] for k in (1, 2, 3)]
+        self.srcnn_tail = SrcnnTail(tail) if tail[0].cin_real <= 4 and gen.out_channels == 1 else None
         self.version = -1
 
     def bind_grads(self):
@@ -159,17 +162,15 @@ class _Engine:
     def ensure_packed(self):
         v = self.gen._flat._version
         if v != self.version:
-            self.packer.run()
-            self.pull_packer.run()
-            if self.pull_rest_on:
-                self.pull_packer_rest.run()
-            self.version = v
+            self.repack()
 
     def repack(self):
         self.packer.run()
         self.pull_packer.run()
         if self.pull_rest_on:
             self.pull_packer_rest.run()
+        if self.srcnn_tail is not None:
+            self.srcnn_tail.pack()
         self.version = self.gen._flat._version
 
     def chain_ok(self, w: int, n: int = 1, h: int = 1) -> bool:
@@ -177,6 +178,15 @@ class _Engine:
         climsr_rdb_chain rejects larger ones; the pull reads the dense buffer as its activation mask, same size);
         anything else runs conv by conv."""
         return bool(self.chains) and n * h * w * self.dc * 2 < (1 << 31)
+
+    def _rdb_wgrad(self, i, src, dz, n, h, w, ws, acc):
+        blk, r = divmod(i, 3)
+        if self.dc % 64 == 0:
+            self.rdb_wgrads[i].run(src, self.dc, 0, h, w, dz, self.dc, n, ws, acc)
+        else:
+            for k in range(1, 6):
+                off = (k - 1) * self.gc
+                self.plans[self.rdb_name(blk, r + 1, k)].wgrad(src, self.dc, 0, h, w, dz[..., off:], self.dc, n, ws, acc)
 
     def rdb_name(self, i, r, c):
         return f"RRDB_trunk.{i}.RDB{r}.conv{c}"
@@ -249,17 +259,23 @@ class _Engine:
         P["conv_last"].fwd(hr, nf, 0, hh, ww, tail, 8, 0, n)
         nchw_to_nhwc(elev.contiguous().float(), tail, 8, oc)
         nchw_to_nhwc(mask.contiguous().float(), tail, 8, oc + 1)
-        s1 = _bf16((n, hh, ww, 64), dev)
-        P["srcnn.conv1"].fwd(tail, 8, 0, hh, ww, s1, 64, 0, n, act=ACT_RELU)
-        s2 = _bf16((n, hh, ww, 32), dev)
-        P["srcnn.conv2"].fwd(s1, 64, 0, hh, ww, s2, 32, 0, n, act=ACT_RELU)
         out = torch.empty((n, oc, hh, ww), dtype=torch.float32, device=dev)
-        if oc == 1:
-            P["srcnn.conv3"].fwd(s2, 32, 0, hh, ww, out, 1, 0, n, out_mode=OUT_F32)
+        s1 = s2 = None
+        if self.srcnn_tail is not None:
+            if keep:  # relu(conv1), relu(conv2) for the backward's weight gradients and ReLU masks
+                s1, s2 = _bf16((n, hh, ww, 64), dev), _bf16((n, hh, ww, 32), dev)
+            self.srcnn_tail.fwd(tail, 8, 0, n, hh, ww, out, s1, s2)
         else:
-            tmp = _f32((n, hh, ww, oc), dev)
-            P["srcnn.conv3"].fwd(s2, 32, 0, hh, ww, tmp, oc, 0, n, out_mode=OUT_F32)
-            out.copy_(tmp.permute(0, 3, 1, 2))
+            s1 = _bf16((n, hh, ww, 64), dev)
+            P["srcnn.conv1"].fwd(tail, 8, 0, hh, ww, s1, 64, 0, n, act=ACT_RELU)
+            s2 = _bf16((n, hh, ww, 32), dev)
+            P["srcnn.conv2"].fwd(s1, 64, 0, hh, ww, s2, 32, 0, n, act=ACT_RELU)
+            if oc == 1:
+                P["srcnn.conv3"].fwd(s2, 32, 0, hh, ww, out, 1, 0, n, out_mode=OUT_F32)
+            else:
+                tmp = _f32((n, hh, ww, oc), dev)
+                P["srcnn.conv3"].fwd(s2, 32, 0, hh, ww, tmp, oc, 0, n, out_mode=OUT_F32)
+                out.copy_(tmp.permute(0, 3, 1, 2))
         saved = None
         if keep:
             saved = dict(n=n, h=h, w=w, hh=hh, ww=ww, lr=lr, dense=dense, fea2=fea2, u1=u1, u2=u2, hr=hr, tail=tail, s1=s1, s2=s2)
@@ -324,6 +340,8 @@ class _Engine:
         # the last RDB (r = 2) sees 0.2 * G at its output; its conv5 output gradient is 0.2 * that
         P["trunk_conv"].dgrad(dz64, nf, h, w, G[L % 4], nf, 0, n, aux=dZ[(L - 1) % 2], aux_cs=dc, aux_co=4 * gc, aux_scale=0.04)
         # ---- RRDB trunk, reverse (esrgan.py:32-54), pull form
+        # (running RDB i's weight gradients on a second stream beside the pull-x / pull-chain launches measured 0.5 ms
+        # SLOWER per GAN step than this serial order)
         for i in reversed(range(L)):
             blk, r = divmod(i, 3)
             s_o = 0.2 if r == 2 else 1.0  # RDB3's output enters the RRDB output scaled by 0.2 (esrgan.py:54)
@@ -346,12 +364,7 @@ class _Engine:
                          res1=g_out, res1_cs=nf, res1_co=0, beta1=s_o,
                          res2=g_skip if r == 0 else None, res2_cs=nf, res2_co=0,
                          aux=aux, aux_cs=dc, aux_co=4 * gc, aux_scale=0.2 * (0.2 if r == 0 else 1.0))
-            if self.dc % 64 == 0:
-                self.rdb_wgrads[i].run(src, dc, 0, h, w, dz, dc, n, ws, acc)
-            else:
-                for k in range(1, 6):
-                    off = (k - 1) * gc
-                    self.plans[self.rdb_name(blk, r + 1, k)].wgrad(src, dc, 0, h, w, dz[..., off:], dc, n, ws, acc)
+            self._rdb_wgrad(i, src, dz, n, h, w, ws, acc)
             hook = self.gen._grad_ready_hook
             if hook is not None and r == 0 and blk in self.gen._grad_ready_blocks:
                 # every gradient from RRDB_trunk.<blk> on (flat order: trunk blocks, tail convs) is final

@@ -127,10 +127,11 @@ class ConvPlan:
             res1: Optional[torch.Tensor] = None, alpha1: float = 1.0, res1_cs: int = 0, res1_co: int = 0,
             res2: Optional[torch.Tensor] = None, alpha2: float = 1.0, res2_cs: int = 0, res2_co: int = 0,
             out_mode: int = OUT_BF16, beta1: float = 1.0, beta2: float = 1.0, aux: Optional[torch.Tensor] = None,
-            aux_cs: int = 0, aux_co: int = 0, aux_scale: float = 1.0, bn_part: Optional[torch.Tensor] = None) -> None:
+            aux_cs: int = 0, aux_co: int = 0, aux_scale: float = 1.0, bn_part: Optional[torch.Tensor] = None,
+            ch_part: Optional[torch.Tensor] = None) -> None:
         """y = epilogue(conv(x)); residuals res1/res2 may be bf16 or fp32 tensors (dtype decides), aux = optional
         second bf16 output aux_scale * y; bn_part (fp64, bn_parts() rows x 2 x cout) = BatchNorm partial sums of y
-        for bn_forward_parts."""
+        for bn_forward_parts; ch_part (fp32, ch_parts() rows x cout) = per-tile channel sums of y (fp32 output)."""
         oh, ow = self.out_hw(in_h, in_w, up)
         if (self.cin_real == 1 and self.ks in (3, 5) and self.stride == 1 and self.pad == self.ks // 2 and up == 1
                 and self.cout in (32, 64) and out_mode == OUT_BF16 and y.dtype == torch.bfloat16 and res1 is None and res2 is None
@@ -149,7 +150,7 @@ class ConvPlan:
         rf = (1 if res1 is not None and res1.dtype == torch.float32 else 0) | \
              (2 if res2 is not None and res2.dtype == torch.float32 else 0)
         ep = Epilogue(act, slope, alpha1, ptr(res1), res1_cs, res1_co, alpha2, ptr(res2), res2_cs, res2_co, out_mode, 0,
-                      rf, beta1, beta2, aux_cs, ptr(aux), aux_co, aux_scale, ptr(bn_part))
+                      rf, beta1, beta2, aux_cs, ptr(aux), aux_co, aux_scale, ptr(bn_part), ch_part=ptr(ch_part))
         b = ptr(self.bias) if (use_bias and self.bias is not None) else None
         flops = 2 * self.cin_real * self.cout * self.ks * self.ks * n * oh * ow
         opx = n * oh * ow
@@ -167,6 +168,16 @@ class ConvPlan:
         d = ConvDesc(n, in_h, in_w, self.cin_k, x_cs, 0, 1, self.ks, self.stride, self.pad, oh, ow, self.cout, y_cs, 0, self.cc)
         ep = Epilogue(ACT_NONE, 0.0, 1.0, None, 0, 0, 1.0, None, 0, 0, OUT_BF16, 0, 0, 1.0, 1.0, 0, None, 0, 1.0, 1)
         return int(_lib.load().climsr_conv2d_fwd_bn_parts(ctypes.byref(d), ctypes.byref(ep)))
+
+    def ch_parts(self, x_cs: int, in_h: int, in_w: int, n: int, y_cs: int) -> tuple:
+        """(rows, rows per image) of the per-tile channel sums fwd(..., out_mode=OUT_F32, ch_part=...) writes, (0, 0)
+        if its kernel cannot (climsr_conv2d_fwd_ch_parts)."""
+        oh, ow = self.out_hw(in_h, in_w)
+        d = ConvDesc(n, in_h, in_w, self.cin_k, x_cs, 0, 1, self.ks, self.stride, self.pad, oh, ow, self.cout, y_cs, 0, self.cc)
+        ep = Epilogue(ACT_NONE, 0.0, 1.0, None, 0, 0, 1.0, None, 0, 0, OUT_F32, 0, 0, 1.0, 1.0, 0, None, 0, 1.0, None)
+        tpi = ctypes.c_int32(0)
+        rows = int(_lib.load().climsr_conv2d_fwd_ch_parts(ctypes.byref(d), ctypes.byref(ep), ctypes.byref(tpi)))
+        return rows, int(tpi.value)
 
     def dgrad(self, dz: torch.Tensor, dz_cs: int, out_h: int, out_w: int, g: torch.Tensor, g_cs: int, g_co: int, n: int,
               accumulate: bool = False, down2: bool = False, cout_t: Optional[int] = None, aux: Optional[torch.Tensor] = None,
@@ -485,6 +496,43 @@ class RdbChain:
             d.moff[L] = 64 + 16 * (j - 1)
         d.mask, d.mcs, d.act, d.slope, d.n, d.h, d.w = ptr(dense), dc, ACT_LRELU_BWD, slope, n, h, w
         self._launch(d, "pull")
+
+
+class SrcnnTail:
+    """srcnn.conv1 -> ReLU -> conv2 -> ReLU -> conv3 (srcnn.py:9-18) of the generator tail as ONE launch
+    (csrc/srcnn.hip): reads the 4-channel bf16 cat[out, elev, mask] input, writes the fp32 output; the 64- / 32-channel
+    intermediates are stored only for a training forward (``s1``/``s2``).  ``convs``: the three bound ConvPlans."""
+
+    def __init__(self, convs, name: str = "srcnn"):
+        self.convs, self.name = convs, name
+        c1, c2, c3 = convs
+        assert (c1.cin_real <= 4 and c1.cout == 64 and c1.ks == 9 and c2.cout == 32 and c2.ks == 1 and c3.cout == 1
+                and c3.ks == 5), "the fused SRCNN tail takes in_c <= 4, 64 / 32 / 1 channels, 9 / 1 / 5 kernels"
+        self.wpk = torch.empty((_lib.load().climsr_srcnn_packed_elems(),), dtype=torch.bfloat16, device=c1.weight.device)
+
+    def pack(self) -> None:
+        c1, c2, c3 = self.convs
+        _launch("srcnn pack", lambda: _lib.load().climsr_srcnn_pack(ptr(c1.weight), ptr(c2.weight), ptr(c3.weight), c1.cin_real,
+                                                                    ptr(self.wpk), _lib.stream_ptr()))
+
+    def fwd(self, x: torch.Tensor, x_cs: int, x_co: int, n: int, h: int, w: int, out: torch.Tensor,
+            s1: Optional[torch.Tensor] = None, s2: Optional[torch.Tensor] = None) -> None:
+        c1, c2, c3 = self.convs
+        assert out.dtype == torch.float32 and out.is_contiguous() and out.numel() == n * h * w
+        assert x.dtype == torch.bfloat16 and x.is_contiguous() and x.numel() == n * h * w * x_cs
+        if s1 is not None:
+            assert s1.dtype == torch.bfloat16 and s1.numel() == n * h * w * 64 and s1.is_contiguous()
+            assert s2.dtype == torch.bfloat16 and s2.numel() == n * h * w * 32 and s2.is_contiguous()
+        d = _lib.SrcnnDesc()
+        d.x, d.x_cs, d.x_co, d.wpk = ptr(x), x_cs, x_co, ptr(self.wpk)
+        d.b1, d.b2, d.b3, d.out = ptr(c1.bias), ptr(c2.bias), ptr(c3.bias), ptr(out)
+        d.s1, d.s2, d.n, d.h, d.w = ptr(s1), ptr(s2), n, h, w
+        npx = n * h * w
+        flops = 2 * npx * (c1.cin_real * 81 * 64 + 64 * 32 + 32 * 25)
+        nbytes = npx * (8 + 4 + (192 if s1 is not None else 0))
+        name = _lib.load().climsr_srcnn_fwd_kernel(ctypes.byref(d)).decode() if PROFILER is not None else ""
+        _run(name, flops, lambda: check(_lib.load().climsr_srcnn_fwd(ctypes.byref(d), _lib.stream_ptr()), "srcnn tail"),
+             "fwd " + self.name, nbytes)
 
 
 class PullPacker:

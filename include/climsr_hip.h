@@ -86,7 +86,15 @@ typedef struct ClimsrEpilogue {
   const float* bn_rstd;
   const float* bn_gamma;
   const float* bn_beta;
+  /* optional (the 64 -> 64 3x3 register-resident conv, climsr_conv2d_fwd_ch_parts > 0): per-tile channel sums of the
+     stored output values, ch_part[tile][out_c] fp32, tiles of one image contiguous -- the global average pool of RCAN's
+     channel attention (rcan.py:50-69) without re-reading the output; finish with climsr_channel_attention_parts */
+  float* ch_part;
 } ClimsrEpilogue;
+
+/* rows (tiles) of ClimsrEpilogue.ch_part for this conv and epilogue, 0 when its kernel cannot emit them; the tiles of
+ * one image are *tiles_per_image consecutive rows */
+int64_t climsr_conv2d_fwd_ch_parts(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, int32_t* tiles_per_image);
 
 const char* climsr_last_error(void);
 int climsr_version(void);
@@ -433,10 +441,40 @@ int climsr_denormalize_mask(const float* sr, const float* mask, const double* mi
 size_t climsr_channel_attention_workspace(int n, int c);
 int climsr_channel_attention(const float* u, int n, int64_t hw, int c, int u_cstride, const float* w1, const float* b1,
                              const float* w2, const float* b2, int cr, double* workspace, float* s, void* stream);
+/* The same from per-tile channel sums already pooled by the conv that produced u (ClimsrEpilogue.ch_part):
+ * part[n][tiles_per_image][c] fp32, summed over the tiles in a fixed order in fp64; hw = pixels per image;
+ * workspace = climsr_channel_attention_workspace(n, c) bytes. */
+int climsr_channel_attention_parts(const float* part, int n, int tiles_per_image, int64_t hw, int c, const float* w1,
+                                   const float* b1, const float* w2, const float* b2, int cr, double* workspace, float* s,
+                                   void* stream);
 /* RCAB residual with the attention scale (rcan.py:104-107): xres = u * s + xres (fp32 [n][hw][c]) and
  * xb = bf16(xres) ([n][hw][xb_cstride], the next conv's input).  c, strides multiples of 4. */
 int climsr_ca_scale_add(const float* u, int u_cstride, const float* s, float* xres, uint16_t* xb, int xb_cstride, int n,
                         int64_t hw, int c, void* stream);
+/* The SRCNN tail of the ESRGAN generator as ONE launch, replacing srcnn.conv1 -> ReLU -> conv2 -> ReLU -> conv3
+ * (srcnn.py:9-18) on torch.cat([out, elev, mask], 1) (esrgan.py:99-100): x = bf16 NHWC, channels x_co .. x_co+3 (the
+ * in_c <= 4 real ones + zeros); out = fp32 [n][1][h][w]; the 64- and 32-channel intermediates stay on chip unless s1
+ * and s2 are given (training: relu(conv1) bf16 [n][h][w][64], relu(conv2) bf16 [n][h][w][32] for the backward).
+ * wpk = climsr_srcnn_packed_elems() bf16 from climsr_srcnn_pack; b1/b2/b3 = the fp32 biases (64 / 32 / 1). */
+typedef struct ClimsrSrcnnDesc {
+  const uint16_t* x;
+  int32_t x_cs, x_co;
+  const uint16_t* wpk;
+  const float* b1;
+  const float* b2;
+  const float* b3;
+  float* out;
+  uint16_t* s1;
+  uint16_t* s2;
+  int32_t n, h, w;
+} ClimsrSrcnnDesc;
+int climsr_srcnn_fwd(const ClimsrSrcnnDesc* d, void* stream);
+/* rocprof name of the kernel climsr_srcnn_fwd launches for d (nothing is launched) */
+const char* climsr_srcnn_fwd_kernel(const ClimsrSrcnnDesc* d);
+/* Pack the three SRCNN weights (fp32 OIHW: w1 [64][in_c][9][9], w2 [32][64][1][1], w3 [1][32][5][5]) into the MFMA
+ * fragment order climsr_srcnn_fwd reads (async on stream; run after every weight update). */
+int climsr_srcnn_pack(const float* w1, const float* w2, const float* w3, int in_c, uint16_t* out, void* stream);
+int64_t climsr_srcnn_packed_elems(void);
 /* nn.PixelShuffle(r) (Upsampler, rcan.py:17-47) on NHWC bf16: y[n][y*r+i][x*r+j][co] = x[n][y][x][co*r*r+i*r+j].
  * Bit-exact index map; c_out and out_cstride multiples of 8. */
 int climsr_pixel_shuffle_bf16(const uint16_t* x, int n, int h, int w, int c_out, int r, int in_cstride, uint16_t* y,

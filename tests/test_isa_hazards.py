@@ -26,7 +26,7 @@ def _kernels(asm_text):
     return out
 
 
-@pytest.mark.parametrize("src", ["rdb_chain.hip", "conv_wr.hip"])
+@pytest.mark.parametrize("src", ["rdb_chain.hip", "conv_wr.hip", "srcnn.hip"])
 def test_asm_mfma_results_are_padded(src, tmp_path):
     if not os.path.exists(HIPCC):
         pytest.skip("hipcc not available")
