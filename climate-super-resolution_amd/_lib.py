@@ -76,6 +76,13 @@ class SrcnnDesc(ctypes.Structure):
                 ("n", ctypes.c_int32), ("h", ctypes.c_int32), ("w", ctypes.c_int32)]
 
 
+class SrcnnBwdDesc(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("x_cs", ctypes.c_int32), ("x_co", ctypes.c_int32), ("gout", c_void_p), ("wpk", c_void_p),
+                ("b1", c_void_p), ("b2", c_void_p), ("dz1", c_void_p), ("part", c_void_p), ("gw2", c_void_p), ("gb2", c_void_p),
+                ("gw3", c_void_p), ("gb3", c_void_p), ("accumulate", ctypes.c_int32), ("n", ctypes.c_int32),
+                ("h", ctypes.c_int32), ("w", ctypes.c_int32)]
+
+
 class TileDesc(ctypes.Structure):
     _fields_ = [(n, c_void_p) for n in ("hr_raw", "elev_raw", "hr_min", "hr_max", "elev_minmax", "xform", "lr", "hr", "elev",
                                         "mask", "nearest", "elev_lr", "hr_lr")] + [
@@ -106,11 +113,14 @@ SIGNATURES = {
     "climsr_pack_conv_weights_batched": (c_int, [c_void_p, c_int, c_int64, c_void_p]),
     "climsr_pack_pull_weights_batched": (c_int, [c_void_p, c_int, c_int64, c_void_p]),
     "climsr_rdb_chain": (c_int, [P(ChainDesc), c_void_p]),
+    "climsr_rdb_chain_kernel": (ctypes.c_char_p, [P(ChainDesc)]),
     "climsr_rdb_chain_kp": (c_int, [c_int]),
     "climsr_srcnn_fwd": (c_int, [P(SrcnnDesc), c_void_p]),
     "climsr_srcnn_fwd_kernel": (ctypes.c_char_p, [P(SrcnnDesc)]),
     "climsr_srcnn_pack": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "climsr_srcnn_packed_elems": (c_int64, []),
+    "climsr_srcnn_bwd": (c_int, [P(SrcnnBwdDesc), c_void_p]),
+    "climsr_srcnn_bwd_workspace": (c_int64, [c_int, c_int, c_int]),
     "climsr_conv2d_fwd": (c_int, [P(ConvDesc), c_void_p, c_void_p, c_void_p, P(Epilogue), c_void_p, c_void_p]),
     "climsr_conv2d_fwd_bn_parts": (ctypes.c_int64, [P(ConvDesc), P(Epilogue)]),
     "climsr_bn_forward_parts": (c_int, [c_void_p, ctypes.c_int64, c_void_p, ctypes.c_int64, c_int, c_void_p, c_void_p, c_int, c_float,

@@ -1,4 +1,6 @@
-// Residual-dense-block chain: the four 16-output 3x3 convs of an RDB in ONE launch (esrgan.py:22-37).
+// Residual-dense-block chain: the four 16-output 3x3 convs of an RDB in ONE launch (esrgan.py:22-37), for images
+// of any width (column windows); widths 16 / 32 / 48 / 64 take rdb_chain_narrow.hip's level-per-wave kernel, which
+// is faster there (two waves per SIMD).
 //
 // Forward:        x1 = lrelu(conv1(x)),  x2 = lrelu(conv2([x,x1])),  x3 = ...,  x4 = lrelu(conv4([x,x1,x2,x3]))
 // Pull backward:  dZ4 = lrelu'(x4) * pull4(dZ5),  dZ3 = lrelu'(x3) * pull3([dZ5,dZ4]),  ...  (climsr_hip.h)
@@ -174,7 +176,7 @@ __device__ __forceinline__ void base_part(const uint16_t* lds, const bf16x8 (&af
 
 // MODE 0: forward (bias + leaky relu); 1: pull (leaky-relu derivative of the stored activation, no bias).
 template <int MODE>
-__global__ __launch_bounds__(256, 1) void rdb_chain_kernel(ChainArgs a) {
+__global__ __launch_bounds__(256, 1) void rdb_chain_wide_kernel(ChainArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint16_t* lds = (uint16_t*)smem;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, col = lane & 15;
@@ -381,6 +383,18 @@ __global__ __launch_bounds__(256, 1) void rdb_chain_kernel(ChainArgs a) {
 
 }  // namespace
 
+namespace climsr {
+int rdb_chain_narrow(const ClimsrChainDesc* d, hipStream_t stream);
+}
+
+static bool narrow_width(int w) { return w <= 64 && w % 16 == 0; }
+
+extern "C" const char* climsr_rdb_chain_kernel(const ClimsrChainDesc* d) {
+  if (!d || d->w <= 0) return "";
+  if (narrow_width(d->w)) return d->act == 1 ? "rdb_chain_kernel<0>" : "rdb_chain_kernel<1>";
+  return d->act == 1 ? "rdb_chain_wide_kernel<0>" : "rdb_chain_wide_kernel<1>";
+}
+
 extern "C" int climsr_rdb_chain(const ClimsrChainDesc* d, void* stream) {
   if (!d || !d->base || !d->out || d->n <= 0 || d->h <= 0 || d->w <= 0 || d->bcs % 8 || d->boff % 8 || d->ocs % 4 ||
       (d->act != 1 && d->act != 3) || (d->act == 3 && (!d->mask || d->mcs % 4)) || !(d->slope >= 0.f && d->slope <= 1.f)) {
@@ -398,6 +412,7 @@ extern "C" int climsr_rdb_chain(const ClimsrChainDesc* d, void* stream) {
     set_error("rdb_chain: tensors over 2 GiB");
     return CLIMSR_EINVAL;
   }
+  if (narrow_width(d->w)) return rdb_chain_narrow(d, (hipStream_t)stream);
   ChainArgs a;
   a.base = d->base; a.bcs = d->bcs; a.boff = d->boff;
   a.out = d->out; a.ocs = d->ocs;
@@ -434,11 +449,11 @@ extern "C" int climsr_rdb_chain(const ClimsrChainDesc* d, void* stream) {
     return CLIMSR_EINVAL;
   }
   if (d->act == 1) {
-    if (int e = lds_opt_in((const void*)rdb_chain_kernel<0>, LDS_BYTES)) return e;
-    hipLaunchKernelGGL(rdb_chain_kernel<0>, dim3((unsigned)grid), dim3(256), LDS_BYTES, (hipStream_t)stream, a);
+    if (int e = lds_opt_in((const void*)rdb_chain_wide_kernel<0>, LDS_BYTES)) return e;
+    hipLaunchKernelGGL(rdb_chain_wide_kernel<0>, dim3((unsigned)grid), dim3(256), LDS_BYTES, (hipStream_t)stream, a);
   } else {
-    if (int e = lds_opt_in((const void*)rdb_chain_kernel<1>, LDS_BYTES)) return e;
-    hipLaunchKernelGGL(rdb_chain_kernel<1>, dim3((unsigned)grid), dim3(256), LDS_BYTES, (hipStream_t)stream, a);
+    if (int e = lds_opt_in((const void*)rdb_chain_wide_kernel<1>, LDS_BYTES)) return e;
+    hipLaunchKernelGGL(rdb_chain_wide_kernel<1>, dim3((unsigned)grid), dim3(256), LDS_BYTES, (hipStream_t)stream, a);
   }
   return check_launch("rdb_chain");
 }

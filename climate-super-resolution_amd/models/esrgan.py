@@ -150,7 +150,7 @@ class _Engine:
             self.rdb_wgrads.append(GroupedWgrad(convs, self.dc, f"RRDB_trunk.{blk}.RDB{r + 1}"))
         # the SRCNN tail as one launch (csrc/srcnn.hip) when its input is the climate cat[out, elev, mask] (<= 4 channels)
         tail = [self.plans[f"srcnn.conv{k}"] for k in (1, 2, 3)]
-        self.srcnn_tail = SrcnnTail(tail) if tail[0].cin_real <= 4 and gen.out_channels == 1 else None
+        self.srcnn_tail = SrcnnTail(tail) if tail[0].cin_real <= 4 and gen.out_channels == 1 and nf == 64 else None
         self.version = -1
 
     def bind_grads(self):
@@ -261,10 +261,8 @@ class _Engine:
         nchw_to_nhwc(mask.contiguous().float(), tail, 8, oc + 1)
         out = torch.empty((n, oc, hh, ww), dtype=torch.float32, device=dev)
         s1 = s2 = None
-        if self.srcnn_tail is not None:
-            if keep:  # relu(conv1), relu(conv2) for the backward's weight gradients and ReLU masks
-                s1, s2 = _bf16((n, hh, ww, 64), dev), _bf16((n, hh, ww, 32), dev)
-            self.srcnn_tail.fwd(tail, 8, 0, n, hh, ww, out, s1, s2)
+        if self.srcnn_tail is not None:  # (its backward recomputes relu(conv1) / relu(conv2) from `tail`)
+            self.srcnn_tail.fwd(tail, 8, 0, n, hh, ww, out)
         else:
             s1 = _bf16((n, hh, ww, 64), dev)
             P["srcnn.conv1"].fwd(tail, 8, 0, hh, ww, s1, 64, 0, n, act=ACT_RELU)
@@ -300,14 +298,20 @@ class _Engine:
         # backward in its epilogue (no fp32 [N,4H,4W,64] intermediates, no separate act_grad passes)
         dzA = self._scratch("dzA", (n, hh, ww, nf), torch.bfloat16, dev)
         dzB = self._scratch("dzB", (n, hh, ww, nf), torch.bfloat16, dev)
-        dz8 = self._scratch("dz8", (n, hh, ww, 8), torch.bfloat16, dev)
-        dz32 = self._scratch("dz32", (n, hh, ww, 32), torch.bfloat16, dev)
         # ---- SRCNN tail (srcnn.py:13-18)
-        act_grad(npx_hr, 1, gout, 1, 0, None, 0, 0, ACT_NONE, dz8, 8)  # also zeroes dz8's pad channels
-        P["srcnn.conv3"].wgrad(sv["s2"], 32, 0, hh, ww, dz8, 8, n, ws, acc)
-        P["srcnn.conv3"].dgrad(dz8, 8, hh, ww, dz32, 32, 0, n, act=ACT_RELU_BWD, res1=sv["s2"], res1_cs=32, res1_co=0)
-        P["srcnn.conv2"].wgrad(sv["s1"], 64, 0, hh, ww, dz32, 32, n, ws, acc)
-        P["srcnn.conv2"].dgrad(dz32, 32, hh, ww, dzA, nf, 0, n, act=ACT_RELU_BWD, res1=sv["s1"], res1_cs=64, res1_co=0)
+        if self.srcnn_tail is not None:
+            # conv3 / conv2 gradients and dZ1 (into dzA) in one launch that recomputes the forward; dz8's channels 1..7
+            # are never written (zero since allocation): conv1's data gradient below fills channel 0
+            dz8 = self._scratch("dz8", (n, hh, ww, 8), torch.bfloat16, dev, zero=True)
+            self.srcnn_tail.bwd(sv["tail"], 8, 0, n, hh, ww, gout, dzA, ws, acc)
+        else:
+            dz8 = self._scratch("dz8", (n, hh, ww, 8), torch.bfloat16, dev)
+            dz32 = self._scratch("dz32", (n, hh, ww, 32), torch.bfloat16, dev)
+            act_grad(npx_hr, 1, gout, 1, 0, None, 0, 0, ACT_NONE, dz8, 8)  # also zeroes dz8's pad channels
+            P["srcnn.conv3"].wgrad(sv["s2"], 32, 0, hh, ww, dz8, 8, n, ws, acc)
+            P["srcnn.conv3"].dgrad(dz8, 8, hh, ww, dz32, 32, 0, n, act=ACT_RELU_BWD, res1=sv["s2"], res1_cs=32, res1_co=0)
+            P["srcnn.conv2"].wgrad(sv["s1"], 64, 0, hh, ww, dz32, 32, n, ws, acc)
+            P["srcnn.conv2"].dgrad(dz32, 32, hh, ww, dzA, nf, 0, n, act=ACT_RELU_BWD, res1=sv["s1"], res1_cs=64, res1_co=0)
         P["srcnn.conv1"].wgrad(sv["tail"], 8, 0, hh, ww, dzA, 64, n, ws, acc)
         # only d(out) (tail channel 0) is needed; channels 1..7 of dz8 stay 0
         P["srcnn.conv1"].dgrad(dzA, 64, hh, ww, dz8, 8, 0, n, cout_t=1)

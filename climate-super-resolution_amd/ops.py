@@ -471,7 +471,8 @@ class RdbChain:
         flops = sum(2 * self.convs[L].cin_real * 16 * 9 for L in range(4)) * npx
         pull = tag == "pull"
         nbytes = npx * 2 * ((64 + 64 + 64) if pull else (64 + 64)) + sum(w.numel() * 2 for w in (self.w_pull if pull else self.w_fwd))
-        _run(f"rdb_chain_kernel<{1 if pull else 0}>", flops, lambda: check(
+        name = _lib.load().climsr_rdb_chain_kernel(ctypes.byref(d)).decode() if PROFILER is not None else ""
+        _run(name, flops, lambda: check(
             _lib.load().climsr_rdb_chain(ctypes.byref(d), _lib.stream_ptr()), f"rdb chain {self.name}"), tag + " " + self.name,
             nbytes)
 
@@ -533,6 +534,30 @@ class SrcnnTail:
         name = _lib.load().climsr_srcnn_fwd_kernel(ctypes.byref(d)).decode() if PROFILER is not None else ""
         _run(name, flops, lambda: check(_lib.load().climsr_srcnn_fwd(ctypes.byref(d), _lib.stream_ptr()), "srcnn tail"),
              "fwd " + self.name, nbytes)
+
+    def bwd(self, x: torch.Tensor, x_cs: int, x_co: int, n: int, h: int, w: int, gout: torch.Tensor, dz1: torch.Tensor,
+            ws: "Workspace", accumulate: bool) -> None:
+        """Backward below conv1 (csrc/srcnn.hip srcnn_bwd_kernel): recomputes relu(conv1) / relu(conv2) from the input
+        x, writes dz1 = the conv1 output gradient (bf16 NHWC, 64 ch) and the conv2 / conv3 weight + bias gradients
+        (into the plans' bound .gw / .gb, += when accumulate)."""
+        c1, c2, c3 = self.convs
+        assert gout.dtype == torch.float32 and gout.is_contiguous() and gout.numel() == n * h * w
+        assert dz1.dtype == torch.bfloat16 and dz1.is_contiguous() and dz1.numel() == n * h * w * 64
+        for c in (c2, c3):
+            assert c.gw is not None and c.gb is not None, "bind_grads() first"
+        L = _lib.load()
+        part = ws.get((L.climsr_srcnn_bwd_workspace(n, h, w) + 3) // 4, x.device)
+        d = _lib.SrcnnBwdDesc()
+        d.x, d.x_cs, d.x_co, d.gout, d.wpk = ptr(x), x_cs, x_co, ptr(gout), ptr(self.wpk)
+        d.b1, d.b2, d.dz1, d.part = ptr(c1.bias), ptr(c2.bias), ptr(dz1), ptr(part)
+        d.gw2, d.gb2, d.gw3, d.gb3 = ptr(c2.gw), ptr(c2.gb), ptr(c3.gw), ptr(c3.gb)
+        d.accumulate, d.n, d.h, d.w = int(accumulate), n, h, w
+        npx = n * h * w
+        # recompute conv1 + conv2, dA2, dA1, dW2, dW3 (algorithmic, own pixels once)
+        flops = 2 * npx * (c1.cin_real * 81 * 64 + 64 * 32 + 32 * 25 + 32 * 64 + 32 * 64 + 32 * 25)
+        nbytes = npx * (8 + 4 + 128)
+        _run("srcnn_bwd_kernel" if PROFILER is not None else "", flops,
+             lambda: check(L.climsr_srcnn_bwd(ctypes.byref(d), _lib.stream_ptr()), "srcnn tail backward"), "bwd " + self.name, nbytes)
 
 
 class PullPacker:

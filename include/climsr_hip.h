@@ -163,6 +163,9 @@ typedef struct ClimsrChainDesc {
   int32_t n, h, w;
 } ClimsrChainDesc;
 int climsr_rdb_chain(const ClimsrChainDesc* d, void* stream);
+/* rocprof name of the kernel climsr_rdb_chain launches for d (nothing is launched; "" if invalid): widths 16 / 32 / 48 /
+ * 64 run the level-per-wave kernel, any other width the column-windowed one */
+const char* climsr_rdb_chain_kernel(const ClimsrChainDesc* d);
 int climsr_rdb_chain_kp(int level);
 
 /* Implicit-GEMM convolution on MFMA (bf16 in, fp32 accumulate), fused epilogue.
@@ -471,6 +474,28 @@ typedef struct ClimsrSrcnnDesc {
 int climsr_srcnn_fwd(const ClimsrSrcnnDesc* d, void* stream);
 /* rocprof name of the kernel climsr_srcnn_fwd launches for d (nothing is launched) */
 const char* climsr_srcnn_fwd_kernel(const ClimsrSrcnnDesc* d);
+/* Backward of the fused SRCNN tail below conv1, recomputing relu(conv1) / relu(conv2) from x instead of storing them:
+ * gout = dL/d(out) fp32 [n][1][h][w]; writes dz1 = dL/d(conv1 output) bf16 [n][h][w][64] (ReLU' applied: what conv1's
+ * weight / data gradients read) and the conv2 / conv3 weight and bias gradients (fp32, OIHW; accumulate = 1: +=),
+ * summed over climsr_srcnn_bwd_workspace(n, h, w) bytes of per-workgroup partials in a fixed order. */
+typedef struct ClimsrSrcnnBwdDesc {
+  const uint16_t* x;
+  int32_t x_cs, x_co;
+  const float* gout;
+  const uint16_t* wpk;
+  const float* b1;
+  const float* b2;
+  uint16_t* dz1;
+  float* part;
+  float* gw2;
+  float* gb2;
+  float* gw3;
+  float* gb3;
+  int32_t accumulate;
+  int32_t n, h, w;
+} ClimsrSrcnnBwdDesc;
+int climsr_srcnn_bwd(const ClimsrSrcnnBwdDesc* d, void* stream);
+int64_t climsr_srcnn_bwd_workspace(int n, int h, int w);
 /* Pack the three SRCNN weights (fp32 OIHW: w1 [64][in_c][9][9], w2 [32][64][1][1], w3 [1][32][5][5]) into the MFMA
  * fragment order climsr_srcnn_fwd reads (async on stream; run after every weight update). */
 int climsr_srcnn_pack(const float* w1, const float* w2, const float* w3, int in_c, uint16_t* out, void* stream);

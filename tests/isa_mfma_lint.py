@@ -16,12 +16,14 @@ BRANCH_C = ("s_cbranch_scc0", "s_cbranch_scc1", "s_cbranch_vccz", "s_cbranch_vcc
 
 
 def vregs(tok):
-    m = re.fullmatch(r"v(\d+)", tok)
+    """Vector registers of an operand: VGPR n -> n, AGPR n -> 1000 + n (an asm MFMA may accumulate in either half)."""
+    m = re.fullmatch(r"([va])(\d+)", tok)
     if m:
-        return {int(m.group(1))}
-    m = re.fullmatch(r"v\[(\d+):(\d+)\]", tok)
+        return {int(m.group(2)) + (1000 if m.group(1) == "a" else 0)}
+    m = re.fullmatch(r"([va])\[(\d+):(\d+)\]", tok)
     if m:
-        return set(range(int(m.group(1)), int(m.group(2)) + 1))
+        base = 1000 if m.group(1) == "a" else 0
+        return set(range(int(m.group(2)) + base, int(m.group(3)) + base + 1))
     return set()
 
 

@@ -720,3 +720,54 @@ def test_srcnn_tail_matches_fp64(n, h, w, keep):
     tail.fwd(xin, 8, 0, n, h, w, out2)
     torch.cuda.synchronize()
     assert torch.equal(out, out2)
+
+
+@pytest.mark.parametrize("n,h,w", [(2, 32, 32), (1, 45, 70), (3, 20, 100), (1, 5, 7)])
+def test_srcnn_tail_backward_matches_fp64(n, h, w):
+    """The fused SRCNN tail backward (csrc/srcnn.hip srcnn_bwd_kernel: recomputes relu(conv1) / relu(conv2), then
+    dZ2 = conv3^T(g) * relu', dZ1 = conv2^T(dZ2) * relu', and the conv2 / conv3 weight + bias gradients) vs fp64 torch
+    autograd on the same bf16 operands, with the intermediates rounded to bf16 where the kernel keeps them in bf16
+    (relu(conv1), relu(conv2), g, dZ2).  Accumulation into existing gradients, ragged tiles, tiny images."""
+    from climsr_amd import ops
+
+    p1, w1, b1 = make_plan(3, 64, 9, seed=51)
+    p2, w2, b2 = make_plan(64, 32, 1, seed=52)
+    p3, w3, b3 = make_plan(32, 1, 5, seed=53)
+    for p in (p2, p3):
+        p.gw = torch.full(tuple(p.weight.shape), 0.5, device=DEV)
+        p.gb = torch.full(tuple(p.bias.shape), 0.25, device=DEV)
+    tail = ops.SrcnnTail([p1, p2, p3])
+    tail.pack()
+    g = torch.Generator().manual_seed(54)
+    x = bf(torch.rand((n, 3, h, w), generator=g) * 2 - 1)
+    gout = torch.randn((n, 1, h, w), generator=g)
+    xin = torch.full((n, h, w, 8), 5.0, dtype=torch.bfloat16, device=DEV)
+    xin[..., :3] = x.permute(0, 2, 3, 1).to(DEV).to(torch.bfloat16)
+    dz1 = torch.full((n, h, w, 64), 7.0, dtype=torch.bfloat16, device=DEV)
+    names = []
+    ops.PROFILER = lambda name, flops, fn, tag="", nbytes=0: (names.append(name), fn())
+    try:
+        tail.bwd(xin, 8, 0, n, h, w, gout.to(DEV).contiguous(), dz1, ops.Workspace(), accumulate=True)
+    finally:
+        ops.PROFILER = None
+    torch.cuda.synchronize()
+    assert names == ["srcnn_bwd_kernel"], names
+    d = torch.float64
+    a1b = F.relu(F.conv2d(x.double(), bf(w1).double(), b1.double(), padding=4)).to(torch.bfloat16).to(d)
+    a2b = F.relu(F.conv2d(a1b, bf(w2).double(), b2.double())).to(torch.bfloat16).to(d)
+    gb = bf(gout).double()
+    a2v = a2b.clone().requires_grad_()
+    w3v = bf(w3).double().requires_grad_()
+    F.conv2d(a2v, w3v, b3.double(), padding=2).backward(gb)
+    dz2b = (a2v.grad * (a2b > 0)).to(torch.bfloat16).to(d)
+    a1v = a1b.clone().requires_grad_()
+    w2v = bf(w2).double().requires_grad_()
+    F.conv2d(a1v, w2v, b2.double()).backward(dz2b)
+    dz1_ref = a1v.grad * (a1b > 0)
+    got = dz1.permute(0, 3, 1, 2).double().cpu()
+    err = float((got - dz1_ref).abs().max())
+    assert err <= 2 ** -7 * float(dz1_ref.abs().max()) + 1e-6, f"dZ1: err {err:.3e} vs {float(dz1_ref.abs().max()):.3e}"
+    check_close(p2.gw.cpu() - 0.5, w2v.grad, 2e-3, "dW2")
+    check_close(p2.gb.cpu() - 0.25, dz2b.sum((0, 2, 3)), 2e-3, "db2")
+    check_close(p3.gw.cpu() - 0.5, w3v.grad, 2e-3, "dW3")
+    check_close(p3.gb.cpu() - 0.25, gb.sum().reshape(1), 2e-3, "db3")

@@ -7,3 +7,4 @@ timeout -k 10 500 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 20 --warmup 5 > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err || exit $?
 timeout -k 10 300 python -u bench.py --mode infer --model esrgan --no-cpu-baseline > gpurun_out/${T}_infer_esrgan.json 2> gpurun_out/${T}_infer.err || exit $?
 timeout -k 10 300 python -u bench.py --mode infer --model rcan --no-cpu-baseline > gpurun_out/${T}_infer_rcan.json 2>> gpurun_out/${T}_infer.err || exit $?
+bash tools/gpu_chain_prof.sh ${T}_ch || exit $?
