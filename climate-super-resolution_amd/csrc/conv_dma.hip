@@ -94,6 +94,9 @@ __device__ __forceinline__ void dma_store_half(const FwdArgs& a, const float* eb
   }
 }
 
+#ifndef CLIMSR_DMA_DIRECT
+#define CLIMSR_DMA_DIRECT 0  // A/B build switch: 1 = EP 3 / 6 / 8 store straight from the accumulators (no LDS staging)
+#endif
 #ifndef CLIMSR_DMA_SPREAD
 #define CLIMSR_DMA_SPREAD 1  // DMA pieces per k-step: 1 (k-steps 0..8, two at the last) or 2 (k-steps 0..4)
 #endif
@@ -114,6 +117,9 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
   constexpr bool BN = EP == 9 || EP == 10;
   // epilogues with a fixed store count per lane (dma_store_half), so the wait for the next item's chunk 0 skips them
   constexpr bool CNT = EP == 1 || EP == 2 || EP == 3 || EP == 6 || EP == 7 || EP == 8;
+  // EP 3 / 6 / 8 with CLIMSR_DMA_DIRECT: the epilogue stores from the accumulators (16 stores per lane and item)
+  constexpr bool DIRECT = CLIMSR_DMA_DIRECT && (EP == 3 || EP == 6 || EP == 8);
+  constexpr int NST_ITEM = DIRECT ? 16 : 2 * DmaEp<CNT ? EP : 8>::NSTORE;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
   const int wvu = __builtin_amdgcn_readfirstlane(wave);
   const int ntile = a.tiles_x * a.tiles_y * a.n, ncob = (a.out_c + 63) / 64;  // = the host's packed-row blocks
@@ -207,7 +213,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
       // wait also drains the previous item's epilogue stores (issued after the DMAs of this chunk)
       if (CNT && j == 0 && v != (int)blockIdx.x) {
         // chunk 0 of a later item: only its DMAs, not the previous item's epilogue stores issued after them
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DmaEp<CNT ? EP : 8>::NSTORE) : "memory");
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST_ITEM) : "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
@@ -260,7 +266,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
     }
     // epilogue through the buffer just computed (buf ^ 1 after the loop's last flip); LDS-only barriers, so the
     // stores stay in flight
-    lds_barrier();  // every wave's fragment reads of it are done
+    if (!DIRECT) lds_barrier();  // every wave's fragment reads of it are done
     if constexpr (BN) {
       float* eb = (float*)smem + wave * (64 * DMA_EPP);  // the whole tile (aliases both buffers: no DMA in flight)
 #pragma unroll
@@ -302,6 +308,34 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
         out[a.out_c + co0 + lane] = (double)tq;
       }
       return;
+    } else if (DIRECT) {
+      // lane (col, g) holds channels co0 + 16 t + 4 g .. + 3 of pixel (oy0 + 4 wave + m, ox0 + col): bias / activation,
+      // bf16, one 8 B store per (m, t) -- 16 per lane per item, issued unconditionally (out-of-range offsets drop)
+      const __amdgpu_buffer_rsrc_t ry = buf_rsrc(a.y, (uint32_t)((long)a.n * a.out_h * a.out_w * a.out_cs * 2));
+      float bb[4][4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float4 b4 = EP == 3 ? *(const float4*)(a.bias + co0 + 16 * t + 4 * g) : make_float4(0.f, 0.f, 0.f, 0.f);
+        bb[t][0] = b4.x; bb[t][1] = b4.y; bb[t][2] = b4.z; bb[t][3] = b4.w;
+      }
+      const int ox = ox0 + col, act = EP == 8 ? 0 : a.act;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int oy = oy0 + wave * 4 + m;
+        const bool ok = oy < a.out_h && ox < a.out_w;
+        const long pix = ((long)nimg * a.out_h + oy) * a.out_w + ox;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          float v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = act_apply(acc[m][t][i] + bb[t][i], act, a.slope);
+          const bf16x2 p0 = {(__bf16)v[0], (__bf16)v[1]}, p1 = {(__bf16)v[2], (__bf16)v[3]};
+          typedef uint32_t v2u32_t __attribute__((ext_vector_type(2)));
+          const v2u32_t pk = {__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1)};
+          const uint32_t off = ok ? (uint32_t)((pix * a.out_cs + a.out_co + co0 + 16 * t + 4 * g) * 2) : BUF_OOB;
+          __builtin_amdgcn_raw_buffer_store_b64(pk, ry, off, 0, 0);
+        }
+      }
     } else {
       constexpr int EPH = 32 + 4;  // staged pitch (floats) of one 32-channel half
       float* eb = (float*)(smem + (buf ^ 1) * DMA_BUF) + wave * (64 * EPH);

@@ -11,7 +11,7 @@ import torch  # noqa: E402
 import climsr_amd  # noqa: E402,F401
 from climsr_amd import _lib  # noqa: E402
 from climsr_amd.ops import ACT_LRELU, OUT_F32, BatchedPacker, ConvPlan, RdbChain, Workspace  # noqa: E402
-from tests.perf_conv_timing import timeit  # noqa: E402
+from tools.perf_conv_timing import timeit  # noqa: E402
 
 dev, n, dc = "cuda", 32, 128
 res = {"label": sys.argv[1] if len(sys.argv) > 1 else "", "lib": _lib.LIB_PATH}
