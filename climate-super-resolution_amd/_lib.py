@@ -72,8 +72,8 @@ class PullPackDesc(ctypes.Structure):
 
 class SrcnnDesc(ctypes.Structure):
     _fields_ = [("x", c_void_p), ("x_cs", ctypes.c_int32), ("x_co", ctypes.c_int32), ("wpk", c_void_p), ("b1", c_void_p),
-                ("b2", c_void_p), ("b3", c_void_p), ("out", c_void_p), ("s1", c_void_p), ("s2", c_void_p),
-                ("n", ctypes.c_int32), ("h", ctypes.c_int32), ("w", ctypes.c_int32)]
+                ("b2", c_void_p), ("b3", c_void_p), ("out", c_void_p), ("n", ctypes.c_int32), ("h", ctypes.c_int32),
+                ("w", ctypes.c_int32)]
 
 
 class SrcnnBwdDesc(ctypes.Structure):
@@ -116,7 +116,6 @@ SIGNATURES = {
     "climsr_rdb_chain_kernel": (ctypes.c_char_p, [P(ChainDesc)]),
     "climsr_rdb_chain_kp": (c_int, [c_int]),
     "climsr_srcnn_fwd": (c_int, [P(SrcnnDesc), c_void_p]),
-    "climsr_srcnn_fwd_kernel": (ctypes.c_char_p, [P(SrcnnDesc)]),
     "climsr_srcnn_pack": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "climsr_srcnn_packed_elems": (c_int64, []),
     "climsr_srcnn_bwd": (c_int, [P(SrcnnBwdDesc), c_void_p]),

@@ -18,8 +18,7 @@
 // The 44 weight fragments of conv1 (plus conv2's and Q's 6) stay in AGPRs for the launch (mfma_agpr.h).
 // LDS: Q 25 x 1300 floats (pitch 1300: the 4 lane groups' tap rows land 16 banks apart) + the footprint.  The next
 // tile's footprint is fetched into registers while the current tile computes.
-// keep (training): the tile's own pixels of relu(conv1) and relu(conv2) are also stored (bf16 NHWC, 64 / 32 channels)
-// for the backward's weight gradients and ReLU masks.
+// Nothing else is stored: the backward (srcnn_bwd_kernel below) recomputes relu(conv1) / relu(conv2).
 #include <algorithm>
 #include <stdio.h>
 
@@ -50,11 +49,9 @@ struct SrcnnArgs {
   const uint16_t* wpk;    // NFRAG_ALL x 64 lanes x 8 bf16
   const float *b1, *b2, *b3;
   float* out;             // fp32 [n][h][w] (= NCHW with one channel)
-  uint16_t* s1;           // keep: relu(conv1) bf16 [n][h][w][64]
-  uint16_t* s2;           // keep: relu(conv2) bf16 [n][h][w][32]
   int n, h, w, x_cs, x_co;
   int tiles_x, tiles_y, ntiles;
-  uint32_t x_bytes, out_bytes, s1_bytes, s2_bytes;
+  uint32_t x_bytes, out_bytes;
 };
 
 typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
@@ -68,7 +65,6 @@ __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, p);
 }
 
-template <bool KEEP>
 __global__ __launch_bounds__(256, 1) void srcnn_tail_kernel(SrcnnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* q = (float*)smem;
@@ -116,8 +112,6 @@ __global__ __launch_bounds__(256, 1) void srcnn_tail_kernel(SrcnnArgs a) {
 
   const __amdgpu_buffer_rsrc_t xr = buf_rsrc(a.x, a.x_bytes);
   const __amdgpu_buffer_rsrc_t orr = buf_rsrc(a.out, a.out_bytes);
-  const __amdgpu_buffer_rsrc_t s1r = buf_rsrc(a.s1, KEEP ? a.s1_bytes : 0u);
-  const __amdgpu_buffer_rsrc_t s2r = buf_rsrc(a.s2, KEEP ? a.s2_bytes : 0u);
   auto decode = [&](int tile, int& nimg, int& oy0, int& ox0) {
     const int tx = tile % a.tiles_x, r = tile / a.tiles_x, ty = r % a.tiles_y;
     nimg = r / a.tiles_y;
@@ -154,34 +148,14 @@ __global__ __launch_bounds__(256, 1) void srcnn_tail_kernel(SrcnnArgs a) {
     int nimg, oy0, ox0;
     decode(T, nimg, oy0, ox0);
 
-    for (int gi = wv; gi < SG; gi += 4) {
+    // groups in pairs (gi, gi + 4): the two groups' conv1 chains interleave, so each k block's two B reads are covered
+    // by eight MFMAs (one wave per SIMD: nothing else hides the LDS latency); a wave's odd last group pairs with itself
+    auto finish = [&](int gi, f32x4 (&c1)[4]) {
       const int gy = gi / SGX, gx = gi - gy * SGX;
       const int ry = 4 * gy + (col >> 2), rx = 4 * gx + (col & 3);
-      const char* xb = xin + (ry * SI + rx) * 8;
-      // ---- conv1: 4 co blocks x 11 k blocks, B double-buffered one k block ahead
-      f32x4 c1[4];
-      bf16x8 bq[2];
-      auto ldb = [&](int s, int buf) {
-        const v2u32 lo = *(const v2u32*)(xb + toff[s][0]);
-        const v2u32 hi = *(const v2u32*)(xb + toff[s][1]);
-        const uint32_t u[4] = {lo[0], lo[1], hi[0], hi[1]};
-        bq[buf] = __builtin_bit_cast(bf16x8, u);
-      };
-      ldb(0, 0);
-#pragma unroll
-      for (int s = 0; s < NK1; ++s) {
-        if (s + 1 < NK1) ldb(s + 1, (s + 1) & 1);
-        __builtin_amdgcn_sched_barrier(0);
-        if (s == 0) mfma4x_agpr<true, false>(c1[0], c1[1], c1[2], c1[3], a1[0][s], a1[1][s], a1[2][s], a1[3][s], bq[0]);
-        else mfma4x_agpr<false, false>(c1[0], c1[1], c1[2], c1[3], a1[0][s], a1[1][s], a1[2][s], a1[3][s], bq[s & 1]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      pad_mfma(c1);
       // ---- bias + ReLU -> conv2's B fragments (k block s2: co blocks 2 s2, 2 s2 + 1)
       const int yy = oy0 - 2 + ry, xx = ox0 - 2 + rx;
       const bool inimg = yy >= 0 && yy < a.h && xx >= 0 && xx < a.w;
-      const bool own = inimg && ry >= 2 && ry < 2 + ST && rx >= 2 && rx < 2 + ST;
-      const long pix = ((long)nimg * a.h + yy) * a.w + xx;
       uint32_t u1[4][2];
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
@@ -190,10 +164,6 @@ __global__ __launch_bounds__(256, 1) void srcnn_tail_kernel(SrcnnArgs a) {
         for (int i = 0; i < 4; ++i) v[i] = fmaxf(c1[b][i] + bias1[b][i], 0.f);
         u1[b][0] = pack2(v[0], v[1]);
         u1[b][1] = pack2(v[2], v[3]);
-        if constexpr (KEEP) {
-          const v2u32 pk = {u1[b][0], u1[b][1]};
-          __builtin_amdgcn_raw_buffer_store_b64(pk, s1r, own ? (uint32_t)((pix * 64 + 16 * b + 4 * g) * 2) : BUF_OOB, 0, 0);
-        }
       }
       bf16x8 b2f[2];
 #pragma unroll
@@ -214,10 +184,6 @@ __global__ __launch_bounds__(256, 1) void srcnn_tail_kernel(SrcnnArgs a) {
         for (int i = 0; i < 4; ++i) v[i] = fmaxf(c2[b][i] + bias2[b][i], 0.f);
         u2[b][0] = pack2(v[0], v[1]);
         u2[b][1] = pack2(v[2], v[3]);
-        if constexpr (KEEP) {
-          const v2u32 pk = {u2[b][0], u2[b][1]};
-          __builtin_amdgcn_raw_buffer_store_b64(pk, s2r, own ? (uint32_t)((pix * 32 + 16 * b + 4 * g) * 2) : BUF_OOB, 0, 0);
-        }
       }
       const uint32_t uq[4] = {u2[0][0], u2[0][1], u2[1][0], u2[1][1]};
       const bf16x8 bqf = __builtin_bit_cast(bf16x8, uq);
@@ -233,6 +199,42 @@ __global__ __launch_bounds__(256, 1) void srcnn_tail_kernel(SrcnnArgs a) {
           const int tap = 16 * b + 4 * g + i;
           if (tap < NTAP3) q[tap * QP + p] = inimg ? cq[b][i] : 0.f;
         }
+    };
+    for (int ga = wv; ga < SG; ga += 8) {
+      const int gb = ga + 4 < SG ? ga + 4 : ga;
+      const char* xa = xin + ((4 * (ga / SGX) + (col >> 2)) * SI + 4 * (ga % SGX) + (col & 3)) * 8;
+      const char* xq = xin + ((4 * (gb / SGX) + (col >> 2)) * SI + 4 * (gb % SGX) + (col & 3)) * 8;
+      // ---- conv1 of both groups: 4 co blocks x 11 k blocks each, B double-buffered one k block ahead
+      f32x4 ca[4], cb[4];
+      bf16x8 ba[2], bb[2];
+      auto ldb = [&](const char* xb, int s) {
+        const v2u32 lo = *(const v2u32*)(xb + toff[s][0]);
+        const v2u32 hi = *(const v2u32*)(xb + toff[s][1]);
+        const uint32_t u[4] = {lo[0], lo[1], hi[0], hi[1]};
+        return __builtin_bit_cast(bf16x8, u);
+      };
+      ba[0] = ldb(xa, 0);
+      bb[0] = ldb(xq, 0);
+#pragma unroll
+      for (int s = 0; s < NK1; ++s) {
+        if (s + 1 < NK1) {
+          ba[(s + 1) & 1] = ldb(xa, s + 1);
+          bb[(s + 1) & 1] = ldb(xq, s + 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (s == 0) {
+          mfma4x_agpr<true, false>(ca[0], ca[1], ca[2], ca[3], a1[0][s], a1[1][s], a1[2][s], a1[3][s], ba[0]);
+          mfma4x_agpr<true, false>(cb[0], cb[1], cb[2], cb[3], a1[0][s], a1[1][s], a1[2][s], a1[3][s], bb[0]);
+        } else {
+          mfma4x_agpr<false, false>(ca[0], ca[1], ca[2], ca[3], a1[0][s], a1[1][s], a1[2][s], a1[3][s], ba[s & 1]);
+          mfma4x_agpr<false, false>(cb[0], cb[1], cb[2], cb[3], a1[0][s], a1[1][s], a1[2][s], a1[3][s], bb[s & 1]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      pad_mfma(ca);
+      pad_mfma(cb);
+      finish(ga, ca);
+      if (gb != ga) finish(gb, cb);
     }
     lds_barrier();  // Q complete (and every footprint read done)
     // ---- conv3: out(oy, ox) = b3 + sum over taps (ky, kx) of Q[tap][(oy + ky, ox + kx)], fixed order
@@ -461,35 +463,50 @@ __global__ __launch_bounds__(256, 1) void srcnn_bwd_kernel(SrcnnBwdArgs a) {
         const int gi = wv + 4 * (pr + ps);
         gyp[ps] = gi / BGX;
         gxp[ps] = gi - gyp[ps] * BGX;
+      }
+      // ---- recompute conv1 at both groups' pixels, the two chains interleaved (8 MFMAs cover each k block's reads)
+      int g2 = 2 * g;
+      asm volatile("" : "+v"(g2));
+      auto toff = [&](int s, int hh) {  // footprint offset of tap 8 s + 2 g + hh (taps past 80 read tap 80)
+        const int t = min(8 * s + g2 + hh, 80), ky = (t * 57) >> 9;  // t / 9 for t < 128
+        return (ky * (BI - 9) + t) * 8;
+      };
+      const char* xa = xin + ((4 * gyp[0] + q4) * BI + 4 * gxp[0] + p4) * 8;
+      const char* xq = xin + ((4 * gyp[1] + q4) * BI + 4 * gxp[1] + p4) * 8;
+      auto ldb = [&](const char* xb, int s) {
+        const v2u32 lo = *(const v2u32*)(xb + toff(s, 0));
+        const v2u32 hi = *(const v2u32*)(xb + toff(s, 1));
+        const uint32_t u[4] = {lo[0], lo[1], hi[0], hi[1]};
+        return __builtin_bit_cast(bf16x8, u);
+      };
+      f32x4 c1p[2][4];
+      bf16x8 ba[2], bb[2];
+      ba[0] = ldb(xa, 0);
+      bb[0] = ldb(xq, 0);
+#pragma unroll
+      for (int s = 0; s < NK1; ++s) {
+        if (s + 1 < NK1) {
+          ba[(s + 1) & 1] = ldb(xa, s + 1);
+          bb[(s + 1) & 1] = ldb(xq, s + 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (s == 0) {
+          mfma4x_agpr<true, false>(c1p[0][0], c1p[0][1], c1p[0][2], c1p[0][3], a1[0][s], a1[1][s], a1[2][s], a1[3][s], ba[0]);
+          mfma4x_agpr<true, false>(c1p[1][0], c1p[1][1], c1p[1][2], c1p[1][3], a1[0][s], a1[1][s], a1[2][s], a1[3][s], bb[0]);
+        } else {
+          mfma4x_agpr<false, false>(c1p[0][0], c1p[0][1], c1p[0][2], c1p[0][3], a1[0][s], a1[1][s], a1[2][s], a1[3][s], ba[s & 1]);
+          mfma4x_agpr<false, false>(c1p[1][0], c1p[1][1], c1p[1][2], c1p[1][3], a1[0][s], a1[1][s], a1[2][s], a1[3][s], bb[s & 1]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      pad_mfma(c1p[0]);
+      pad_mfma(c1p[1]);
+#pragma unroll
+      for (int ps = 0; ps < 2; ++ps) {
         const int ry = 4 * gyp[ps] + q4, rx = 4 * gxp[ps] + p4;
         const int yy = oy0 + ry, xx = ox0 + rx;
         const bool inimg = yy < a.h && xx < a.w;
-        // ---- recompute conv1 / conv2 at the group's pixels
-        const char* xb = xin + (ry * BI + rx) * 8;
-        int g2 = 2 * g;
-        asm volatile("" : "+v"(g2));
-        auto toff = [&](int s, int hh) {  // footprint offset of tap 8 s + 2 g + hh (taps past 80 read tap 80)
-          const int t = min(8 * s + g2 + hh, 80), ky = (t * 57) >> 9;  // t / 9 for t < 128
-          return (ky * (BI - 9) + t) * 8;
-        };
-        f32x4 c1[4];
-        bf16x8 bq[2];
-        auto ldb = [&](int s, int buf) {
-          const v2u32 lo = *(const v2u32*)(xb + toff(s, 0));
-          const v2u32 hi = *(const v2u32*)(xb + toff(s, 1));
-          const uint32_t u[4] = {lo[0], lo[1], hi[0], hi[1]};
-          bq[buf] = __builtin_bit_cast(bf16x8, u);
-        };
-        ldb(0, 0);
-#pragma unroll
-        for (int s = 0; s < NK1; ++s) {
-          if (s + 1 < NK1) ldb(s + 1, (s + 1) & 1);
-          __builtin_amdgcn_sched_barrier(0);
-          if (s == 0) mfma4x_agpr<true, false>(c1[0], c1[1], c1[2], c1[3], a1[0][s], a1[1][s], a1[2][s], a1[3][s], bq[0]);
-          else mfma4x_agpr<false, false>(c1[0], c1[1], c1[2], c1[3], a1[0][s], a1[1][s], a1[2][s], a1[3][s], bq[s & 1]);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        pad_mfma(c1);
+        f32x4 (&c1)[4] = c1p[ps];
         uint32_t u1[4][2];
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
@@ -674,20 +691,15 @@ extern "C" int climsr_srcnn_pack(const float* w1, const float* w2, const float* 
   return check_launch("srcnn_pack");
 }
 
-extern "C" const char* climsr_srcnn_fwd_kernel(const ClimsrSrcnnDesc* d) {
-  if (!d) return "";
-  return d->s1 ? "srcnn_tail_kernel<true>" : "srcnn_tail_kernel<false>";
-}
-
 extern "C" int climsr_srcnn_fwd(const ClimsrSrcnnDesc* d, void* stream) {
   if (!d || !d->x || !d->wpk || !d->b1 || !d->b2 || !d->b3 || !d->out || d->n <= 0 || d->h <= 0 || d->w <= 0 ||
-      d->x_cs % 4 || d->x_co % 4 || d->x_co + 4 > d->x_cs || (!d->s1) != (!d->s2)) {
-    set_error("srcnn_fwd: bad args (x channel stride / offset multiples of 4, offset + 4 <= stride; s1, s2 both or neither)");
+      d->x_cs % 4 || d->x_co % 4 || d->x_co + 4 > d->x_cs) {
+    set_error("srcnn_fwd: bad args (x channel stride / offset multiples of 4, offset + 4 <= stride)");
     return CLIMSR_EINVAL;
   }
   const long npx = (long)d->n * d->h * d->w;
-  const long xb = npx * d->x_cs * 2, s1b = d->s1 ? npx * 128 : 0;
-  if (xb >= (1L << 31) || s1b >= (1L << 31)) {
+  const long xb = npx * d->x_cs * 2;
+  if (xb >= (1L << 31)) {
     set_error("srcnn_fwd: buffers past 2 GiB (32-bit buffer offsets)");
     return CLIMSR_EINVAL;
   }
@@ -698,8 +710,6 @@ extern "C" int climsr_srcnn_fwd(const ClimsrSrcnnDesc* d, void* stream) {
   a.b2 = d->b2;
   a.b3 = d->b3;
   a.out = d->out;
-  a.s1 = d->s1;
-  a.s2 = d->s2;
   a.n = d->n;
   a.h = d->h;
   a.w = d->w;
@@ -710,16 +720,9 @@ extern "C" int climsr_srcnn_fwd(const ClimsrSrcnnDesc* d, void* stream) {
   a.ntiles = a.tiles_x * a.tiles_y * d->n;
   a.x_bytes = (uint32_t)xb;
   a.out_bytes = (uint32_t)(npx * 4);
-  a.s1_bytes = (uint32_t)s1b;
-  a.s2_bytes = (uint32_t)(s1b / 2);
   const int grid = std::min(a.ntiles, device_cus());
-  if (d->s1) {
-    if (int e = lds_opt_in((const void*)srcnn_tail_kernel<true>, S_LDS)) return e;
-    hipLaunchKernelGGL(srcnn_tail_kernel<true>, dim3(grid), dim3(256), S_LDS, (hipStream_t)stream, a);
-  } else {
-    if (int e = lds_opt_in((const void*)srcnn_tail_kernel<false>, S_LDS)) return e;
-    hipLaunchKernelGGL(srcnn_tail_kernel<false>, dim3(grid), dim3(256), S_LDS, (hipStream_t)stream, a);
-  }
+  if (int e = lds_opt_in((const void*)srcnn_tail_kernel, S_LDS)) return e;
+  hipLaunchKernelGGL(srcnn_tail_kernel, dim3(grid), dim3(256), S_LDS, (hipStream_t)stream, a);
   return check_launch("srcnn_fwd");
 }
 

@@ -502,7 +502,7 @@ class RdbChain:
 class SrcnnTail:
     """srcnn.conv1 -> ReLU -> conv2 -> ReLU -> conv3 (srcnn.py:9-18) of the generator tail as ONE launch
     (csrc/srcnn.hip): reads the 4-channel bf16 cat[out, elev, mask] input, writes the fp32 output; the 64- / 32-channel
-    intermediates are stored only for a training forward (``s1``/``s2``).  ``convs``: the three bound ConvPlans."""
+    intermediates never leave the chip (the backward recomputes them).  ``convs``: the three bound ConvPlans."""
 
     def __init__(self, convs, name: str = "srcnn"):
         self.convs, self.name = convs, name
@@ -516,24 +516,18 @@ class SrcnnTail:
         _launch("srcnn pack", lambda: _lib.load().climsr_srcnn_pack(ptr(c1.weight), ptr(c2.weight), ptr(c3.weight), c1.cin_real,
                                                                     ptr(self.wpk), _lib.stream_ptr()))
 
-    def fwd(self, x: torch.Tensor, x_cs: int, x_co: int, n: int, h: int, w: int, out: torch.Tensor,
-            s1: Optional[torch.Tensor] = None, s2: Optional[torch.Tensor] = None) -> None:
+    def fwd(self, x: torch.Tensor, x_cs: int, x_co: int, n: int, h: int, w: int, out: torch.Tensor) -> None:
         c1, c2, c3 = self.convs
         assert out.dtype == torch.float32 and out.is_contiguous() and out.numel() == n * h * w
         assert x.dtype == torch.bfloat16 and x.is_contiguous() and x.numel() == n * h * w * x_cs
-        if s1 is not None:
-            assert s1.dtype == torch.bfloat16 and s1.numel() == n * h * w * 64 and s1.is_contiguous()
-            assert s2.dtype == torch.bfloat16 and s2.numel() == n * h * w * 32 and s2.is_contiguous()
         d = _lib.SrcnnDesc()
         d.x, d.x_cs, d.x_co, d.wpk = ptr(x), x_cs, x_co, ptr(self.wpk)
         d.b1, d.b2, d.b3, d.out = ptr(c1.bias), ptr(c2.bias), ptr(c3.bias), ptr(out)
-        d.s1, d.s2, d.n, d.h, d.w = ptr(s1), ptr(s2), n, h, w
+        d.n, d.h, d.w = n, h, w
         npx = n * h * w
         flops = 2 * npx * (c1.cin_real * 81 * 64 + 64 * 32 + 32 * 25)
-        nbytes = npx * (8 + 4 + (192 if s1 is not None else 0))
-        name = _lib.load().climsr_srcnn_fwd_kernel(ctypes.byref(d)).decode() if PROFILER is not None else ""
-        _run(name, flops, lambda: check(_lib.load().climsr_srcnn_fwd(ctypes.byref(d), _lib.stream_ptr()), "srcnn tail"),
-             "fwd " + self.name, nbytes)
+        _run("srcnn_tail_kernel" if PROFILER is not None else "", flops,
+             lambda: check(_lib.load().climsr_srcnn_fwd(ctypes.byref(d), _lib.stream_ptr()), "srcnn tail"), "fwd " + self.name, npx * 12)
 
     def bwd(self, x: torch.Tensor, x_cs: int, x_co: int, n: int, h: int, w: int, gout: torch.Tensor, dz1: torch.Tensor,
             ws: "Workspace", accumulate: bool) -> None:

@@ -456,9 +456,9 @@ int climsr_ca_scale_add(const float* u, int u_cstride, const float* s, float* xr
                         int64_t hw, int c, void* stream);
 /* The SRCNN tail of the ESRGAN generator as ONE launch, replacing srcnn.conv1 -> ReLU -> conv2 -> ReLU -> conv3
  * (srcnn.py:9-18) on torch.cat([out, elev, mask], 1) (esrgan.py:99-100): x = bf16 NHWC, channels x_co .. x_co+3 (the
- * in_c <= 4 real ones + zeros); out = fp32 [n][1][h][w]; the 64- and 32-channel intermediates stay on chip unless s1
- * and s2 are given (training: relu(conv1) bf16 [n][h][w][64], relu(conv2) bf16 [n][h][w][32] for the backward).
- * wpk = climsr_srcnn_packed_elems() bf16 from climsr_srcnn_pack; b1/b2/b3 = the fp32 biases (64 / 32 / 1). */
+ * in_c <= 4 real ones + zeros); out = fp32 [n][1][h][w]; the 64- and 32-channel intermediates stay on chip (the
+ * backward, climsr_srcnn_bwd, recomputes them).  wpk = climsr_srcnn_packed_elems() bf16 from climsr_srcnn_pack;
+ * b1/b2/b3 = the fp32 biases (64 / 32 / 1). */
 typedef struct ClimsrSrcnnDesc {
   const uint16_t* x;
   int32_t x_cs, x_co;
@@ -467,13 +467,9 @@ typedef struct ClimsrSrcnnDesc {
   const float* b2;
   const float* b3;
   float* out;
-  uint16_t* s1;
-  uint16_t* s2;
   int32_t n, h, w;
 } ClimsrSrcnnDesc;
 int climsr_srcnn_fwd(const ClimsrSrcnnDesc* d, void* stream);
-/* rocprof name of the kernel climsr_srcnn_fwd launches for d (nothing is launched) */
-const char* climsr_srcnn_fwd_kernel(const ClimsrSrcnnDesc* d);
 /* Backward of the fused SRCNN tail below conv1, recomputing relu(conv1) / relu(conv2) from x instead of storing them:
  * gout = dL/d(out) fp32 [n][1][h][w]; writes dz1 = dL/d(conv1 output) bf16 [n][h][w][64] (ReLU' applied: what conv1's
  * weight / data gradients read) and the conv2 / conv3 weight and bias gradients (fp32, OIHW; accumulate = 1: +=),

@@ -675,13 +675,12 @@ def test_conv_wr_fp32_out_channel_sums(n, h, w):
     check_close(sums, y.double().cpu().sum((1, 2)), 1e-5, "channel sums")
 
 
-@pytest.mark.parametrize("n,h,w,keep", [(2, 32, 32, True), (1, 45, 70, True), (3, 20, 100, False), (1, 5, 7, True),
-                                        (2, 64, 96, False)])
-def test_srcnn_tail_matches_fp64(n, h, w, keep):
+@pytest.mark.parametrize("n,h,w", [(2, 32, 32), (1, 45, 70), (3, 20, 100), (1, 5, 7), (2, 64, 96), (1, 37, 36)])
+def test_srcnn_tail_matches_fp64(n, h, w):
     """The fused SRCNN tail (csrc/srcnn.hip: conv1 9x9 -> ReLU -> conv2 1x1 -> ReLU -> conv3 5x5 in one launch,
     srcnn.py:9-18) vs fp64 torch on the same bf16 input and weights, with the two intermediates rounded to bf16 as the
-    kernel keeps them; ragged tiles, images smaller than a tile, and the stored intermediates of a training forward.
-    Input channels past the three real ones hold garbage (their weights are zero)."""
+    kernel keeps them; ragged tiles, images smaller than a tile, odd group counts per wave.  Input channels past the
+    three real ones hold garbage (their weights are zero).  Reruns are bit-identical."""
     from climsr_amd import ops
 
     p1, w1, b1 = make_plan(3, 64, 9, seed=41)
@@ -694,28 +693,18 @@ def test_srcnn_tail_matches_fp64(n, h, w, keep):
     xin = torch.full((n, h, w, 8), 5.0, dtype=torch.bfloat16, device=DEV)
     xin[..., :3] = x.permute(0, 2, 3, 1).to(DEV).to(torch.bfloat16)
     out = torch.full((n, 1, h, w), 7.0, dtype=torch.float32, device=DEV)
-    s1 = torch.full((n, h, w, 64), 7.0, dtype=torch.bfloat16, device=DEV) if keep else None
-    s2 = torch.full((n, h, w, 32), 7.0, dtype=torch.bfloat16, device=DEV) if keep else None
     names = []
     ops.PROFILER = lambda name, flops, fn, tag="", nbytes=0: (names.append(name), fn())
     try:
-        tail.fwd(xin, 8, 0, n, h, w, out, s1, s2)
+        tail.fwd(xin, 8, 0, n, h, w, out)
     finally:
         ops.PROFILER = None
     torch.cuda.synchronize()
-    assert names == [f"srcnn_tail_kernel<{'true' if keep else 'false'}>"], names
+    assert names == ["srcnn_tail_kernel"], names
     a1 = F.relu(F.conv2d(x.double(), bf(w1).double(), b1.double(), padding=4))
-    a1b = a1.to(torch.bfloat16).double()
-    a2 = F.relu(F.conv2d(a1b, bf(w2).double(), b2.double()))
-    a2b = a2.to(torch.bfloat16).double()
-    want = F.conv2d(a2b, bf(w3).double(), b3.double(), padding=2)
+    a2 = F.relu(F.conv2d(a1.to(torch.bfloat16).double(), bf(w2).double(), b2.double()))
+    want = F.conv2d(a2.to(torch.bfloat16).double(), bf(w3).double(), b3.double(), padding=2)
     check_close(out.cpu(), want, 4e-3, "srcnn out")
-    if keep:
-        for got, ref, what in ((s1, a1, "relu(conv1)"), (s2, a2, "relu(conv2)")):
-            gotd = got.permute(0, 3, 1, 2).double().cpu()
-            err = float((gotd - ref).abs().max())
-            assert err <= 2 ** -7 * float(ref.abs().max()) + 1e-6, f"{what}: err {err:.3e}"
-    # deterministic: a rerun is bit-identical
     out2 = torch.empty_like(out)
     tail.fwd(xin, 8, 0, n, h, w, out2)
     torch.cuda.synchronize()
