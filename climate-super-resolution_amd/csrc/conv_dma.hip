@@ -115,7 +115,9 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
   // epilogues with a fixed store count per lane (dma_store_half), so the wait for the next item's chunk 0 skips them
   constexpr bool CNT = EP == 1 || EP == 2 || EP == 3 || EP == 6 || EP == 7 || EP == 8;
   // EP 3 / 6 / 8 store straight from the accumulators (16 stores per lane and item): no LDS staging, no barrier --
-  // VGG 256 ch @64^2 295 -> 277 us, 512 ch @32^2 263 -> 249 us against the staged form (tools/perf_diag.py, r04dd)
+  // VGG 256 ch @64^2 295 -> 277 us, 512 ch @32^2 263 -> 249 us against the staged form (tools/perf_diag.py, r04dd).
+  // (EP 9 the same way, with its BatchNorm sums xor-shuffled over the pixel columns, measured 9 % slower in the GAN
+  // step, r04h: it keeps the staged tile)
   constexpr bool DIRECT = EP == 3 || EP == 6 || EP == 8;
   constexpr int NST_ITEM = DIRECT ? 16 : 2 * DmaEp<CNT ? EP : 8>::NSTORE;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
@@ -265,67 +267,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
     // epilogue through the buffer just computed (buf ^ 1 after the loop's last flip); LDS-only barriers, so the
     // stores stay in flight
     if (!DIRECT) lds_barrier();  // every wave's fragment reads of it are done
-    if constexpr (EP == 9) {
-      // plain bf16 out straight from the accumulators + BatchNorm partials of the stored (bf16-rounded) values: per lane
-      // over its 4 rows, xor-shuffled over the 16 pixel columns, then the 4 waves of each 16-row half in a fixed order
-      const __amdgpu_buffer_rsrc_t ry = buf_rsrc(a.y, (uint32_t)((long)a.n * a.out_h * a.out_w * a.out_cs * 2));
-      const int ox = ox0 + col;
-      float ss[4][4] = {}, sq[4][4] = {};
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const int oy = oy0 + wave * 4 + m;
-        const bool ok = oy < a.out_h && ox < a.out_w;
-        const long pix = ((long)nimg * a.out_h + oy) * a.out_w + ox;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const bf16x2 p0 = {(__bf16)acc[m][t][0], (__bf16)acc[m][t][1]}, p1 = {(__bf16)acc[m][t][2], (__bf16)acc[m][t][3]};
-          typedef uint32_t v2u32_t __attribute__((ext_vector_type(2)));
-          const v2u32_t pk = {__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1)};
-          const uint32_t off = ok ? (uint32_t)((pix * a.out_cs + a.out_co + co0 + 16 * t + 4 * g) * 2) : BUF_OOB;
-          __builtin_amdgcn_raw_buffer_store_b64(pk, ry, off, 0, 0);
-          if (ok) {
-            const float r[4] = {(float)p0[0], (float)p0[1], (float)p1[0], (float)p1[1]};
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              ss[t][i] += r[i];
-              sq[t][i] = fmaf(r[i], r[i], sq[t][i]);
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int k = 1; k < 16; k <<= 1) {
-            ss[t][i] += __shfl_xor(ss[t][i], k);
-            sq[t][i] += __shfl_xor(sq[t][i], k);
-          }
-      lds_barrier();  // every wave's fragment reads of the chunk buffers are done (the sums alias them)
-      float* red = (float*)smem + wave * 128;  // [wave][sum 64 | sq 64]
-      if (col == 0) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            red[16 * t + 4 * g + i] = ss[t][i];
-            red[64 + 16 * t + 4 * g + i] = sq[t][i];
-          }
-      }
-      lds_barrier();
-      if (tid < 128) {  // half h = tid >> 6 (waves 4h .. 4h + 3), channel c = tid & 63
-        const int hh = tid >> 6, c = tid & 63;
-        const float* rb = (const float*)smem + hh * 4 * 128;
-        const float ts = ((rb[c] + rb[128 + c]) + rb[256 + c]) + rb[384 + c];
-        const float tq = ((rb[64 + c] + rb[192 + c]) + rb[320 + c]) + rb[448 + c];
-        const long tile16 = ((long)nimg * (2 * a.tiles_y) + 2 * ty + hh) * a.tiles_x + ox0 / TW;
-        double* out = a.bn_part + tile16 * 2 * a.out_c;
-        out[co0 + c] = (double)ts;
-        out[a.out_c + co0 + c] = (double)tq;
-      }
-      return;
-    } else if constexpr (BN) {
+    if constexpr (BN) {
       float* eb = (float*)smem + wave * (64 * DMA_EPP);  // the whole tile (aliases both buffers: no DMA in flight)
 #pragma unroll
       for (int m = 0; m < 4; ++m)
