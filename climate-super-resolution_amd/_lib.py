@@ -196,7 +196,7 @@ SIGNATURES = {
     "climsr_channel_attention_parts": (c_int, [c_void_p, c_int, c_int, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                                c_int, c_void_p, c_void_p, c_void_p]),
     "climsr_conv2d_fwd_ch_parts": (ctypes.c_int64, [P(ConvDesc), P(Epilogue), c_void_p]),
-    "climsr_ca_scale_add": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int64, c_int, c_void_p]),
+    "climsr_ca_scale_add": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int64, c_int, c_void_p]),
     "climsr_pixel_shuffle_bf16": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
 }
 

@@ -2621,8 +2621,8 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
     set_error("conv2d_fwd: act %d invalid (3/4 need res1 = the activation output)", ep->act);
     return CLIMSR_EINVAL;
   }
-  if (ep->ch_part && conv_wr_ep(d, ep, bias) != 3) {
-    set_error("conv2d_fwd: per-tile channel sums only from the 64 -> 64 3x3 fp32-output register-resident conv "
+  if (ep->ch_part && conv_wr_ep(d, ep, bias) != 3 && conv_wr_ep(d, ep, bias) != 4) {
+    set_error("conv2d_fwd: per-tile channel sums only from the 64 -> 64 3x3 register-resident conv "
               "(climsr_conv2d_fwd_ch_parts)");
     return CLIMSR_EINVAL;
   }

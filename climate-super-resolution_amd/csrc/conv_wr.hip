@@ -32,7 +32,9 @@ constexpr int WR_SLOTS = WR_PR * WR_PC * WR_SPP;        // 1080
 constexpr int WR_NI = (WR_SLOTS + 63) / 64;             // LDS-DMA instructions per footprint (17)
 constexpr int WR_BUF = WR_NI * 1024;                    // bytes per footprint buffer
 constexpr int WR_LDS = 4 * 2 * WR_BUF;                  // 4 waves x 2 buffers: 139,264 B
-static_assert(WR_LDS <= 160 * 1024, "conv_wr LDS");
+constexpr int WR_RED = 64 * 17 * 4;                     // per wave: the channel-sum transpose [64 ch][17] (EP 3 / 4)
+constexpr int WR_LDS_ALL = WR_LDS + 4 * WR_RED;         // 156,672 B
+static_assert(WR_LDS_ALL <= 160 * 1024, "conv_wr LDS");
 
 struct WrArgs {
   const uint16_t* x;
@@ -40,7 +42,7 @@ struct WrArgs {
   const float* bias;     // may be null
   uint16_t* y;
   const uint16_t* res1;  // EP 1: residual (v = alpha1 v + beta1 r); EP 2: the activation output (act 3 / 4)
-  float* ch_part;        // EP 3 (fp32 output): per-tile channel sums [tile][64] (null: none)
+  float* ch_part;        // EP 3 / 4: per-tile channel sums [tile][64] of the fp32 values (null: none)
   int n, in_h, in_w, in_cs, in_co, up, out_h, out_w, out_cs, out_co, kpk;
   int act;  // forward: 0 none, 1 leaky relu, 2 relu; EP 2: 3 / 4 = backward of leaky relu / relu
   float slope, alpha1, beta1;
@@ -55,7 +57,8 @@ template <int EP>
 __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // vector-memory operations of one epilogue (loads + stores), fixed per lane
-  constexpr int NEPI = EP == 0 ? 16 : (EP == 3 ? 20 : 32);
+  constexpr int NEPI = EP == 0 ? 16 : (EP == 3 || EP == 4 ? 17 : 32);
+  constexpr bool SUMS = EP == 3 || EP == 4;  // per-tile channel sums (EP 3: fp32 out, EP 4: bf16 out)
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, col = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int G4 = (int)gridDim.x * 4;
@@ -114,8 +117,8 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
   };
 
   const __amdgpu_buffer_rsrc_t yr = buf_rsrc(a.y, a.y_bytes);
-  const __amdgpu_buffer_rsrc_t pr = buf_rsrc(a.ch_part, EP == 3 && a.ch_part ? (uint32_t)a.ntiles * 256u : 0u);
-  const __amdgpu_buffer_rsrc_t rr = buf_rsrc(a.res1, EP ? a.r1_bytes : 0u);
+  const __amdgpu_buffer_rsrc_t pr = buf_rsrc(a.ch_part, SUMS && a.ch_part ? (uint32_t)a.ntiles * 256u : 0u);
+  const __amdgpu_buffer_rsrc_t rr = buf_rsrc(a.res1, (EP == 1 || EP == 2) ? a.r1_bytes : 0u);
   const int lb = col * WR_XP * 2 + g * 16;  // this lane's byte offset in a footprint row: pixel col, channels 8 g ..
   issue(T, 0);
   for (int it = 0;; ++it) {
@@ -160,7 +163,7 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
       const bool ok = oy < a.out_h && ox < a.out_w;
       const long pix = ((long)nimg * a.out_h + oy) * a.out_w + ox;
       off[m] = ok ? (uint32_t)((pix * a.out_cs + a.out_co + 4 * g) * (EP == 3 ? 4 : 2)) : BUF_OOB;
-      if constexpr (EP != 0) {
+      if constexpr (EP == 1 || EP == 2) {
         const uint32_t ro = ok ? (uint32_t)((pix * a.r1_cs + a.r1_co + 4 * g) * 2) : BUF_OOB;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -169,7 +172,7 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
         }
       }
     }
-    float csum[4][4] = {};  // EP 3: this lane's channel sums over its 4 pixels (rows)
+    float csum[4][4] = {};  // EP 3 / 4: this lane's channel sums over its 4 pixels (rows)
 #pragma unroll
     for (int m = 0; m < 4; ++m)
 #pragma unroll
@@ -204,19 +207,25 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
           const bf16x2 p0 = {(__bf16)v[0], (__bf16)v[1]}, p1 = {(__bf16)v[2], (__bf16)v[3]};
           const v2u32 pk = {__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1)};
           __builtin_amdgcn_raw_buffer_store_b64(pk, yr, off[m] == BUF_OOB ? BUF_OOB : off[m] + (uint32_t)(t * 32), 0, 0);
+          if (EP == 4 && off[m] != BUF_OOB) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) csum[t][i] += v[i];
+          }
         }
       }
-    if constexpr (EP == 3) {  // per-tile channel sums: the 16 pixel columns by a fixed xor tree, lane col 0 stores
+    if constexpr (SUMS) {
+      // per-tile channel sums: the lanes' column sums transposed through this wave's LDS corner ([channel][17]: both
+      // passes conflict-free), then lane l adds channel l's 16 columns in order and stores it (one 4 B store a lane;
+      // the xor-shuffle tree it replaces took 64 ds_bpermute per lane).  Wave-private: LDS order within the wave suffices.
+      float* red = (float*)(smem + WR_LDS) + wv * (WR_RED / 4);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
+      for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i) red[(16 * t + 4 * g + i) * 17 + col] = csum[t][i];
+      float cs = 0.f;
 #pragma unroll
-          for (int k = 1; k < 16; k <<= 1) csum[t][i] += __shfl_xor(csum[t][i], k);
-        const v4u32 pk = {__float_as_uint(csum[t][0]), __float_as_uint(csum[t][1]), __float_as_uint(csum[t][2]),
-                          __float_as_uint(csum[t][3])};
-        __builtin_amdgcn_raw_buffer_store_b128(pk, pr, col == 0 ? (uint32_t)((T * 64 + t * 16 + 4 * g) * 4) : BUF_OOB, 0, 0);
-      }
+      for (int c = 0; c < 16; ++c) cs += red[lane * 17 + c];
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(cs), pr, (uint32_t)((T * 64 + lane) * 4), 0, 0);
     }
     if (Tn >= a.ntiles) break;
     T = Tn;
@@ -230,16 +239,16 @@ namespace climsr {
 
 // the conv_wr epilogue for (d, ep), or -1 when the conv is not this kernel's: 0 bias / activation, bf16 out; 1 + bf16
 // residual; 2 activation backward from the stored activation (no bias); 3 bias / activation, fp32 out (+ per-tile
-// channel sums).  ch_part only with 3.
+// channel sums); 4 bias / activation, bf16 out + per-tile channel sums (of the fp32 values).
 int conv_wr_ep(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const float* bias) {
   const bool res = ep->res1 != nullptr;
   int epk = -1;
-  if (ep->out_mode == 0 && !res && ep->act >= 0 && ep->act <= 2) epk = 0;
+  if (ep->out_mode == 0 && !res && ep->act >= 0 && ep->act <= 2) epk = ep->ch_part ? 4 : 0;
   else if (ep->out_mode == 0 && res && ep->act == 0 && !(ep->res_f32 & 1)) epk = 1;
   else if (ep->out_mode == 0 && res && (ep->act == 3 || ep->act == 4) && !bias && !(ep->res_f32 & 1)) epk = 2;
   else if (ep->out_mode == 1 && !res && ep->act >= 0 && ep->act <= 2) epk = 3;
   const long opx = (long)d->n * d->out_h * d->out_w;
-  if (epk < 0 || (ep->ch_part && epk != 3) || d->in_c != 64 || d->out_c != 64 || d->cc != 64 || d->ks != 3 || d->stride != 1 ||
+  if (epk < 0 || (ep->ch_part && epk != 3 && epk != 4) || d->in_c != 64 || d->out_c != 64 || d->cc != 64 || d->ks != 3 || d->stride != 1 ||
       d->pad != 1 || (d->up != 1 && d->up != 2) || d->out_h != d->in_h * d->up || d->out_w != d->in_w * d->up ||
       d->in_cstride % 8 || d->in_coff % 8 || (d->out_cstride | d->out_coff) & 3 || ep->down2 || ep->res2 || ep->aux ||
       ep->bn_part || (res && ((ep->res1_cstride | ep->res1_coff) & 3)) ||
@@ -253,8 +262,9 @@ int conv_wr_ep(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const float* b
 // tiles (rows of ch_part) of the conv, and per image; 0 when conv_wr does not take (d, ep)
 long conv_wr_ch_parts(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, int* tiles_per_image) {
   ClimsrEpilogue e = *ep;
-  e.out_mode = 1;
-  if (conv_wr_ep(d, &e, nullptr) != 3) return 0;
+  e.ch_part = (float*)1;  // (only its presence matters here)
+  const int k = conv_wr_ep(d, &e, nullptr);
+  if (k != 3 && k != 4) return 0;
   const int tpi = ceil_div(d->out_w, WR_TC) * ceil_div(d->out_h, WR_TR);
   if (tiles_per_image) *tiles_per_image = tpi;
   return (long)tpi * d->n;
@@ -283,9 +293,11 @@ int conv_wr_launch(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const uint
   a.r1_bytes = res ? (uint32_t)(opx * ep->res1_cstride * 2) : 0u;
   const int ncu = device_cus();
   const int grid = std::min(ceil_div(a.ntiles, 4), ncu);
-  void (*k)(WrArgs) = epk == 0 ? conv_wr_kernel<0> : epk == 1 ? conv_wr_kernel<1> : epk == 2 ? conv_wr_kernel<2> : conv_wr_kernel<3>;
-  if (int e = lds_opt_in((const void*)k, WR_LDS)) return e;
-  hipLaunchKernelGGL(k, dim3(grid), dim3(256), WR_LDS, s, a);
+  void (*k)(WrArgs) = epk == 0 ? conv_wr_kernel<0> : epk == 1 ? conv_wr_kernel<1> : epk == 2 ? conv_wr_kernel<2>
+                      : epk == 3 ? conv_wr_kernel<3> : conv_wr_kernel<4>;
+  const int lds = (epk == 3 || epk == 4) ? WR_LDS_ALL : WR_LDS;
+  if (int e = lds_opt_in((const void*)k, WR_LDS_ALL)) return e;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, s, a);
   return check_launch("conv2d_fwd (wr)");
 }
 

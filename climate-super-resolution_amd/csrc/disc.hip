@@ -1249,11 +1249,14 @@ __global__ void l1_bf16_partial_kernel(const uint16_t* __restrict__ a, const uin
   if (threadIdx.x == 0) ws[blockIdx.x] = sh[0];
 }
 
+// one wave: lane l sums ws[l], ws[l + 64], .. in order, then a fixed xor tree (deterministic; a single thread summing
+// the 512 partials serially took 31 us)
 __global__ void l1_bf16_final_kernel(const double* ws, int nb, long n, float* out) {
-  if (threadIdx.x != 0) return;
   double s = 0.0;
-  for (int i = 0; i < nb; ++i) s += ws[i];
-  out[0] = (float)(s / (double)n);
+  for (int i = threadIdx.x; i < nb; i += 64) s += ws[i];
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) s += __shfl_xor(s, m);
+  if (threadIdx.x == 0) out[0] = (float)(s / (double)n);
 }
 
 extern "C" int climsr_l1_loss_bf16(const uint16_t* a, const uint16_t* b, int64_t n, double* workspace, float* out, void* stream) {

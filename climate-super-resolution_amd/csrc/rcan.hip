@@ -131,8 +131,9 @@ extern "C" int climsr_channel_attention_parts(const float* part, int n, int tile
   return check_launch("channel_attention_parts");
 }
 
-// xres[p][c] = u[p][c] * s[n][c] + xres[p][c];  xb[p][c] = bf16(xres[p][c])   (RCAB: body(x) + x)
-__global__ __launch_bounds__(256) void ca_scale_add_kernel(const float* __restrict__ u, int u_cs, const float* __restrict__ s,
+// xres[p][c] = u[p][c] * s[n][c] + xres[p][c];  xb[p][c] = bf16(xres[p][c])   (RCAB: body(x) + x); u fp32 or bf16
+template <bool UB>
+__global__ __launch_bounds__(256) void ca_scale_add_kernel(const void* __restrict__ u, int u_cs, const float* __restrict__ s,
                                                            float* __restrict__ xres, uint16_t* __restrict__ xb, int xb_cs, long hw,
                                                            int c, long total4) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -141,7 +142,14 @@ __global__ __launch_bounds__(256) void ca_scale_add_kernel(const float* __restri
   const long pix = i / cg;
   const int c0 = (int)(i % cg) * 4;
   const int nimg = (int)(pix / hw);
-  const float4 uv = *(const float4*)(u + pix * u_cs + c0);
+  float4 uv;
+  if constexpr (UB) {
+    const uint2 raw = *(const uint2*)((const uint16_t*)u + pix * u_cs + c0);
+    uv = make_float4(__uint_as_float(raw.x << 16), __uint_as_float(raw.x & 0xFFFF0000u), __uint_as_float(raw.y << 16),
+                     __uint_as_float(raw.y & 0xFFFF0000u));
+  } else {
+    uv = *(const float4*)((const float*)u + pix * u_cs + c0);
+  }
   const float4 sv = *(const float4*)(s + (long)nimg * c + c0);
   float4 r = *(const float4*)(xres + pix * c + c0);
   r.x = uv.x * sv.x + r.x;
@@ -155,16 +163,20 @@ __global__ __launch_bounds__(256) void ca_scale_add_kernel(const float* __restri
   *(uint2*)(xb + pix * xb_cs + c0) = pk;
 }
 
-extern "C" int climsr_ca_scale_add(const float* u, int u_cstride, const float* s, float* xres, uint16_t* xb, int xb_cstride, int n,
-                                   int64_t hw, int c, void* stream) {
+extern "C" int climsr_ca_scale_add(const void* u, int u_bf16, int u_cstride, const float* s, float* xres, uint16_t* xb, int xb_cstride,
+                                   int n, int64_t hw, int c, void* stream) {
   if (!u || !s || !xres || !xb || n <= 0 || hw <= 0 || c % 4 || u_cstride % 4 || xb_cstride % 4 || u_cstride < c ||
       xb_cstride < c) {
     set_error("ca_scale_add: bad args (c, strides multiples of 4)");
     return CLIMSR_EINVAL;
   }
   const long total4 = (long)n * hw * (c / 4);
-  hipLaunchKernelGGL(ca_scale_add_kernel, dim3(ceil_div(total4, 256)), dim3(256), 0, (hipStream_t)stream, u, u_cstride, s, xres, xb,
-                     xb_cstride, (long)hw, c, total4);
+  if (u_bf16)
+    hipLaunchKernelGGL(ca_scale_add_kernel<true>, dim3(ceil_div(total4, 256)), dim3(256), 0, (hipStream_t)stream, u, u_cstride, s,
+                       xres, xb, xb_cstride, (long)hw, c, total4);
+  else
+    hipLaunchKernelGGL(ca_scale_add_kernel<false>, dim3(ceil_div(total4, 256)), dim3(256), 0, (hipStream_t)stream, u, u_cstride, s,
+                       xres, xb, xb_cstride, (long)hw, c, total4);
   return check_launch("ca_scale_add");
 }
 

@@ -638,13 +638,20 @@ __global__ __launch_bounds__(256, 1) void srcnn_bwd_kernel(SrcnnBwdArgs a) {
   }
 }
 
-// grads (+)= sum over the workgroup slabs in order: conv2 weight [32][64] + bias [32], conv3 weight [1][32][5][5] + bias
+// grads (+)= sum over the workgroup slabs in a fixed order: thread (q, e) sums slabs q, q + 4, .. of element e, the
+// four chains then combine in order (one serial chain over every slab took 62 us)
 __global__ __launch_bounds__(256) void srcnn_bwd_reduce_kernel(const float* __restrict__ part, int nparts, float* gw2, float* gb2,
                                                                float* gw3, float* gb3, int accumulate) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= NPART) return;
+  __shared__ float red[4][64];
+  const int q = threadIdx.x >> 6, e = blockIdx.x * 64 + (threadIdx.x & 63);
   float s = 0.f;
-  for (int k = 0; k < nparts; ++k) s += part[(long)k * NPART_P + e];
+  if (e < NPART)
+    for (int k = q; k < nparts; k += 4) s += part[(long)k * NPART_P + e];
+  red[q][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (q != 0 || e >= NPART) return;
+  const int l = threadIdx.x & 63;
+  s = ((red[0][l] + red[1][l]) + red[2][l]) + red[3][l];
   float* dst = e < 2048 ? gw2 + e : (e < 2080 ? gb2 + (e - 2048) : (e < NPART - 1 ? gw3 + (e - 2080) : gb3));
   *dst = accumulate ? *dst + s : s;
 }
@@ -771,7 +778,7 @@ extern "C" int climsr_srcnn_bwd(const ClimsrSrcnnBwdDesc* d, void* stream) {
   if (int e = lds_opt_in((const void*)srcnn_bwd_kernel, B_LDS_ALL)) return e;
   hipLaunchKernelGGL(srcnn_bwd_kernel, dim3(grid), dim3(256), B_LDS_ALL, s, a);
   if (int e = check_launch("srcnn_bwd")) return e;
-  hipLaunchKernelGGL(srcnn_bwd_reduce_kernel, dim3(ceil_div(NPART, 256)), dim3(256), 0, s, d->part, grid, d->gw2, d->gb2, d->gw3,
+  hipLaunchKernelGGL(srcnn_bwd_reduce_kernel, dim3(ceil_div(NPART, 64)), dim3(256), 0, s, d->part, grid, d->gw2, d->gb2, d->gw3,
                      d->gb3, d->accumulate);
   return check_launch("srcnn_bwd_reduce");
 }

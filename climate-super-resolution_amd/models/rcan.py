@@ -193,7 +193,6 @@ class _RcanEngine:
         xb_alt = bf(n, h, w, nf)
         gin = f32(n, h, w, nf)
         t = bf(n, h, w, nf)
-        u = f32(n, h, w, nf)
         s = f32(n, nf)
         ws_bytes = L.climsr_channel_attention_workspace(n, nf)
         if self.ca_ws is None or self.ca_ws.numel() * 8 < ws_bytes or self.ca_ws.device != dev:
@@ -202,6 +201,9 @@ class _RcanEngine:
         # the register-resident 64 -> 64 conv) when it can; else the pooling pass re-reads u
         cp_rows, cp_tpi = P["body.0.body.0.body.2"].ch_parts(nf, h, w, n, nf)
         cpart = f32(max(cp_rows, 1), nf)
+        # u (the RCAB body's output) in bf16 when the conv pools it itself: the attention's mean comes from the fp32
+        # values in the epilogue, only the scale-add reads u (half the bytes of the fp32 round trip)
+        u = bf(n, h, w, nf) if cp_rows else f32(n, h, w, nf)
         for g in range(m.n_resgroups):
             gin.copy_(xres)
             for b in range(m.n_resblocks):
@@ -210,14 +212,15 @@ class _RcanEngine:
                 ca = self.mods[f"{pre}.3"].conv_du
                 w1, b1, w2, b2 = ca[0].weight, ca[0].bias, ca[2].weight, ca[2].bias
                 if cp_rows:
-                    P[f"{pre}.2"].fwd(t, nf, 0, h, w, u, nf, 0, n, out_mode=OUT_F32, ch_part=cpart)
+                    P[f"{pre}.2"].fwd(t, nf, 0, h, w, u, nf, 0, n, ch_part=cpart)
                     check(L.climsr_channel_attention_parts(ptr(cpart), n, cp_tpi, h * w, nf, ptr(w1), ptr(b1), ptr(w2), ptr(b2),
                                                            w1.shape[0], ptr(self.ca_ws), ptr(s), st), f"channel attention {pre}")
                 else:
                     P[f"{pre}.2"].fwd(t, nf, 0, h, w, u, nf, 0, n, out_mode=OUT_F32)
                     check(L.climsr_channel_attention(ptr(u), n, h * w, nf, nf, ptr(w1), ptr(b1), ptr(w2), ptr(b2), w1.shape[0],
                                                      ptr(self.ca_ws), ptr(s), st), f"channel attention {pre}")
-                check(L.climsr_ca_scale_add(ptr(u), nf, ptr(s), ptr(xres), ptr(xb), nf, n, h * w, nf, st), f"rcab residual {pre}")
+                check(L.climsr_ca_scale_add(ptr(u), int(bool(cp_rows)), nf, ptr(s), ptr(xres), ptr(xb), nf, n, h * w, nf, st),
+                      f"rcab residual {pre}")
             # group tail conv + group skip (rcan.py:133-135), fp32 stream + bf16 shadow.  The shadow goes to the other
             # buffer of a pair: written in place, a tile's aux store would race the halo reads of its neighbours.
             P[f"body.{g}.body.{m.n_resblocks}"].fwd(xb, nf, 0, h, w, xres, nf, 0, n, res1=gin, res1_cs=nf, out_mode=OUT_F32,

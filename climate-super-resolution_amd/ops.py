@@ -170,7 +170,7 @@ class ConvPlan:
         return int(_lib.load().climsr_conv2d_fwd_bn_parts(ctypes.byref(d), ctypes.byref(ep)))
 
     def ch_parts(self, x_cs: int, in_h: int, in_w: int, n: int, y_cs: int) -> tuple:
-        """(rows, rows per image) of the per-tile channel sums fwd(..., out_mode=OUT_F32, ch_part=...) writes, (0, 0)
+        """(rows, rows per image) of the per-tile channel sums fwd(..., ch_part=...) writes (fp32 or bf16 output), (0, 0)
         if its kernel cannot (climsr_conv2d_fwd_ch_parts)."""
         oh, ow = self.out_hw(in_h, in_w)
         d = ConvDesc(n, in_h, in_w, self.cin_k, x_cs, 0, 1, self.ks, self.stride, self.pad, oh, ow, self.cout, y_cs, 0, self.cc)

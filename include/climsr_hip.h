@@ -86,9 +86,9 @@ typedef struct ClimsrEpilogue {
   const float* bn_rstd;
   const float* bn_gamma;
   const float* bn_beta;
-  /* optional (the 64 -> 64 3x3 register-resident conv, climsr_conv2d_fwd_ch_parts > 0): per-tile channel sums of the
-     stored output values, ch_part[tile][out_c] fp32, tiles of one image contiguous -- the global average pool of RCAN's
-     channel attention (rcan.py:50-69) without re-reading the output; finish with climsr_channel_attention_parts */
+  /* optional (the 64 -> 64 3x3 register-resident conv, climsr_conv2d_fwd_ch_parts > 0; fp32 or bf16 output): per-tile
+     channel sums of the output values before any bf16 rounding, ch_part[tile][out_c] fp32, tiles of one image
+     contiguous -- the global average pool of RCAN's channel attention (rcan.py:50-69) without re-reading the output; finish with climsr_channel_attention_parts */
   float* ch_part;
 } ClimsrEpilogue;
 
@@ -451,9 +451,10 @@ int climsr_channel_attention_parts(const float* part, int n, int tiles_per_image
                                    const float* b1, const float* w2, const float* b2, int cr, double* workspace, float* s,
                                    void* stream);
 /* RCAB residual with the attention scale (rcan.py:104-107): xres = u * s + xres (fp32 [n][hw][c]) and
- * xb = bf16(xres) ([n][hw][xb_cstride], the next conv's input).  c, strides multiples of 4. */
-int climsr_ca_scale_add(const float* u, int u_cstride, const float* s, float* xres, uint16_t* xb, int xb_cstride, int n,
-                        int64_t hw, int c, void* stream);
+ * xb = bf16(xres) ([n][hw][xb_cstride], the next conv's input); u = the RCAB body's output, fp32 or (u_bf16 = 1)
+ * bf16, channel stride u_cstride.  c, strides multiples of 4. */
+int climsr_ca_scale_add(const void* u, int u_bf16, int u_cstride, const float* s, float* xres, uint16_t* xb, int xb_cstride,
+                        int n, int64_t hw, int c, void* stream);
 /* The SRCNN tail of the ESRGAN generator as ONE launch, replacing srcnn.conv1 -> ReLU -> conv2 -> ReLU -> conv3
  * (srcnn.py:9-18) on torch.cat([out, elev, mask], 1) (esrgan.py:99-100): x = bf16 NHWC, channels x_co .. x_co+3 (the
  * in_c <= 4 real ones + zeros); out = fp32 [n][1][h][w]; the 64- and 32-channel intermediates stay on chip (the

@@ -647,8 +647,8 @@ def test_conv_wr_matches_fp64(n, h, w, up, mode):
     assert err <= 2 ** -7 * float(want.abs().max()) + 1e-6, f"{mode}: err {err:.3e} vs {float(want.abs().max()):.3e}"
 
 
-@pytest.mark.parametrize("n,h,w", [(2, 13, 37), (1, 45, 90)])
-def test_conv_wr_fp32_out_channel_sums(n, h, w):
+@pytest.mark.parametrize("n,h,w,f32", [(2, 13, 37, True), (1, 45, 90, True), (2, 13, 37, False), (1, 30, 70, False)])
+def test_conv_wr_fp32_out_channel_sums(n, h, w, f32):
     """conv_wr's fp32-output epilogue (RCAN's RCAB conv2, rcan.py:50-69) and the per-tile channel sums it emits for the
     channel attention's global pool (climsr_conv2d_fwd_ch_parts rows, tiles of an image contiguous): the output vs
     fp64 torch, the sums of each image's tiles vs the image's channel sums of that output."""
@@ -657,22 +657,23 @@ def test_conv_wr_fp32_out_channel_sums(n, h, w):
     p, wt, b = make_plan(64, 64, 3, seed=21)
     g = torch.Generator().manual_seed(22)
     x = bf(torch.rand((n, 64, h, w), generator=g) * 2 - 1)
-    y = torch.full((n, h, w, 64), 7.0, dtype=torch.float32, device=DEV)
+    y = torch.full((n, h, w, 64), 7.0, dtype=torch.float32 if f32 else torch.bfloat16, device=DEV)
     rows, tpi = p.ch_parts(64, h, w, n, 64)
     assert rows == n * tpi and tpi == ((w + 15) // 16) * ((h + 3) // 4)
     part = torch.full((rows, 64), 7.0, dtype=torch.float32, device=DEV)
     names = []
     ops.PROFILER = lambda name, flops, fn, tag="", nbytes=0: (names.append(name), fn())
     try:
-        p.fwd(to_nhwc(x), 64, 0, h, w, y, 64, 0, n, out_mode=OUT_F32, ch_part=part)
+        p.fwd(to_nhwc(x), 64, 0, h, w, y, 64, 0, n, out_mode=OUT_F32 if f32 else OUT_BF16, ch_part=part)
     finally:
         ops.PROFILER = None
     torch.cuda.synchronize()
-    assert names and names[-1].startswith("conv_wr_kernel<3>"), names
+    assert names and names[-1].startswith("conv_wr_kernel<3>" if f32 else "conv_wr_kernel<4>"), names
     want = F.conv2d(x.double(), bf(wt).double(), b.double(), padding=1)
-    check_close(from_nhwc(y, 64).cpu(), want, 1e-5, "fp32 out")
+    check_close(from_nhwc(y, 64).cpu(), want, 1e-5 if f32 else 2 ** -8, "out")
     sums = part.double().cpu().reshape(n, tpi, 64).sum(1)
-    check_close(sums, y.double().cpu().sum((1, 2)), 1e-5, "channel sums")
+    # the sums are of the fp32 values (before the bf16 rounding of a bf16 output)
+    check_close(sums, want.sum((2, 3)), 1e-5, "channel sums")
 
 
 @pytest.mark.parametrize("n,h,w", [(2, 32, 32), (1, 45, 70), (3, 20, 100), (1, 5, 7), (2, 64, 96), (1, 37, 36)])

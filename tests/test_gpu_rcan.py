@@ -97,7 +97,8 @@ def test_channel_attention_and_rcab_residual():
     st = _lib.stream_ptr()
     check(L.climsr_channel_attention(ptr(d["u"]), n, h * w, c, c, ptr(d["w1"]), ptr(d["b1"]), ptr(d["w2"]), ptr(d["b2"]), cr,
                                      ptr(ws), ptr(s), st), "ca")
-    check(L.climsr_ca_scale_add(ptr(d["u"]), c, ptr(s), ptr(d["xres"]), ptr(xb), c, n, h * w, c, st), "scale add")
+    xres0 = d["xres"].clone()
+    check(L.climsr_ca_scale_add(ptr(d["u"]), 0, c, ptr(s), ptr(d["xres"]), ptr(xb), c, n, h * w, c, st), "scale add")
     torch.cuda.synchronize()
     ud = u.double()
     mean = ud.mean(dim=(1, 2))
@@ -106,3 +107,11 @@ def test_channel_attention_and_rcab_residual():
     x_ref = ud * s_ref[:, None, None, :] + xres.double()
     assert (d["xres"].cpu().double() - x_ref).abs().max() <= 1e-5 * x_ref.abs().max()
     assert torch.equal(xb.cpu(), d["xres"].cpu().to(torch.bfloat16))
+    # the bf16-u form (the RCAB's second conv stores u in bf16): the same update from the bf16-rounded u
+    ub = d["u"].to(torch.bfloat16)
+    xr2, xb2 = xres0.clone(), torch.empty_like(xb)
+    check(L.climsr_ca_scale_add(ptr(ub), 1, c, ptr(s), ptr(xr2), ptr(xb2), c, n, h * w, c, st), "scale add bf16 u")
+    torch.cuda.synchronize()
+    x_ref2 = ub.double().cpu() * s.cpu().double()[:, None, None, :] + xres.double()
+    assert (xr2.cpu().double() - x_ref2).abs().max() <= 1e-5 * x_ref2.abs().max()
+    assert torch.equal(xb2.cpu(), xr2.cpu().to(torch.bfloat16))
