@@ -2245,171 +2245,23 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_s2_kernel(FwdArgs a) {
   }
 }
 
-// ------------------------------------------------------------------------------------------
-// Forward of a 3x3 / stride-2 / pad-1 conv with 32-channel chunks (the discriminator's downsampling convs,
-// rfb_esrgan.py:30-48, bf16 out for the BatchNorm).  A 16 x 16 output tile needs a 33 x 33 input tile, so one
-// workgroup fills the CU's LDS (126 KB) and the 4-wave form ran one wave per SIMD with nothing to hide its
-// LDS latency (~400 TFLOP/s).  Here 8 waves share the tile: wave w computes output rows 4(w&3)..+3 for the taps
-// [0,5) (w < 4) or [5,9) (w >= 4); waves w and w+4 share a SIMD, so each SIMD still issues 9 taps' MFMAs per
-// chunk but from two waves, and the per-thread staging halves.  The two tap groups' accumulators meet in LDS
-// (fixed order) and the first 4 waves store through the generic bf16 epilogue.
-// ------------------------------------------------------------------------------------------
-constexpr int S2F_TP = 33, S2F_CCP = 40, S2F_WP = 9 * 32 + WPAD;
-constexpr int S2F_LDS_X = S2F_TP * S2F_TP * S2F_CCP * 2, S2F_LDS_OP = S2F_LDS_X + 64 * S2F_WP * 2;
-constexpr int S2F_EPP = 64 + 4;
-constexpr int S2F_LDS_RED = 4 * 16 * 64 * 16, S2F_LDS_EP = 4 * 64 * S2F_EPP * 4;
-constexpr int S2F_LDS = S2F_LDS_OP > S2F_LDS_RED + S2F_LDS_EP ? S2F_LDS_OP : S2F_LDS_RED + S2F_LDS_EP;
-
-template <bool STATS>
-__global__ __launch_bounds__(512) void conv_fwd_s2_kernel(FwdArgs a) {
-  constexpr int MW = 4, NT = 4, NRX = (S2F_TP * S2F_TP * 4 + 511) / 512, NRW = (64 * 36 + 511) / 512;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint16_t* xs = (uint16_t*)smem;
-  uint16_t* ws = (uint16_t*)(smem + S2F_LDS_X);
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
-  const int r = wave & 3, h = wave >> 2;
-  int bid = blockIdx.x;
-  const int tx = bid % a.tiles_x;
-  bid /= a.tiles_x;
-  const int ty = bid % a.tiles_y;
-  const int nimg = bid / a.tiles_y;
-  const int ox0 = tx * 16, oy0 = ty * 16, co0 = blockIdx.y * 64;
-  const int iy0 = 2 * oy0 - 1, ix0 = 2 * ox0 - 1;
-
-  f32x4 acc[MW][NT];
-#pragma unroll
-  for (int m = 0; m < MW; ++m)
-#pragma unroll
-    for (int t = 0; t < NT; ++t) acc[m][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  uint4 px[NRX], pw[NRW];
-  auto issue = [&](int j) {
-#pragma unroll
-    for (int i = 0; i < NRX; ++i) {
-      const int v = tid + 512 * i, pix = v >> 2, cg = v & 3;
-      const int iy = iy0 + pix / S2F_TP, ix = ix0 + pix % S2F_TP;
-      px[i] = make_uint4(0, 0, 0, 0);
-      if (pix < S2F_TP * S2F_TP && iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w)
-        px[i] = *(const uint4*)(a.x + (((long)nimg * a.in_h + iy) * a.in_w + ix) * a.in_cs + a.in_co + j * 32 + cg * 8);
-    }
-#pragma unroll
-    for (int i = 0; i < NRW; ++i) {
-      const int v = tid + 512 * i, row = v / 36, kv = v % 36;
-      pw[i] = make_uint4(0, 0, 0, 0);
-      if (row < 64) pw[i] = *(const uint4*)(a.w + (long)(co0 + row) * a.kpk + (long)j * 288 + kv * 8);
-    }
-  };
-  auto stash = [&]() {
-#pragma unroll
-    for (int i = 0; i < NRX; ++i) {
-      const int v = tid + 512 * i, pix = v >> 2, cg = v & 3;
-      if (pix < S2F_TP * S2F_TP) *(uint4*)(xs + pix * S2F_CCP + cg * 8) = px[i];
-    }
-#pragma unroll
-    for (int i = 0; i < NRW; ++i) {
-      const int v = tid + 512 * i, row = v / 36, kv = v % 36;
-      if (row < 64) *(uint4*)(ws + row * S2F_WP + kv * 8) = pw[i];
-    }
-  };
-  // output (row 4r + m, col) reads input tile pixel (2 (4r + m) + ky, 2 col + kx)
-  const uint16_t* xb = xs + (2 * 4 * r * S2F_TP + 2 * col) * S2F_CCP + g * 8;
-  const uint16_t* wb = ws + col * S2F_WP + g * 8;
-  auto compute = [&]() {
-    bf16x8 af[2][NT], bf[2][MW];
-    auto ld = [&](int tap, int b) {
-      const int off = ((tap / 3) * S2F_TP + (tap % 3)) * S2F_CCP;
-#pragma unroll
-      for (int t = 0; t < NT; ++t) af[b][t] = *(const bf16x8*)(wb + t * 16 * S2F_WP + tap * 32);
-#pragma unroll
-      for (int m = 0; m < MW; ++m) bf[b][m] = *(const bf16x8*)(xb + m * 2 * S2F_TP * S2F_CCP + off);
-    };
-    auto mm = [&](int b) {
-#pragma unroll
-      for (int m = 0; m < MW; ++m)
-#pragma unroll
-        for (int t = 0; t < NT; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[b][t], bf[b][m], acc[m][t], 0, 0, 0);
-    };
-    // each tap's fragment reads go out as one burst ahead of the previous tap's MFMAs (sched_barrier: the compiler
-    // otherwise sinks every read next to its first use and waits for it there)
-    if (h == 0) {
-      ld(0, 0);
-#pragma unroll
-      for (int k = 0; k < 5; ++k) {
-        if (k + 1 < 5) ld(k + 1, (k + 1) & 1);
-        __builtin_amdgcn_sched_barrier(0);
-        mm(k & 1);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    } else {
-      ld(5, 0);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (k + 1 < 4) ld(6 + k, (k + 1) & 1);
-        __builtin_amdgcn_sched_barrier(0);
-        mm(k & 1);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  };
-  issue(0);
-  for (int j = 0; j < a.nchunk; ++j) {
-    __syncthreads();  // chunk j-1's fragment reads are done
-    stash();
-    if (j + 1 < a.nchunk) issue(j + 1);  // lands while chunk j computes
-    __syncthreads();
-    compute();
-  }
-  // tap group 1 parks its sums, tap group 0 adds them (fixed order) and stores
-  float4* red = (float4*)smem + r * (16 * 64);
-  float* eb = (float*)(smem + S2F_LDS_RED) + r * (64 * S2F_EPP);
-  __syncthreads();
-  if (h == 1) {
-#pragma unroll
-    for (int m = 0; m < MW; ++m)
-#pragma unroll
-      for (int t = 0; t < NT; ++t) red[(m * NT + t) * 64 + lane] = make_float4(acc[m][t][0], acc[m][t][1], acc[m][t][2], acc[m][t][3]);
-  }
-  __syncthreads();
-  float ssum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, ssq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (h == 0) {
-#pragma unroll
-    for (int m = 0; m < MW; ++m)
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const float4 o = red[(m * NT + t) * 64 + lane];
-        acc[m][t][0] += o.x;
-        acc[m][t][1] += o.y;
-        acc[m][t][2] += o.z;
-        acc[m][t][3] += o.w;
-        *(f32x4*)(eb + (m * 16 + col) * S2F_EPP + t * 16 + g * 4) = acc[m][t];
-      }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-    store_tile_lds<false, MW * 16, NT * 16, 64, STATS ? 9 : 8>(a, eb, S2F_EPP, lane, nimg, oy0 + r * MW, ox0, co0, ssum, ssq);
-  }
-  if constexpr (STATS) bn_tile_partials(a, ssum, ssq, h == 0, r, lane, blockIdx.x, co0, (float*)smem);
-}
-
 static int plain_ep(const FwdArgs& a);
 static bool fwd_s2_shape(const ClimsrConvDesc* d, const FwdArgs& a) {
   return d->stride == 2 && d->ks == 3 && d->pad == 1 && d->up == 1 && d->cc == 32 && d->in_c % 32 == 0 && d->out_c % 64 == 0 &&
          d->in_coff % 8 == 0 && d->in_cstride % 8 == 0 && a.kcpad == 288 && plain_ep(a) == 8;
 }
 
+// the LDS-DMA kernel (conv_dma.hip conv_fwd_s2_dma_kernel); the register-staged 8-wave kernel it replaced measured
+// 352 against 332 us over the four discriminator stride-2 layers at B=32 (tools/perf_s2.py A/B, r04l)
 static int launch_fwd_s2(const ClimsrConvDesc* d, FwdArgs a, hipStream_t s) {
   a.tiles_x = ceil_div(d->out_w, 16);
   a.tiles_y = ceil_div(d->out_h, 16);
   if (g_dry) {
-    snprintf(g_dry_name, sizeof(g_dry_name), "conv_fwd_s2_kernel<%s>", a.bn_part ? "true" : "false");
+    snprintf(g_dry_name, sizeof(g_dry_name), "conv_fwd_s2_dma_kernel<%s>", a.bn_part ? "true" : "false");
     return CLIMSR_OK;
   }
-  if (int e = lds_opt_in(a.bn_part ? (const void*)conv_fwd_s2_kernel<true> : (const void*)conv_fwd_s2_kernel<false>, 160 * 1024))
-    return e;
-  const dim3 grid(a.tiles_x * a.tiles_y * a.n, d->out_c / 64);
-  if (a.bn_part) hipLaunchKernelGGL(conv_fwd_s2_kernel<true>, grid, dim3(512), S2F_LDS, s, a);
-  else hipLaunchKernelGGL(conv_fwd_s2_kernel<false>, grid, dim3(512), S2F_LDS, s, a);
-  return check_launch("conv2d_fwd (s2)");
+  const int rc = fwd_s2_dma_launch(a, s);
+  return rc == CLIMSR_OK ? check_launch("conv2d_fwd (s2 LDS-DMA)") : rc;
 }
 
 static bool dgrad_s2_shape(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const float* bias) {
@@ -2549,7 +2401,7 @@ static int plain_ep(const FwdArgs& a) {
   return 0;
 }
 
-// The convs whose epilogue can emit BatchNorm partials (EP 9 / conv_fwd_s2_kernel<true>): plain bf16 out over 16x16
+// The convs whose epilogue can emit BatchNorm partials (EP 9 / conv_fwd_s2_dma_kernel<true>): plain bf16 out over 16x16
 // tiles of 64-channel blocks -- the stride-2 kernel, or the chunk-pipelined generic kernel with >= 2 channel blocks
 // (so neither conv_pw nor conv_n16 takes it).  Mirrors the dispatch below.
 static bool bn_parts_ok(const ClimsrConvDesc* d, const FwdArgs& a, const FwdGeom& g) {

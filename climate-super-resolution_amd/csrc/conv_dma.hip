@@ -383,3 +383,231 @@ int fwd_dma_launch(int ep, const FwdArgs& a, int ncob, hipStream_t s) {
   return CLIMSR_OK;
 }
 }  // namespace climsr
+
+// ------------------------------------------------------------------------------------------
+// LDS-DMA form of the 3x3 / stride-2 / pad-1 forward (the discriminator's downsampling convs rfb_esrgan.py:30-48,
+// plain bf16 out, optionally with the BatchNorm partials of each 16 x 16 output tile).  The chunks are 16 channels,
+// moved by LDS-DMA into three 53 KB buffers -- x = [33 x 33 px][2 x 16 B], weights = [64 rows][9 taps][2 x 16 B] --
+// chunk c + 2 requested while chunk c computes (the register-staged kernel it replaced alternated staging and MFMAs
+// over one buffer: MFMA busy 0.17); 8 waves, wave w owns output rows 2w, 2w+1 (x 64 channels); a k block is a PAIR
+// of taps (lanes 0-31 tap 2kk, 32-63 tap 2kk+1, 16 channels each: 5 k blocks per chunk, the last half zero-weighted).
+// Persistent over (tile, 64-channel block) items; the epilogue stores straight from the accumulators (8 B per lane and
+// fragment) and folds the BatchNorm sums per channel through a small per-wave LDS transpose in the buffer just
+// computed.
+// ------------------------------------------------------------------------------------------
+constexpr int S2D_TP = 33;                             // input tile side of a 16 x 16 output tile
+constexpr int S2D_XI = (S2D_TP * S2D_TP * 2 + 63) / 64;  // x DMA instructions per chunk (35)
+constexpr int S2D_WI = 64 * 9 * 2 / 64;                // weight DMA instructions per chunk (18)
+constexpr int S2D_XB = S2D_XI * 1024, S2D_BUF = S2D_XB + S2D_WI * 1024;  // 54,272 B per buffer
+constexpr int S2D_RED = 64 * 17 * 4;                   // per wave: channel-sum transpose [64][17]
+constexpr int S2D_LDS = 3 * S2D_BUF;                   // 162,816 B: three chunk buffers, two chunks in flight
+static_assert(S2D_LDS <= 160 * 1024, "stride-2 LDS-DMA conv");
+static_assert(8 * S2D_RED + 8 * 2 * 64 * 4 <= S2D_BUF, "BatchNorm scratch (aliases the buffer just computed)");
+
+template <bool STATS>
+__global__ __launch_bounds__(512, 1) void conv_fwd_s2_dma_kernel(FwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
+  const int wvu = __builtin_amdgcn_readfirstlane(wave);
+  const int ntile = a.tiles_x * a.tiles_y * a.n, ncob = a.out_c / 64, nitem = ntile * ncob;
+  const int nch = a.in_c / 16;  // 16-channel chunks
+  auto decode = [&](int v, int& nimg, int& oy0, int& ox0, int& co0, int& tile) {
+    const int idx = xcd_major(v, nitem);  // a tile's channel blocks consecutive on one XCD: its x chunks hit that L2
+    tile = idx / ncob;
+    co0 = (idx - tile * ncob) * 64;
+    const int tx = tile % a.tiles_x, ty = (tile / a.tiles_x) % a.tiles_y;
+    nimg = tile / (a.tiles_x * a.tiles_y);
+    ox0 = tx * 16;
+    oy0 = ty * 16;
+  };
+  const __amdgpu_buffer_rsrc_t xr = buf_rsrc(a.x, (uint32_t)((long)a.n * a.in_h * a.in_w * a.in_cs * 2));
+  const __amdgpu_buffer_rsrc_t wr = buf_rsrc(a.w, (uint32_t)((long)ncob * 64 * a.kpk * 2));
+  // this wave's DMA pieces: x instructions wave + 8 j (j < 5), weight instructions wave + 8 j (j < 3)
+  uint32_t xo[5], wo[3];
+  auto offsets = [&](int nimg, int oy0, int ox0, int co0) {
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const int u = (wave + 8 * j) * 64 + lane, p = u >> 1, h = u & 1, r = p / S2D_TP, c = p - r * S2D_TP;
+      const int iy = 2 * oy0 - 1 + r, ix = 2 * ox0 - 1 + c;
+      const bool ok = p < S2D_TP * S2D_TP && iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w;
+      xo[j] = ok ? (uint32_t)((((nimg * a.in_h + iy) * a.in_w + ix) * a.in_cs + a.in_co + 8 * h) * 2) : BUF_OOB;
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int u = (wave + 8 * j) * 64 + lane, row = u / 18, rem = u - row * 18;
+      wo[j] = u < 64 * 18 ? (uint32_t)(((co0 + row) * a.kpk + (rem >> 1) * 32 + 8 * (rem & 1)) * 2) : BUF_OOB;
+    }
+  };
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
+  auto glds = [&](__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(off), "s"(rs), "s"(lds) : "memory");
+  };
+  // chunk c (16 channels): x source offset + 32 c bytes; weights: packing chunk c / 2 (288 elements each), half c % 2
+  auto piece = [&](int p, int c, int b) {
+    const uint32_t base = lds0 + (uint32_t)(b * S2D_BUF);
+    if (p < 5) {
+      if (wvu + 8 * p < S2D_XI) glds(xr, xo[p] == BUF_OOB ? BUF_OOB : xo[p] + (uint32_t)(32 * c), base + (uint32_t)((wvu + 8 * p) * 1024));
+    } else if (wvu + 8 * (p - 5) < S2D_WI) {
+      const uint32_t add = (uint32_t)(((c >> 1) * 288 + 16 * (c & 1)) * 2);
+      glds(wr, wo[p - 5] == BUF_OOB ? BUF_OOB : wo[p - 5] + add, base + (uint32_t)(S2D_XB + (wvu + 8 * (p - 5)) * 1024));
+    }
+  };
+  // fragment reads: k block kk, lane group g -> tap 2 kk + (g >> 1) (tap 9: read tap 8 under zero weights), half g & 1
+  const int hh = g & 1;
+  auto tap_of = [&](int kk) { return min(2 * kk + (g >> 1), 8); };
+
+  int v = blockIdx.x;
+  if (v >= nitem) return;
+  int nimg, oy0, ox0, co0, tile;
+  decode(v, nimg, oy0, ox0, co0, tile);
+  offsets(nimg, oy0, ox0, co0);
+  // chunks 0 and 1 in flight before the loop; chunk c + 2 (of this item, or of the next one) is requested during chunk
+  // c into the third buffer.  A wave's DMA pieces per chunk: 8 (waves 0, 1), 7 (wave 2), 6 (waves 3-7)
+#pragma unroll
+  for (int p = 0; p < 8; ++p) piece(p, 0, 0);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) piece(p, 1, 1);
+  const int npc = wvu < 2 ? 8 : (wvu == 2 ? 7 : 6);
+  int cur = 0;  // the buffer of the chunk being computed
+  for (;;) {
+    const int vn = v + (int)gridDim.x;
+    int nimg_n = 0, oy0_n = 0, ox0_n = 0, co0_n = 0, tile_n = 0;
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[m][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < nch; ++c, cur = cur == 2 ? 0 : cur + 1) {
+      // chunk c has landed once at most the younger requests are outstanding: the next chunk's pieces, and at chunks
+      // 0 / 1 of a later item also the previous item's 8 epilogue stores (issued between them)
+      const bool st = c < 2 && v != (int)blockIdx.x;
+      if (npc == 8) {
+        if (st) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else if (npc == 7) {
+        if (st) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+      } else {
+        if (st) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      }
+      lds_barrier();
+      // the request of this chunk: chunk c + 2 of this item, or chunk c + 2 - nch of the next one (whose offsets
+      // replace this item's once every piece of this item has been requested)
+      if (c + 2 == nch && vn < nitem) {
+        decode(vn, nimg_n, oy0_n, ox0_n, co0_n, tile_n);
+        offsets(nimg_n, oy0_n, ox0_n, co0_n);
+      }
+      const bool more = c + 2 < nch || vn < nitem;
+      const int cn = c + 2 < nch ? c + 2 : c + 2 - nch;
+      const int bn = cur == 0 ? 2 : cur - 1;  // (cur + 2) % 3
+      const char* xb = smem + cur * S2D_BUF;
+      const char* wb = xb + S2D_XB;
+      bf16x8 af[2][4], bq[2][2];
+      auto ld = [&](int kk, int s) {
+        const int tap = tap_of(kk), ky = tap / 3, kx = tap - ky * 3;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) af[s][t] = *(const bf16x8*)(wb + ((16 * t + col) * 9 + tap) * 32 + 16 * hh);
+        if (kk == 4 && g >= 2) {  // the pair's second tap of block 4 does not exist: zero weights (its B reads tap 8)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) af[s][t] = (bf16x8){};
+        }
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+          bq[s][m] = *(const bf16x8*)(xb + ((2 * (2 * wave + m) + ky) * S2D_TP + 2 * col + kx) * 32 + 16 * hh);
+      };
+      ld(0, 0);
+#pragma unroll
+      for (int kk = 0; kk < 5; ++kk) {
+        if (kk + 1 < 5) ld(kk + 1, (kk + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk & 1][t], bq[kk & 1][m], acc[m][t], 0, 0, 0);
+        if (more && kk < 4) {  // the requested chunk's 8 DMA pieces, two per k block behind its MFMAs
+          piece(2 * kk, cn, bn);
+          piece(2 * kk + 1, cn, bn);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // ---- epilogue straight from the accumulators: lane (col, g) holds channels co0 + 16 t + 4 g .. + 3 of output pixel
+    // (oy0 + 2 wave + m, ox0 + col); 8 stores per lane, issued unconditionally
+    const __amdgpu_buffer_rsrc_t ry = buf_rsrc(a.y, (uint32_t)((long)a.n * a.out_h * a.out_w * a.out_cs * 2));
+    const int ox = ox0 + col;
+    float ss[4][4] = {}, sq[4][4] = {};
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int oy = oy0 + 2 * wave + m;
+      const bool ok = oy < a.out_h && ox < a.out_w;
+      const long pix = ((long)nimg * a.out_h + oy) * a.out_w + ox;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bf16x2 p0 = {(__bf16)acc[m][t][0], (__bf16)acc[m][t][1]}, p1 = {(__bf16)acc[m][t][2], (__bf16)acc[m][t][3]};
+        typedef uint32_t v2u32_t __attribute__((ext_vector_type(2)));
+        const v2u32_t pk = {__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1)};
+        __builtin_amdgcn_raw_buffer_store_b64(pk, ry, ok ? (uint32_t)((pix * a.out_cs + a.out_co + co0 + 16 * t + 4 * g) * 2) : BUF_OOB,
+                                              0, 0);
+        if (STATS && ok) {
+          const float r[4] = {(float)p0[0], (float)p0[1], (float)p1[0], (float)p1[1]};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            ss[t][i] += r[i];
+            sq[t][i] = fmaf(r[i], r[i], sq[t][i]);
+          }
+        }
+      }
+    }
+    if constexpr (STATS) {
+      // per channel over the tile's 256 pixels: each wave transposes its column sums through its own LDS corner (sum,
+      // then square sum), lane l = channel l adds its 16 columns in order; the 8 waves meet in LDS, fixed order, fp64
+      // scratch in the buffer just computed ((cur + 2) % 3 after the loop; the other two hold the next item's chunks 0
+      // and 1 in flight), once every wave is past its fragment reads of it
+      lds_barrier();
+      const int fb = cur == 0 ? 2 : cur - 1;
+      float* red = (float*)(smem + fb * S2D_BUF) + wave * (S2D_RED / 4);
+      float* fin = (float*)(smem + fb * S2D_BUF + 8 * S2D_RED);  // [wave][2][64]
+      float cs[2];
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) red[(16 * t + 4 * g + i) * 17 + col] = st ? sq[t][i] : ss[t][i];
+        float x = 0.f;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x += red[lane * 17 + k];
+        cs[st] = x;
+      }
+      fin[wave * 128 + lane] = cs[0];
+      fin[wave * 128 + 64 + lane] = cs[1];
+      lds_barrier();
+      if (tid < 128) {
+        const int st = tid >> 6, ch = tid & 63;
+        float x = 0.f;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) x += fin[w * 128 + st * 64 + ch];
+        a.bn_part[(long)tile * 2 * a.out_c + st * a.out_c + co0 + ch] = (double)x;
+      }
+      lds_barrier();  // fin is reused by the next item
+    }
+    if (vn >= nitem) break;
+    v = vn;
+    nimg = nimg_n; oy0 = oy0_n; ox0 = ox0_n; co0 = co0_n; tile = tile_n;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+namespace climsr {
+int fwd_s2_dma_launch(const FwdArgs& a, hipStream_t s) {
+  void (*k)(FwdArgs) = a.bn_part ? conv_fwd_s2_dma_kernel<true> : conv_fwd_s2_dma_kernel<false>;
+  if (int e = lds_opt_in((const void*)k, S2D_LDS)) return e;
+  const int nitem = a.tiles_x * a.tiles_y * a.n * (a.out_c / 64);
+  const int grid = std::min(nitem, device_cus());
+  hipLaunchKernelGGL(k, dim3(grid), dim3(512), S2D_LDS, s, a);
+  return CLIMSR_OK;
+}
+}  // namespace climsr

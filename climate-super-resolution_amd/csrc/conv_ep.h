@@ -317,4 +317,6 @@ __device__ __forceinline__ void bn_tile_partials(const FwdArgs& a, float* ssum, 
 namespace climsr {
 constexpr int DMA_TH = 32;
 int fwd_dma_launch(int ep, const FwdArgs& a, int ncob, hipStream_t s);
+// stride-2 3x3 forward, plain bf16 out (+ BatchNorm partials when a.bn_part), 16 x 16 tiles (a.tiles_x / tiles_y)
+int fwd_s2_dma_launch(const FwdArgs& a, hipStream_t s);
 }  // namespace climsr

@@ -522,7 +522,7 @@ def test_conv_dgrad_stride2_bf16(cin, cout, h, w, act):
 @pytest.mark.parametrize("cin,cout,h,w", [(64, 64, 64, 48), (64, 128, 34, 20), (128, 64, 16, 16), (96, 64, 40, 66)])
 def test_conv_fwd_stride2_plain_bf16(cin, cout, h, w):
     """The discriminator's stride-2 convs as its forward runs them (rfb_esrgan.py:30-48): no bias, no activation,
-    bf16 out for the BatchNorm (conv_fwd_s2_kernel: 8 waves over two tap groups; ragged 17-row / 10- and 33-column
+    bf16 out for the BatchNorm (conv_fwd_s2_dma_kernel: LDS-DMA, three chunk buffers; ragged 17-row / 10- and 33-column
     output tiles included) vs F.conv2d in float64 on the same bf16 operands.  Tolerance: bf16 rounding."""
     n = 2
     p, wt, _b = make_plan(cin, cout, 3, stride=2, bias=False)
