@@ -2951,10 +2951,13 @@ struct W64 {
 
 // TS = 2: 8 waves, wave w owns ci block w & 3 and taps [0,5) or [5,9) (w >> 2): 20 accumulators instead of 36, so
 // two waves share each SIMD (latency hiding) at the price of each wave re-reading the shared dz fragments.
-// G (TS 1, S 1): the LDS-DMA form -- see conv_wgrad64_glds_kernel below.
+// G (TS 1): the LDS-DMA form -- see conv_wgrad64_glds_kernel below.
+#ifndef CLIMSR_W64S2_GLDS
+#define CLIMSR_W64S2_GLDS 1  // A/B builds only (tools/diag_build.sh): 0 = the register-staged stride-2 kernel
+#endif
 template <int TS, int S, bool G>
 __device__ __forceinline__ void wgrad64_body(const WgArgs& a) {
-  static_assert(!G || (TS == 1 && S == 1), "LDS-DMA form: 256 threads, stride 1");
+  static_assert(!G || TS == 1, "LDS-DMA form: 256 threads");
   constexpr int NTHR = 256 * TS, NU = TS == 1 ? 9 : 5;
   constexpr int TH = W64<S>::TH, TPW = W64<S>::TPW, NZ = W64<S>::NZ, NX = W64<S>::NX, XP = W64<S>::XP;
   extern __shared__ __attribute__((aligned(16))) char smem[];  // TS 1: two buffers of W64<S>::LDS
@@ -3100,20 +3103,27 @@ __device__ __forceinline__ void wgrad64_body(const WgArgs& a) {
     // lane l of an instruction fills pixel slot 8 i + (l >> 3), 16 B position l & 7, with that pixel's channel chunk
     // (l & 7) ^ (column & 7) -- an XOR swizzle chosen on the global (source) side that spreads the 8 pixels of a
     // transposed fragment read over all 64 banks, as the register path's 80-element pitch did.
-    constexpr int ZB = TH * TW * 128, XB = 24 * 1024, BUF = ZB + XB, NXP = W64<1>::TPH * TPW;
+    // per wave and tile: NZI dz and NXI x instructions (stride 1: 4 + 6, stride 2: 2 + 10)
+    constexpr int NZI = TH / 2, NXI = S == 1 ? 6 : 10;
+    constexpr int ZB = TH * TW * 128, XB = 4 * NXI * 1024, BUF = ZB + XB, NXP = W64<S>::TPH * TPW;
+    static_assert(4 * NXI * 8 >= NXP && 3 * BUF <= 160 * 1024, "LDS-DMA wgrad64 tile buffers");
     const int l8 = lane >> 3, c8 = lane & 7, wv = tid >> 6;
-    // dz: wave w issues instructions w + 4 j (j < 4): tile row (w >> 1) + 2 j, column 8 (w & 1) + l8
+    // dz: wave w issues instructions w + 4 j (j < NZI): tile row (w >> 1) + 2 j, column 8 (w & 1) + l8
     const int zcol = 8 * (wv & 1) + l8, zrow0 = wv >> 1;
     const uint32_t zrow_b = (uint32_t)a.out_w * a.dz_cs * 2;
     const uint32_t z_lane = (uint32_t)((zcol * a.dz_cs + co0 + 8 * (c8 ^ (zcol & 7))) * 2) + (uint32_t)zrow0 * zrow_b;
     const __amdgpu_buffer_rsrc_t zrs = buf_rsrc(a.dz, (uint32_t)((long)a.n * a.out_h * a.out_w * a.dz_cs * 2));
-    // x: instructions w + 4 j (j < 6): footprint pixel 8 (w + 4 j) + l8 of the 10 x 18 footprint (180 pixels; the
-    // slots past it get zeros): (row << 16) | (column << 8) | source chunk
-    int xrc[6];
+    // x: instructions w + 4 j (j < NXI): footprint slot 8 (w + 4 j) + l8 of the 10 x 18 (stride 2: 9 x 33) footprint
+    // (the slots past it get zeros): (row << 16) | (column << 8) | source chunk.  Stride 2 stores each footprint row's
+    // 17 even columns first, then its 16 odd ones: the stride-2 pixels 2 c + dx of a fragment read then sit in
+    // consecutive slots, alternating bank halves as the stride-1 reads do (in column order all of them would share one
+    // half of the 64 banks: two-way conflicts)
+    int xrc[NXI];
 #pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      const int P = 8 * (wv + 4 * j) + l8, row = P < NXP ? P / TPW : 1023, cx = P % TPW;
-      xrc[j] = (row << 16) | (cx << 8) | (c8 ^ (cx & 7));
+    for (int j = 0; j < NXI; ++j) {
+      const int P = 8 * (wv + 4 * j) + l8, row = P < NXP ? P / TPW : 1023, slot = P % TPW;
+      const int cx = S == 1 ? slot : (slot < (TPW + 1) / 2 ? 2 * slot : 2 * (slot - (TPW + 1) / 2) + 1);
+      xrc[j] = (row << 16) | (cx << 8) | (c8 ^ (slot & 7));
     }
     const uint32_t ximg_b = (uint32_t)a.in_h * a.in_w * a.in_cs * 2, pxb = (uint32_t)a.in_cs * 2;
     const uint32_t x_ch = (uint32_t)((a.in_co + ci0) * 2);
@@ -3122,7 +3132,7 @@ __device__ __forceinline__ void wgrad64_body(const WgArgs& a) {
     int ntx = split % a.tiles_x, nty = (split / a.tiles_x) % a.tiles_y, nn = split / (a.tiles_x * a.tiles_y);
     // in asm, not __builtin_amdgcn_raw_ptr_buffer_load_lds: hipcc treats the builtin as an LDS write of unknown
     // extent and waits vmcnt(0) before the next ds_read, i.e. for the tile just requested; hidden from it, the DMAs
-    // are counted by hand (vmcnt(10) below) and drained before the epilogue.  M0 (the wave's LDS destination) is set
+    // are counted by hand (vmcnt(NZI + NXI) below) and drained before the epilogue.  M0 (the wave's LDS destination) is set
     // and restored inside the statement.
     const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
     const int wvu = __builtin_amdgcn_readfirstlane(wv);  // provably wave-uniform: the LDS destination is an "s" operand
@@ -3145,13 +3155,13 @@ __device__ __forceinline__ void wgrad64_body(const WgArgs& a) {
       const uint32_t zt = (uint32_t)(((nimg * a.out_h + oy0) * a.out_w + ox0) * a.dz_cs * 2) + z_lane;
       const bool zok = live & (ox0 + zcol < a.out_w);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NZI; ++j) {
         const bool ok = zok & (oy0 + zrow0 + 2 * j < a.out_h);
         glds(zrs, ok ? zt + (uint32_t)(2 * j) * zrow_b : BUF_OOB, zb + (uint32_t)((wvu + 4 * j) * 1024));
       }
-      const uint32_t iy0 = (uint32_t)(oy0 - a.pad), ix0 = (uint32_t)(ox0 - a.pad), xt = (uint32_t)nimg * ximg_b + x_ch;
+      const uint32_t iy0 = (uint32_t)(S * oy0 - a.pad), ix0 = (uint32_t)(S * ox0 - a.pad), xt = (uint32_t)nimg * ximg_b + x_ch;
 #pragma unroll
-      for (int j = 0; j < 6; ++j) {
+      for (int j = 0; j < NXI; ++j) {
         const uint32_t iy = iy0 + (uint32_t)(xrc[j] >> 16), ix = ix0 + (uint32_t)((xrc[j] >> 8) & 255);
         const bool ok = live & (iy < (uint32_t)lh) & (ix < (uint32_t)lw);
         const uint32_t off = xt + ((iy >> upsh) * (uint32_t)a.in_w + (ix >> upsh)) * pxb + (uint32_t)((xrc[j] & 7) * 16);
@@ -3159,28 +3169,32 @@ __device__ __forceinline__ void wgrad64_body(const WgArgs& a) {
       }
     };
     // fragment reads: k-step kk, lane (g, q, p) = output pixel c0 = 4 g + q of rows 2 kk (k0) and 2 kk + 1 (k1),
-    // channels 4 p.. of the 16-channel group: dz group t (chunk 2 t + (p >> 1)), x group wave (chunk 2 wave + (p >> 1))
+    // channels 4 p.. of the 16-channel group: dz group t (chunk 2 t + (p >> 1)), x group wave (chunk 2 wave + (p >> 1));
+    // tap column dx reads footprint column S c0 + dx (its slot)
     const int c0 = 4 * g + q;
     int zoff[4], xoff[3];
 #pragma unroll
     for (int t = 0; t < 4; ++t) zoff[t] = c0 * 128 + (((2 * t + (p >> 1)) ^ (c0 & 7)) << 4) + 8 * (p & 1);
 #pragma unroll
-    for (int dx = 0; dx < 3; ++dx) xoff[dx] = (c0 + dx) * 128 + (((2 * wave + (p >> 1)) ^ ((c0 + dx) & 7)) << 4) + 8 * (p & 1);
+    for (int dx = 0; dx < 3; ++dx) {
+      const int sl = S == 1 ? c0 + dx : (dx == 1 ? (TPW + 1) / 2 + c0 : c0 + dx / 2);
+      xoff[dx] = sl * 128 + (((2 * wave + (p >> 1)) ^ (sl & 7)) << 4) + 8 * (p & 1);
+    }
     auto ld_af = [&](const char* zb, int kk, bf16x8 (&af)[4]) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) af[t] = cat_tr(ds_read_tr16(zb + kk * 32 * 128 + zoff[t]), ds_read_tr16(zb + (kk * 32 + 16) * 128 + zoff[t]));
     };
     auto ld_bf = [&](const char* xb, int kk, int u) {
       const int dy = u / 3, dx = u % 3;
-      return cat_tr(ds_read_tr16(xb + (2 * kk + dy) * TPW * 128 + xoff[dx]), ds_read_tr16(xb + (2 * kk + 1 + dy) * TPW * 128 + xoff[dx]));
+      return cat_tr(ds_read_tr16(xb + (S * 2 * kk + dy) * TPW * 128 + xoff[dx]), ds_read_tr16(xb + (S * (2 * kk + 1) + dy) * TPW * 128 + xoff[dx]));
     };
     issue(tile < a.ntiles, 0);
     issue(tile + a.nsplit < a.ntiles, 1);
     int cur = 0;
     for (; tile < a.ntiles; tile += a.nsplit) {
-      // this tile's 10 DMAs (per wave) have landed once at most the next tile's 10 are outstanding; the barrier makes
-      // that true for every wave, and every wave is past its reads of the tile before last (buffer (cur + 2) % 3)
-      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      // this tile's NZI + NXI DMAs (per wave) have landed once at most the next tile's are outstanding; the barrier
+      // makes that true for every wave, and every wave is past its reads of the tile before last (buffer (cur + 2) % 3)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NZI + NXI) : "memory");
       __builtin_amdgcn_s_barrier();
       issue(tile + 2 * a.nsplit < a.ntiles, cur == 0 ? 2 : cur - 1);
       const char* zb = smem + cur * BUF;
@@ -3281,7 +3295,8 @@ __device__ __forceinline__ void wgrad64_body(const WgArgs& a) {
   }
 }
 constexpr size_t W64_EP_LDS = (size_t)64 * (9 * 64 + 4) * 4;  // the slab staging of conv_wgrad64_kernel
-constexpr size_t W64G_LDS = (size_t)3 * (8 * 16 * 128 + 24 * 1024);  // three LDS-DMA tile buffers (G form)
+constexpr size_t W64G_LDS = (size_t)3 * (8 * 16 * 128 + 24 * 1024);     // three LDS-DMA tile buffers (G form)
+constexpr size_t W64G2_LDS = (size_t)3 * (4 * 16 * 128 + 40 * 1024);    // (G form, stride 2)
 
 template <int TS, int S = 1>
 __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
@@ -3290,6 +3305,7 @@ __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
 // at most 256 registers (one workgroup per CU either way: 148 KB of LDS): the accumulators stay in VGPRs -- the
 // 512-register form kept some of them in AGPRs and shuffled them every tile
 __global__ __launch_bounds__(256, 2) void conv_wgrad64_glds_kernel(WgArgs a) { wgrad64_body<1, 1, true>(a); }
+__global__ __launch_bounds__(256, 2) void conv_wgrad64_glds_s2_kernel(WgArgs a) { wgrad64_body<1, 2, true>(a); }
 
 // ------------------------------------------------------------------------------------------
 // Weight gradient of a 1x1 conv with 64 inputs and <= 64 outputs (srcnn.conv2): dW[co][ci] = sum_p dz[p][co]
@@ -3687,7 +3703,12 @@ extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, c
     const bool ts2 = d->stride == 1 && (long)d->n * d->out_h * d->out_w >= (1L << 20);
     a.xcd = 1;
     const dim3 grid = dim3((d->out_c / 64) * (d->in_c / 64) * nsplit);
-    if (d->stride == 2) {
+    if (d->stride == 2 && CLIMSR_W64S2_GLDS) {
+      a.tph = W64<2>::TPH; a.tpw = W64<2>::TPW;
+      if (dry_run("conv_wgrad64_glds_s2_kernel")) return CLIMSR_OK;
+      if (int e = lds_opt_in((const void*)conv_wgrad64_glds_s2_kernel, 160 * 1024)) return e;
+      hipLaunchKernelGGL(conv_wgrad64_glds_s2_kernel, grid, dim3(256), std::max(W64G2_LDS, W64_EP_LDS), (hipStream_t)stream, a);
+    } else if (d->stride == 2) {
       a.tph = W64<2>::TPH; a.tpw = W64<2>::TPW;
       if (dry_run("conv_wgrad64_kernel<1, 2>")) return CLIMSR_OK;
       if (int e = lds_opt_in((const void*)conv_wgrad64_kernel<1, 2>, 160 * 1024)) return e;

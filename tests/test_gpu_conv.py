@@ -263,6 +263,28 @@ def test_conv_wgrad_matches_autograd(cin, cout, ks, stride, up):
     check_close(p.gb.cpu(), gb, tol=2e-5, what="bgrad")
 
 
+@pytest.mark.parametrize("cin,cout,n,h,w", [(64, 64, 3, 37, 45), (128, 64, 2, 9, 33), (64, 128, 1, 64, 64)])
+def test_conv_wgrad64_stride2_ragged(cin, cout, n, h, w):
+    """Stride-2 64-block weight gradient (conv_wgrad64_glds_s2_kernel) on odd / ragged sizes: partial 4 x 16 output
+    tiles, footprints past the bottom / right edge (zero-filled by the LDS-DMA), one image, two 64-row co blocks."""
+    p, wt, b = make_plan(cin, cout, 3, 2)
+    g = torch.Generator().manual_seed(7)
+    x = bf(torch.rand((n, cin, h, w), generator=g) * 2 - 1)
+    oh, ow = p.out_hw(h, w, 1)
+    dz = bf(torch.rand((n, cout, oh, ow), generator=g) * 2 - 1)
+    xb, dzb = to_nhwc(x), to_nhwc(dz)
+    p.gw = torch.zeros_like(p.weight)
+    p.gb = torch.zeros_like(p.bias)
+    p.wgrad(xb, xb.shape[-1], 0, h, w, dzb, dzb.shape[-1], n, Workspace(), accumulate=False)
+    torch.cuda.synchronize()
+    wr = bf(wt).double().requires_grad_(True)
+    br = b.double().requires_grad_(True)
+    y = F.conv2d(x.double(), wr, br, stride=2, padding=1)
+    gw, gb = torch.autograd.grad(y, (wr, br), dz.double())
+    check_close(p.gw.cpu(), gw, tol=2e-5, what="wgrad s2")
+    check_close(p.gb.cpu(), gb, tol=2e-5, what="bgrad s2")
+
+
 @pytest.mark.parametrize("cin,ks,n,h,w", [(64, 3, 3, 70, 150), (32, 5, 2, 45, 131), (16, 3, 1, 9, 64), (48, 5, 2, 33, 65)])
 def test_conv_wgrad_single_output_channel(cin, ks, n, h, w):
     """conv_last / srcnn.conv3 weight gradient on the Toeplitz-fragment MFMA kernel: several 64-column strips,
