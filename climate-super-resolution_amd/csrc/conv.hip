@@ -1055,11 +1055,19 @@ static int launch_n16(const FwdArgs& a, hipStream_t s) {
 //     T[y][x'][kx] = sum_{ky, ci} x[y + ky - R][x'][ci] * w[ky][kx][ci]        (M = x', N = kx, K = ky x ci)
 //     out[y][x]    = sum_kx T[y][x + kx - R][kx]                               (shift-sum through LDS)
 // so the 16-wide N tile carries KS useful columns instead of 1 (KS/16 vs 1/16 of the MFMA).  A wave
-// computes 4 output rows x 64 columns (5 M-fragments of x'), streaming its 4 + KS - 1 input rows straight
+// computes ROWS output rows x 64 columns (5 M-fragments of x'), streaming its ROWS + KS - 1 input rows straight
 // from global memory (16 B per lane, next row in flight during the current row's MFMAs); every input row
-// feeds the up-to-4 output rows it touches.  Weights sit in VGPRs for the whole wave.
+// feeds the up-to-KS output rows it touches.  Output row r is complete once input row r + KS - 1 is in: its
+// shift-sum and store run right there and its accumulators take row r + KS, so a ring of min(KS, ROWS) rows is
+// live -- which lets the 3x3 / 5x5 forms stream 16 rows per wave (input rows fetched 18/16 or 20/16 times instead
+// of 6/4 or 8/4: conv_last read 1.76x its input at 4 rows).  Weights sit in VGPRs for the whole wave.
 // ------------------------------------------------------------------------------------------
-constexpr int CO1M_NF = 5, CO1M_COLS = 64, CO1M_ROWS = 4;
+constexpr int CO1M_NF = 5, CO1M_COLS = 64;
+template <int KS>
+struct Co1m {
+  static constexpr int ROWS = KS <= 5 ? 16 : 4;                  // output rows per wave
+  static constexpr int NSLOT = KS < ROWS ? KS : ROWS;            // live accumulator rows
+};
 
 static bool co1m_shape(const ClimsrConvDesc* d) {
   return d->out_c == 1 && d->stride == 1 && d->up == 1 && (d->ks == 3 || d->ks == 5 || d->ks == 9) && d->pad == d->ks / 2 &&
@@ -1068,10 +1076,10 @@ static bool co1m_shape(const ClimsrConvDesc* d) {
 
 template <int KS, int NCH>
 __global__ __launch_bounds__(256, 2) void conv_co1m_kernel(FwdArgs a) {
-  constexpr int R = KS / 2, NR = CO1M_ROWS + KS - 1;
+  constexpr int R = KS / 2, ROWS = Co1m<KS>::ROWS, NSLOT = Co1m<KS>::NSLOT, NR = ROWS + KS - 1;
   __shared__ float sc[4][CO1M_NF * 16][17];  // per-wave T rows (x' x kx), padded pitch
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
-  const int x0 = blockIdx.x * CO1M_COLS, y0 = (blockIdx.y * 4 + wave) * CO1M_ROWS, nimg = blockIdx.z;
+  const int x0 = blockIdx.x * CO1M_COLS, y0 = (blockIdx.y * 4 + wave) * ROWS, nimg = blockIdx.z;
   // B fragments: B[k = ci][n = kx] of tap row ky, channel block c (packed row 0: k = (ci/cc)*kcpad + tap*cc + ci%cc)
   bf16x8 bw[KS][NCH];
 #pragma unroll
@@ -1083,9 +1091,9 @@ __global__ __launch_bounds__(256, 2) void conv_co1m_kernel(FwdArgs a) {
       if (col < KS && ci < a.in_c)
         bw[ky][c] = *(const bf16x8*)(a.w + (long)(ci / a.cc) * a.kcpad + (ky * KS + col) * a.cc + (ci % a.cc));
     }
-  f32x4 acc[CO1M_ROWS][CO1M_NF];
+  f32x4 acc[NSLOT][CO1M_NF];
 #pragma unroll
-  for (int r = 0; r < CO1M_ROWS; ++r)
+  for (int r = 0; r < NSLOT; ++r)
 #pragma unroll
     for (int f = 0; f < CO1M_NF; ++f) acc[r][f] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
@@ -1106,30 +1114,18 @@ __global__ __launch_bounds__(256, 2) void conv_co1m_kernel(FwdArgs a) {
       }
     }
   };
-  load_row(0, 0);
-#pragma unroll
-  for (int iyr = 0; iyr < NR; ++iyr) {
-    if (iyr + 1 < NR) load_row((iyr + 1) & 1, iyr + 1);
-#pragma unroll
-    for (int ky = 0; ky < KS; ++ky) {
-      const int r = iyr - ky;  // output row fed by input row iyr through tap row ky
-      if (r < 0 || r >= CO1M_ROWS) continue;
-#pragma unroll
-      for (int f = 0; f < CO1M_NF; ++f)
-#pragma unroll
-        for (int c = 0; c < NCH; ++c)
-          acc[r][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[iyr & 1][f][c], bw[ky][c], acc[r][f], 0, 0, 0);
-    }
-  }
-  // shift-sum: out[x0 + l] = sum_kx T[x' = l + kx][kx]; then the fused epilogue (same as conv_co1_kernel)
+  // shift-sum of output row r (slot r % NSLOT): out[x0 + l] = sum_kx T[x' = l + kx][kx]; then the fused epilogue
+  // (same as conv_co1_kernel); the slot is cleared for row r + NSLOT
   const float bias = a.bias ? a.bias[0] : 0.f;
   const bool f1 = a.res_f32 & 1;
-#pragma unroll
-  for (int r = 0; r < CO1M_ROWS; ++r) {
+  auto finish = [&](int r) {
+    const int sl = r % NSLOT;
 #pragma unroll
     for (int f = 0; f < CO1M_NF; ++f)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) sc[wave][f * 16 + g * 4 + i][col] = acc[r][f][i];
+      for (int i = 0; i < 4; ++i) sc[wave][f * 16 + g * 4 + i][col] = acc[sl][f][i];
+#pragma unroll
+    for (int f = 0; f < CO1M_NF; ++f) acc[sl][f] = (f32x4){0.f, 0.f, 0.f, 0.f};
     float v = 0.f;
 #pragma unroll
     for (int kx = 0; kx < KS; ++kx) v += sc[wave][lane + kx][kx];
@@ -1145,6 +1141,26 @@ __global__ __launch_bounds__(256, 2) void conv_co1m_kernel(FwdArgs a) {
       else ((float*)a.y)[ob] = v;
       if (a.aux) a.aux[pidx * a.aux_cs + a.aux_co] = f2bf(a.aux_scale * v);
     }
+  };
+  load_row(0, 0);
+#pragma unroll
+  for (int iyr = 0; iyr < NR; ++iyr) {
+    if (iyr + 1 < NR) load_row((iyr + 1) & 1, iyr + 1);
+#pragma unroll
+    for (int ky = KS - 1; ky >= 0; --ky) {  // oldest row first: row iyr - KS + 1 completes here
+      const int r = iyr - ky;  // output row fed by input row iyr through tap row ky
+      if (r < 0 || r >= ROWS) continue;
+#pragma unroll
+      for (int f = 0; f < CO1M_NF; ++f)
+#pragma unroll
+        for (int c = 0; c < NCH; ++c)
+          acc[r % NSLOT][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[iyr & 1][f][c], bw[ky][c], acc[r % NSLOT][f], 0, 0, 0);
+      if (NSLOT < ROWS && ky == KS - 1) finish(r);
+    }
+  }
+  if constexpr (NSLOT == ROWS) {  // no slot reuse (9x9): every row finishes after the stream, as fewer registers stay live
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) finish(r);
   }
 }
 
@@ -1154,7 +1170,7 @@ static int launch_co1m(const FwdArgs& a, hipStream_t s) {
     snprintf(g_dry_name, sizeof(g_dry_name), "conv_co1m_kernel<%d, %d>", KS, NCH);
     return CLIMSR_OK;
   }
-  dim3 grid(ceil_div(a.out_w, CO1M_COLS), ceil_div(a.out_h, 4 * CO1M_ROWS), a.n);
+  dim3 grid(ceil_div(a.out_w, CO1M_COLS), ceil_div(a.out_h, 4 * Co1m<KS>::ROWS), a.n);
   hipLaunchKernelGGL((conv_co1m_kernel<KS, NCH>), grid, dim3(256), 0, s, a);
   return check_launch("conv2d_fwd (co1m)");
 }

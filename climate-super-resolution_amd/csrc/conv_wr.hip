@@ -53,7 +53,9 @@ struct WrArgs {
 typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
 typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 
-template <int EP>
+// ACT: the activation as a template parameter (0 none, 1 leaky relu, 2 relu; EP 2: 3 / 4 their backward) -- as a
+// kernel argument it cost a three-way uniform branch per accumulator element (~390 branch instructions per tile)
+template <int EP, int ACT>
 __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // vector-memory operations of one epilogue (loads + stores), fixed per lane
@@ -80,11 +82,16 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
 
   // ---- footprint DMA: instruction i, lane l fills 16 B slot q = 64 i + l = (pixel q / 10, slot q % 10); slots 8, 9
   // of a pixel (the pitch padding) and slots past the footprint get zeros (out-of-range source offset)
+  // rel: the slot's source offset from the footprint's corner pixel for an interior tile without upsampling (pad
+  // slots: 2^31, past every buffer's range), so such a tile's DMA offsets are one add each
   int dg[WR_NI];
+  uint32_t rel[WR_NI];
 #pragma unroll
   for (int i = 0; i < WR_NI; ++i) {
     const int q = i * 64 + lane, p = q / WR_SPP, c = q - p * WR_SPP;
-    dg[i] = (p < WR_PR * WR_PC && c < 8) ? ((p / WR_PC) << 16) | ((p % WR_PC) << 8) | c : -1;
+    const bool live = p < WR_PR * WR_PC && c < 8;
+    dg[i] = live ? ((p / WR_PC) << 16) | ((p % WR_PC) << 8) | c : -1;
+    rel[i] = live ? (uint32_t)((((p / WR_PC) * a.in_w + p % WR_PC) * a.in_cs + c * 8) * 2) : 0x80000000u;
   }
   const __amdgpu_buffer_rsrc_t xr = buf_rsrc(a.x, a.x_bytes);
   const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
@@ -107,12 +114,19 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
     int nimg = 0, oy0 = -1 << 20, ox0 = 0;
     if (tile >= 0) decode(tile, nimg, oy0, ox0);
     const uint32_t dst = mybuf + (uint32_t)(b * WR_BUF);
+    if (ups == 0 && oy0 >= 1 && oy0 - 1 + WR_PR <= a.in_h && ox0 >= 1 && ox0 - 1 + WR_PC <= a.in_w) {
+      // interior (wave-uniform): the corner's offset on the scalar unit, one add per instruction
+      const uint32_t base = (uint32_t)((((nimg * a.in_h + oy0 - 1) * a.in_w + ox0 - 1) * a.in_cs + a.in_co) * 2);
 #pragma unroll
-    for (int i = 0; i < WR_NI; ++i) {
-      const int iy = oy0 - 1 + (dg[i] >> 16), ix = ox0 - 1 + ((dg[i] >> 8) & 255), c = dg[i] & 255;
-      const bool ok = dg[i] >= 0 && iy >= 0 && iy < lh && ix >= 0 && ix < lw;
-      const uint32_t off = (uint32_t)((((long)(nimg * a.in_h + (iy >> ups)) * a.in_w + (ix >> ups)) * a.in_cs + a.in_co + c * 8) * 2);
-      glds(ok ? off : BUF_OOB, dst + (uint32_t)(i * 1024));
+      for (int i = 0; i < WR_NI; ++i) glds(base + rel[i], dst + (uint32_t)(i * 1024));
+    } else {
+#pragma unroll
+      for (int i = 0; i < WR_NI; ++i) {
+        const int iy = oy0 - 1 + (dg[i] >> 16), ix = ox0 - 1 + ((dg[i] >> 8) & 255), c = dg[i] & 255;
+        const bool ok = dg[i] >= 0 && iy >= 0 && iy < lh && ix >= 0 && ix < lw;
+        const uint32_t off = (uint32_t)((((long)(nimg * a.in_h + (iy >> ups)) * a.in_w + (ix >> ups)) * a.in_cs + a.in_co + c * 8) * 2);
+        glds(ok ? off : BUF_OOB, dst + (uint32_t)(i * 1024));
+      }
     }
   };
 
@@ -184,10 +198,10 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
           if constexpr (EP == 2) {
             const uint32_t w = i < 2 ? rv[m][t].x : rv[m][t].y;
             const float r = __uint_as_float((i & 1) ? (w & 0xFFFF0000u) : (w << 16));
-            x = r > 0.f ? x : (a.act == 3 ? x * a.slope : 0.f);
+            x = r > 0.f ? x : (ACT == 3 ? x * a.slope : 0.f);
           } else {
-            if (a.act == 1) x = x > 0.f ? x : x * a.slope;
-            else if (a.act == 2) x = x > 0.f ? x : 0.f;
+            if constexpr (ACT == 1) x = x > 0.f ? x : x * a.slope;
+            else if constexpr (ACT == 2) x = x > 0.f ? x : 0.f;
             if constexpr (EP == 1) {
               const uint32_t w = i < 2 ? rv[m][t].x : rv[m][t].y;
               const float r = __uint_as_float((i & 1) ? (w & 0xFFFF0000u) : (w << 16));
@@ -277,7 +291,7 @@ int conv_wr_launch(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const uint
   const long opx = (long)d->n * d->out_h * d->out_w;
   if (epk < 0 || kpk < 576) return -1;
   if (dry) {
-    snprintf(name, name_len, "conv_wr_kernel<%d>", epk);
+    snprintf(name, name_len, "conv_wr_kernel<%d, %d>", epk, ep->act);
     return CLIMSR_OK;
   }
   WrArgs a;
@@ -293,8 +307,18 @@ int conv_wr_launch(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const uint
   a.r1_bytes = res ? (uint32_t)(opx * ep->res1_cstride * 2) : 0u;
   const int ncu = device_cus();
   const int grid = std::min(ceil_div(a.ntiles, 4), ncu);
-  void (*k)(WrArgs) = epk == 0 ? conv_wr_kernel<0> : epk == 1 ? conv_wr_kernel<1> : epk == 2 ? conv_wr_kernel<2>
-                      : epk == 3 ? conv_wr_kernel<3> : conv_wr_kernel<4>;
+  // [epilogue][activation] (EP 1: no activation; EP 2: 3 / 4)
+  static void (*const kt[5][5])(WrArgs) = {
+      {conv_wr_kernel<0, 0>, conv_wr_kernel<0, 1>, conv_wr_kernel<0, 2>, nullptr, nullptr},
+      {conv_wr_kernel<1, 0>, nullptr, nullptr, nullptr, nullptr},
+      {nullptr, nullptr, nullptr, conv_wr_kernel<2, 3>, conv_wr_kernel<2, 4>},
+      {conv_wr_kernel<3, 0>, conv_wr_kernel<3, 1>, conv_wr_kernel<3, 2>, nullptr, nullptr},
+      {conv_wr_kernel<4, 0>, conv_wr_kernel<4, 1>, conv_wr_kernel<4, 2>, nullptr, nullptr}};
+  void (*k)(WrArgs) = (ep->act >= 0 && ep->act < 5) ? kt[epk][ep->act] : nullptr;
+  if (!k) {
+    set_error("conv2d_fwd (wr): epilogue %d with activation %d", epk, ep->act);
+    return CLIMSR_EINVAL;
+  }
   const int lds = (epk == 3 || epk == 4) ? WR_LDS_ALL : WR_LDS;
   if (int e = lds_opt_in((const void*)k, WR_LDS_ALL)) return e;
   hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, s, a);

@@ -690,7 +690,7 @@ def test_conv_wr_fp32_out_channel_sums(n, h, w, f32):
     finally:
         ops.PROFILER = None
     torch.cuda.synchronize()
-    assert names and names[-1].startswith("conv_wr_kernel<3>" if f32 else "conv_wr_kernel<4>"), names
+    assert names and names[-1].startswith("conv_wr_kernel<3," if f32 else "conv_wr_kernel<4,"), names
     want = F.conv2d(x.double(), bf(wt).double(), b.double(), padding=1)
     check_close(from_nhwc(y, 64).cpu(), want, 1e-5 if f32 else 2 ** -8, "out")
     sums = part.double().cpu().reshape(n, tpi, 64).sum(1)
