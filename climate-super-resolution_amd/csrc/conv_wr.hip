@@ -200,7 +200,7 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
             const float r = __uint_as_float((i & 1) ? (w & 0xFFFF0000u) : (w << 16));
             x = r > 0.f ? x : (ACT == 3 ? x * a.slope : 0.f);
           } else {
-            if constexpr (ACT == 1) x = x > 0.f ? x : x * a.slope;
+            if constexpr (ACT == 1) x = fmaxf(x, x * a.slope);  // = (x > 0 ? x : slope x) for 0 <= slope <= 1 (host)
             else if constexpr (ACT == 2) x = x > 0.f ? x : 0.f;
             if constexpr (EP == 1) {
               const uint32_t w = i < 2 ? rv[m][t].x : rv[m][t].y;
@@ -262,7 +262,7 @@ int conv_wr_ep(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const float* b
   else if (ep->out_mode == 0 && res && (ep->act == 3 || ep->act == 4) && !bias && !(ep->res_f32 & 1)) epk = 2;
   else if (ep->out_mode == 1 && !res && ep->act >= 0 && ep->act <= 2) epk = 3;
   const long opx = (long)d->n * d->out_h * d->out_w;
-  if (epk < 0 || (ep->ch_part && epk != 3 && epk != 4) || d->in_c != 64 || d->out_c != 64 || d->cc != 64 || d->ks != 3 || d->stride != 1 ||
+  if (epk < 0 || (ep->ch_part && epk != 3 && epk != 4) || (ep->act == 1 && !(ep->slope >= 0.f && ep->slope <= 1.f)) || d->in_c != 64 || d->out_c != 64 || d->cc != 64 || d->ks != 3 || d->stride != 1 ||
       d->pad != 1 || (d->up != 1 && d->up != 2) || d->out_h != d->in_h * d->up || d->out_w != d->in_w * d->up ||
       d->in_cstride % 8 || d->in_coff % 8 || (d->out_cstride | d->out_coff) & 3 || ep->down2 || ep->res2 || ep->aux ||
       ep->bn_part || (res && ((ep->res1_cstride | ep->res1_coff) & 3)) ||
