@@ -1,5 +1,5 @@
 # conv_wr with the activation as a template parameter and one-add DMA offsets for interior tiles: the conv / RCAN
-# parity suites, A/B timing against the previous conv_wr (diag/wrold), stride-2 wgrad A/B (diag/w64s2old), GAN bench.
+# parity suites, A/B timing against the previous conv_wr (diag/wrold; diag/wrmid: templated, DMA issued at the tile's start), stride-2 wgrad A/B (diag/w64s2old), GAN bench.
 #   usage: bash tools/gpu_r04n.sh <tag>
 set -o pipefail
 mkdir -p gpurun_out
@@ -9,6 +9,7 @@ D=$PWD/climate-super-resolution_amd/csrc/diag
 for i in 1 2; do
   timeout -k 10 120 python -u tools/perf_wr.py new >> gpurun_out/${T}_wr.jsonl 2>> gpurun_out/${T}_wr.err || exit $?
   CLIMSR_HIP_LIB=$D/wrold/libclimsr_hip.so timeout -k 10 120 python -u tools/perf_wr.py old >> gpurun_out/${T}_wr.jsonl 2>> gpurun_out/${T}_wr.err || exit $?
+  CLIMSR_HIP_LIB=$D/wrmid/libclimsr_hip.so timeout -k 10 120 python -u tools/perf_wr.py mid >> gpurun_out/${T}_wr.jsonl 2>> gpurun_out/${T}_wr.err || exit $?
   timeout -k 10 120 python -u tools/perf_s2.py glds >> gpurun_out/${T}_s2.jsonl 2>> gpurun_out/${T}_s2.err || exit $?
   CLIMSR_HIP_LIB=$D/w64s2old/libclimsr_hip.so timeout -k 10 120 python -u tools/perf_s2.py old >> gpurun_out/${T}_s2.jsonl 2>> gpurun_out/${T}_s2.err || exit $?
 done
