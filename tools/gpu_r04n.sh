@@ -1,5 +1,5 @@
 # conv_wr with the activation as a template parameter and one-add DMA offsets for interior tiles: the conv / RCAN
-# parity suites, A/B timing against the previous conv_wr (diag/wrold; diag/wrmid: templated, DMA issued at the tile's start), stride-2 wgrad A/B (diag/w64s2old), GAN bench.
+# parity suites, LDS-DMA conv with the epilogue activation resolved per item (diag/dmaold: per element), A/B timing against the previous conv_wr (diag/wrold; diag/wrmid: templated, DMA issued at the tile's start), stride-2 wgrad A/B (diag/w64s2old), GAN bench.
 #   usage: bash tools/gpu_r04n.sh <tag>
 set -o pipefail
 mkdir -p gpurun_out
@@ -12,6 +12,8 @@ for i in 1 2; do
   CLIMSR_HIP_LIB=$D/wrmid/libclimsr_hip.so timeout -k 10 120 python -u tools/perf_wr.py mid >> gpurun_out/${T}_wr.jsonl 2>> gpurun_out/${T}_wr.err || exit $?
   timeout -k 10 120 python -u tools/perf_s2.py glds >> gpurun_out/${T}_s2.jsonl 2>> gpurun_out/${T}_s2.err || exit $?
   CLIMSR_HIP_LIB=$D/w64s2old/libclimsr_hip.so timeout -k 10 120 python -u tools/perf_s2.py old >> gpurun_out/${T}_s2.jsonl 2>> gpurun_out/${T}_s2.err || exit $?
+  timeout -k 10 120 python -u tools/perf_diag.py dma_act1 >> gpurun_out/${T}_diag.jsonl 2>> gpurun_out/${T}_diag.err || exit $?
+  CLIMSR_HIP_LIB=$D/dmaold/libclimsr_hip.so timeout -k 10 120 python -u tools/perf_diag.py dma_old >> gpurun_out/${T}_diag.jsonl 2>> gpurun_out/${T}_diag.err || exit $?
 done
 timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 20 --warmup 5 > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err || exit $?
 timeout -k 10 300 python -u bench.py --mode infer --model rcan --no-cpu-baseline > gpurun_out/${T}_rcan.json 2> gpurun_out/${T}_rcan.err || exit $?
