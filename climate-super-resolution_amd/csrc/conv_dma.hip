@@ -2,7 +2,6 @@
 // path (VGG19 perceptual-loss convs climsr/losses/perceptual.py:22-36, RDB conv5 / its data gradient
 // climsr/models/esrgan.py:26,32-38, the discriminator's stride-1 layers climsr/models/rfb_esrgan.py:28-52).
 #include <algorithm>
-#include <type_traits>
 
 #include "conv_ep.h"
 
@@ -320,31 +319,23 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
         bb[t][0] = b4.x; bb[t][1] = b4.y; bb[t][2] = b4.z; bb[t][3] = b4.w;
       }
       const int ox = ox0 + col, act = EP == 8 ? 0 : a.act;
-      // the activation resolved once per item (one uniform branch) instead of per element: act_apply with a run-time
-      // act compiled to a branch tree around each of the 64 values (~470 branch instructions per kernel)
-      auto store_all = [&](auto actc) {
-        constexpr int ACT = decltype(actc)::value;
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          const int oy = oy0 + wave * 4 + m;
-          const bool ok = oy < a.out_h && ox < a.out_w;
-          const long pix = ((long)nimg * a.out_h + oy) * a.out_w + ox;
+      for (int m = 0; m < 4; ++m) {
+        const int oy = oy0 + wave * 4 + m;
+        const bool ok = oy < a.out_h && ox < a.out_w;
+        const long pix = ((long)nimg * a.out_h + oy) * a.out_w + ox;
 #pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            float v[4];
+        for (int t = 0; t < 4; ++t) {
+          float v[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) v[i] = act_apply(acc[m][t][i] + bb[t][i], ACT, a.slope);
-            const bf16x2 p0 = {(__bf16)v[0], (__bf16)v[1]}, p1 = {(__bf16)v[2], (__bf16)v[3]};
-            typedef uint32_t v2u32_t __attribute__((ext_vector_type(2)));
-            const v2u32_t pk = {__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1)};
-            const uint32_t off = ok ? (uint32_t)((pix * a.out_cs + a.out_co + co0 + 16 * t + 4 * g) * 2) : BUF_OOB;
-            __builtin_amdgcn_raw_buffer_store_b64(pk, ry, off, 0, 0);
-          }
+          for (int i = 0; i < 4; ++i) v[i] = act_apply(acc[m][t][i] + bb[t][i], act, a.slope);
+          const bf16x2 p0 = {(__bf16)v[0], (__bf16)v[1]}, p1 = {(__bf16)v[2], (__bf16)v[3]};
+          typedef uint32_t v2u32_t __attribute__((ext_vector_type(2)));
+          const v2u32_t pk = {__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1)};
+          const uint32_t off = ok ? (uint32_t)((pix * a.out_cs + a.out_co + co0 + 16 * t + 4 * g) * 2) : BUF_OOB;
+          __builtin_amdgcn_raw_buffer_store_b64(pk, ry, off, 0, 0);
         }
-      };
-      if (act == 1) store_all(std::integral_constant<int, 1>{});
-      else if (act == 2) store_all(std::integral_constant<int, 2>{});
-      else store_all(std::integral_constant<int, 0>{});
+      }
     } else {
       constexpr int EPH = 32 + 4;  // staged pitch (floats) of one 32-channel half
       float* eb = (float*)(smem + (buf ^ 1) * DMA_BUF) + wave * (64 * EPH);

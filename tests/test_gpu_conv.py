@@ -265,7 +265,7 @@ def test_conv_wgrad_matches_autograd(cin, cout, ks, stride, up):
 
 @pytest.mark.parametrize("cin,cout,n,h,w", [(64, 64, 3, 37, 45), (128, 64, 2, 9, 33), (64, 128, 1, 64, 64)])
 def test_conv_wgrad64_stride2_ragged(cin, cout, n, h, w):
-    """Stride-2 64-block weight gradient (conv_wgrad64_glds_s2_kernel) on odd / ragged sizes: partial 4 x 16 output
+    """Stride-2 64-block weight gradient (conv_wgrad64_kernel<1, 2>) on odd / ragged sizes: partial 4 x 16 output
     tiles, footprints past the bottom / right edge (zero-filled by the LDS-DMA), one image, two 64-row co blocks."""
     p, wt, b = make_plan(cin, cout, 3, 2)
     g = torch.Generator().manual_seed(7)
@@ -690,7 +690,7 @@ def test_conv_wr_fp32_out_channel_sums(n, h, w, f32):
     finally:
         ops.PROFILER = None
     torch.cuda.synchronize()
-    assert names and names[-1].startswith("conv_wr_kernel<3," if f32 else "conv_wr_kernel<4,"), names
+    assert names and names[-1].startswith("conv_wr_kernel<3>" if f32 else "conv_wr_kernel<4>"), names
     want = F.conv2d(x.double(), bf(wt).double(), b.double(), padding=1)
     check_close(from_nhwc(y, 64).cpu(), want, 1e-5 if f32 else 2 ** -8, "out")
     sums = part.double().cpu().reshape(n, tpi, 64).sum(1)
