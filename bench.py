@@ -145,10 +145,13 @@ def cpu_info():
 def pmc_traffic(kernel, mode):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of this workload
     (profiles/r*_<mode>_pmc_traffic.json: separate FETCH_SIZE / WRITE_SIZE passes of this bench,
-    FETCH_SIZE x2 gfx950 correction, MI355X_MICROARCH.md).  None if no summary covers it."""
+    FETCH_SIZE x2 gfx950 correction, MI355X_MICROARCH.md).  The summary carries the sha256 of the library it
+    profiled; counters of any other build describe other code, so they are refused: (None, reason)."""
     import glob
-
+    import hashlib
     import re
+
+    from climsr_amd import _lib
 
     def build_key(path):  # r02_v11 after r02_v9: (round, version) as numbers, not as text
         m = re.match(r"r(\d+)_v(\d+)_", os.path.basename(path))
@@ -156,13 +159,20 @@ def pmc_traffic(kernel, mode):
 
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{mode}_pmc_traffic.json")), key=build_key)
     if not files:
-        return None, None
-    f = files[-1]  # only the newest build's counters: an older build's bytes would describe other code
-    try:
-        rec = json.load(open(f))["kernels"].get(kernel)
-    except (OSError, ValueError, KeyError):
-        return None, None
-    return (rec["hbm_bytes_per_launch"], os.path.basename(f)) if rec else (None, None)
+        return None, "no PMC summary for this workload under profiles/"
+    running = hashlib.sha256(open(_lib.LIB_PATH, "rb").read()).hexdigest()
+    for f in reversed(files):
+        try:
+            doc = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if doc.get("lib_sha256") != running:
+            continue
+        rec = doc.get("kernels", {}).get(kernel)
+        if not rec:
+            return None, f"{os.path.basename(f)} (this build) has no record of {kernel}"
+        return rec["hbm_bytes_per_launch"], os.path.basename(f)
+    return None, f"no PMC summary under profiles/ was taken on this build (libclimsr_hip.so sha256 {running[:16]})"
 
 
 class KernelTimer:
@@ -381,6 +391,12 @@ def run_infer(args, world, rank, dev):
             roof = {"bound": r["bound"], "achieved": r["achieved"], "peak": r["peak"], "unit": r["unit"], "frac": r["frac"],
                     "traffic": None}
             roof.update({k: v for k, v in r.items() if k not in roof})
+            tb, src = pmc_traffic(name, f"infer_{args.model}")
+            if tb is None:
+                roof["traffic_note"] = src
+            else:
+                roof.update(traffic=round(tb / 1e6, 2), traffic_unit="MB/launch", traffic_source=src,
+                            traffic_over_algorithmic=round(tb / max(1, r["bytes_per_launch"]), 2))
             kern = {k: {"launches": v[0], "ms_total": round(v[1], 3), "tflops": round(v[2] / (v[1] / 1e3) / 1e12, 1),
                         "gbs": round(v[3] / (v[1] / 1e3) / 1e9, 1) if v[3] else None}
                     for k, v in sorted(agg.items(), key=lambda kv: -kv[1][1])}
@@ -702,7 +718,9 @@ def kernel_profile(step, mode, ops):
     roof = {"bound": r["bound"], "achieved": r["achieved"], "peak": r["peak"], "unit": r["unit"], "frac": r["frac"], "traffic": None}
     roof.update({k: v for k, v in r.items() if k not in roof})
     tb, src = pmc_traffic(name, mode)
-    if tb is not None:  # HBM bytes per launch (PMC) and the bandwidth they imply at the measured launch time
+    if tb is None:
+        roof["traffic_note"] = src
+    else:  # HBM bytes per launch (PMC) and the bandwidth they imply at the measured launch time
         roof.update(traffic=round(tb / 1e6, 2), traffic_unit="MB/launch", traffic_source=src,
                     traffic_gbs=round(tb / (r["avg_launch_us"] / 1e6) / 1e9, 1),
                     traffic_over_algorithmic=round(tb / max(1, r["bytes_per_launch"]), 2))

@@ -1055,11 +1055,19 @@ static int launch_n16(const FwdArgs& a, hipStream_t s) {
 //     T[y][x'][kx] = sum_{ky, ci} x[y + ky - R][x'][ci] * w[ky][kx][ci]        (M = x', N = kx, K = ky x ci)
 //     out[y][x]    = sum_kx T[y][x + kx - R][kx]                               (shift-sum through LDS)
 // so the 16-wide N tile carries KS useful columns instead of 1 (KS/16 vs 1/16 of the MFMA).  A wave
-// computes 4 output rows x 64 columns (5 M-fragments of x'), streaming its 4 + KS - 1 input rows straight
+// computes ROWS output rows x 64 columns (5 M-fragments of x'), streaming its ROWS + KS - 1 input rows straight
 // from global memory (16 B per lane, next row in flight during the current row's MFMAs); every input row
-// feeds the up-to-4 output rows it touches.  Weights sit in VGPRs for the whole wave.
+// feeds the up-to-KS output rows it touches.  Output row r is complete once input row r + KS - 1 is in: its
+// shift-sum and store run right there and its accumulators take row r + KS, so a ring of min(KS, ROWS) rows is
+// live -- which lets the 3x3 / 5x5 forms stream 16 rows per wave (input rows fetched 18/16 or 20/16 times instead
+// of 6/4 or 8/4: conv_last read 1.76x its input at 4 rows).  Weights sit in VGPRs for the whole wave.
 // ------------------------------------------------------------------------------------------
-constexpr int CO1M_NF = 5, CO1M_COLS = 64, CO1M_ROWS = 4;
+constexpr int CO1M_NF = 5, CO1M_COLS = 64;
+template <int KS>
+struct Co1m {
+  static constexpr int ROWS = KS <= 5 ? 16 : 4;                  // output rows per wave
+  static constexpr int NSLOT = KS < ROWS ? KS : ROWS;            // live accumulator rows
+};
 
 static bool co1m_shape(const ClimsrConvDesc* d) {
   return d->out_c == 1 && d->stride == 1 && d->up == 1 && (d->ks == 3 || d->ks == 5 || d->ks == 9) && d->pad == d->ks / 2 &&
@@ -1068,10 +1076,10 @@ static bool co1m_shape(const ClimsrConvDesc* d) {
 
 template <int KS, int NCH>
 __global__ __launch_bounds__(256, 2) void conv_co1m_kernel(FwdArgs a) {
-  constexpr int R = KS / 2, NR = CO1M_ROWS + KS - 1;
+  constexpr int R = KS / 2, ROWS = Co1m<KS>::ROWS, NSLOT = Co1m<KS>::NSLOT, NR = ROWS + KS - 1;
   __shared__ float sc[4][CO1M_NF * 16][17];  // per-wave T rows (x' x kx), padded pitch
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
-  const int x0 = blockIdx.x * CO1M_COLS, y0 = (blockIdx.y * 4 + wave) * CO1M_ROWS, nimg = blockIdx.z;
+  const int x0 = blockIdx.x * CO1M_COLS, y0 = (blockIdx.y * 4 + wave) * ROWS, nimg = blockIdx.z;
   // B fragments: B[k = ci][n = kx] of tap row ky, channel block c (packed row 0: k = (ci/cc)*kcpad + tap*cc + ci%cc)
   bf16x8 bw[KS][NCH];
 #pragma unroll
@@ -1083,9 +1091,9 @@ __global__ __launch_bounds__(256, 2) void conv_co1m_kernel(FwdArgs a) {
       if (col < KS && ci < a.in_c)
         bw[ky][c] = *(const bf16x8*)(a.w + (long)(ci / a.cc) * a.kcpad + (ky * KS + col) * a.cc + (ci % a.cc));
     }
-  f32x4 acc[CO1M_ROWS][CO1M_NF];
+  f32x4 acc[NSLOT][CO1M_NF];
 #pragma unroll
-  for (int r = 0; r < CO1M_ROWS; ++r)
+  for (int r = 0; r < NSLOT; ++r)
 #pragma unroll
     for (int f = 0; f < CO1M_NF; ++f) acc[r][f] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
@@ -1106,30 +1114,18 @@ __global__ __launch_bounds__(256, 2) void conv_co1m_kernel(FwdArgs a) {
       }
     }
   };
-  load_row(0, 0);
-#pragma unroll
-  for (int iyr = 0; iyr < NR; ++iyr) {
-    if (iyr + 1 < NR) load_row((iyr + 1) & 1, iyr + 1);
-#pragma unroll
-    for (int ky = 0; ky < KS; ++ky) {
-      const int r = iyr - ky;  // output row fed by input row iyr through tap row ky
-      if (r < 0 || r >= CO1M_ROWS) continue;
-#pragma unroll
-      for (int f = 0; f < CO1M_NF; ++f)
-#pragma unroll
-        for (int c = 0; c < NCH; ++c)
-          acc[r][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[iyr & 1][f][c], bw[ky][c], acc[r][f], 0, 0, 0);
-    }
-  }
-  // shift-sum: out[x0 + l] = sum_kx T[x' = l + kx][kx]; then the fused epilogue (same as conv_co1_kernel)
+  // shift-sum of output row r (slot r % NSLOT): out[x0 + l] = sum_kx T[x' = l + kx][kx]; then the fused epilogue
+  // (same as conv_co1_kernel); the slot is cleared for row r + NSLOT
   const float bias = a.bias ? a.bias[0] : 0.f;
   const bool f1 = a.res_f32 & 1;
-#pragma unroll
-  for (int r = 0; r < CO1M_ROWS; ++r) {
+  auto finish = [&](int r) {
+    const int sl = r % NSLOT;
 #pragma unroll
     for (int f = 0; f < CO1M_NF; ++f)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) sc[wave][f * 16 + g * 4 + i][col] = acc[r][f][i];
+      for (int i = 0; i < 4; ++i) sc[wave][f * 16 + g * 4 + i][col] = acc[sl][f][i];
+#pragma unroll
+    for (int f = 0; f < CO1M_NF; ++f) acc[sl][f] = (f32x4){0.f, 0.f, 0.f, 0.f};
     float v = 0.f;
 #pragma unroll
     for (int kx = 0; kx < KS; ++kx) v += sc[wave][lane + kx][kx];
@@ -1145,6 +1141,26 @@ __global__ __launch_bounds__(256, 2) void conv_co1m_kernel(FwdArgs a) {
       else ((float*)a.y)[ob] = v;
       if (a.aux) a.aux[pidx * a.aux_cs + a.aux_co] = f2bf(a.aux_scale * v);
     }
+  };
+  load_row(0, 0);
+#pragma unroll
+  for (int iyr = 0; iyr < NR; ++iyr) {
+    if (iyr + 1 < NR) load_row((iyr + 1) & 1, iyr + 1);
+#pragma unroll
+    for (int ky = KS - 1; ky >= 0; --ky) {  // oldest row first: row iyr - KS + 1 completes here
+      const int r = iyr - ky;  // output row fed by input row iyr through tap row ky
+      if (r < 0 || r >= ROWS) continue;
+#pragma unroll
+      for (int f = 0; f < CO1M_NF; ++f)
+#pragma unroll
+        for (int c = 0; c < NCH; ++c)
+          acc[r % NSLOT][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[iyr & 1][f][c], bw[ky][c], acc[r % NSLOT][f], 0, 0, 0);
+      if (NSLOT < ROWS && ky == KS - 1) finish(r);
+    }
+  }
+  if constexpr (NSLOT == ROWS) {  // no slot reuse (9x9): every row finishes after the stream, as fewer registers stay live
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) finish(r);
   }
 }
 
@@ -1154,7 +1170,7 @@ static int launch_co1m(const FwdArgs& a, hipStream_t s) {
     snprintf(g_dry_name, sizeof(g_dry_name), "conv_co1m_kernel<%d, %d>", KS, NCH);
     return CLIMSR_OK;
   }
-  dim3 grid(ceil_div(a.out_w, CO1M_COLS), ceil_div(a.out_h, 4 * CO1M_ROWS), a.n);
+  dim3 grid(ceil_div(a.out_w, CO1M_COLS), ceil_div(a.out_h, 4 * Co1m<KS>::ROWS), a.n);
   hipLaunchKernelGGL((conv_co1m_kernel<KS, NCH>), grid, dim3(256), 0, s, a);
   return check_launch("conv2d_fwd (co1m)");
 }
@@ -2248,7 +2264,10 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_s2_kernel(FwdArgs a) {
 static int plain_ep(const FwdArgs& a);
 static bool fwd_s2_shape(const ClimsrConvDesc* d, const FwdArgs& a) {
   return d->stride == 2 && d->ks == 3 && d->pad == 1 && d->up == 1 && d->cc == 32 && d->in_c % 32 == 0 && d->out_c % 64 == 0 &&
-         d->in_coff % 8 == 0 && d->in_cstride % 8 == 0 && a.kcpad == 288 && plain_ep(a) == 8;
+         d->in_coff % 8 == 0 && d->in_cstride % 8 == 0 && a.kcpad == 288 && plain_ep(a) == 8 &&
+         // the LDS-DMA kernel's buffer offsets are 32-bit (BUF_OOB past every buffer): larger tensors take the generic conv
+         (long)a.n * a.in_h * a.in_w * a.in_cs * 2 < (1L << 31) && (long)a.n * a.out_h * a.out_w * a.out_cs * 2 < (1L << 31) &&
+         (long)d->out_c * a.kpk * 2 < (1L << 31);
 }
 
 // the LDS-DMA kernel (conv_dma.hip conv_fwd_s2_dma_kernel); the register-staged 8-wave kernel it replaced measured
@@ -2951,10 +2970,13 @@ struct W64 {
 
 // TS = 2: 8 waves, wave w owns ci block w & 3 and taps [0,5) or [5,9) (w >> 2): 20 accumulators instead of 36, so
 // two waves share each SIMD (latency hiding) at the price of each wave re-reading the shared dz fragments.
-// G (TS 1, S 1): the LDS-DMA form -- see conv_wgrad64_glds_kernel below.
+// G (TS 1): the LDS-DMA form -- see conv_wgrad64_glds_kernel below.
+#ifndef CLIMSR_W64S2_GLDS
+#define CLIMSR_W64S2_GLDS 1  // A/B builds only (tools/diag_build.sh): 0 = the register-staged stride-2 kernel
+#endif
 template <int TS, int S, bool G>
 __device__ __forceinline__ void wgrad64_body(const WgArgs& a) {
-  static_assert(!G || (TS == 1 && S == 1), "LDS-DMA form: 256 threads, stride 1");
+  static_assert(!G || TS == 1, "LDS-DMA form: 256 threads");
   constexpr int NTHR = 256 * TS, NU = TS == 1 ? 9 : 5;
   constexpr int TH = W64<S>::TH, TPW = W64<S>::TPW, NZ = W64<S>::NZ, NX = W64<S>::NX, XP = W64<S>::XP;
   extern __shared__ __attribute__((aligned(16))) char smem[];  // TS 1: two buffers of W64<S>::LDS
@@ -3100,20 +3122,27 @@ __device__ __forceinline__ void wgrad64_body(const WgArgs& a) {
     // lane l of an instruction fills pixel slot 8 i + (l >> 3), 16 B position l & 7, with that pixel's channel chunk
     // (l & 7) ^ (column & 7) -- an XOR swizzle chosen on the global (source) side that spreads the 8 pixels of a
     // transposed fragment read over all 64 banks, as the register path's 80-element pitch did.
-    constexpr int ZB = TH * TW * 128, XB = 24 * 1024, BUF = ZB + XB, NXP = W64<1>::TPH * TPW;
+    // per wave and tile: NZI dz and NXI x instructions (stride 1: 4 + 6, stride 2: 2 + 10)
+    constexpr int NZI = TH / 2, NXI = S == 1 ? 6 : 10;
+    constexpr int ZB = TH * TW * 128, XB = 4 * NXI * 1024, BUF = ZB + XB, NXP = W64<S>::TPH * TPW;
+    static_assert(4 * NXI * 8 >= NXP && 3 * BUF <= 160 * 1024, "LDS-DMA wgrad64 tile buffers");
     const int l8 = lane >> 3, c8 = lane & 7, wv = tid >> 6;
-    // dz: wave w issues instructions w + 4 j (j < 4): tile row (w >> 1) + 2 j, column 8 (w & 1) + l8
+    // dz: wave w issues instructions w + 4 j (j < NZI): tile row (w >> 1) + 2 j, column 8 (w & 1) + l8
     const int zcol = 8 * (wv & 1) + l8, zrow0 = wv >> 1;
     const uint32_t zrow_b = (uint32_t)a.out_w * a.dz_cs * 2;
     const uint32_t z_lane = (uint32_t)((zcol * a.dz_cs + co0 + 8 * (c8 ^ (zcol & 7))) * 2) + (uint32_t)zrow0 * zrow_b;
     const __amdgpu_buffer_rsrc_t zrs = buf_rsrc(a.dz, (uint32_t)((long)a.n * a.out_h * a.out_w * a.dz_cs * 2));
-    // x: instructions w + 4 j (j < 6): footprint pixel 8 (w + 4 j) + l8 of the 10 x 18 footprint (180 pixels; the
-    // slots past it get zeros): (row << 16) | (column << 8) | source chunk
-    int xrc[6];
+    // x: instructions w + 4 j (j < NXI): footprint slot 8 (w + 4 j) + l8 of the 10 x 18 (stride 2: 9 x 33) footprint
+    // (the slots past it get zeros): (row << 16) | (column << 8) | source chunk.  Stride 2 stores each footprint row's
+    // 17 even columns first, then its 16 odd ones: the stride-2 pixels 2 c + dx of a fragment read then sit in
+    // consecutive slots, alternating bank halves as the stride-1 reads do (in column order all of them would share one
+    // half of the 64 banks: two-way conflicts)
+    int xrc[NXI];
 #pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      const int P = 8 * (wv + 4 * j) + l8, row = P < NXP ? P / TPW : 1023, cx = P % TPW;
-      xrc[j] = (row << 16) | (cx << 8) | (c8 ^ (cx & 7));
+    for (int j = 0; j < NXI; ++j) {
+      const int P = 8 * (wv + 4 * j) + l8, row = P < NXP ? P / TPW : 1023, slot = P % TPW;
+      const int cx = S == 1 ? slot : (slot < (TPW + 1) / 2 ? 2 * slot : 2 * (slot - (TPW + 1) / 2) + 1);
+      xrc[j] = (row << 16) | (cx << 8) | (c8 ^ (slot & 7));
     }
     const uint32_t ximg_b = (uint32_t)a.in_h * a.in_w * a.in_cs * 2, pxb = (uint32_t)a.in_cs * 2;
     const uint32_t x_ch = (uint32_t)((a.in_co + ci0) * 2);
@@ -3122,7 +3151,7 @@ __device__ __forceinline__ void wgrad64_body(const WgArgs& a) {
     int ntx = split % a.tiles_x, nty = (split / a.tiles_x) % a.tiles_y, nn = split / (a.tiles_x * a.tiles_y);
     // in asm, not __builtin_amdgcn_raw_ptr_buffer_load_lds: hipcc treats the builtin as an LDS write of unknown
     // extent and waits vmcnt(0) before the next ds_read, i.e. for the tile just requested; hidden from it, the DMAs
-    // are counted by hand (vmcnt(10) below) and drained before the epilogue.  M0 (the wave's LDS destination) is set
+    // are counted by hand (vmcnt(NZI + NXI) below) and drained before the epilogue.  M0 (the wave's LDS destination) is set
     // and restored inside the statement.
     const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
     const int wvu = __builtin_amdgcn_readfirstlane(wv);  // provably wave-uniform: the LDS destination is an "s" operand
@@ -3145,13 +3174,13 @@ __device__ __forceinline__ void wgrad64_body(const WgArgs& a) {
       const uint32_t zt = (uint32_t)(((nimg * a.out_h + oy0) * a.out_w + ox0) * a.dz_cs * 2) + z_lane;
       const bool zok = live & (ox0 + zcol < a.out_w);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NZI; ++j) {
         const bool ok = zok & (oy0 + zrow0 + 2 * j < a.out_h);
         glds(zrs, ok ? zt + (uint32_t)(2 * j) * zrow_b : BUF_OOB, zb + (uint32_t)((wvu + 4 * j) * 1024));
       }
-      const uint32_t iy0 = (uint32_t)(oy0 - a.pad), ix0 = (uint32_t)(ox0 - a.pad), xt = (uint32_t)nimg * ximg_b + x_ch;
+      const uint32_t iy0 = (uint32_t)(S * oy0 - a.pad), ix0 = (uint32_t)(S * ox0 - a.pad), xt = (uint32_t)nimg * ximg_b + x_ch;
 #pragma unroll
-      for (int j = 0; j < 6; ++j) {
+      for (int j = 0; j < NXI; ++j) {
         const uint32_t iy = iy0 + (uint32_t)(xrc[j] >> 16), ix = ix0 + (uint32_t)((xrc[j] >> 8) & 255);
         const bool ok = live & (iy < (uint32_t)lh) & (ix < (uint32_t)lw);
         const uint32_t off = xt + ((iy >> upsh) * (uint32_t)a.in_w + (ix >> upsh)) * pxb + (uint32_t)((xrc[j] & 7) * 16);
@@ -3159,28 +3188,32 @@ __device__ __forceinline__ void wgrad64_body(const WgArgs& a) {
       }
     };
     // fragment reads: k-step kk, lane (g, q, p) = output pixel c0 = 4 g + q of rows 2 kk (k0) and 2 kk + 1 (k1),
-    // channels 4 p.. of the 16-channel group: dz group t (chunk 2 t + (p >> 1)), x group wave (chunk 2 wave + (p >> 1))
+    // channels 4 p.. of the 16-channel group: dz group t (chunk 2 t + (p >> 1)), x group wave (chunk 2 wave + (p >> 1));
+    // tap column dx reads footprint column S c0 + dx (its slot)
     const int c0 = 4 * g + q;
     int zoff[4], xoff[3];
 #pragma unroll
     for (int t = 0; t < 4; ++t) zoff[t] = c0 * 128 + (((2 * t + (p >> 1)) ^ (c0 & 7)) << 4) + 8 * (p & 1);
 #pragma unroll
-    for (int dx = 0; dx < 3; ++dx) xoff[dx] = (c0 + dx) * 128 + (((2 * wave + (p >> 1)) ^ ((c0 + dx) & 7)) << 4) + 8 * (p & 1);
+    for (int dx = 0; dx < 3; ++dx) {
+      const int sl = S == 1 ? c0 + dx : (dx == 1 ? (TPW + 1) / 2 + c0 : c0 + dx / 2);
+      xoff[dx] = sl * 128 + (((2 * wave + (p >> 1)) ^ (sl & 7)) << 4) + 8 * (p & 1);
+    }
     auto ld_af = [&](const char* zb, int kk, bf16x8 (&af)[4]) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) af[t] = cat_tr(ds_read_tr16(zb + kk * 32 * 128 + zoff[t]), ds_read_tr16(zb + (kk * 32 + 16) * 128 + zoff[t]));
     };
     auto ld_bf = [&](const char* xb, int kk, int u) {
       const int dy = u / 3, dx = u % 3;
-      return cat_tr(ds_read_tr16(xb + (2 * kk + dy) * TPW * 128 + xoff[dx]), ds_read_tr16(xb + (2 * kk + 1 + dy) * TPW * 128 + xoff[dx]));
+      return cat_tr(ds_read_tr16(xb + (S * 2 * kk + dy) * TPW * 128 + xoff[dx]), ds_read_tr16(xb + (S * (2 * kk + 1) + dy) * TPW * 128 + xoff[dx]));
     };
     issue(tile < a.ntiles, 0);
     issue(tile + a.nsplit < a.ntiles, 1);
     int cur = 0;
     for (; tile < a.ntiles; tile += a.nsplit) {
-      // this tile's 10 DMAs (per wave) have landed once at most the next tile's 10 are outstanding; the barrier makes
-      // that true for every wave, and every wave is past its reads of the tile before last (buffer (cur + 2) % 3)
-      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      // this tile's NZI + NXI DMAs (per wave) have landed once at most the next tile's are outstanding; the barrier
+      // makes that true for every wave, and every wave is past its reads of the tile before last (buffer (cur + 2) % 3)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NZI + NXI) : "memory");
       __builtin_amdgcn_s_barrier();
       issue(tile + 2 * a.nsplit < a.ntiles, cur == 0 ? 2 : cur - 1);
       const char* zb = smem + cur * BUF;
@@ -3281,7 +3314,8 @@ __device__ __forceinline__ void wgrad64_body(const WgArgs& a) {
   }
 }
 constexpr size_t W64_EP_LDS = (size_t)64 * (9 * 64 + 4) * 4;  // the slab staging of conv_wgrad64_kernel
-constexpr size_t W64G_LDS = (size_t)3 * (8 * 16 * 128 + 24 * 1024);  // three LDS-DMA tile buffers (G form)
+constexpr size_t W64G_LDS = (size_t)3 * (8 * 16 * 128 + 24 * 1024);     // three LDS-DMA tile buffers (G form)
+constexpr size_t W64G2_LDS = (size_t)3 * (4 * 16 * 128 + 40 * 1024);    // (G form, stride 2)
 
 template <int TS, int S = 1>
 __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
@@ -3290,6 +3324,7 @@ __global__ __launch_bounds__(256 * TS, 1) void conv_wgrad64_kernel(WgArgs a) {
 // at most 256 registers (one workgroup per CU either way: 148 KB of LDS): the accumulators stay in VGPRs -- the
 // 512-register form kept some of them in AGPRs and shuffled them every tile
 __global__ __launch_bounds__(256, 2) void conv_wgrad64_glds_kernel(WgArgs a) { wgrad64_body<1, 1, true>(a); }
+__global__ __launch_bounds__(256, 2) void conv_wgrad64_glds_s2_kernel(WgArgs a) { wgrad64_body<1, 2, true>(a); }
 
 // ------------------------------------------------------------------------------------------
 // Weight gradient of a 1x1 conv with 64 inputs and <= 64 outputs (srcnn.conv2): dW[co][ci] = sum_p dz[p][co]
@@ -3687,7 +3722,12 @@ extern "C" int climsr_conv2d_wgrad(const ClimsrConvDesc* d, const uint16_t* x, c
     const bool ts2 = d->stride == 1 && (long)d->n * d->out_h * d->out_w >= (1L << 20);
     a.xcd = 1;
     const dim3 grid = dim3((d->out_c / 64) * (d->in_c / 64) * nsplit);
-    if (d->stride == 2) {
+    if (d->stride == 2 && CLIMSR_W64S2_GLDS) {
+      a.tph = W64<2>::TPH; a.tpw = W64<2>::TPW;
+      if (dry_run("conv_wgrad64_glds_s2_kernel")) return CLIMSR_OK;
+      if (int e = lds_opt_in((const void*)conv_wgrad64_glds_s2_kernel, 160 * 1024)) return e;
+      hipLaunchKernelGGL(conv_wgrad64_glds_s2_kernel, grid, dim3(256), std::max(W64G2_LDS, W64_EP_LDS), (hipStream_t)stream, a);
+    } else if (d->stride == 2) {
       a.tph = W64<2>::TPH; a.tpw = W64<2>::TPW;
       if (dry_run("conv_wgrad64_kernel<1, 2>")) return CLIMSR_OK;
       if (int e = lds_opt_in((const void*)conv_wgrad64_kernel<1, 2>, 160 * 1024)) return e;

@@ -2,6 +2,7 @@
 // path (VGG19 perceptual-loss convs climsr/losses/perceptual.py:22-36, RDB conv5 / its data gradient
 // climsr/models/esrgan.py:26,32-38, the discriminator's stride-1 layers climsr/models/rfb_esrgan.py:28-52).
 #include <algorithm>
+#include <type_traits>
 
 #include "conv_ep.h"
 
@@ -319,23 +320,31 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
         bb[t][0] = b4.x; bb[t][1] = b4.y; bb[t][2] = b4.z; bb[t][3] = b4.w;
       }
       const int ox = ox0 + col, act = EP == 8 ? 0 : a.act;
+      // the activation resolved once per item (one uniform branch) instead of per element: act_apply with a run-time
+      // act compiled to a branch tree around each of the 64 values (~470 branch instructions per kernel)
+      auto store_all = [&](auto actc) {
+        constexpr int ACT = decltype(actc)::value;
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const int oy = oy0 + wave * 4 + m;
-        const bool ok = oy < a.out_h && ox < a.out_w;
-        const long pix = ((long)nimg * a.out_h + oy) * a.out_w + ox;
+        for (int m = 0; m < 4; ++m) {
+          const int oy = oy0 + wave * 4 + m;
+          const bool ok = oy < a.out_h && ox < a.out_w;
+          const long pix = ((long)nimg * a.out_h + oy) * a.out_w + ox;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          float v[4];
+          for (int t = 0; t < 4; ++t) {
+            float v[4];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = act_apply(acc[m][t][i] + bb[t][i], act, a.slope);
-          const bf16x2 p0 = {(__bf16)v[0], (__bf16)v[1]}, p1 = {(__bf16)v[2], (__bf16)v[3]};
-          typedef uint32_t v2u32_t __attribute__((ext_vector_type(2)));
-          const v2u32_t pk = {__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1)};
-          const uint32_t off = ok ? (uint32_t)((pix * a.out_cs + a.out_co + co0 + 16 * t + 4 * g) * 2) : BUF_OOB;
-          __builtin_amdgcn_raw_buffer_store_b64(pk, ry, off, 0, 0);
+            for (int i = 0; i < 4; ++i) v[i] = act_apply(acc[m][t][i] + bb[t][i], ACT, a.slope);
+            const bf16x2 p0 = {(__bf16)v[0], (__bf16)v[1]}, p1 = {(__bf16)v[2], (__bf16)v[3]};
+            typedef uint32_t v2u32_t __attribute__((ext_vector_type(2)));
+            const v2u32_t pk = {__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1)};
+            const uint32_t off = ok ? (uint32_t)((pix * a.out_cs + a.out_co + co0 + 16 * t + 4 * g) * 2) : BUF_OOB;
+            __builtin_amdgcn_raw_buffer_store_b64(pk, ry, off, 0, 0);
+          }
         }
-      }
+      };
+      if (act == 1) store_all(std::integral_constant<int, 1>{});
+      else if (act == 2) store_all(std::integral_constant<int, 2>{});
+      else store_all(std::integral_constant<int, 0>{});
     } else {
       constexpr int EPH = 32 + 4;  // staged pitch (floats) of one 32-channel half
       float* eb = (float*)(smem + (buf ^ 1) * DMA_BUF) + wave * (64 * EPH);
@@ -471,6 +480,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_s2_dma_kernel(FwdArgs a) {
   for (int p = 0; p < 8; ++p) piece(p, 1, 1);
   const int npc = wvu < 2 ? 8 : (wvu == 2 ? 7 : 6);
   int cur = 0;  // the buffer of the chunk being computed
+  bool pm = true;  // the previous chunk requested pieces (chunk 1's went out before the loop)
   for (;;) {
     const int vn = v + (int)gridDim.x;
     int nimg_n = 0, oy0_n = 0, ox0_n = 0, co0_n = 0, tile_n = 0;
@@ -483,7 +493,10 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_s2_dma_kernel(FwdArgs a) {
       // chunk c has landed once at most the younger requests are outstanding: the next chunk's pieces, and at chunks
       // 0 / 1 of a later item also the previous item's 8 epilogue stores (issued between them)
       const bool st = c < 2 && v != (int)blockIdx.x;
-      if (npc == 8) {
+      if (!pm) {  // the last chunks of the last item: nothing was requested behind this chunk (at most the stores)
+        if (st) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else if (npc == 8) {
         if (st) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       } else if (npc == 7) {
@@ -533,6 +546,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_s2_dma_kernel(FwdArgs a) {
         }
         __builtin_amdgcn_sched_barrier(0);
       }
+      pm = more;
     }
     // ---- epilogue straight from the accumulators: lane (col, g) holds channels co0 + 16 t + 4 g .. + 3 of output pixel
     // (oy0 + 2 wave + m, ox0 + col); 8 stores per lane, issued unconditionally

@@ -53,7 +53,9 @@ struct WrArgs {
 typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
 typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 
-template <int EP>
+// ACT: the activation as a template parameter (0 none, 1 leaky relu, 2 relu; EP 2: 3 / 4 their backward) -- as a
+// kernel argument it cost a three-way uniform branch per accumulator element (~390 branch instructions per tile)
+template <int EP, int ACT>
 __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // vector-memory operations of one epilogue (loads + stores), fixed per lane
@@ -80,11 +82,16 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
 
   // ---- footprint DMA: instruction i, lane l fills 16 B slot q = 64 i + l = (pixel q / 10, slot q % 10); slots 8, 9
   // of a pixel (the pitch padding) and slots past the footprint get zeros (out-of-range source offset)
+  // rel: the slot's source offset from the footprint's corner pixel for an interior tile without upsampling (pad
+  // slots: 2^31, past every buffer's range), so such a tile's DMA offsets are one add each
   int dg[WR_NI];
+  uint32_t rel[WR_NI];
 #pragma unroll
   for (int i = 0; i < WR_NI; ++i) {
     const int q = i * 64 + lane, p = q / WR_SPP, c = q - p * WR_SPP;
-    dg[i] = (p < WR_PR * WR_PC && c < 8) ? ((p / WR_PC) << 16) | ((p % WR_PC) << 8) | c : -1;
+    const bool live = p < WR_PR * WR_PC && c < 8;
+    dg[i] = live ? ((p / WR_PC) << 16) | ((p % WR_PC) << 8) | c : -1;
+    rel[i] = live ? (uint32_t)((((p / WR_PC) * a.in_w + p % WR_PC) * a.in_cs + c * 8) * 2) : 0x80000000u;
   }
   const __amdgpu_buffer_rsrc_t xr = buf_rsrc(a.x, a.x_bytes);
   const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
@@ -103,16 +110,30 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
     oy0 = ty * WR_TR;
     ox0 = tx * WR_TC;
   };
-  auto issue = [&](int tile, int b) {  // tile < 0: zeros (keeps the per-iteration DMA count fixed)
-    int nimg = 0, oy0 = -1 << 20, ox0 = 0;
-    if (tile >= 0) decode(tile, nimg, oy0, ox0);
-    const uint32_t dst = mybuf + (uint32_t)(b * WR_BUF);
-#pragma unroll
-    for (int i = 0; i < WR_NI; ++i) {
-      const int iy = oy0 - 1 + (dg[i] >> 16), ix = ox0 - 1 + ((dg[i] >> 8) & 255), c = dg[i] & 255;
+  // the footprint DMA of a tile (tile < 0: zeros, which keeps the per-iteration DMA count fixed) in WR_NI pieces:
+  // prep() once, piece(i) for every instruction i
+  struct Fp {
+    int nimg, oy0, ox0;
+    bool fast;      // interior tile, no upsampling (wave-uniform): the corner's offset on the scalar unit, one add a piece
+    uint32_t base, dst;
+  };
+  auto prep = [&](int tile, int b) {
+    Fp f{0, -1 << 20, 0, false, 0u, mybuf + (uint32_t)(b * WR_BUF)};
+    if (tile >= 0) decode(tile, f.nimg, f.oy0, f.ox0);
+    f.fast = ups == 0 && f.oy0 >= 1 && f.oy0 - 1 + WR_PR <= a.in_h && f.ox0 >= 1 && f.ox0 - 1 + WR_PC <= a.in_w;
+    // (unsigned: for the zero tile's sentinel row the product wraps instead of overflowing; base is unused then)
+    const uint32_t corner = (uint32_t)(f.nimg * a.in_h + f.oy0 - 1) * (uint32_t)a.in_w + (uint32_t)(f.ox0 - 1);
+    f.base = (corner * (uint32_t)a.in_cs + (uint32_t)a.in_co) * 2u;
+    return f;
+  };
+  auto piece = [&](const Fp& f, int i) {
+    if (f.fast) {
+      glds(f.base + rel[i], f.dst + (uint32_t)(i * 1024));
+    } else {
+      const int iy = f.oy0 - 1 + (dg[i] >> 16), ix = f.ox0 - 1 + ((dg[i] >> 8) & 255), c = dg[i] & 255;
       const bool ok = dg[i] >= 0 && iy >= 0 && iy < lh && ix >= 0 && ix < lw;
-      const uint32_t off = (uint32_t)((((long)(nimg * a.in_h + (iy >> ups)) * a.in_w + (ix >> ups)) * a.in_cs + a.in_co + c * 8) * 2);
-      glds(ok ? off : BUF_OOB, dst + (uint32_t)(i * 1024));
+      const uint32_t off = (uint32_t)((((long)(f.nimg * a.in_h + (iy >> ups)) * a.in_w + (ix >> ups)) * a.in_cs + a.in_co + c * 8) * 2);
+      glds(ok ? off : BUF_OOB, f.dst + (uint32_t)(i * 1024));
     }
   };
 
@@ -120,14 +141,19 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
   const __amdgpu_buffer_rsrc_t pr = buf_rsrc(a.ch_part, SUMS && a.ch_part ? (uint32_t)a.ntiles * 256u : 0u);
   const __amdgpu_buffer_rsrc_t rr = buf_rsrc(a.res1, (EP == 1 || EP == 2) ? a.r1_bytes : 0u);
   const int lb = col * WR_XP * 2 + g * 16;  // this lane's byte offset in a footprint row: pixel col, channels 8 g ..
-  issue(T, 0);
+  {
+    const Fp f0 = prep(T, 0);
+#pragma unroll
+    for (int i = 0; i < WR_NI; ++i) piece(f0, i);
+  }
   for (int it = 0;; ++it) {
     const int Tn = T + G4;
-    issue(Tn < a.ntiles ? Tn : -1, (it + 1) & 1);
-    // tile T's footprint has landed once at most the younger operations are outstanding: the last epilogue's and
-    // the DMA just issued
-    if (it == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WR_NI) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WR_NI + NEPI) : "memory");
+    // the next tile's footprint goes out two pieces per k block over the first 9, under the MFMAs of this one (issued
+    // all at once ahead of them, their address arithmetic ran with the MFMA pipe idle)
+    const Fp fn = prep(Tn < a.ntiles ? Tn : -1, (it + 1) & 1);
+    // tile T's footprint has landed once at most the younger operations are outstanding: the last epilogue's
+    if (it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NEPI) : "memory");
     const char* xb = smem + (wv * 2 + (it & 1)) * WR_BUF + lb;
     f32x4 acc[4][4];  // [output row m][co block t]
     bf16x8 bq[2][4];
@@ -140,6 +166,8 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
 #pragma unroll
     for (int j = 0; j < 18; ++j) {
       if (j + 1 < 18) ldb(j + 1, (j + 1) & 1);
+      if (2 * j < WR_NI) piece(fn, 2 * j);
+      if (2 * j + 1 < WR_NI) piece(fn, 2 * j + 1);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
@@ -184,10 +212,10 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
           if constexpr (EP == 2) {
             const uint32_t w = i < 2 ? rv[m][t].x : rv[m][t].y;
             const float r = __uint_as_float((i & 1) ? (w & 0xFFFF0000u) : (w << 16));
-            x = r > 0.f ? x : (a.act == 3 ? x * a.slope : 0.f);
+            x = r > 0.f ? x : (ACT == 3 ? x * a.slope : 0.f);
           } else {
-            if (a.act == 1) x = x > 0.f ? x : x * a.slope;
-            else if (a.act == 2) x = x > 0.f ? x : 0.f;
+            if constexpr (ACT == 1) x = fmaxf(x, x * a.slope);  // = (x > 0 ? x : slope x) for 0 <= slope <= 1 (host)
+            else if constexpr (ACT == 2) x = x > 0.f ? x : 0.f;
             if constexpr (EP == 1) {
               const uint32_t w = i < 2 ? rv[m][t].x : rv[m][t].y;
               const float r = __uint_as_float((i & 1) ? (w & 0xFFFF0000u) : (w << 16));
@@ -248,7 +276,7 @@ int conv_wr_ep(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const float* b
   else if (ep->out_mode == 0 && res && (ep->act == 3 || ep->act == 4) && !bias && !(ep->res_f32 & 1)) epk = 2;
   else if (ep->out_mode == 1 && !res && ep->act >= 0 && ep->act <= 2) epk = 3;
   const long opx = (long)d->n * d->out_h * d->out_w;
-  if (epk < 0 || (ep->ch_part && epk != 3 && epk != 4) || d->in_c != 64 || d->out_c != 64 || d->cc != 64 || d->ks != 3 || d->stride != 1 ||
+  if (epk < 0 || (ep->ch_part && epk != 3 && epk != 4) || (ep->act == 1 && !(ep->slope >= 0.f && ep->slope <= 1.f)) || d->in_c != 64 || d->out_c != 64 || d->cc != 64 || d->ks != 3 || d->stride != 1 ||
       d->pad != 1 || (d->up != 1 && d->up != 2) || d->out_h != d->in_h * d->up || d->out_w != d->in_w * d->up ||
       d->in_cstride % 8 || d->in_coff % 8 || (d->out_cstride | d->out_coff) & 3 || ep->down2 || ep->res2 || ep->aux ||
       ep->bn_part || (res && ((ep->res1_cstride | ep->res1_coff) & 3)) ||
@@ -277,7 +305,7 @@ int conv_wr_launch(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const uint
   const long opx = (long)d->n * d->out_h * d->out_w;
   if (epk < 0 || kpk < 576) return -1;
   if (dry) {
-    snprintf(name, name_len, "conv_wr_kernel<%d>", epk);
+    snprintf(name, name_len, "conv_wr_kernel<%d, %d>", epk, ep->act);
     return CLIMSR_OK;
   }
   WrArgs a;
@@ -293,8 +321,18 @@ int conv_wr_launch(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const uint
   a.r1_bytes = res ? (uint32_t)(opx * ep->res1_cstride * 2) : 0u;
   const int ncu = device_cus();
   const int grid = std::min(ceil_div(a.ntiles, 4), ncu);
-  void (*k)(WrArgs) = epk == 0 ? conv_wr_kernel<0> : epk == 1 ? conv_wr_kernel<1> : epk == 2 ? conv_wr_kernel<2>
-                      : epk == 3 ? conv_wr_kernel<3> : conv_wr_kernel<4>;
+  // [epilogue][activation] (EP 1: no activation; EP 2: 3 / 4)
+  static void (*const kt[5][5])(WrArgs) = {
+      {conv_wr_kernel<0, 0>, conv_wr_kernel<0, 1>, conv_wr_kernel<0, 2>, nullptr, nullptr},
+      {conv_wr_kernel<1, 0>, nullptr, nullptr, nullptr, nullptr},
+      {nullptr, nullptr, nullptr, conv_wr_kernel<2, 3>, conv_wr_kernel<2, 4>},
+      {conv_wr_kernel<3, 0>, conv_wr_kernel<3, 1>, conv_wr_kernel<3, 2>, nullptr, nullptr},
+      {conv_wr_kernel<4, 0>, conv_wr_kernel<4, 1>, conv_wr_kernel<4, 2>, nullptr, nullptr}};
+  void (*k)(WrArgs) = (ep->act >= 0 && ep->act < 5) ? kt[epk][ep->act] : nullptr;
+  if (!k) {
+    set_error("conv2d_fwd (wr): epilogue %d with activation %d", epk, ep->act);
+    return CLIMSR_EINVAL;
+  }
   const int lds = (epk == 3 || epk == 4) ? WR_LDS_ALL : WR_LDS;
   if (int e = lds_opt_in((const void*)k, WR_LDS_ALL)) return e;
   hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, s, a);

@@ -60,13 +60,13 @@ def test_generator_forward_routes(routes):
     assert last(routes) == "conv_fwd_kernel<4, 4, false, 4, 6, 9, 1, 1>"
     pt = plan(NF, NF)
     pt.fwd(bf(), DC, 0, H, H, bf(), NF, 0, N, res1=bf(), alpha1=1.0, res1_cs=NF, res1_co=0)
-    assert last(routes) == "conv_wr_kernel<1>"
+    assert last(routes) == "conv_wr_kernel<1, 0>"
     pu = plan(NF, NF)
     for s in (1, 2):  # upconv1 (64 -> 128), upconv2 (128 -> 256)
         pu.fwd(bf(), NF, 0, s * H, s * H, bf(), NF, 0, N, up=2, act=ACT_LRELU)
-        assert last(routes) == "conv_wr_kernel<0>"
+        assert last(routes) == "conv_wr_kernel<0, 1>"
     pu.fwd(bf(), NF, 0, 4 * H, 4 * H, bf(), NF, 0, N, act=ACT_LRELU)
-    assert last(routes) == "conv_wr_kernel<0>"
+    assert last(routes) == "conv_wr_kernel<0, 1>"
     pl = plan(NF, 1)
     pl.fwd(bf(), NF, 0, 4 * H, 4 * H, bf(), 8, 0, N)
     assert last(routes) == "conv_co1m_kernel<3, 2>"
@@ -74,7 +74,7 @@ def test_generator_forward_routes(routes):
 
 @pytest.mark.parametrize("cin,cout,hw,want", [
     (3, 64, 256, "conv_pw_kernel<8, 2, 4, false, 2, 3, 2>"),     # conv1_1: 4-channel taps
-    (64, 64, 256, "conv_wr_kernel<0>"),                         # conv1_2: weights in registers
+    (64, 64, 256, "conv_wr_kernel<0, 2>"),                         # conv1_2: weights in registers
     (64, 128, 128, "conv_fwd_dma_kernel<3, false>"),            # conv2_1 .. conv4_4: the roofline kernel
     (128, 128, 128, "conv_fwd_dma_kernel<3, false>"),
     (128, 256, 64, "conv_fwd_dma_kernel<3, false>"),
@@ -129,4 +129,4 @@ def test_weight_gradient_routes(routes):
     routes.clear()
     p2 = plan(128, 128, 3, 2, bias=False)
     p2.wgrad(bf(), 128, 0, 128, 128, bf(), 128, N, Workspace(), accumulate=False)
-    assert _wgrad_name(routes) == "conv_wgrad64_kernel<1, 2>"
+    assert _wgrad_name(routes) == "conv_wgrad64_glds_s2_kernel"

@@ -142,7 +142,7 @@ def test_rdb_grouped_wgrad_split_k_at_bench_shape():
 @pytest.mark.parametrize("cin,cout,h", [(64, 64, 256), (128, 128, 128), (256, 256, 64), (512, 512, 32)])
 def test_wgrad64_stride2_discriminator_layers(cin, cout, h):
     """The RFB discriminator's stride-2 convs (features.2/8/14/20, rfb_esrgan.py:29-49) at B=32 of 256^2 tiles: weight
-    gradient on conv_wgrad64_kernel<1, 2> (4 x 16 output tiles over a (2*4+1) x (2*16+1) input footprint)."""
+    gradient on conv_wgrad64_glds_s2_kernel (4 x 16 output tiles over a (2*4+1) x (2*16+1) input footprint, LDS-DMA)."""
     from climsr_amd import ops
 
     n = 32
@@ -161,7 +161,7 @@ def test_wgrad64_stride2_discriminator_layers(cin, cout, h):
     finally:
         ops.PROFILER = None
     torch.cuda.synchronize()
-    assert "conv_wgrad64_kernel<1, 2>" in names, names
+    assert "conv_wgrad64_glds_s2_kernel" in names, names
     want = None
     for i in range(0, n, 4):
         cols = F.unfold(x[i:i + 4].double(), 3, padding=1, stride=2)

@@ -10,9 +10,18 @@ a wide streaming read (x2).  Writes <out_prefix>.json (read by bench.py for `roo
 import collections
 import csv
 import glob
+import hashlib
 import json
 import os
 import sys
+
+LIB = os.environ.get("CLIMSR_HIP_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                                     "climate-super-resolution_amd", "csrc", "libclimsr_hip.so"))
+
+
+def lib_sha256(path=LIB):
+    """The fingerprint bench.py matches before it attaches these counters to a roofline line."""
+    return hashlib.sha256(open(path, "rb").read()).hexdigest()
 
 
 def load(d, counter):
@@ -44,9 +53,10 @@ def main():
     src = (f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes): {title}; values per launch, averaged over all "
            "launches of the kernel in the run; FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 reports half of a wide "
            "streaming read); KB->bytes x1024")
-    json.dump({"source": src, "kernels": rows}, open(out + ".json", "w"), indent=1)
+    meta = {"lib_sha256": lib_sha256(), "git_head": os.environ.get("CLIMSR_GIT_HEAD")}
+    json.dump({"source": src, **meta, "kernels": rows}, open(out + ".json", "w"), indent=1)
     with open(out + ".md", "w") as f:
-        f.write(f"# {title}\n\n| kernel | launches | fetch MB/launch (x2 corrected) | write MB/launch |\n|---|---|---|---|\n")
+        f.write(f"# {title}\n\nlibclimsr_hip.so sha256 {meta['lib_sha256'][:16]}, git head {meta['git_head']}\n\n| kernel | launches | fetch MB/launch (x2 corrected) | write MB/launch |\n|---|---|---|---|\n")
         for k, v in list(rows.items())[:25]:
             f.write(f"| {k} | {v['launches']} | {v['fetch_bytes_per_launch'] / 1e6:.1f} | {v['write_bytes_per_launch'] / 1e6:.1f} |\n")
     print(open(out + ".md").read())
