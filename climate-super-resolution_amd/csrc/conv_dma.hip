@@ -257,6 +257,14 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
               piece(2 * k, jn, buf ^ 1);
               piece(2 * k + 1, jn, buf ^ 1);
             }
+          } else if (CLIMSR_DMA_SPREAD == 3) {  // pieces 0-3 / 4-6 / 7-9 behind the first three k-steps' MFMAs
+            if (k == 0) {
+              piece(0, jn, buf ^ 1); piece(1, jn, buf ^ 1); piece(2, jn, buf ^ 1); piece(3, jn, buf ^ 1);
+            } else if (k == 1) {
+              piece(4, jn, buf ^ 1); piece(5, jn, buf ^ 1); piece(6, jn, buf ^ 1);
+            } else if (k == 2) {
+              piece(7, jn, buf ^ 1); piece(8, jn, buf ^ 1); piece(9, jn, buf ^ 1);
+            }
           } else {
             piece(k, jn, buf ^ 1);
             if (k == 8) piece(9, jn, buf ^ 1);
