@@ -2445,6 +2445,9 @@ int conv_wr_launch(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const uint
                    const float* bias, void* y, hipStream_t s, bool dry, char* name, int name_len);
 long conv_wr_ch_parts(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, int* tiles_per_image);
 int conv_wr_ep(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const float* bias);
+int rdb5_route(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const float* bias, int kcpad);
+int rdb5_launch(int mode, const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const uint16_t* x, const uint16_t* wpk, int kpk,
+                const float* bias, void* y, hipStream_t s, bool dry, char* name, int name_len);
 }
 
 extern "C" int64_t climsr_conv2d_fwd_ch_parts(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, int32_t* tiles_per_image) {
@@ -2587,6 +2590,11 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
   if (dgrad_s2_shape(d, ep, bias) && (long)d->n * d->out_h * d->out_w * ep->res1_cstride * 2 < (1L << 32) - 64)
     return launch_dgrad_s2(d, a, s);
   if (fwd_s2_shape(d, a)) return launch_fwd_s2(d, a, s);
+  // RDB conv5 / pull-x (128 -> 64 3x3): row streaming with input-row reuse (rdb_conv5.hip)
+  if (const int m5 = rdb5_route(d, ep, bias, g.kcpad)) {
+    const int rc = rdb5_launch(m5, d, ep, x, wpk, g.kpk, bias, y, s, g_dry, g_dry_name, (int)sizeof(g_dry_name));
+    return rc == CLIMSR_OK && !g_dry ? CLIMSR_OK : rc;
+  }
   if (pt_shape(d, ep) && (d->out_c == 16 || d->out_c == 32 || d->out_c == 64) &&
       (d->in_c == 32 || d->in_c == 64 || d->in_c == 128))
     return dispatch_pt(d, a, s);

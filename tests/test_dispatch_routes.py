@@ -16,7 +16,7 @@ import pytest
 import torch
 
 from climsr_amd import _lib, ops
-from climsr_amd.ops import ACT_LRELU, ACT_RELU, ConvPlan, GroupedWgrad, Workspace
+from climsr_amd.ops import ACT_LRELU, ACT_RELU, OUT_F32, ConvPlan, GroupedWgrad, Workspace
 
 N, H, DC, NF, GC = 32, 64, 128, 64, 16
 
@@ -54,10 +54,10 @@ def test_generator_forward_routes(routes):
     on load + LeakyReLU), HRconv, conv_last (64 -> 1) at B=32, 64^2 LR."""
     p5 = plan(DC, NF)
     p5.fwd(bf(), DC, 0, H, H, bf(), DC, 0, N, res1=bf(), alpha1=0.2, res1_cs=DC, res1_co=0)
-    assert last(routes) == "conv_fwd_kernel<4, 4, false, 4, 6, 9, 1, 1>"
+    assert last(routes) == "rdb5_kernel<1>"
     p5.fwd(bf(), DC, 0, H, H, bf(), DC, 0, N, res1=bf(), alpha1=0.2, res1_cs=DC, res1_co=0, res2=bf(), alpha2=0.2, res2_cs=DC,
            res2_co=0)
-    assert last(routes) == "conv_fwd_kernel<4, 4, false, 4, 6, 9, 1, 1>"
+    assert last(routes) == "rdb5_kernel<1>"
     pt = plan(NF, NF)
     pt.fwd(bf(), DC, 0, H, H, bf(), NF, 0, N, res1=bf(), alpha1=1.0, res1_cs=NF, res1_co=0)
     assert last(routes) == "conv_wr_kernel<1, 0>"
@@ -105,6 +105,16 @@ def test_discriminator_bn_conv_routes(routes, stride, cin, cout, hw, want):
     assert p.bn_parts(cin, hw, hw, N, cout) > 0, "BatchNorm partials must come from the conv epilogue"
     p.fwd(bf(), cin, 0, hw, hw, bf(), cout, 0, N, use_bias=False, bn_part=torch.empty(1, dtype=torch.float64))
     assert last(routes) == want
+
+
+def test_rdb_pullx_route(routes):
+    """pull-x (the RDB-input gradient as one 128 -> 64 conv over [dZ1 .. dZ5]: fp32 out, fp32 skip gradients, the
+    previous RDB's bf16 dZ5 as aux) takes the row-streaming kernel."""
+    px = plan(DC, NF, bias=False)
+    f32 = torch.empty(8, dtype=torch.float32)
+    px.fwd(bf(), DC, 0, H, H, f32, NF, 0, N, use_bias=False, out_mode=OUT_F32, res1=f32, res1_cs=NF, res1_co=0, beta1=0.2,
+           res2=f32, res2_cs=NF, res2_co=0, aux=bf(), aux_cs=DC, aux_co=4 * GC, aux_scale=0.04)
+    assert last(routes) == "rdb5_kernel<2>"
 
 
 def _wgrad_name(routes):

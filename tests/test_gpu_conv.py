@@ -785,3 +785,77 @@ def test_srcnn_tail_backward_matches_fp64(n, h, w):
     check_close(p2.gb.cpu() - 0.25, dz2b.sum((0, 2, 3)), 2e-3, "db2")
     check_close(p3.gw.cpu() - 0.5, w3v.grad, 2e-3, "dW3")
     check_close(p3.gb.cpu() - 0.25, gb.sum().reshape(1), 2e-3, "db3")
+
+
+# RDB conv5 / pull-x on the row-streaming 128 -> 64 kernel (rdb_conv5.hip rdb5_kernel<1 / 2>): strips of rows with the
+# two halo rows ingested once, 64-column tiles (ragged widths, images narrower than a tile, rows not a multiple of the
+# strip height), both epilogue forms incl. the optional second residual / aux output, bit-identical reruns.
+RDB5_CASES = [
+    (4, 64, 64, "conv5", True), (3, 37, 100, "conv5", False), (2, 32, 32, "pullx", True), (1, 9, 130, "pullx", False),
+    (5, 64, 64, "pullx", True), (2, 13, 17, "conv5", True),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h,w,mode,two", RDB5_CASES)
+def test_rdb5_conv5_pullx_matches_fp64(n, h, w, mode, two):
+    """esrgan.py:26,38,54 (conv5 + x5 * 0.2 + x, the RRDB out * 0.2 + x) and its pull-x data gradient (fp32 out = conv +
+    beta1 * g_out (+ g_skip), bf16 aux = aux_scale * out into the previous dZ5 slot) vs float64 on the same bf16
+    operands.  Tolerances: fp32 out 1e-5 of the scale; bf16 out one rounding (2^-8 relative) of the fp32 value."""
+    import climsr_amd.ops as ops
+
+    dc, nf = 128, 64
+    conv5 = mode == "conv5"
+    p, wt, b = make_plan(dc, nf, 3, seed=31, bias=conv5)
+    g = torch.Generator().manual_seed(32)
+    x = bf(torch.rand((n, dc, h, w), generator=g) * 2 - 1)
+    xin = to_nhwc(x)
+    r1 = torch.rand((n, nf, h, w), generator=g) * 2 - 1
+    r2 = torch.rand((n, nf, h, w), generator=g) * 2 - 1
+    if conv5:
+        y = torch.full((n, h, w, dc), 7.0, dtype=torch.bfloat16, device=DEV)  # the next RDB's dense buffer, channels 0..63
+        r2d = to_nhwc(bf(r2), cs=dc)
+        kw = dict(res1=xin, alpha1=0.2, res1_cs=dc, res1_co=0)
+        if two:
+            kw.update(res2=r2d, alpha2=0.2, res2_cs=dc, res2_co=0)
+        ycs = dc
+    else:
+        y = torch.full((n, h, w, nf), 7.0, dtype=torch.float32, device=DEV)
+        aux = torch.full((n, h, w, dc), 3.0, dtype=torch.bfloat16, device=DEV)
+        kw = dict(use_bias=False, out_mode=OUT_F32, res1=to_nhwc(r1, dtype=torch.float32), res1_cs=nf, res1_co=0, beta1=0.2,
+                  aux=aux, aux_cs=dc, aux_co=64, aux_scale=0.04)
+        if two:
+            kw.update(res2=to_nhwc(r2, dtype=torch.float32), res2_cs=nf, res2_co=0)
+        ycs = nf
+    names = []
+    ops.PROFILER = lambda name, flops, fn, tag="", nbytes=0: (names.append(name), fn())
+    try:
+        p.fwd(xin, dc, 0, h, w, y, ycs, 0, n, **kw)
+    finally:
+        ops.PROFILER = None
+    torch.cuda.synchronize()
+    assert names and names[-1] == f"rdb5_kernel<{1 if conv5 else 2}>", names
+    first = y.clone()
+    p.fwd(xin, dc, 0, h, w, y, ycs, 0, n, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(first, y), "rerun not bit-identical"
+    want = F.conv2d(x.double(), bf(wt).double(), None if b is None else b.double(), padding=1)
+    if conv5:
+        want = want * 0.2 + x[:, :nf].double()
+        if two:
+            want = want * 0.2 + bf(r2).double()
+        got = from_nhwc(y, nf).cpu().double()
+        scale = want.abs().max().item()
+        err = ((got - want).abs() - want.abs() * 2.0 ** -8).max().item()
+        assert err <= 1e-5 * scale, f"conv5 bf16 err {err:.3e} vs scale {scale:.3e}"
+        assert torch.all(y[..., nf:].float() == 7.0), "conv5 wrote outside its 64 channels"
+    else:
+        want = want + 0.2 * r1.double()
+        if two:
+            want = want + r2.double()
+        got = from_nhwc(y, nf).cpu().double()
+        check_close(got, want, what="pullx")
+        ga = from_nhwc(aux, nf, 64).cpu().double()
+        err = ((ga - 0.04 * want).abs() - (0.04 * want).abs() * 2.0 ** -8).max().item()
+        assert err <= 1e-5 * 0.04 * want.abs().max().item(), f"pullx aux err {err:.3e}"
+        assert torch.all(aux[..., :64].float() == 3.0), "pull-x aux wrote outside its slot"
