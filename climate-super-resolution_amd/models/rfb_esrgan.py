@@ -150,15 +150,18 @@ class _DEngine:
         acc = accumulate
         ops.d_head_bwd(sv["hid"], sv["s"], ds, fc2.weight, n, o, n_pad, fc2.weight.grad if need_w else None,
                        fc2.bias.grad if need_w else None, fc0.bias.grad if need_w else None, acc, du0, du0_t)
+        # grad-ready reports (core/ddp.OverlappedGradAllReducer): only in the step's last weight-gradient backward
+        # (loss_d runs D twice, pl_gan.py:51-61), where each slice below becomes final
+        hook = d._grad_ready_hook if need_w else None
+        if hook is not None:
+            calls = d._ready_calls + 1
+            object.__setattr__(d, "_ready_calls", 0 if calls >= d._ready_need else calls)
+            if calls < d._ready_need:
+                hook = None
         if need_w:
             ops.linear_wgrad(du0_t, sv["p_t"], n_pad, feat, o, fc0.weight.grad, acc)
-            hook = d._grad_ready_hook
-            if hook is not None:  # fc.0 / fc.2 (the last flat entries, 103 M of 107 M parameters) are final once
-                # every backward of the step has accumulated into them (loss_d runs D twice, pl_gan.py:51-61)
-                object.__setattr__(d, "_ready_calls", d._ready_calls + 1)
-                if d._ready_calls >= d._ready_need:
-                    object.__setattr__(d, "_ready_calls", 0)
-                    hook(d._fc_flat_lo())
+            if hook is not None:  # fc.0 / fc.2: the last flat entries, 103 M of 107 M parameters
+                hook(d._fc_flat_lo())
         dp = self._scr("dp", (n, feat), torch.float32, dev)
         ops.linear_dgrad(du0, self.fc0_bf16, n, feat, o, dp)
         hh, ww, c = sv["hh"], sv["ww"], sv["c"]
@@ -195,6 +198,8 @@ class _DEngine:
                 plan.gw = conv.weight.grad
                 plan.gb = None
                 plan.wgrad(L["a_in"], L["cs_in"], 0, L["h_in"], L["w_in"], dz, cz, n, self.ws, acc)
+                if hook is not None and li in d._ready_layers:  # this layer group's conv + BN gradients are final
+                    hook(d._layer_flat_lo(li))
             if li > 0 or need_x:
                 prev_bn = self.layers[li - 1][1] if li > 0 else None
                 if prev_bn is None and li > 0:
@@ -295,6 +300,9 @@ class RFBESRGANDiscriminator(FlatParamsMixin, nn.Module):
         object.__setattr__(self, "_grad_ready_hook", None)
         object.__setattr__(self, "_ready_calls", 0)
         object.__setattr__(self, "_ready_need", 1)
+        # conv-tower slices reported during the last backward: layers 6-7 (3.5 M parameters), 3-5 (1.0 M); layers 0-2
+        # (0.1 M) go with finish()
+        object.__setattr__(self, "_ready_layers", (6, 3))
 
     def set_grad_ready_hook(self, fn, calls_per_step: int = 1) -> None:
         """Call ``fn(lo)`` during backward once the fc gradients (flat offsets >= lo; 103 M of the 107 M
@@ -309,6 +317,20 @@ class RFBESRGANDiscriminator(FlatParamsMixin, nn.Module):
         """(flat offset, numel, bf16 buffer) of fc.0's weight: its MFMA copy, written by the fused AdamW pass."""
         eng = self.engine()
         return self._fc_flat_lo(), self.fc[0].weight.numel(), eng.fc0_bf16
+
+    def grad_ready_los(self):
+        """The flat offsets the backward reports through the grad-ready hook, in its order (fc first, then the conv
+        tower's layer groups from the top): every gradient at or above an offset is final when it is reported."""
+        return [self._fc_flat_lo()] + [self._layer_flat_lo(li) for li in self._ready_layers]
+
+    def _layer_flat_lo(self, li: int) -> int:
+        """Flat offset of the li-th conv's weight (its BatchNorm follows it; later layers sit above it)."""
+        convs = [m for m in self.features if isinstance(m, nn.Conv2d)]
+        p = convs[li].weight
+        for q, off, _n in self._flat_index:
+            if q is p:
+                return off
+        raise KeyError(f"features conv {li} not in the flat parameter index")
 
     def _fc_flat_lo(self) -> int:
         p = self.fc[0].weight

@@ -509,10 +509,13 @@ class SrcnnTail:
         c1, c2, c3 = convs
         assert (c1.cin_real <= 4 and c1.cout == 64 and c1.ks == 9 and c2.cout == 32 and c2.ks == 1 and c3.cout == 1
                 and c3.ks == 5), "the fused SRCNN tail takes in_c <= 4, 64 / 32 / 1 channels, 9 / 1 / 5 kernels"
+        # the kernel hard-codes stride 1 and 'same' padding 4 / 0 / 2 (srcnn.py:9-11) and adds all three biases
+        assert all(c.stride == 1 and c.pad == c.ks // 2 for c in convs), "the fused SRCNN tail takes stride 1, padding ks // 2"
         self.wpk = torch.empty((_lib.load().climsr_srcnn_packed_elems(),), dtype=torch.bfloat16, device=c1.weight.device)
 
     def pack(self) -> None:
         c1, c2, c3 = self.convs
+        assert c1.bias is not None and c2.bias is not None and c3.bias is not None, "the fused SRCNN tail adds all three biases"
         _launch("srcnn pack", lambda: _lib.load().climsr_srcnn_pack(ptr(c1.weight), ptr(c2.weight), ptr(c3.weight), c1.cin_real,
                                                                     ptr(self.wpk), _lib.stream_ptr()))
 

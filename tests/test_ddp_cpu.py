@@ -364,7 +364,9 @@ def _gan_d_worker(rank, world, port, q):
         for k, prm in d.named_parameters():
             prm.grad.copy_(local[k])
         ov = OverlappedGradAllReducer(d)
-        ov.ready(d._fc_flat_lo())
+        los = d.grad_ready_los()  # the slices the native backward reports, in its order: fc, then conv layer groups
+        for lo in los:
+            ov.ready(lo)
         ov.finish()
         avg = {k: prm.grad.double().clone() for k, prm in d.named_parameters()}
         # expected: the mean of the two shards' gradients, each with its own BN statistics (computed here in one process)
@@ -377,7 +379,15 @@ def _gan_d_worker(rank, world, port, q):
             num = sum(float((a[k] - b[k]).norm() ** 2) for k in keys) ** 0.5
             return num / (sum(float(b[k].norm() ** 2) for k in keys) ** 0.5)
 
-        q.put((rank, shard, loss, rel(avg, want), rel(want, whole), stats, per[rank][2], list(ov.launched)))
+        # each reported slice holds exactly the parameters that are final at that point: fc.*, then features.17 ..
+        # (conv 6, its BN, conv 7, its BN), then features.8 .. features.15, then the rest at finish()
+        names = {}
+        for (prm, off, num), (k, _p) in zip(d._flat_index, d.named_parameters()):
+            names[k] = (off, off + num)
+        slices = []
+        for lo, hi in ov.launched:
+            slices.append(sorted(k for k, (a, b) in names.items() if a >= lo and b <= hi))
+        q.put((rank, shard, loss, rel(avg, want), rel(want, whole), stats, per[rank][2], list(ov.launched), slices, los))
     finally:
         dist.destroy_process_group()
 
@@ -393,11 +403,19 @@ def test_gloo_world2_gan_discriminator_pass():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, shard, loss, rel_avg, rel_whole, stats, stats_check, launched in res:
+    for rank, shard, loss, rel_avg, rel_whole, stats, stats_check, launched, slices, los in res:
         assert rel_avg < 1e-6, (rank, rel_avg)  # product reducer + D flat layout: the average of the per-shard gradients
         assert rel_whole > 1e-3, (rank, rel_whole)  # per-rank BN statistics: not the whole-batch (SyncBN) gradient
         assert torch.equal(stats, stats_check)
-        assert len(launched) == 2 and launched[0][1] - launched[0][0] == 1024 * 100352 + 1024 + 1024 + 1
+        assert len(launched) == 4 and launched[0][1] - launched[0][0] == 1024 * 100352 + 1024 + 1024 + 1
+        assert [lo for lo, _hi in launched] == los + [0] and los == sorted(los, reverse=True)
+        # contiguous, descending, covering the whole flat buffer
+        assert all(launched[i][0] == launched[i + 1][1] for i in range(3))
+        assert slices[0] == ["fc.0.bias", "fc.0.weight", "fc.2.bias", "fc.2.weight"]
+        assert slices[1] == ["features.17.weight", "features.18.bias", "features.18.weight", "features.20.weight",
+                             "features.21.bias", "features.21.weight"]
+        assert slices[2][0] == "features.11.weight" and "features.8.weight" in slices[2] and "features.15.weight" in slices[2]
+        assert "features.0.weight" in slices[3] and "features.6.weight" in slices[3]
     assert res[0][1] == [0, 2] and res[1][1] == [1, 3]
     assert not torch.allclose(res[0][5], res[1][5])  # each rank's running statistics follow its own shard
     assert res[0][2] != res[1][2]  # and so do the per-rank losses
