@@ -391,7 +391,7 @@ static bool narrow_width(int w) { return w <= 64 && w % 16 == 0; }
 
 extern "C" const char* climsr_rdb_chain_kernel(const ClimsrChainDesc* d) {
   if (!d || d->w <= 0) return "";
-  if (narrow_width(d->w)) return d->act == 1 ? "rdb_chain_kernel<0>" : "rdb_chain_kernel<1>";
+  if (narrow_width(d->w)) return d->act == 1 ? "rdb_chain_rr_kernel<0>" : "rdb_chain_rr_kernel<1>";
   return d->act == 1 ? "rdb_chain_wide_kernel<0>" : "rdb_chain_wide_kernel<1>";
 }
 

@@ -2,20 +2,23 @@
 // RDB in ONE launch (esrgan.py:22-37), forward (conv1..conv4 -> x1..x4) and pull backward (pull4..pull1 -> dZ4..dZ1);
 // wider images take rdb_chain.hip's column-windowed kernel.
 //
-// One workgroup owns R full-width image rows and streams down them.  Step s: level 1 computes row y1 = r0 - 3 + s,
-// level L row y1 - 2(L - 1) (every row it reads from level L-1 was written in an earlier step: one barrier per step).
-// LDS holds a 10-row ring of the base (64 ch: each level reads the base rows around its own row) and an 8-row ring
-// of the level outputs [out1|out2|out3] (48 ch); only the strip's own rows are stored to HBM, the 3 + 2 + 1 halo rows
-// above / below each strip are recomputed by the neighbouring strips.
-// Eight waves, two per SIMD: wave w < 4 computes level w + 1, wave w >= 4 level 8 - w, so each SIMD pairs a light and
-// a heavy level (1 + 4, 2 + 3: 50 of the 100 MFMA blocks per row each); waves 0-3 cover column fragments 0, 1 and
-// waves 4-7 fragments 2, 3.  A wave keeps its level's A fragments (16 co x 32 k, 18 + dense blocks) in registers for
-// the launch, and every A fragment feeds two MFMAs (its two column fragments); B = one 16-pixel x 32-channel
-// ds_read_b128 per MFMA.  The second wave of a SIMD hides the other's LDS latency (the column-windowed kernel's one
-// wave per SIMD measured 43 / 52 us per forward / pull launch at B=32 64x64 against 32 / 40 us here).
-// K blocking: the base part of a level is 9 taps x 2 blocks of 32 channels; the dense part is one block per tap for
-// 32 channels (out1|out2) and, for a 16-channel group (out1 of level 2, out3 of level 4), PAIRS of taps in one block
-// (lanes 0-31 read tap 2p, lanes 32-63 tap 2p+1): 5 blocks instead of 9 half-empty ones.
+// One workgroup owns R full-width image rows and streams down them, one barrier per step.  Each level ingests one
+// input row per step and reuses it for all three kernel rows: the B fragment of (row i, tap column kx) is multiplied
+// by the weights of taps (0, kx), (1, kx), (2, kx) into the accumulators of output rows i + 1, i, i - 1 (three rows
+// rotate), so a 1 KB fragment read from LDS feeds three MFMAs instead of one -- a level computed one output row at a
+// time needs a fresh fragment per MFMA, which is the whole LDS read rate of the CU (1 KB per 16-cycle MFMA per SIMD).
+// Output row i - 1 of a level is complete once its row i is in; it goes through the epilogue into that level's LDS ring
+// and, for the strip's own rows, to HBM.  Level L + 1 ingests that row in the next step, so level L ingests row
+// r0 - 2 - 2L + s in step s.  Only the rows the next levels consume are computed: level L finishes rows
+// [r0 - 4 + L, r1 + 4 - L) (3 + 2 + 1 halo rows above / below a strip are recomputed by its neighbours).
+// LDS: an 8-row ring of the base (64 ch, 160 B pixel pitch: the 16 lanes of each ds_read_b128 bank group cover the 64
+// banks once) filled by LDS-DMA one step ahead, and rings of the level outputs x1 / x2 / x3 (16 ch, 32 B pitch; 6 / 4
+// / 2 rows: the steps until their last reader).
+// Eight waves, two per SIMD: wave w < 4 computes level w + 1, wave w >= 4 level 8 - w (each SIMD pairs a light and a
+// heavy level: 36 + 66 / 48 + 54 MFMAs per row); waves 0-3 cover column fragments 0, 1 and waves 4-7 fragments 2, 3.
+// A wave keeps its level's A fragments (16 co x 32 k: 18 base + 6 / 9 / 15 dense per level) in registers for the
+// launch.  Dense blocks: x1 | x2 of one tap in one block, a 16-channel group alone as a PAIR of tap columns (lanes
+// 0-31 column a, 32-63 column b; the third column pairs with zero weights).
 // MFMA v_mfma_f32_16x16x32_bf16: A = weights [16 co][32 k], B = [32 k][16 pixels], C lane = 4 co of one pixel.
 #include "common.h"
 
@@ -23,18 +26,6 @@ using namespace climsr;
 
 
 namespace {
-
-constexpr int RC_W = 64;                         // widest image row (4 fragments)
-constexpr int RC_COLS = RC_W + 2;                // LDS pixel slots per row: image columns -1 .. 64
-constexpr int RC_XP = 64 + 16;                   // base pixel pitch (bf16): == 16 (mod 32), conflict-free b128 reads
-constexpr int RC_DP = 48;                        // dense pixel pitch: out1 | out2 | out3 (== 16 mod 32)
-constexpr int RC_XD = 10;                        // base ring rows (y1-7 .. y1+1 read, y1+2 staged)
-constexpr int RC_DD = 8;                         // dense ring rows (y1-7 .. y1-1 read, y1 written)
-constexpr int RC_XROW = RC_COLS * RC_XP;
-constexpr int RC_DROW = RC_COLS * RC_DP;
-constexpr int RC_OFF_D = RC_XD * RC_XROW;        // elements
-constexpr int RC_LDS = (RC_OFF_D + RC_DD * RC_DROW) * 2;  // 156,288 B
-constexpr int RC_XCH = RC_COLS * 8;              // 16 B chunks of one base row (528)
 
 struct ChainArgs {
   const uint16_t* base;
@@ -53,276 +44,241 @@ struct ChainArgs {
 };
 typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
 
+// 32-channel blocks of a level's packed K row (KP = 64 + 16 (L - 1) rounded up to 32)
 __host__ __device__ constexpr int kp_blocks(int L) { return L == 1 ? 2 : (L == 4 ? 4 : 3); }
-__host__ __device__ constexpr int nd_blocks(int L) { return L == 1 ? 0 : (L == 2 ? 5 : (L == 3 ? 9 : 14)); }
-__host__ __device__ constexpr int n_blocks(int L) { return 18 + nd_blocks(L); }
 
-// The (tap, channel offset in the dense pixel) of lane group g in dense block j of level L; tap < 0: padding
-// (zero weights; the B read goes to tap 8 of the same block so every value read is finite).
-__device__ __forceinline__ void dense_src(int L, int j, int g, int& tap, int& ch) {
-  if (L == 3 || (L == 4 && j < 9)) {
-    tap = j;
-    ch = 8 * g;
-  } else {
-    const int p = L == 2 ? j : j - 9;
-    tap = 2 * p + (g >> 1);
-    ch = (L == 2 ? 0 : 32) + 8 * (g & 1);
-    if (tap > 8) tap = -1;
-  }
-}
-
-// A fragments of level L (16 co x 32 k per block) straight from the packed global weights ([16][9*KP], row pitch
-// 9*KP) into registers, kept for the whole launch: no LDS weight image, no workgroup barrier before the first base
-// rows are staged (the two waves of a level each fetch their 18-32 x 1 KB, L2-resident across the grid).
-template <int L>
-__device__ __forceinline__ void load_af_global(const uint16_t* __restrict__ wt, int lane, bf16x8 (&af)[n_blocks(L)]) {
-  constexpr int KP = kp_blocks(L) * 32;
-  const int g = lane >> 4, col = lane & 15;
-  const uint16_t* wr = wt + col * 9 * KP;
-#pragma unroll
-  for (int j = 0; j < 18; ++j) af[j] = *(const bf16x8*)(wr + (j >> 1) * KP + (j & 1) * 32 + g * 8);
-#pragma unroll
-  for (int j = 0; j < nd_blocks(L); ++j) {
-    int tap, ch;
-    dense_src(L, j, g, tap, ch);
-    af[18 + j] = tap >= 0 ? *(const bf16x8*)(wr + tap * KP + 64 + ch) : (bf16x8){};
-  }
-}
-
-// One level row, two column fragments (16 pixels apart): acc0/acc1 = sum over the level's blocks.  xr[ky] / dr[ky]:
-// LDS element offsets of the base / dense ring rows y-1+ky; lx / ld / lp: this lane's pixel-column (+ channel
-// group) offsets within a row.  Every A fragment feeds two independent accumulators.
-template <int L>
-__device__ __forceinline__ const uint16_t* block_src(const uint16_t* lds, const int (&xr)[3], const int (&dr)[3], int lx,
-                                                     int ld, int lp, int g, int j) {
-  if (j < 18) {
-    const int t = j >> 1, ky = t / 3, kx = t % 3;
-    return lds + xr[ky] + lx + kx * RC_XP + (j & 1) * 32;
-  }
-  j -= 18;
-  int off;
-  if (L == 3 || (L == 4 && j < 9)) {
-    off = dr[j / 3] + ld + (j % 3) * RC_DP;
-  } else {
-    const int p = L == 2 ? j : j - 9;
-    const int ta = 2 * p, tb = 2 * p + 1 <= 8 ? 2 * p + 1 : 2 * p;
-    const int oa = dr[ta / 3] + (ta % 3) * RC_DP, ob = dr[tb / 3] + (tb % 3) * RC_DP;
-    off = (g >= 2 ? ob : oa) + lp + (L == 2 ? 0 : 32);
-  }
-  return lds + RC_OFF_D + off;
-}
-
-// Blocks run in groups of rc_group(L): the B fragments of group k+1 are read while group k is on the MFMA pipe, so
-// 2 x rc_group reads stay in flight (the group size is what each level's weight registers leave room for).
-__host__ __device__ constexpr int rc_group(int L) { return L <= 2 ? 6 : (L == 3 ? 5 : 4); }
-
-template <int L>
-__device__ __forceinline__ void level_acc(const uint16_t* lds, const bf16x8 (&af)[n_blocks(L)], const int (&xr)[3],
-                                          const int (&dr)[3], int lx, int ld, int lp, int g, f32x4& acc0, f32x4& acc1) {
-  constexpr int NB = n_blocks(L), G = rc_group(L), NG = (NB + G - 1) / G;
-  acc0 = (f32x4){0.f, 0.f, 0.f, 0.f};
-  acc1 = acc0;
-  bf16x8 b[2][G][2];
-  auto load = [&](int gi, bf16x8 (&bb)[G][2]) {
-#pragma unroll
-    for (int i = 0; i < G; ++i) {
-      const int j = gi * G + i;
-      if (j < NB) {
-        const uint16_t* p = block_src<L>(lds, xr, dr, lx, ld, lp, g, j);
-        bb[i][0] = *(const bf16x8*)p;
-        bb[i][1] = *(const bf16x8*)(p + (j < 18 ? 16 * RC_XP : 16 * RC_DP));  // the second fragment: 16 pixels on
-      }
-    }
-  };
-  load(0, b[0]);
-#pragma unroll
-  for (int gi = 0; gi < NG; ++gi) {
-    if (gi + 1 < NG) load(gi + 1, b[(gi + 1) & 1]);
-    __builtin_amdgcn_sched_barrier(0);  // the next group's reads go out before this group's MFMAs
-#pragma unroll
-    for (int i = 0; i < G; ++i) {
-      const int j = gi * G + i;
-      if (j < NB) {
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], b[gi & 1][i][0], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j], b[gi & 1][i][1], acc1, 0, 0, 0);
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
-__device__ __forceinline__ int xslot(int y) { return (y + 4 * RC_XD) % RC_XD; }  // y >= -8
-__device__ __forceinline__ int dslot(int y) { return (y + 4 * RC_DD) & (RC_DD - 1); }
+constexpr int RR_PX = 66;                               // pixel slots per row: image columns -1 .. 64
+constexpr int RR_BP = 160;                              // base pixel pitch: 64 ch + 32 B pad (10 units of 16 B)
+constexpr int RR_BNI = (RR_PX * 10 + 63) / 64;          // base-row DMA instructions (11)
+constexpr int RR_BSLOT = RR_BNI * 1024;                 // 11,264 B per base row (whole DMA instructions)
+constexpr int RR_NB = 8;                                // base ring rows
+constexpr int RR_DP = 32;                               // dense pixel pitch (16 ch)
+constexpr int RR_DROW = RR_PX * RR_DP;                  // 2,112 B
+constexpr int RR_N1 = 6, RR_N2 = 4, RR_N3 = 2;          // x1 / x2 / x3 ring rows
+constexpr int RR_OFF_D = RR_NB * RR_BSLOT;              // 90,112
+constexpr int RR_OFF_2 = RR_OFF_D + RR_N1 * RR_DROW, RR_OFF_3 = RR_OFF_2 + RR_N2 * RR_DROW;
+constexpr int RR_LDS = RR_OFF_3 + RR_N3 * RR_DROW;      // 115,456 B
 
 __device__ __forceinline__ uint32_t pack2_bf16(float a, float b) {
   const bf16x2 v = {(__bf16)a, (__bf16)b};  // v_cvt_pk_bf16_f32 (RNE)
   return __builtin_bit_cast(uint32_t, v);
 }
 
-// The whole strip walk of one wave: level L, column fragments 2h and 2h+1.  Every wave runs the same step loop
-// (base-row staging + one barrier per step); level L computes in steps 3(L-1) .. R+4+L.
-// MODE 0: forward (bias + leaky relu); 1: pull (leaky-relu derivative of the stored activation, no bias).
-// Address arithmetic is split into per-lane constants (computed once) and per-step wave-uniform row offsets.
+// dense block groups per kernel row of level L (see the file comment)
+__host__ __device__ constexpr int rr_nd(int L) { return L == 1 ? 0 : (L == 2 ? 2 : (L == 3 ? 3 : 5)); }
+
+// One wave's whole strip walk: level L, column fragments 2 fp and 2 fp + 1.  Every wave runs the same steps (base-row
+// DMA + one barrier each).  MODE 0: forward (bias + leaky relu); 1: pull (leaky-relu derivative of the stored
+// activation, no bias).
 template <int MODE, int L>
-__device__ __forceinline__ void run_level(const ChainArgs& a, uint16_t* lds, int tid, int nimg, int r0) {
-  const int lane = tid & 63, g = lane >> 4, col = lane & 15, h = tid >> 8;
-  const int px0 = 32 * h + col;                  // this lane's image column in fragment 2h (fragment 2h+1: + 16)
-  const bool live0 = 32 * h < a.w, live1 = 32 * h + 16 < a.w;
+__device__ __forceinline__ void run_level(const ChainArgs& a, char* smem, int tid, int nimg, int r0, int r1) {
+  constexpr int ND = rr_nd(L), NG = 6 + ND, KP = kp_blocks(L) * 32;
+  const int lane = tid & 63, g = lane >> 4, col = lane & 15;
+  const int wvu = __builtin_amdgcn_readfirstlane(tid >> 6), fp = wvu >> 2;
+  const bool live0 = 32 * fp < a.w, live1 = 32 * fp + 16 < a.w;
   const __amdgpu_buffer_rsrc_t br = buf_rsrc(a.base, a.base_bytes);
   const __amdgpu_buffer_rsrc_t mr = buf_rsrc(a.mask, MODE == 1 ? a.mask_bytes : 0u);
-  const int R = a.rows, row0 = nimg * a.h;       // row0: this image's first row in the batch
-
-  // base row staging: chunk q = tid (+ 512) of a row is (slot q / 8 = image column + 1, 16 B channel group q % 8)
-  int xg[2], xl[2];  // byte offset within a base row in HBM (-1: zero chunk) / element offset within a ring row (-1: none)
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int q = tid + 512 * i, p = q >> 3, c = q & 7, ix = p - 1;
-    xl[i] = q < RC_XCH ? p * RC_XP + c * 8 : -1;
-    xg[i] = q < RC_XCH && ix >= 0 && ix < a.w ? (ix * a.bcs + a.boff + c * 8) * 2 : -1;
-  }
-  const uint32_t xrow_bytes = (uint32_t)(a.w * a.bcs * 2);
-  auto issue_row = [&](int y, uint4 (&v)[2]) {
-    const bool rok = y >= 0 && y < a.h;
-    const uint32_t rb = (uint32_t)(row0 + y) * xrow_bytes;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) v[i] = buf_load16(br, rok && xg[i] >= 0 ? rb + (uint32_t)xg[i] : BUF_OOB);
-  };
-  auto store_row = [&](int y, const uint4 (&v)[2]) {
-    uint16_t* row = lds + xslot(y) * RC_XROW;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      if (xl[i] >= 0) *(uint4*)(row + xl[i]) = v[i];
-  };
-  // pull: the activation x_j of this level's row in step s for both fragments (zeros outside), one step ahead
-  int ml[2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int px = px0 + 16 * k;
-    ml[k] = px < a.w ? (px * a.mcs + a.moff[L - 1] + 4 * g) * 2 : -1;
-  }
-  const uint32_t mrow_bytes = (uint32_t)(a.w * a.mcs * 2);
-  auto issue_mask = [&](int s, uint2 (&m)[2]) {
-    const int y = r0 - 3 + s - 2 * (L - 1);
-    const bool rok = y >= 0 && y < a.h;
-    const uint32_t rb = (uint32_t)(row0 + y) * mrow_bytes;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const auto v = __builtin_amdgcn_raw_buffer_load_b64(mr, rok && ml[k] >= 0 ? rb + (uint32_t)ml[k] : BUF_OOB, 0, 0);
-      m[k] = make_uint2(v[0], v[1]);
-    }
-  };
-  // Prologue: the first base rows are in flight while each wave loads its level's A fragments.
-  // Base rows are loaded one step before the step that stores them (two steps before their first use) and masks
-  // one step before their use; the loop is unrolled x2 with alternating register sets, so no register copy of a
-  // load still in flight (which would wait for it) is ever needed.
-  uint4 v0[2], v1[2], v2[2], ra[2], rb[2];
-  issue_row(r0 - 4, v0);
-  issue_row(r0 - 3, v1);
-  issue_row(r0 - 2, v2);
-  issue_row(r0 - 1, ra);
-  uint2 ma[2] = {}, mb[2] = {};
-  if constexpr (MODE == 1) issue_mask(0, ma);
-  const float4 bias = MODE == 0 ? *(const float4*)(a.bias[L - 1] + 4 * g) : make_float4(0.f, 0.f, 0.f, 0.f);
-  bf16x8 af[n_blocks(L)];
-  load_af_global<L>(a.wt[L - 1], lane, af);
-  // dense ring: the slots of image columns -1 and >= w are never written, they are the zero padding
-  for (int i = tid; i < RC_DD * (RC_COLS - a.w) * (RC_DP / 8); i += 512) {
-    const int c = i % (RC_DP / 8), k = (i / (RC_DP / 8)) % (RC_COLS - a.w), r = i / (RC_DP / 8) / (RC_COLS - a.w);
-    const int p = k == 0 ? 0 : a.w + k;
-    *(uint4*)(lds + RC_OFF_D + r * RC_DROW + p * RC_DP + c * 8) = make_uint4(0, 0, 0, 0);
-  }
-  store_row(r0 - 4, v0);
-  store_row(r0 - 3, v1);
-  store_row(r0 - 2, v2);
-  lds_barrier();
-  // retire the remaining loads here: with no VMEM result carried into the loop, hipcc's wait counting inside it
-  // stays exact (otherwise every step waits with a count that also drains the base-row prefetch)
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-
-  const int lx = px0 * RC_XP + 8 * g;  // + kx * RC_XP: input column px - 1 + kx sits in slot px + kx
-  const int ld = px0 * RC_DP + 8 * g;
-  const int lp = px0 * RC_DP + 8 * (g & 1);
-  const int dl = (px0 + 1) * RC_DP + 16 * (L - 1) + 4 * g;    // this lane's dense-ring store (fragment 2h)
-  const int ol = px0 * a.ocs + a.ooff[L - 1] + 4 * g;          // and HBM store, elements within an image row
-  const long orow = (long)a.w * a.ocs;
-  const float bb[4] = {bias.x, bias.y, bias.z, bias.w};
-  // step s: `cur` holds base row y1 + 2 (stored after the MFMAs), `nxt` receives row y1 + 3; `mcur` = this step's
-  // masks, `mnxt` receives the next step's
-  // output stores are raw buffer stores issued unconditionally every step (an out-of-range offset drops them): a store
-  // under the step's level-active / own-row branches made the compiler's vmcnt for the next base-row wait count it as
-  // maybe-not-issued, so that wait also drained this step's stores (measured: 7 of 31 us per forward launch)
   const __amdgpu_buffer_rsrc_t orr = buf_rsrc(a.out, a.out_bytes);
-  auto step = [&](int s, uint4 (&cur)[2], uint4 (&nxt)[2], const uint2 (&mcur)[2], uint2 (&mnxt)[2]) {
-    const int y1 = r0 - 3 + s;
-    issue_row(y1 + 3, nxt);
-    if constexpr (MODE == 1) issue_mask(s + 1, mnxt);
-    const bool active = live0 && s >= 3 * (L - 1) && s <= R + 4 + L;
-    const int y = y1 - 2 * (L - 1);
-    const bool own = active && y >= 0 && y < a.h && y >= r0 && y < r0 + R;
-    uint2 pko[2] = {make_uint2(0, 0), make_uint2(0, 0)};
-    if (active) {
-      int xr[3], dr[3];
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
+
+  // base-row DMA: instructions wvu and wvu + 8 (< 11); lane -> 16-B unit 64 k + lane = (pixel slot p, chunk j < 8)
+  uint32_t po[2];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        xr[k] = xslot(y - 1 + k) * RC_XROW;
-        dr[k] = dslot(y - 1 + k) * RC_DROW;
+  for (int j = 0; j < 2; ++j) {
+    const int k = wvu + 8 * j, u = 64 * k + lane, p = u / 10, jj = u - 10 * p, ix = p - 1;
+    po[j] = (k < RR_BNI && jj < 8 && p < RR_PX && ix >= 0 && ix < a.w) ? (uint32_t)((ix * a.bcs + a.boff + 8 * jj) * 2) : BUF_OOB;
+  }
+  const uint32_t brow = (uint32_t)a.w * (uint32_t)a.bcs * 2u;
+  auto dma_row = [&](int row) {  // base row `row` into its ring slot (row - r0 + 4) % 8
+    const uint32_t rb = (uint32_t)(nimg * a.h + row) * brow;
+    const uint32_t slot = lds0 + (uint32_t)(((row - r0 + 4) & (RR_NB - 1)) * RR_BSLOT);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      if (wvu + 8 * j < RR_BNI) {
+        uint32_t keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(po[j] == BUF_OOB ? BUF_OOB : po[j] + rb), "s"(br), "s"(slot + (uint32_t)((wvu + 8 * j) * 1024))
+                     : "memory");
       }
-      f32x4 acc[2];
-      level_acc<L>(lds, af, xr, dr, lx, ld, lp, g, acc[0], acc[1]);
-      const bool in = y >= 0 && y < a.h;  // rows outside the image: zeros, the next level's padding
-      uint16_t* drow = lds + RC_OFF_D + dslot(y) * RC_DROW + dl;
+  };
+
+  // A fragments: base [ky][kx][cb] and dense [ky][d] from the packed [16][9 KP] weights (k = tap KP + channel: base |
+  // out1 | out2 | out3 at channels 0 / 64 / 80 / 96)
+  bf16x8 Ab[3][3][2], Ad[3][ND > 0 ? ND : 1];
+  {
+    const uint16_t* wr = a.wt[L - 1] + col * 9 * KP;
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        float v[4];
+    for (int ky = 0; ky < 3; ++ky) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float t = acc[k][i] + bb[i];
-          if (MODE == 0) {
-            v[i] = fmaxf(t, t * a.slope);  // leaky relu, 0 <= slope <= 1 (checked on the host)
+      for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) Ab[ky][kx][cb] = *(const bf16x8*)(wr + (3 * ky + kx) * KP + cb * 32 + 8 * g);
+#pragma unroll
+      for (int d = 0; d < ND; ++d) {
+        int kx, ch;
+        bool zero = false;
+        if (L == 2 || d >= 3) {  // a 16-channel group (x1 at level 2, x3 at level 4) as a pair of tap columns
+          const int pr = L == 2 ? d : d - 3;
+          kx = pr == 0 ? (g < 2 ? 0 : 1) : 2;
+          zero = pr == 1 && g >= 2;
+          ch = (L == 2 ? 64 : 96) + 8 * (g & 1);
+        } else {  // x1 | x2 of tap column d
+          kx = d;
+          ch = 64 + 8 * g;
+        }
+        Ad[ky][d] = zero ? (bf16x8){} : *(const bf16x8*)(wr + (3 * ky + kx) * KP + ch);
+      }
+    }
+  }
+  float bb[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (MODE == 0) {
+    const float4 b4 = *(const float4*)(a.bias[L - 1] + 4 * g);
+    bb[0] = b4.x; bb[1] = b4.y; bb[2] = b4.z; bb[3] = b4.w;
+  }
+  // per-lane LDS offsets: base pixel slot col (+ 16 f + kx), chunk 4 cb + g; dense pixel slot col (+ ...), chunk g & 1
+  const int lb = col * RR_BP + g * 16;
+  const int ldn = col * RR_DP + (g & 1) * 16;
+  // completed-row epilogue: ring store of this lane's 4 channels (slot 1 + col of fragment f) and the HBM row store
+  const int dl = (1 + 32 * fp + col) * RR_DP + g * 8;
+  const int ol = (32 * fp + col) * a.ocs + a.ooff[L - 1] + 4 * g;
+  const int ml = (32 * fp + col) * a.mcs + a.moff[L - 1] + 4 * g;
+  const uint32_t orow = (uint32_t)a.w * (uint32_t)a.ocs * 2u, mrow = (uint32_t)a.w * (uint32_t)a.mcs * 2u;
+
+  f32x4 acc[3][2];  // rows i - 1, i, i + 1 of the ingested row i
+#pragma unroll
+  for (int r = 0; r < 3; ++r) acc[r][0] = acc[r][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // rows of this level: ingested [r0 - 5 + L, r1 + 4 - L], finished [r0 - 4 + L, r1 + 4 - L)
+  const int ilo = r0 - 5 + L, ihi = r1 + 4 - L, clo = r0 - 4 + L, chi = r1 + 4 - L;
+  const int nsteps = r1 - r0 + 11;
+  if (r0 - 4 >= 0) dma_row(r0 - 4);  // level 1's row of step 0
+  for (int s = 0; s < nsteps; ++s) {
+    const int i = r0 - 2 - 2 * L + s;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    // pull: the stored activation of the row finished in this step (used after the MFMAs)
+    const int y = i - 1;
+    const bool fin = y >= clo && y < chi, yin = y >= 0 && y < a.h;
+    v2u32 m[2] = {};
+    if (MODE == 1) {
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        const bool ok = fin && yin && (f == 0 ? live0 : live1);
+        m[f] = __builtin_amdgcn_raw_buffer_load_b64(mr, ok ? (uint32_t)(nimg * a.h + y) * mrow + (uint32_t)((ml + 16 * f * a.mcs) * 2) : BUF_OOB, 0, 0);
+      }
+    }
+    // the base row level 1 ingests next step
+    {
+      const int b = r0 - 3 + s;
+      if (b <= r1 + 3 && b >= 0 && b < a.h) dma_row(b);
+    }
+    // ingest row i.  All three kernel rows and both fragments are computed unconditionally: a target row outside this
+    // level's finished range or outside the image is never finished from its accumulator (the rows a finished row
+    // needs are all ingested), and the pixel slots of a fragment past the image width hold zeros
+    if (i >= ilo && i <= ihi && i >= 0 && i < a.h) {
+      const char* bsl = smem + ((i - r0 + 4) & (RR_NB - 1)) * RR_BSLOT + lb;
+      const char* x1r = smem + RR_OFF_D + ((i - r0 + 3) % RR_N1) * RR_DROW + ldn;
+      const char* x2r = smem + RR_OFF_2 + ((i - r0 + 2) % RR_N2) * RR_DROW + ldn;
+      const char* x3r = smem + RR_OFF_3 + ((i - r0 + 1) % RR_N3) * RR_DROW + ldn;
+      bf16x8 B[2][2];
+      auto ldB = [&](int grp, int buf) {
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          const int px = 16 * (2 * fp + f);
+          if (grp < 6) {
+            const int kx = grp >> 1, cb = grp & 1;
+            B[buf][f] = *(const bf16x8*)(bsl + (px + kx) * RR_BP + cb * 64);
           } else {
-            const uint32_t mw = i < 2 ? mcur[k].x : mcur[k].y;
-            const float m = __uint_as_float((i & 1) ? (mw & 0xFFFF0000u) : (mw << 16));  // the stored activation
-            v[i] = m > 0.f ? t : t * a.slope;
+            const int d = grp - 6;
+            const char* src;
+            int kx;
+            if (L == 2 || d >= 3) {
+              const int pr = L == 2 ? d : d - 3;
+              kx = pr == 0 ? (g < 2 ? 0 : 1) : 2;
+              src = L == 2 ? x1r : x3r;
+            } else {
+              kx = d;
+              src = g < 2 ? x1r : x2r;
+            }
+            B[buf][f] = *(const bf16x8*)(src + (px + kx) * RR_DP);
           }
         }
-        uint2 pk = make_uint2(pack2_bf16(v[0], v[1]), pack2_bf16(v[2], v[3]));
-        if (!in) pk = make_uint2(0, 0);
-        if (L < 4 && (k == 0 || live1)) *(uint2*)(drow + 16 * k * RC_DP) = pk;
-        pko[k] = pk;
+      };
+      ldB(0, 0);
+#pragma unroll
+      for (int grp = 0; grp < NG; ++grp) {
+        if (grp + 1 < NG) ldB(grp + 1, (grp + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          const bf16x8 af = grp < 6 ? Ab[ky][grp >> 1][grp & 1] : Ad[ky][grp < 6 ? 0 : grp - 6];
+#pragma unroll
+          for (int f = 0; f < 2; ++f) acc[2 - ky][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, B[grp & 1][f], acc[2 - ky][f], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
-    const uint32_t ob = (uint32_t)((row0 + y) * orow + ol) * 2u;
+    // row y = i - 1 is complete: epilogue into this level's ring (zeros outside the image: the next level's padding)
+    // and the strip's own rows to HBM (raw stores issued unconditionally; an out-of-range offset drops them)
+    if (fin) {
+      uint2 pk[2];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const bool ok = own && (k == 0 || live1);
-      __builtin_amdgcn_raw_buffer_store_b64((v2u32){pko[k].x, pko[k].y}, orr, ok ? ob + (uint32_t)(16 * k * a.ocs * 2) : BUF_OOB, 0, 0);
+      for (int f = 0; f < 2; ++f) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float t = acc[0][f][e] + bb[e];
+          if (MODE == 0) {
+            v[e] = fmaxf(t, t * a.slope);  // leaky relu, 0 <= slope <= 1 (checked on the host)
+          } else {
+            const uint32_t mw = e < 2 ? m[f][0] : m[f][1];
+            const float mv = __uint_as_float((e & 1) ? (mw & 0xFFFF0000u) : (mw << 16));
+            v[e] = mv > 0.f ? t : t * a.slope;
+          }
+        }
+        pk[f] = yin ? make_uint2(pack2_bf16(v[0], v[1]), pack2_bf16(v[2], v[3])) : make_uint2(0u, 0u);
+      }
+      if constexpr (L < 4) {
+        char* ring = smem + (L == 1 ? RR_OFF_D + ((y - r0 + 3) % RR_N1) * RR_DROW
+                                    : (L == 2 ? RR_OFF_2 + ((y - r0 + 2) % RR_N2) * RR_DROW : RR_OFF_3 + ((y - r0 + 1) % RR_N3) * RR_DROW));
+        if (live0) *(uint2*)(ring + dl) = pk[0];
+        if (live1) *(uint2*)(ring + dl + 16 * RR_DP) = pk[1];
+      }
+      const bool own = yin && y >= r0 && y < r1;
+      const uint32_t ob = (uint32_t)(nimg * a.h + y) * orow + (uint32_t)(ol * 2);
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        const bool ok = own && (f == 0 ? live0 : live1);
+        __builtin_amdgcn_raw_buffer_store_b64((v2u32){pk[f].x, pk[f].y}, orr, ok ? ob + (uint32_t)(16 * f * a.ocs * 2) : BUF_OOB, 0, 0);
+      }
     }
-    store_row(y1 + 2, cur);  // its slot held row y1 - 8, which no level reads in this step
-    lds_barrier();
-  };
-  for (int s = 0; s < R + 9; s += 2) {
-    step(s, ra, rb, ma, mb);
-    if (s + 1 < R + 9) step(s + 1, rb, ra, mb, ma);
+    // rotate: row i becomes the next step's row i - 1
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      acc[0][f] = acc[1][f];
+      acc[1][f] = acc[2][f];
+      acc[2][f] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
   }
 }
 
 // Waves w and w + 4 share a SIMD (a workgroup's waves go round the 4 SIMDs in a fixed cyclic order).  Wave w < 4
-// computes level w + 1, wave w >= 4 level 8 - w, so each SIMD pairs a light and a heavy level (1+4, 2+3: 50 of the
-// 100 MFMA blocks per row each) instead of carrying one level: the per-step critical path is the slowest SIMD.
-// Wave w covers column fragments 2 (w >> 2) and 2 (w >> 2) + 1.
+// computes level w + 1, wave w >= 4 level 8 - w; wave w covers column fragments 2 (w >> 2) and 2 (w >> 2) + 1.
 template <int MODE>
-__global__ __launch_bounds__(512, 1) void rdb_chain_kernel(ChainArgs a) {
+__global__ __launch_bounds__(512, 1) void rdb_chain_rr_kernel(ChainArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint16_t* lds = (uint16_t*)smem;
   const int tid = threadIdx.x;
   const int nimg = blockIdx.x / a.strips_y, r0 = (blockIdx.x % a.strips_y) * a.rows;
+  const int r1 = min(r0 + a.rows, a.h);
+  // the level-output rings start zeroed: their pixel slots of image columns -1 and >= w are never written (padding)
+  for (int i = tid; i < (RR_LDS - RR_OFF_D) / 16; i += 512) *(uint4*)(smem + RR_OFF_D + 16 * i) = make_uint4(0, 0, 0, 0);
   const int w = tid >> 6;
   switch (w < 4 ? w : 7 - w) {
-    case 0: run_level<MODE, 1>(a, lds, tid, nimg, r0); break;
-    case 1: run_level<MODE, 2>(a, lds, tid, nimg, r0); break;
-    case 2: run_level<MODE, 3>(a, lds, tid, nimg, r0); break;
-    default: run_level<MODE, 4>(a, lds, tid, nimg, r0); break;
+    case 0: run_level<MODE, 1>(a, smem, tid, nimg, r0, r1); break;
+    case 1: run_level<MODE, 2>(a, smem, tid, nimg, r0, r1); break;
+    case 2: run_level<MODE, 3>(a, smem, tid, nimg, r0, r1); break;
+    default: run_level<MODE, 4>(a, smem, tid, nimg, r0, r1); break;
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 }  // namespace
@@ -347,7 +303,7 @@ int rdb_chain_narrow(const ClimsrChainDesc* d, hipStream_t stream) {
   a.base_bytes = (uint32_t)(px * d->bcs * 2);
   a.out_bytes = (uint32_t)(px * d->ocs * 2);
   a.mask_bytes = d->act == 3 ? (uint32_t)(px * d->mcs * 2) : 0u;
-  // strip height: enough strips to give every CU one (a strip recomputes 3 + 2 + 1 halo rows per level chain)
+  // strip height: enough strips to give every CU one (a strip recomputes 3 + 2 + 1 halo rows per level)
   int rows = ceil_div((long)d->n * d->h, device_cus());
   if (rows < 2) rows = 2;
   if (rows > 32) rows = 32;
@@ -355,11 +311,11 @@ int rdb_chain_narrow(const ClimsrChainDesc* d, hipStream_t stream) {
   a.rows = rows;
   a.strips_y = ceil_div(d->h, rows);
   if (d->act == 1) {
-    if (int e = lds_opt_in((const void*)rdb_chain_kernel<0>, RC_LDS)) return e;
-    hipLaunchKernelGGL(rdb_chain_kernel<0>, dim3(a.strips_y * a.n), dim3(512), RC_LDS, stream, a);
+    if (int e = lds_opt_in((const void*)rdb_chain_rr_kernel<0>, RR_LDS)) return e;
+    hipLaunchKernelGGL(rdb_chain_rr_kernel<0>, dim3(a.strips_y * a.n), dim3(512), RR_LDS, stream, a);
   } else {
-    if (int e = lds_opt_in((const void*)rdb_chain_kernel<1>, RC_LDS)) return e;
-    hipLaunchKernelGGL(rdb_chain_kernel<1>, dim3(a.strips_y * a.n), dim3(512), RC_LDS, stream, a);
+    if (int e = lds_opt_in((const void*)rdb_chain_rr_kernel<1>, RR_LDS)) return e;
+    hipLaunchKernelGGL(rdb_chain_rr_kernel<1>, dim3(a.strips_y * a.n), dim3(512), RR_LDS, stream, a);
   }
   return check_launch("rdb_chain");
 }

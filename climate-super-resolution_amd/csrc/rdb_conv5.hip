@@ -106,10 +106,6 @@ __global__ __launch_bounds__(512, 1) void rdb5_kernel(R5Args a) {
   const bool has2 = a.res2 != nullptr, has_aux = MODE == 2 && a.aux != nullptr;
   const __amdgpu_buffer_rsrc_t rr1 = buf_rsrc(a.res1, a.r1_bytes), rr2 = buf_rsrc(a.res2, has2 ? a.r2_bytes : 0u);
   const __amdgpu_buffer_rsrc_t ry = buf_rsrc(a.y, a.y_bytes), rax = buf_rsrc(a.aux, has_aux ? a.aux_bytes : 0u);
-  bool fon[4];  // 16-pixel fragments inside the image
-#pragma unroll
-  for (int f = 0; f < 4; ++f) fon[f] = c0 + 16 * f < a.w;
-
   f32x4 acc[3][4];
 #pragma unroll
   for (int s = 0; s < 3; ++s)
@@ -164,7 +160,7 @@ __global__ __launch_bounds__(512, 1) void rdb5_kernel(R5Args a) {
       for (int m = 0; m < 2; ++m) {
         const int f = 2 * hh + m;
         const f32x4 other = *(const f32x4*)(part + (q * 4 + f) * 1024 + lane * 16);
-        const f32x4 own = acc[SA][f];
+        const f32x4 own = hh == 0 ? acc[SA][m] : acc[SA][2 + m];  // (a register select: acc is never indexed at run time)
         const f32x4 sum = hh == 0 ? own + other : other + own;
         const bool ok = pix_ok(yf, m);
         const uint32_t p = ok ? pidx(yf, m) : 0u;
@@ -195,10 +191,9 @@ __global__ __launch_bounds__(512, 1) void rdb5_kernel(R5Args a) {
     // the next row lands in the other slot (its previous row was last read in the previous step)
     if (i + 1 <= r1 && i + 1 < a.h) dma_row(i + 1, (K + 1) & 1);
     // ingest row i: kernel row ky adds to output row i + 1 - ky
+    // ingest row i.  Every MFMA is issued unconditionally: a target row outside the strip lands in an accumulator row
+    // that is zeroed before its next use and never finished, and a fragment past the image width reads zeros
     if (i >= 0 && i < a.h && i <= r1) {
-      bool kyon[3];
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky) kyon[ky] = i + 1 - ky >= r0 && i + 1 - ky < r1;
       const char* xs = smem + (K & 1) * R5_SLOT + lb;
       bf16x8 B[2][4];
       auto ldB = [&](int grp, int buf) {
@@ -214,16 +209,10 @@ __global__ __launch_bounds__(512, 1) void rdb5_kernel(R5Args a) {
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky) {
-          if (kyon[ky]) {
-            const int sl = ky == 0 ? SA : (ky == 1 ? (K + 2) % 3 : SC);  // rows r0 + s, r0 + s - 1, r0 + s - 2
+          constexpr int SL[3] = {SA, (K + 2) % 3, SC};  // rows r0 + s, r0 + s - 1, r0 + s - 2
 #pragma unroll
-            for (int f = 0; f < 4; ++f)
-              if (fon[f]) {
-                if (sl == 0) acc[0][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ky][kx][cb], B[grp & 1][f], acc[0][f], 0, 0, 0);
-                else if (sl == 1) acc[1][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ky][kx][cb], B[grp & 1][f], acc[1][f], 0, 0, 0);
-                else acc[2][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ky][kx][cb], B[grp & 1][f], acc[2][f], 0, 0, 0);
-              }
-          }
+          for (int f = 0; f < 4; ++f)
+            acc[SL[ky]][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ky][kx][cb], B[grp & 1][f], acc[SL[ky]][f], 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -234,7 +223,7 @@ __global__ __launch_bounds__(512, 1) void rdb5_kernel(R5Args a) {
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
         const int f = 2 * (1 - hh) + m;
-        *(f32x4*)(part + (q * 4 + f) * 1024 + lane * 16) = acc[SC][f];
+        *(f32x4*)(part + (q * 4 + f) * 1024 + lane * 16) = hh == 0 ? acc[SC][2 + m] : acc[SC][m];
       }
     }
   };
