@@ -51,13 +51,15 @@ constexpr int RR_PX = 66;                               // pixel slots per row: 
 constexpr int RR_BP = 160;                              // base pixel pitch: 64 ch + 32 B pad (10 units of 16 B)
 constexpr int RR_BNI = (RR_PX * 10 + 63) / 64;          // base-row DMA instructions (11)
 constexpr int RR_BSLOT = RR_BNI * 1024;                 // 11,264 B per base row (whole DMA instructions)
-constexpr int RR_NB = 8;                                // base ring rows
+constexpr int RR_NB = 9;                                // base ring rows (requested two steps ahead, read until L4)
 constexpr int RR_DP = 32;                               // dense pixel pitch (16 ch)
 constexpr int RR_DROW = RR_PX * RR_DP;                  // 2,112 B
 constexpr int RR_N1 = 6, RR_N2 = 4, RR_N3 = 2;          // x1 / x2 / x3 ring rows
 constexpr int RR_OFF_D = RR_NB * RR_BSLOT;              // 90,112
 constexpr int RR_OFF_2 = RR_OFF_D + RR_N1 * RR_DROW, RR_OFF_3 = RR_OFF_2 + RR_N2 * RR_DROW;
-constexpr int RR_LDS = RR_OFF_3 + RR_N3 * RR_DROW;      // 115,456 B
+constexpr int RR_OFF_DUMMY = RR_OFF_3 + RR_N3 * RR_DROW;  // one KB the padding DMA pieces write (zeros, never read)
+constexpr int RR_LDS = RR_OFF_DUMMY + 1024;             // 127,744 B
+constexpr int RR_K = 2;                                 // base-row DMA pieces per wave (11 real + 5 padding)
 
 __device__ __forceinline__ uint32_t pack2_bf16(float a, float b) {
   const bf16x2 v = {(__bf16)a, (__bf16)b};  // v_cvt_pk_bf16_f32 (RNE)
@@ -89,17 +91,21 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, char* smem, int ti
     po[j] = (k < RR_BNI && jj < 8 && p < RR_PX && ix >= 0 && ix < a.w) ? (uint32_t)((ix * a.bcs + a.boff + 8 * jj) * 2) : BUF_OOB;
   }
   const uint32_t brow = (uint32_t)a.w * (uint32_t)a.bcs * 2u;
-  auto dma_row = [&](int row) {  // base row `row` into its ring slot (row - r0 + 4) % 8
-    const uint32_t rb = (uint32_t)(nimg * a.h + row) * brow;
-    const uint32_t slot = lds0 + (uint32_t)(((row - r0 + 4) & (RR_NB - 1)) * RR_BSLOT);
+  // base row `row` into ring slot (row - r0 + 4) % 9; every wave issues exactly RR_K pieces (rows outside the strip's
+  // range or the image, and pieces past the 11th, read out of range into the dummy KB)
+  auto dma_row = [&](int row) {
+    const bool ok = row >= r0 - 4 && row <= r1 + 3 && row >= 0 && row < a.h;
+    const uint32_t rb = ok ? (uint32_t)(nimg * a.h + row) * brow : 0u;
+    const uint32_t slot = lds0 + (uint32_t)((ok ? (row - r0 + 4) % RR_NB : 0) * RR_BSLOT);
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-      if (wvu + 8 * j < RR_BNI) {
-        uint32_t keep;
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep) : "v"(po[j] == BUF_OOB ? BUF_OOB : po[j] + rb), "s"(br), "s"(slot + (uint32_t)((wvu + 8 * j) * 1024))
-                     : "memory");
-      }
+    for (int j = 0; j < RR_K; ++j) {
+      const bool real = ok && wvu + 8 * j < RR_BNI;
+      uint32_t keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(real && po[j] != BUF_OOB ? po[j] + rb : BUF_OOB), "s"(br),
+                     "s"(real ? slot + (uint32_t)((wvu + 8 * j) * 1024) : lds0 + (uint32_t)RR_OFF_DUMMY)
+                   : "memory");
+    }
   };
 
   // A fragments: base [ky][kx][cb] and dense [ky][d] from the packed [16][9 KP] weights (k = tap KP + channel: base |
@@ -144,41 +150,45 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, char* smem, int ti
   const int ml = (32 * fp + col) * a.mcs + a.moff[L - 1] + 4 * g;
   const uint32_t orow = (uint32_t)a.w * (uint32_t)a.ocs * 2u, mrow = (uint32_t)a.w * (uint32_t)a.mcs * 2u;
 
-  f32x4 acc[3][2];  // rows i - 1, i, i + 1 of the ingested row i
+  // Per step every wave issues, in this order: RL mask loads (pull: the activation of the row it finishes two steps
+  // later), RR_K DMA pieces (the base row level 1 ingests two steps later), 2 row stores (raw, unconditional).  Step s
+  // needs the DMA of step s - 2; younger are step s - 2's stores and step s - 1's operations.
+  constexpr int RL = MODE == 1 ? 2 : 0, NW = 2 + RL + RR_K + 2;
+  f32x4 acc[3][2];  // accumulator row of output row y: (y - r0) mod 3 (phase-resolved at compile time)
 #pragma unroll
   for (int r = 0; r < 3; ++r) acc[r][0] = acc[r][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  v2u32 msk[3][2];  // pull: the stored activation of the row finished in step s, loaded in step s - 2 (set s mod 3)
   // rows of this level: ingested [r0 - 5 + L, r1 + 4 - L], finished [r0 - 4 + L, r1 + 4 - L)
   const int ilo = r0 - 5 + L, ihi = r1 + 4 - L, clo = r0 - 4 + L, chi = r1 + 4 - L;
   const int nsteps = r1 - r0 + 11;
-  if (r0 - 4 >= 0) dma_row(r0 - 4);  // level 1's row of step 0
-  for (int s = 0; s < nsteps; ++s) {
+  dma_row(r0 - 4);  // level 1's rows of steps 0 and 1
+  dma_row(r0 - 3);
+  // step s (phase K = s mod 3): level L ingests row i = r0 - 2 - 2L + s and finishes row i - 1
+  auto step = [&](auto kc, int s) {
+    constexpr int K = decltype(kc)::value;
     const int i = r0 - 2 - 2 * L + s;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (s == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NW) : "memory");
     lds_barrier();
-    // pull: the stored activation of the row finished in this step (used after the MFMAs)
-    const int y = i - 1;
-    const bool fin = y >= clo && y < chi, yin = y >= 0 && y < a.h;
-    v2u32 m[2] = {};
-    if (MODE == 1) {
+    if constexpr (MODE == 1) {  // the activation of row i + 1 (finished two steps later)
+      const int y2 = i + 1;
+      const bool ok2 = y2 >= clo && y2 < chi && y2 >= 0 && y2 < a.h;
 #pragma unroll
-      for (int f = 0; f < 2; ++f) {
-        const bool ok = fin && yin && (f == 0 ? live0 : live1);
-        m[f] = __builtin_amdgcn_raw_buffer_load_b64(mr, ok ? (uint32_t)(nimg * a.h + y) * mrow + (uint32_t)((ml + 16 * f * a.mcs) * 2) : BUF_OOB, 0, 0);
-      }
+      for (int f = 0; f < 2; ++f)
+        msk[K][f] = __builtin_amdgcn_raw_buffer_load_b64(mr, ok2 && (f == 0 ? live0 : live1)
+                                                                 ? (uint32_t)(nimg * a.h + y2) * mrow + (uint32_t)((ml + 16 * f * a.mcs) * 2)
+                                                                 : BUF_OOB, 0, 0);
     }
-    // the base row level 1 ingests next step
-    {
-      const int b = r0 - 3 + s;
-      if (b <= r1 + 3 && b >= 0 && b < a.h) dma_row(b);
-    }
+    dma_row(r0 - 2 + s);  // the base row level 1 ingests in step s + 2
     // ingest row i.  All three kernel rows and both fragments are computed unconditionally: a target row outside this
     // level's finished range or outside the image is never finished from its accumulator (the rows a finished row
     // needs are all ingested), and the pixel slots of a fragment past the image width hold zeros
+    constexpr int SN = (K + 2) % 3, SI = (K + 1) % 3, SP = K;  // accumulator rows of output rows i + 1, i, i - 1
     if (i >= ilo && i <= ihi && i >= 0 && i < a.h) {
-      const char* bsl = smem + ((i - r0 + 4) & (RR_NB - 1)) * RR_BSLOT + lb;
-      const char* x1r = smem + RR_OFF_D + ((i - r0 + 3) % RR_N1) * RR_DROW + ldn;
-      const char* x2r = smem + RR_OFF_2 + ((i - r0 + 2) % RR_N2) * RR_DROW + ldn;
-      const char* x3r = smem + RR_OFF_3 + ((i - r0 + 1) % RR_N3) * RR_DROW + ldn;
+      const char* bsl = smem + ((i - r0 + 4) % RR_NB) * RR_BSLOT + lb;
+      const char* x1r = smem + RR_OFF_D + ((i - r0 + 3 + RR_N1) % RR_N1) * RR_DROW + ldn;
+      const char* x2r = smem + RR_OFF_2 + ((i - r0 + 2 + RR_N2) % RR_N2) * RR_DROW + ldn;
+      const char* x3r = smem + RR_OFF_3 + ((i - r0 + 1 + RR_N3) % RR_N3) * RR_DROW + ldn;
       bf16x8 B[2][2];
       auto ldB = [&](int grp, int buf) {
 #pragma unroll
@@ -211,53 +221,56 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, char* smem, int ti
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky) {
           const bf16x8 af = grp < 6 ? Ab[ky][grp >> 1][grp & 1] : Ad[ky][grp < 6 ? 0 : grp - 6];
+          constexpr int SL[3] = {SN, SI, SP};
 #pragma unroll
-          for (int f = 0; f < 2; ++f) acc[2 - ky][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, B[grp & 1][f], acc[2 - ky][f], 0, 0, 0);
+          for (int f = 0; f < 2; ++f) acc[SL[ky]][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, B[grp & 1][f], acc[SL[ky]][f], 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
     }
     // row y = i - 1 is complete: epilogue into this level's ring (zeros outside the image: the next level's padding)
-    // and the strip's own rows to HBM (raw stores issued unconditionally; an out-of-range offset drops them)
-    if (fin) {
-      uint2 pk[2];
+    // and the strip's own rows to HBM (2 raw stores, unconditional; an out-of-range offset drops them)
+    const int y = i - 1;
+    const bool fin = y >= clo && y < chi, yin = y >= 0 && y < a.h;
+    uint2 pk[2];
 #pragma unroll
-      for (int f = 0; f < 2; ++f) {
-        float v[4];
+    for (int f = 0; f < 2; ++f) {
+      float v[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float t = acc[0][f][e] + bb[e];
-          if (MODE == 0) {
-            v[e] = fmaxf(t, t * a.slope);  // leaky relu, 0 <= slope <= 1 (checked on the host)
-          } else {
-            const uint32_t mw = e < 2 ? m[f][0] : m[f][1];
-            const float mv = __uint_as_float((e & 1) ? (mw & 0xFFFF0000u) : (mw << 16));
-            v[e] = mv > 0.f ? t : t * a.slope;
-          }
+      for (int e = 0; e < 4; ++e) {
+        const float t = acc[SP][f][e] + bb[e];
+        if (MODE == 0) {
+          v[e] = fmaxf(t, t * a.slope);  // leaky relu, 0 <= slope <= 1 (checked on the host)
+        } else {
+          const uint32_t mw = e < 2 ? msk[(K + 1) % 3][f][0] : msk[(K + 1) % 3][f][1];
+          const float mv = __uint_as_float((e & 1) ? (mw & 0xFFFF0000u) : (mw << 16));
+          v[e] = mv > 0.f ? t : t * a.slope;
         }
-        pk[f] = yin ? make_uint2(pack2_bf16(v[0], v[1]), pack2_bf16(v[2], v[3])) : make_uint2(0u, 0u);
       }
-      if constexpr (L < 4) {
+      pk[f] = yin ? make_uint2(pack2_bf16(v[0], v[1]), pack2_bf16(v[2], v[3])) : make_uint2(0u, 0u);
+    }
+    if constexpr (L < 4) {
+      if (fin) {
         char* ring = smem + (L == 1 ? RR_OFF_D + ((y - r0 + 3) % RR_N1) * RR_DROW
                                     : (L == 2 ? RR_OFF_2 + ((y - r0 + 2) % RR_N2) * RR_DROW : RR_OFF_3 + ((y - r0 + 1) % RR_N3) * RR_DROW));
         if (live0) *(uint2*)(ring + dl) = pk[0];
         if (live1) *(uint2*)(ring + dl + 16 * RR_DP) = pk[1];
       }
-      const bool own = yin && y >= r0 && y < r1;
-      const uint32_t ob = (uint32_t)(nimg * a.h + y) * orow + (uint32_t)(ol * 2);
-#pragma unroll
-      for (int f = 0; f < 2; ++f) {
-        const bool ok = own && (f == 0 ? live0 : live1);
-        __builtin_amdgcn_raw_buffer_store_b64((v2u32){pk[f].x, pk[f].y}, orr, ok ? ob + (uint32_t)(16 * f * a.ocs * 2) : BUF_OOB, 0, 0);
-      }
     }
-    // rotate: row i becomes the next step's row i - 1
+    const bool own = fin && yin && y >= r0 && y < r1;
+    const uint32_t ob = own ? (uint32_t)(nimg * a.h + y) * orow + (uint32_t)(ol * 2) : 0u;
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
-      acc[0][f] = acc[1][f];
-      acc[1][f] = acc[2][f];
-      acc[2][f] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      const bool ok = own && (f == 0 ? live0 : live1);
+      __builtin_amdgcn_raw_buffer_store_b64((v2u32){pk[f].x, pk[f].y}, orr, ok ? ob + (uint32_t)(16 * f * a.ocs * 2) : BUF_OOB, 0, 0);
     }
+#pragma unroll
+    for (int f = 0; f < 2; ++f) acc[SP][f] = (f32x4){0.f, 0.f, 0.f, 0.f};  // becomes row i + 2's next step
+  };
+  for (int s = 0; s < nsteps; s += 3) {
+    step(std::integral_constant<int, 0>{}, s);
+    if (s + 1 < nsteps) step(std::integral_constant<int, 1>{}, s + 1);
+    if (s + 2 < nsteps) step(std::integral_constant<int, 2>{}, s + 2);
   }
 }
 

@@ -4,7 +4,7 @@
 // [dZ1 | .. | dZ5] (fp32 out + skip gradients + the previous block's bf16 dZ5).
 //
 // Row streaming with input-row reuse.  A workgroup owns a strip of R output rows x 64 columns and ingests the R + 2
-// input rows it needs one at a time (LDS-DMA, two row slots, the next row landing under the current row's MFMAs).
+// input rows it needs one at a time (LDS-DMA into three row slots: two rows in flight under the current row's MFMAs).
 // An ingested row feeds all three kernel rows at once: B fragment (row i, tap column kx) is multiplied by the weights
 // of taps (0, kx), (1, kx), (2, kx) into the accumulators of output rows i + 1, i, i - 1, so each 1 KB fragment read
 // from LDS feeds three MFMAs (a per-output-row implicit GEMM reads it three times).  Output row i - 1 is complete
@@ -13,8 +13,8 @@
 // 16-pixel fragments of a row; its 18 weight fragments (3 x 3 taps x 2 channel blocks of 32) stay in registers for
 // the launch.  The two channel halves of an output block are summed through LDS (each wave finishes two of the four
 // fragments, in a fixed order: half 0 + half 1, deterministic) before the epilogue.
-// One barrier per row: every VMEM operation of a step (residual loads, the next row's DMA, stores) is waited for at
-// the next step's `s_waitcnt vmcnt(0)`, one step (~ 72 MFMAs per wave) after it was issued.
+// One barrier per row; the residual operands of a row are loaded two steps before it is finished, and the waits are
+// counted by hand (see the step loop) so that the next row's DMA stays in flight across them.
 // LDS pixel slots are 288 B (128 channels + 32 B pad): the 16-B unit of channel chunk c of slot p is 18 p + c, so
 // the 16 lanes of each ds_read_b128 bank group (two channel groups, 8 pixels each) cover the 64 banks once.
 // MFMA v_mfma_f32_16x16x32_bf16: A = weights [16 co][32 channels], B = [32 channels][16 pixels].
@@ -27,8 +27,12 @@ constexpr int R5_PITCH = 288;                      // bytes per pixel slot (18 u
 constexpr int R5_UNITS = R5_PX * 18;               // 1188
 constexpr int R5_NI = (R5_UNITS + 63) / 64;        // DMA instructions per row (19)
 constexpr int R5_SLOT = R5_NI * 1024;              // 19,456 B
+constexpr int R5_NSLOT = 3;                        // row slots: the row being read, and two in flight
 constexpr int R5_PART = 16 * 1024;                 // one partial-sum exchange region: [co block][fragment][lane] f32x4
-constexpr int R5_LDS = 2 * R5_SLOT + 2 * R5_PART;  // 71,680 B
+constexpr int R5_OFF_P = R5_NSLOT * R5_SLOT;       // 58,368
+constexpr int R5_OFF_DUMMY = R5_OFF_P + 2 * R5_PART;  // one KB the padding DMA pieces write (zeros, never read)
+constexpr int R5_LDS = R5_OFF_DUMMY + 1024;        // 92,160 B
+constexpr int R5_K = 3;                            // DMA pieces per wave and row (19 real + 5 padding over 8 waves)
 
 struct R5Args {
   const uint16_t* x;
@@ -80,13 +84,6 @@ __global__ __launch_bounds__(512, 1) void rdb5_kernel(R5Args a) {
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(off), "s"(xr), "s"(lds) : "memory");
   };
-  auto dma_row = [&](int row, int slot) {
-    const uint32_t rb = (uint32_t)(nimg * a.h + row) * xrow;
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-      if (wvu + 8 * j < R5_NI) glds(po[j] == BUF_OOB ? BUF_OOB : po[j] + rb, lds0 + (uint32_t)(slot * R5_SLOT + (wvu + 8 * j) * 1024));
-  };
-
   // the 18 weight fragments: tap (ky, kx), channel block 2 hh + cb (packed [co][chunk][tap][32], chunk pitch 288)
   bf16x8 A[3][3][2];
   {
@@ -111,9 +108,9 @@ __global__ __launch_bounds__(512, 1) void rdb5_kernel(R5Args a) {
   for (int s = 0; s < 3; ++s)
 #pragma unroll
     for (int f = 0; f < 4; ++f) acc[s][f] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  // residual operands of the two fragments this wave finishes (f = 2 hh + m), two sets (loaded one step ahead)
+  // residual operands of the two fragments this wave finishes (f = 2 hh + m): three sets, loaded two steps ahead
   typedef uint32_t rv_t __attribute__((ext_vector_type(F32 ? 4 : 2)));
-  rv_t rs1[2][2], rs2[2][2];
+  rv_t rs1[3][2], rs2[3][2];
   auto pix_ok = [&](int y, int m) { return y >= r0 && y < r1 && c0 + 16 * (2 * hh + m) + col < a.w; };
   auto pidx = [&](int y, int m) { return (uint32_t)((nimg * a.h + y) * a.w + c0 + 16 * (2 * hh + m) + col); };
   auto load_res = [&](int y, rv_t (&r1v)[2], rv_t (&r2v)[2]) {
@@ -139,62 +136,81 @@ __global__ __launch_bounds__(512, 1) void rdb5_kernel(R5Args a) {
   };
   const int lb = col * R5_PITCH + (8 * hh + g) * 16;  // this lane's B offset: pixel slot col (+ 16 f + kx), chunk 8 hh + 4 cb + g
 
+  // Hand-counted waits.  Per step every wave issues, in this order, RL residual loads (for the row it finishes two
+  // steps later), ST stores (the row it finishes now) and R5_K DMA pieces (the row it ingests two steps later), all
+  // unconditionally (out-of-range offsets / the dummy KB where there is nothing to move).  Step s needs the DMA of
+  // step s - 2: younger are step s - 1's RL + ST + R5_K operations.  hipcc's own wait for the residuals of step s - 2
+  // counts only its loads and stores (2 ST + 2 RL younger ones), which with ST >= R5_K also leaves step s - 1's DMA
+  // in flight.
+  constexpr int RL = 4, ST = F32 ? 4 : 3, NW = RL + ST + R5_K;
+  static_assert(ST >= R5_K, "the compiler's residual wait must not drain the next row's DMA");
   const int nsteps = r1 - r0 + 3;  // ingest rows r0 - 1 .. r1, finish rows r0 .. r1 - 1 one step after completion
-  if (r0 - 1 >= 0) dma_row(r0 - 1, 0);
+  auto dma_step = [&](int row, int slot) {
+    const bool ok = row >= r0 - 1 && row <= r1 && row >= 0 && row < a.h;
+    const uint32_t rb = ok ? (uint32_t)(nimg * a.h + row) * xrow : 0u;
+#pragma unroll
+    for (int j = 0; j < R5_K; ++j) {
+      const bool real = ok && wvu + 8 * j < R5_NI;
+      glds(real && po[j] != BUF_OOB ? po[j] + rb : BUF_OOB,
+           lds0 + (uint32_t)(real ? slot * R5_SLOT + (wvu + 8 * j) * 1024 : R5_OFF_DUMMY));
+    }
+  };
+  dma_step(r0 - 1, 0);
+  dma_step(r0, 1);
 
-  // step s (compile-time phase K = s mod 6: LDS slot / partial region / residual set by K & 1, accumulator row by K % 3)
+  // step s (compile-time phase K = s mod 6: row slot, residual set and accumulator row by K % 3, partial region by K & 1)
   auto step = [&](auto kc, int s) {
     constexpr int K = decltype(kc)::value;
     constexpr int SA = K % 3;         // accumulator row of output row r0 + s (ky = 0 target) == the row finished here
     constexpr int SC = (K + 1) % 3;   // accumulator row of output row r0 + s - 2 (completed in this step)
-    const int i = r0 - 1 + s;         // the row ingested in this step
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int i = r0 - 1 + s;         // the row ingested in this step (slot K % 3)
+    if (s == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NW) : "memory");
     lds_barrier();
-    // residual operands of row i - 1 (finished next step)
-    load_res(i - 1, rs1[K & 1], rs2[K & 1]);
-    // finish row i - 2 (completed last step): its other channel half from LDS, fixed order, epilogue, stores
-    const int yf = i - 2;
-    if (yf >= r0 && yf < r1) {
-      const char* part = smem + 2 * R5_SLOT + ((K + 1) & 1) * R5_PART;
+    // residual operands of row i (finished two steps later)
+    load_res(i, rs1[K % 3], rs2[K % 3]);
+    // finish row i - 2 (completed last step): its other channel half from LDS, fixed order, epilogue, ST stores
+    {
+      const int yf = i - 2;
+      const bool fin = yf >= r0 && yf < r1;
+      const char* part = smem + R5_OFF_P + ((K + 1) & 1) * R5_PART;
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
         const int f = 2 * hh + m;
         const f32x4 other = *(const f32x4*)(part + (q * 4 + f) * 1024 + lane * 16);
         const f32x4 own = hh == 0 ? acc[SA][m] : acc[SA][2 + m];  // (a register select: acc is never indexed at run time)
         const f32x4 sum = hh == 0 ? own + other : other + own;
-        const bool ok = pix_ok(yf, m);
+        const bool ok = fin && pix_ok(yf, m);
         const uint32_t p = ok ? pidx(yf, m) : 0u;
         const int co = 16 * q + 4 * g;
         float v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float t = sum[e] + bb[e];
-          t = t * a.alpha1 + a.beta1 * rval(rs1[(K + 1) & 1][m], e);
-          if (has2) t = t * a.alpha2 + a.beta2 * rval(rs2[(K + 1) & 1][m], e);
+          t = t * a.alpha1 + a.beta1 * rval(rs1[(K + 1) % 3][m], e);
+          if (has2) t = t * a.alpha2 + a.beta2 * rval(rs2[(K + 1) % 3][m], e);
           v[e] = t;
         }
         if constexpr (F32) {
           const v4u32 o = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
           __builtin_amdgcn_raw_buffer_store_b128(o, ry, ok ? (p * a.ycs + a.yco + co) * 4u : BUF_OOB, 0, 0);
-          if (has_aux) {
-            const v2u32 x2 = {pk2(a.aux_scale * v[0], a.aux_scale * v[1]), pk2(a.aux_scale * v[2], a.aux_scale * v[3])};
-            __builtin_amdgcn_raw_buffer_store_b64(x2, rax, ok ? (p * a.auxcs + a.auxco + co) * 2u : BUF_OOB, 0, 0);
-          }
+          const v2u32 x2 = {pk2(a.aux_scale * v[0], a.aux_scale * v[1]), pk2(a.aux_scale * v[2], a.aux_scale * v[3])};
+          __builtin_amdgcn_raw_buffer_store_b64(x2, rax, ok ? (p * a.auxcs + a.auxco + co) * 2u : BUF_OOB, 0, 0);
         } else {
           const v2u32 o = {pk2(v[0], v[1]), pk2(v[2], v[3])};
           __builtin_amdgcn_raw_buffer_store_b64(o, ry, ok ? (p * a.ycs + a.yco + co) * 2u : BUF_OOB, 0, 0);
         }
       }
+      if constexpr (!F32) __builtin_amdgcn_raw_buffer_store_b32(0u, ry, BUF_OOB, 0, 0);  // (ST = 3: see above)
     }
 #pragma unroll
     for (int f = 0; f < 4; ++f) acc[SA][f] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    // the next row lands in the other slot (its previous row was last read in the previous step)
-    if (i + 1 <= r1 && i + 1 < a.h) dma_row(i + 1, (K + 1) & 1);
-    // ingest row i: kernel row ky adds to output row i + 1 - ky
+    // row i + 2 into the slot of row i - 1 (last read in the previous step)
+    dma_step(i + 2, (K + 2) % 3);
     // ingest row i.  Every MFMA is issued unconditionally: a target row outside the strip lands in an accumulator row
     // that is zeroed before its next use and never finished, and a fragment past the image width reads zeros
     if (i >= 0 && i < a.h && i <= r1) {
-      const char* xs = smem + (K & 1) * R5_SLOT + lb;
+      const char* xs = smem + (K % 3) * R5_SLOT + lb;
       bf16x8 B[2][4];
       auto ldB = [&](int grp, int buf) {
         const int kx = grp >> 1, cb = grp & 1;
@@ -219,7 +235,7 @@ __global__ __launch_bounds__(512, 1) void rdb5_kernel(R5Args a) {
     }
     // row i - 1 is complete: hand the partner the two fragments it finishes
     if (i - 1 >= r0 && i - 1 < r1) {
-      char* part = smem + 2 * R5_SLOT + (K & 1) * R5_PART;
+      char* part = smem + R5_OFF_P + (K & 1) * R5_PART;
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
         const int f = 2 * (1 - hh) + m;

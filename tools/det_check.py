@@ -51,6 +51,14 @@ def check(name, run, out, fill=True):
     res[name] = int(sum(int((o.view(torch.int16 if o.dtype == torch.bfloat16 else torch.int32) !=
                              outs[0].view(torch.int16 if o.dtype == torch.bfloat16 else torch.int32)).sum()) for o in outs[1:]))
     res[name + "_nan"] = int(torch.isnan(outs[0].float()).sum())
+    if res[name] and out.dim() == 4:  # where: (image, row, column, channel) of up to 12 differing elements, and the run
+        for k, o in enumerate(outs[1:], 1):
+            vi = (o.view(torch.int16 if o.dtype == torch.bfloat16 else torch.int32) !=
+                  outs[0].view(torch.int16 if o.dtype == torch.bfloat16 else torch.int32)).nonzero()
+            if len(vi):
+                res[name + f"_where{k}"] = vi[:12].tolist()
+                res[name + f"_rows{k}"] = sorted(set(int(r) for r in vi[:, 1].tolist()))[:40]
+                res[name + f"_chans{k}"] = sorted(set(int(c) for c in vi[:, 3].tolist()))[:64]
 
 
 dc, h = 128, 64
