@@ -44,6 +44,12 @@ class Epilogue(ctypes.Structure):
         super().__init__(*args, **kw)
 
 
+class StemDesc(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("x_cs", ctypes.c_int32), ("w0", c_void_p), ("w2", c_void_p), ("kpk2", ctypes.c_int32),
+                ("a0", c_void_p), ("z2", c_void_p), ("bn_part", c_void_p), ("slope", c_float), ("n", ctypes.c_int32),
+                ("h", ctypes.c_int32), ("w", ctypes.c_int32)]
+
+
 class Planes8(ctypes.Structure):
     _fields_ = [("p", c_void_p * 8), ("img_stride", ctypes.c_int64 * 8)]
 
@@ -172,6 +178,8 @@ SIGNATURES = {
     "climsr_linear_dgrad": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     "climsr_linear_wgrad": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     "climsr_d_head_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "climsr_d_stem_s2": (c_int, [c_void_p, c_void_p]),
+    "climsr_d_stem_s2_bn_parts": (c_int64, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
     "climsr_d_head_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int, c_void_p, c_void_p,
                                   c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "climsr_relativistic_bce": (c_int, [c_void_p, c_void_p, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -1,0 +1,291 @@
+// The discriminator's stem, features.0 (1 -> 64, 3x3, LeakyReLU) and features.2 (64 -> 64, 3x3 / stride 2, the
+// pre-BatchNorm output with the BatchNorm partial sums of its tiles) in ONE launch (rfb_esrgan.py:28-31).
+//
+// features.0's output is the largest tensor of the discriminator (B x 256^2 x 64 bf16 = 268 MB at B = 32) and holds 9
+// MACs per element of information: it is recomputed from the 1-channel input where features.2 needs it instead of
+// being written by one launch and read back by the next (the stride-2 conv reading it was bound by that read at
+// ~2.3 TB/s).  It is still written once (own pixels of each tile) when the caller keeps it for the backward.
+//
+// A workgroup (8 waves) walks 16 x 16 output tiles (all 64 output channels).  Per tile: the 35 x 35 input pixels go to
+// LDS; each wave gathers its im2col fragments of the 33 x 33 features.0 region once (tap k of pixel p in lane group
+// k / 8: 9 taps of a 32-deep K, the rest zero); then per 16-channel chunk c of features.0 one MFMA per 16 pixels
+// computes that chunk (A = W0 rows 16c .. 16c + 15), LeakyReLU, bf16, into an LDS image the stride-2 conv reads,
+// while the previous chunk's conv MFMAs run (two image buffers, one barrier per chunk).  features.2's weights
+// (4 chunks x 18 KB) stay in LDS for the launch.  The conv part is conv_fwd_s2_dma_kernel's (conv_dma.hip): wave w
+// owns output rows 2w, 2w + 1; a k block is a pair of taps x 16 channels; BatchNorm sums per 16 x 16 tile in the same
+// fixed order.  Image rows keep their 17 even columns before their 16 odd ones, so the 8 pixels 2 apart that a
+// stride-2 fragment read touches sit in consecutive slots (conflict-free ds_read_b128).
+#include "conv_ep.h"
+
+namespace {
+
+constexpr int ST_TP = 33;                              // features.0 region side per 16 x 16 output tile
+constexpr int ST_IN = 35;                              // input region side
+constexpr int ST_NF = (ST_TP * ST_TP + 15) / 16;       // 16-pixel im2col fragments of the region (69)
+constexpr int ST_FPW = (ST_NF + 7) / 8;                // per wave (9)
+constexpr int ST_WCH = 64 * 9 * 32;                    // features.2 weights of one 16-channel chunk: [co][tap][2 x 16 B]
+constexpr int ST_XB = ST_TP * ST_TP * 32;              // one 16-channel image of the region: [row][slot][2 x 16 B]
+constexpr int ST_OFF_X = 4 * ST_WCH;                   // 73,728
+constexpr int ST_OFF_IN = ST_OFF_X + 2 * ST_XB;        // 143,424
+constexpr int ST_OFF_FIN = ST_OFF_IN + 2464;           // 145,888: BatchNorm [wave][2][64] fp32
+constexpr int ST_LDS = ST_OFF_FIN + 8 * 2 * 64 * 4;    // 149,984
+constexpr int ST_RED = 64 * 17 * 4;                    // per wave: the channel-sum transpose (in image buffer 0)
+constexpr int ST_T8 = ST_TP * ST_TP * 16;              // im2col (in image buffer 1): tap 8 after taps 0..7
+static_assert(ST_T8 + ST_TP * ST_TP * 2 <= ST_XB, "im2col fits one image buffer");
+static_assert(8 * ST_RED <= ST_XB, "BatchNorm transpose fits one image buffer");
+static_assert(ST_LDS <= 160 * 1024, "stem LDS");
+
+struct StemArgs {
+  const uint16_t* x;
+  const float* w0;
+  const uint16_t* w2;
+  uint16_t* a0;
+  uint16_t* z2;
+  double* bn_part;
+  int x_cs, kpk2, n, h, w, oh, ow, tiles_x, tiles_y;
+  float slope;
+  uint32_t x_bytes, a0_bytes, z_bytes;
+};
+typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ int slot_of(int c) { return (c & 1) ? 17 + (c >> 1) : (c >> 1); }  // even columns first
+
+template <bool STATS, bool KEEP>
+__global__ __launch_bounds__(512, 1) void stem_s2_kernel(StemArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15, hh = g & 1;
+  const int ntile = a.tiles_x * a.tiles_y * a.n;
+  // features.2's weights into LDS once: chunk c, row co, tap t, half hf <- packed [co][c / 2][t][32] at (c & 1) * 16
+  for (int u = tid; u < 4 * 64 * 9 * 2; u += 512) {
+    const int hf = u & 1, t = (u >> 1) % 9, co = (u / 18) % 64, c = u / (18 * 64);
+    const uint4 v = *(const uint4*)(a.w2 + (long)co * a.kpk2 + (c >> 1) * 288 + t * 32 + (c & 1) * 16 + hf * 8);
+    *(uint4*)(smem + c * ST_WCH + ((co * 9 + t) * 2 + hf) * 16) = v;
+  }
+  // features.0's A fragments: rows 16 c + col, lane group g: taps 8 g .. 8 g + 7 (tap 8 alone in group 1), bf16 RNE
+  bf16x8 A0[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    bf16x8 v = {};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int t = 8 * g + e;
+      v[e] = t < 9 ? (__bf16)a.w0[(16 * c + col) * 9 + t] : (__bf16)0.f;
+    }
+    A0[c] = v;
+  }
+  const __amdgpu_buffer_rsrc_t xr = buf_rsrc(a.x, a.x_bytes);
+  const __amdgpu_buffer_rsrc_t ar = buf_rsrc(a.a0, KEEP ? a.a0_bytes : 0u);
+  const __amdgpu_buffer_rsrc_t zr = buf_rsrc(a.z2, a.z_bytes);
+  const uint16_t* in = (const uint16_t*)(smem + ST_OFF_IN);
+
+  for (int tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
+    const int tx = tile % a.tiles_x, ty = (tile / a.tiles_x) % a.tiles_y, nimg = tile / (a.tiles_x * a.tiles_y);
+    const int ox0 = 16 * tx, oy0 = 16 * ty, iy0 = 2 * oy0 - 1, ix0 = 2 * ox0 - 1;  // region origin (features.0 pixels)
+    // the 35 x 35 input pixels around the region (zeros outside the image); the previous tile's readers of this
+    // buffer are two barriers back
+    for (int u = tid; u < ST_IN * ST_IN; u += 512) {
+      const int r = u / ST_IN, c = u - r * ST_IN, iy = iy0 - 1 + r, ix = ix0 - 1 + c;
+      const bool ok = iy >= 0 && iy < a.h && ix >= 0 && ix < a.w;
+      const uint32_t off = ok ? (uint32_t)((((long)nimg * a.h + iy) * a.w + ix) * a.x_cs * 2) : BUF_OOB;
+      ((uint16_t*)(smem + ST_OFF_IN))[u] = (uint16_t)__builtin_amdgcn_raw_buffer_load_b32(xr, off, 0, 0);
+    }
+    lds_barrier();
+    // im2col of the region into image buffer 1 (free until chunk 1's features.0 is written, two barriers on): taps 0..7
+    // of pixel p as 16 B at 16 p, tap 8 as 2 B at ST_T8 + 2 p
+    {
+      char* ic = smem + ST_OFF_X + ST_XB;
+      for (int p = tid; p < ST_TP * ST_TP; p += 512) {
+        const int r = p / ST_TP, c = p - r * ST_TP;
+        const uint16_t* q = in + r * ST_IN + c;
+        uint4 v;
+        v.x = (uint32_t)q[0] | ((uint32_t)q[1] << 16);
+        v.y = (uint32_t)q[2] | ((uint32_t)q[ST_IN] << 16);
+        v.z = (uint32_t)q[ST_IN + 1] | ((uint32_t)q[ST_IN + 2] << 16);
+        v.w = (uint32_t)q[2 * ST_IN] | ((uint32_t)q[2 * ST_IN + 1] << 16);
+        *(uint4*)(ic + 16 * p) = v;
+        *(uint16_t*)(ic + ST_T8 + 2 * p) = q[2 * ST_IN + 2];
+      }
+    }
+    lds_barrier();
+    // this wave's im2col fragments j = wave + 8 i of the region (pixel p = 16 j + col): lane group 0 = taps 0..7,
+    // group 1 = tap 8 and zeros, groups 2 / 3 zeros (K = 9 of 32)
+    bf16x8 Bs[ST_FPW];
+    {
+      const char* ic = smem + ST_OFF_X + ST_XB;
+#pragma unroll
+      for (int i = 0; i < ST_FPW; ++i) {
+        const int p0 = 16 * (wave + 8 * i) + col, pv = p0 < ST_TP * ST_TP, p = pv ? p0 : 0;
+        const uint4 t07 = *(const uint4*)(ic + 16 * p);
+        const uint16_t t8 = *(const uint16_t*)(ic + ST_T8 + 2 * p);
+        const uint4 v = !pv || g >= 2 ? make_uint4(0, 0, 0, 0) : (g == 0 ? t07 : make_uint4((uint32_t)t8, 0, 0, 0));
+        Bs[i] = __builtin_bit_cast(bf16x8, v);
+      }
+    }
+    // where each of this wave's region pixels goes: its LDS image slot (bit 30 set: outside the image, the slot gets
+    // zeros) and, when kept, its byte offset in a0 (own pixels only; BUF_OOB otherwise), channel 0
+    uint32_t soff[ST_FPW], aoff[ST_FPW];
+#pragma unroll
+    for (int i = 0; i < ST_FPW; ++i) {
+      const int p0 = 16 * (wave + 8 * i) + col, pv = p0 < ST_TP * ST_TP, p = pv ? p0 : 0, r = p / ST_TP, cc = p - r * ST_TP;
+      const int iy = iy0 + r, ix = ix0 + cc;
+      const bool in_img = iy >= 0 && iy < a.h && ix >= 0 && ix < a.w;
+      soff[i] = pv ? (uint32_t)((r * ST_TP + slot_of(cc)) * 32 + g * 8) | (in_img ? 0u : 0x40000000u) : 0xFFFFFFFFu;
+      aoff[i] = KEEP && pv && in_img && r >= 1 && cc >= 1 ? (uint32_t)(((nimg * a.h + iy) * a.w + ix) * 64 + 4 * g) * 2u : BUF_OOB;
+    }
+    // features.0 chunk c (channels 16 c ..) of the region -> image buffer c & 1 (and the kept output), three MFMAs at a
+    // time
+    auto stem = [&](int c) {
+      char* xb = smem + ST_OFF_X + (c & 1) * ST_XB;
+#pragma unroll
+      for (int i0 = 0; i0 < ST_FPW; i0 += 3) {
+        f32x4 z[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) z[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A0[c], Bs[i0 + k], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const int i = i0 + k;
+          if (wave + 8 * i < ST_NF) {
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = fmaxf(z[k][e], z[k][e] * a.slope);  // LeakyReLU, 0 <= slope <= 1
+            const bf16x2 q0 = {(__bf16)v[0], (__bf16)v[1]}, q1 = {(__bf16)v[2], (__bf16)v[3]};
+            const bool zero = soff[i] & 0x40000000u;
+            const v2u32 pk = {zero ? 0u : __builtin_bit_cast(uint32_t, q0), zero ? 0u : __builtin_bit_cast(uint32_t, q1)};
+            if (soff[i] != 0xFFFFFFFFu) *(v2u32*)(xb + (soff[i] & 0x3FFFFFFFu)) = pk;
+            if constexpr (KEEP)
+              __builtin_amdgcn_raw_buffer_store_b64(pk, ar, aoff[i] == BUF_OOB ? BUF_OOB : aoff[i] + (uint32_t)(32 * c), 0, 0);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    stem(0);
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[m][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {  // (unrolled: the chunk picks registers A0[c])
+      lds_barrier();  // chunk c's image is complete; every wave is past its reads of the other buffer
+      const char* xb = smem + ST_OFF_X + (c & 1) * ST_XB;
+      const char* wb = smem + c * ST_WCH;
+      // k block kk: lane group g -> tap 2 kk + (g >> 1) (tap 9: tap 8 under zero weights), channels 8 hh ..
+      bf16x8 af[1][4], bq[1][2];
+      auto ld = [&](int kk, int s) {
+        const int tap = min(2 * kk + (g >> 1), 8), ky = tap / 3, kx = tap - ky * 3;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) af[s][t] = *(const bf16x8*)(wb + ((16 * t + col) * 9 + tap) * 32 + 16 * hh);
+        if (kk == 4 && g >= 2) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) af[s][t] = (bf16x8){};
+        }
+        const int sl = slot_of(2 * col + kx);
+#pragma unroll
+        for (int m = 0; m < 2; ++m) bq[s][m] = *(const bf16x8*)(xb + ((2 * (2 * wave + m) + ky) * ST_TP + sl) * 32 + 16 * hh);
+      };
+      
+#pragma unroll
+      for (int kk = 0; kk < 5; ++kk) {  // (fragments single-buffered: the SIMD's other wave covers their latency)
+        ld(kk, 0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][t], bq[0][m], acc[m][t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (c + 1 < 4) stem(c + 1);  // into the other buffer, read by chunk c - 1 (every wave is past the barrier above)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- epilogue straight from the accumulators: lane (col, g) holds channels 16 t + 4 g .. + 3 of output pixel
+    // (oy0 + 2 wave + m, ox0 + col)
+    const int ox = ox0 + col;
+    float ss[4][4] = {}, sq[4][4] = {};
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int oy = oy0 + 2 * wave + m;
+      const bool ok = oy < a.oh && ox < a.ow;
+      const long pix = ((long)nimg * a.oh + oy) * a.ow + ox;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bf16x2 p0 = {(__bf16)acc[m][t][0], (__bf16)acc[m][t][1]}, p1 = {(__bf16)acc[m][t][2], (__bf16)acc[m][t][3]};
+        const v2u32 pk = {__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1)};
+        __builtin_amdgcn_raw_buffer_store_b64(pk, zr, ok ? (uint32_t)((pix * 64 + 16 * t + 4 * g) * 2) : BUF_OOB, 0, 0);
+        if (STATS && ok) {
+          const float r[4] = {(float)p0[0], (float)p0[1], (float)p1[0], (float)p1[1]};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            ss[t][i] += r[i];
+            sq[t][i] = fmaf(r[i], r[i], sq[t][i]);
+          }
+        }
+      }
+    }
+    if constexpr (STATS) {
+      // per channel over the tile's 256 pixels (conv_fwd_s2_dma_kernel's order): each wave transposes its column sums
+      // through its own LDS corner in image buffer 0 (free: chunk 3 read buffer 1), lane l = channel l adds its 16
+      // columns in order; the 8 waves meet in LDS, fixed order, fp64 out
+      float* red = (float*)(smem + ST_OFF_X) + wave * (ST_RED / 4);
+      float* fin = (float*)(smem + ST_OFF_FIN);
+      float cs[2];
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) red[(16 * t + 4 * g + i) * 17 + col] = st ? sq[t][i] : ss[t][i];
+        float x = 0.f;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x += red[lane * 17 + k];
+        cs[st] = x;
+      }
+      fin[wave * 128 + lane] = cs[0];
+      fin[wave * 128 + 64 + lane] = cs[1];
+      lds_barrier();
+      if (tid < 128) {
+        const int st = tid >> 6, ch = tid & 63;
+        float x = 0.f;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) x += fin[w * 128 + st * 64 + ch];
+        a.bn_part[(long)tile * 2 * 64 + st * 64 + ch] = (double)x;
+      }
+    }
+    lds_barrier();  // buffer 0 / fin / the input region are rewritten by the next tile
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+}  // namespace
+
+extern "C" int climsr_d_stem_s2(const ClimsrStemDesc* d, void* stream) {
+  if (!d || !d->x || !d->w0 || !d->w2 || !d->z2 || d->n <= 0 || d->h <= 0 || d->w <= 0 || d->x_cs <= 0 || d->x_cs % 8 ||
+      d->kpk2 != 2 * 288 || !(d->slope >= 0.f && d->slope <= 1.f)) {
+    set_error("d_stem_s2: bad args");
+    return CLIMSR_EINVAL;
+  }
+  const long px = (long)d->n * d->h * d->w, opx = (long)d->n * ((d->h + 1) / 2) * ((d->w + 1) / 2);
+  if (px * d->x_cs * 2 >= (1L << 31) || px * 64 * 2 >= (1L << 31) || opx * 64 * 2 >= (1L << 31)) {
+    set_error("d_stem_s2: tensors over 2 GiB (32-bit buffer offsets)");
+    return CLIMSR_EINVAL;
+  }
+  StemArgs a{};
+  a.x = d->x; a.w0 = d->w0; a.w2 = d->w2; a.a0 = d->a0; a.z2 = d->z2; a.bn_part = d->bn_part;
+  a.x_cs = d->x_cs; a.kpk2 = d->kpk2; a.n = d->n; a.h = d->h; a.w = d->w;
+  a.oh = (d->h + 1) / 2; a.ow = (d->w + 1) / 2;
+  a.tiles_x = ceil_div(a.ow, 16); a.tiles_y = ceil_div(a.oh, 16);
+  a.slope = d->slope;
+  a.x_bytes = (uint32_t)(px * d->x_cs * 2); a.a0_bytes = (uint32_t)(px * 64 * 2); a.z_bytes = (uint32_t)(opx * 64 * 2);
+  void (*k)(StemArgs) = d->bn_part ? (d->a0 ? stem_s2_kernel<true, true> : stem_s2_kernel<true, false>)
+                                   : (d->a0 ? stem_s2_kernel<false, true> : stem_s2_kernel<false, false>);
+  if (int e = lds_opt_in((const void*)k, ST_LDS)) return e;
+  const int ntile = a.tiles_x * a.tiles_y * a.n;
+  const int grid = ntile < device_cus() ? ntile : device_cus();
+  hipLaunchKernelGGL(k, dim3(grid), dim3(512), ST_LDS, (hipStream_t)stream, a);
+  return check_launch("d_stem_s2");
+}
+
+extern "C" int64_t climsr_d_stem_s2_bn_parts(int32_t n, int32_t h, int32_t w) {
+  return (int64_t)n * ((((h + 1) / 2) + 15) / 16) * ((((w + 1) / 2) + 15) / 16);
+}

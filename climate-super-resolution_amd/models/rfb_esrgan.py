@@ -89,7 +89,24 @@ class _DEngine:
         a_prev, cs_prev, hh, ww = x8, cpad, h, w
         saved = []
         training = d.training
-        for conv, bn, plan in self.layers:
+        # features.0 + features.2 as one launch (csrc/stem.hip): features.0's 64-channel output is recomputed from the
+        # image where features.2 reads it and written only when the backward needs it
+        stem = None
+        (c0, bn0, p0), (c1, bn1, p1) = self.layers[0], self.layers[1]
+        if (cin == 1 and bn0 is None and bn1 is not None and p0.cout == 64 and p1.cin_real == 64 and p1.cout == 64 and p1.stride == 2
+                and p1.kpk == 576):
+            oh, ow = p1.out_hw(h, w)
+            a0 = _bf16((n, h, w, 64), dev) if keep else None
+            z = _bf16((n, oh, ow, 64), dev)
+            nparts = ops.d_stem_s2_bn_parts(n, h, w) if training else 0
+            part = self._scr("bnpart1", (max(nparts, 1) * 2 * 64,), torch.float64, dev) if nparts else None
+            ops.d_stem_s2(x8, cpad, c0.weight, p1, a0, z, part, n, h, w, slope=0.2)
+            saved.append(dict(a_in=x8, cs_in=cpad, h_in=h, w_in=w, z=None, a=a0, mean=None, rstd=None, oh=h, ow=w))
+            stem = (z, part, nparts, oh, ow)
+        for li, (conv, bn, plan) in enumerate(self.layers):
+            if stem is not None and li == 0:
+                a_prev, cs_prev = saved[0]["a"], 64  # (None when not kept: nothing reads it then)
+                continue
             oh, ow = plan.out_hw(hh, ww)
             c = plan.cout
             if bn is None:
@@ -97,13 +114,16 @@ class _DEngine:
                 plan.fwd(a_prev, cs_prev, 0, hh, ww, a, c, 0, n, act=ACT_LRELU, use_bias=False)
                 saved.append(dict(a_in=a_prev, cs_in=cs_prev, h_in=hh, w_in=ww, z=None, a=a, mean=None, rstd=None, oh=oh, ow=ow))
             else:
-                z = _bf16((n, oh, ow, c), dev)
                 a = _bf16((n, oh, ow, c), dev)
                 npix = n * oh * ow
-                # train mode: the conv epilogue emits the batch statistics' partial sums (no pass over z for them)
-                nparts = plan.bn_parts(cs_prev, hh, ww, n, c) if training else 0
-                part = self._scr(f"bnpart{len(saved)}", (max(nparts, 1) * 2 * c,), torch.float64, dev) if nparts else None
-                plan.fwd(a_prev, cs_prev, 0, hh, ww, z, c, 0, n, use_bias=False, bn_part=part)
+                if stem is not None and li == 1:  # z and its BatchNorm partials came from the stem launch
+                    z, part, nparts, _oh, _ow = stem
+                else:
+                    z = _bf16((n, oh, ow, c), dev)
+                    # train mode: the conv epilogue emits the batch statistics' partial sums (no pass over z for them)
+                    nparts = plan.bn_parts(cs_prev, hh, ww, n, c) if training else 0
+                    part = self._scr(f"bnpart{len(saved)}", (max(nparts, 1) * 2 * c,), torch.float64, dev) if nparts else None
+                    plan.fwd(a_prev, cs_prev, 0, hh, ww, z, c, 0, n, use_bias=False, bn_part=part)
                 if training:
                     mean, rstd = _f32((c,), dev), _f32((c,), dev)
                     if nparts:

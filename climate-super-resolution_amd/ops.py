@@ -684,6 +684,29 @@ def relativistic_bce(s_real, s_fake, n, t_rf, t_fr, loss=None, gscale=None, g_re
                                        _lib.stream_ptr()))
 
 
+def d_stem_s2(x, x_cs, w0, plan2, a0, z2, bn_part, n, h, w, slope=0.2):
+    """The RFB discriminator's features.0 (1 -> 64 + LeakyReLU, recomputed on chip) and features.2 (64 -> 64 / stride 2,
+    pre-BatchNorm z2 + the BatchNorm partial sums of its 16x16 tiles) in one launch (csrc/stem.hip,
+    rfb_esrgan.py:28-31); a0 (features.0's output for the backward) is written only when given."""
+    assert x.dtype == torch.bfloat16 and z2.dtype == torch.bfloat16 and w0.dtype == torch.float32 and w0.is_contiguous()
+    assert tuple(w0.shape) == (64, 1, 3, 3) and plan2.cin_real == 64 and plan2.cout == 64 and plan2.stride == 2 and plan2.kpk == 576
+    assert a0 is None or (a0.dtype == torch.bfloat16 and a0.numel() == n * h * w * 64)
+    oh, ow = (h + 1) // 2, (w + 1) // 2
+    assert z2.numel() == n * oh * ow * 64
+    d = _lib.StemDesc()
+    d.x, d.x_cs, d.w0, d.w2, d.kpk2 = ptr(x), x_cs, ptr(w0), ptr(plan2.wpk), plan2.kpk
+    d.a0, d.z2, d.bn_part = ptr(a0) if a0 is not None else None, ptr(z2), ptr(bn_part) if bn_part is not None else None
+    d.slope, d.n, d.h, d.w = slope, n, h, w
+    flops = 2 * n * h * w * 64 * 9 + 2 * n * oh * ow * 64 * 576
+    _run("stem_s2_kernel" if PROFILER is not None else "", flops,
+         lambda: check(_L().climsr_d_stem_s2(ctypes.byref(d), _lib.stream_ptr()), "d_stem_s2"), "features.0+2",
+         n * h * w * 2 + n * oh * ow * 128 + (n * h * w * 128 if a0 is not None else 0))
+
+
+def d_stem_s2_bn_parts(n, h, w):
+    return int(_L().climsr_d_stem_s2_bn_parts(n, h, w))
+
+
 def maxpool2(x, n, h, w, c, y):
     _launch("maxpool2", lambda: _L().climsr_maxpool2_bf16(ptr(x), n, h, w, c, ptr(y), _lib.stream_ptr()))
 

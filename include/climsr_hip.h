@@ -334,6 +334,28 @@ int climsr_linear_dgrad(const uint16_t* dy, const uint16_t* w, int n, int k, int
 /* dw[o][k] (+)= sum_n dy_t[o][n] x_t[k][n] (K = n_pad, multiple of 32; k % 64 == 0, o % 64 == 0). */
 int climsr_linear_wgrad(const uint16_t* dy_t, const uint16_t* x_t, int n_pad, int k, int o, float* dw, int accumulate,
                         void* stream);
+/* The RFB discriminator's stem in one launch (rfb_esrgan.py:28-31): features.0 (1 -> 64, 3x3, pad 1, LeakyReLU slope)
+ * recomputed where features.2 (64 -> 64, 3x3, stride 2, pad 1, no bias) needs it, z2 = features.2's pre-BatchNorm
+ * output (bf16 [n][h/2][w/2][64]) with the BatchNorm partial sums of each 16x16 output tile in bn_part ([tiles][2][64],
+ * climsr_d_stem_s2_bn_parts rows, the layout climsr_bn_forward_parts reads; NULL: none).  a0 (bf16 [n][h][w][64]) gets
+ * features.0's output for the backward when non-NULL.  x: bf16 NHWC with the image in channel 0 (channel stride x_cs);
+ * w0: features.0's fp32 OIHW weight [64][1][3][3]; w2: features.2's packed bf16 weight (climsr_pack_conv_weight,
+ * cc 32: kpk2 = 576).  Replaces the features.0 stencil + the stride-2 conv launch (climsr_conv2d_fwd x 2). */
+typedef struct ClimsrStemDesc {
+  const uint16_t* x;
+  int32_t x_cs;
+  const float* w0;
+  const uint16_t* w2;
+  int32_t kpk2;
+  uint16_t* a0;
+  uint16_t* z2;
+  double* bn_part;
+  float slope;
+  int32_t n, h, w;
+} ClimsrStemDesc;
+int climsr_d_stem_s2(const ClimsrStemDesc* d, void* stream);
+int64_t climsr_d_stem_s2_bn_parts(int32_t n, int32_t h, int32_t w);
+
 /* Discriminator head after fc.0 (+LeakyReLU) (h [n][o] fp32): s[n] = sigmoid(h.w2 + b2) (rfb_esrgan.py:59-60),
  * or h.w2 + b2 with sigmoid = 0 (plain discriminator's classification.1, discriminator.py:40). */
 int climsr_d_head_fwd(const float* h, const float* w2, const float* b2, int n, int o, int sigmoid, float* s, void* stream);

@@ -859,3 +859,44 @@ def test_rdb5_conv5_pullx_matches_fp64(n, h, w, mode, two):
         err = ((ga - 0.04 * want).abs() - (0.04 * want).abs() * 2.0 ** -8).max().item()
         assert err <= 1e-5 * 0.04 * want.abs().max().item(), f"pullx aux err {err:.3e}"
         assert torch.all(aux[..., :64].float() == 3.0), "pull-x aux wrote outside its slot"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h,w,keep", [(2, 64, 64, True), (3, 40, 34, True), (2, 64, 96, False), (1, 30, 18, True)])
+def test_d_stem_s2_matches_fp64(n, h, w, keep):
+    """The RFB discriminator's features.0 (1 -> 64, LeakyReLU 0.2) + features.2 (64 -> 64 / stride 2) in one launch
+    (csrc/stem.hip, rfb_esrgan.py:28-31) vs float64 on the same bf16 operands: a0 (kept output) within one bf16 rounding,
+    z2 within 8e-3 of its scale (bf16 store), the BatchNorm partial sums per channel vs the fp64 sums of the stored z2
+    (fp32 summation noise), bit-identical reruns; without `keep` nothing is written to a0."""
+    from climsr_amd import ops
+
+    g = torch.Generator().manual_seed(41)
+    x = bf(torch.rand((n, 1, h, w), generator=g) * 2 - 1)
+    w0 = ((torch.rand((64, 1, 3, 3), generator=g) * 2 - 1) / 3).to(DEV).contiguous()
+    p2, w2, _b = make_plan(64, 64, 3, stride=2, seed=42, bias=False)
+    x8 = to_nhwc(x, cs=8)
+    oh, ow = (h + 1) // 2, (w + 1) // 2
+    a0 = torch.full((n, h, w, 64), 5.0, dtype=torch.bfloat16, device=DEV) if keep else None
+    z2 = torch.empty((n, oh, ow, 64), dtype=torch.bfloat16, device=DEV)
+    nparts = ops.d_stem_s2_bn_parts(n, h, w)
+    part = torch.full((nparts * 2 * 64,), float("nan"), dtype=torch.float64, device=DEV)
+    ops.d_stem_s2(x8, 8, w0, p2, a0, z2, part, n, h, w)
+    torch.cuda.synchronize()
+    z_first, p_first = z2.clone(), part.clone()
+    ops.d_stem_s2(x8, 8, w0, p2, a0, z2, part, n, h, w)
+    torch.cuda.synchronize()
+    assert torch.equal(z_first, z2) and torch.equal(p_first, part), "rerun not bit-identical"
+    a_ref = F.leaky_relu(F.conv2d(x.double(), bf(w0.cpu()).double(), padding=1), 0.2)
+    if keep:
+        got_a = from_nhwc(a0, 64).cpu().double()
+        err = ((got_a - a_ref).abs() - a_ref.abs() * 2.0 ** -8).max().item()
+        assert err <= 1e-6 * a_ref.abs().max().item(), f"a0 err {err:.3e}"
+    z_ref = F.conv2d(bf(a_ref.float()).double(), bf(w2).double(), padding=1, stride=2)
+    got_z = from_nhwc(z2, 64).cpu().double()
+    err = (got_z - z_ref).abs().max().item()
+    assert err <= 8e-3 * z_ref.abs().max().item(), f"z2 err {err:.3e}"
+    pp = part.view(nparts, 2, 64).cpu()
+    s_ref = got_z.sum(dim=(0, 2, 3))
+    q_ref = (got_z ** 2).sum(dim=(0, 2, 3))
+    assert torch.allclose(pp[:, 0].sum(0), s_ref, rtol=1e-4, atol=1e-3 * (oh * ow * n) ** 0.5)
+    assert torch.allclose(pp[:, 1].sum(0), q_ref, rtol=1e-4, atol=1e-3)

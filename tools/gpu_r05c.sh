@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 T=${1:-r05c}
 D=$PWD/climate-super-resolution_amd/csrc/diag
 timeout -k 10 240 python -u tools/det_check.py new > gpurun_out/${T}_det.jsonl 2> gpurun_out/${T}_det.err || exit $?
-timeout -k 10 400 python -u -m pytest tests/test_gpu_conv.py -q --timeout 120 --timeout-method thread > gpurun_out/${T}_conv.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_conv.py tests/test_gpu_gan.py tests/test_gpu_bench_shapes.py -q --timeout 120 --timeout-method thread > gpurun_out/${T}_conv.log 2>&1
 for i in 1 2; do
   timeout -k 10 120 python -u tools/perf_diag.py new >> gpurun_out/${T}_diag.jsonl 2>> gpurun_out/${T}_diag.err || exit $?
   CLIMSR_HIP_LIB=$D/main/libclimsr_hip.so timeout -k 10 120 python -u tools/perf_diag.py main >> gpurun_out/${T}_diag.jsonl 2>> gpurun_out/${T}_diag.err || exit $?
