@@ -33,7 +33,7 @@ class Epilogue(ctypes.Structure):
                 ("aux_cstride", ctypes.c_int32), ("aux", c_void_p), ("aux_coff", ctypes.c_int32), ("aux_scale", c_float),
                 ("bn_part", c_void_p), ("bn_z", c_void_p), ("bn_z_cstride", ctypes.c_int32), ("bn_slope", c_float),
                 ("bn_mean", c_void_p), ("bn_rstd", c_void_p), ("bn_gamma", c_void_p), ("bn_beta", c_void_p),
-                ("ch_part", c_void_p)]
+                ("ch_part", c_void_p), ("pool2", ctypes.c_int32)]
 
     def __init__(self, *args, **kw):
         # plain residual adds unless a caller scales them (beta1 / beta2 are positional fields 13 / 14)
@@ -179,6 +179,7 @@ SIGNATURES = {
     "climsr_linear_wgrad": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     "climsr_d_head_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "climsr_d_stem_s2": (c_int, [c_void_p, c_void_p]),
+    "climsr_conv2d_fwd_pool_ok": (c_int, [c_void_p, c_void_p]),
     "climsr_d_stem_s2_bn_parts": (c_int64, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
     "climsr_d_head_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int, c_void_p, c_void_p,
                                   c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
@@ -224,12 +225,22 @@ def load() -> ctypes.CDLL:
         raise ClimsrError(f"libclimsr_hip.so not found at {LIB_PATH}: build it with `python -c 'import __graft_entry__ as g; "
                           f"g.build()'` (the product path has no CPU fallback)")
     lib = ctypes.CDLL(LIB_PATH)
+    # an A/B build named by CLIMSR_HIP_LIB (tools/perf_*.py) may predate later entry points: those stay unbound and
+    # fail when called; the in-tree library must export every one
+    ab = "CLIMSR_HIP_LIB" in os.environ
     for name, (res, args) in SIGNATURES.items():
+        if ab and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+def has(name: str) -> bool:
+    """Whether the loaded library exports name (always, for the in-tree build; see load())."""
+    return hasattr(load(), name)
 
 
 def check(rc: int, what: str) -> None:

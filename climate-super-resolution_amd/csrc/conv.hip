@@ -2472,6 +2472,29 @@ extern "C" int64_t climsr_conv2d_fwd_bn_parts(const ClimsrConvDesc* d, const Cli
   return (int64_t)ceil_div(d->out_w, TW) * ceil_div(d->out_h, 16) * d->n;
 }
 
+// the LDS-DMA conv's pooled epilogue (EP 11): its GEO-1 shapes (3x3 / stride 1 / 32-channel chunks, 64-channel
+// blocks, 32-row tiles) with bias + activation, bf16 out
+static bool pool_dma_ok(const ClimsrConvDesc* d, const FwdArgs& a, const FwdGeom& g, int ncob) {
+  return d->ks == 3 && d->stride == 1 && d->pad == 1 && d->up == 1 && d->cc == 32 && d->in_c % 32 == 0 && g.kcpad == 288 &&
+         g.nchunk * 32 == d->in_c && d->out_c % 64 == 0 && ncob * 64 == d->out_c && d->in_coff % 8 == 0 && d->in_cstride % 8 == 0 &&
+         ((d->out_cstride | d->out_coff) & 7) == 0 && a.bias != nullptr && (a.act == 1 || a.act == 2) &&
+         (d->out_h % DMA_TH == 0 || d->out_h >= 3 * DMA_TH) && d->out_w % 2 == 0 &&
+         (long)d->n * d->in_h * d->in_w * d->in_cstride * 2 < (1L << 31) && (long)d->out_c * g.kpk * 2 < (1L << 31);
+}
+
+extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, const uint16_t* wpk, const float* bias,
+                                 const ClimsrEpilogue* ep, void* y, void* stream);
+
+extern "C" int climsr_conv2d_fwd_pool_ok(const ClimsrConvDesc* d, const ClimsrEpilogue* ep) {
+  if (!d || !ep || !ep->pool2) return 0;
+  static uint16_t dummy[8];
+  static float fdummy[64];
+  g_dry = true;
+  const int rc = climsr_conv2d_fwd(d, dummy, dummy, fdummy, ep, dummy, nullptr);
+  g_dry = false;
+  return rc == CLIMSR_OK ? 1 : 0;
+}
+
 extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, const uint16_t* wpk, const float* bias,
                                  const ClimsrEpilogue* ep, void* y, void* stream) {
   if (!d || !x || !wpk || !ep || !y) {
@@ -2515,6 +2538,11 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
       return CLIMSR_EINVAL;
     }
   }
+  if (ep->pool2 && (ep->out_mode != 0 || ep->act < 0 || ep->act > 2 || ep->res1 || ep->res2 || ep->aux || ep->bn_part || ep->bn_z ||
+                    ep->ch_part || ep->down2 || ((d->out_h | d->out_w) & 1))) {
+    set_error("conv2d_fwd: pool2 takes bf16 out, bias / activation only, even output size");
+    return CLIMSR_EINVAL;
+  }
   FwdGeom g;
   // 16x16 output tiles (64 px per wave) for the 64-channel layers; 8x16 otherwise
   const int mw = (d->out_h >= 12 && fwd_nt(d->out_c) == 4) ? 4 : 2;
@@ -2546,6 +2574,13 @@ extern "C" int climsr_conv2d_fwd(const ClimsrConvDesc* d, const uint16_t* x, con
   int rows = climsr_conv_packed_rows(d->out_c);
   int ncob = rows / (g.nt * 16);
   hipStream_t s = (hipStream_t)stream;
+  if (ep->pool2) {  // conv + 2x2 max pool: the register-resident 64 -> 64 conv, or the LDS-DMA conv (EP 11)
+    const int rc = conv_wr_launch(d, ep, x, wpk, g.kpk, bias, y, s, g_dry, g_dry_name, (int)sizeof(g_dry_name));
+    if (rc != -1) return rc;
+    if (pool_dma_ok(d, a, g, ncob)) return launch_fwd_dma<11>(a, ncob, s);
+    set_error("conv2d_fwd: no conv + max-pool kernel for this shape (climsr_conv2d_fwd_pool_ok)");
+    return CLIMSR_EINVAL;
+  }
   if (ep->bn_part && !(ep->bn_z ? bn_bwd_parts_ok(d, ep, a, g) : bn_parts_ok(d, a, g))) {
     set_error("conv2d_fwd: BatchNorm partials only for the 16x16-tile bf16 paths (climsr_conv2d_fwd_bn_parts)");
     return CLIMSR_EINVAL;

@@ -114,13 +114,16 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool BN = EP == 9 || EP == 10;
   // epilogues with a fixed store count per lane (dma_store_half), so the wait for the next item's chunk 0 skips them
-  constexpr bool CNT = EP == 1 || EP == 2 || EP == 3 || EP == 6 || EP == 7 || EP == 8;
+  constexpr bool CNT = EP == 1 || EP == 2 || EP == 3 || EP == 6 || EP == 7 || EP == 8 || EP == 11;
   // EP 3 / 6 / 8 store straight from the accumulators (16 stores per lane and item): no LDS staging, no barrier --
   // VGG 256 ch @64^2 295 -> 277 us, 512 ch @32^2 263 -> 249 us against the staged form (tools/perf_diag.py, r04dd).
   // (EP 9 the same way, with its BatchNorm sums xor-shuffled over the pixel columns, measured 9 % slower in the GAN
   // step, r04h: it keeps the staged tile)
-  constexpr bool DIRECT = EP == 3 || EP == 6 || EP == 8;
-  constexpr int NST_ITEM = DIRECT ? 16 : 2 * DmaEp<CNT ? EP : 8>::NSTORE;
+  // EP 11: EP 3 followed by the 2x2 max pool of the activated output (VGG19's conv2_2 / conv3_4 / conv4_4 + MaxPool2d,
+  // perceptual.py:16): a wave's 4 rows pool to 2 in registers, column pairs across lanes col / col ^ 1, even lanes store
+  constexpr bool POOL = EP == 11;
+  constexpr bool DIRECT = EP == 3 || EP == 6 || EP == 8 || POOL;
+  constexpr int NST_ITEM = POOL ? 8 : DIRECT ? 16 : 2 * DmaEp<CNT ? EP : 8>::NSTORE;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
   const int wvu = __builtin_amdgcn_readfirstlane(wave);
   const int ntile = a.tiles_x * a.tiles_y * a.n, ncob = (a.out_c + 63) / 64;  // = the host's packed-row blocks
@@ -320,11 +323,12 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
     } else if (DIRECT) {
       // lane (col, g) holds channels co0 + 16 t + 4 g .. + 3 of pixel (oy0 + 4 wave + m, ox0 + col): bias / activation,
       // bf16, one 8 B store per (m, t) -- 16 per lane per item, issued unconditionally (out-of-range offsets drop)
-      const __amdgpu_buffer_rsrc_t ry = buf_rsrc(a.y, (uint32_t)((long)a.n * a.out_h * a.out_w * a.out_cs * 2));
+      const long ypx = POOL ? (long)a.n * (a.out_h >> 1) * (a.out_w >> 1) : (long)a.n * a.out_h * a.out_w;
+      const __amdgpu_buffer_rsrc_t ry = buf_rsrc(a.y, (uint32_t)(ypx * a.out_cs * 2));
       float bb[4][4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        const float4 b4 = EP == 3 ? *(const float4*)(a.bias + co0 + 16 * t + 4 * g) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 b4 = (EP == 3 || POOL) ? *(const float4*)(a.bias + co0 + 16 * t + 4 * g) : make_float4(0.f, 0.f, 0.f, 0.f);
         bb[t][0] = b4.x; bb[t][1] = b4.y; bb[t][2] = b4.z; bb[t][3] = b4.w;
       }
       const int ox = ox0 + col, act = EP == 8 ? 0 : a.act;
@@ -332,6 +336,33 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
       // act compiled to a branch tree around each of the 64 values (~470 branch instructions per kernel)
       auto store_all = [&](auto actc) {
         constexpr int ACT = decltype(actc)::value;
+        if constexpr (POOL) {
+          // pooled output pixel (oy0 / 2 + 2 wave + mp, (ox0 + col) / 2), stored by the even-column lanes (8 per lane)
+          const int ph = a.out_h >> 1, pw = a.out_w >> 1, px = (ox0 + col) >> 1;
+#pragma unroll
+          for (int mp = 0; mp < 2; ++mp) {
+            const int py = (oy0 >> 1) + 2 * wave + mp;
+            const bool ok = (col & 1) == 0 && py < ph && px < pw;
+            const long pix = ((long)nimg * ph + py) * pw + px;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              float v[4];
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const float r0 = act_apply(acc[2 * mp][t][i] + bb[t][i], ACT, a.slope);
+                const float r1 = act_apply(acc[2 * mp + 1][t][i] + bb[t][i], ACT, a.slope);
+                const float rm = fmaxf(r0, r1);
+                v[i] = fmaxf(rm, __shfl_xor(rm, 1));
+              }
+              const bf16x2 p0 = {(__bf16)v[0], (__bf16)v[1]}, p1 = {(__bf16)v[2], (__bf16)v[3]};
+              typedef uint32_t v2u32_t __attribute__((ext_vector_type(2)));
+              const v2u32_t pk = {__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1)};
+              const uint32_t off = ok ? (uint32_t)((pix * a.out_cs + a.out_co + co0 + 16 * t + 4 * g) * 2) : BUF_OOB;
+              __builtin_amdgcn_raw_buffer_store_b64(pk, ry, off, 0, 0);
+            }
+          }
+          return;
+        }
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
           const int oy = oy0 + wave * 4 + m;
@@ -368,7 +399,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
         if (a.n < 0)
 #endif
         {
-          if constexpr (CNT) dma_store_half<CNT ? EP : 8>(a, eb, EPH, lane, nimg, oy0 + wave * 4, ox0, co0 + 32 * h);
+          if constexpr (CNT) dma_store_half<(CNT && !POOL) ? EP : 8>(a, eb, EPH, lane, nimg, oy0 + wave * 4, ox0, co0 + 32 * h);
           else store_tile_lds<RF, 64, 32, 64, EP>(a, eb, EPH, lane, nimg, oy0 + wave * 4, ox0, co0 + 32 * h);
         }
       }
@@ -386,7 +417,7 @@ int fwd_dma_launch(int ep, const FwdArgs& a, int ncob, hipStream_t s) {
 #define DMA_EP(E) \
   case E: k = rf ? conv_fwd_dma_kernel<E, true> : conv_fwd_dma_kernel<E, false>; break;
   switch (ep) {
-    DMA_EP(0) DMA_EP(3) DMA_EP(4) DMA_EP(6) DMA_EP(7) DMA_EP(8) DMA_EP(9) DMA_EP(10)
+    DMA_EP(0) DMA_EP(3) DMA_EP(4) DMA_EP(6) DMA_EP(7) DMA_EP(8) DMA_EP(9) DMA_EP(10) DMA_EP(11)
     default: set_error("conv2d_fwd: no LDS-DMA kernel for epilogue %d", ep); return CLIMSR_EINVAL;
   }
 #undef DMA_EP

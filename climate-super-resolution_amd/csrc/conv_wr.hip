@@ -59,7 +59,8 @@ template <int EP, int ACT>
 __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // vector-memory operations of one epilogue (loads + stores), fixed per lane
-  constexpr int NEPI = EP == 0 ? 16 : (EP == 3 || EP == 4 ? 17 : 32);
+  // EP 5: EP 0 followed by the 2x2 max pool (VGG19 conv1_2 + MaxPool2d, perceptual.py:16): 8 stores a lane
+  constexpr int NEPI = EP == 0 ? 16 : (EP == 5 ? 8 : (EP == 3 || EP == 4 ? 17 : 32));
   constexpr bool SUMS = EP == 3 || EP == 4;  // per-tile channel sums (EP 3: fp32 out, EP 4: bf16 out)
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, col = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -183,6 +184,40 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
     int nimg, oy0, ox0;
     decode(T, nimg, oy0, ox0);
     const int ox = ox0 + col;
+    if constexpr (EP == 5) {
+      // pooled pixel (oy0 / 2 + mp, ox / 2): rows m = 2 mp, 2 mp + 1 in registers, columns col / col ^ 1 across lanes;
+      // the even-column lanes store
+      const int ph = a.out_h >> 1, pw = a.out_w >> 1, px = ox >> 1;
+#pragma unroll
+      for (int mp = 0; mp < 2; ++mp) {
+        const int py = (oy0 >> 1) + mp;
+        const bool ok = (col & 1) == 0 && py < ph && px < pw;
+        const uint32_t po = ok ? (uint32_t)(((((long)nimg * ph + py) * pw + px) * a.out_cs + a.out_co + 4 * g) * 2) : BUF_OOB;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          float v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float x0 = acc[2 * mp][t][i] + bias[t][i], x1 = acc[2 * mp + 1][t][i] + bias[t][i];
+            if constexpr (ACT == 1) {
+              x0 = fmaxf(x0, x0 * a.slope);
+              x1 = fmaxf(x1, x1 * a.slope);
+            } else if constexpr (ACT == 2) {
+              x0 = x0 > 0.f ? x0 : 0.f;
+              x1 = x1 > 0.f ? x1 : 0.f;
+            }
+            const float rm = fmaxf(x0, x1);
+            v[i] = fmaxf(rm, __shfl_xor(rm, 1));
+          }
+          const bf16x2 p0 = {(__bf16)v[0], (__bf16)v[1]}, p1 = {(__bf16)v[2], (__bf16)v[3]};
+          const v2u32 pk = {__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1)};
+          __builtin_amdgcn_raw_buffer_store_b64(pk, yr, po == BUF_OOB ? BUF_OOB : po + (uint32_t)(t * 32), 0, 0);
+        }
+      }
+      if (Tn >= a.ntiles) break;
+      T = Tn;
+      continue;
+    }
     uint32_t off[4];
     uint2 rv[4][4];
 #pragma unroll
@@ -271,12 +306,12 @@ namespace climsr {
 int conv_wr_ep(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const float* bias) {
   const bool res = ep->res1 != nullptr;
   int epk = -1;
-  if (ep->out_mode == 0 && !res && ep->act >= 0 && ep->act <= 2) epk = ep->ch_part ? 4 : 0;
+  if (ep->out_mode == 0 && !res && ep->act >= 0 && ep->act <= 2) epk = ep->pool2 ? 5 : (ep->ch_part ? 4 : 0);
   else if (ep->out_mode == 0 && res && ep->act == 0 && !(ep->res_f32 & 1)) epk = 1;
   else if (ep->out_mode == 0 && res && (ep->act == 3 || ep->act == 4) && !bias && !(ep->res_f32 & 1)) epk = 2;
   else if (ep->out_mode == 1 && !res && ep->act >= 0 && ep->act <= 2) epk = 3;
   const long opx = (long)d->n * d->out_h * d->out_w;
-  if (epk < 0 || (ep->ch_part && epk != 3 && epk != 4) || (ep->act == 1 && !(ep->slope >= 0.f && ep->slope <= 1.f)) || d->in_c != 64 || d->out_c != 64 || d->cc != 64 || d->ks != 3 || d->stride != 1 ||
+  if (epk < 0 || (ep->ch_part && epk != 3 && epk != 4) || (ep->pool2 && (epk != 5 || ep->ch_part || (d->out_h | d->out_w) & 1)) || (ep->act == 1 && !(ep->slope >= 0.f && ep->slope <= 1.f)) || d->in_c != 64 || d->out_c != 64 || d->cc != 64 || d->ks != 3 || d->stride != 1 ||
       d->pad != 1 || (d->up != 1 && d->up != 2) || d->out_h != d->in_h * d->up || d->out_w != d->in_w * d->up ||
       d->in_cstride % 8 || d->in_coff % 8 || (d->out_cstride | d->out_coff) & 3 || ep->down2 || ep->res2 || ep->aux ||
       ep->bn_part || (res && ((ep->res1_cstride | ep->res1_coff) & 3)) ||
@@ -317,17 +352,18 @@ int conv_wr_launch(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const uint
   a.tiles_x = ceil_div(d->out_w, WR_TC); a.tiles_y = ceil_div(d->out_h, WR_TR);
   a.ntiles = a.tiles_x * a.tiles_y * d->n;
   a.x_bytes = (uint32_t)((long)d->n * d->in_h * d->in_w * d->in_cstride * 2);
-  a.y_bytes = (uint32_t)(opx * d->out_cstride * (epk == 3 ? 4 : 2));
+  a.y_bytes = (uint32_t)((epk == 5 ? opx / 4 : opx) * d->out_cstride * (epk == 3 ? 4 : 2));
   a.r1_bytes = res ? (uint32_t)(opx * ep->res1_cstride * 2) : 0u;
   const int ncu = device_cus();
   const int grid = std::min(ceil_div(a.ntiles, 4), ncu);
   // [epilogue][activation] (EP 1: no activation; EP 2: 3 / 4)
-  static void (*const kt[5][5])(WrArgs) = {
+  static void (*const kt[6][5])(WrArgs) = {
       {conv_wr_kernel<0, 0>, conv_wr_kernel<0, 1>, conv_wr_kernel<0, 2>, nullptr, nullptr},
       {conv_wr_kernel<1, 0>, nullptr, nullptr, nullptr, nullptr},
       {nullptr, nullptr, nullptr, conv_wr_kernel<2, 3>, conv_wr_kernel<2, 4>},
       {conv_wr_kernel<3, 0>, conv_wr_kernel<3, 1>, conv_wr_kernel<3, 2>, nullptr, nullptr},
-      {conv_wr_kernel<4, 0>, conv_wr_kernel<4, 1>, conv_wr_kernel<4, 2>, nullptr, nullptr}};
+      {conv_wr_kernel<4, 0>, conv_wr_kernel<4, 1>, conv_wr_kernel<4, 2>, nullptr, nullptr},
+      {conv_wr_kernel<5, 0>, conv_wr_kernel<5, 1>, conv_wr_kernel<5, 2>, nullptr, nullptr}};
   void (*k)(WrArgs) = (ep->act >= 0 && ep->act < 5) ? kt[epk][ep->act] : nullptr;
   if (!k) {
     set_error("conv2d_fwd (wr): epilogue %d with activation %d", epk, ep->act);

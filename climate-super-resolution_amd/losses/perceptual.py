@@ -72,8 +72,15 @@ class PerceptualLoss(nn.Module):
         """x3: NHWC bf16 [n,h,w,8] with channels 0..2 = the image.  Returns conv5_4 features (bf16)."""
         a, cs = x3, 8
         for p, relu, pool in self._plans:
+            act = ACT_RELU if relu else ACT_NONE
+            if pool and p.pool_ok(cs, h, w, n, p.cout, act):  # conv + ReLU + 2x2 max pool in one kernel
+                h, w = h // 2, w // 2
+                y = torch.empty((n, h, w, p.cout), dtype=torch.bfloat16, device=x3.device)
+                p.fwd(a, cs, 0, 2 * h, 2 * w, y, p.cout, 0, n, act=act, out_mode=OUT_BF16, pool2=True)
+                a, cs = y, p.cout
+                continue
             y = torch.empty((n, h, w, p.cout), dtype=torch.bfloat16, device=x3.device)
-            p.fwd(a, cs, 0, h, w, y, p.cout, 0, n, act=ACT_RELU if relu else ACT_NONE, out_mode=OUT_BF16)
+            p.fwd(a, cs, 0, h, w, y, p.cout, 0, n, act=act, out_mode=OUT_BF16)
             a, cs = y, p.cout
             if pool:
                 h2, w2 = h // 2, w // 2

@@ -128,12 +128,13 @@ class ConvPlan:
             res2: Optional[torch.Tensor] = None, alpha2: float = 1.0, res2_cs: int = 0, res2_co: int = 0,
             out_mode: int = OUT_BF16, beta1: float = 1.0, beta2: float = 1.0, aux: Optional[torch.Tensor] = None,
             aux_cs: int = 0, aux_co: int = 0, aux_scale: float = 1.0, bn_part: Optional[torch.Tensor] = None,
-            ch_part: Optional[torch.Tensor] = None) -> None:
+            ch_part: Optional[torch.Tensor] = None, pool2: bool = False) -> None:
         """y = epilogue(conv(x)); residuals res1/res2 may be bf16 or fp32 tensors (dtype decides), aux = optional
         second bf16 output aux_scale * y; bn_part (fp64, bn_parts() rows x 2 x cout) = BatchNorm partial sums of y
-        for bn_forward_parts; ch_part (fp32, ch_parts() rows x cout) = per-tile channel sums of y (fp32 output)."""
+        for bn_forward_parts; ch_part (fp32, ch_parts() rows x cout) = per-tile channel sums of y (fp32 output);
+        pool2: y is the 2x2 max pool of the activated output (half the height and width; pool_ok())."""
         oh, ow = self.out_hw(in_h, in_w, up)
-        if (self.cin_real == 1 and self.ks in (3, 5) and self.stride == 1 and self.pad == self.ks // 2 and up == 1
+        if (not pool2 and self.cin_real == 1 and self.ks in (3, 5) and self.stride == 1 and self.pad == self.ks // 2 and up == 1
                 and self.cout in (32, 64) and out_mode == OUT_BF16 and y.dtype == torch.bfloat16 and res1 is None and res2 is None
                 and aux is None and act in (ACT_NONE, ACT_LRELU, ACT_RELU) and (y_cs | y_co) % 8 == 0):
             # one input channel: a 1 -> C stencil (climsr_conv_single_input), not a GEMM with K padded 9 -> 96
@@ -150,16 +151,23 @@ class ConvPlan:
         rf = (1 if res1 is not None and res1.dtype == torch.float32 else 0) | \
              (2 if res2 is not None and res2.dtype == torch.float32 else 0)
         ep = Epilogue(act, slope, alpha1, ptr(res1), res1_cs, res1_co, alpha2, ptr(res2), res2_cs, res2_co, out_mode, 0,
-                      rf, beta1, beta2, aux_cs, ptr(aux), aux_co, aux_scale, ptr(bn_part), ch_part=ptr(ch_part))
+                      rf, beta1, beta2, aux_cs, ptr(aux), aux_co, aux_scale, ptr(bn_part), ch_part=ptr(ch_part), pool2=int(pool2))
         b = ptr(self.bias) if (use_bias and self.bias is not None) else None
         flops = 2 * self.cin_real * self.cout * self.ks * self.ks * n * oh * ow
-        opx = n * oh * ow
+        opx = n * oh * ow // (4 if pool2 else 1)
         nbytes = (n * in_h * in_w * self.cin_real * 2 + self.rows * self.kpk * 2 +
                   opx * self.cout * (y.element_size() * (2 if out_mode == OUT_F32_ADD else 1) + _esize(res1) + _esize(res2) +
                                      _esize(aux)))
         _run(_kname(d, b, ep), flops, lambda: check(
             _lib.load().climsr_conv2d_fwd(ctypes.byref(d), ptr(x), ptr(self.wpk), b, ctypes.byref(ep), ptr(y), _lib.stream_ptr()),
             f"conv fwd {self.name}"), "fwd " + self.name, nbytes)
+
+    def pool_ok(self, x_cs: int, in_h: int, in_w: int, n: int, y_cs: int, act: int = ACT_RELU) -> bool:
+        """Whether fwd(..., act=act, pool2=True) has a fused conv + 2x2 max-pool kernel (climsr_conv2d_fwd_pool_ok)."""
+        oh, ow = self.out_hw(in_h, in_w)
+        d = ConvDesc(n, in_h, in_w, self.cin_k, x_cs, 0, 1, self.ks, self.stride, self.pad, oh, ow, self.cout, y_cs, 0, self.cc)
+        ep = Epilogue(act, 0.2, 1.0, None, 0, 0, 1.0, None, 0, 0, OUT_BF16, 0, 0, 1.0, 1.0, 0, None, 0, 1.0, None, pool2=1)
+        return bool(_lib.load().climsr_conv2d_fwd_pool_ok(ctypes.byref(d), ctypes.byref(ep)))
 
     def bn_parts(self, x_cs: int, in_h: int, in_w: int, n: int, y_cs: int) -> int:
         """Rows of BatchNorm partials fwd(..., use_bias=False, bn_part=...) writes (plain bf16 output), 0 if its kernel

@@ -90,11 +90,19 @@ typedef struct ClimsrEpilogue {
      channel sums of the output values before any bf16 rounding, ch_part[tile][out_c] fp32, tiles of one image
      contiguous -- the global average pool of RCAN's channel attention (rcan.py:50-69) without re-reading the output; finish with climsr_channel_attention_parts */
   float* ch_part;
+  /* 1: a 2x2 / stride-2 max pool of the (biased, activated) output is what gets stored: out[y/2][x/2] of the
+     (out_h/2) x (out_w/2) image (even out_h / out_w; bf16 out, no residual / aux / BatchNorm / channel sums) -- VGG19's
+     conv + ReLU + MaxPool2d (perceptual.py:16) without the full-size activation.  climsr_conv2d_fwd_pool_ok tells which
+     convs have such a kernel. */
+  int32_t pool2;
 } ClimsrEpilogue;
 
 /* rows (tiles) of ClimsrEpilogue.ch_part for this conv and epilogue, 0 when its kernel cannot emit them; the tiles of
  * one image are *tiles_per_image consecutive rows */
 int64_t climsr_conv2d_fwd_ch_parts(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, int32_t* tiles_per_image);
+/* 1 when climsr_conv2d_fwd has a kernel for this conv with ep->pool2 = 1 (the 64 -> 64 register-resident conv, or the
+ * LDS-DMA 3x3 conv with bias + activation), else 0 (store the full output and pool it with climsr_maxpool2_bf16). */
+int climsr_conv2d_fwd_pool_ok(const ClimsrConvDesc* d, const ClimsrEpilogue* ep);
 
 const char* climsr_last_error(void);
 int climsr_version(void);

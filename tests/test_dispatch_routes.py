@@ -90,6 +90,21 @@ def test_vgg19_routes(routes, cin, cout, hw, want):
     assert last(routes) == want
 
 
+@pytest.mark.parametrize("cin,cout,hw,want", [
+    (64, 64, 256, "conv_wr_kernel<5, 2>"),              # conv1_2 + pool1
+    (128, 128, 128, "conv_fwd_dma_kernel<11, false>"),  # conv2_2 + pool2
+    (256, 256, 64, "conv_fwd_dma_kernel<11, false>"),   # conv3_4 + pool3
+    (512, 512, 32, "conv_fwd_dma_kernel<11, false>"),   # conv4_4 + pool4
+])
+def test_vgg19_pooled_routes(routes, cin, cout, hw, want):
+    """The VGG19 convs followed by ReLU + 2x2 max pool take the fused pooled epilogue (losses/perceptual.py)."""
+    p = plan(cin, cout)
+    assert p.pool_ok(p.cin, hw, hw, 2 * N, cout)
+    p.fwd(bf(), p.cin, 0, hw, hw, bf(), cout, 0, 2 * N, act=ACT_RELU, pool2=True)
+    assert last(routes) == want
+    assert not p.pool_ok(p.cin, hw + 1, hw + 1, 2 * N, cout)  # odd sizes: no fused pool
+
+
 @pytest.mark.parametrize("stride,cin,cout,hw,want", [
     (2, 64, 64, 256, "conv_fwd_s2_dma_kernel<true>"),
     (2, 128, 128, 128, "conv_fwd_s2_dma_kernel<true>"),

@@ -900,3 +900,30 @@ def test_d_stem_s2_matches_fp64(n, h, w, keep):
     q_ref = (got_z ** 2).sum(dim=(0, 2, 3))
     assert torch.allclose(pp[:, 0].sum(0), s_ref, rtol=1e-4, atol=1e-3 * (oh * ow * n) ** 0.5)
     assert torch.allclose(pp[:, 1].sum(0), q_ref, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,n,h,w", [(64, 64, 2, 40, 36), (64, 64, 1, 18, 100), (128, 128, 2, 32, 48), (256, 256, 1, 96, 34),
+                                            (128, 64, 2, 64, 16), (512, 512, 1, 32, 32)])
+def test_conv_relu_maxpool_fused(cin, cout, n, h, w):
+    """conv + bias + ReLU + 2x2 max pool in one kernel (the VGG19 block ends, losses/perceptual.py; the register-resident
+    64 -> 64 conv's EP 5 or the LDS-DMA conv's EP 11) vs max_pool2d(relu(conv)) in fp64 on the same bf16 operands."""
+    from climsr_amd import ops
+
+    p, wt, b = make_plan(cin, cout, 3, seed=21)
+    g = torch.Generator().manual_seed(22)
+    x = bf(torch.rand((n, cin, h, w), generator=g) * 2 - 1)
+    assert p.pool_ok(cin, h, w, n, cout)
+    y = torch.full((n, h // 2, w // 2, cout), 7.0, dtype=torch.bfloat16, device=DEV)
+    names = []
+    ops.PROFILER = lambda name, flops, fn, tag="", nbytes=0: (names.append(name), fn())
+    try:
+        p.fwd(to_nhwc(x), cin, 0, h, w, y, cout, 0, n, act=ACT_RELU, pool2=True)
+    finally:
+        ops.PROFILER = None
+    torch.cuda.synchronize()
+    assert names and ("<5, 2>" in names[-1] or "<11, false>" in names[-1]), names
+    want = F.max_pool2d(F.relu(F.conv2d(x.double(), bf(wt).double(), b.double(), padding=1)), 2)
+    got = from_nhwc(y, cout).double().cpu()
+    err = float((got - want).abs().max())
+    assert err <= 2 ** -7 * float(want.abs().max()) + 1e-6, f"err {err:.3e} vs {float(want.abs().max()):.3e}"
