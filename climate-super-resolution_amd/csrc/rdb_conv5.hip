@@ -34,6 +34,27 @@ constexpr int R5_OFF_DUMMY = R5_OFF_P + 2 * R5_PART;  // one KB the padding DMA 
 constexpr int R5_LDS = R5_OFF_DUMMY + 1024;        // 92,160 B
 constexpr int R5_K = 3;                            // DMA pieces per wave and row (19 real + 5 padding over 8 waves)
 
+#ifdef CLIMSR_R5_STAMP
+// Timing diagnostic (tools/stamp_r5.py; never in the product build): waves 0 and 4 record (s_memrealtime, s_memtime)
+// at R5_NST points into LDS past the kernel's own bytes; the block copies them to r5_stamps at the end.
+constexpr int R5_NST = 48, R5_STAMP_BLOCKS = 1024;
+constexpr int R5_LDS_ALL = R5_LDS + 2 * R5_NST * 16;
+__device__ unsigned long long r5_stamps[R5_STAMP_BLOCKS * 2 * R5_NST * 2];
+#define R5_STAMP(k)                                                                                              \
+  do {                                                                                                           \
+    if (lane == 0 && (wvu & 3) == 0 && (k) < R5_NST) {                                                           \
+      unsigned long long* sl_ = (unsigned long long*)(smem + R5_LDS + ((wvu >> 2) * R5_NST + (k)) * 16);          \
+      sl_[0] = __builtin_amdgcn_s_memrealtime();                                                                 \
+      sl_[1] = __builtin_amdgcn_s_memtime();                                                                     \
+    }                                                                                                            \
+  } while (0)
+#else
+constexpr int R5_LDS_ALL = R5_LDS;
+#define R5_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
+
 struct R5Args {
   const uint16_t* x;
   const uint16_t* wt;
@@ -69,6 +90,7 @@ __global__ __launch_bounds__(512, 1) void rdb5_kernel(R5Args a) {
   const int c0 = tile * 64;
   const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
   const __amdgpu_buffer_rsrc_t xr = buf_rsrc(a.x, a.x_bytes);
+  R5_STAMP(0);
 
   // this wave's DMA pieces of a row: instructions wvu, wvu + 8, wvu + 16 (< 19); lane -> 16-B unit 64 k + lane =
   // (pixel slot p, channel chunk j); pad units and out-of-image pixels get BUF_OOB (zeros land)
@@ -157,6 +179,7 @@ __global__ __launch_bounds__(512, 1) void rdb5_kernel(R5Args a) {
   };
   dma_step(r0 - 1, 0);
   dma_step(r0, 1);
+  R5_STAMP(1);
 
   // step s (compile-time phase K = s mod 6: row slot, residual set and accumulator row by K % 3, partial region by K & 1)
   auto step = [&](auto kc, int s) {
@@ -164,9 +187,11 @@ __global__ __launch_bounds__(512, 1) void rdb5_kernel(R5Args a) {
     constexpr int SA = K % 3;         // accumulator row of output row r0 + s (ky = 0 target) == the row finished here
     constexpr int SC = (K + 1) % 3;   // accumulator row of output row r0 + s - 2 (completed in this step)
     const int i = r0 - 1 + s;         // the row ingested in this step (slot K % 3)
+    R5_STAMP(2 + 3 * s);
     if (s == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NW) : "memory");
     lds_barrier();
+    R5_STAMP(3 + 3 * s);
     // residual operands of row i (finished two steps later)
     load_res(i, rs1[K % 3], rs2[K % 3]);
     // finish row i - 2 (completed last step): its other channel half from LDS, fixed order, epilogue, ST stores
@@ -207,6 +232,7 @@ __global__ __launch_bounds__(512, 1) void rdb5_kernel(R5Args a) {
     for (int f = 0; f < 4; ++f) acc[SA][f] = (f32x4){0.f, 0.f, 0.f, 0.f};
     // row i + 2 into the slot of row i - 1 (last read in the previous step)
     dma_step(i + 2, (K + 2) % 3);
+    R5_STAMP(4 + 3 * s);
     // ingest row i.  Every MFMA is issued unconditionally: a target row outside the strip lands in an accumulator row
     // that is zeroed before its next use and never finished, and a fragment past the image width reads zeros
     if (i >= 0 && i < a.h && i <= r1) {
@@ -252,6 +278,12 @@ __global__ __launch_bounds__(512, 1) void rdb5_kernel(R5Args a) {
     if (s + 5 < nsteps) step(std::integral_constant<int, 5>{}, s + 5);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef CLIMSR_R5_STAMP
+  R5_STAMP(R5_NST - 1);
+  __syncthreads();
+  if (tid < 4 * R5_NST && blockIdx.x < R5_STAMP_BLOCKS)
+    r5_stamps[(long)blockIdx.x * 4 * R5_NST + tid] = ((const unsigned long long*)(smem + R5_LDS))[tid];
+#endif
 }
 
 }  // namespace
@@ -302,9 +334,16 @@ int rdb5_launch(int mode, const ClimsrConvDesc* d, const ClimsrEpilogue* ep, con
     return CLIMSR_OK;
   }
   void (*k)(R5Args) = mode == 2 ? rdb5_kernel<2> : rdb5_kernel<1>;
-  if (int e = lds_opt_in((const void*)k, R5_LDS)) return e;
-  hipLaunchKernelGGL(k, dim3(a.tiles_x * a.strips * a.n), dim3(512), R5_LDS, s, a);
+  if (int e = lds_opt_in((const void*)k, R5_LDS_ALL)) return e;
+  hipLaunchKernelGGL(k, dim3(a.tiles_x * a.strips * a.n), dim3(512), R5_LDS_ALL, s, a);
   return check_launch("conv2d_fwd (rdb5)");
 }
 
 }  // namespace climsr
+
+#ifdef CLIMSR_R5_STAMP
+extern "C" int climsr_diag_r5_stamps(void* dst, long bytes) {
+  const long cap = (long)sizeof(unsigned long long) * R5_STAMP_BLOCKS * 2 * R5_NST * 2;
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(r5_stamps), bytes < cap ? bytes : cap, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -20,7 +20,7 @@ import torch
 import torch.nn as nn
 from torch import Tensor
 
-from .. import ops
+from .. import _lib, ops
 from ..core.flat import FlatParamsMixin
 from ..ops import ACT_LRELU, ACT_LRELU_BWD, BatchedPacker, ConvPlan, Workspace
 
@@ -52,6 +52,7 @@ class _DEngine:
         self.version = -1
         self.ws = Workspace()
         self.scratch: Dict[str, Tensor] = {}
+        self.fuse_stem = True  # features.0 + features.2 as one launch (False: per layer; tools/perf_stem.py's A/B)
 
     def ensure_packed(self):
         v = self.d._flat._version
@@ -94,7 +95,7 @@ class _DEngine:
         stem = None
         (c0, bn0, p0), (c1, bn1, p1) = self.layers[0], self.layers[1]
         if (cin == 1 and bn0 is None and bn1 is not None and p0.cout == 64 and p1.cin_real == 64 and p1.cout == 64 and p1.stride == 2
-                and p1.kpk == 576):
+                and p1.kpk == 576 and self.fuse_stem and _lib.has("climsr_d_stem_s2")):
             oh, ow = p1.out_hw(h, w)
             a0 = _bf16((n, h, w, 64), dev) if keep else None
             z = _bf16((n, oh, ow, 64), dev)

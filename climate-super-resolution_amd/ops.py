@@ -164,6 +164,8 @@ class ConvPlan:
 
     def pool_ok(self, x_cs: int, in_h: int, in_w: int, n: int, y_cs: int, act: int = ACT_RELU) -> bool:
         """Whether fwd(..., act=act, pool2=True) has a fused conv + 2x2 max-pool kernel (climsr_conv2d_fwd_pool_ok)."""
+        if not _lib.has("climsr_conv2d_fwd_pool_ok"):  # (an older A/B build: _lib.load)
+            return False
         oh, ow = self.out_hw(in_h, in_w)
         d = ConvDesc(n, in_h, in_w, self.cin_k, x_cs, 0, 1, self.ks, self.stride, self.pad, oh, ow, self.cout, y_cs, 0, self.cc)
         ep = Epilogue(act, 0.2, 1.0, None, 0, 0, 1.0, None, 0, 0, OUT_BF16, 0, 0, 1.0, 1.0, 0, None, 0, 1.0, None, pool2=1)

@@ -52,7 +52,7 @@ def test_struct_layouts_match_header(lib):
     assert ctypes.sizeof(_lib.ConvDesc) == 16 * 4
     # ClimsrEpilogue: int, float, float, ptr, int, int, float, ptr, int, int, int, int, int, float, float, int, ptr,
     # int, float, ptr (bn_part), ptr (bn_z), int, float, 4 ptrs (natural alignment)
-    assert ctypes.sizeof(_lib.Epilogue) == 160  # ... bn_beta, ch_part (pointer)
+    assert ctypes.sizeof(_lib.Epilogue) == 168  # ... bn_beta, ch_part (pointer), pool2 (int, padded)
     assert _lib.Epilogue.aux.offset == 80 and _lib.Epilogue.aux_scale.offset == 92
     assert _lib.Epilogue().beta1 == 1.0 and _lib.Epilogue().beta2 == 1.0
     # ClimsrPullPackDesc: ptr, ptr[5], int[5], int[5], 6 ints
