@@ -168,12 +168,14 @@ __global__ __launch_bounds__(512, 1) void rdb5_kernel(R5Args a) {
   static_assert(ST >= R5_K, "the compiler's residual wait must not drain the next row's DMA");
   const int nsteps = r1 - r0 + 3;  // ingest rows r0 - 1 .. r1, finish rows r0 .. r1 - 1 one step after completion
   auto dma_step = [&](int row, int slot) {
-    const bool ok = row >= r0 - 1 && row <= r1 && row >= 0 && row < a.h;
-    const uint32_t rb = ok ? (uint32_t)(nimg * a.h + row) * xrow : 0u;
+    // rows of the strip's window [r0 - 1, r1] land in their slot (zeros outside the image); any other row's pieces go
+    // to the dummy KB (the MFMAs of that step only touch accumulator rows that are never finished)
+    const bool win = row >= r0 - 1 && row <= r1, img = row >= 0 && row < a.h;
+    const uint32_t rb = img ? (uint32_t)(nimg * a.h + row) * xrow : 0u;
 #pragma unroll
     for (int j = 0; j < R5_K; ++j) {
-      const bool real = ok && wvu + 8 * j < R5_NI;
-      glds(real && po[j] != BUF_OOB ? po[j] + rb : BUF_OOB,
+      const bool real = win && wvu + 8 * j < R5_NI;
+      glds(real && img && po[j] != BUF_OOB ? po[j] + rb : BUF_OOB,
            lds0 + (uint32_t)(real ? slot * R5_SLOT + (wvu + 8 * j) * 1024 : R5_OFF_DUMMY));
     }
   };
@@ -181,7 +183,34 @@ __global__ __launch_bounds__(512, 1) void rdb5_kernel(R5Args a) {
   dma_step(r0, 1);
   R5_STAMP(1);
 
-  // step s (compile-time phase K = s mod 6: row slot, residual set and accumulator row by K % 3, partial region by K & 1)
+  // the epilogue of one fragment of row yf: the partner's channel half (LDS) + this wave's, fixed order, ST stores
+  auto finish = [&](int m, int yf, bool fin, const f32x4& own, const f32x4& other, const rv_t& r1v, const rv_t& r2v) {
+    const f32x4 sum = hh == 0 ? own + other : other + own;
+    const bool ok = fin && pix_ok(yf, m);
+    const uint32_t p = ok ? pidx(yf, m) : 0u;
+    const int co = 16 * q + 4 * g;
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float t = sum[e] + bb[e];
+      t = t * a.alpha1 + a.beta1 * rval(r1v, e);
+      if (has2) t = t * a.alpha2 + a.beta2 * rval(r2v, e);
+      v[e] = t;
+    }
+    if constexpr (F32) {
+      const v4u32 o = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+      __builtin_amdgcn_raw_buffer_store_b128(o, ry, ok ? (p * a.ycs + a.yco + co) * 4u : BUF_OOB, 0, 0);
+      const v2u32 x2 = {pk2(a.aux_scale * v[0], a.aux_scale * v[1]), pk2(a.aux_scale * v[2], a.aux_scale * v[3])};
+      __builtin_amdgcn_raw_buffer_store_b64(x2, rax, ok ? (p * a.auxcs + a.auxco + co) * 2u : BUF_OOB, 0, 0);
+    } else {
+      const v2u32 o = {pk2(v[0], v[1]), pk2(v[2], v[3])};
+      __builtin_amdgcn_raw_buffer_store_b64(o, ry, ok ? (p * a.ycs + a.yco + co) * 2u : BUF_OOB, 0, 0);
+    }
+  };
+
+  // step s (compile-time phase K = s mod 6: row slot, residual set and accumulator row by K % 3, partial region by K & 1).
+  // One basic block from the barrier to the partial-sum hand-off: the residual loads, the epilogue of row i - 2 and
+  // the DMA of row i + 2 are issued between the MFMA groups of row i, so the MFMA pipe does not idle behind them
   auto step = [&](auto kc, int s) {
     constexpr int K = decltype(kc)::value;
     constexpr int SA = K % 3;         // accumulator row of output row r0 + s (ky = 0 target) == the row finished here
@@ -192,72 +221,51 @@ __global__ __launch_bounds__(512, 1) void rdb5_kernel(R5Args a) {
     else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NW) : "memory");
     lds_barrier();
     R5_STAMP(3 + 3 * s);
-    // residual operands of row i (finished two steps later)
-    load_res(i, rs1[K % 3], rs2[K % 3]);
-    // finish row i - 2 (completed last step): its other channel half from LDS, fixed order, epilogue, ST stores
+    // row i - 2 (completed last step): this wave's two fragments and the partner's halves of them
+    const int yf = i - 2;
+    const bool fin = yf >= r0 && yf < r1;
+    f32x4 own[2], other[2];
     {
-      const int yf = i - 2;
-      const bool fin = yf >= r0 && yf < r1;
       const char* part = smem + R5_OFF_P + ((K + 1) & 1) * R5_PART;
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
-        const int f = 2 * hh + m;
-        const f32x4 other = *(const f32x4*)(part + (q * 4 + f) * 1024 + lane * 16);
-        const f32x4 own = hh == 0 ? acc[SA][m] : acc[SA][2 + m];  // (a register select: acc is never indexed at run time)
-        const f32x4 sum = hh == 0 ? own + other : other + own;
-        const bool ok = fin && pix_ok(yf, m);
-        const uint32_t p = ok ? pidx(yf, m) : 0u;
-        const int co = 16 * q + 4 * g;
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float t = sum[e] + bb[e];
-          t = t * a.alpha1 + a.beta1 * rval(rs1[(K + 1) % 3][m], e);
-          if (has2) t = t * a.alpha2 + a.beta2 * rval(rs2[(K + 1) % 3][m], e);
-          v[e] = t;
-        }
-        if constexpr (F32) {
-          const v4u32 o = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
-          __builtin_amdgcn_raw_buffer_store_b128(o, ry, ok ? (p * a.ycs + a.yco + co) * 4u : BUF_OOB, 0, 0);
-          const v2u32 x2 = {pk2(a.aux_scale * v[0], a.aux_scale * v[1]), pk2(a.aux_scale * v[2], a.aux_scale * v[3])};
-          __builtin_amdgcn_raw_buffer_store_b64(x2, rax, ok ? (p * a.auxcs + a.auxco + co) * 2u : BUF_OOB, 0, 0);
-        } else {
-          const v2u32 o = {pk2(v[0], v[1]), pk2(v[2], v[3])};
-          __builtin_amdgcn_raw_buffer_store_b64(o, ry, ok ? (p * a.ycs + a.yco + co) * 2u : BUF_OOB, 0, 0);
-        }
+        other[m] = *(const f32x4*)(part + (q * 4 + 2 * hh + m) * 1024 + lane * 16);
+        own[m] = hh == 0 ? acc[SA][m] : acc[SA][2 + m];  // (a register select: acc is never indexed at run time)
       }
-      if constexpr (!F32) __builtin_amdgcn_raw_buffer_store_b32(0u, ry, BUF_OOB, 0, 0);  // (ST = 3: see above)
     }
 #pragma unroll
     for (int f = 0; f < 4; ++f) acc[SA][f] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    // row i + 2 into the slot of row i - 1 (last read in the previous step)
-    dma_step(i + 2, (K + 2) % 3);
-    R5_STAMP(4 + 3 * s);
-    // ingest row i.  Every MFMA is issued unconditionally: a target row outside the strip lands in an accumulator row
-    // that is zeroed before its next use and never finished, and a fragment past the image width reads zeros
-    if (i >= 0 && i < a.h && i <= r1) {
-      const char* xs = smem + (K % 3) * R5_SLOT + lb;
-      bf16x8 B[2][4];
-      auto ldB = [&](int grp, int buf) {
-        const int kx = grp >> 1, cb = grp & 1;
+    // ingest row i.  Every MFMA is issued: rows of the window outside the image are zeros in their slot, and the
+    // last step's row (r1 + 1) only reaches accumulator rows that are never finished
+    const char* xs = smem + (K % 3) * R5_SLOT + lb;
+    bf16x8 B[2][4];
+    auto ldB = [&](int grp, int buf) {
+      const int kx = grp >> 1, cb = grp & 1;
 #pragma unroll
-        for (int f = 0; f < 4; ++f) B[buf][f] = *(const bf16x8*)(xs + (16 * f + kx) * R5_PITCH + cb * 64);
-      };
-      ldB(0, 0);
+      for (int f = 0; f < 4; ++f) B[buf][f] = *(const bf16x8*)(xs + (16 * f + kx) * R5_PITCH + cb * 64);
+    };
+    ldB(0, 0);
 #pragma unroll
-      for (int grp = 0; grp < 6; ++grp) {
-        const int kx = grp >> 1, cb = grp & 1;
-        if (grp + 1 < 6) ldB(grp + 1, (grp + 1) & 1);
-        __builtin_amdgcn_sched_barrier(0);
+    for (int grp = 0; grp < 6; ++grp) {
+      const int kx = grp >> 1, cb = grp & 1;
+      if (grp + 1 < 6) ldB(grp + 1, (grp + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int ky = 0; ky < 3; ++ky) {
-          constexpr int SL[3] = {SA, (K + 2) % 3, SC};  // rows r0 + s, r0 + s - 1, r0 + s - 2
+      for (int ky = 0; ky < 3; ++ky) {
+        constexpr int SL[3] = {SA, (K + 2) % 3, SC};  // rows r0 + s, r0 + s - 1, r0 + s - 2
 #pragma unroll
-          for (int f = 0; f < 4; ++f)
-            acc[SL[ky]][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ky][kx][cb], B[grp & 1][f], acc[SL[ky]][f], 0, 0, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
+        for (int f = 0; f < 4; ++f)
+          acc[SL[ky]][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ky][kx][cb], B[grp & 1][f], acc[SL[ky]][f], 0, 0, 0);
       }
+      // the step's memory work, in the hand-counted order RL, ST, DMA (see above)
+      if (grp == 0) load_res(i, rs1[K % 3], rs2[K % 3]);  // residuals of row i (finished two steps later)
+      if (grp == 1) finish(0, yf, fin, own[0], other[0], rs1[(K + 1) % 3][0], rs2[(K + 1) % 3][0]);
+      if (grp == 2) {
+        finish(1, yf, fin, own[1], other[1], rs1[(K + 1) % 3][1], rs2[(K + 1) % 3][1]);
+        if constexpr (!F32) __builtin_amdgcn_raw_buffer_store_b32(0u, ry, BUF_OOB, 0, 0);  // (ST = 3: see above)
+      }
+      if (grp == 3) dma_step(i + 2, (K + 2) % 3);  // row i + 2 into the slot of row i - 1 (last read last step)
+      __builtin_amdgcn_sched_barrier(0);
     }
     // row i - 1 is complete: hand the partner the two fragments it finishes
     if (i - 1 >= r0 && i - 1 < r1) {
