@@ -33,6 +33,9 @@ constexpr int R5_OFF_P = R5_NSLOT * R5_SLOT;       // 58,368
 constexpr int R5_OFF_DUMMY = R5_OFF_P + 2 * R5_PART;  // one KB the padding DMA pieces write (zeros, never read)
 constexpr int R5_LDS = R5_OFF_DUMMY + 1024;        // 92,160 B
 constexpr int R5_K = 3;                            // DMA pieces per wave and row (19 real + 5 padding over 8 waves)
+#ifndef CLIMSR_R5_EXP  // timing experiments of diagnostic builds only (tools/gpu_r05f.sh): 1 no step DMA, 2 no residual
+#define CLIMSR_R5_EXP 0  // loads, 3 no stores, 4 none of the three, 5 no MFMAs -- their results are wrong
+#endif
 
 #ifdef CLIMSR_R5_STAMP
 // Timing diagnostic (tools/stamp_r5.py; never in the product build): waves 0 and 4 record (s_memrealtime, s_memtime)
@@ -255,16 +258,20 @@ __global__ __launch_bounds__(512, 1) void rdb5_kernel(R5Args a) {
         constexpr int SL[3] = {SA, (K + 2) % 3, SC};  // rows r0 + s, r0 + s - 1, r0 + s - 2
 #pragma unroll
         for (int f = 0; f < 4; ++f)
-          acc[SL[ky]][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ky][kx][cb], B[grp & 1][f], acc[SL[ky]][f], 0, 0, 0);
+          if (CLIMSR_R5_EXP != 5)
+            acc[SL[ky]][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[ky][kx][cb], B[grp & 1][f], acc[SL[ky]][f], 0, 0, 0);
+          else
+            acc[SL[ky]][f] += __builtin_bit_cast(f32x4, B[grp & 1][f]);
       }
       // the step's memory work, in the hand-counted order RL, ST, DMA (see above)
-      if (grp == 0) load_res(i, rs1[K % 3], rs2[K % 3]);  // residuals of row i (finished two steps later)
-      if (grp == 1) finish(0, yf, fin, own[0], other[0], rs1[(K + 1) % 3][0], rs2[(K + 1) % 3][0]);
-      if (grp == 2) {
+      constexpr int X = CLIMSR_R5_EXP;
+      if (grp == 0 && X != 2 && X != 4) load_res(i, rs1[K % 3], rs2[K % 3]);  // residuals of row i (finished two steps later)
+      if (grp == 1 && X != 3 && X != 4) finish(0, yf, fin, own[0], other[0], rs1[(K + 1) % 3][0], rs2[(K + 1) % 3][0]);
+      if (grp == 2 && X != 3 && X != 4) {
         finish(1, yf, fin, own[1], other[1], rs1[(K + 1) % 3][1], rs2[(K + 1) % 3][1]);
         if constexpr (!F32) __builtin_amdgcn_raw_buffer_store_b32(0u, ry, BUF_OOB, 0, 0);  // (ST = 3: see above)
       }
-      if (grp == 3) dma_step(i + 2, (K + 2) % 3);  // row i + 2 into the slot of row i - 1 (last read last step)
+      if (grp == 3 && X != 1 && X != 4) dma_step(i + 2, (K + 2) % 3);  // row i + 2 into the slot of row i - 1 (last read last step)
       __builtin_amdgcn_sched_barrier(0);
     }
     // row i - 1 is complete: hand the partner the two fragments it finishes
