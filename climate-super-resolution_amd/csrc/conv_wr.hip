@@ -111,30 +111,24 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
     oy0 = ty * WR_TR;
     ox0 = tx * WR_TC;
   };
-  // the footprint DMA of a tile (tile < 0: zeros, which keeps the per-iteration DMA count fixed) in WR_NI pieces:
-  // prep() once, piece(i) for every instruction i
-  struct Fp {
-    int nimg, oy0, ox0;
-    bool fast;      // interior tile, no upsampling (wave-uniform): the corner's offset on the scalar unit, one add a piece
-    uint32_t base, dst;
-  };
-  auto prep = [&](int tile, int b) {
-    Fp f{0, -1 << 20, 0, false, 0u, mybuf + (uint32_t)(b * WR_BUF)};
-    if (tile >= 0) decode(tile, f.nimg, f.oy0, f.ox0);
-    f.fast = ups == 0 && f.oy0 >= 1 && f.oy0 - 1 + WR_PR <= a.in_h && f.ox0 >= 1 && f.ox0 - 1 + WR_PC <= a.in_w;
-    // (unsigned: for the zero tile's sentinel row the product wraps instead of overflowing; base is unused then)
-    const uint32_t corner = (uint32_t)(f.nimg * a.in_h + f.oy0 - 1) * (uint32_t)a.in_w + (uint32_t)(f.ox0 - 1);
-    f.base = (corner * (uint32_t)a.in_cs + (uint32_t)a.in_co) * 2u;
-    return f;
-  };
-  auto piece = [&](const Fp& f, int i) {
-    if (f.fast) {
-      glds(f.base + rel[i], f.dst + (uint32_t)(i * 1024));
+  auto issue = [&](int tile, int b) {  // tile < 0: zeros (keeps the per-iteration DMA count fixed)
+    int nimg = 0, oy0 = -1 << 20, ox0 = 0;
+    if (tile >= 0) decode(tile, nimg, oy0, ox0);
+    const uint32_t dst = mybuf + (uint32_t)(b * WR_BUF);
+    if (ups == 0 && oy0 >= 1 && oy0 - 1 + WR_PR <= a.in_h && ox0 >= 1 && ox0 - 1 + WR_PC <= a.in_w) {
+      // interior (wave-uniform): the corner's offset on the scalar unit, one add per instruction
+      const uint32_t corner = (uint32_t)(nimg * a.in_h + oy0 - 1) * (uint32_t)a.in_w + (uint32_t)(ox0 - 1);
+      const uint32_t base = (corner * (uint32_t)a.in_cs + (uint32_t)a.in_co) * 2u;
+#pragma unroll
+      for (int i = 0; i < WR_NI; ++i) glds(base + rel[i], dst + (uint32_t)(i * 1024));
     } else {
-      const int iy = f.oy0 - 1 + (dg[i] >> 16), ix = f.ox0 - 1 + ((dg[i] >> 8) & 255), c = dg[i] & 255;
-      const bool ok = dg[i] >= 0 && iy >= 0 && iy < lh && ix >= 0 && ix < lw;
-      const uint32_t off = (uint32_t)((((long)(f.nimg * a.in_h + (iy >> ups)) * a.in_w + (ix >> ups)) * a.in_cs + a.in_co + c * 8) * 2);
-      glds(ok ? off : BUF_OOB, f.dst + (uint32_t)(i * 1024));
+#pragma unroll
+      for (int i = 0; i < WR_NI; ++i) {
+        const int iy = oy0 - 1 + (dg[i] >> 16), ix = ox0 - 1 + ((dg[i] >> 8) & 255), c = dg[i] & 255;
+        const bool ok = dg[i] >= 0 && iy >= 0 && iy < lh && ix >= 0 && ix < lw;
+        const uint32_t off = (uint32_t)((((long)(nimg * a.in_h + (iy >> ups)) * a.in_w + (ix >> ups)) * a.in_cs + a.in_co + c * 8) * 2);
+        glds(ok ? off : BUF_OOB, dst + (uint32_t)(i * 1024));
+      }
     }
   };
 
@@ -142,19 +136,14 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
   const __amdgpu_buffer_rsrc_t pr = buf_rsrc(a.ch_part, SUMS && a.ch_part ? (uint32_t)a.ntiles * 256u : 0u);
   const __amdgpu_buffer_rsrc_t rr = buf_rsrc(a.res1, (EP == 1 || EP == 2) ? a.r1_bytes : 0u);
   const int lb = col * WR_XP * 2 + g * 16;  // this lane's byte offset in a footprint row: pixel col, channels 8 g ..
-  {
-    const Fp f0 = prep(T, 0);
-#pragma unroll
-    for (int i = 0; i < WR_NI; ++i) piece(f0, i);
-  }
+  issue(T, 0);
   for (int it = 0;; ++it) {
     const int Tn = T + G4;
-    // the next tile's footprint goes out two pieces per k block over the first 9, under the MFMAs of this one (issued
-    // all at once ahead of them, their address arithmetic ran with the MFMA pipe idle)
-    const Fp fn = prep(Tn < a.ntiles ? Tn : -1, (it + 1) & 1);
-    // tile T's footprint has landed once at most the younger operations are outstanding: the last epilogue's
-    if (it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NEPI) : "memory");
+    issue(Tn < a.ntiles ? Tn : -1, (it + 1) & 1);
+    // tile T's footprint has landed once at most the younger operations are outstanding: the last epilogue's and
+    // the DMA just issued
+    if (it == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WR_NI) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WR_NI + NEPI) : "memory");
     const char* xb = smem + (wv * 2 + (it & 1)) * WR_BUF + lb;
     f32x4 acc[4][4];  // [output row m][co block t]
     bf16x8 bq[2][4];
@@ -167,8 +156,6 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
 #pragma unroll
     for (int j = 0; j < 18; ++j) {
       if (j + 1 < 18) ldb(j + 1, (j + 1) & 1);
-      if (2 * j < WR_NI) piece(fn, 2 * j);
-      if (2 * j + 1 < WR_NI) piece(fn, 2 * j + 1);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int m = 0; m < 4; ++m) {

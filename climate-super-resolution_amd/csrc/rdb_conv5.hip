@@ -12,8 +12,10 @@
 // Eight waves: wave w owns output channels 16 (w & 3) .. + 15 and input channels 64 (w >> 2) .. + 63 for all four
 // 16-pixel fragments of a row; its 18 weight fragments (3 x 3 taps x 2 channel blocks of 32) stay in registers for
 // the launch.  The two channel halves of an output block are summed through LDS (each wave finishes two of the four
-// fragments, in a fixed order: half 0 + half 1, deterministic) before the epilogue.
-// One barrier per row; the residual operands of a row are loaded two steps before it is finished, and the waits are
+// fragments, in a fixed order: half 0 + half 1, deterministic) before the epilogue.  The epilogue trades halves of
+// the two fragments between lane rows g and g ^ 1 (v_permlane16_swap) so that each lane holds 8 consecutive channels
+// of one pixel: residuals and outputs move as 16-B loads / stores (8-B ones cost twice the issue per byte).
+// One barrier per row; the residual operands of a row are loaded one step before it is finished, and the waits are
 // counted by hand (see the step loop) so that the next row's DMA stays in flight across them.
 // LDS pixel slots are 288 B (128 channels + 32 B pad): the 16-B unit of channel chunk c of slot p is 18 p + c, so
 // the 16 lanes of each ds_read_b128 bank group (two channel groups, 8 pixels each) cover the 64 banks once.
@@ -80,7 +82,7 @@ __device__ __forceinline__ uint32_t pk2(float a, float b) {
 }
 
 // MODE 1: conv5 (bias, bf16 residuals, bf16 out); MODE 2: pull-x (no bias, fp32 residuals, fp32 out, optional bf16 aux)
-template <int MODE>
+template <int MODE, bool R2>
 __global__ __launch_bounds__(512, 1) void rdb5_kernel(R5Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool F32 = MODE == 2;
@@ -120,55 +122,54 @@ __global__ __launch_bounds__(512, 1) void rdb5_kernel(R5Args a) {
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) A[ky][kx][cb] = *(const bf16x8*)(wr + (2 * hh + cb) * 288 + (3 * ky + kx) * 32);
   }
-  float bb[4] = {0.f, 0.f, 0.f, 0.f};
+  // after the swap (see finish) lane (col, g) holds channels co8 .. co8 + 7 of fragment 2 hh + (g & 1), pixel col
+  const int co8 = 16 * q + 8 * (g >> 1), fm = g & 1;
+  float bb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if constexpr (MODE == 1) {
-    const float4 b4 = *(const float4*)(a.bias + 16 * q + 4 * g);
-    bb[0] = b4.x; bb[1] = b4.y; bb[2] = b4.z; bb[3] = b4.w;
+    const float4 b0 = *(const float4*)(a.bias + co8), b1 = *(const float4*)(a.bias + co8 + 4);
+    bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w; bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
   }
-  const bool has2 = a.res2 != nullptr, has_aux = MODE == 2 && a.aux != nullptr;
-  const __amdgpu_buffer_rsrc_t rr1 = buf_rsrc(a.res1, a.r1_bytes), rr2 = buf_rsrc(a.res2, has2 ? a.r2_bytes : 0u);
+  const bool has_aux = MODE == 2 && a.aux != nullptr;
+  const __amdgpu_buffer_rsrc_t rr1 = buf_rsrc(a.res1, a.r1_bytes), rr2 = buf_rsrc(a.res2, R2 ? a.r2_bytes : 0u);
   const __amdgpu_buffer_rsrc_t ry = buf_rsrc(a.y, a.y_bytes), rax = buf_rsrc(a.aux, has_aux ? a.aux_bytes : 0u);
   f32x4 acc[3][4];
 #pragma unroll
   for (int s = 0; s < 3; ++s)
 #pragma unroll
     for (int f = 0; f < 4; ++f) acc[s][f] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  // residual operands of the two fragments this wave finishes (f = 2 hh + m): three sets, loaded two steps ahead
-  typedef uint32_t rv_t __attribute__((ext_vector_type(F32 ? 4 : 2)));
-  rv_t rs1[3][2], rs2[3][2];
-  auto pix_ok = [&](int y, int m) { return y >= r0 && y < r1 && c0 + 16 * (2 * hh + m) + col < a.w; };
-  auto pidx = [&](int y, int m) { return (uint32_t)((nimg * a.h + y) * a.w + c0 + 16 * (2 * hh + m) + col); };
-  auto load_res = [&](int y, rv_t (&r1v)[2], rv_t (&r2v)[2]) {
+  // residual operands of this lane's 8 channels of the row it finishes: two sets, loaded one step ahead; 16 B each
+  // (bf16), two 16-B halves (fp32)
+  constexpr int NR = F32 ? 2 : 1;
+  struct Rv {
+    v4u32 v[NR];
+  };
+  Rv rs1[2], rs2[2];
+  const bool col_ok = c0 + 16 * (2 * hh + fm) + col < a.w;
+  auto pidx = [&](int y) { return (uint32_t)((nimg * a.h + y) * a.w + c0 + 16 * (2 * hh + fm) + col); };
+  auto load_res = [&](int y, Rv& r1v, Rv& r2v) {
+    const bool ok = y >= r0 && y < r1 && col_ok;
+    const uint32_t p = ok ? pidx(y) : 0u;
 #pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const bool ok = pix_ok(y, m);
-      const uint32_t p = ok ? pidx(y, m) : 0u;
-      const int co = 16 * q + 4 * g;
-      const uint32_t o1 = ok ? (p * a.r1cs + a.r1co + co) * (F32 ? 4u : 2u) : BUF_OOB;
-      const uint32_t o2 = ok ? (p * a.r2cs + a.r2co + co) * (F32 ? 4u : 2u) : BUF_OOB;
-      if constexpr (F32) {
-        r1v[m] = __builtin_bit_cast(rv_t, __builtin_amdgcn_raw_buffer_load_b128(rr1, o1, 0, 0));
-        r2v[m] = __builtin_bit_cast(rv_t, __builtin_amdgcn_raw_buffer_load_b128(rr2, o2, 0, 0));
-      } else {
-        r1v[m] = __builtin_bit_cast(rv_t, __builtin_amdgcn_raw_buffer_load_b64(rr1, o1, 0, 0));
-        r2v[m] = __builtin_bit_cast(rv_t, __builtin_amdgcn_raw_buffer_load_b64(rr2, o2, 0, 0));
-      }
+    for (int h = 0; h < NR; ++h) {
+      r1v.v[h] = __builtin_bit_cast(v4u32, __builtin_amdgcn_raw_buffer_load_b128(
+                                               rr1, ok ? (p * a.r1cs + a.r1co + co8 + 4 * h) * (F32 ? 4u : 2u) : BUF_OOB, 0, 0));
+      if constexpr (R2)
+        r2v.v[h] = __builtin_bit_cast(v4u32, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 rr2, ok ? (p * a.r2cs + a.r2co + co8 + 4 * h) * (F32 ? 4u : 2u) : BUF_OOB, 0, 0));
     }
   };
-  auto rval = [&](const rv_t& r, int i) -> float {
-    if constexpr (F32) return __uint_as_float(r[i]);
-    else return bf2f((uint16_t)((i & 1) ? (r[i >> 1] >> 16) : r[i >> 1]));
+  auto rval = [&](const Rv& r, int i) -> float {  // channel co8 + i
+    if constexpr (F32) return __uint_as_float(r.v[i >> 2][i & 3]);
+    else return bf2f((uint16_t)((i & 1) ? (r.v[0][i >> 1] >> 16) : r.v[0][i >> 1]));
   };
   const int lb = col * R5_PITCH + (8 * hh + g) * 16;  // this lane's B offset: pixel slot col (+ 16 f + kx), chunk 8 hh + 4 cb + g
 
-  // Hand-counted waits.  Per step every wave issues, in this order, RL residual loads (for the row it finishes two
-  // steps later), ST stores (the row it finishes now) and R5_K DMA pieces (the row it ingests two steps later), all
+  // Hand-counted waits.  Per step every wave issues, in this order, RL residual loads (for the row it finishes in the
+  // next step), ST stores (the row it finishes now) and R5_K DMA pieces (the row it ingests two steps later), all
   // unconditionally (out-of-range offsets / the dummy KB where there is nothing to move).  Step s needs the DMA of
-  // step s - 2: younger are step s - 1's RL + ST + R5_K operations.  hipcc's own wait for the residuals of step s - 2
-  // counts only its loads and stores (2 ST + 2 RL younger ones), which with ST >= R5_K also leaves step s - 1's DMA
-  // in flight.
-  constexpr int RL = 4, ST = F32 ? 4 : 3, NW = RL + ST + R5_K;
-  static_assert(ST >= R5_K, "the compiler's residual wait must not drain the next row's DMA");
+  // step s - 2: younger are step s - 1's RL + ST + R5_K operations.  (hipcc's own wait for the residuals of step s - 1,
+  // which counts only loads and stores, may also cover step s - 1's DMA: issued half a step earlier, landed by then.)
+  constexpr int RL = NR * (R2 ? 2 : 1), ST = F32 ? 3 : 1, NW = RL + ST + R5_K;
   const int nsteps = r1 - r0 + 3;  // ingest rows r0 - 1 .. r1, finish rows r0 .. r1 - 1 one step after completion
   auto dma_step = [&](int row, int slot) {
     // rows of the strip's window [r0 - 1, r1] land in their slot (zeros outside the image); any other row's pieces go
@@ -186,28 +187,41 @@ __global__ __launch_bounds__(512, 1) void rdb5_kernel(R5Args a) {
   dma_step(r0, 1);
   R5_STAMP(1);
 
-  // the epilogue of one fragment of row yf: the partner's channel half (LDS) + this wave's, fixed order, ST stores
-  auto finish = [&](int m, int yf, bool fin, const f32x4& own, const f32x4& other, const rv_t& r1v, const rv_t& r2v) {
-    const f32x4 sum = hh == 0 ? own + other : other + own;
-    const bool ok = fin && pix_ok(yf, m);
-    const uint32_t p = ok ? pidx(yf, m) : 0u;
-    const int co = 16 * q + 4 * g;
-    float v[4];
+  // the epilogue of row yf: this wave's two fragments (own channel half + the partner's, fixed order), the fragment
+  // halves traded so that each lane holds 8 channels of one pixel, bias / residuals, one 16-B store (fp32: two, and the
+  // bf16 aux)
+  auto finish = [&](int yf, bool fin, const f32x4 (&own)[2], const f32x4 (&other)[2], const Rv& r1v, const Rv& r2v) {
+    f32x4 s0 = hh == 0 ? own[0] + other[0] : other[0] + own[0];
+    f32x4 s1 = hh == 0 ? own[1] + other[1] : other[1] + own[1];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float t = sum[e] + bb[e];
+    for (int e = 0; e < 4; ++e) {  // rows 1, 3 of fragment 0 <-> rows 0, 2 of fragment 1
+      const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(s0[e]), __float_as_uint(s1[e]), false, false);
+      s0[e] = __uint_as_float(sw[0]);
+      s1[e] = __uint_as_float(sw[1]);
+    }
+    const bool ok = fin && col_ok;
+    const uint32_t p = ok ? pidx(yf) : 0u;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float t = (e < 4 ? s0[e] : s1[e - 4]) + bb[e];
       t = t * a.alpha1 + a.beta1 * rval(r1v, e);
-      if (has2) t = t * a.alpha2 + a.beta2 * rval(r2v, e);
+      if (R2) t = t * a.alpha2 + a.beta2 * rval(r2v, e);
       v[e] = t;
     }
     if constexpr (F32) {
-      const v4u32 o = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
-      __builtin_amdgcn_raw_buffer_store_b128(o, ry, ok ? (p * a.ycs + a.yco + co) * 4u : BUF_OOB, 0, 0);
-      const v2u32 x2 = {pk2(a.aux_scale * v[0], a.aux_scale * v[1]), pk2(a.aux_scale * v[2], a.aux_scale * v[3])};
-      __builtin_amdgcn_raw_buffer_store_b64(x2, rax, ok ? (p * a.auxcs + a.auxco + co) * 2u : BUF_OOB, 0, 0);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const v4u32 o = {__float_as_uint(v[4 * h]), __float_as_uint(v[4 * h + 1]), __float_as_uint(v[4 * h + 2]),
+                         __float_as_uint(v[4 * h + 3])};
+        __builtin_amdgcn_raw_buffer_store_b128(o, ry, ok ? (p * a.ycs + a.yco + co8 + 4 * h) * 4u : BUF_OOB, 0, 0);
+      }
+      const v4u32 x4 = {pk2(a.aux_scale * v[0], a.aux_scale * v[1]), pk2(a.aux_scale * v[2], a.aux_scale * v[3]),
+                        pk2(a.aux_scale * v[4], a.aux_scale * v[5]), pk2(a.aux_scale * v[6], a.aux_scale * v[7])};
+      __builtin_amdgcn_raw_buffer_store_b128(x4, rax, ok ? (p * a.auxcs + a.auxco + co8) * 2u : BUF_OOB, 0, 0);
     } else {
-      const v2u32 o = {pk2(v[0], v[1]), pk2(v[2], v[3])};
-      __builtin_amdgcn_raw_buffer_store_b64(o, ry, ok ? (p * a.ycs + a.yco + co) * 2u : BUF_OOB, 0, 0);
+      const v4u32 o = {pk2(v[0], v[1]), pk2(v[2], v[3]), pk2(v[4], v[5]), pk2(v[6], v[7])};
+      __builtin_amdgcn_raw_buffer_store_b128(o, ry, ok ? (p * a.ycs + a.yco + co8) * 2u : BUF_OOB, 0, 0);
     }
   };
 
@@ -265,15 +279,12 @@ __global__ __launch_bounds__(512, 1) void rdb5_kernel(R5Args a) {
       }
       // the step's memory work, in the hand-counted order RL, ST, DMA (see above)
       constexpr int X = CLIMSR_R5_EXP;
-      if (grp == 0 && X != 2 && X != 4) load_res(i, rs1[K % 3], rs2[K % 3]);  // residuals of row i (finished two steps later)
-      if (grp == 1 && X != 3 && X != 4) finish(0, yf, fin, own[0], other[0], rs1[(K + 1) % 3][0], rs2[(K + 1) % 3][0]);
-      if (grp == 2 && X != 3 && X != 4) {
-        finish(1, yf, fin, own[1], other[1], rs1[(K + 1) % 3][1], rs2[(K + 1) % 3][1]);
-        if constexpr (!F32) __builtin_amdgcn_raw_buffer_store_b32(0u, ry, BUF_OOB, 0, 0);  // (ST = 3: see above)
-      }
+      if (grp == 0 && X != 2 && X != 4) load_res(i - 1, rs1[K & 1], rs2[K & 1]);  // residuals of row i - 1 (finished next step)
+      if (grp == 1 && X != 3 && X != 4) finish(yf, fin, own, other, rs1[(K + 1) & 1], rs2[(K + 1) & 1]);
       if (grp == 3 && X != 1 && X != 4) dma_step(i + 2, (K + 2) % 3);  // row i + 2 into the slot of row i - 1 (last read last step)
       __builtin_amdgcn_sched_barrier(0);
     }
+    R5_STAMP(4 + 3 * s);
     // row i - 1 is complete: hand the partner the two fragments it finishes
     if (i - 1 >= r0 && i - 1 < r1) {
       char* part = smem + R5_OFF_P + (K & 1) * R5_PART;
@@ -345,10 +356,11 @@ int rdb5_launch(int mode, const ClimsrConvDesc* d, const ClimsrEpilogue* ep, con
   a.rows = rows;
   a.strips = ceil_div(d->in_h, rows);
   if (dry) {
-    snprintf(name, name_len, "rdb5_kernel<%d>", mode);
+    snprintf(name, name_len, "rdb5_kernel<%d, %s>", mode, ep->res2 ? "true" : "false");
     return CLIMSR_OK;
   }
-  void (*k)(R5Args) = mode == 2 ? rdb5_kernel<2> : rdb5_kernel<1>;
+  const bool r2 = ep->res2 != nullptr;
+  void (*k)(R5Args) = mode == 2 ? (r2 ? rdb5_kernel<2, true> : rdb5_kernel<2, false>) : (r2 ? rdb5_kernel<1, true> : rdb5_kernel<1, false>);
   if (int e = lds_opt_in((const void*)k, R5_LDS_ALL)) return e;
   hipLaunchKernelGGL(k, dim3(a.tiles_x * a.strips * a.n), dim3(512), R5_LDS_ALL, s, a);
   return check_launch("conv2d_fwd (rdb5)");

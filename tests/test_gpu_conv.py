@@ -834,7 +834,7 @@ def test_rdb5_conv5_pullx_matches_fp64(n, h, w, mode, two):
     finally:
         ops.PROFILER = None
     torch.cuda.synchronize()
-    assert names and names[-1] == f"rdb5_kernel<{1 if conv5 else 2}>", names
+    assert names and names[-1] == f"rdb5_kernel<{1 if conv5 else 2}, {'true' if two else 'false'}>", names
     first = y.clone()
     p.fwd(xin, dc, 0, h, w, y, ycs, 0, n, **kw)
     torch.cuda.synchronize()

@@ -1,7 +1,7 @@
 """Where the time of one rdb5_kernel launch goes (GPU box only; the stamp build tools/diag_build of rdb_conv5.hip with
 -DCLIMSR_R5_STAMP, passed as CLIMSR_HIP_LIB): conv5 (mode 1) at the GAN step's shape (B=32, 64^2, 128 -> 64), waves 0 and
 4 of every block stamp (s_memrealtime 100 MHz, s_memtime) at kernel entry, after the prologue, and per step before the
-DMA wait, after the barrier and before the MFMAs.  Prints one JSON line of medians over blocks (us)."""
+DMA wait, after the barrier and after the MFMA groups (with the epilogue / DMA issued between them).  Prints one JSON line of medians over blocks (us)."""
 import ctypes
 import json
 import os
@@ -48,8 +48,8 @@ while 4 + 3 * s < NST - 1 and (rt[:, 0, 4 + 3 * s] > 0).all():
     a, b, c = us[:, :, 2 + 3 * s], us[:, :, 3 + 3 * s], us[:, :, 4 + 3 * s]
     nxt = us[:, :, 2 + 3 * (s + 1)] if (rt[:, 0, 2 + 3 * (s + 1)] > 0).all() and 2 + 3 * (s + 1) < NST - 1 else us[:, :, NST - 1]
     steps.append({"wait_barrier": [round(float(np.median(b[:, w] - a[:, w])), 3) for w in (0, 1)],
-                  "finalize": [round(float(np.median(c[:, w] - b[:, w])), 3) for w in (0, 1)],
-                  "mfma_part": [round(float(np.median(nxt[:, w] - c[:, w])), 3) for w in (0, 1)]})
+                  "groups": [round(float(np.median(c[:, w] - b[:, w])), 3) for w in (0, 1)],
+                  "handoff": [round(float(np.median(nxt[:, w] - c[:, w])), 3) for w in (0, 1)]})
     s += 1
 res["steps"] = steps
 dck = (ck[:, 0, NST - 1] - ck[:, 0, 0]).astype(np.float64)
