@@ -60,6 +60,9 @@ constexpr int RR_OFF_2 = RR_OFF_D + RR_N1 * RR_DROW, RR_OFF_3 = RR_OFF_2 + RR_N2
 constexpr int RR_OFF_DUMMY = RR_OFF_3 + RR_N3 * RR_DROW;  // one KB the padding DMA pieces write (zeros, never read)
 constexpr int RR_LDS = RR_OFF_DUMMY + 1024;             // 127,744 B
 constexpr int RR_K = 2;                                 // base-row DMA pieces per wave (11 real + 5 padding)
+#ifndef CLIMSR_RR_EXP  // timing experiments of diagnostic builds only: 1 no step DMA, 3 no HBM row stores, 5 no MFMAs
+#define CLIMSR_RR_EXP 0  // -- their results are wrong
+#endif
 
 __device__ __forceinline__ uint32_t pack2_bf16(float a, float b) {
   const bf16x2 v = {(__bf16)a, (__bf16)b};  // v_cvt_pk_bf16_f32 (RNE)
@@ -179,7 +182,7 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, char* smem, int ti
                                                                  ? (uint32_t)(nimg * a.h + y2) * mrow + (uint32_t)((ml + 16 * f * a.mcs) * 2)
                                                                  : BUF_OOB, 0, 0);
     }
-    dma_row(r0 - 2 + s);  // the base row level 1 ingests in step s + 2
+    if (CLIMSR_RR_EXP != 1) dma_row(r0 - 2 + s);  // the base row level 1 ingests in step s + 2
     // ingest row i.  All three kernel rows and both fragments are computed unconditionally: a target row outside this
     // level's finished range or outside the image is never finished from its accumulator (the rows a finished row
     // needs are all ingested), and the pixel slots of a fragment past the image width hold zeros
@@ -223,7 +226,9 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, char* smem, int ti
           const bf16x8 af = grp < 6 ? Ab[ky][grp >> 1][grp & 1] : Ad[ky][grp < 6 ? 0 : grp - 6];
           constexpr int SL[3] = {SN, SI, SP};
 #pragma unroll
-          for (int f = 0; f < 2; ++f) acc[SL[ky]][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, B[grp & 1][f], acc[SL[ky]][f], 0, 0, 0);
+          for (int f = 0; f < 2; ++f)
+            if (CLIMSR_RR_EXP != 5) acc[SL[ky]][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, B[grp & 1][f], acc[SL[ky]][f], 0, 0, 0);
+            else acc[SL[ky]][f] += __builtin_bit_cast(f32x4, B[grp & 1][f]);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -262,7 +267,8 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, char* smem, int ti
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
       const bool ok = own && (f == 0 ? live0 : live1);
-      __builtin_amdgcn_raw_buffer_store_b64((v2u32){pk[f].x, pk[f].y}, orr, ok ? ob + (uint32_t)(16 * f * a.ocs * 2) : BUF_OOB, 0, 0);
+      if (CLIMSR_RR_EXP != 3)
+        __builtin_amdgcn_raw_buffer_store_b64((v2u32){pk[f].x, pk[f].y}, orr, ok ? ob + (uint32_t)(16 * f * a.ocs * 2) : BUF_OOB, 0, 0);
     }
 #pragma unroll
     for (int f = 0; f < 2; ++f) acc[SP][f] = (f32x4){0.f, 0.f, 0.f, 0.f};  // becomes row i + 2's next step

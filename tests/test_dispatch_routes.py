@@ -54,10 +54,10 @@ def test_generator_forward_routes(routes):
     on load + LeakyReLU), HRconv, conv_last (64 -> 1) at B=32, 64^2 LR."""
     p5 = plan(DC, NF)
     p5.fwd(bf(), DC, 0, H, H, bf(), DC, 0, N, res1=bf(), alpha1=0.2, res1_cs=DC, res1_co=0)
-    assert last(routes) == "rdb5_kernel<1, false>"
+    assert last(routes) == "conv_fwd_kernel<4, 4, false, 4, 6, 9, 1, 1>"
     p5.fwd(bf(), DC, 0, H, H, bf(), DC, 0, N, res1=bf(), alpha1=0.2, res1_cs=DC, res1_co=0, res2=bf(), alpha2=0.2, res2_cs=DC,
            res2_co=0)
-    assert last(routes) == "rdb5_kernel<1, true>"
+    assert last(routes) == "conv_fwd_kernel<4, 4, false, 4, 6, 9, 1, 1>"
     pt = plan(NF, NF)
     pt.fwd(bf(), DC, 0, H, H, bf(), NF, 0, N, res1=bf(), alpha1=1.0, res1_cs=NF, res1_co=0)
     assert last(routes) == "conv_wr_kernel<1, 0>"
@@ -129,7 +129,7 @@ def test_rdb_pullx_route(routes):
     f32 = torch.empty(8, dtype=torch.float32)
     px.fwd(bf(), DC, 0, H, H, f32, NF, 0, N, use_bias=False, out_mode=OUT_F32, res1=f32, res1_cs=NF, res1_co=0, beta1=0.2,
            res2=f32, res2_cs=NF, res2_co=0, aux=bf(), aux_cs=DC, aux_co=4 * GC, aux_scale=0.04)
-    assert last(routes) == "rdb5_kernel<2, true>"
+    assert last(routes) == "conv_fwd_kernel<4, 4, true, 4, 6, 9, 2, 1>"
 
 
 def _wgrad_name(routes):
