@@ -16,6 +16,11 @@
 // workgroups is what held conv_pw and the generic conv).
 // Tiles: wave w of workgroup b (XCD-major renumbered) takes tiles 4 (b + k G) + w: the four waves of a CU work on four
 // horizontally adjacent tiles (shared halo columns) and consecutive workgroups of an XCD on the next ones.
+// Prologue: the 72 KB weight matrix comes into LDS once per workgroup (LDS-DMA in fragment order: one 1 KB piece per
+// A fragment, lane-contiguous, so each wave's ds_read_b128 of a fragment is conflict-free), into the regions the
+// second footprint buffers and the channel-sum transposes use later; every wave copies its registers from there.
+// Loading them straight from global memory cost each CU four copies (296 KB) of L2 traffic before its first MFMA --
+// on a small grid (RCAN's 360 x 720 LR convs: about four tiles per wave) that prologue was a third of the launch.
 #include <algorithm>
 #include <stdio.h>
 
@@ -66,14 +71,26 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int G4 = (int)gridDim.x * 4;
   int T = xcd_major(blockIdx.x, gridDim.x) * 4 + wv;
-  if (T >= a.ntiles) return;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
 
-  // ---- the weight matrix: A fragment (co block t, k block j) = rows 16 t + col, k = 32 j + 8 g ..
-  bf16x8 afb[4][18];
+  // ---- the weight matrix: A fragment f = 18 t + j (co block t, k block j) = rows 16 t + col, k = 32 j + 8 g ..,
+  // staged in LDS piece wr_piece(f) (see the file comment); wave w moves fragments 18 w .. 18 w + 17
+  auto wr_piece = [](int f) {
+    return f < 68 ? ((f / 17) * 2 + 1) * WR_BUF + (f % 17) * 1024 : WR_LDS + (f - 68) * 1024;
+  };
+  {
+    const __amdgpu_buffer_rsrc_t wrs = buf_rsrc(a.w, (uint32_t)(64 * a.kpk * 2));
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int j = 0; j < 18; ++j) afb[t][j] = *(const bf16x8*)(a.w + (long)(t * 16 + col) * a.kpk + j * 32 + g * 8);
+    for (int i = 0; i < 18; ++i) {
+      const int f = 18 * wv + i, t = f / 18, j = f % 18;
+      uint32_t keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"((uint32_t)(((t * 16 + col) * a.kpk + j * 32 + g * 8) * 2)), "s"(wrs),
+                     "s"(lds0 + (uint32_t)wr_piece(f))
+                   : "memory");
+    }
+  }
+  static_assert(WR_LDS + 4 * 1024 <= WR_LDS_ALL && 4 * 17 + 4 == 72, "conv_wr weight staging regions");
   float bias[4][4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
@@ -95,7 +112,6 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
     rel[i] = live ? (uint32_t)((((p / WR_PC) * a.in_w + p % WR_PC) * a.in_cs + c * 8) * 2) : 0x80000000u;
   }
   const __amdgpu_buffer_rsrc_t xr = buf_rsrc(a.x, a.x_bytes);
-  const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
   const uint32_t mybuf = lds0 + (uint32_t)(wv * 2 * WR_BUF);
   const int ups = a.up == 2 ? 1 : 0, lh = a.in_h << ups, lw = a.in_w << ups;
   // in asm (not the builtin): hipcc would wait vmcnt(0) before the next ds_read for an LDS write of unknown extent;
@@ -136,7 +152,20 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
   const __amdgpu_buffer_rsrc_t pr = buf_rsrc(a.ch_part, SUMS && a.ch_part ? (uint32_t)a.ntiles * 256u : 0u);
   const __amdgpu_buffer_rsrc_t rr = buf_rsrc(a.res1, (EP == 1 || EP == 2) ? a.r1_bytes : 0u);
   const int lb = col * WR_XP * 2 + g * 16;  // this lane's byte offset in a footprint row: pixel col, channels 8 g ..
-  issue(T, 0);
+  if (T < a.ntiles) issue(T, 0);
+  // the weights: this wave's 18 pieces have landed once only the footprint just requested is younger; after the
+  // barrier every wave's have, and every wave copies all 72 fragments to its registers; the second barrier retires
+  // those reads before any second footprint buffer (where the pieces lie) is written
+  if (T < a.ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WR_NI) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lds_barrier();
+  bf16x8 afb[4][18];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int j = 0; j < 18; ++j) afb[t][j] = *(const bf16x8*)(smem + wr_piece(18 * t + j) + lane * 16);
+  lds_barrier();
+  if (T >= a.ntiles) return;
   for (int it = 0;; ++it) {
     const int Tn = T + G4;
     issue(Tn < a.ntiles ? Tn : -1, (it + 1) & 1);

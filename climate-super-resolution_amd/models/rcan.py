@@ -19,7 +19,7 @@ from __future__ import annotations
 
 import logging
 import math
-from typing import Dict, List, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import torch
 import torch.nn as nn
@@ -27,7 +27,7 @@ from torch import Tensor
 
 from .. import _lib
 from .._lib import check, ptr
-from ..ops import ACT_RELU, OUT_BF16, OUT_F32, BatchedPacker, ConvPlan, nchw_to_nhwc
+from ..ops import ACT_RELU, OUT_BF16, OUT_F32, BatchedPacker, ConvPlan, SrcnnTail, nchw_to_nhwc
 from .srcnn import SRCNN
 
 
@@ -157,6 +157,13 @@ class _RcanEngine:
         self.packer = BatchedPacker(list(self.plans.values()), self.device)
         self.version = None
         self.ca_ws = None
+        # the SRCNN tail as one launch (csrc/srcnn.hip, as models/esrgan.py) where its shape is the fused kernel's
+        sc = [self.plans.get(f"srcnn.conv{i}") for i in (1, 2, 3)]
+        self.srcnn = None
+        if (all(c is not None and c.bias is not None for c in sc) and m.out_channels == 1 and sc[0].cin_real <= 4 and
+                sc[0].cout == 64 and sc[0].ks == 9 and sc[1].cout == 32 and sc[1].ks == 1 and sc[2].cout == 1 and sc[2].ks == 5 and
+                all(c.stride == 1 and c.pad == c.ks // 2 for c in sc)):
+            self.srcnn = SrcnnTail(sc, "srcnn")
 
     def _params_version(self):
         return tuple(p._version for p in self.m.parameters()) + tuple(p.data_ptr() for p in self.m.parameters())
@@ -169,6 +176,8 @@ class _RcanEngine:
                 p.bind(mod.weight, mod.bias, need_t=False)
             self.packer = BatchedPacker(list(self.plans.values()), self.device)
             self.packer.run()
+            if self.srcnn is not None:
+                self.srcnn.pack()
             self.version = v
 
     def forward(self, x: Tensor, elev: Tensor, mask: Tensor) -> Tensor:
@@ -238,18 +247,22 @@ class _RcanEngine:
             check(L.climsr_pixel_shuffle_bf16(ptr(t4), n, ch, cw, nf, r, c4, ptr(nxt), nf, st), f"pixel shuffle {name}")
             cur, ch, cw = nxt, ch * r, cw * r
         assert (ch, cw) == (hh, ww)
-        return srcnn_tail(P, "tail.1", cur, nf, n, hh, ww, m.out_channels, elev, mask)
+        return srcnn_tail(P, "tail.1", cur, nf, n, hh, ww, m.out_channels, elev, mask, self.srcnn)
 
 
 def srcnn_tail(P: Dict[str, ConvPlan], last: str, feat: Tensor, feat_cs: int, n: int, hh: int, ww: int, oc: int, elev: Tensor,
-               mask: Tensor) -> Tensor:
+               mask: Tensor, fused: Optional[SrcnnTail] = None) -> Tensor:
     """Last conv into channels [0, oc) of an 8-channel buffer, elev / mask after them (the torch.cat of rcan.py:190),
-    then SRCNN (srcnn.py:13-18) with fused ReLUs."""
+    then SRCNN (srcnn.py:13-18) with fused ReLUs: one launch (``fused``, csrc/srcnn.hip) or three convs."""
     dev = feat.device
     tail = torch.zeros((n, hh, ww, 8), dtype=torch.bfloat16, device=dev)
     P[last].fwd(feat, feat_cs, 0, hh, ww, tail, 8, 0, n)
     nchw_to_nhwc(elev.contiguous().float(), tail, 8, oc)
     nchw_to_nhwc(mask.contiguous().float(), tail, 8, oc + 1)
+    if fused is not None and oc == 1:
+        out = torch.empty((n, 1, hh, ww), dtype=torch.float32, device=dev)
+        fused.fwd(tail, 8, 0, n, hh, ww, out)
+        return out
     s1 = torch.empty((n, hh, ww, 64), dtype=torch.bfloat16, device=dev)
     P["srcnn.conv1"].fwd(tail, 8, 0, hh, ww, s1, 64, 0, n, act=ACT_RELU)
     s2 = torch.empty((n, hh, ww, 32), dtype=torch.bfloat16, device=dev)
