@@ -385,7 +385,7 @@ int conv_wr_launch(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const uint
     set_error("conv2d_fwd (wr): epilogue %d with activation %d", epk, ep->act);
     return CLIMSR_EINVAL;
   }
-  const int lds = (epk == 3 || epk == 4) ? WR_LDS_ALL : WR_LDS;
+  const int lds = WR_LDS_ALL;  // (every form: the last 4 weight pieces are staged in the channel-sum region)
   if (int e = lds_opt_in((const void*)k, WR_LDS_ALL)) return e;
   hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, s, a);
   return check_launch("conv2d_fwd (wr)");

@@ -6,7 +6,7 @@ set -o pipefail
 mkdir -p gpurun_out
 T=${1:-r05i}
 D=$PWD/climate-super-resolution_amd/csrc/diag
-timeout -k 10 900 python -u -m pytest tests/test_gpu_conv.py tests/test_gpu_rcan.py tests/test_gpu_configs.py tests/test_gpu_gan.py -q --timeout 120 --timeout-method thread > gpurun_out/${T}_tests.log 2>&1 || exit $?
+timeout -k 10 900 python -u -m pytest tests/test_gpu_conv.py tests/test_gpu_rcan.py tests/test_gpu_configs.py tests/test_gpu_gan.py -x -q --timeout 120 --timeout-method thread > gpurun_out/${T}_tests.log 2>&1 || exit $?
 timeout -k 10 240 python -u tools/det_check.py new > gpurun_out/${T}_det.jsonl 2> gpurun_out/${T}_det.err || exit $?
 for i in 1 2; do
   timeout -k 10 120 python -u tools/perf_wr.py new >> gpurun_out/${T}_wr.jsonl 2>> gpurun_out/${T}_wr.err || exit $?
