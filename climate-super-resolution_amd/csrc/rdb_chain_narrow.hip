@@ -43,6 +43,7 @@ struct ChainArgs {
   uint32_t base_bytes, mask_bytes, out_bytes;
 };
 typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 
 // 32-channel blocks of a level's packed K row (KP = 64 + 16 (L - 1) rounded up to 32)
 __host__ __device__ constexpr int kp_blocks(int L) { return L == 1 ? 2 : (L == 4 ? 4 : 3); }
@@ -147,16 +148,21 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, char* smem, int ti
   // per-lane LDS offsets: base pixel slot col (+ 16 f + kx), chunk 4 cb + g; dense pixel slot col (+ ...), chunk g & 1
   const int lb = col * RR_BP + g * 16;
   const int ldn = col * RR_DP + (g & 1) * 16;
-  // completed-row epilogue: ring store of this lane's 4 channels (slot 1 + col of fragment f) and the HBM row store
-  const int dl = (1 + 32 * fp + col) * RR_DP + g * 8;
-  const int ol = (32 * fp + col) * a.ocs + a.ooff[L - 1] + 4 * g;
+  // completed-row epilogue, after the fragment halves are traded between lane rows g and g ^ 1 (v_permlane16_swap):
+  // lane (col, g) holds channels 8 (g >> 1) .. + 7 of fragment g & 1's pixel col -- one 16-B ring store (slot 1 + the
+  // pixel) and one 16-B HBM row store
+  const int fq = g & 1;
+  const bool liveq = fq == 0 ? live0 : live1;
+  const int dl = (1 + 32 * fp + 16 * fq + col) * RR_DP + (g >> 1) * 16;
+  const int ol = (32 * fp + 16 * fq + col) * a.ocs + a.ooff[L - 1] + 8 * (g >> 1);
   const int ml = (32 * fp + col) * a.mcs + a.moff[L - 1] + 4 * g;
   const uint32_t orow = (uint32_t)a.w * (uint32_t)a.ocs * 2u, mrow = (uint32_t)a.w * (uint32_t)a.mcs * 2u;
 
   // Per step every wave issues, in this order: RL mask loads (pull: the activation of the row it finishes two steps
-  // later), RR_K DMA pieces (the base row level 1 ingests two steps later), 2 row stores (raw, unconditional).  Step s
-  // needs the DMA of step s - 2; younger are step s - 2's stores and step s - 1's operations.
-  constexpr int RL = MODE == 1 ? 2 : 0, NW = 2 + RL + RR_K + 2;
+  // later), RR_K DMA pieces (the base row level 1 ingests two steps later) and, on the steps that finish one of the
+  // strip's own rows, one row store.  Step s needs the DMA of step s - 2; younger are step s - 2's store and step
+  // s - 1's operations: at least RL + RR_K of them (a step without a store), so that is what the wait leaves.
+  constexpr int RL = MODE == 1 ? 2 : 0, NW = RL + RR_K;
   f32x4 acc[3][2];  // accumulator row of output row y: (y - r0) mod 3 (phase-resolved at compile time)
 #pragma unroll
   for (int r = 0; r < 3; ++r) acc[r][0] = acc[r][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -254,22 +260,20 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, char* smem, int ti
       }
       pk[f] = yin ? make_uint2(pack2_bf16(v[0], v[1]), pack2_bf16(v[2], v[3])) : make_uint2(0u, 0u);
     }
+    // rows 1, 3 of fragment 0 <-> rows 0, 2 of fragment 1 (the packed channel pairs move whole)
+    const auto sx = __builtin_amdgcn_permlane16_swap(pk[0].x, pk[1].x, false, false);
+    const auto sy = __builtin_amdgcn_permlane16_swap(pk[0].y, pk[1].y, false, false);
+    const uint4 o8 = make_uint4(sx[0], sy[0], sx[1], sy[1]);
     if constexpr (L < 4) {
       if (fin) {
         char* ring = smem + (L == 1 ? RR_OFF_D + ((y - r0 + 3) % RR_N1) * RR_DROW
                                     : (L == 2 ? RR_OFF_2 + ((y - r0 + 2) % RR_N2) * RR_DROW : RR_OFF_3 + ((y - r0 + 1) % RR_N3) * RR_DROW));
-        if (live0) *(uint2*)(ring + dl) = pk[0];
-        if (live1) *(uint2*)(ring + dl + 16 * RR_DP) = pk[1];
+        if (liveq) *(uint4*)(ring + dl) = o8;
       }
     }
-    const bool own = fin && yin && y >= r0 && y < r1;
-    const uint32_t ob = own ? (uint32_t)(nimg * a.h + y) * orow + (uint32_t)(ol * 2) : 0u;
-#pragma unroll
-    for (int f = 0; f < 2; ++f) {
-      const bool ok = own && (f == 0 ? live0 : live1);
-      if (CLIMSR_RR_EXP != 3)
-        __builtin_amdgcn_raw_buffer_store_b64((v2u32){pk[f].x, pk[f].y}, orr, ok ? ob + (uint32_t)(16 * f * a.ocs * 2) : BUF_OOB, 0, 0);
-    }
+    if (fin && yin && y >= r0 && y < r1 && CLIMSR_RR_EXP != 3)  // (wave-uniform) one of the strip's own rows
+      __builtin_amdgcn_raw_buffer_store_b128((v4u32){o8.x, o8.y, o8.z, o8.w}, orr,
+                                             liveq ? (uint32_t)(nimg * a.h + y) * orow + (uint32_t)(ol * 2) : BUF_OOB, 0, 0);
 #pragma unroll
     for (int f = 0; f < 2; ++f) acc[SP][f] = (f32x4){0.f, 0.f, 0.f, 0.f};  // becomes row i + 2's next step
   };
