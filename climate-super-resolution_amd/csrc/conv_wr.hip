@@ -65,7 +65,8 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // vector-memory operations of one epilogue (loads + stores), fixed per lane
   // EP 5: EP 0 followed by the 2x2 max pool (VGG19 conv1_2 + MaxPool2d, perceptual.py:16): 8 stores a lane
-  constexpr int NEPI = EP == 0 ? 16 : (EP == 5 ? 8 : (EP == 3 || EP == 4 ? 17 : 32));
+  // bf16 outputs leave as 16-B stores, two per output row m (see the epilogue): EP 0 8, EP 4 8 + 1, EP 1 / 2 16 + 8
+  constexpr int NEPI = EP == 0 ? 8 : (EP == 5 ? 8 : (EP == 3 ? 17 : (EP == 4 ? 9 : 24)));
   constexpr bool SUMS = EP == 3 || EP == 4;  // per-tile channel sums (EP 3: fp32 out, EP 4: bf16 out)
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, col = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -236,12 +237,15 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
     }
     uint32_t off[4];
     uint2 rv[4][4];
+    v2u32 pkm[4];  // bf16 forms: this row's four packed 4-channel groups (co blocks t)
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
       const int oy = oy0 + m;
       const bool ok = oy < a.out_h && ox < a.out_w;
       const long pix = ((long)nimg * a.out_h + oy) * a.out_w + ox;
-      off[m] = ok ? (uint32_t)((pix * a.out_cs + a.out_co + 4 * g) * (EP == 3 ? 4 : 2)) : BUF_OOB;
+      // fp32 (EP 3): channels 16 t + 4 g ..; bf16: the 8 channels 16 (t0 + (g & 1)) + 8 (g >> 1) .. of co-block pair t0
+      off[m] = ok ? (uint32_t)((pix * a.out_cs + a.out_co + (EP == 3 ? 4 * g : 16 * (g & 1) + 8 * (g >> 1))) * (EP == 3 ? 4 : 2))
+                  : BUF_OOB;
       if constexpr (EP == 1 || EP == 2) {
         const uint32_t ro = ok ? (uint32_t)((pix * a.r1_cs + a.r1_co + 4 * g) * 2) : BUF_OOB;
 #pragma unroll
@@ -284,11 +288,18 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
           }
         } else {
           const bf16x2 p0 = {(__bf16)v[0], (__bf16)v[1]}, p1 = {(__bf16)v[2], (__bf16)v[3]};
-          const v2u32 pk = {__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1)};
-          __builtin_amdgcn_raw_buffer_store_b64(pk, yr, off[m] == BUF_OOB ? BUF_OOB : off[m] + (uint32_t)(t * 32), 0, 0);
+          pkm[t] = (v2u32){__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1)};
           if (EP == 4 && off[m] != BUF_OOB) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) csum[t][i] += v[i];
+          }
+          if (t & 1) {
+            // co blocks t - 1, t: rows 1, 3 of block t - 1 <-> rows 0, 2 of block t (v_permlane16_swap), so lane (col, g)
+            // holds channels 16 (t - 1 + (g & 1)) + 8 (g >> 1) .. + 7 of pixel (m, col): one 16-B store
+            const auto sx = __builtin_amdgcn_permlane16_swap(pkm[t - 1][0], pkm[t][0], false, false);
+            const auto sy = __builtin_amdgcn_permlane16_swap(pkm[t - 1][1], pkm[t][1], false, false);
+            const v4u32 o = {sx[0], sy[0], sx[1], sy[1]};
+            __builtin_amdgcn_raw_buffer_store_b128(o, yr, off[m] == BUF_OOB ? BUF_OOB : off[m] + (uint32_t)((t - 1) * 32), 0, 0);
           }
         }
       }
