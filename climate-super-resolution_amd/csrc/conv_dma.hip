@@ -123,7 +123,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
   // perceptual.py:16): a wave's 4 rows pool to 2 in registers, column pairs across lanes col / col ^ 1, even lanes store
   constexpr bool POOL = EP == 11;
   constexpr bool DIRECT = EP == 3 || EP == 6 || EP == 8 || POOL;
-  constexpr int NST_ITEM = POOL ? 8 : DIRECT ? 16 : 2 * DmaEp<CNT ? EP : 8>::NSTORE;
+  constexpr int NST_ITEM = POOL ? 8 : DIRECT ? 8 : 2 * DmaEp<CNT ? EP : 8>::NSTORE;  // (direct: 16-B stores, below)
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
   const int wvu = __builtin_amdgcn_readfirstlane(wave);
   const int ntile = a.tiles_x * a.tiles_y * a.n, ncob = (a.out_c + 63) / 64;  // = the host's packed-row blocks
@@ -322,7 +322,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
       return;
     } else if (DIRECT) {
       // lane (col, g) holds channels co0 + 16 t + 4 g .. + 3 of pixel (oy0 + 4 wave + m, ox0 + col): bias / activation,
-      // bf16, one 8 B store per (m, t) -- 16 per lane per item, issued unconditionally (out-of-range offsets drop)
+      // bf16, one 16 B store per (m, co-block pair) -- 8 per lane per item, issued unconditionally (out-of-range offsets drop)
       const long ypx = POOL ? (long)a.n * (a.out_h >> 1) * (a.out_w >> 1) : (long)a.n * a.out_h * a.out_w;
       const __amdgpu_buffer_rsrc_t ry = buf_rsrc(a.y, (uint32_t)(ypx * a.out_cs * 2));
       float bb[4][4];
@@ -368,16 +368,25 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
           const int oy = oy0 + wave * 4 + m;
           const bool ok = oy < a.out_h && ox < a.out_w;
           const long pix = ((long)nimg * a.out_h + oy) * a.out_w + ox;
+          uint32_t pk[4][2];
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
             float v[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) v[i] = act_apply(acc[m][t][i] + bb[t][i], ACT, a.slope);
             const bf16x2 p0 = {(__bf16)v[0], (__bf16)v[1]}, p1 = {(__bf16)v[2], (__bf16)v[3]};
-            typedef uint32_t v2u32_t __attribute__((ext_vector_type(2)));
-            const v2u32_t pk = {__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1)};
-            const uint32_t off = ok ? (uint32_t)((pix * a.out_cs + a.out_co + co0 + 16 * t + 4 * g) * 2) : BUF_OOB;
-            __builtin_amdgcn_raw_buffer_store_b64(pk, ry, off, 0, 0);
+            pk[t][0] = __builtin_bit_cast(uint32_t, p0);
+            pk[t][1] = __builtin_bit_cast(uint32_t, p1);
+            if (t & 1) {
+              // co blocks t - 1, t: rows 1, 3 of block t - 1 <-> rows 0, 2 of block t (v_permlane16_swap): lane (col, g)
+              // then holds channels 16 (t - 1 + (g & 1)) + 8 (g >> 1) .. + 7 of its pixel, one 16-B store
+              const auto sx = __builtin_amdgcn_permlane16_swap(pk[t - 1][0], pk[t][0], false, false);
+              const auto sy = __builtin_amdgcn_permlane16_swap(pk[t - 1][1], pk[t][1], false, false);
+              typedef uint32_t v4u32_t __attribute__((ext_vector_type(4)));
+              const v4u32_t o = {sx[0], sy[0], sx[1], sy[1]};
+              const uint32_t off = ok ? (uint32_t)((pix * a.out_cs + a.out_co + co0 + 16 * (t - 1 + (g & 1)) + 8 * (g >> 1)) * 2) : BUF_OOB;
+              __builtin_amdgcn_raw_buffer_store_b128(o, ry, off, 0, 0);
+            }
           }
         }
       };
