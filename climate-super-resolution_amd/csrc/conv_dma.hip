@@ -539,19 +539,19 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_s2_dma_kernel(FwdArgs a) {
       for (int t = 0; t < 4; ++t) acc[m][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
     for (int c = 0; c < nch; ++c, cur = cur == 2 ? 0 : cur + 1) {
       // chunk c has landed once at most the younger requests are outstanding: the next chunk's pieces, and at chunks
-      // 0 / 1 of a later item also the previous item's 8 epilogue stores (issued between them)
+      // 0 / 1 of a later item also the previous item's 4 epilogue stores (issued between them)
       const bool st = c < 2 && v != (int)blockIdx.x;
       if (!pm) {  // the last chunks of the last item: nothing was requested behind this chunk (at most the stores)
-        if (st) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        if (st) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       } else if (npc == 8) {
-        if (st) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        if (st) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       } else if (npc == 7) {
-        if (st) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+        if (st) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
       } else {
-        if (st) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+        if (st) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       }
       lds_barrier();
@@ -597,7 +597,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_s2_dma_kernel(FwdArgs a) {
       pm = more;
     }
     // ---- epilogue straight from the accumulators: lane (col, g) holds channels co0 + 16 t + 4 g .. + 3 of output pixel
-    // (oy0 + 2 wave + m, ox0 + col); 8 stores per lane, issued unconditionally
+    // (oy0 + 2 wave + m, ox0 + col); co-block pairs traded between lane rows (v_permlane16_swap) -> 4 16-B stores per
+    // lane, issued unconditionally
     const __amdgpu_buffer_rsrc_t ry = buf_rsrc(a.y, (uint32_t)((long)a.n * a.out_h * a.out_w * a.out_cs * 2));
     const int ox = ox0 + col;
     float ss[4][4] = {}, sq[4][4] = {};
@@ -606,13 +607,20 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_s2_dma_kernel(FwdArgs a) {
       const int oy = oy0 + 2 * wave + m;
       const bool ok = oy < a.out_h && ox < a.out_w;
       const long pix = ((long)nimg * a.out_h + oy) * a.out_w + ox;
+      uint32_t pk[4][2];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const bf16x2 p0 = {(__bf16)acc[m][t][0], (__bf16)acc[m][t][1]}, p1 = {(__bf16)acc[m][t][2], (__bf16)acc[m][t][3]};
-        typedef uint32_t v2u32_t __attribute__((ext_vector_type(2)));
-        const v2u32_t pk = {__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1)};
-        __builtin_amdgcn_raw_buffer_store_b64(pk, ry, ok ? (uint32_t)((pix * a.out_cs + a.out_co + co0 + 16 * t + 4 * g) * 2) : BUF_OOB,
-                                              0, 0);
+        pk[t][0] = __builtin_bit_cast(uint32_t, p0);
+        pk[t][1] = __builtin_bit_cast(uint32_t, p1);
+        if (t & 1) {  // lane (col, g): channels co0 + 16 (t - 1 + (g & 1)) + 8 (g >> 1) .. + 7 after the trade
+          const auto sx = __builtin_amdgcn_permlane16_swap(pk[t - 1][0], pk[t][0], false, false);
+          const auto sy = __builtin_amdgcn_permlane16_swap(pk[t - 1][1], pk[t][1], false, false);
+          typedef uint32_t v4u32_t __attribute__((ext_vector_type(4)));
+          const v4u32_t o = {sx[0], sy[0], sx[1], sy[1]};
+          __builtin_amdgcn_raw_buffer_store_b128(
+              o, ry, ok ? (uint32_t)((pix * a.out_cs + a.out_co + co0 + 16 * (t - 1 + (g & 1)) + 8 * (g >> 1)) * 2) : BUF_OOB, 0, 0);
+        }
         if (STATS && ok) {
           const float r[4] = {(float)p0[0], (float)p0[1], (float)p1[0], (float)p1[1]};
 #pragma unroll

@@ -208,11 +208,19 @@ __global__ __launch_bounds__(512, 1) void stem_s2_kernel(StemArgs a) {
       const int oy = oy0 + 2 * wave + m;
       const bool ok = oy < a.oh && ox < a.ow;
       const long pix = ((long)nimg * a.oh + oy) * a.ow + ox;
+      uint32_t pk[4][2];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const bf16x2 p0 = {(__bf16)acc[m][t][0], (__bf16)acc[m][t][1]}, p1 = {(__bf16)acc[m][t][2], (__bf16)acc[m][t][3]};
-        const v2u32 pk = {__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1)};
-        __builtin_amdgcn_raw_buffer_store_b64(pk, zr, ok ? (uint32_t)((pix * 64 + 16 * t + 4 * g) * 2) : BUF_OOB, 0, 0);
+        pk[t][0] = __builtin_bit_cast(uint32_t, p0);
+        pk[t][1] = __builtin_bit_cast(uint32_t, p1);
+        if (t & 1) {  // co-block pair traded between lane rows (v_permlane16_swap): channels 16 (t - 1 + (g & 1)) + 8 (g >> 1) ..
+          const auto sx = __builtin_amdgcn_permlane16_swap(pk[t - 1][0], pk[t][0], false, false);
+          const auto sy = __builtin_amdgcn_permlane16_swap(pk[t - 1][1], pk[t][1], false, false);
+          typedef uint32_t v4u32_t __attribute__((ext_vector_type(4)));
+          const v4u32_t o = {sx[0], sy[0], sx[1], sy[1]};
+          __builtin_amdgcn_raw_buffer_store_b128(o, zr, ok ? (uint32_t)((pix * 64 + 16 * (t - 1 + (g & 1)) + 8 * (g >> 1)) * 2) : BUF_OOB, 0, 0);
+        }
         if (STATS && ok) {
           const float r[4] = {(float)p0[0], (float)p0[1], (float)p1[0], (float)p1[1]};
 #pragma unroll
