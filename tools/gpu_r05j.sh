@@ -1,4 +1,5 @@
-# Round 5, call j: conv_wr's bf16 epilogue as 16-B stores and the RDB chain with 16-B epilogue stores (fragment halves traded by v_permlane16_swap, HBM row stores
+# Round 5, call j: 16-B epilogue stores (v_permlane16_swap) in conv_wr, the LDS-DMA convs (stride 1 / 2), the D stem
+# and the RDB chain (fragment halves traded by v_permlane16_swap, HBM row stores
 # only on the strip's own rows): determinism, the conv / GAN / bench-shape suites, timing vs the previous chain, GAN
 # step (alternating).   usage: bash tools/gpu_r05j.sh <tag>
 set -o pipefail
@@ -12,6 +13,8 @@ for i in 1 2; do
   CLIMSR_HIP_LIB=$D/chainprev/libclimsr_hip.so timeout -k 10 120 python -u tools/perf_diag.py chainprev >> gpurun_out/${T}_diag.jsonl 2>> gpurun_out/${T}_diag.err || exit $?
   timeout -k 10 120 python -u tools/perf_wr.py new >> gpurun_out/${T}_wr.jsonl 2>> gpurun_out/${T}_wr.err || exit $?
   CLIMSR_HIP_LIB=$D/chainprev/libclimsr_hip.so timeout -k 10 120 python -u tools/perf_wr.py prev >> gpurun_out/${T}_wr.jsonl 2>> gpurun_out/${T}_wr.err || exit $?
+  timeout -k 10 120 python -u tools/perf_s2.py new >> gpurun_out/${T}_s2.jsonl 2>> gpurun_out/${T}_s2.err || exit $?
+  CLIMSR_HIP_LIB=$D/chainprev/libclimsr_hip.so timeout -k 10 120 python -u tools/perf_s2.py prev >> gpurun_out/${T}_s2.jsonl 2>> gpurun_out/${T}_s2.err || exit $?
 done
 for i in 1 2; do
   timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-config2 --steps 20 --warmup 5 > gpurun_out/${T}_bench_new_$i.json 2> gpurun_out/${T}_bench_new_$i.err || exit $?
