@@ -25,6 +25,8 @@ for mode in gan esrgan rcan; do
   python3 tools/prof_record.py gpurun_out/${T}_${M}_s gpurun_out/${T}_${M}_kernel_stats.csv "$S" || exit $?
   rm -rf gpurun_out/${T}_${M}_f gpurun_out/${T}_${M}_w gpurun_out/${T}_${M}_s
 done
+bash tools/gpu_sq.sh ${T}_gan_sq > gpurun_out/${T}_gan_sq.log 2>&1 || exit $?
+rm -rf gpurun_out/${T}_gan_sq1 gpurun_out/${T}_gan_sq2
 timeout -k 10 400 python3 -u bench.py > gpurun_out/${T}_gan_bench.json 2> gpurun_out/${T}_gan_bench.err || exit $?
 timeout -k 10 300 python3 -u bench.py --mode infer --model rcan > gpurun_out/${T}_infer_rcan_bench.json 2> gpurun_out/${T}_infer_rcan_bench.err || exit $?
 timeout -k 10 300 python3 -u bench.py --mode infer --model esrgan > gpurun_out/${T}_infer_esrgan_bench.json 2> gpurun_out/${T}_infer_esrgan_bench.err || exit $?
