@@ -140,10 +140,10 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, char* smem, int ti
       }
     }
   }
-  float bb[4] = {0.f, 0.f, 0.f, 0.f};
+  float bb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // channels 8 (g >> 1) .. + 7 (the epilogue's traded layout)
   if constexpr (MODE == 0) {
-    const float4 b4 = *(const float4*)(a.bias[L - 1] + 4 * g);
-    bb[0] = b4.x; bb[1] = b4.y; bb[2] = b4.z; bb[3] = b4.w;
+    const float4 b0 = *(const float4*)(a.bias[L - 1] + 8 * (g >> 1)), b1 = *(const float4*)(a.bias[L - 1] + 8 * (g >> 1) + 4);
+    bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w; bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
   }
   // per-lane LDS offsets: base pixel slot col (+ 16 f + kx), chunk 4 cb + g; dense pixel slot col (+ ...), chunk g & 1
   const int lb = col * RR_BP + g * 16;
@@ -155,18 +155,19 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, char* smem, int ti
   const bool liveq = fq == 0 ? live0 : live1;
   const int dl = (1 + 32 * fp + 16 * fq + col) * RR_DP + (g >> 1) * 16;
   const int ol = (32 * fp + 16 * fq + col) * a.ocs + a.ooff[L - 1] + 8 * (g >> 1);
-  const int ml = (32 * fp + col) * a.mcs + a.moff[L - 1] + 4 * g;
+  const int ml = (32 * fp + 16 * fq + col) * a.mcs + a.moff[L - 1] + 8 * (g >> 1);  // (the traded layout, as ol)
   const uint32_t orow = (uint32_t)a.w * (uint32_t)a.ocs * 2u, mrow = (uint32_t)a.w * (uint32_t)a.mcs * 2u;
 
-  // Per step every wave issues, in this order: RL mask loads (pull: the activation of the row it finishes two steps
-  // later), RR_K DMA pieces (the base row level 1 ingests two steps later) and, on the steps that finish one of the
-  // strip's own rows, one row store.  Step s needs the DMA of step s - 2; younger are step s - 2's store and step
-  // s - 1's operations: at least RL + RR_K of them (a step without a store), so that is what the wait leaves.
-  constexpr int RL = MODE == 1 ? 2 : 0, NW = RL + RR_K;
+  // Per step every wave issues, in this order: the pull's mask load (the activation of the row it finishes two steps
+  // later, when that row is one the level finishes), RR_K DMA pieces (the base row level 1 ingests two steps later)
+  // and, on the steps that finish one of the strip's own rows, one row store.  Step s needs the DMA of step s - 2;
+  // younger are step s - 2's store and step s - 1's operations: at least RR_K of them, so that is what the wait leaves.
+  constexpr int NW = RR_K;
   f32x4 acc[3][2];  // accumulator row of output row y: (y - r0) mod 3 (phase-resolved at compile time)
 #pragma unroll
   for (int r = 0; r < 3; ++r) acc[r][0] = acc[r][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  v2u32 msk[3][2];  // pull: the stored activation of the row finished in step s, loaded in step s - 2 (set s mod 3)
+  v4u32 msk[3];  // pull: this lane's 8 channels of the stored activation of the row finished in step s, loaded in
+                 // step s - 2 (set s mod 3; traded layout)
   // rows of this level: ingested [r0 - 5 + L, r1 + 4 - L], finished [r0 - 4 + L, r1 + 4 - L)
   const int ilo = r0 - 5 + L, ihi = r1 + 4 - L, clo = r0 - 4 + L, chi = r1 + 4 - L;
   const int nsteps = r1 - r0 + 11;
@@ -181,12 +182,9 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, char* smem, int ti
     lds_barrier();
     if constexpr (MODE == 1) {  // the activation of row i + 1 (finished two steps later)
       const int y2 = i + 1;
-      const bool ok2 = y2 >= clo && y2 < chi && y2 >= 0 && y2 < a.h;
-#pragma unroll
-      for (int f = 0; f < 2; ++f)
-        msk[K][f] = __builtin_amdgcn_raw_buffer_load_b64(mr, ok2 && (f == 0 ? live0 : live1)
-                                                                 ? (uint32_t)(nimg * a.h + y2) * mrow + (uint32_t)((ml + 16 * f * a.mcs) * 2)
-                                                                 : BUF_OOB, 0, 0);
+      if (y2 >= clo && y2 < chi && y2 >= 0 && y2 < a.h)  // (wave-uniform)
+        msk[K] = __builtin_bit_cast(v4u32, __builtin_amdgcn_raw_buffer_load_b128(
+                                               mr, liveq ? (uint32_t)(nimg * a.h + y2) * mrow + (uint32_t)(ml * 2) : BUF_OOB, 0, 0));
     }
     if (CLIMSR_RR_EXP != 1) dma_row(r0 - 2 + s);  // the base row level 1 ingests in step s + 2
     // ingest row i.  All three kernel rows and both fragments are computed unconditionally: a target row outside this
@@ -243,27 +241,29 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, char* smem, int ti
     // and the strip's own rows to HBM (2 raw stores, unconditional; an out-of-range offset drops them)
     const int y = i - 1;
     const bool fin = y >= clo && y < chi, yin = y >= 0 && y < a.h;
-    uint2 pk[2];
+    // rows 1, 3 of fragment 0 <-> rows 0, 2 of fragment 1 (v_permlane16_swap on the fp32 sums): lane (col, g) then holds
+    // channels 8 (g >> 1) .. + 7 of fragment g & 1's pixel col
+    float t8[8];
 #pragma unroll
-    for (int f = 0; f < 2; ++f) {
-      float v[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float t = acc[SP][f][e] + bb[e];
-        if (MODE == 0) {
-          v[e] = fmaxf(t, t * a.slope);  // leaky relu, 0 <= slope <= 1 (checked on the host)
-        } else {
-          const uint32_t mw = e < 2 ? msk[(K + 1) % 3][f][0] : msk[(K + 1) % 3][f][1];
-          const float mv = __uint_as_float((e & 1) ? (mw & 0xFFFF0000u) : (mw << 16));
-          v[e] = mv > 0.f ? t : t * a.slope;
-        }
-      }
-      pk[f] = yin ? make_uint2(pack2_bf16(v[0], v[1]), pack2_bf16(v[2], v[3])) : make_uint2(0u, 0u);
+    for (int e = 0; e < 4; ++e) {
+      const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[SP][0][e]), __float_as_uint(acc[SP][1][e]), false, false);
+      t8[e] = __uint_as_float(sw[0]);
+      t8[4 + e] = __uint_as_float(sw[1]);
     }
-    // rows 1, 3 of fragment 0 <-> rows 0, 2 of fragment 1 (the packed channel pairs move whole)
-    const auto sx = __builtin_amdgcn_permlane16_swap(pk[0].x, pk[1].x, false, false);
-    const auto sy = __builtin_amdgcn_permlane16_swap(pk[0].y, pk[1].y, false, false);
-    const uint4 o8 = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float t = t8[e] + bb[e];
+      if (MODE == 0) {
+        v[e] = fmaxf(t, t * a.slope);  // leaky relu, 0 <= slope <= 1 (checked on the host)
+      } else {
+        const uint32_t mw = msk[(K + 1) % 3][e >> 1];
+        const float mv = __uint_as_float((e & 1) ? (mw & 0xFFFF0000u) : (mw << 16));
+        v[e] = mv > 0.f ? t : t * a.slope;
+      }
+    }
+    const uint4 o8 = yin ? make_uint4(pack2_bf16(v[0], v[1]), pack2_bf16(v[2], v[3]), pack2_bf16(v[4], v[5]), pack2_bf16(v[6], v[7]))
+                         : make_uint4(0u, 0u, 0u, 0u);
     if constexpr (L < 4) {
       if (fin) {
         char* ring = smem + (L == 1 ? RR_OFF_D + ((y - r0 + 3) % RR_N1) * RR_DROW
