@@ -484,7 +484,11 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_s2_dma_kernel(FwdArgs a) {
   auto offsets = [&](int nimg, int oy0, int ox0, int co0) {
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
-      const int u = (wave + 8 * j) * 64 + lane, p = u >> 1, h = u & 1, r = p / S2D_TP, c = p - r * S2D_TP;
+      // slot sl of a footprint row holds column 2 sl (sl < 17) or 2 (sl - 17) + 1: the even columns first, then the
+      // odd ones, so a stride-2 fragment read (columns 2 col + kx) hits consecutive slots -- conflict-free b128 reads
+      // (in column order the 16 lanes of a bank group covered half of the banks twice)
+      const int u = (wave + 8 * j) * 64 + lane, p = u >> 1, h = u & 1, r = p / S2D_TP, sl = p - r * S2D_TP;
+      const int c = sl < 17 ? 2 * sl : 2 * (sl - 17) + 1;
       const int iy = 2 * oy0 - 1 + r, ix = 2 * ox0 - 1 + c;
       const bool ok = p < S2D_TP * S2D_TP && iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w;
       xo[j] = ok ? (uint32_t)((((nimg * a.in_h + iy) * a.in_w + ix) * a.in_cs + a.in_co + 8 * h) * 2) : BUF_OOB;
@@ -577,7 +581,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_s2_dma_kernel(FwdArgs a) {
         }
 #pragma unroll
         for (int m = 0; m < 2; ++m)
-          bq[s][m] = *(const bf16x8*)(xb + ((2 * (2 * wave + m) + ky) * S2D_TP + 2 * col + kx) * 32 + 16 * hh);
+          bq[s][m] = *(const bf16x8*)(xb + ((2 * (2 * wave + m) + ky) * S2D_TP + col + (kx == 1 ? 17 : kx >> 1)) * 32 + 16 * hh);
       };
       ld(0, 0);
 #pragma unroll
