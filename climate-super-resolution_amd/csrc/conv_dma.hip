@@ -123,7 +123,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
   // perceptual.py:16): a wave's 4 rows pool to 2 in registers, column pairs across lanes col / col ^ 1, even lanes store
   constexpr bool POOL = EP == 11;
   constexpr bool DIRECT = EP == 3 || EP == 6 || EP == 8 || POOL;
-  constexpr int NST_ITEM = POOL ? 8 : DIRECT ? 8 : 2 * DmaEp<CNT ? EP : 8>::NSTORE;  // (direct: 16-B stores, below)
+  constexpr int NST_ITEM = POOL ? 4 : DIRECT ? 8 : 2 * DmaEp<CNT ? EP : 8>::NSTORE;  // (direct: 16-B stores, below)
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
   const int wvu = __builtin_amdgcn_readfirstlane(wave);
   const int ntile = a.tiles_x * a.tiles_y * a.n, ncob = (a.out_c + 63) / 64;  // = the host's packed-row blocks
@@ -337,27 +337,33 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
       auto store_all = [&](auto actc) {
         constexpr int ACT = decltype(actc)::value;
         if constexpr (POOL) {
-          // pooled output pixel (oy0 / 2 + 2 wave + mp, (ox0 + col) / 2), stored by the even-column lanes (8 per lane)
-          const int ph = a.out_h >> 1, pw = a.out_w >> 1, px = (ox0 + col) >> 1;
+          // pooled output pixel (oy0 / 2 + 2 wave + mp, (ox0 + col) / 2), held by lanes col and col ^ 1 alike: of each
+          // co-block pair (t, t + 1) the even lane stores block t and the odd lane block t + 1 (4 stores per lane)
+          const int ph = a.out_h >> 1, pw = a.out_w >> 1, px = (ox0 + col) >> 1, odd = col & 1;
 #pragma unroll
           for (int mp = 0; mp < 2; ++mp) {
             const int py = (oy0 >> 1) + 2 * wave + mp;
-            const bool ok = (col & 1) == 0 && py < ph && px < pw;
+            const bool ok = py < ph && px < pw;
             const long pix = ((long)nimg * ph + py) * pw + px;
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
-              float v[4];
+            for (int tp = 0; tp < 4; tp += 2) {
+              float w[4];  // block tp + odd: both blocks' maxima are formed (the xor shuffle needs every lane), one kept
 #pragma unroll
               for (int i = 0; i < 4; ++i) {
-                const float r0 = act_apply(acc[2 * mp][t][i] + bb[t][i], ACT, a.slope);
-                const float r1 = act_apply(acc[2 * mp + 1][t][i] + bb[t][i], ACT, a.slope);
-                const float rm = fmaxf(r0, r1);
-                v[i] = fmaxf(rm, __shfl_xor(rm, 1));
+                float m2[2];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                  const float r0 = act_apply(acc[2 * mp][tp + u][i] + bb[tp + u][i], ACT, a.slope);
+                  const float r1 = act_apply(acc[2 * mp + 1][tp + u][i] + bb[tp + u][i], ACT, a.slope);
+                  const float rm = fmaxf(r0, r1);
+                  m2[u] = fmaxf(rm, __shfl_xor(rm, 1));
+                }
+                w[i] = odd ? m2[1] : m2[0];
               }
-              const bf16x2 p0 = {(__bf16)v[0], (__bf16)v[1]}, p1 = {(__bf16)v[2], (__bf16)v[3]};
+              const bf16x2 p0 = {(__bf16)w[0], (__bf16)w[1]}, p1 = {(__bf16)w[2], (__bf16)w[3]};
               typedef uint32_t v2u32_t __attribute__((ext_vector_type(2)));
               const v2u32_t pk = {__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1)};
-              const uint32_t off = ok ? (uint32_t)((pix * a.out_cs + a.out_co + co0 + 16 * t + 4 * g) * 2) : BUF_OOB;
+              const uint32_t off = ok ? (uint32_t)((pix * a.out_cs + a.out_co + co0 + 16 * (tp + odd) + 4 * g) * 2) : BUF_OOB;
               __builtin_amdgcn_raw_buffer_store_b64(pk, ry, off, 0, 0);
             }
           }

@@ -64,9 +64,9 @@ template <int EP, int ACT>
 __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // vector-memory operations of one epilogue (loads + stores), fixed per lane
-  // EP 5: EP 0 followed by the 2x2 max pool (VGG19 conv1_2 + MaxPool2d, perceptual.py:16): 8 stores a lane
+  // EP 5: EP 0 followed by the 2x2 max pool (VGG19 conv1_2 + MaxPool2d, perceptual.py:16): 4 stores a lane
   // bf16 outputs leave as 16-B stores, two per output row m (see the epilogue): EP 0 8, EP 4 8 + 1, EP 1 / 2 16 + 8
-  constexpr int NEPI = EP == 0 ? 8 : (EP == 5 ? 8 : (EP == 3 ? 17 : (EP == 4 ? 9 : 24)));
+  constexpr int NEPI = EP == 0 ? 8 : (EP == 5 ? 4 : (EP == 3 ? 17 : (EP == 4 ? 9 : 24)));
   constexpr bool SUMS = EP == 3 || EP == 4;  // per-tile channel sums (EP 3: fp32 out, EP 4: bf16 out)
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, col = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -202,33 +202,38 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
     decode(T, nimg, oy0, ox0);
     const int ox = ox0 + col;
     if constexpr (EP == 5) {
-      // pooled pixel (oy0 / 2 + mp, ox / 2): rows m = 2 mp, 2 mp + 1 in registers, columns col / col ^ 1 across lanes;
-      // the even-column lanes store
-      const int ph = a.out_h >> 1, pw = a.out_w >> 1, px = ox >> 1;
+      // pooled pixel (oy0 / 2 + mp, ox / 2): rows m = 2 mp, 2 mp + 1 in registers, columns col / col ^ 1 across lanes
+      // (both lanes hold the result); of each co-block pair (t, t + 1) the even lane stores block t, the odd one t + 1
+      const int ph = a.out_h >> 1, pw = a.out_w >> 1, px = ox >> 1, odd = col & 1;
 #pragma unroll
       for (int mp = 0; mp < 2; ++mp) {
         const int py = (oy0 >> 1) + mp;
-        const bool ok = (col & 1) == 0 && py < ph && px < pw;
+        const bool ok = py < ph && px < pw;
         const uint32_t po = ok ? (uint32_t)(((((long)nimg * ph + py) * pw + px) * a.out_cs + a.out_co + 4 * g) * 2) : BUF_OOB;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          float v[4];
+        for (int tp = 0; tp < 4; tp += 2) {
+          float w[4];  // block tp + odd: both blocks' maxima are formed (the xor shuffle needs every lane), one kept
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            float x0 = acc[2 * mp][t][i] + bias[t][i], x1 = acc[2 * mp + 1][t][i] + bias[t][i];
-            if constexpr (ACT == 1) {
-              x0 = fmaxf(x0, x0 * a.slope);
-              x1 = fmaxf(x1, x1 * a.slope);
-            } else if constexpr (ACT == 2) {
-              x0 = x0 > 0.f ? x0 : 0.f;
-              x1 = x1 > 0.f ? x1 : 0.f;
+            float m2[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              float x0 = acc[2 * mp][tp + u][i] + bias[tp + u][i], x1 = acc[2 * mp + 1][tp + u][i] + bias[tp + u][i];
+              if constexpr (ACT == 1) {
+                x0 = fmaxf(x0, x0 * a.slope);
+                x1 = fmaxf(x1, x1 * a.slope);
+              } else if constexpr (ACT == 2) {
+                x0 = x0 > 0.f ? x0 : 0.f;
+                x1 = x1 > 0.f ? x1 : 0.f;
+              }
+              const float rm = fmaxf(x0, x1);
+              m2[u] = fmaxf(rm, __shfl_xor(rm, 1));
             }
-            const float rm = fmaxf(x0, x1);
-            v[i] = fmaxf(rm, __shfl_xor(rm, 1));
+            w[i] = odd ? m2[1] : m2[0];
           }
-          const bf16x2 p0 = {(__bf16)v[0], (__bf16)v[1]}, p1 = {(__bf16)v[2], (__bf16)v[3]};
+          const bf16x2 p0 = {(__bf16)w[0], (__bf16)w[1]}, p1 = {(__bf16)w[2], (__bf16)w[3]};
           const v2u32 pk = {__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1)};
-          __builtin_amdgcn_raw_buffer_store_b64(pk, yr, po == BUF_OOB ? BUF_OOB : po + (uint32_t)(t * 32), 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(pk, yr, po == BUF_OOB ? BUF_OOB : po + (uint32_t)((tp + odd) * 32), 0, 0);
         }
       }
       if (Tn >= a.ntiles) break;
