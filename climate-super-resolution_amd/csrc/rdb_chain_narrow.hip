@@ -112,21 +112,25 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, char* smem, int ti
     }
   };
 
-  // A fragments: base [ky][kx][cb] and dense [ky][d] from the packed [16][9 KP] weights (k = tap KP + channel: base |
-  // out1 | out2 | out3 at channels 0 / 64 / 80 / 96)
-  bf16x8 Ab[3][3][2], Ad[3][ND > 0 ? ND : 1];
+  // A fragments: base [ky][kx][cb] (fragment 6 ky + 2 kx + cb) and dense [ky][d] (fragment 18 + ND ky + d) from the
+  // packed [16][9 KP] weights (k = tap KP + channel: base | out1 | out2 | out3 at channels 0 / 64 / 80 / 96), staged
+  // through LDS once per workgroup: the level's two waves move its fragments by LDS-DMA (one lane-linear 1 KB piece
+  // each, into the ring space before the rings are used) and both read all of them.  Loaded straight from global
+  // memory, every wave fetched its level's whole weight set: 2 x 110 KB per CU ahead of the first MFMA.
+  constexpr int NF = 18 + 3 * ND, PB = L == 1 ? 0 : (L == 2 ? 18 : (L == 3 ? 42 : 69));  // fragments, first piece
+  static_assert((69 + 33) * 1024 <= RR_OFF_DUMMY, "chain weight staging fits the ring space");
   {
-    const uint16_t* wr = a.wt[L - 1] + col * 9 * KP;
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx)
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb) Ab[ky][kx][cb] = *(const bf16x8*)(wr + (3 * ky + kx) * KP + cb * 32 + 8 * g);
-#pragma unroll
-      for (int d = 0; d < ND; ++d) {
-        int kx, ch;
-        bool zero = false;
+    const __amdgpu_buffer_rsrc_t wrs = buf_rsrc(a.wt[L - 1], (uint32_t)(16 * 9 * KP * 2));
+    for (int f = fp; f < NF; f += 2) {
+      int ky, kx, ch;
+      bool zero = false;
+      if (f < 18) {
+        ky = f / 6;
+        kx = (f % 6) >> 1;
+        ch = (f & 1) * 32 + 8 * g;
+      } else {
+        const int e = f - 18, d = e % (ND > 0 ? ND : 1);
+        ky = e / (ND > 0 ? ND : 1);
         if (L == 2 || d >= 3) {  // a 16-channel group (x1 at level 2, x3 at level 4) as a pair of tap columns
           const int pr = L == 2 ? d : d - 3;
           kx = pr == 0 ? (g < 2 ? 0 : 1) : 2;
@@ -136,10 +140,29 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, char* smem, int ti
           kx = d;
           ch = 64 + 8 * g;
         }
-        Ad[ky][d] = zero ? (bf16x8){} : *(const bf16x8*)(wr + (3 * ky + kx) * KP + ch);
       }
+      uint32_t keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(zero ? BUF_OOB : (uint32_t)((col * 9 * KP + (3 * ky + kx) * KP + ch) * 2)), "s"(wrs),
+                     "s"(lds0 + (uint32_t)((PB + f) * 1024))
+                   : "memory");
     }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lds_barrier();  // every level's pieces have landed
+  bf16x8 Ab[3][3][2], Ad[3][ND > 0 ? ND : 1];
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky) {
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) Ab[ky][kx][cb] = *(const bf16x8*)(smem + (PB + 6 * ky + 2 * kx + cb) * 1024 + lane * 16);
+#pragma unroll
+    for (int d = 0; d < ND; ++d) Ad[ky][d] = *(const bf16x8*)(smem + (PB + 18 + ND * ky + d) * 1024 + lane * 16);
+  }
+  lds_barrier();  // every wave's reads are done: the rings may be written
+  // the level-output rings start zeroed: their pixel slots of image columns -1 and >= w are never written (padding)
+  for (int i = tid; i < (RR_LDS - RR_OFF_D) / 16; i += 512) *(uint4*)(smem + RR_OFF_D + 16 * i) = make_uint4(0, 0, 0, 0);
   float bb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // channels 8 (g >> 1) .. + 7 (the epilogue's traded layout)
   if constexpr (MODE == 0) {
     const float4 b0 = *(const float4*)(a.bias[L - 1] + 8 * (g >> 1)), b1 = *(const float4*)(a.bias[L - 1] + 8 * (g >> 1) + 4);
@@ -292,8 +315,6 @@ __global__ __launch_bounds__(512, 1) void rdb_chain_rr_kernel(ChainArgs a) {
   const int tid = threadIdx.x;
   const int nimg = blockIdx.x / a.strips_y, r0 = (blockIdx.x % a.strips_y) * a.rows;
   const int r1 = min(r0 + a.rows, a.h);
-  // the level-output rings start zeroed: their pixel slots of image columns -1 and >= w are never written (padding)
-  for (int i = tid; i < (RR_LDS - RR_OFF_D) / 16; i += 512) *(uint4*)(smem + RR_OFF_D + 16 * i) = make_uint4(0, 0, 0, 0);
   const int w = tid >> 6;
   switch (w < 4 ? w : 7 - w) {
     case 0: run_level<MODE, 1>(a, smem, tid, nimg, r0, r1); break;
