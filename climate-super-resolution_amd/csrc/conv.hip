@@ -2350,6 +2350,9 @@ static int launch_fwd_dma(const FwdArgs& a0, int ncob, hipStream_t s) {
 }
 
 #define WIDE_GEO(pfx) ((pfx) == 18)
+#ifndef CLIMSR_DMA_EP12
+#define CLIMSR_DMA_EP12 0  // A/B builds only (tools/diag_build.sh): 1 = RDB conv5 / pull-x on the LDS-DMA conv as well
+#endif
 template <int MW, int NT, int PFX, int PFW, int EP, int GEO>
 static int launch_fwd_geo(const FwdArgs& a0, int ncob, size_t lds, hipStream_t s) {
   if constexpr (GEO == 1 && !WIDE_GEO(PFX) && MW == 4 && NT == 4) {
@@ -2359,7 +2362,7 @@ static int launch_fwd_geo(const FwdArgs& a0, int ncob, size_t lds, hipStream_t s
     // the GAN step than the two-workgroups-per-CU form (its chunk-0 latency and epilogue are not hidden in a single
     // round)
     const bool fits = (EP == 9 || EP == 10) ? a0.out_h % DMA_TH == 0 : (a0.out_h % DMA_TH == 0 || a0.out_h >= 3 * DMA_TH);
-    if (EP != 1 && EP != 2 && !a0.down2 && fits) return launch_fwd_dma<EP>(a0, ncob, s);
+    if ((CLIMSR_DMA_EP12 || (EP != 1 && EP != 2)) && !a0.down2 && fits) return launch_fwd_dma<EP>(a0, ncob, s);
   }
   FwdArgs a = a0;
   a.xgrp = GEO == 1 ? conv_xcd_group(ncob, (long)NT * 16 * a.kpk * 2) : 0;
