@@ -433,6 +433,9 @@ int fwd_dma_launch(int ep, const FwdArgs& a, int ncob, hipStream_t s) {
   case E: k = rf ? conv_fwd_dma_kernel<E, true> : conv_fwd_dma_kernel<E, false>; break;
   switch (ep) {
     DMA_EP(0) DMA_EP(3) DMA_EP(4) DMA_EP(6) DMA_EP(7) DMA_EP(8) DMA_EP(9) DMA_EP(10) DMA_EP(11)
+#if CLIMSR_DMA_EP12  // (A/B builds: RDB conv5 / pull-x on this kernel, conv.hip)
+    DMA_EP(1) DMA_EP(2)
+#endif
     default: set_error("conv2d_fwd: no LDS-DMA kernel for epilogue %d", ep); return CLIMSR_EINVAL;
   }
 #undef DMA_EP
