@@ -61,7 +61,7 @@ class _PlainDEngine:
         self.b0 = torch.zeros((FC_PAD,), dtype=torch.float32, device=dev)
         self.w1 = torch.zeros((FC_PAD,), dtype=torch.float32, device=dev)
         self.version = -1
-        self.ws = Workspace(overlap=True)  # weight-gradient reductions beside the backward (joined at its end)
+        self.ws = Workspace()
         self.scratch: Dict[str, Tensor] = {}
 
     def ensure_packed(self):
@@ -212,7 +212,6 @@ class _PlainDEngine:
             if li == 0 and need_x:
                 dx = torch.empty((n, 1, sv["h"], sv["w"]), dtype=torch.float32, device=dev)
                 ops.nhwc_to_nchw(da, n, 1, sv["h"], sv["w"], plan.cin, 0, dx)
-        self.ws.join()  # the weight-gradient reductions ran on the side stream (ops.Workspace): final from here on
         return dx
 
 

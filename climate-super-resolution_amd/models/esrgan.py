@@ -78,7 +78,7 @@ class _Engine:
         self.cin = gen.in_channels
         self.cin_pad = (self.cin + 7) // 8 * 8
         self.plans: Dict[str, ConvPlan] = {}
-        self.ws = Workspace(overlap=True)  # weight-gradient reductions beside the backward (joined at its end)
+        self.ws = Workspace()
         self.version = -1
         self.scratch: Dict[str, Tensor] = {}
 
@@ -371,15 +371,12 @@ class _Engine:
             self._rdb_wgrad(i, src, dz, n, h, w, ws, acc)
             hook = self.gen._grad_ready_hook
             if hook is not None and r == 0 and blk in self.gen._grad_ready_blocks:
-                # every gradient from RRDB_trunk.<blk> on (flat order: trunk blocks, tail convs) is final once the
-                # side-stream reductions are (ops.Workspace)
-                ws.join()
+                # every gradient from RRDB_trunk.<blk> on (flat order: trunk blocks, tail convs) is final
                 hook(self.gen._block_flat_lo(blk))
         # ---- conv_first: grad wrt fea = trunk path + global skip
         axpby(npx_lr, nf, 1.0, g_fea2, nf, 0, 1.0, G[0], nf, 0)
         act_grad(npx_lr, nf, G[0], nf, 0, None, 0, 0, ACT_NONE, dz64, nf)
         P["conv_first"].wgrad(sv["lr"], self.cin_pad, 0, h, w, dz64, nf, n, ws, acc)
-        ws.join()  # the weight-gradient reductions ran on the side stream (ops.Workspace): final from here on
 
 
 class _GeneratorFn(torch.autograd.Function):

@@ -50,7 +50,7 @@ class _DEngine:
         self.packer = BatchedPacker([p for _c, _b, p in self.layers], dev)
         self.fc0_bf16 = torch.empty(d.fc[0].weight.shape, dtype=torch.bfloat16, device=dev)
         self.version = -1
-        self.ws = Workspace(overlap=True)  # weight-gradient reductions beside the backward (joined at its end)
+        self.ws = Workspace()
         self.scratch: Dict[str, Tensor] = {}
         self.fuse_stem = True  # features.0 + features.2 as one launch (False: per layer; tools/perf_stem.py's A/B)
 
@@ -182,7 +182,6 @@ class _DEngine:
         if need_w:
             ops.linear_wgrad(du0_t, sv["p_t"], n_pad, feat, o, fc0.weight.grad, acc)
             if hook is not None:  # fc.0 / fc.2: the last flat entries, 103 M of 107 M parameters
-                self.ws.join()
                 hook(d._fc_flat_lo())
         dp = self._scr("dp", (n, feat), torch.float32, dev)
         ops.linear_dgrad(du0, self.fc0_bf16, n, feat, o, dp)
@@ -221,7 +220,6 @@ class _DEngine:
                 plan.gb = None
                 plan.wgrad(L["a_in"], L["cs_in"], 0, L["h_in"], L["w_in"], dz, cz, n, self.ws, acc)
                 if hook is not None and li in d._ready_layers:  # this layer group's conv + BN gradients are final
-                    self.ws.join()  # (once the side-stream weight-gradient reductions are: ops.Workspace)
                     hook(d._layer_flat_lo(li))
             if li > 0 or need_x:
                 prev_bn = self.layers[li - 1][1] if li > 0 else None
@@ -252,7 +250,6 @@ class _DEngine:
             if li == 0 and need_x:
                 dx = torch.empty((n, 1, sv["h"], sv["w"]), dtype=torch.float32, device=dev)
                 ops.nhwc_to_nchw(da, n, 1, sv["h"], sv["w"], plan.cin, 0, dx)
-        self.ws.join()  # the weight-gradient reductions ran on the side stream (ops.Workspace): final from here on
         return dx
 
 

@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from typing import Dict, List, Optional
+from typing import Optional
 
 import torch
 
@@ -272,6 +272,7 @@ class ConvPlan:
         rows_c = need // (ns * (cw * self.ks * self.ks + 1))  # co_rows
         part = ws
         bpart = ws[ns * rows_c * cw * self.ks * self.ks:]
+        s = _lib.stream_ptr()
         has_b = self.bias is not None and self.gb is not None
         flops = 2 * self.cin_real * self.cout * self.ks * self.ks * n * d.out_h * d.out_w
         nbytes = n * in_h * in_w * self.cin_real * 2 + n * d.out_h * d.out_w * self.cout * 2 + self.cout * self.cin_real * self.ks ** 2 * 4
@@ -279,9 +280,9 @@ class ConvPlan:
              lambda: check(
             lib.climsr_conv2d_wgrad(ctypes.byref(d), ptr(x), ptr(dz), dz_cs, ptr(part), ptr(bpart) if has_b else None, ns,
                                     _lib.stream_ptr()), f"conv wgrad {self.name}"), "wgrad " + self.name, nbytes)
-        workspace.reduce_on_side(x.device, lambda: _launch(f"wgrad reduce {self.name}", lambda: lib.climsr_conv2d_wgrad_reduce(
-            ptr(part), ptr(bpart) if has_b else None, ns, self.cout, self.cin_real, cw, self.ks, ptr(self.gw),
-            ptr(self.gb) if has_b else None, 1 if accumulate else 0, _lib.stream_ptr())))
+        _launch(f"wgrad reduce {self.name}", lambda: lib.climsr_conv2d_wgrad_reduce(ptr(part), ptr(bpart) if has_b else None, ns, self.cout, self.cin_real, cw,
+                                             self.ks, ptr(self.gw), ptr(self.gb) if has_b else None,
+                                             1 if accumulate else 0, s))
 
 
 class GroupedWgrad:
@@ -322,83 +323,27 @@ class GroupedWgrad:
         ws = workspace.get(need, x.device)
         part = ws
         bpart = ws[ns * self.out_c * self.in_c * 9:]
+        s = _lib.stream_ptr()
         flops = sum(2 * p.cin_real * p.cout * 9 for p in self.plans) * n * in_h * in_w
         nbytes = n * in_h * in_w * (self.in_c + self.out_c) * 2 + sum(p.cout * p.cin_real * 9 * 4 for p in self.plans)
         _run(lib.climsr_conv2d_wgrad_kernel(ctypes.byref(d)).decode() if PROFILER is not None else "", flops, lambda: check(
             lib.climsr_conv2d_wgrad(ctypes.byref(d), ptr(x), ptr(dz), dz_cs, ptr(part), ptr(bpart), ns, _lib.stream_ptr()),
             f"grouped wgrad {self.name}"), "wgrad " + self.name, nbytes)
         tab = self._table(x.device)
-        workspace.reduce_on_side(x.device, lambda: _launch(f"grouped wgrad reduce {self.name}", lambda: lib.climsr_conv2d_wgrad_reduce_rows(
-            ptr(part), ptr(bpart), ns, self.out_c, self.in_c * 9, 3, ptr(tab), len(self.plans), self.max_elems, 1 if accumulate else 0,
-            _lib.stream_ptr())))
-
-
-_SIDE: Dict[int, "torch.cuda.Stream"] = {}
-
-
-def side_stream(device) -> "torch.cuda.Stream":
-    """The stream the weight-gradient split-K reductions run on (one per device), beside the backward's main stream."""
-    idx = torch.device(device).index or 0
-    if idx not in _SIDE:
-        _SIDE[idx] = torch.cuda.Stream(device=device)
-    return _SIDE[idx]
+        _launch(f"grouped wgrad reduce {self.name}", lambda: lib.climsr_conv2d_wgrad_reduce_rows(ptr(part), ptr(bpart), ns, self.out_c, self.in_c * 9, 3, ptr(tab),
+                                                  len(self.plans), self.max_elems, 1 if accumulate else 0, s))
 
 
 class Workspace:
-    """The wgrad split-K partial slabs: a ring of RING grow-only fp32 buffers.  A weight gradient writes its slabs on
-    the current stream and its reduction (``reduce_on_side``) reads them on the side stream, so it overlaps the
-    backward's next kernels (it is bandwidth-bound, they are MFMA-bound); a buffer is handed out again only after the
-    reduction that last read it (its event), and ``join`` makes the current stream wait for every reduction -- the
-    engines call it at the end of each backward and before a grad-ready hook reads a gradient slice."""
+    """Grow-only fp32 scratch buffer (wgrad split partials)."""
 
-    RING = 3
-
-    def __init__(self, overlap: bool = False):
-        # overlap: reductions on the side stream (the model engines, which join); off, they run in stream order on the
-        # current stream (direct ConvPlan.wgrad / GroupedWgrad.run callers read the gradient right after)
-        self.overlap = overlap
-        self.bufs: List[Optional[torch.Tensor]] = [None] * self.RING
-        self.events: List[Optional["torch.cuda.Event"]] = [None] * self.RING
-        self.i = 0
-        self.cur = 0
-        self.pending = None  # the device with reductions in flight on its side stream
+    def __init__(self):
+        self.buf: Optional[torch.Tensor] = None
 
     def get(self, nfloats: int, device) -> torch.Tensor:
-        i = self.i
-        self.i = (i + 1) % self.RING
-        ev = self.events[i]
-        if ev is not None:  # the side-stream reduction that read this buffer last
-            torch.cuda.current_stream(device).wait_event(ev)
-            self.events[i] = None
-        b = self.bufs[i]
-        if b is None or b.numel() < nfloats or b.device != device:
-            # (regrown only before the first join: every earlier reader has finished by then -- see join)
-            b = self.bufs[i] = torch.empty(max(nfloats, 1 << 20), dtype=torch.float32, device=device)
-        self.cur = i
-        return b
-
-    def reduce_on_side(self, device, launch) -> None:
-        """Run ``launch`` (a reduction reading the buffer ``get`` returned last) on the side stream, after everything
-        already queued on the current stream."""
-        if not self.overlap:
-            launch()
-            return
-        side = side_stream(device)
-        side.wait_stream(torch.cuda.current_stream(device))
-        with torch.cuda.stream(side):
-            launch()
-        ev = torch.cuda.Event()
-        ev.record(side)
-        self.events[self.cur] = ev
-        self.pending = device
-
-    def join(self) -> None:
-        """The current stream waits for every reduction in flight (their gradients are final after this)."""
-        if self.pending is None:
-            return
-        torch.cuda.current_stream(self.pending).wait_stream(side_stream(self.pending))
-        self.events = [None] * self.RING
-        self.pending = None
+        if self.buf is None or self.buf.numel() < nfloats or self.buf.device != device:
+            self.buf = torch.empty(max(nfloats, 1 << 20), dtype=torch.float32, device=device)
+        return self.buf
 
 
 def act_grad(npix: int, c_real: int, g: torch.Tensor, g_cs: int, g_co: int, y: Optional[torch.Tensor], y_cs: int, y_co: int,
