@@ -3011,6 +3011,9 @@ struct W64 {
 // TS = 2: 8 waves, wave w owns ci block w & 3 and taps [0,5) or [5,9) (w >> 2): 20 accumulators instead of 36, so
 // two waves share each SIMD (latency hiding) at the price of each wave re-reading the shared dz fragments.
 // G (TS 1): the LDS-DMA form -- see conv_wgrad64_glds_kernel below.
+#ifndef CLIMSR_W64_LA
+#define CLIMSR_W64_LA 2  // the LDS-DMA wgrad64's x-fragment lookahead (A/B builds vary it)
+#endif
 #ifndef CLIMSR_W64S2_GLDS
 #define CLIMSR_W64S2_GLDS 1  // A/B builds only (tools/diag_build.sh): 0 = the register-staged stride-2 kernel
 #endif
@@ -3260,14 +3263,15 @@ __device__ __forceinline__ void wgrad64_body(const WgArgs& a) {
       const char* xb = zb + ZB;
       // the 36 (k-step, tap) groups of 4 MFMAs read their x fragment from a 3-register ring loaded 2 groups ahead,
       // the next k-step's dz fragments half-way through the current one (one whole fragment set: 56 registers)
-      bf16x8 af[2][4], bq[3];
+      constexpr int LA = S == 1 ? CLIMSR_W64_LA : 2;  // x-fragment lookahead in (k-step, tap) groups (ring of LA + 1)
+      bf16x8 af[2][4], bq[LA + 1];
       ld_af(zb, 0, af[0]);
-      bq[0] = ld_bf(xb, 0, 0);
-      bq[1] = ld_bf(xb, 0, 1);
+#pragma unroll
+      for (int j = 0; j < LA; ++j) bq[j] = ld_bf(xb, 0, j);
 #pragma unroll
       for (int gi = 0; gi < NK * 9; ++gi) {
-        const int kk = gi / 9, u = gi % 9, gn = gi + 2;
-        if (gn < NK * 9) bq[gn % 3] = ld_bf(xb, gn / 9, gn % 9);
+        const int kk = gi / 9, u = gi % 9, gn = gi + LA;
+        if (gn < NK * 9) bq[gn % (LA + 1)] = ld_bf(xb, gn / 9, gn % 9);
         if (u == 4 && kk + 1 < NK) ld_af(zb, kk + 1, af[(kk + 1) & 1]);
         __builtin_amdgcn_sched_barrier(0);
         if (u == 0) {
@@ -3275,7 +3279,7 @@ __device__ __forceinline__ void wgrad64_body(const WgArgs& a) {
           for (int t = 0; t < 4; ++t) accb[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk & 1][t], ones, accb[t], 0, 0, 0);
         }
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk & 1][t], bq[gi % 3], acc[t][u], 0, 0, 0);
+        for (int t = 0; t < 4; ++t) acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk & 1][t], bq[gi % (LA + 1)], acc[t][u], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
       }
       cur = cur == 2 ? 0 : cur + 1;
