@@ -159,6 +159,8 @@ SIGNATURES = {
     "climsr_adamw_step": (c_int, [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "climsr_adamw_step_mirror": (c_int, [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p,
                                          c_void_p]),
+    "climsr_adamw_step_mirror_frag": (c_int, [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int,
+                                              c_void_p, c_void_p]),
     "climsr_bn_workspace_doubles": (c_int64, [c_int64, c_int]),
     "climsr_bn_forward": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_int, c_float, c_float, c_float, c_void_p,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -176,7 +178,12 @@ SIGNATURES = {
     "climsr_linear_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p, c_int64,
                                   c_void_p, c_void_p]),
     "climsr_linear_dgrad": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
+    "climsr_linear_pack_frag": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "climsr_linear_fwd_frag": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p, c_int64,
+                                       c_void_p, c_void_p]),
+    "climsr_linear_dgrad_frag": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     "climsr_linear_wgrad": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
+    "climsr_linear_wgrad2": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     "climsr_d_head_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "climsr_d_stem_s2": (c_int, [c_void_p, c_void_p]),
     "climsr_conv2d_fwd_pool_ok": (c_int, [c_void_p, c_void_p]),

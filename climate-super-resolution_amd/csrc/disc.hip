@@ -735,7 +735,11 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(const uint16_t* __restr
 // load instructions of the form above.  Workgroup = 256 rows, grid = (o / 256) x nsplit.  Measured at fc.0 (n 32,
 // k 100352, o 1024): 65 us = 3.2 TB/s of weights with 3 workgroups per CU; 8 or 16 waves per workgroup splitting K
 // inside it (partials met in LDS) were slower (68-110 us), as were 1.5 or 6 workgroups per CU.
-template <int NF>
+//
+// FRAG: W in fragment order (linear_frag_index below): the wave's 64 rows x 32 k of one k-step are one contiguous 4 KB
+// piece, so an LU round streams 16 KB straight from HBM (the row-major form reads 64 B from each of 64 rows 200 KB
+// apart per fragment load).
+template <int NF, bool FRAG>
 __global__ __launch_bounds__(256) void linear_fwd_wide_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, int n,
                                                               int k, int o, int ksplit, float* __restrict__ part) {
   constexpr int NA = 4, LU = 4;
@@ -748,14 +752,18 @@ __global__ __launch_bounds__(256) void linear_fwd_wide_kernel(const uint16_t* __
   for (int t = 0; t < NA; ++t)
 #pragma unroll
     for (int f = 0; f < NF; ++f) acc[t][f] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const uint16_t* wrow = w + (long)(o0 + col) * k + g * 8;
+  // A fragment t of k-step kk: row-major w[(o0 + 16t + col) * k + kk + 8g]; fragment order: piece (o0/64, kk/32, t)
+  const uint16_t* wrow = FRAG ? w + (long)(o0 >> 6) * (k >> 5) * 2048 + lane * 8 : w + (long)(o0 + col) * k + g * 8;
+  auto wfrag = [&](int t, int kk) -> bf16x8 {
+    return FRAG ? *(const bf16x8*)(wrow + (long)(kk >> 5) * 2048 + t * 512) : *(const bf16x8*)(wrow + (long)t * 16 * k + kk);
+  };
   int kk = kb;
   for (; kk + 32 * LU <= ke; kk += 32 * LU) {
     bf16x8 af[LU][NA], bfr[LU][NF];
 #pragma unroll
     for (int u = 0; u < LU; ++u)
 #pragma unroll
-      for (int t = 0; t < NA; ++t) af[u][t] = *(const bf16x8*)(wrow + (long)t * 16 * k + kk + 32 * u);
+      for (int t = 0; t < NA; ++t) af[u][t] = wfrag(t, kk + 32 * u);
 #pragma unroll
     for (int u = 0; u < LU; ++u)
 #pragma unroll
@@ -773,7 +781,7 @@ __global__ __launch_bounds__(256) void linear_fwd_wide_kernel(const uint16_t* __
   for (; kk < ke; kk += 32) {
     bf16x8 af[NA], bfr[NF];
 #pragma unroll
-    for (int t = 0; t < NA; ++t) af[t] = *(const bf16x8*)(wrow + (long)t * 16 * k + kk);
+    for (int t = 0; t < NA; ++t) af[t] = wfrag(t, kk);
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
       const int nn = f * 16 + col;
@@ -816,10 +824,11 @@ __global__ void linear_reduce_kernel(const float* __restrict__ part, int nsplit,
   if (ybf) ybf[idx] = f2bf(s);
 }
 
-extern "C" int climsr_linear_fwd(const uint16_t* x, const uint16_t* w, const float* bias, int n, int k, int o, int act, float slope,
-                                 float* workspace, int64_t ws_floats, float* y, void* stream) {
-  if (!x || !w || !y || !workspace || n <= 0 || n > 64 || k % 32 || o % 16) {
-    set_error("linear_fwd: bad args (n=%d k=%d o=%d; need n<=64, k%%32==0, o%%16==0)", n, k, o);
+static int linear_fwd_launch(const uint16_t* x, const uint16_t* w, const float* bias, int n, int k, int o, int act, float slope,
+                             float* workspace, int64_t ws_floats, float* y, void* stream, bool frag) {
+  const char* who = frag ? "linear_fwd_frag" : "linear_fwd";
+  if (!x || !w || !y || !workspace || n <= 0 || n > 64 || k % 32 || o % (frag ? 256 : 16)) {
+    set_error("%s: bad args (n=%d k=%d o=%d; need n<=64, k%%32==0, o%%%d==0)", who, n, k, o, frag ? 256 : 16);
     return CLIMSR_EINVAL;
   }
   const bool wide = o % 256 == 0;
@@ -830,22 +839,58 @@ extern "C" int climsr_linear_fwd(const uint16_t* x, const uint16_t* w, const flo
   int ksplit = round_up(ceil_div(k, nsplit), k >= rnd * nsplit ? rnd : 32);
   nsplit = ceil_div(k, ksplit);
   if ((int64_t)nsplit * n * o > ws_floats) {
-    set_error("linear_fwd: workspace too small (%lld floats needed)", (long long)nsplit * n * o);
+    set_error("%s: workspace too small (%lld floats needed)", who, (long long)nsplit * n * o);
     return CLIMSR_EINVAL;
   }
   hipStream_t s = (hipStream_t)stream;
   const int nf = (n + 15) / 16;
   dim3 grid(oblk, nsplit);
-  if (wide) {
-    if (nf == 1) hipLaunchKernelGGL(linear_fwd_wide_kernel<1>, grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
-    else if (nf == 2) hipLaunchKernelGGL(linear_fwd_wide_kernel<2>, grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
-    else hipLaunchKernelGGL(linear_fwd_wide_kernel<4>, grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
+  if (frag) {
+    if (nf == 1) hipLaunchKernelGGL((linear_fwd_wide_kernel<1, true>), grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
+    else if (nf == 2) hipLaunchKernelGGL((linear_fwd_wide_kernel<2, true>), grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
+    else hipLaunchKernelGGL((linear_fwd_wide_kernel<4, true>), grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
+  } else if (wide) {
+    if (nf == 1) hipLaunchKernelGGL((linear_fwd_wide_kernel<1, false>), grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
+    else if (nf == 2) hipLaunchKernelGGL((linear_fwd_wide_kernel<2, false>), grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
+    else hipLaunchKernelGGL((linear_fwd_wide_kernel<4, false>), grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
   } else if (nf == 1) hipLaunchKernelGGL(linear_fwd_kernel<1>, grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
   else if (nf == 2) hipLaunchKernelGGL(linear_fwd_kernel<2>, grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
   else hipLaunchKernelGGL(linear_fwd_kernel<4>, grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
   hipLaunchKernelGGL(linear_reduce_kernel, dim3(ceil_div((long)n * o, 256)), dim3(256), 0, s, workspace, nsplit, n, o, bias, act, slope,
                      y, (uint16_t*)nullptr);
-  return check_launch("linear_fwd");
+  return check_launch(who);
+}
+
+extern "C" int climsr_linear_fwd(const uint16_t* x, const uint16_t* w, const float* bias, int n, int k, int o, int act, float slope,
+                                 float* workspace, int64_t ws_floats, float* y, void* stream) {
+  return linear_fwd_launch(x, w, bias, n, k, o, act, slope, workspace, ws_floats, y, stream, false);
+}
+
+extern "C" int climsr_linear_fwd_frag(const uint16_t* x, const uint16_t* wf, const float* bias, int n, int k, int o, int act, float slope,
+                                      float* workspace, int64_t ws_floats, float* y, void* stream) {
+  return linear_fwd_launch(x, wf, bias, n, k, o, act, slope, workspace, ws_floats, y, stream, true);
+}
+
+// fp32 [o][k] -> bf16 fragment order; one thread per 16 B of output (sequential stores, 32 B row-segment reads)
+__global__ void linear_pack_frag_kernel(const float* __restrict__ w, int k, long n8, uint16_t* __restrict__ wf) {
+  const long e8 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e8 >= n8) return;
+  const int lane = e8 & 63, t = (e8 >> 6) & 3;
+  const long kbn = k >> 5, piece = e8 >> 8, ob = piece / kbn, kb = piece - ob * kbn;
+  const long r = ob * 64 + t * 16 + (lane & 15), c = kb * 32 + (lane >> 4) * 8;
+  const float4 a = *(const float4*)(w + r * k + c), b = *(const float4*)(w + r * k + c + 4);
+  *(uint4*)(wf + e8 * 8) = make_uint4((uint32_t)f2bf(a.x) | ((uint32_t)f2bf(a.y) << 16), (uint32_t)f2bf(a.z) | ((uint32_t)f2bf(a.w) << 16),
+                                      (uint32_t)f2bf(b.x) | ((uint32_t)f2bf(b.y) << 16), (uint32_t)f2bf(b.z) | ((uint32_t)f2bf(b.w) << 16));
+}
+
+extern "C" int climsr_linear_pack_frag(const float* w, int o, int k, uint16_t* wf, void* stream) {
+  if (!w || !wf || o <= 0 || k <= 0 || o % 64 || k % 32) {
+    set_error("linear_pack_frag: bad args (o=%d k=%d; need o%%64==0, k%%32==0)", o, k);
+    return CLIMSR_EINVAL;
+  }
+  const long n8 = (long)o * k / 8;
+  hipLaunchKernelGGL(linear_pack_frag_kernel, dim3(ceil_div(n8, 256)), dim3(256), 0, (hipStream_t)stream, w, k, n8, wf);
+  return check_launch("linear_pack_frag");
 }
 
 // data gradient dx[n][k] = sum_o dy[n][o] W[o][k]:  A = dy rows (n, o-contiguous), B = W^T taken
@@ -917,7 +962,9 @@ __global__ __launch_bounds__(256) void linear_dgrad_kernel(const uint16_t* __res
 // Wide form (k % 128 == 0, the fc.0 case): a workgroup owns 128 k columns (two 16-column fragments per wave), so a W
 // tile row is 256 contiguous bytes, and the dy fragments of the next 128-row o tile are loaded into registers together
 // with the next W tile (the form above reads them from global memory right before each MFMA).
-template <int NF>
+// FRAG: W in fragment order (common.h linear_frag_index); a 128 o x 128 k tile is then two contiguous 16 KB runs (the
+// row-major tile is 128 rows of 256 B, 200 KB apart), written to the same LDS positions.
+template <int NF, bool FRAG>
 __global__ __launch_bounds__(256) void linear_dgrad_wide_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ w, int n,
                                                                 int k, int o, float* __restrict__ dx, int accumulate) {
   constexpr int WP = 128 + 8;  // LDS row pitch (bf16)
@@ -932,12 +979,25 @@ __global__ __launch_bounds__(256) void linear_dgrad_wide_kernel(const uint16_t* 
     for (int f = 0; f < NF; ++f) acc[b][f] = (f32x4){0.f, 0.f, 0.f, 0.f};
   uint4 buf[8];
   bf16x8 dyf[4][NF];
+  // vector v (16 B) of a tile: row-major, row v / 16 and k 8 (v % 16); fragment order, piece (obl, kbl, t) = v / 64
+  // and lane v % 64, i.e. row 64 obl + 16 t + lane % 16 and k 32 kbl + 8 (lane / 16)
+  auto lds_pos = [&](int v) -> int {
+    if (!FRAG) return (v >> 4) * WP + (v & 15) * 8;
+    return ((v >> 10) * 64 + ((v >> 6) & 3) * 16 + (v & 15)) * WP + ((v >> 8) & 3) * 32 + ((v >> 4) & 3) * 8;
+  };
+  const long kbn = k >> 5;
   auto issue = [&](int ob) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int v = tid + i * 256;
-      const int r = v >> 4, cv = v & 15;
-      buf[i] = ob + r < o ? *(const uint4*)(w + (long)(ob + r) * k + k0 + cv * 8) : make_uint4(0, 0, 0, 0);
+      if (FRAG) {
+        const int obl = v >> 10;
+        const long piece = ((long)((ob >> 6) + obl) * kbn + (k0 >> 5) + ((v >> 8) & 3)) * 4 + ((v >> 6) & 3);
+        buf[i] = ob + obl * 64 < o ? *(const uint4*)(w + piece * 512 + (v & 63) * 8) : make_uint4(0, 0, 0, 0);
+      } else {
+        const int r = v >> 4, cv = v & 15;
+        buf[i] = ob + r < o ? *(const uint4*)(w + (long)(ob + r) * k + k0 + cv * 8) : make_uint4(0, 0, 0, 0);
+      }
     }
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks)
@@ -951,10 +1011,7 @@ __global__ __launch_bounds__(256) void linear_dgrad_wide_kernel(const uint16_t* 
   for (int ob = 0; ob < o; ob += 128) {
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int v = tid + i * 256;
-      *(uint4*)(ws_ + (v >> 4) * WP + (v & 15) * 8) = buf[i];
-    }
+    for (int i = 0; i < 8; ++i) *(uint4*)(ws_ + lds_pos(tid + i * 256)) = buf[i];
     bf16x8 af[4][NF];
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks)
@@ -992,6 +1049,21 @@ __global__ __launch_bounds__(256) void linear_dgrad_wide_kernel(const uint16_t* 
   }
 }
 
+extern "C" int climsr_linear_dgrad_frag(const uint16_t* dy, const uint16_t* wf, int n, int k, int o, float* dx, int accumulate,
+                                        void* stream) {
+  if (!dy || !wf || !dx || n <= 0 || n > 64 || k % 128 || o % 64) {
+    set_error("linear_dgrad_frag: bad args (n=%d k=%d o=%d; need n<=64, k%%128==0, o%%64==0)", n, k, o);
+    return CLIMSR_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int nf = (n + 15) / 16;
+  dim3 gw(k / 128);
+  if (nf == 1) hipLaunchKernelGGL((linear_dgrad_wide_kernel<1, true>), gw, dim3(256), 0, s, dy, wf, n, k, o, dx, accumulate);
+  else if (nf == 2) hipLaunchKernelGGL((linear_dgrad_wide_kernel<2, true>), gw, dim3(256), 0, s, dy, wf, n, k, o, dx, accumulate);
+  else hipLaunchKernelGGL((linear_dgrad_wide_kernel<4, true>), gw, dim3(256), 0, s, dy, wf, n, k, o, dx, accumulate);
+  return check_launch("linear_dgrad_frag");
+}
+
 extern "C" int climsr_linear_dgrad(const uint16_t* dy, const uint16_t* w, int n, int k, int o, float* dx, int accumulate,
                                    void* stream) {
   if (!dy || !w || !dx || n <= 0 || n > 64 || k % 64 || o % 32) {
@@ -1002,9 +1074,9 @@ extern "C" int climsr_linear_dgrad(const uint16_t* dy, const uint16_t* w, int n,
   const int nf = (n + 15) / 16;
   if (k % 128 == 0) {
     dim3 gw(k / 128);
-    if (nf == 1) hipLaunchKernelGGL(linear_dgrad_wide_kernel<1>, gw, dim3(256), 0, s, dy, w, n, k, o, dx, accumulate);
-    else if (nf == 2) hipLaunchKernelGGL(linear_dgrad_wide_kernel<2>, gw, dim3(256), 0, s, dy, w, n, k, o, dx, accumulate);
-    else hipLaunchKernelGGL(linear_dgrad_wide_kernel<4>, gw, dim3(256), 0, s, dy, w, n, k, o, dx, accumulate);
+    if (nf == 1) hipLaunchKernelGGL((linear_dgrad_wide_kernel<1, false>), gw, dim3(256), 0, s, dy, w, n, k, o, dx, accumulate);
+    else if (nf == 2) hipLaunchKernelGGL((linear_dgrad_wide_kernel<2, false>), gw, dim3(256), 0, s, dy, w, n, k, o, dx, accumulate);
+    else hipLaunchKernelGGL((linear_dgrad_wide_kernel<4, false>), gw, dim3(256), 0, s, dy, w, n, k, o, dx, accumulate);
     return check_launch("linear_dgrad");
   }
   dim3 grid(k / 64);
@@ -1016,31 +1088,46 @@ extern "C" int climsr_linear_dgrad(const uint16_t* dy, const uint16_t* w, int n,
 
 // weight gradient dW[o][k] (+)= sum_n dy[n][o] x[n][k] with K = n_pad (multiple of 32):
 // A = dy^T [o][n_pad], B = x^T [k][n_pad] (both n-contiguous).  Each wave: 16 o x 64 k.
+// Optional second pair (dyt2, xt2, n_pad2): the same sum continued over a second batch, so two backward passes through
+// the layer (the discriminator's real and fake calls, pl_gan.py:51-61) write dW once instead of a write plus a
+// read-modify-write of the 411 MB fp32 gradient.
 __global__ __launch_bounds__(256) void linear_wgrad_kernel(const uint16_t* __restrict__ dyt, const uint16_t* __restrict__ xt, int n_pad,
-                                                           int k, int o, float* __restrict__ dw, int accumulate) {
+                                                           const uint16_t* __restrict__ dyt2, const uint16_t* __restrict__ xt2,
+                                                           int n_pad2, int k, int o, float* __restrict__ dw, int accumulate) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
   const int o0 = blockIdx.y * 64 + wave * 16;
   const int k0 = blockIdx.x * 64;
-  f32x4 acc[4];
+  // one accumulator set per batch, added in the order two separate launches would: (old + a) + b, bit-identical to
+  // them and to torch DDP's AccumulateGrad sum of the two calls' gradients
+  f32x4 acc[2][4];
 #pragma unroll
-  for (int f = 0; f < 4; ++f) acc[f] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int sidx = 0; sidx < 2; ++sidx)
+#pragma unroll
+    for (int f = 0; f < 4; ++f) acc[sidx][f] = (f32x4){0.f, 0.f, 0.f, 0.f};
   // A = x^T rows (k), B = dy^T columns (o): C[row = k (4g+i)][col = o], so a lane holds 4 consecutive k of one dW row
   // and stores (and, accumulating, loads) them as one 16 B vector (the dy-as-A form wrote 4 B per lane, k floats apart)
-  for (int nb = 0; nb < n_pad; nb += 32) {
-    const bf16x8 bo = *(const bf16x8*)(dyt + (long)(o0 + col) * n_pad + nb + g * 8);
+  auto run = [&](const uint16_t* dy_, const uint16_t* x_, int np, f32x4* ac) {
+    for (int nb = 0; nb < np; nb += 32) {
+      const bf16x8 bo = *(const bf16x8*)(dy_ + (long)(o0 + col) * np + nb + g * 8);
 #pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      const bf16x8 ak = *(const bf16x8*)(xt + (long)(k0 + f * 16 + col) * n_pad + nb + g * 8);
-      acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, bo, acc[f], 0, 0, 0);
+      for (int f = 0; f < 4; ++f) {
+        const bf16x8 ak = *(const bf16x8*)(x_ + (long)(k0 + f * 16 + col) * np + nb + g * 8);
+        ac[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, bo, ac[f], 0, 0, 0);
+      }
     }
-  }
+  };
+  run(dyt, xt, n_pad, acc[0]);
+  if (dyt2) run(dyt2, xt2, n_pad2, acc[1]);
   float* row = dw + (long)(o0 + col) * k + k0 + g * 4;
   float4 old[4];
 #pragma unroll
   for (int f = 0; f < 4; ++f) old[f] = accumulate ? *(const float4*)(row + f * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-  for (int f = 0; f < 4; ++f)
-    *(float4*)(row + f * 16) = make_float4(old[f].x + acc[f][0], old[f].y + acc[f][1], old[f].z + acc[f][2], old[f].w + acc[f][3]);
+  for (int f = 0; f < 4; ++f) {
+    float4 r = make_float4(old[f].x + acc[0][f][0], old[f].y + acc[0][f][1], old[f].z + acc[0][f][2], old[f].w + acc[0][f][3]);
+    if (dyt2) r = make_float4(r.x + acc[1][f][0], r.y + acc[1][f][1], r.z + acc[1][f][2], r.w + acc[1][f][3]);
+    *(float4*)(row + f * 16) = r;
+  }
 }
 
 extern "C" int climsr_linear_wgrad(const uint16_t* dy_t, const uint16_t* x_t, int n_pad, int k, int o, float* dw, int accumulate,
@@ -1049,9 +1136,20 @@ extern "C" int climsr_linear_wgrad(const uint16_t* dy_t, const uint16_t* x_t, in
     set_error("linear_wgrad: bad args (n_pad=%d k=%d o=%d)", n_pad, k, o);
     return CLIMSR_EINVAL;
   }
-  hipLaunchKernelGGL(linear_wgrad_kernel, dim3(k / 64, o / 64), dim3(256), 0, (hipStream_t)stream, dy_t, x_t, n_pad, k, o, dw,
-                     accumulate);
+  hipLaunchKernelGGL(linear_wgrad_kernel, dim3(k / 64, o / 64), dim3(256), 0, (hipStream_t)stream, dy_t, x_t, n_pad,
+                     (const uint16_t*)nullptr, (const uint16_t*)nullptr, 0, k, o, dw, accumulate);
   return check_launch("linear_wgrad");
+}
+
+extern "C" int climsr_linear_wgrad2(const uint16_t* dy_t, const uint16_t* x_t, int n_pad, const uint16_t* dy_t2, const uint16_t* x_t2,
+                                    int n_pad2, int k, int o, float* dw, int accumulate, void* stream) {
+  if (!dy_t || !x_t || !dy_t2 || !x_t2 || !dw || n_pad % 32 || n_pad2 % 32 || k % 64 || o % 64) {
+    set_error("linear_wgrad2: bad args (n_pad=%d n_pad2=%d k=%d o=%d)", n_pad, n_pad2, k, o);
+    return CLIMSR_EINVAL;
+  }
+  hipLaunchKernelGGL(linear_wgrad_kernel, dim3(k / 64, o / 64), dim3(256), 0, (hipStream_t)stream, dy_t, x_t, n_pad, dy_t2, x_t2,
+                     n_pad2, k, o, dw, accumulate);
+  return check_launch("linear_wgrad2");
 }
 
 // ---------------------------------------------------------------------------------------------

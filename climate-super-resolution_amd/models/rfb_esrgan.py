@@ -14,6 +14,7 @@ requires grad.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List
 
 import torch
@@ -48,11 +49,20 @@ class _DEngine:
                 plan.bind(m.weight, None, need_t=True)
                 self.layers.append((m, bn, plan))
         self.packer = BatchedPacker([p for _c, _b, p in self.layers], dev)
-        self.fc0_bf16 = torch.empty(d.fc[0].weight.shape, dtype=torch.bfloat16, device=dev)
+        # fc.0's bf16 MFMA copy in fragment order (CLIMSR_FC0_FRAG=1, ops.linear_pack_frag): the forward and data
+        # gradient stream it as whole 4 KB / 16 KB runs (-11 / -3 us per launch), but the AdamW pass that writes it
+        # costs as much more: off by default, the row-major copy and one AdamW launch
+        o0, k0 = d.fc[0].weight.shape
+        self.fc0_frag = (os.environ.get("CLIMSR_FC0_FRAG", "0") == "1" and o0 % 256 == 0 and k0 % 256 == 0
+                         and d._fc_flat_lo() % 4 == 0 and _lib.has("climsr_linear_fwd_frag"))
+        self.fc0_bf16 = torch.empty((o0 * k0,) if self.fc0_frag else (o0, k0), dtype=torch.bfloat16, device=dev)
         self.version = -1
         self.ws = Workspace()
         self.scratch: Dict[str, Tensor] = {}
         self.fuse_stem = True  # features.0 + features.2 as one launch (False: per layer; tools/perf_stem.py's A/B)
+        # the two D backwards of loss_d share one fc.0 weight-gradient launch (CLIMSR_FC0_WGRAD_MERGE=0: one each)
+        self.merge_wgrad = os.environ.get("CLIMSR_FC0_WGRAD_MERGE", "1") != "0" and _lib.has("climsr_linear_wgrad2")
+        self._wpend = None
 
     def ensure_packed(self):
         v = self.d._flat._version
@@ -63,7 +73,11 @@ class _DEngine:
         """mirror_done: the optimizer's AdamW pass already wrote fc0_bf16 (climsr_adamw_step_mirror)."""
         self.packer.run()
         if not mirror_done:
-            ops.f32_to_bf16(self.d.fc[0].weight, self.fc0_bf16)
+            w0 = self.d.fc[0].weight
+            if self.fc0_frag:
+                ops.linear_pack_frag(w0, w0.shape[0], w0.shape[1], self.fc0_bf16)
+            else:
+                ops.f32_to_bf16(w0, self.fc0_bf16)
         self.version = self.d._flat._version
 
     def _scr(self, key, shape, dtype, dev):
@@ -150,7 +164,8 @@ class _DEngine:
         hid = _f32((n, fc0.out_features), dev)
         nsplit_max = 3072 // ((fc0.out_features + 63) // 64) + 1
         lin_ws = self._scr("linws", (nsplit_max * n * fc0.out_features,), torch.float32, dev)
-        ops.linear_fwd(p, self.fc0_bf16, fc0.bias, n, feat, fc0.out_features, hid, lin_ws, act=ACT_LRELU, slope=0.2)
+        lin = ops.linear_fwd_frag if self.fc0_frag else ops.linear_fwd
+        lin(p, self.fc0_bf16, fc0.bias, n, feat, fc0.out_features, hid, lin_ws, act=ACT_LRELU, slope=0.2)
         s = _f32((n, 1), dev)
         ops.d_head_fwd(hid, fc2.weight, fc2.bias, n, fc0.out_features, s)
         sv = None
@@ -159,7 +174,15 @@ class _DEngine:
         return s, sv
 
     # ------------------------------------------------------------------ backward
-    def backward(self, ds: Tensor, sv: dict, need_w: bool, need_x: bool, accumulate: bool):
+    def flush_wgrad(self):
+        """Launch a held fc.0 weight gradient (backward's defer) that no second call of the pass picked up."""
+        pend, self._wpend = self._wpend, None
+        if pend is not None:
+            du0_t, p_t, n_pad, w0g, acc, feat, o, stream = pend
+            with torch.cuda.stream(stream):
+                ops.linear_wgrad(du0_t, p_t, n_pad, feat, o, w0g, acc)
+
+    def backward(self, ds: Tensor, sv: dict, need_w: bool, need_x: bool, accumulate: bool, defer: bool = False):
         d = self.d
         dev = ds.device
         n, n_pad, feat = sv["n"], sv["n_pad"], sv["feat"]
@@ -180,11 +203,26 @@ class _DEngine:
             if calls < d._ready_need:
                 hook = None
         if need_w:
-            ops.linear_wgrad(du0_t, sv["p_t"], n_pad, feat, o, fc0.weight.grad, acc)
+            w0g = fc0.weight.grad
+            pend = self._wpend
+            if pend is not None and (pend[3].data_ptr() != w0g.data_ptr() or pend[2] % 32 or n_pad % 32):
+                self.flush_wgrad()
+                pend = None
+            if pend is not None:  # the pass's other D call: one weight-gradient launch for both batches
+                self._wpend = None
+                ops.linear_wgrad2(pend[0], pend[1], pend[2], du0_t, sv["p_t"], n_pad, feat, o, w0g, pend[4])
+            elif defer and hook is None and self.merge_wgrad:
+                # loss_d backpropagates through D twice in one pass (real and fake, pl_gan.py:51-61): hold this call's
+                # fc.0 operands so the next call writes the 411 MB gradient once; a pass with no second call launches
+                # it from the end-of-pass callback, on this call's stream
+                self._wpend = (du0_t, sv["p_t"], n_pad, w0g, acc, feat, o, torch.cuda.current_stream(dev))
+                torch.autograd.Variable._execution_engine.queue_callback(self.flush_wgrad)
+            else:
+                ops.linear_wgrad(du0_t, sv["p_t"], n_pad, feat, o, w0g, acc)
             if hook is not None:  # fc.0 / fc.2: the last flat entries, 103 M of 107 M parameters
                 hook(d._fc_flat_lo())
         dp = self._scr("dp", (n, feat), torch.float32, dev)
-        ops.linear_dgrad(du0, self.fc0_bf16, n, feat, o, dp)
+        (ops.linear_dgrad_frag if self.fc0_frag else ops.linear_dgrad)(du0, self.fc0_bf16, n, feat, o, dp)
         hh, ww, c = sv["hh"], sv["ww"], sv["c"]
         da = _f32((n, hh, ww, c), dev)
         ops.adaptive_pool_bwd(dp, n, hh, ww, c, POOL, POOL, da)
@@ -274,7 +312,7 @@ class _DFn(torch.autograd.Function):
             ctx.sv = None
             return (dx, None) + engine.d._end_autograd_grads(buf, prev, ctx.needs_input_grad[2:])
         acc = engine.d.grads_as_views() if need_w else True
-        dx = engine.backward(ds, sv, need_w, need_x, acc)
+        dx = engine.backward(ds, sv, need_w, need_x, acc, defer=True)
         ctx.sv = None
         return (dx, None) + tuple(None for _ in range(len(ctx.needs_input_grad) - 2))
 
@@ -335,9 +373,10 @@ class RFBESRGANDiscriminator(FlatParamsMixin, nn.Module):
         object.__setattr__(self, "_ready_need", max(1, int(calls_per_step)))
 
     def bf16_mirror(self):
-        """(flat offset, numel, bf16 buffer) of fc.0's weight: its MFMA copy, written by the fused AdamW pass."""
+        """(flat offset, numel, bf16 buffer, (o, k) or None) of fc.0's weight: its MFMA copy, written by the fused AdamW
+        pass; (o, k) when the copy is in fragment order."""
         eng = self.engine()
-        return self._fc_flat_lo(), self.fc[0].weight.numel(), eng.fc0_bf16
+        return self._fc_flat_lo(), self.fc[0].weight.numel(), eng.fc0_bf16, tuple(self.fc[0].weight.shape) if eng.fc0_frag else None
 
     def grad_ready_los(self):
         """The flat offsets the backward reports through the grad-ready hook, in its order (fc first, then the conv

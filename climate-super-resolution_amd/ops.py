@@ -674,10 +674,41 @@ def linear_dgrad(dy, w, n, k, o, dx, accumulate=False):
         "dgrad fc.0")
 
 
+def linear_pack_frag(w, o, k, wf):
+    """fp32 [o][k] -> bf16 fragment order (include/climsr_hip.h climsr_linear_pack_frag)."""
+    _launch("linear_pack_frag", lambda: _L().climsr_linear_pack_frag(ptr(w), o, k, ptr(wf), _lib.stream_ptr()))
+
+
+def linear_fwd_frag(x, wf, bias, n, k, o, y, ws, act=ACT_NONE, slope=0.2):
+    """linear_fwd with the weight in fragment order (linear_pack_frag / the fragment-order AdamW mirror)."""
+    _run("linear_fwd_wide_kernel", 2 * n * k * o, lambda: check(
+        _L().climsr_linear_fwd_frag(ptr(x), ptr(wf), ptr(bias), n, k, o, act, slope, ptr(ws), ws.numel(), ptr(y), _lib.stream_ptr()),
+        "linear_fwd_frag"), "fwd fc.0")
+
+
+def linear_dgrad_frag(dy, wf, n, k, o, dx, accumulate=False):
+    _run("linear_dgrad_wide_kernel", 2 * n * k * o, lambda: check(
+        _L().climsr_linear_dgrad_frag(ptr(dy), ptr(wf), n, k, o, ptr(dx), int(accumulate), _lib.stream_ptr()), "linear_dgrad_frag"),
+        "dgrad fc.0")
+
+
+def linear_frag_order(w):
+    """Host-side (torch) fragment order of a [o][k] tensor -- the layout climsr_linear_pack_frag writes (tests only)."""
+    o, k = w.shape
+    return w.reshape(o // 64, 4, 16, k // 32, 4, 8).permute(0, 3, 1, 4, 2, 5).reshape(-1)
+
+
 def linear_wgrad(dy_t, x_t, n_pad, k, o, dw, accumulate):
     _run("linear_wgrad_kernel", 2 * n_pad * k * o, lambda: check(
         _L().climsr_linear_wgrad(ptr(dy_t), ptr(x_t), n_pad, k, o, ptr(dw), int(accumulate), _lib.stream_ptr()), "linear_wgrad"),
         "wgrad fc.0")
+
+
+def linear_wgrad2(dy_t, x_t, n_pad, dy_t2, x_t2, n_pad2, k, o, dw, accumulate):
+    """linear_wgrad over two batches in one launch: dw (+)= dy_t . x_t^T + dy_t2 . x_t2^T."""
+    _run("linear_wgrad_kernel", 2 * (n_pad + n_pad2) * k * o, lambda: check(
+        _L().climsr_linear_wgrad2(ptr(dy_t), ptr(x_t), n_pad, ptr(dy_t2), ptr(x_t2), n_pad2, k, o, ptr(dw), int(accumulate),
+                                  _lib.stream_ptr()), "linear_wgrad2"), "wgrad fc.0")
 
 
 def d_head_fwd(h, w2, b2, n, o, s, sigmoid=True):

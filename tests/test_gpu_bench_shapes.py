@@ -479,3 +479,83 @@ def test_linear_fwd_dgrad_wgrad_vs_float64(n, k, o):
         ops.linear_wgrad(dy_t, x_t, n_pad, k, o, dw, accumulate=False)
         torch.cuda.synchronize()
         close(dw, dy.double().t() @ x.double(), rel=1e-5, what="linear wgrad")
+
+
+@pytest.mark.parametrize("n,k,o", [(32, 100352, 1024), (5, 4096, 256)])
+def test_linear_frag_order_matches_row_major(n, k, o):
+    """fc.0 with its bf16 weight in fragment order (climsr_linear_pack_frag, include/climsr_hip.h): the pack equals the
+    host-side permutation of the row-major bf16 copy, and the fragment-order forward / data gradient are bit-identical
+    to the row-major kernels (same fragments, same MFMA order)."""
+    from climsr_amd import ops
+
+    g = torch.Generator(device=DEV).manual_seed(7 * n + o)
+    w32 = torch.randn((o, k), generator=g, device=DEV) / k ** 0.5
+    w = w32.to(torch.bfloat16)
+    wf = torch.empty(o * k, dtype=torch.bfloat16, device=DEV)
+    ops.linear_pack_frag(w32, o, k, wf)
+    torch.cuda.synchronize()
+    assert torch.equal(wf, ops.linear_frag_order(w)), "pack_frag != permuted row-major bf16"
+    x = (torch.randn((n, k), generator=g, device=DEV) * 0.5).to(torch.bfloat16)
+    b = torch.randn(o, generator=g, device=DEV) * 0.1
+    ws = torch.empty((3072 // max(1, o // 64) + 2) * n * o, device=DEV)
+    y0, y1 = torch.empty((n, o), device=DEV), torch.empty((n, o), device=DEV)
+    ops.linear_fwd(x, w, b, n, k, o, y0, ws, act=ops.ACT_LRELU, slope=0.2)
+    ops.linear_fwd_frag(x, wf, b, n, k, o, y1, ws, act=ops.ACT_LRELU, slope=0.2)
+    dy = torch.randn((n, o), generator=g, device=DEV).to(torch.bfloat16)
+    dx0, dx1 = torch.full((n, k), 0.25, device=DEV), torch.full((n, k), 0.25, device=DEV)
+    ops.linear_dgrad(dy, w, n, k, o, dx0, accumulate=True)
+    ops.linear_dgrad_frag(dy, wf, n, k, o, dx1, accumulate=True)
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1), f"fwd frag vs row-major: max diff {float((y0 - y1).abs().max()):.3e}"
+    assert torch.equal(dx0, dx1), f"dgrad frag vs row-major: max diff {float((dx0 - dx1).abs().max()):.3e}"
+    close(y1, F.leaky_relu(x.double() @ w.double().t() + b.double(), 0.2), rel=1e-5, what="linear fwd (frag)")
+
+
+def test_adamw_mirror_frag_matches_row_major_mirror():
+    """climsr_adamw_step_mirror_frag: p / m / v bit-identical to climsr_adamw_step_mirror over a flat buffer with the
+    mirrored [o][k] block inside it (parameters before and after, a ragged tail), and the bf16 copy equal to the
+    row-major mirror in fragment order."""
+    from climsr_amd import _lib, ops
+
+    lib = _lib.load()
+    o, k, lo, tail = 128, 1024, 100, 37
+    n = lo + o * k + tail
+    g = torch.Generator(device=DEV).manual_seed(3)
+    p0 = torch.randn(n, generator=g, device=DEV)
+    gr = torch.randn(n, generator=g, device=DEV) * 0.1
+    m0 = torch.randn(n, generator=g, device=DEV) * 0.01
+    v0 = torch.rand(n, generator=g, device=DEV) * 1e-3
+    hp = torch.tensor([1e-3, 0.9, 0.999, 1e-8, 1e-4, 1e-3 / 0.1, 0.999 ** 0.5 / 0.1 ** 0.5, 0.0], device=DEV)
+    a = [t.clone() for t in (p0, m0, v0)]
+    b = [t.clone() for t in (p0, m0, v0)]
+    mir_rm = torch.empty(o * k, dtype=torch.bfloat16, device=DEV)
+    mir_fr = torch.empty(o * k, dtype=torch.bfloat16, device=DEV)
+    s = _lib.stream_ptr()
+    ptr = lambda t: t.data_ptr()  # noqa: E731
+    _lib.check(lib.climsr_adamw_step_mirror(n, ptr(a[0]), ptr(gr), ptr(a[1]), ptr(a[2]), ptr(hp), lo, o * k, ptr(mir_rm), s), "rm")
+    _lib.check(lib.climsr_adamw_step_mirror_frag(n, ptr(b[0]), ptr(gr), ptr(b[1]), ptr(b[2]), ptr(hp), lo, o, k, ptr(mir_fr), s), "frag")
+    torch.cuda.synchronize()
+    for name, x, y in zip("pmv", a, b):
+        assert torch.equal(x, y), f"adamw {name}: frag pass differs from the row-major pass"
+    assert torch.equal(mir_fr, ops.linear_frag_order(mir_rm.view(o, k))), "fragment-order mirror != permuted row-major mirror"
+    assert lib.climsr_adamw_step_mirror_frag(n, ptr(b[0]), ptr(gr), ptr(b[1]), ptr(b[2]), ptr(hp), lo + 2, o, k, ptr(mir_fr), s) != 0
+
+
+@pytest.mark.parametrize("acc", [False, True])
+def test_linear_wgrad2_two_batches_vs_float64(acc):
+    """climsr_linear_wgrad2: fc.0's weight gradient over the discriminator's two backward calls of loss_d (real and fake
+    batches, pl_gan.py:51-61) in one launch, with and without accumulation, vs float64 at the bench shape."""
+    from climsr_amd import ops
+
+    n, k, o = 32, 100352, 1024
+    g = torch.Generator(device=DEV).manual_seed(11 + int(acc))
+    cols = []
+    for _ in range(2):
+        dy_t = torch.randn((o, n), generator=g, device=DEV).to(torch.bfloat16)
+        x_t = (torch.randn((k, n), generator=g, device=DEV) * 0.5).to(torch.bfloat16)
+        cols.append((dy_t, x_t))
+    dw = torch.full((o, k), 0.5, device=DEV)
+    ops.linear_wgrad2(cols[0][0], cols[0][1], n, cols[1][0], cols[1][1], n, k, o, dw, acc)
+    torch.cuda.synchronize()
+    want = sum(dy_t.double() @ x_t.double().t() for dy_t, x_t in cols)
+    close(dw - 0.5 if acc else dw, want, rel=1e-5, what="linear wgrad2")
