@@ -556,9 +556,12 @@ __global__ __launch_bounds__(256) void adaptive_pool_fwd_tile_kernel(const uint1
   const int b = blockIdx.y, c0 = blockIdx.x * AP_CB, hw = h * w, pitch = hw + 1, no = oh * ow;
   ap_win_tables(h, w, oh, ow, ty0, ty1, tx0, tx1);
   const uint16_t* xb = x + (long)b * hw * c + c0;
-  for (int i = threadIdx.x; i < hw * AP_CB; i += 256) {  // coalesced NHWC read (64 channels = 128 B per pixel)
-    const int px = i / AP_CB, ch = i - px * AP_CB;
-    xs[ch * pitch + px] = xb[(long)px * c + ch];
+  for (int i = threadIdx.x; i < hw * (AP_CB / 8); i += 256) {  // coalesced NHWC read, 16 B (8 channels) per lane
+    const int px = i >> 3, cv = i & 7;
+    const uint4 u = *(const uint4*)(xb + (long)px * c + cv * 8);
+    const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xs[(cv * 8 + j) * pitch + px] = (uint16_t)(wd[j >> 1] >> (16 * (j & 1)));
   }
   __syncthreads();
   const int r0 = no * blockIdx.z / AP_SPLIT, r1 = no * (blockIdx.z + 1) / AP_SPLIT, nr = r1 - r0;
@@ -601,17 +604,22 @@ __global__ __launch_bounds__(256) void adaptive_pool_bwd_tile_kernel(const float
   ap_cand_tables(h, oh, rc, re);
   ap_cand_tables(w, ow, cc_, ce);
   const float* db = dp + (long)b * c * no + (long)c0 * no;
-  for (int i = threadIdx.x; i < AP_CB * no; i += 256) {  // contiguous read of the 64 channels' pooled gradients
-    const int ch = i / no;
-    ds[ch * pitch + (i - ch * no)] = db[i];
+  for (int i4 = threadIdx.x * 4; i4 < AP_CB * no; i4 += 1024) {  // contiguous 16 B reads of the pooled gradients
+    const float4 f = *(const float4*)(db + i4);
+    const float fv[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = i4 + j, ch = i / no;
+      ds[ch * pitch + (i - ch * no)] = fv[j];
+    }
   }
   __syncthreads();
   const int y0 = h * blockIdx.z / AP_SPLIT, y1 = h * (blockIdx.z + 1) / AP_SPLIT;
   float* xb = dx + (long)b * h * w * c + c0;
-  const int ch = threadIdx.x % AP_CB;
-  for (int q = threadIdx.x / AP_CB; q < (y1 - y0) * w; q += 256 / AP_CB) {  // (pixel, channel), channel fastest
+  const int cq = threadIdx.x % (AP_CB / 4);  // 4 channels per lane: one 16 B store per pixel
+  for (int q = threadIdx.x / (AP_CB / 4); q < (y1 - y0) * w; q += 256 / (AP_CB / 4)) {  // (pixel, channel quad)
     const int yy = y0 + q / w, xx = q - (q / w) * w;
-    float sm = 0.f;
+    float sm[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int u = 0; u < AP_MAXC; ++u) {
       const int oi = rc[yy][u];
@@ -620,10 +628,12 @@ __global__ __launch_bounds__(256) void adaptive_pool_bwd_tile_kernel(const float
       for (int v = 0; v < AP_MAXC; ++v) {
         const int oj = cc_[xx][v];
         if (oj < 0) break;
-        sm += ds[ch * pitch + oi * ow + oj] / (float)(re[yy][u] * ce[xx][v]);
+        const float den = (float)(re[yy][u] * ce[xx][v]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sm[j] += ds[(cq * 4 + j) * pitch + oi * ow + oj] / den;
       }
     }
-    xb[((long)yy * w + xx) * c + ch] = sm;
+    *(float4*)(xb + ((long)yy * w + xx) * c + cq * 4) = make_float4(sm[0], sm[1], sm[2], sm[3]);
   }
 }
 

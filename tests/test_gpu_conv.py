@@ -563,12 +563,13 @@ def test_conv_fwd_stride2_plain_bf16(cin, cout, h, w, n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cin,cout,stride,h,w", [(64, 128, 1, 32, 48), (128, 128, 2, 34, 40), (64, 64, 2, 64, 64), (64, 64, 1, 32, 32)])
+@pytest.mark.parametrize("cin,cout,stride,h,w", [(64, 128, 1, 32, 48), (128, 128, 2, 34, 40), (64, 64, 2, 64, 64), (64, 64, 1, 32, 32),
+                                                 (64, 128, 1, 128, 128), (128, 512, 2, 256, 160)])
 def test_conv_bn_partials_match_bn_forward(cin, cout, stride, h, w):
     """BatchNorm statistics from the conv epilogue (ClimsrEpilogue.bn_part -> climsr_bn_forward_parts; the discriminator's
     train-mode conv + BatchNorm2d + LeakyReLU, rfb_esrgan.py:30-50) vs climsr_bn_forward's own pass over the same z:
     batch mean / rstd / running stats within fp32 summation-order noise, the activation within one bf16 ulp.  A conv
-    whose kernel cannot emit partials (64 -> 64 stride 1: conv_pw) reports 0 rows."""
+    whose kernel cannot emit partials (64 -> 64 stride 1: conv_pw) reports 0 rows.  The last two: 128 and 80 partial rows."""
     from climsr_amd import ops
 
     n = 2

@@ -115,3 +115,30 @@ def test_channel_attention_and_rcab_residual():
     x_ref2 = ub.double().cpu() * s.cpu().double()[:, None, None, :] + xres.double()
     assert (xr2.cpu().double() - x_ref2).abs().max() <= 1e-5 * x_ref2.abs().max()
     assert torch.equal(xb2.cpu(), xr2.cpu().to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("n,tpi,c,cr", [(2, 1035, 64, 4), (1, 7, 64, 4), (3, 300, 96, 6), (1, 50, 1024, 16)])
+def test_channel_attention_parts_vs_float64(n, tpi, c, cr):
+    """climsr_channel_attention_parts (tile sums folded into fp64 slices -> mean -> 1x1-ReLU-1x1-sigmoid, CALayer
+    rcan.py:50-69) from per-tile channel sums as the RCAB conv2 epilogue writes them, vs float64; ragged tile counts,
+    wide c."""
+    from climsr_amd import _lib
+    from climsr_amd._lib import check, ptr
+
+    g = torch.Generator().manual_seed(tpi + c)
+    part = torch.randn((n, tpi, c), generator=g) * 30.0
+    hw = tpi * 256
+    w1 = torch.randn((cr, c), generator=g) * 0.2
+    b1 = torch.randn((cr,), generator=g) * 0.1
+    w2 = torch.randn((c, cr), generator=g) * 0.2
+    b2 = torch.randn((c,), generator=g) * 0.1
+    L = _lib.load()
+    d = {k: v.to(DEV).contiguous() for k, v in dict(part=part, w1=w1, b1=b1, w2=w2, b2=b2).items()}
+    s = torch.empty((n, c), device=DEV)
+    ws = torch.empty(L.climsr_channel_attention_workspace(n, c) // 8, dtype=torch.float64, device=DEV)
+    check(L.climsr_channel_attention_parts(ptr(d["part"]), n, tpi, hw, c, ptr(d["w1"]), ptr(d["b1"]), ptr(d["w2"]), ptr(d["b2"]), cr,
+                                           ptr(ws), ptr(s), _lib.stream_ptr()), "ca parts")
+    torch.cuda.synchronize()
+    mean = part.double().sum(1) / hw
+    s_ref = torch.sigmoid(torch.relu(mean @ w1.double().T + b1.double()) @ w2.double().T + b2.double())
+    assert (s.cpu().double() - s_ref).abs().max() <= 1e-5
