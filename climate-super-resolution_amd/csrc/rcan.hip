@@ -11,6 +11,7 @@ using namespace climsr;
 
 namespace {
 constexpr int POOL_SPLIT = 256;  // pixel slices per image of the pooling pass (>= 1 block per CU for one grid)
+constexpr int TILE_SPLIT = 256;  // slices per image of the per-tile sums (channel_attention_parts; 64 measured neutral)
 }
 
 // part[n][split][c] = sum over the split's pixels of x[n][p][c] (fp32 NHWC, cstride).  A block is
@@ -43,41 +44,69 @@ __global__ __launch_bounds__(256) void channel_sum_partial_kernel(const float* _
 }
 
 // s[n][c] = sigmoid(W2 relu(W1 mean + b1) + b2)  (conv_du of CALayer on the pooled [n, c, 1, 1] map)
-__global__ __launch_bounds__(1024) void ca_mlp_kernel(const double* __restrict__ part, long hw, int c, int cr, const float* __restrict__ w1,
+// The slice sums of a slice group are loaded 4 at a time (independent fp64 chains, combined in a fixed order); W1 / W2
+// are staged in LDS by every thread at once when they fit; a hidden unit is one wave's strided dot product finished
+// by a fixed xor-shuffle tree (the serial per-thread loops over global W1 / W2 took most of this kernel's 8.9 us).
+constexpr int CA_STAGE_MAX = 8192;  // floats of W1 + W2 staged in LDS
+__global__ __launch_bounds__(1024) void ca_mlp_kernel(const double* __restrict__ part, int nsl, long hw, int c, int cr, const float* __restrict__ w1,
                               const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2,
                               float* __restrict__ s) {
   extern __shared__ float sm[];
   float* mean = sm;      // [c]
   float* hid = sm + c;   // [cr]
+  __shared__ float wst[CA_STAGE_MAX];
   constexpr int NT = 1024;
   __shared__ double grp[NT];
-  const int nimg = blockIdx.x;
+  const int nimg = blockIdx.x, t = threadIdx.x;
+  const bool staged = 2 * cr * c <= CA_STAGE_MAX;
+  if (staged)
+    for (int i = t; i < cr * c; i += NT) {
+      wst[i] = w1[i];
+      wst[cr * c + i] = w2[i];
+    }
+  const float* W1 = staged ? wst : w1;
+  const float* W2 = staged ? wst + cr * c : w2;
   const int cw = c < NT ? c : NT;  // channels per round
   const int G = NT / cw;           // split groups summed in parallel, then combined in a fixed order
   for (int c0 = 0; c0 < c; c0 += cw) {
-    const int i = c0 + (int)threadIdx.x % cw, gi = (int)threadIdx.x / cw;
-    double t = 0.0;
-    if (i < c && gi < G)
-      for (int sp = gi; sp < POOL_SPLIT; sp += G) t += part[((long)nimg * POOL_SPLIT + sp) * c + i];
-    grp[threadIdx.x] = t;
+    const int i = c0 + t % cw, gi = t / cw;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    if (i < c && gi < G) {
+      const double* pp = part + (long)nimg * nsl * c + i;
+      int sp = gi;
+      for (; sp + 3 * G < nsl; sp += 4 * G) {
+        a0 += pp[(long)sp * c];
+        a1 += pp[(long)(sp + G) * c];
+        a2 += pp[(long)(sp + 2 * G) * c];
+        a3 += pp[(long)(sp + 3 * G) * c];
+      }
+      for (; sp < nsl; sp += G) a0 += pp[(long)sp * c];
+    }
+    grp[t] = (a0 + a1) + (a2 + a3);
     __syncthreads();
-    if ((int)threadIdx.x < cw && c0 + (int)threadIdx.x < c) {
+    if (t < cw && c0 + t < c) {
       double m = 0.0;
-      for (int k = 0; k < G; ++k) m += grp[k * cw + threadIdx.x];
-      mean[c0 + threadIdx.x] = (float)(m / (double)hw);
+      for (int k = 0; k < G; ++k) m += grp[k * cw + t];
+      mean[c0 + t] = (float)(m / (double)hw);
     }
     __syncthreads();
   }
-  for (int j = threadIdx.x; j < cr; j += blockDim.x) {
-    float t = b1 ? b1[j] : 0.f;
-    for (int i = 0; i < c; ++i) t += w1[j * c + i] * mean[i];
-    hid[j] = t > 0.f ? t : 0.f;
+  const int wave = t >> 6, lane = t & 63;
+  for (int j = wave; j < cr; j += NT / 64) {
+    float v = 0.f;
+    for (int i = lane; i < c; i += 64) v += W1[j * c + i] * mean[i];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if (lane == 0) {
+      v += b1 ? b1[j] : 0.f;
+      hid[j] = v > 0.f ? v : 0.f;
+    }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < c; i += blockDim.x) {
-    float t = b2 ? b2[i] : 0.f;
-    for (int j = 0; j < cr; ++j) t += w2[i * cr + j] * hid[j];
-    s[nimg * c + i] = 1.f / (1.f + expf(-t));
+  for (int i = t; i < c; i += NT) {
+    float v = b2 ? b2[i] : 0.f;
+    for (int j = 0; j < cr; ++j) v += W2[i * cr + j] * hid[j];
+    s[nimg * c + i] = 1.f / (1.f + expf(-v));
   }
 }
 
@@ -90,19 +119,19 @@ extern "C" int climsr_channel_attention(const float* u, int n, int64_t hw, int c
   }
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(channel_sum_partial_kernel, dim3(POOL_SPLIT, n), dim3(256), 0, st, u, (long)hw, c, u_cstride, workspace);
-  hipLaunchKernelGGL(ca_mlp_kernel, dim3(n), dim3(1024), (size_t)(c + cr) * sizeof(float), st, workspace, (long)hw, c, cr, w1, b1,
+  hipLaunchKernelGGL(ca_mlp_kernel, dim3(n), dim3(1024), (size_t)(c + cr) * sizeof(float), st, workspace, POOL_SPLIT, (long)hw, c, cr, w1, b1,
                      w2, b2, s);
   return check_launch("channel_attention");
 }
 
 extern "C" size_t climsr_channel_attention_workspace(int n, int c) { return (size_t)n * POOL_SPLIT * c * sizeof(double); }
 
-// channel_attention from per-tile channel sums: the image's tile rows folded into POOL_SPLIT fp64 slices (slice sp =
-// tiles [tpi sp / POOL_SPLIT, tpi (sp + 1) / POOL_SPLIT), summed in order), then ca_mlp_kernel over the slices -- the
+// channel_attention from per-tile channel sums: the image's tile rows folded into TILE_SPLIT fp64 slices (slice sp =
+// tiles [tpi sp / TILE_SPLIT, tpi (sp + 1) / TILE_SPLIT), summed in order), then ca_mlp_kernel over the slices -- the
 // same fixed order every run.  One workgroup per (slice, image): 256 threads = 4 tile lanes x 64 channels per round.
 __global__ __launch_bounds__(256) void tile_parts_fold_kernel(const float* __restrict__ part, int tpi, int c, double* __restrict__ out) {
   const int nimg = blockIdx.y, sp = blockIdx.x;
-  const long t0 = (long)tpi * sp / POOL_SPLIT, t1 = (long)tpi * (sp + 1) / POOL_SPLIT;
+  const long t0 = (long)tpi * sp / TILE_SPLIT, t1 = (long)tpi * (sp + 1) / TILE_SPLIT;
   __shared__ double sh[256];
   for (int c0 = 0; c0 < c; c0 += 64) {
     const int ch = c0 + (threadIdx.x & 63), tl = threadIdx.x >> 6;
@@ -112,7 +141,7 @@ __global__ __launch_bounds__(256) void tile_parts_fold_kernel(const float* __res
     sh[threadIdx.x] = t;
     __syncthreads();
     if (threadIdx.x < 64 && ch < c)
-      out[((long)nimg * POOL_SPLIT + sp) * c + ch] = ((sh[threadIdx.x] + sh[64 + threadIdx.x]) + sh[128 + threadIdx.x]) + sh[192 + threadIdx.x];
+      out[((long)nimg * TILE_SPLIT + sp) * c + ch] = ((sh[threadIdx.x] + sh[64 + threadIdx.x]) + sh[128 + threadIdx.x]) + sh[192 + threadIdx.x];
     __syncthreads();
   }
 }
@@ -125,8 +154,8 @@ extern "C" int climsr_channel_attention_parts(const float* part, int n, int tile
     return CLIMSR_EINVAL;
   }
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(tile_parts_fold_kernel, dim3(POOL_SPLIT, n), dim3(256), 0, st, part, tiles_per_image, c, workspace);
-  hipLaunchKernelGGL(ca_mlp_kernel, dim3(n), dim3(1024), (size_t)(c + cr) * sizeof(float), st, workspace, (long)hw, c, cr, w1, b1,
+  hipLaunchKernelGGL(tile_parts_fold_kernel, dim3(TILE_SPLIT, n), dim3(256), 0, st, part, tiles_per_image, c, workspace);
+  hipLaunchKernelGGL(ca_mlp_kernel, dim3(n), dim3(1024), (size_t)(c + cr) * sizeof(float), st, workspace, TILE_SPLIT, (long)hw, c, cr, w1, b1,
                      w2, b2, s);
   return check_launch("channel_attention_parts");
 }

@@ -1,4 +1,4 @@
-# Round 5, call t: RCAN's one-launch channel attention (ca_parts_mlp_kernel, batched 16 B loads) and the 16 B
+# Round 5, call t: RCAN channel attention (call t: one-launch ca_parts_mlp_kernel; call u: ca_mlp_kernel with staged weights) and the 16 B
 # adaptive-pool tile kernels: their tests, a rocprofv3 kernel-stats pass of the RCAN whole-grid bench, then the RCAN
 # and GAN benches.   usage: bash tools/gpu_r05t.sh <tag>
 set -o pipefail
