@@ -214,6 +214,15 @@ SIGNATURES = {
     "climsr_conv2d_fwd_ch_parts": (ctypes.c_int64, [P(ConvDesc), P(Epilogue), c_void_p]),
     "climsr_ca_scale_add": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int64, c_int, c_void_p]),
     "climsr_pixel_shuffle_bf16": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
+    "climsr_pixel_unshuffle_bf16": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
+    "climsr_channel_attention_mean": (c_int, [c_void_p, c_int, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                              c_void_p, c_void_p, c_void_p, c_void_p]),
+    "climsr_channel_attention_parts_mean": (c_int, [c_void_p, c_int, c_int, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                                    c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "climsr_ca_backward_workspace": (c_size_t, [c_int, c_int64, c_int, c_int]),
+    "climsr_ca_backward": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int64, c_int, c_void_p,
+                                   c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,
+                                   c_void_p]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

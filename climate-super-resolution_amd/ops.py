@@ -192,7 +192,8 @@ class ConvPlan:
     def dgrad(self, dz: torch.Tensor, dz_cs: int, out_h: int, out_w: int, g: torch.Tensor, g_cs: int, g_co: int, n: int,
               accumulate: bool = False, down2: bool = False, cout_t: Optional[int] = None, aux: Optional[torch.Tensor] = None,
               aux_cs: int = 0, aux_co: int = 0, aux_scale: float = 1.0, act: int = ACT_NONE, res1: Optional[torch.Tensor] = None,
-              res1_cs: int = 0, res1_co: int = 0, bn_bwd: Optional[tuple] = None) -> None:
+              res1_cs: int = 0, res1_co: int = 0, bn_bwd: Optional[tuple] = None, res2: Optional[torch.Tensor] = None,
+              res2_cs: int = 0, res2_co: int = 0) -> None:
         """Data gradient: g[:, :, :, g_co:g_co+cin_real] (+)= conv^T(dz); (out_h, out_w) are dz's dims.  g is fp32
         (= or += with accumulate), or bf16: then it is the NEXT layer's conv output gradient directly, with
         act = ACT_LRELU_BWD / ACT_RELU_BWD applied from that layer's stored activation res1.  With down2 the
@@ -200,11 +201,12 @@ class ConvPlan:
         Stride-2 convs (pad 1, even input) run as a stride-1 conv over the zero-inserted dz.
         bn_bwd = (part, z, z_cs, mean, rstd, gamma, beta): g (bf16) is dL/da of the previous BatchNorm + LeakyReLU(0.2)
         layer and the epilogue writes that layer's backward statistics partials into part (fp64, dgrad_bn_parts() rows x 2
-        x cin) for bn_backward_parts."""
+        x cin) for bn_backward_parts.  With act = ACT_NONE, res1 / res2 (bf16 or fp32, dtype decides) are added to the
+        result (g = conv^T(dz) + res1 + res2; the aux copy is of that sum)."""
         ct = self.cout_t if cout_t is None else cout_t
         if (self.cout == 1 and self.stride == 1 and self.ks in (3, 5) and self.pad == self.ks // 2 and g.dtype == torch.bfloat16
                 and not down2 and aux is None and act in (ACT_NONE, ACT_LRELU_BWD, ACT_RELU_BWD) and ct == self.cin_real
-                and ct in (32, 64)):
+                and ct in (32, 64) and res2 is None and (res1 is None or act != ACT_NONE)):
             # one output channel: its data gradient is a 1 -> C stencil (climsr_dgrad_single_output), not a GEMM
             hw = n * out_h * out_w
             nbytes = hw * 2 + hw * ct * 2 * (2 if res1 is not None else 1)
@@ -218,8 +220,10 @@ class ConvPlan:
         d = self._dgrad_desc(dz_cs, out_h, out_w, g_cs, g_co, n, ct)
         out_h, out_w = d.out_h, d.out_w
         mode = OUT_BF16 if g.dtype == torch.bfloat16 else (OUT_F32_ADD if accumulate else OUT_F32)
-        ep = Epilogue(act, 0.2 if act == ACT_LRELU_BWD else 0.0, 1.0, ptr(res1), res1_cs, res1_co, 1.0, None, 0, 0, mode,
-                      1 if down2 else 0, 0, 1.0, 1.0, aux_cs, ptr(aux), aux_co, aux_scale)
+        rf = (1 if res1 is not None and res1.dtype == torch.float32 else 0) | \
+             (2 if res2 is not None and res2.dtype == torch.float32 else 0)
+        ep = Epilogue(act, 0.2 if act == ACT_LRELU_BWD else 0.0, 1.0, ptr(res1), res1_cs, res1_co, 1.0, ptr(res2), res2_cs, res2_co,
+                      mode, 1 if down2 else 0, rf, 1.0, 1.0, aux_cs, ptr(aux), aux_co, aux_scale)
         if bn_bwd is not None:
             part, z, z_cs, mean, rstd, gamma, beta = bn_bwd
             ep.bn_part, ep.bn_z, ep.bn_z_cstride, ep.bn_slope = ptr(part), ptr(z), z_cs, 0.2
@@ -228,7 +232,7 @@ class ConvPlan:
         flops = 2 * self.cout * ct * self.ks * self.ks * n * out_h * out_w // (self.stride * self.stride)
         gpx = n * out_h * out_w // (4 if down2 else 1)  # result pixels (after the 2x2 sum)
         nbytes = (n * d.in_h * d.in_w * self.cout * 2 + self.rows_t * self.kpk_t * 2 +
-                  gpx * ct * (g.element_size() * (2 if mode == OUT_F32_ADD else 1) + _esize(res1) + _esize(aux)))
+                  gpx * ct * (g.element_size() * (2 if mode == OUT_F32_ADD else 1) + _esize(res1) + _esize(res2) + _esize(aux)))
         _run(_kname(d, None, ep), flops, lambda: check(
             _lib.load().climsr_conv2d_fwd(ctypes.byref(d), ptr(dz), ptr(self.wpk_t), None, ctypes.byref(ep), ptr(g),
                                           _lib.stream_ptr()), f"conv dgrad {self.name}"), "dgrad " + self.name, nbytes)

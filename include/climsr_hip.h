@@ -498,6 +498,25 @@ int climsr_channel_attention(const float* u, int n, int64_t hw, int c, int u_cst
 int climsr_channel_attention_parts(const float* part, int n, int tiles_per_image, int64_t hw, int c, const float* w1,
                                    const float* b1, const float* w2, const float* b2, int cr, double* workspace, float* s,
                                    void* stream);
+/* climsr_channel_attention / climsr_channel_attention_parts that also keep the pooled mean (mean_out fp32 [n][c]) for
+ * the training backward (climsr_ca_backward). */
+int climsr_channel_attention_mean(const float* u, int n, int64_t hw, int c, int u_cstride, const float* w1, const float* b1,
+                                  const float* w2, const float* b2, int cr, double* workspace, float* s, float* mean_out, void* stream);
+int climsr_channel_attention_parts_mean(const float* part, int n, int tiles_per_image, int64_t hw, int c, const float* w1,
+                                        const float* b1, const float* w2, const float* b2, int cr, double* workspace, float* s,
+                                        float* mean_out, void* stream);
+/* Backward of the RCAB's channel attention + residual (CALayer / RCAB.forward, rcan.py:50-69,98-101; replaces the autograd
+ * of AdaptiveAvgPool2d -> 1x1 -> ReLU -> 1x1 -> Sigmoid -> x * y under the reference's RCAN pre-training,
+ * conf/experiment/rcan_pre_training.yaml).  y = u * s + x, s = sigmoid(w2 relu(w1 mean + b1) + b2): given gy = dL/dy
+ * (fp32 [n][hw][gy_cstride]), u (fp32, or bf16 with u_bf16 = 1), s and mean (fp32 [n][c], the forward's; mean from
+ * climsr_channel_attention*_mean), writes gu = dL/du = gy * s + (w1^T g_a1) / hw (bf16 [n][hw][gu_cstride]) and the
+ * conv_du gradients gw1 [cr][c], gb1 [cr], gw2 [c][cr], gb2 [c] (fp32, '=' or '+=' with accumulate; gb1 / gb2 null
+ * exactly when b1 / b2 are).  dL/dx = gy is left to the caller.  Deterministic (fixed-order fp64 slices, images summed
+ * in order).  workspace = climsr_ca_backward_workspace(n, hw, c, cr) bytes; c a multiple of 8 (<= 1024). */
+size_t climsr_ca_backward_workspace(int n, int64_t hw, int c, int cr);
+int climsr_ca_backward(const float* gy, int gy_cstride, const void* u, int u_bf16, int u_cstride, const float* s, const float* mean, int n,
+                       int64_t hw, int c, const float* w1, const float* b1, const float* w2, int cr, float* gw1, float* gb1, float* gw2,
+                       float* gb2, int accumulate, void* workspace, uint16_t* gu, int gu_cstride, void* stream);
 /* RCAB residual with the attention scale (rcan.py:104-107): xres = u * s + xres (fp32 [n][hw][c]) and
  * xb = bf16(xres) ([n][hw][xb_cstride], the next conv's input); u = the RCAB body's output, fp32 or (u_bf16 = 1)
  * bf16, channel stride u_cstride.  c, strides multiples of 4. */
@@ -549,6 +568,11 @@ int64_t climsr_srcnn_packed_elems(void);
  * Bit-exact index map; c_out and out_cstride multiples of 8. */
 int climsr_pixel_shuffle_bf16(const uint16_t* x, int n, int h, int w, int c_out, int r, int in_cstride, uint16_t* y,
                               int out_cstride, void* stream);
+
+/* Backward of nn.PixelShuffle(r) (rcan.py:32; replaces its autograd under RCAN training): the inverse index map,
+ * gx[n][y][x][co*r*r+i*r+j] = gy[n][y*r+i][x*r+j][co], NHWC bf16, bit-exact.  c_out*r*r and gx_cstride multiples of 8. */
+int climsr_pixel_unshuffle_bf16(const uint16_t* gy, int n, int h, int w, int c_out, int r, int gy_cstride, uint16_t* gx,
+                                int gx_cstride, void* stream);
 
 #ifdef __cplusplus
 }

@@ -120,3 +120,29 @@ def update_envelope(native, ref64, amps, floor=2e-2, pool_below=0):
     bad = [(k, round(r, 4), round(ra, 4)) for k, (r, ra) in rows.items() if r > max(2.0 * ra, floor)]
     worst = max(rows.items(), key=lambda kv: kv[1][0] / max(2.0 * kv[1][1], floor))
     return bad, worst, rows
+
+
+RCAN_TRAIN = {"rcan_g2b2_x4": (2, 2, 4, 2, 16), "rcan_g1b2_x2": (1, 2, 2, 2, 12), "rcan_g1b1_x3": (1, 1, 3, 1, 10)}
+
+
+def rcan_train_batch(b, lr_size, sf, seed=7, dtype=torch.float64):
+    """The inputs of tests/golden/make_rcan_golden.py's training records: hr [b,1,H,W] in [-1,1), elev, mask, and
+    lr = cat[hr, elev, mask] subsampled by sf (the reference RCAN's 3-channel input)."""
+    hrs = lr_size * sf
+    g = torch.Generator().manual_seed(seed)
+    hr = torch.rand((b, 1, hrs, hrs), generator=g, dtype=torch.float64) * 2 - 1
+    e = torch.rand((b, 1, hrs, hrs), generator=g, dtype=torch.float64) * 2 - 1
+    m = (torch.rand((b, 1, hrs, hrs), generator=g) < 0.7).double()
+    lr = torch.cat([hr, e, m], 1)[:, :, ::sf, ::sf].contiguous()
+    return {k: v.to(dtype) for k, v in dict(lr=lr, hr=hr, elevation=e, mask=m).items()}
+
+
+def rcan_params(ng, nb, sf, dtype=torch.float64):
+    """The deterministic RCAN weights of the golden records (climsr_amd.core.init keyed by state_dict name)."""
+    import numpy as np
+
+    from climsr_amd.core.init import init_state, spec_from_shapes
+    from climsr_amd.models.rcan import RCAN
+
+    shapes = {k: tuple(v.shape) for k, v in RCAN(n_resgroups=ng, n_resblocks=nb, scaling_factor=sf).state_dict().items()}
+    return {k: torch.from_numpy(np.asarray(v)).to(dtype) for k, v in init_state(spec_from_shapes(shapes)).items()}

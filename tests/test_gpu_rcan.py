@@ -5,7 +5,13 @@
 * channel attention (pool -> 1x1 -> ReLU -> 1x1 -> sigmoid) and the RCAB residual: rel 1e-5 vs torch fp64;
 * whole model: PSNR >= 50 dB and centred correlation >= 0.999 vs the fp64 reference (bf16 activations, fp32
   residual stream; 2x2 and 10x20 residual groups/blocks, x4 and x2 upsamplers).
+* training (rcan_pre_training.yaml: the L1 pre-training task with generator rcan): the PixelShuffle backward
+  bit-exact vs torch; the channel-attention backward (climsr_ca_backward) vs fp64 autograd; the whole RCAN gradient
+  vs the fp64 oracle (itself pinned to the reference module's gradients, tests/golden/rcan_train.json) per tensor
+  within 2x the deviation of the oracle's own autocast fp16 / bf16 runs; a Trainer step of
+  SuperResolutionLightningModule(generator=rcan) with AdamW + OneCycleLR; bit-identical reruns.
 """
+import json
 import os
 
 import numpy as np
@@ -51,15 +57,6 @@ def test_rcan_forward_vs_reference_golden(golden_dir, name):
     gc, wc = got - got.mean(), want - want.mean()
     corr = float((gc * wc).sum() / (gc.norm() * wc.norm()))
     assert p >= 50.0 and corr >= 0.999, f"PSNR {p:.2f} dB, centred correlation {corr:.6f}"
-
-
-def test_rcan_refuses_training_mode():
-    from climsr_amd.models.rcan import RCAN
-
-    net = RCAN(n_resgroups=1, n_resblocks=1).to(DEV).train()
-    lr, e, m = batch(1, 32)
-    with pytest.raises(NotImplementedError, match="inference-only"):
-        net(lr.to(DEV), e.to(DEV), m.to(DEV))
 
 
 @pytest.mark.parametrize("r,c_out,h,w", [(2, 64, 5, 7), (3, 64, 4, 4), (2, 8, 9, 3)])
@@ -142,3 +139,200 @@ def test_channel_attention_parts_vs_float64(n, tpi, c, cr):
     mean = part.double().sum(1) / hw
     s_ref = torch.sigmoid(torch.relu(mean @ w1.double().T + b1.double()) @ w2.double().T + b2.double())
     assert (s.cpu().double() - s_ref).abs().max() <= 1e-5
+
+
+@pytest.mark.parametrize("r,c_out,h,w", [(2, 64, 5, 7), (3, 64, 4, 4), (2, 8, 9, 3), (2, 64, 16, 16)])
+def test_pixel_unshuffle_bit_exact(r, c_out, h, w):
+    """climsr_pixel_unshuffle_bf16 (the backward of nn.PixelShuffle, rcan.py:32) == F.pixel_unshuffle, bit for bit."""
+    from climsr_amd import _lib
+    from climsr_amd._lib import check, ptr
+
+    n = 2
+    gy = torch.randn((n, c_out, h * r, w * r)).to(torch.bfloat16)
+    want = F.pixel_unshuffle(gy, r)  # [n, c_out r r, h, w]
+    gyd = gy.permute(0, 2, 3, 1).contiguous().to(DEV)
+    gx = torch.empty((n, h, w, c_out * r * r), dtype=torch.bfloat16, device=DEV)
+    check(_lib.load().climsr_pixel_unshuffle_bf16(ptr(gyd), n, h, w, c_out, r, c_out, ptr(gx), c_out * r * r, _lib.stream_ptr()), "pu")
+    torch.cuda.synchronize()
+    assert torch.equal(gx.cpu().permute(0, 3, 1, 2), want)
+    # it is the adjoint of the forward map: shuffle(unshuffle(gy)) == gy
+    y = torch.empty_like(gyd)
+    check(_lib.load().climsr_pixel_shuffle_bf16(ptr(gx), n, h, w, c_out, r, c_out * r * r, ptr(y), c_out, _lib.stream_ptr()), "ps")
+    torch.cuda.synchronize()
+    assert torch.equal(y, gyd)
+
+
+@pytest.mark.parametrize("n,h,w,c,cr,u_bf16,acc", [(2, 13, 17, 64, 4, True, False), (3, 32, 32, 64, 4, False, True),
+                                                   (1, 5, 3, 96, 6, True, True), (2, 40, 40, 64, 4, True, False)])
+def test_ca_backward_vs_float64(n, h, w, c, cr, u_bf16, acc):
+    """climsr_ca_backward (CALayer + RCAB residual backward, rcan.py:50-69,98-101) vs torch fp64 autograd of
+    y = u * sigmoid(W2 relu(W1 mean(u) + b1) + b2) on the same u: dL/du (bf16: within bf16 rounding), conv_du
+    gradients rel 1e-5 ('=' and '+='); ragged pixel counts, wider c; bit-identical reruns."""
+    from climsr_amd import _lib
+    from climsr_amd._lib import check, ptr
+
+    g = torch.Generator().manual_seed(n * 1000 + h * 10 + c)
+    u = torch.randn((n, h, w, c), generator=g)
+    if u_bf16:
+        u = u.to(torch.bfloat16).float()
+    gy = torch.randn((n, h, w, c), generator=g)
+    w1 = torch.randn((cr, c), generator=g) * 0.2
+    b1 = torch.randn((cr,), generator=g) * 0.1
+    w2 = torch.randn((c, cr), generator=g) * 0.2
+    b2 = torch.randn((c,), generator=g) * 0.1
+    # fp64 reference
+    u64, w1d, b1d, w2d, b2d = (t.double().requires_grad_(True) for t in (u, w1, b1, w2, b2))
+    mean = u64.mean(dim=(1, 2))
+    s64 = torch.sigmoid(torch.relu(mean @ w1d.T + b1d) @ w2d.T + b2d)
+    y = u64 * s64[:, None, None, :]
+    gu_ref, gw1_ref, gb1_ref, gw2_ref, gb2_ref = torch.autograd.grad(y, [u64, w1d, b1d, w2d, b2d], gy.double())
+    L = _lib.load()
+    st = _lib.stream_ptr()
+    dd = {k: v.to(DEV).contiguous() for k, v in dict(u=u, gy=gy, w1=w1, b1=b1, w2=w2, b2=b2).items()}
+    s = torch.empty((n, c), device=DEV)
+    mn = torch.empty((n, c), device=DEV)
+    caws = torch.empty(L.climsr_channel_attention_workspace(n, c) // 8, dtype=torch.float64, device=DEV)
+    check(L.climsr_channel_attention_mean(ptr(dd["u"]), n, h * w, c, c, ptr(dd["w1"]), ptr(dd["b1"]), ptr(dd["w2"]), ptr(dd["b2"]), cr,
+                                          ptr(caws), ptr(s), ptr(mn), st), "ca fwd")
+    ud = dd["u"].to(torch.bfloat16) if u_bf16 else dd["u"]
+    ws = torch.empty(L.climsr_ca_backward_workspace(n, h * w, c, cr), dtype=torch.uint8, device=DEV)
+    base = [torch.randn(t.shape, generator=g).to(DEV) if acc else torch.full(t.shape, float("nan"), device=DEV) for t in (w1, b1, w2, b2)]
+    outs = []
+    for rep in range(2):
+        gr = [b.clone() for b in base]
+        gu = torch.empty((n, h, w, c), dtype=torch.bfloat16, device=DEV)
+        check(L.climsr_ca_backward(ptr(dd["gy"]), c, ptr(ud), int(u_bf16), c, ptr(s), ptr(mn), n, h * w, c, ptr(dd["w1"]), ptr(dd["b1"]),
+                                   ptr(dd["w2"]), cr, ptr(gr[0]), ptr(gr[1]), ptr(gr[2]), ptr(gr[3]), int(acc), ptr(ws), ptr(gu), c, st), "ca bwd")
+        torch.cuda.synchronize()
+        outs.append([gu.cpu()] + [t.cpu() for t in gr])
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b), "ca backward rerun not bit-identical"
+    gu_got = outs[0][0].double()
+    err = (gu_got - gu_ref).abs()
+    assert bool((err <= 2.0 ** -8 * gu_ref.abs() + 1e-6).all()), f"gu max err {float(err.max())}"
+    for got, want, b0, nm in zip(outs[0][1:], (gw1_ref, gb1_ref, gw2_ref, gb2_ref), base, ("gw1", "gb1", "gw2", "gb2")):
+        want = want.double() + (b0.cpu().double() if acc else 0.0)
+        rel = float((got.double() - want).norm() / want.norm())
+        assert rel <= 1e-5, (nm, rel)
+
+
+def _native_rcan(ng, nb, sf):
+    from climsr_amd.models.rcan import RCAN
+    from tests.helpers import rcan_params
+
+    net = RCAN(n_resgroups=ng, n_resblocks=nb, n_feats=64, reduction=16, scaling_factor=sf, in_channels=3, out_channels=1)
+    net.load_state_dict({k: v.float() for k, v in rcan_params(ng, nb, sf).items()}, strict=True)
+    return net.to(DEV).train()
+
+
+def _oracle_grads(p_state, bt, keys, ng, nb, sf, dev, dtype, autocast=None, scale=1.0, halves=False):
+    from oracle import climsr_ref as ref
+
+    b = bt["hr"].shape[0]
+    q = {k: v.to(dev, dtype).requires_grad_(True) for k, v in p_state.items()}
+    b_ = {k: v.to(dev, dtype) for k, v in bt.items()}
+    parts = [slice(0, b // 2), slice(b // 2, b)] if halves and b > 1 else [slice(0, b)]
+    out = {k: 0.0 for k in keys}
+    for sl in parts:
+        with torch.autocast("cuda", dtype=autocast or torch.float16, enabled=autocast is not None):
+            sr = ref.rcan_forward(q, b_["lr"][sl], b_["elevation"][sl], b_["mask"][sl], ng, nb, sf)
+        loss = ref.l1_loss(sr.to(dtype), b_["hr"][sl]) * ((sl.stop - sl.start) / b)
+        gs = torch.autograd.grad(loss * scale, [q[k] for k in keys])
+        for k, gk in zip(keys, gs):
+            out[k] = out[k] + gk.double().cpu() / scale
+    assert all(torch.isfinite(v).all() for v in out.values()), "loss scale overflowed"
+    return out
+
+
+@pytest.mark.parametrize("name", ["rcan_g2b2_x4", "rcan_g1b2_x2", "rcan_g1b1_x3"])
+def test_rcan_training_grads_vs_oracle(golden_dir, name, monkeypatch):
+    """The native RCAN backward (L1 loss, rcan_pre_training.yaml's task) vs the fp64 oracle's gradient at the same
+    parameters and batch, per tensor within 2x the deviation of the oracle's own torch-autocast fp16 (loss x 2^16, as
+    precision=16's GradScaler) / bf16 runs, whole batch and two half-batch passes (helpers.update_envelope; tensors under
+    256 elements pooled); the loss vs the reference module's (rcan_train.json) within 2x the autocast loss deviation;
+    x4 / x2 / x3 upsamplers; a second backward is bit-identical."""
+    from oracle import climsr_ref as ref
+    from tests.helpers import RCAN_TRAIN, gemm_conv, rcan_params, rcan_train_batch, update_envelope
+
+    ng, nb, sf, b, lr_size = RCAN_TRAIN[name]
+    want = json.load(open(os.path.join(golden_dir, "rcan_train.json")))[name]
+    net = _native_rcan(ng, nb, sf)
+    bt = {k: v.float().to(DEV) for k, v in rcan_train_batch(b, lr_size, sf).items()}
+    runs = []
+    for rep in range(2):
+        net.zero_grad(set_to_none=True)
+        sr = net(bt["lr"], bt["elevation"], bt["mask"])
+        loss = F.l1_loss(sr, bt["hr"])
+        loss.backward()
+        torch.cuda.synchronize()
+        runs.append((float(loss), {k: p.grad.detach().double().cpu().clone() for k, p in net.named_parameters()}))
+    assert runs[0][0] == runs[1][0] and all(torch.equal(runs[0][1][k], runs[1][1][k]) for k in runs[0][1]), "rerun not bit-identical"
+    loss_n, grads = runs[0]
+    keys = list(grads)
+    p64 = rcan_params(ng, nb, sf)
+    bt64 = rcan_train_batch(b, lr_size, sf)
+    g64 = _oracle_grads(p64, bt64, keys, ng, nb, sf, "cpu", torch.float64)
+    with monkeypatch.context() as mp:
+        mp.setattr(ref, "_conv", gemm_conv)
+        torch.backends.cuda.matmul.allow_tf32 = False
+        amps = [_oracle_grads(p64, bt64, keys, ng, nb, sf, DEV, torch.float32, dt, scale=sc, halves=hv)
+                for dt, sc in ((torch.float16, 2.0 ** 16), (torch.bfloat16, 1.0)) for hv in (False, True)]
+        amp_losses = []
+        for dt in (torch.float16, torch.bfloat16):
+            with torch.no_grad(), torch.autocast("cuda", dtype=dt):
+                q = {k: v.to(DEV, torch.float32) for k, v in p64.items()}
+                srq = ref.rcan_forward(q, bt["lr"], bt["elevation"], bt["mask"], ng, nb, sf)
+            amp_losses.append(float(ref.l1_loss(srq.float(), bt["hr"])))
+    bad, worst, rows = update_envelope(grads, g64, amps, pool_below=256)
+    ratios = sorted(r / ra for r, ra in rows.values())
+    print(f"{name}: loss native {loss_n:.7f} reference {want['loss']:.7f} autocast {amp_losses}; gradient rel L2 vs fp64 worst {worst}, "
+          f"native / envelope median {ratios[len(ratios) // 2]:.2f} max {ratios[-1]:.2f}", flush=True)
+    assert not bad, f"{len(bad)} gradients outside 2x the autocast deviation: {bad[:8]}"
+    dev_amp = max(abs(a - want["loss"]) for a in amp_losses)
+    assert abs(loss_n - want["loss"]) <= max(2.0 * dev_amp, 1e-6 * abs(want["loss"])), (loss_n, want["loss"], amp_losses)
+    # every parameter received a gradient that matches the reference module's checksum scale
+    for k in keys:
+        assert torch.isfinite(grads[k]).all(), k
+
+
+def test_rcan_pretrain_trainer_steps(monkeypatch):
+    """conf/experiment/rcan_pre_training.yaml's task: SuperResolutionLightningModule with generator
+    ``climsr_amd.models.rcan.RCAN`` (the drop-in for conf/generator/rcan.yaml) through the built-in Trainer with the
+    zero-argument configure_optimizers() (AdamW + OneCycleLR, per-step): two steps; each step's fused AdamW update given
+    the native gradients equals the fp64 AdamW + OneCycleLR update within 1e-3 (rel L2 per tensor)."""
+    from climsr_amd.core.trainer import Trainer
+    from climsr_amd.task.pl_generator_pre_training import SuperResolutionLightningModule
+    from oracle import climsr_ref as ref
+    from tests.helpers import rcan_params, rcan_train_batch
+
+    ng, nb, sf = 1, 2, 4
+    m = SuperResolutionLightningModule(
+        generator={"_target_": "climsr_amd.models.rcan.RCAN", "n_resgroups": ng, "n_resblocks": nb, "n_feats": 64, "reduction": 16,
+                   "scaling_factor": sf, "in_channels": 3, "out_channels": 1},
+        optimizers={"generator_optimizer": {"_target_": "torch.optim.AdamW", "lr": 1e-4, "weight_decay": 1e-4}},
+        schedulers={"generator_scheduler": {"_target_": "torch.optim.lr_scheduler.OneCycleLR", "max_lr": 1e-4,
+                                            "num_training_steps": -1, "pct_start": 0.05, "div_factor": 2, "final_div_factor": 100}},
+        generator_type="rcan")
+    m.generator.load_state_dict({k: v.float() for k, v in rcan_params(ng, nb, sf).items()}, strict=True)
+    m = m.to(DEV)
+    tr = Trainer(m, limit_train_batches=4, max_epochs=1)
+    from climsr_amd.core.optim import AdamW
+
+    assert isinstance(tr.optimizers[0], AdamW), "the native RCAN takes the fused flat AdamW"
+    keys = [k for k, _ in m.generator.named_parameters()]
+    opt64 = ref.AdamWState({k: v.detach().double().cpu().clone() for k, v in m.generator.named_parameters()}, keys, lr=1e-4,
+                           total_steps=4)
+    for i, seed in enumerate((11, 12)):
+        bt = {k: v.float().to(DEV) for k, v in rcan_train_batch(2, 12, sf, seed=seed).items()}
+        before = {k: v.detach().double().cpu().clone() for k, v in m.generator.named_parameters()}
+        out = tr.training_batch(bt, i)
+        torch.cuda.synchronize()
+        assert torch.isfinite(out[0]).all() and "train/loss" in m.logged
+        grads = {k: p.grad.detach().double().cpu().clone() for k, p in m.generator.named_parameters()}
+        after = {k: v.detach().double().cpu().clone() for k, v in m.generator.named_parameters()}
+        q = {k: v.clone() for k, v in before.items()}
+        opt64.step(q, grads)
+        opt64.sched()
+        worst = max((float(((after[k] - before[k]) - (q[k] - before[k])).norm() / ((q[k] - before[k]).norm() + 1e-30)), k) for k in keys)
+        print(f"rcan pretrain step {i}: loss {float(out[0]):.6f}; AdamW update rel L2 vs fp64 (native gradients) worst {worst}", flush=True)
+        assert worst[0] <= 1e-3, worst

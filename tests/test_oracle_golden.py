@@ -182,3 +182,24 @@ def test_pixel_shuffle_index_map_bit_exact():
     x = torch.arange(2 * 36 * 3 * 5, dtype=torch.float64).reshape(2, 36, 3, 5)
     for r in (2, 3):
         assert torch.equal(ref.pixel_shuffle(x, r), torch.nn.functional.pixel_shuffle(x, r))
+
+
+@pytest.mark.parametrize("name", ["rcan_g2b2_x4", "rcan_g1b2_x2", "rcan_g1b1_x3"])
+def test_rcan_oracle_training_grads_match_reference(golden_dir, name):
+    """oracle.rcan_forward + L1 (task.py:141) autograd gradients vs the reference module's own (make_rcan_golden.py,
+    tests/golden/rcan_train.json), fp64: loss and every parameter's (sum, norm)."""
+    import torch
+
+    from tests.helpers import RCAN_TRAIN, rcan_params, rcan_train_batch
+
+    ng, nb, sf, b, lr_size = RCAN_TRAIN[name]
+    want = json.load(open(os.path.join(golden_dir, "rcan_train.json")))[name]
+    p = {k: v.requires_grad_(True) for k, v in rcan_params(ng, nb, sf).items()}
+    bt = rcan_train_batch(b, lr_size, sf)
+    loss = ref.l1_loss(ref.rcan_forward(p, bt["lr"], bt["elevation"], bt["mask"], ng, nb, sf), bt["hr"])
+    keys = list(p)
+    gs = torch.autograd.grad(loss, [p[k] for k in keys])
+    assert abs(float(loss) - want["loss"]) <= 1e-12
+    assert set(keys) == set(want["grads"])
+    for k, gk in zip(keys, gs):
+        np.testing.assert_allclose([float(gk.sum()), float(gk.norm())], want["grads"][k], rtol=1e-9, atol=1e-13, err_msg=k)
