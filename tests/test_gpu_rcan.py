@@ -225,7 +225,9 @@ def _native_rcan(ng, nb, sf):
     return net.to(DEV).train()
 
 
-def _oracle_grads(p_state, bt, keys, ng, nb, sf, dev, dtype, autocast=None, scale=1.0, halves=False):
+def _oracle_grads(p_state, bt, keys, ng, nb, sf, dev, dtype, autocast=None, scale=1.0, halves=False, gout=None):
+    """Oracle parameter gradients of the L1 loss, or (gout given) the vector-Jacobian product with that upstream
+    gradient of the generator output."""
     from oracle import climsr_ref as ref
 
     b = bt["hr"].shape[0]
@@ -236,7 +238,10 @@ def _oracle_grads(p_state, bt, keys, ng, nb, sf, dev, dtype, autocast=None, scal
     for sl in parts:
         with torch.autocast("cuda", dtype=autocast or torch.float16, enabled=autocast is not None):
             sr = ref.rcan_forward(q, b_["lr"][sl], b_["elevation"][sl], b_["mask"][sl], ng, nb, sf)
-        loss = ref.l1_loss(sr.to(dtype), b_["hr"][sl]) * ((sl.stop - sl.start) / b)
+        if gout is None:
+            loss = ref.l1_loss(sr.to(dtype), b_["hr"][sl]) * ((sl.stop - sl.start) / b)
+        else:
+            loss = (sr.to(dtype) * gout[sl].to(dev, dtype)).sum()
         gs = torch.autograd.grad(loss * scale, [q[k] for k in keys])
         for k, gk in zip(keys, gs):
             out[k] = out[k] + gk.double().cpu() / scale
@@ -250,7 +255,11 @@ def test_rcan_training_grads_vs_oracle(golden_dir, name, monkeypatch):
     parameters and batch, per tensor within 2x the deviation of the oracle's own torch-autocast fp16 (loss x 2^16, as
     precision=16's GradScaler) / bf16 runs, whole batch and two half-batch passes (helpers.update_envelope; tensors under
     256 elements pooled); the loss vs the reference module's (rcan_train.json) within 2x the autocast loss deviation;
-    x4 / x2 / x3 upsamplers; a second backward is bit-identical."""
+    x4 / x2 / x3 upsamplers; a second backward is bit-identical.  The backward is compared as the vector-Jacobian product
+    with the native upstream gradient dL/dsr = sign(sr - hr) / N (the L1 loss's): the fp64 and autocast oracle gradients
+    are taken with that same gout, so a pixel where |sr - hr| is below the forward's rounding (whose sign then differs
+    between any two precisions) does not decide the comparison -- srcnn.conv3's weight gradient is a sum of such signs
+    over the pixels, each flip moving it by about 2 / sqrt(N) of its norm."""
     from oracle import climsr_ref as ref
     from tests.helpers import RCAN_TRAIN, gemm_conv, rcan_params, rcan_train_batch, update_envelope
 
@@ -265,31 +274,45 @@ def test_rcan_training_grads_vs_oracle(golden_dir, name, monkeypatch):
         loss = F.l1_loss(sr, bt["hr"])
         loss.backward()
         torch.cuda.synchronize()
-        runs.append((float(loss), {k: p.grad.detach().double().cpu().clone() for k, p in net.named_parameters()}))
+        runs.append((float(loss.detach()), {k: p.grad.detach().double().cpu().clone() for k, p in net.named_parameters()}))
     assert runs[0][0] == runs[1][0] and all(torch.equal(runs[0][1][k], runs[1][1][k]) for k in runs[0][1]), "rerun not bit-identical"
     loss_n, grads = runs[0]
+    gout = (torch.sign(sr.detach().double() - bt["hr"].double()) / sr.numel()).cpu()
     keys = list(grads)
     p64 = rcan_params(ng, nb, sf)
     bt64 = rcan_train_batch(b, lr_size, sf)
-    g64 = _oracle_grads(p64, bt64, keys, ng, nb, sf, "cpu", torch.float64)
+    g64 = _oracle_grads(p64, bt64, keys, ng, nb, sf, "cpu", torch.float64, gout=gout)
     with monkeypatch.context() as mp:
         mp.setattr(ref, "_conv", gemm_conv)
         torch.backends.cuda.matmul.allow_tf32 = False
-        amps = [_oracle_grads(p64, bt64, keys, ng, nb, sf, DEV, torch.float32, dt, scale=sc, halves=hv)
+        amps = [_oracle_grads(p64, bt64, keys, ng, nb, sf, DEV, torch.float32, dt, scale=sc, halves=hv, gout=gout)
                 for dt, sc in ((torch.float16, 2.0 ** 16), (torch.bfloat16, 1.0)) for hv in (False, True)]
-        amp_losses = []
+        amp_losses, amp_sr = [], []
         for dt in (torch.float16, torch.bfloat16):
             with torch.no_grad(), torch.autocast("cuda", dtype=dt):
                 q = {k: v.to(DEV, torch.float32) for k, v in p64.items()}
                 srq = ref.rcan_forward(q, bt["lr"], bt["elevation"], bt["mask"], ng, nb, sf)
             amp_losses.append(float(ref.l1_loss(srq.float(), bt["hr"])))
+            amp_sr.append(srq.double().cpu())
+    with torch.no_grad():
+        sr64 = ref.rcan_forward(p64, bt64["lr"], bt64["elevation"], bt64["mask"], ng, nb, sf)
     bad, worst, rows = update_envelope(grads, g64, amps, pool_below=256)
     ratios = sorted(r / ra for r, ra in rows.values())
     print(f"{name}: loss native {loss_n:.7f} reference {want['loss']:.7f} autocast {amp_losses}; gradient rel L2 vs fp64 worst {worst}, "
           f"native / envelope median {ratios[len(ratios) // 2]:.2f} max {ratios[-1]:.2f}", flush=True)
+    top = sorted(rows.items(), key=lambda kv: -kv[1][0] / max(kv[1][1], 1e-30))[:6]
+    print("  highest native / envelope: " + ", ".join(f"{k} {r:.2e}/{ra:.2e}" for k, (r, ra) in top), flush=True)
     assert not bad, f"{len(bad)} gradients outside 2x the autocast deviation: {bad[:8]}"
-    dev_amp = max(abs(a - want["loss"]) for a in amp_losses)
-    assert abs(loss_n - want["loss"]) <= max(2.0 * dev_amp, 1e-6 * abs(want["loss"])), (loss_n, want["loss"], amp_losses)
+    # the forward: the output vs fp64 within 2x the autocast runs' deviation; the loss scalar within SURVEY 8c's 1e-3 (a
+    # mean of |sr - hr| over N pixels: its deviation is bounded by the output's, and at a few thousand pixels it is too
+    # noisy a statistic to carry a tighter bound of its own)
+    rel_sr = float((sr.detach().double().cpu() - sr64).norm() / sr64.norm())
+    rel_amp = max(float((a - sr64).norm() / sr64.norm()) for a in amp_sr)
+    rel_loss = abs(loss_n - want["loss"]) / abs(want["loss"])
+    print(f"  output rel L2 vs fp64 {rel_sr:.2e} (autocast {rel_amp:.2e}); loss rel deviation {rel_loss:.2e} (autocast "
+          f"{max(abs(a - want['loss']) for a in amp_losses) / abs(want['loss']):.2e})", flush=True)
+    assert rel_sr <= 2.0 * rel_amp, (rel_sr, rel_amp)
+    assert rel_loss <= 1e-3, (loss_n, want["loss"])
     # every parameter received a gradient that matches the reference module's checksum scale
     for k in keys:
         assert torch.isfinite(grads[k]).all(), k
