@@ -159,8 +159,6 @@ SIGNATURES = {
     "climsr_adamw_step": (c_int, [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "climsr_adamw_step_mirror": (c_int, [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p,
                                          c_void_p]),
-    "climsr_adamw_step_mirror_frag": (c_int, [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int,
-                                              c_void_p, c_void_p]),
     "climsr_bn_workspace_doubles": (c_int64, [c_int64, c_int]),
     "climsr_bn_forward": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_int, c_float, c_float, c_float, c_void_p,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -178,10 +176,6 @@ SIGNATURES = {
     "climsr_linear_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p, c_int64,
                                   c_void_p, c_void_p]),
     "climsr_linear_dgrad": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
-    "climsr_linear_pack_frag": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
-    "climsr_linear_fwd_frag": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p, c_int64,
-                                       c_void_p, c_void_p]),
-    "climsr_linear_dgrad_frag": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     "climsr_linear_wgrad": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     "climsr_linear_wgrad2": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
     "climsr_d_head_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
@@ -252,11 +246,6 @@ def load() -> ctypes.CDLL:
         fn.argtypes = args
     _lib = lib
     return lib
-
-
-def has(name: str) -> bool:
-    """Whether the loaded library exports name (always, for the in-tree build; see load())."""
-    return hasattr(load(), name)
 
 
 def check(rc: int, what: str) -> None:

@@ -116,8 +116,7 @@ class AdamW(torch.optim.Optimizer):
 
 
 def _mirror_of(module):
-    """(offset, numel, bf16 buffer[, (o, k) when the copy is in fragment order]) of a weight the module reads as a bf16
-    copy of its flat buffer, or None."""
+    """(offset, numel, bf16 buffer) of a weight the module reads as a bf16 copy of its flat buffer, or None."""
     fn = getattr(module, "bf16_mirror", None)
     return fn() if fn is not None else None
 
@@ -129,12 +128,8 @@ def _adamw_flat(lib, module, flat, gflat, m, v, hp, stream):
     if mir is None:
         _launch("adamw", lambda: lib.climsr_adamw_step(flat.numel(), ptr(flat), ptr(gflat), ptr(m), ptr(v), ptr(hp), stream),
                 nbytes=28 * flat.numel())
-    elif len(mir) == 4 and mir[3] is not None:  # (lo, numel, buf, (o, k)): the copy in fragment order
-        lo, n, buf, (o, k) = mir
-        _launch("adamw", lambda: lib.climsr_adamw_step_mirror_frag(flat.numel(), ptr(flat), ptr(gflat), ptr(m), ptr(v), ptr(hp), lo,
-                                                                   o, k, ptr(buf), stream), nbytes=28 * flat.numel() + 2 * n)
     else:
-        lo, n, buf = mir[:3]
+        lo, n, buf = mir
         _launch("adamw", lambda: lib.climsr_adamw_step_mirror(flat.numel(), ptr(flat), ptr(gflat), ptr(m), ptr(v), ptr(hp), lo, n,
                                                               ptr(buf), stream), nbytes=28 * flat.numel() + 2 * n)
 

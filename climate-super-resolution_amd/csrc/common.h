@@ -18,6 +18,11 @@ int check_launch(const char* what);
 int device_cus();
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device), thread-safe, error checked
 int lds_opt_in(const void* fn, int bytes);
+// dispatcher dry run (climsr_*_kernel name queries): set, the dispatchers record the kernel they would launch in
+// g_dry_name and return before launching; dry_run(fmt, ...) records the name and answers whether to return
+extern thread_local bool g_dry;
+extern thread_local char g_dry_name[96];
+bool dry_run(const char* fmt, ...);
 
 __device__ __forceinline__ uint16_t f2bf(float f) {
   __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32: RNE, NaN-preserving
@@ -69,13 +74,5 @@ __device__ __forceinline__ void lds_barrier() {
 
 static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
-
-// Fragment order of a [o][k] bf16 weight (o % 64 == 0, k % 32 == 0): element (r, c) at
-//   (((r / 64) * (k / 32) + c / 32) * 4 + (r % 64) / 16) * 512 + ((r % 16) + 16 * ((c % 32) / 8)) * 8 + c % 8,
-// i.e. 1 KB pieces that are exactly the 16x32 A fragments of v_mfma_f32_16x16x32_bf16 in lane order, four row groups
-// of one 32-wide k-step side by side (4 KB), k-steps next, 64-row blocks outermost.
-__device__ __forceinline__ long linear_frag_index(long r, long c, long kb) {
-  return (((r >> 6) * kb + (c >> 5)) * 4 + ((r >> 4) & 3)) * 512 + ((r & 15) + 16 * ((c >> 3) & 3)) * 8 + (c & 7);
-}
 
 }  // namespace climsr

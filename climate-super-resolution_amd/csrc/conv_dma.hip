@@ -95,13 +95,6 @@ __device__ __forceinline__ void dma_store_half(const FwdArgs& a, const float* eb
   }
 }
 
-#ifndef CLIMSR_DMA_SPREAD
-#define CLIMSR_DMA_SPREAD 1  // DMA pieces per k-step: 1 (k-steps 0..8, two at the last) or 2 (k-steps 0..4)
-#endif
-#ifndef CLIMSR_DMA_DIAG
-#define CLIMSR_DMA_DIAG 0  // diagnostic builds only: >= 1 = chunk 0 DMA'd, later chunks computed on stale buffers (3 / 5: no
-                           // epilogue stores, 4 / 5: no per-k-step fragment reads)
-#endif
 
 // Persistent over (tile, channel block) items v = blockIdx.x + k gridDim.x (host: gridDim.x <= #CUs, a multiple of 8,
 // so v's XCD is blockIdx.x's and xcd_major keeps a tile's channel blocks on one L2): the chunks of consecutive items
@@ -203,6 +196,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
 #pragma unroll
   for (int p = 0; p < 10; ++p) piece(p, 0, 0);
   int buf = 0;  // the buffer chunk j of the current item is in
+  bool later = false;  // an item after the workgroup's first (its epilogue stores were issued behind chunk 0's DMAs)
   for (;;) {
     const int vn = BN ? nitem : v + (int)gridDim.x;  // the next item (none with BatchNorm partials)
     int nimg_n = 0, oy0_n = 0, ox0_n = 0, co0_n = 0, ty_n = 0;
@@ -215,7 +209,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
       // chunk j's DMAs (this wave's) have landed; after the barrier every wave's have, and every wave is past its
       // fragment reads of the other buffer (and of its epilogue staging), which the next chunk now overwrites.  The
       // wait also drains the previous item's epilogue stores (issued after the DMAs of this chunk)
-      if (CNT && j == 0 && v != (int)blockIdx.x) {
+      if (CNT && j == 0 && later) {
         // chunk 0 of a later item: only its DMAs, not the previous item's epilogue stores issued after them
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST_ITEM) : "memory");
       } else {
@@ -229,7 +223,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
         decode(vn, nimg_n, oy0_n, ox0_n, co0_n, ty_n);
         offsets(nimg_n, oy0_n, ox0_n, co0_n);
       }
-      const bool more = CLIMSR_DMA_DIAG == 0 && (!last || vn < nitem);
+      const bool more = !last || vn < nitem;
       const uint32_t jn = last ? 0u : (uint32_t)(j + 1);
       const char* xb = smem + buf * DMA_BUF;
       const char* wb = xb + DMA_XB;
@@ -244,34 +238,15 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
       ld(0, 0);
 #pragma unroll
       for (int k = 0; k < 9; ++k) {
-#if CLIMSR_DMA_DIAG >= 4  // diagnostic 4: k-step fragments read once per chunk (MFMAs without LDS traffic)
-        if (k == 0) ld(1, 1);
-#else
         if (k + 1 < 9) ld(k + 1, (k + 1) & 1);
-#endif
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int m = 0; m < 4; ++m)
 #pragma unroll
           for (int t = 0; t < 4; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k & 1][t], bf[k & 1][m], acc[m][t], 0, 0, 0);
-        if (more) {
-          if (CLIMSR_DMA_SPREAD == 2) {
-            if (k < 5) {
-              piece(2 * k, jn, buf ^ 1);
-              piece(2 * k + 1, jn, buf ^ 1);
-            }
-          } else if (CLIMSR_DMA_SPREAD == 3) {  // pieces 0-3 / 4-6 / 7-9 behind the first three k-steps' MFMAs
-            if (k == 0) {
-              piece(0, jn, buf ^ 1); piece(1, jn, buf ^ 1); piece(2, jn, buf ^ 1); piece(3, jn, buf ^ 1);
-            } else if (k == 1) {
-              piece(4, jn, buf ^ 1); piece(5, jn, buf ^ 1); piece(6, jn, buf ^ 1);
-            } else if (k == 2) {
-              piece(7, jn, buf ^ 1); piece(8, jn, buf ^ 1); piece(9, jn, buf ^ 1);
-            }
-          } else {
-            piece(k, jn, buf ^ 1);
-            if (k == 8) piece(9, jn, buf ^ 1);
-          }
+        if (more) {  // one piece behind each k-step's MFMAs, two at the last (2 per k-step / 3-4-3 spreads: neutral)
+          piece(k, jn, buf ^ 1);
+          if (k == 8) piece(9, jn, buf ^ 1);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -410,9 +385,6 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
 #pragma unroll
           for (int t = 0; t < 2; ++t) *(f32x4*)(eb + (m * 16 + col) * EPH + t * 16 + g * 4) = acc[m][2 * h + t];
         lds_barrier();  // (orders the staging writes before the reads: another vector type)
-#if CLIMSR_DMA_DIAG == 3 || CLIMSR_DMA_DIAG == 5  // diagnostics 3 / 5: no epilogue
-        if (a.n < 0)
-#endif
         {
           if constexpr (CNT) dma_store_half<(CNT && !POOL) ? EP : 8>(a, eb, EPH, lane, nimg, oy0 + wave * 4, ox0, co0 + 32 * h);
           else store_tile_lds<RF, 64, 32, 64, EP>(a, eb, EPH, lane, nimg, oy0 + wave * 4, ox0, co0 + 32 * h);
@@ -421,6 +393,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_dma_kernel(FwdArgs a) {
     }
     if (vn >= nitem) break;
     v = vn;
+    later = true;
     nimg = nimg_n; oy0 = oy0_n; ox0 = ox0_n; co0 = co0_n; ty = ty_n;
   }
 }
@@ -433,9 +406,6 @@ int fwd_dma_launch(int ep, const FwdArgs& a, int ncob, hipStream_t s) {
   case E: k = rf ? conv_fwd_dma_kernel<E, true> : conv_fwd_dma_kernel<E, false>; break;
   switch (ep) {
     DMA_EP(0) DMA_EP(3) DMA_EP(4) DMA_EP(6) DMA_EP(7) DMA_EP(8) DMA_EP(9) DMA_EP(10) DMA_EP(11)
-#if CLIMSR_DMA_EP12  // (A/B builds: RDB conv5 / pull-x on this kernel, conv.hip)
-    DMA_EP(1) DMA_EP(2)
-#endif
     default: set_error("conv2d_fwd: no LDS-DMA kernel for epilogue %d", ep); return CLIMSR_EINVAL;
   }
 #undef DMA_EP
@@ -466,7 +436,8 @@ constexpr int S2D_XI = (S2D_TP * S2D_TP * 2 + 63) / 64;  // x DMA instructions p
 constexpr int S2D_WI = 64 * 9 * 2 / 64;                // weight DMA instructions per chunk (18)
 constexpr int S2D_XB = S2D_XI * 1024, S2D_BUF = S2D_XB + S2D_WI * 1024;  // 54,272 B per buffer
 constexpr int S2D_RED = 64 * 17 * 4;                   // per wave: channel-sum transpose [64][17]
-constexpr int S2D_LDS = 3 * S2D_BUF;                   // 162,816 B: three chunk buffers, two chunks in flight
+constexpr int S2D_DUMMY = 3 * S2D_BUF;                 // 162,816 B: three chunk buffers, two chunks in flight,
+constexpr int S2D_LDS = S2D_DUMMY + 1024;              // then one KB the padding DMA pieces write (zeros, never read)
 static_assert(S2D_LDS <= 160 * 1024, "stride-2 LDS-DMA conv");
 static_assert(8 * S2D_RED + 8 * 2 * 64 * 4 <= S2D_BUF, "BatchNorm scratch (aliases the buffer just computed)");
 
@@ -509,19 +480,35 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_s2_dma_kernel(FwdArgs a) {
     }
   };
   const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem;
+  // lag (tests/isa_waitcnt_lint.py): chunk 0's pieces are retired by the first hand wait after their issue, every later
+  // chunk's by the second (the next chunk is requested behind it)
+  bool lag2 = false;
   auto glds = [&](__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t lds) {
     uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(off), "s"(rs), "s"(lds) : "memory");
+    if (lag2)
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds ; dma-lag 2\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(off), "s"(rs), "s"(lds) : "memory");
+    else
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(off), "s"(rs), "s"(lds) : "memory");
   };
-  // chunk c (16 channels): x source offset + 32 c bytes; weights: packing chunk c / 2 (288 elements each), half c % 2
-  auto piece = [&](int p, int c, int b) {
+  // chunk c (16 channels): x source offset + 32 c bytes; weights: packing chunk c / 2 (288 elements each), half c % 2.
+  // Every wave issues all 8 pieces of a chunk: those past the 35 x / 18 weight instructions read out of range into the
+  // dummy KB, so one count fits every wave's waits (with 8 / 7 / 6 real pieces per wave the waits were per-wave counts
+  // that depended on the same wave index as the issue conditions).  (7 pieces per wave -- 3 padding pieces instead of
+  // 11 -- leaves 10 operations behind a chunk's fourth piece, fewer than the 11 the first two chunks of a later item
+  // wait for; the wait lint cannot tell those chunks from the rest, so the padding stays at 8.)
+  auto piece = [&](int p, int c, int b, bool any = true) {  // any = false: nothing to request (dummy pieces only)
     const uint32_t base = lds0 + (uint32_t)(b * S2D_BUF);
     if (p < 5) {
-      if (wvu + 8 * p < S2D_XI) glds(xr, xo[p] == BUF_OOB ? BUF_OOB : xo[p] + (uint32_t)(32 * c), base + (uint32_t)((wvu + 8 * p) * 1024));
-    } else if (wvu + 8 * (p - 5) < S2D_WI) {
+      const bool real = any && wvu + 8 * p < S2D_XI;
+      glds(xr, real && xo[p] != BUF_OOB ? xo[p] + (uint32_t)(32 * c) : BUF_OOB,
+           real ? base + (uint32_t)((wvu + 8 * p) * 1024) : lds0 + (uint32_t)S2D_DUMMY);
+    } else {
+      const bool real = any && wvu + 8 * (p - 5) < S2D_WI;
       const uint32_t add = (uint32_t)(((c >> 1) * 288 + 16 * (c & 1)) * 2);
-      glds(wr, wo[p - 5] == BUF_OOB ? BUF_OOB : wo[p - 5] + add, base + (uint32_t)(S2D_XB + (wvu + 8 * (p - 5)) * 1024));
+      glds(wr, real && wo[p - 5] != BUF_OOB ? wo[p - 5] + add : BUF_OOB,
+           real ? base + (uint32_t)(S2D_XB + (wvu + 8 * (p - 5)) * 1024) : lds0 + (uint32_t)S2D_DUMMY);
     }
   };
   // fragment reads: k block kk, lane group g -> tap 2 kk + (g >> 1) (tap 9: read tap 8 under zero weights), half g & 1
@@ -534,14 +521,14 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_s2_dma_kernel(FwdArgs a) {
   decode(v, nimg, oy0, ox0, co0, tile);
   offsets(nimg, oy0, ox0, co0);
   // chunks 0 and 1 in flight before the loop; chunk c + 2 (of this item, or of the next one) is requested during chunk
-  // c into the third buffer.  A wave's DMA pieces per chunk: 8 (waves 0, 1), 7 (wave 2), 6 (waves 3-7)
+  // c into the third buffer: 8 DMA pieces per wave and chunk
 #pragma unroll
   for (int p = 0; p < 8; ++p) piece(p, 0, 0);
+  lag2 = true;
 #pragma unroll
   for (int p = 0; p < 8; ++p) piece(p, 1, 1);
-  const int npc = wvu < 2 ? 8 : (wvu == 2 ? 7 : 6);
   int cur = 0;  // the buffer of the chunk being computed
-  bool pm = true;  // the previous chunk requested pieces (chunk 1's went out before the loop)
+  bool later = false;  // an item after the workgroup's first (its epilogue stores were issued between its chunks 0 and 1)
   for (;;) {
     const int vn = v + (int)gridDim.x;
     int nimg_n = 0, oy0_n = 0, ox0_n = 0, co0_n = 0, tile_n = 0;
@@ -551,22 +538,11 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_s2_dma_kernel(FwdArgs a) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) acc[m][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
     for (int c = 0; c < nch; ++c, cur = cur == 2 ? 0 : cur + 1) {
-      // chunk c has landed once at most the younger requests are outstanding: the next chunk's pieces, and at chunks
-      // 0 / 1 of a later item also the previous item's 4 epilogue stores (issued between them)
-      const bool st = c < 2 && v != (int)blockIdx.x;
-      if (!pm) {  // the last chunks of the last item: nothing was requested behind this chunk (at most the stores)
-        if (st) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      } else if (npc == 8) {
-        if (st) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      } else if (npc == 7) {
-        if (st) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-      } else {
-        if (st) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      }
+      // chunk c has landed once at most the younger requests are outstanding: the next chunk's 8 pieces (dummies behind
+      // the last two chunks of the last item), and at chunks 0 / 1 of a later item also the previous item's 4 epilogue
+      // stores (issued between them)
+      if (c < 2 && later) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       lds_barrier();
       // the request of this chunk: chunk c + 2 of this item, or chunk c + 2 - nch of the next one (whose offsets
       // replace this item's once every piece of this item has been requested)
@@ -601,13 +577,12 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_s2_dma_kernel(FwdArgs a) {
         for (int m = 0; m < 2; ++m)
 #pragma unroll
           for (int t = 0; t < 4; ++t) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk & 1][t], bq[kk & 1][m], acc[m][t], 0, 0, 0);
-        if (more && kk < 4) {  // the requested chunk's 8 DMA pieces, two per k block behind its MFMAs
-          piece(2 * kk, cn, bn);
-          piece(2 * kk + 1, cn, bn);
+        if (kk < 4) {  // the requested chunk's 8 DMA pieces, two per k block behind its MFMAs
+          piece(2 * kk, cn, bn, more);
+          piece(2 * kk + 1, cn, bn, more);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
-      pm = more;
     }
     // ---- epilogue straight from the accumulators: lane (col, g) holds channels co0 + 16 t + 4 g .. + 3 of output pixel
     // (oy0 + 2 wave + m, ox0 + col); co-block pairs traded between lane rows (v_permlane16_swap) -> 4 16-B stores per
@@ -679,6 +654,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_s2_dma_kernel(FwdArgs a) {
     }
     if (vn >= nitem) break;
     v = vn;
+    later = true;
     nimg = nimg_n; oy0 = oy0_n; ox0 = ox0_n; co0 = co0_n; tile = tile_n;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -117,9 +117,9 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
   const int ups = a.up == 2 ? 1 : 0, lh = a.in_h << ups, lw = a.in_w << ups;
   // in asm (not the builtin): hipcc would wait vmcnt(0) before the next ds_read for an LDS write of unknown extent;
   // the DMAs are counted by hand.  M0 = the instruction's LDS destination (wave-uniform).
-  auto glds = [&](uint32_t off, uint32_t lds) {
+  auto glds = [&](uint32_t off, uint32_t lds) {  // (retired by the second hand wait after it: tests/isa_waitcnt_lint.py)
     uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds ; dma-lag 2\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(off), "s"(xr), "s"(lds) : "memory");
   };
   auto decode = [&](int tile, int& nimg, int& oy0, int& ox0) {

@@ -744,12 +744,10 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(const uint16_t* __restr
 // per k-step feeds 4 MFMAs instead of one -- the x operand (re-read by every workgroup of a K slice) was 2/3 of the
 // load instructions of the form above.  Workgroup = 256 rows, grid = (o / 256) x nsplit.  Measured at fc.0 (n 32,
 // k 100352, o 1024): 65 us = 3.2 TB/s of weights with 3 workgroups per CU; 8 or 16 waves per workgroup splitting K
-// inside it (partials met in LDS) were slower (68-110 us), as were 1.5 or 6 workgroups per CU.
-//
-// FRAG: W in fragment order (linear_frag_index below): the wave's 64 rows x 32 k of one k-step are one contiguous 4 KB
-// piece, so an LU round streams 16 KB straight from HBM (the row-major form reads 64 B from each of 64 rows 200 KB
-// apart per fragment load).
-template <int NF, bool FRAG>
+// inside it (partials met in LDS) were slower (68-110 us), as were 1.5 or 6 workgroups per CU.  (A fragment-order copy
+// of W -- 4 KB contiguous per wave and k-step -- ran 53 instead of 64 us, but the AdamW pass that writes the copy gave
+// the time back: DESIGN.md 3.6; removed.)
+template <int NF>
 __global__ __launch_bounds__(256) void linear_fwd_wide_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, int n,
                                                               int k, int o, int ksplit, float* __restrict__ part) {
   constexpr int NA = 4, LU = 4;
@@ -762,11 +760,9 @@ __global__ __launch_bounds__(256) void linear_fwd_wide_kernel(const uint16_t* __
   for (int t = 0; t < NA; ++t)
 #pragma unroll
     for (int f = 0; f < NF; ++f) acc[t][f] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  // A fragment t of k-step kk: row-major w[(o0 + 16t + col) * k + kk + 8g]; fragment order: piece (o0/64, kk/32, t)
-  const uint16_t* wrow = FRAG ? w + (long)(o0 >> 6) * (k >> 5) * 2048 + lane * 8 : w + (long)(o0 + col) * k + g * 8;
-  auto wfrag = [&](int t, int kk) -> bf16x8 {
-    return FRAG ? *(const bf16x8*)(wrow + (long)(kk >> 5) * 2048 + t * 512) : *(const bf16x8*)(wrow + (long)t * 16 * k + kk);
-  };
+  // A fragment t of k-step kk: w[(o0 + 16t + col) * k + kk + 8g]
+  const uint16_t* wrow = w + (long)(o0 + col) * k + g * 8;
+  auto wfrag = [&](int t, int kk) -> bf16x8 { return *(const bf16x8*)(wrow + (long)t * 16 * k + kk); };
   int kk = kb;
   for (; kk + 32 * LU <= ke; kk += 32 * LU) {
     bf16x8 af[LU][NA], bfr[LU][NF];
@@ -834,11 +830,11 @@ __global__ void linear_reduce_kernel(const float* __restrict__ part, int nsplit,
   if (ybf) ybf[idx] = f2bf(s);
 }
 
-static int linear_fwd_launch(const uint16_t* x, const uint16_t* w, const float* bias, int n, int k, int o, int act, float slope,
-                             float* workspace, int64_t ws_floats, float* y, void* stream, bool frag) {
-  const char* who = frag ? "linear_fwd_frag" : "linear_fwd";
-  if (!x || !w || !y || !workspace || n <= 0 || n > 64 || k % 32 || o % (frag ? 256 : 16)) {
-    set_error("%s: bad args (n=%d k=%d o=%d; need n<=64, k%%32==0, o%%%d==0)", who, n, k, o, frag ? 256 : 16);
+extern "C" int climsr_linear_fwd(const uint16_t* x, const uint16_t* w, const float* bias, int n, int k, int o, int act, float slope,
+                                 float* workspace, int64_t ws_floats, float* y, void* stream) {
+  const char* who = "linear_fwd";
+  if (!x || !w || !y || !workspace || n <= 0 || n > 64 || k % 32 || o % 16) {
+    set_error("%s: bad args (n=%d k=%d o=%d; need n<=64, k%%32==0, o%%16==0)", who, n, k, o);
     return CLIMSR_EINVAL;
   }
   const bool wide = o % 256 == 0;
@@ -855,52 +851,16 @@ static int linear_fwd_launch(const uint16_t* x, const uint16_t* w, const float* 
   hipStream_t s = (hipStream_t)stream;
   const int nf = (n + 15) / 16;
   dim3 grid(oblk, nsplit);
-  if (frag) {
-    if (nf == 1) hipLaunchKernelGGL((linear_fwd_wide_kernel<1, true>), grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
-    else if (nf == 2) hipLaunchKernelGGL((linear_fwd_wide_kernel<2, true>), grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
-    else hipLaunchKernelGGL((linear_fwd_wide_kernel<4, true>), grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
-  } else if (wide) {
-    if (nf == 1) hipLaunchKernelGGL((linear_fwd_wide_kernel<1, false>), grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
-    else if (nf == 2) hipLaunchKernelGGL((linear_fwd_wide_kernel<2, false>), grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
-    else hipLaunchKernelGGL((linear_fwd_wide_kernel<4, false>), grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
+  if (wide) {
+    if (nf == 1) hipLaunchKernelGGL(linear_fwd_wide_kernel<1>, grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
+    else if (nf == 2) hipLaunchKernelGGL(linear_fwd_wide_kernel<2>, grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
+    else hipLaunchKernelGGL(linear_fwd_wide_kernel<4>, grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
   } else if (nf == 1) hipLaunchKernelGGL(linear_fwd_kernel<1>, grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
   else if (nf == 2) hipLaunchKernelGGL(linear_fwd_kernel<2>, grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
   else hipLaunchKernelGGL(linear_fwd_kernel<4>, grid, dim3(256), 0, s, x, w, n, k, o, ksplit, workspace);
   hipLaunchKernelGGL(linear_reduce_kernel, dim3(ceil_div((long)n * o, 256)), dim3(256), 0, s, workspace, nsplit, n, o, bias, act, slope,
                      y, (uint16_t*)nullptr);
   return check_launch(who);
-}
-
-extern "C" int climsr_linear_fwd(const uint16_t* x, const uint16_t* w, const float* bias, int n, int k, int o, int act, float slope,
-                                 float* workspace, int64_t ws_floats, float* y, void* stream) {
-  return linear_fwd_launch(x, w, bias, n, k, o, act, slope, workspace, ws_floats, y, stream, false);
-}
-
-extern "C" int climsr_linear_fwd_frag(const uint16_t* x, const uint16_t* wf, const float* bias, int n, int k, int o, int act, float slope,
-                                      float* workspace, int64_t ws_floats, float* y, void* stream) {
-  return linear_fwd_launch(x, wf, bias, n, k, o, act, slope, workspace, ws_floats, y, stream, true);
-}
-
-// fp32 [o][k] -> bf16 fragment order; one thread per 16 B of output (sequential stores, 32 B row-segment reads)
-__global__ void linear_pack_frag_kernel(const float* __restrict__ w, int k, long n8, uint16_t* __restrict__ wf) {
-  const long e8 = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e8 >= n8) return;
-  const int lane = e8 & 63, t = (e8 >> 6) & 3;
-  const long kbn = k >> 5, piece = e8 >> 8, ob = piece / kbn, kb = piece - ob * kbn;
-  const long r = ob * 64 + t * 16 + (lane & 15), c = kb * 32 + (lane >> 4) * 8;
-  const float4 a = *(const float4*)(w + r * k + c), b = *(const float4*)(w + r * k + c + 4);
-  *(uint4*)(wf + e8 * 8) = make_uint4((uint32_t)f2bf(a.x) | ((uint32_t)f2bf(a.y) << 16), (uint32_t)f2bf(a.z) | ((uint32_t)f2bf(a.w) << 16),
-                                      (uint32_t)f2bf(b.x) | ((uint32_t)f2bf(b.y) << 16), (uint32_t)f2bf(b.z) | ((uint32_t)f2bf(b.w) << 16));
-}
-
-extern "C" int climsr_linear_pack_frag(const float* w, int o, int k, uint16_t* wf, void* stream) {
-  if (!w || !wf || o <= 0 || k <= 0 || o % 64 || k % 32) {
-    set_error("linear_pack_frag: bad args (o=%d k=%d; need o%%64==0, k%%32==0)", o, k);
-    return CLIMSR_EINVAL;
-  }
-  const long n8 = (long)o * k / 8;
-  hipLaunchKernelGGL(linear_pack_frag_kernel, dim3(ceil_div(n8, 256)), dim3(256), 0, (hipStream_t)stream, w, k, n8, wf);
-  return check_launch("linear_pack_frag");
 }
 
 // data gradient dx[n][k] = sum_o dy[n][o] W[o][k]:  A = dy rows (n, o-contiguous), B = W^T taken
@@ -972,9 +932,7 @@ __global__ __launch_bounds__(256) void linear_dgrad_kernel(const uint16_t* __res
 // Wide form (k % 128 == 0, the fc.0 case): a workgroup owns 128 k columns (two 16-column fragments per wave), so a W
 // tile row is 256 contiguous bytes, and the dy fragments of the next 128-row o tile are loaded into registers together
 // with the next W tile (the form above reads them from global memory right before each MFMA).
-// FRAG: W in fragment order (common.h linear_frag_index); a 128 o x 128 k tile is then two contiguous 16 KB runs (the
-// row-major tile is 128 rows of 256 B, 200 KB apart), written to the same LDS positions.
-template <int NF, bool FRAG>
+template <int NF>
 __global__ __launch_bounds__(256) void linear_dgrad_wide_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ w, int n,
                                                                 int k, int o, float* __restrict__ dx, int accumulate) {
   constexpr int WP = 128 + 8;  // LDS row pitch (bf16)
@@ -989,25 +947,14 @@ __global__ __launch_bounds__(256) void linear_dgrad_wide_kernel(const uint16_t* 
     for (int f = 0; f < NF; ++f) acc[b][f] = (f32x4){0.f, 0.f, 0.f, 0.f};
   uint4 buf[8];
   bf16x8 dyf[4][NF];
-  // vector v (16 B) of a tile: row-major, row v / 16 and k 8 (v % 16); fragment order, piece (obl, kbl, t) = v / 64
-  // and lane v % 64, i.e. row 64 obl + 16 t + lane % 16 and k 32 kbl + 8 (lane / 16)
-  auto lds_pos = [&](int v) -> int {
-    if (!FRAG) return (v >> 4) * WP + (v & 15) * 8;
-    return ((v >> 10) * 64 + ((v >> 6) & 3) * 16 + (v & 15)) * WP + ((v >> 8) & 3) * 32 + ((v >> 4) & 3) * 8;
-  };
-  const long kbn = k >> 5;
+  // vector v (16 B) of a tile: row v / 16, k 8 (v % 16)
+  auto lds_pos = [&](int v) -> int { return (v >> 4) * WP + (v & 15) * 8; };
   auto issue = [&](int ob) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int v = tid + i * 256;
-      if (FRAG) {
-        const int obl = v >> 10;
-        const long piece = ((long)((ob >> 6) + obl) * kbn + (k0 >> 5) + ((v >> 8) & 3)) * 4 + ((v >> 6) & 3);
-        buf[i] = ob + obl * 64 < o ? *(const uint4*)(w + piece * 512 + (v & 63) * 8) : make_uint4(0, 0, 0, 0);
-      } else {
-        const int r = v >> 4, cv = v & 15;
-        buf[i] = ob + r < o ? *(const uint4*)(w + (long)(ob + r) * k + k0 + cv * 8) : make_uint4(0, 0, 0, 0);
-      }
+      const int r = v >> 4, cv = v & 15;
+      buf[i] = ob + r < o ? *(const uint4*)(w + (long)(ob + r) * k + k0 + cv * 8) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks)
@@ -1059,21 +1006,6 @@ __global__ __launch_bounds__(256) void linear_dgrad_wide_kernel(const uint16_t* 
   }
 }
 
-extern "C" int climsr_linear_dgrad_frag(const uint16_t* dy, const uint16_t* wf, int n, int k, int o, float* dx, int accumulate,
-                                        void* stream) {
-  if (!dy || !wf || !dx || n <= 0 || n > 64 || k % 128 || o % 64) {
-    set_error("linear_dgrad_frag: bad args (n=%d k=%d o=%d; need n<=64, k%%128==0, o%%64==0)", n, k, o);
-    return CLIMSR_EINVAL;
-  }
-  hipStream_t s = (hipStream_t)stream;
-  const int nf = (n + 15) / 16;
-  dim3 gw(k / 128);
-  if (nf == 1) hipLaunchKernelGGL((linear_dgrad_wide_kernel<1, true>), gw, dim3(256), 0, s, dy, wf, n, k, o, dx, accumulate);
-  else if (nf == 2) hipLaunchKernelGGL((linear_dgrad_wide_kernel<2, true>), gw, dim3(256), 0, s, dy, wf, n, k, o, dx, accumulate);
-  else hipLaunchKernelGGL((linear_dgrad_wide_kernel<4, true>), gw, dim3(256), 0, s, dy, wf, n, k, o, dx, accumulate);
-  return check_launch("linear_dgrad_frag");
-}
-
 extern "C" int climsr_linear_dgrad(const uint16_t* dy, const uint16_t* w, int n, int k, int o, float* dx, int accumulate,
                                    void* stream) {
   if (!dy || !w || !dx || n <= 0 || n > 64 || k % 64 || o % 32) {
@@ -1084,9 +1016,9 @@ extern "C" int climsr_linear_dgrad(const uint16_t* dy, const uint16_t* w, int n,
   const int nf = (n + 15) / 16;
   if (k % 128 == 0) {
     dim3 gw(k / 128);
-    if (nf == 1) hipLaunchKernelGGL((linear_dgrad_wide_kernel<1, false>), gw, dim3(256), 0, s, dy, w, n, k, o, dx, accumulate);
-    else if (nf == 2) hipLaunchKernelGGL((linear_dgrad_wide_kernel<2, false>), gw, dim3(256), 0, s, dy, w, n, k, o, dx, accumulate);
-    else hipLaunchKernelGGL((linear_dgrad_wide_kernel<4, false>), gw, dim3(256), 0, s, dy, w, n, k, o, dx, accumulate);
+    if (nf == 1) hipLaunchKernelGGL(linear_dgrad_wide_kernel<1>, gw, dim3(256), 0, s, dy, w, n, k, o, dx, accumulate);
+    else if (nf == 2) hipLaunchKernelGGL(linear_dgrad_wide_kernel<2>, gw, dim3(256), 0, s, dy, w, n, k, o, dx, accumulate);
+    else hipLaunchKernelGGL(linear_dgrad_wide_kernel<4>, gw, dim3(256), 0, s, dy, w, n, k, o, dx, accumulate);
     return check_launch("linear_dgrad");
   }
   dim3 grid(k / 64);

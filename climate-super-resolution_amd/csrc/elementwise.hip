@@ -413,68 +413,6 @@ extern "C" int climsr_adamw_step(int64_t n, float* p, const float* g, float* m, 
   return check_launch("adamw_step");
 }
 
-// The mirrored weight [o][k] at p[0, o*k) (p = flat + lo) with its bf16 copy in fragment order (common.h
-// linear_frag_index, the operand layout of climsr_linear_fwd_frag / _dgrad_frag).  Tiles of 16 rows x 256 k: a wave
-// issues the loads of its 4 rows (one fully used 1 KB fp32 run per array each) before any update, and the copy is
-// staged in LDS and stored as eight whole 1 KB fragments.  fc.0 block (102.8 M parameters) on one MI355X: 581 us
-// against 566 us for the row-major mirror's share of its pass; 8 B scattered copy stores were 629-688 us, one row
-// per wave 655 us (tools/bench_linear_fc0.py).
-__global__ __launch_bounds__(256) void adamw_frag_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                                                         float* __restrict__ v, const float* __restrict__ hp, int k,
-                                                         uint16_t* __restrict__ mirror) {
-  __shared__ __attribute__((aligned(16))) uint16_t stage[8 * 512];
-  const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4], step_size = hp[5], bc2s = hp[6];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const long c = (long)blockIdx.x * 256 + lane * 4, kbn = k >> 5;
-  float4 pp[4], gg[4], mm[4], vv[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const long e = ((long)blockIdx.y * 16 + wave * 4 + i) * k + c;
-    pp[i] = *(float4*)(p + e); gg[i] = *(const float4*)(g + e); mm[i] = *(float4*)(m + e); vv[i] = *(float4*)(v + e);
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int rl = wave * 4 + i, cl = lane * 4;  // (row, k) inside the 16 x 256 tile
-    const long e = ((long)blockIdx.y * 16 + rl) * k + c;
-    // the update of adamw_update4, operation for operation (p / m / v bit-identical to climsr_adamw_step)
-    float* P = (float*)&pp[i]; const float* G = (const float*)&gg[i]; float* M = (float*)&mm[i]; float* V = (float*)&vv[i];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      P[q] *= 1.f - lr * wd;
-      M[q] = M[q] + (G[q] - M[q]) * (1.f - b1);
-      V[q] = V[q] * b2 + G[q] * G[q] * (1.f - b2);
-      P[q] -= step_size * (M[q] / (sqrtf(V[q]) / bc2s + eps));
-    }
-    *(float4*)(p + e) = pp[i]; *(float4*)(m + e) = mm[i]; *(float4*)(v + e) = vv[i];
-    *(uint2*)(stage + ((cl >> 5) * 64 + rl + 16 * ((cl >> 3) & 3)) * 8 + (cl & 7)) = bf16x4_pack(pp[i]);
-  }
-  __syncthreads();
-  const long r0 = (long)blockIdx.y * 16, ob = r0 >> 6, t = (r0 >> 4) & 3, kb0 = (long)blockIdx.x * 8;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int u = threadIdx.x + h * 256, f = u >> 6, ln = u & 63;
-    *(uint4*)(mirror + (((ob * kbn + kb0 + f) * 4 + t) * 64 + ln) * 8) = *(const uint4*)(stage + u * 8);
-  }
-}
-
-extern "C" int climsr_adamw_step_mirror_frag(int64_t n, float* p, const float* g, float* m, float* v, const float* hp, int64_t mirror_lo,
-                                             int o, int k, uint16_t* mirror, void* stream) {
-  if (!p || !g || !m || !v || !hp || n <= 0 || !mirror || mirror_lo < 0 || mirror_lo % 4 || o <= 0 || k <= 0 || o % 64 || k % 256 ||
-      mirror_lo + (int64_t)o * k > n) {
-    set_error("adamw_step_mirror_frag: bad args (lo=%lld o=%d k=%d; need lo%%4==0, o%%64==0, k%%256==0)", (long long)mirror_lo, o, k);
-    return CLIMSR_EINVAL;
-  }
-  hipStream_t s = (hipStream_t)stream;
-  const long lo = mirror_lo, hi = mirror_lo + (long)o * k;
-  if (lo > 0)
-    hipLaunchKernelGGL(adamw_kernel, dim3(ceil_div((lo + 3) / 4, 256)), dim3(256), 0, s, lo, p, g, m, v, hp, (uint16_t*)nullptr, 0L, 0L);
-  hipLaunchKernelGGL(adamw_frag_kernel, dim3(k / 256, o / 16), dim3(256), 0, s, p + lo, g + lo, m + lo, v + lo, hp, k, mirror);
-  if (hi < n)
-    hipLaunchKernelGGL(adamw_kernel, dim3(ceil_div((n - hi + 3) / 4, 256)), dim3(256), 0, s, (long)(n - hi), p + hi, g + hi, m + hi,
-                       v + hi, hp, (uint16_t*)nullptr, 0L, 0L);
-  return check_launch("adamw_step_mirror_frag");
-}
-
 extern "C" int climsr_adamw_step_mirror(int64_t n, float* p, const float* g, float* m, float* v, const float* hp, int64_t mirror_lo,
                                         int64_t mirror_n, uint16_t* mirror, void* stream) {
   if (!p || !g || !m || !v || !hp || n <= 0 || !mirror || mirror_lo < 0 || mirror_n <= 0 || mirror_lo + mirror_n > n) {

@@ -61,9 +61,6 @@ constexpr int RR_OFF_2 = RR_OFF_D + RR_N1 * RR_DROW, RR_OFF_3 = RR_OFF_2 + RR_N2
 constexpr int RR_OFF_DUMMY = RR_OFF_3 + RR_N3 * RR_DROW;  // one KB the padding DMA pieces write (zeros, never read)
 constexpr int RR_LDS = RR_OFF_DUMMY + 1024;             // 127,744 B
 constexpr int RR_K = 2;                                 // base-row DMA pieces per wave (11 real + 5 padding)
-#ifndef CLIMSR_RR_EXP  // timing experiments of diagnostic builds only: 1 no step DMA, 3 no HBM row stores, 5 no MFMAs
-#define CLIMSR_RR_EXP 0  // -- their results are wrong
-#endif
 
 __device__ __forceinline__ uint32_t pack2_bf16(float a, float b) {
   const bf16x2 v = {(__bf16)a, (__bf16)b};  // v_cvt_pk_bf16_f32 (RNE)
@@ -105,7 +102,7 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, char* smem, int ti
     for (int j = 0; j < RR_K; ++j) {
       const bool real = ok && wvu + 8 * j < RR_BNI;
       uint32_t keep;
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds ; dma-lag 2\n\ts_mov_b32 m0, %0"
                    : "=&s"(keep) : "v"(real && po[j] != BUF_OOB ? po[j] + rb : BUF_OOB), "s"(br),
                      "s"(real ? slot + (uint32_t)((wvu + 8 * j) * 1024) : lds0 + (uint32_t)RR_OFF_DUMMY)
                    : "memory");
@@ -209,7 +206,7 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, char* smem, int ti
         msk[K] = __builtin_bit_cast(v4u32, __builtin_amdgcn_raw_buffer_load_b128(
                                                mr, liveq ? (uint32_t)(nimg * a.h + y2) * mrow + (uint32_t)(ml * 2) : BUF_OOB, 0, 0));
     }
-    if (CLIMSR_RR_EXP != 1) dma_row(r0 - 2 + s);  // the base row level 1 ingests in step s + 2
+    dma_row(r0 - 2 + s);  // the base row level 1 ingests in step s + 2
     // ingest row i.  All three kernel rows and both fragments are computed unconditionally: a target row outside this
     // level's finished range or outside the image is never finished from its accumulator (the rows a finished row
     // needs are all ingested), and the pixel slots of a fragment past the image width hold zeros
@@ -254,8 +251,7 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, char* smem, int ti
           constexpr int SL[3] = {SN, SI, SP};
 #pragma unroll
           for (int f = 0; f < 2; ++f)
-            if (CLIMSR_RR_EXP != 5) acc[SL[ky]][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, B[grp & 1][f], acc[SL[ky]][f], 0, 0, 0);
-            else acc[SL[ky]][f] += __builtin_bit_cast(f32x4, B[grp & 1][f]);
+            acc[SL[ky]][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, B[grp & 1][f], acc[SL[ky]][f], 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -294,7 +290,7 @@ __device__ __forceinline__ void run_level(const ChainArgs& a, char* smem, int ti
         if (liveq) *(uint4*)(ring + dl) = o8;
       }
     }
-    if (fin && yin && y >= r0 && y < r1 && CLIMSR_RR_EXP != 3)  // (wave-uniform) one of the strip's own rows
+    if (fin && yin && y >= r0 && y < r1)  // (wave-uniform) one of the strip's own rows
       __builtin_amdgcn_raw_buffer_store_b128((v4u32){o8.x, o8.y, o8.z, o8.w}, orr,
                                              liveq ? (uint32_t)(nimg * a.h + y) * orow + (uint32_t)(ol * 2) : BUF_OOB, 0, 0);
 #pragma unroll

@@ -122,7 +122,7 @@ __global__ __launch_bounds__(512, 1) void stem_s2_kernel(StemArgs a) {
       }
     }
     // where each of this wave's region pixels goes: its LDS image slot (bit 30 set: outside the image, the slot gets
-    // zeros) and, when kept, its byte offset in a0 (own pixels only; BUF_OOB otherwise), channel 0
+    // zeros) and, when kept, the byte offset of its channel 0 in a0 (own pixels only; BUF_OOB otherwise)
     uint32_t soff[ST_FPW], aoff[ST_FPW];
 #pragma unroll
     for (int i = 0; i < ST_FPW; ++i) {
@@ -130,30 +130,51 @@ __global__ __launch_bounds__(512, 1) void stem_s2_kernel(StemArgs a) {
       const int iy = iy0 + r, ix = ix0 + cc;
       const bool in_img = iy >= 0 && iy < a.h && ix >= 0 && ix < a.w;
       soff[i] = pv ? (uint32_t)((r * ST_TP + slot_of(cc)) * 32 + g * 8) | (in_img ? 0u : 0x40000000u) : 0xFFFFFFFFu;
-      aoff[i] = KEEP && pv && in_img && r >= 1 && cc >= 1 ? (uint32_t)(((nimg * a.h + iy) * a.w + ix) * 64 + 4 * g) * 2u : BUF_OOB;
+      aoff[i] = KEEP && pv && in_img && r >= 1 && cc >= 1 ? (uint32_t)(((nimg * a.h + iy) * a.w + ix) * 64) * 2u : BUF_OOB;
     }
     // features.0 chunk c (channels 16 c ..) of the region -> image buffer c & 1 (and the kept output), three MFMAs at a
-    // time
+    // time.  The kept output is stored per chunk pair, by the odd chunk: it recomputes the even chunk's values (one more
+    // MFMA per fragment; holding them in registers across the conv spilled), trades the pair's channel groups between
+    // lane rows g, g ^ 1 (v_permlane16_swap) so that each lane holds 8 consecutive channels, and the 4 lanes of a pixel
+    // store the pair's 64 contiguous bytes as 16-B stores (8-B stores per chunk wrote 32 B of each 128-B pixel run:
+    // 2.3x the tensor in WRITE_SIZE)
+    auto lrelu_pack = [&](const f32x4& z) -> v2u32 {
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaxf(z[e], z[e] * a.slope);  // LeakyReLU, 0 <= slope <= 1
+      const bf16x2 q0 = {(__bf16)v[0], (__bf16)v[1]}, q1 = {(__bf16)v[2], (__bf16)v[3]};
+      return (v2u32){__builtin_bit_cast(uint32_t, q0), __builtin_bit_cast(uint32_t, q1)};
+    };
     auto stem = [&](int c) {
       char* xb = smem + ST_OFF_X + (c & 1) * ST_XB;
 #pragma unroll
       for (int i0 = 0; i0 < ST_FPW; i0 += 3) {
         f32x4 z[3];
+        f32x4 zp[3];  // (KEEP, odd chunk: the even chunk recomputed)
 #pragma unroll
-        for (int k = 0; k < 3; ++k) z[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A0[c], Bs[i0 + k], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        for (int k = 0; k < 3; ++k) {
+          z[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A0[c], Bs[i0 + k], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          if (KEEP && (c & 1)) zp[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A0[c - 1], Bs[i0 + k], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        }
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
           const int i = i0 + k;
           if (wave + 8 * i < ST_NF) {
-            float v[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = fmaxf(z[k][e], z[k][e] * a.slope);  // LeakyReLU, 0 <= slope <= 1
-            const bf16x2 q0 = {(__bf16)v[0], (__bf16)v[1]}, q1 = {(__bf16)v[2], (__bf16)v[3]};
+            const v2u32 pv = lrelu_pack(z[k]);
             const bool zero = soff[i] & 0x40000000u;
-            const v2u32 pk = {zero ? 0u : __builtin_bit_cast(uint32_t, q0), zero ? 0u : __builtin_bit_cast(uint32_t, q1)};
+            const v2u32 pk = {zero ? 0u : pv[0], zero ? 0u : pv[1]};
             if (soff[i] != 0xFFFFFFFFu) *(v2u32*)(xb + (soff[i] & 0x3FFFFFFFu)) = pk;
-            if constexpr (KEEP)
-              __builtin_amdgcn_raw_buffer_store_b64(pk, ar, aoff[i] == BUF_OOB ? BUF_OOB : aoff[i] + (uint32_t)(32 * c), 0, 0);
+            if constexpr (KEEP) {
+              if (c & 1) {  // lane (col, g): channels 16 (c - 1 + (g & 1)) + 8 (g >> 1) .. + 7 of its pixel
+                const v2u32 pe = lrelu_pack(zp[k]);
+                const auto sx = __builtin_amdgcn_permlane16_swap(pe[0], pv[0], false, false);
+                const auto sy = __builtin_amdgcn_permlane16_swap(pe[1], pv[1], false, false);
+                typedef uint32_t v4u32_t __attribute__((ext_vector_type(4)));
+                const v4u32_t o = {sx[0], sy[0], sx[1], sy[1]};
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    o, ar, aoff[i] == BUF_OOB ? BUF_OOB : aoff[i] + (uint32_t)((16 * (c - 1 + (g & 1)) + 8 * (g >> 1)) * 2), 0, 0);
+              }
+            }
           }
         }
         __builtin_amdgcn_sched_barrier(0);

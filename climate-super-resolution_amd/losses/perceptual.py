@@ -50,7 +50,6 @@ class PerceptualLoss(nn.Module):
         self.loss_network = loss_network
         self._plans = None
         self._dev = None
-        self.fuse_pool = True  # conv + ReLU + max pool in one launch where pool_ok (False: tools/perf_stem.py's A/B)
 
     def _build(self, dev):
         plans = []
@@ -74,7 +73,7 @@ class PerceptualLoss(nn.Module):
         a, cs = x3, 8
         for p, relu, pool in self._plans:
             act = ACT_RELU if relu else ACT_NONE
-            if pool and self.fuse_pool and p.pool_ok(cs, h, w, n, p.cout, act):  # conv + ReLU + 2x2 max pool in one kernel
+            if pool and p.pool_ok(cs, h, w, n, p.cout, act):  # conv + ReLU + 2x2 max pool in one kernel
                 h, w = h // 2, w // 2
                 y = torch.empty((n, h, w, p.cout), dtype=torch.bfloat16, device=x3.device)
                 p.fwd(a, cs, 0, 2 * h, 2 * w, y, p.cout, 0, n, act=act, out_mode=OUT_BF16, pool2=True)

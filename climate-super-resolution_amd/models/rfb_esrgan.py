@@ -14,14 +14,13 @@ requires grad.
 """
 from __future__ import annotations
 
-import os
 from typing import Dict, List
 
 import torch
 import torch.nn as nn
 from torch import Tensor
 
-from .. import _lib, ops
+from .. import ops
 from ..core.flat import FlatParamsMixin
 from ..ops import ACT_LRELU, ACT_LRELU_BWD, BatchedPacker, ConvPlan, Workspace
 
@@ -49,19 +48,12 @@ class _DEngine:
                 plan.bind(m.weight, None, need_t=True)
                 self.layers.append((m, bn, plan))
         self.packer = BatchedPacker([p for _c, _b, p in self.layers], dev)
-        # fc.0's bf16 MFMA copy in fragment order (CLIMSR_FC0_FRAG=1, ops.linear_pack_frag): the forward and data
-        # gradient stream it as whole 4 KB / 16 KB runs (-11 / -3 us per launch), but the AdamW pass that writes it
-        # costs as much more: off by default, the row-major copy and one AdamW launch
-        o0, k0 = d.fc[0].weight.shape
-        self.fc0_frag = (os.environ.get("CLIMSR_FC0_FRAG", "0") == "1" and o0 % 256 == 0 and k0 % 256 == 0
-                         and d._fc_flat_lo() % 4 == 0 and _lib.has("climsr_linear_fwd_frag"))
-        self.fc0_bf16 = torch.empty((o0 * k0,) if self.fc0_frag else (o0, k0), dtype=torch.bfloat16, device=dev)
+        # fc.0's bf16 MFMA copy, row-major (written by the optimizer's AdamW pass, climsr_adamw_step_mirror)
+        self.fc0_bf16 = torch.empty(tuple(d.fc[0].weight.shape), dtype=torch.bfloat16, device=dev)
         self.version = -1
         self.ws = Workspace()
         self.scratch: Dict[str, Tensor] = {}
-        self.fuse_stem = True  # features.0 + features.2 as one launch (False: per layer; tools/perf_stem.py's A/B)
-        # the two D backwards of loss_d share one fc.0 weight-gradient launch (CLIMSR_FC0_WGRAD_MERGE=0: one each)
-        self.merge_wgrad = os.environ.get("CLIMSR_FC0_WGRAD_MERGE", "1") != "0" and _lib.has("climsr_linear_wgrad2")
+        # the two D backwards of loss_d share one fc.0 weight-gradient launch (backward's defer)
         self._wpend = None
 
     def ensure_packed(self):
@@ -73,11 +65,7 @@ class _DEngine:
         """mirror_done: the optimizer's AdamW pass already wrote fc0_bf16 (climsr_adamw_step_mirror)."""
         self.packer.run()
         if not mirror_done:
-            w0 = self.d.fc[0].weight
-            if self.fc0_frag:
-                ops.linear_pack_frag(w0, w0.shape[0], w0.shape[1], self.fc0_bf16)
-            else:
-                ops.f32_to_bf16(w0, self.fc0_bf16)
+            ops.f32_to_bf16(self.d.fc[0].weight, self.fc0_bf16)
         self.version = self.d._flat._version
 
     def _scr(self, key, shape, dtype, dev):
@@ -93,6 +81,10 @@ class _DEngine:
         n, cin, h, w = x.shape
         dev = x.device
         self.ensure_packed()
+        if keep:
+            # a held fc.0 weight gradient still pending here belongs to a backward that never finished (the pass's
+            # end-of-pass callback did not run): drop it, so it cannot merge into the next pass's gradient
+            self._wpend = None
         cpad = (cin + 7) // 8 * 8
         xc = x.contiguous().float()
         if cpad == 8:  # channels 0..cin-1 + zero padding in one full-pixel pass
@@ -109,7 +101,7 @@ class _DEngine:
         stem = None
         (c0, bn0, p0), (c1, bn1, p1) = self.layers[0], self.layers[1]
         if (cin == 1 and bn0 is None and bn1 is not None and p0.cout == 64 and p1.cin_real == 64 and p1.cout == 64 and p1.stride == 2
-                and p1.kpk == 576 and self.fuse_stem and _lib.has("climsr_d_stem_s2")):
+                and p1.kpk == 576):
             oh, ow = p1.out_hw(h, w)
             a0 = _bf16((n, h, w, 64), dev) if keep else None
             z = _bf16((n, oh, ow, 64), dev)
@@ -164,8 +156,7 @@ class _DEngine:
         hid = _f32((n, fc0.out_features), dev)
         nsplit_max = 3072 // ((fc0.out_features + 63) // 64) + 1
         lin_ws = self._scr("linws", (nsplit_max * n * fc0.out_features,), torch.float32, dev)
-        lin = ops.linear_fwd_frag if self.fc0_frag else ops.linear_fwd
-        lin(p, self.fc0_bf16, fc0.bias, n, feat, fc0.out_features, hid, lin_ws, act=ACT_LRELU, slope=0.2)
+        ops.linear_fwd(p, self.fc0_bf16, fc0.bias, n, feat, fc0.out_features, hid, lin_ws, act=ACT_LRELU, slope=0.2)
         s = _f32((n, 1), dev)
         ops.d_head_fwd(hid, fc2.weight, fc2.bias, n, fc0.out_features, s)
         sv = None
@@ -211,7 +202,7 @@ class _DEngine:
             if pend is not None:  # the pass's other D call: one weight-gradient launch for both batches
                 self._wpend = None
                 ops.linear_wgrad2(pend[0], pend[1], pend[2], du0_t, sv["p_t"], n_pad, feat, o, w0g, pend[4])
-            elif defer and hook is None and self.merge_wgrad:
+            elif defer and hook is None:
                 # loss_d backpropagates through D twice in one pass (real and fake, pl_gan.py:51-61): hold this call's
                 # fc.0 operands so the next call writes the 411 MB gradient once; a pass with no second call launches
                 # it from the end-of-pass callback, on this call's stream
@@ -222,7 +213,7 @@ class _DEngine:
             if hook is not None:  # fc.0 / fc.2: the last flat entries, 103 M of 107 M parameters
                 hook(d._fc_flat_lo())
         dp = self._scr("dp", (n, feat), torch.float32, dev)
-        (ops.linear_dgrad_frag if self.fc0_frag else ops.linear_dgrad)(du0, self.fc0_bf16, n, feat, o, dp)
+        ops.linear_dgrad(du0, self.fc0_bf16, n, feat, o, dp)
         hh, ww, c = sv["hh"], sv["ww"], sv["c"]
         da = _f32((n, hh, ww, c), dev)
         ops.adaptive_pool_bwd(dp, n, hh, ww, c, POOL, POOL, da)
@@ -373,10 +364,8 @@ class RFBESRGANDiscriminator(FlatParamsMixin, nn.Module):
         object.__setattr__(self, "_ready_need", max(1, int(calls_per_step)))
 
     def bf16_mirror(self):
-        """(flat offset, numel, bf16 buffer, (o, k) or None) of fc.0's weight: its MFMA copy, written by the fused AdamW
-        pass; (o, k) when the copy is in fragment order."""
-        eng = self.engine()
-        return self._fc_flat_lo(), self.fc[0].weight.numel(), eng.fc0_bf16, tuple(self.fc[0].weight.shape) if eng.fc0_frag else None
+        """(flat offset, numel, bf16 buffer) of fc.0's weight: its row-major MFMA copy, written by the fused AdamW pass."""
+        return self._fc_flat_lo(), self.fc[0].weight.numel(), self.engine().fc0_bf16
 
     def grad_ready_los(self):
         """The flat offsets the backward reports through the grad-ready hook, in its order (fc first, then the conv

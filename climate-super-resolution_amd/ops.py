@@ -164,8 +164,6 @@ class ConvPlan:
 
     def pool_ok(self, x_cs: int, in_h: int, in_w: int, n: int, y_cs: int, act: int = ACT_RELU) -> bool:
         """Whether fwd(..., act=act, pool2=True) has a fused conv + 2x2 max-pool kernel (climsr_conv2d_fwd_pool_ok)."""
-        if not _lib.has("climsr_conv2d_fwd_pool_ok"):  # (an older A/B build: _lib.load)
-            return False
         oh, ow = self.out_hw(in_h, in_w)
         d = ConvDesc(n, in_h, in_w, self.cin_k, x_cs, 0, 1, self.ks, self.stride, self.pad, oh, ow, self.cout, y_cs, 0, self.cc)
         ep = Epilogue(act, 0.2, 1.0, None, 0, 0, 1.0, None, 0, 0, OUT_BF16, 0, 0, 1.0, 1.0, 0, None, 0, 1.0, None, pool2=1)
@@ -676,30 +674,6 @@ def linear_dgrad(dy, w, n, k, o, dx, accumulate=False):
     _run("linear_dgrad_wide_kernel" if k % 128 == 0 else "linear_dgrad_kernel", 2 * n * k * o, lambda: check(
         _L().climsr_linear_dgrad(ptr(dy), ptr(w), n, k, o, ptr(dx), int(accumulate), _lib.stream_ptr()), "linear_dgrad"),
         "dgrad fc.0")
-
-
-def linear_pack_frag(w, o, k, wf):
-    """fp32 [o][k] -> bf16 fragment order (include/climsr_hip.h climsr_linear_pack_frag)."""
-    _launch("linear_pack_frag", lambda: _L().climsr_linear_pack_frag(ptr(w), o, k, ptr(wf), _lib.stream_ptr()))
-
-
-def linear_fwd_frag(x, wf, bias, n, k, o, y, ws, act=ACT_NONE, slope=0.2):
-    """linear_fwd with the weight in fragment order (linear_pack_frag / the fragment-order AdamW mirror)."""
-    _run("linear_fwd_wide_kernel", 2 * n * k * o, lambda: check(
-        _L().climsr_linear_fwd_frag(ptr(x), ptr(wf), ptr(bias), n, k, o, act, slope, ptr(ws), ws.numel(), ptr(y), _lib.stream_ptr()),
-        "linear_fwd_frag"), "fwd fc.0")
-
-
-def linear_dgrad_frag(dy, wf, n, k, o, dx, accumulate=False):
-    _run("linear_dgrad_wide_kernel", 2 * n * k * o, lambda: check(
-        _L().climsr_linear_dgrad_frag(ptr(dy), ptr(wf), n, k, o, ptr(dx), int(accumulate), _lib.stream_ptr()), "linear_dgrad_frag"),
-        "dgrad fc.0")
-
-
-def linear_frag_order(w):
-    """Host-side (torch) fragment order of a [o][k] tensor -- the layout climsr_linear_pack_frag writes (tests only)."""
-    o, k = w.shape
-    return w.reshape(o // 64, 4, 16, k // 32, 4, 8).permute(0, 3, 1, 4, 2, 5).reshape(-1)
 
 
 def linear_wgrad(dy_t, x_t, n_pad, k, o, dw, accumulate):

@@ -282,12 +282,6 @@ int climsr_adamw_step(int64_t n, float* p, const float* g, float* m, float* v, c
  * weight inside the flat buffer: the RFB discriminator's fc.0, rfb_esrgan.py:56-61). */
 int climsr_adamw_step_mirror(int64_t n, float* p, const float* g, float* m, float* v, const float* hp, int64_t mirror_lo,
                              int64_t mirror_n, uint16_t* mirror, void* stream);
-/* The same update with the mirrored weight [o][k] at p[mirror_lo, mirror_lo + o*k) copied in fragment order (see
- * climsr_linear_pack_frag) for climsr_linear_fwd_frag / climsr_linear_dgrad_frag; mirror_lo % 4 == 0, o % 64 == 0,
- * k % 256 == 0.  p / m / v end bit-identical to climsr_adamw_step's. */
-int climsr_adamw_step_mirror_frag(int64_t n, float* p, const float* g, float* m, float* v, const float* hp, int64_t mirror_lo,
-                                  int o, int k, uint16_t* mirror, void* stream);
-
 /* ---------------- discriminator / perceptual loss / GAN loss (disc.hip) ---------------- */
 
 /* nn.BatchNorm2d in train mode over z [npix][c] (bf16 NHWC; c % 8 == 0, c <= 2048, npix*c < 2^31), fused with
@@ -344,15 +338,6 @@ int climsr_linear_fwd(const uint16_t* x, const uint16_t* w, const float* bias, i
                       float* workspace, int64_t ws_floats, float* y, void* stream);
 /* dx[n][k] (+)= dy[n][o] . w[o][k] (bf16 in, fp32 out); k % 64 == 0, o % 32 == 0. */
 int climsr_linear_dgrad(const uint16_t* dy, const uint16_t* w, int n, int k, int o, float* dx, int accumulate, void* stream);
-/* Fragment order of a bf16 weight [o][k] (o % 64 == 0, k % 32 == 0): element (r, c) at
- * (((r/64)*(k/32) + c/32)*4 + (r%64)/16)*512 + ((r%16) + 16*((c%32)/8))*8 + c%8 -- contiguous 1 KB pieces that are
- * the 16x32 MFMA operand fragments in lane order.  climsr_linear_pack_frag writes it from the fp32 [o][k] weight. */
-int climsr_linear_pack_frag(const float* w, int o, int k, uint16_t* wf, void* stream);
-/* climsr_linear_fwd / climsr_linear_dgrad with w in fragment order (fwd: o % 256 == 0; dgrad: k % 128 == 0,
- * o % 64 == 0): the D fc.0 weight stream (205 MB) read as whole 4 KB / 16 KB runs.  Same results as the row-major forms. */
-int climsr_linear_fwd_frag(const uint16_t* x, const uint16_t* wf, const float* bias, int n, int k, int o, int act, float slope,
-                           float* workspace, int64_t ws_floats, float* y, void* stream);
-int climsr_linear_dgrad_frag(const uint16_t* dy, const uint16_t* wf, int n, int k, int o, float* dx, int accumulate, void* stream);
 /* dw[o][k] (+)= sum_n dy_t[o][n] x_t[k][n] (K = n_pad, multiple of 32; k % 64 == 0, o % 64 == 0). */
 int climsr_linear_wgrad(const uint16_t* dy_t, const uint16_t* x_t, int n_pad, int k, int o, float* dw, int accumulate,
                         void* stream);

@@ -1,5 +1,7 @@
 import os
+import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 import pytest
 
@@ -15,3 +17,31 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden_dir():
     return os.path.join(ROOT, "tests", "golden")
+
+
+# translation units whose compiled gfx950 ISA the build-time lints read (test_isa_hazards, test_isa_waitcnt)
+ISA_SOURCES = ("conv_dma.hip", "conv_wr.hip", "rdb_chain_narrow.hip", "conv_wgrad.hip", "rdb_chain.hip", "srcnn.hip")
+HIPCC = "/opt/rocm/bin/hipcc"
+
+
+def _compile_isa(src, tmp):
+    csrc = os.path.join(ROOT, "climate-super-resolution_amd", "csrc")
+    d = os.path.join(tmp, src)
+    os.makedirs(d, exist_ok=True)
+    subprocess.run([HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", f"-I{ROOT}/include", f"-I{csrc}", "--save-temps",
+                    "-c", os.path.join(csrc, src), "-o", os.path.join(d, "k.o")], cwd=d, check=True, capture_output=True)
+    asm = [f for f in os.listdir(d) if f.endswith("gfx950.s")]
+    assert asm, os.listdir(d)
+    with open(os.path.join(d, asm[0])) as f:
+        return f.read()
+
+
+@pytest.fixture(scope="session")
+def gfx950_isa(tmp_path_factory):
+    """src -> the gfx950 assembly hipcc emits for csrc/<src> (the product's flags); every lint source compiles once per
+    session, all in parallel."""
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not available")
+    tmp = str(tmp_path_factory.mktemp("isa"))
+    with ThreadPoolExecutor(len(ISA_SOURCES)) as ex:
+        return dict(zip(ISA_SOURCES, ex.map(lambda s: _compile_isa(s, tmp), ISA_SOURCES)))

@@ -122,6 +122,36 @@ def update_envelope(native, ref64, amps, floor=2e-2, pool_below=0):
     return bad, worst, rows
 
 
+SCALAR_CAP = 1e-3  # loss scalars rel <= 1e-3 (bf16)
+
+
+def scalar_envelope(what, got, want, amps, cap=SCALAR_CAP):
+    """A loss scalar vs the oracle's value on the same inputs: relative deviation <= 2x the reduced-precision spread of
+    the same scalar (the oracle's own torch-autocast fp16 / bf16 values' distances from ``want`` and from each other,
+    as update_envelope does for tensors), or ``cap`` (SURVEY's 1e-3) where that spread is smaller.  Prints the measured
+    deviations; returns (rel, bound)."""
+    den = abs(want) + 1e-30
+    rel = abs(got - want) / den
+    rel_amp = max(abs(a - want) / den for a in amps)
+    for i in range(len(amps)):
+        for j in range(i + 1, len(amps)):
+            rel_amp = max(rel_amp, abs(amps[i] - amps[j]) / den)
+    bound = max(2.0 * rel_amp, cap)
+    print(f"[loss-scalar] {what}: native {got:.7g} oracle {want:.7g} rel {rel:.3e} autocast {rel_amp:.3e} bound {bound:.3e}",
+          flush=True)
+    assert rel <= bound, (what, got, want, rel, rel_amp)
+    return rel, bound
+
+
+def scalar_cap(what, got, want, cap=SCALAR_CAP):
+    """A loss scalar vs a reference value with no autocast runs beside it: SURVEY 8c's rel <= 1e-3, measured value
+    printed."""
+    rel = abs(got - want) / (abs(want) + 1e-30)
+    print(f"[loss-scalar] {what}: native {got:.7g} reference {want:.7g} rel {rel:.3e} bound {cap:.1e}", flush=True)
+    assert rel <= cap, (what, got, want, rel)
+    return rel
+
+
 RCAN_TRAIN = {"rcan_g2b2_x4": (2, 2, 4, 2, 16), "rcan_g1b2_x2": (1, 2, 2, 2, 12), "rcan_g1b1_x3": (1, 1, 3, 1, 10)}
 
 

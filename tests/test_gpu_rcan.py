@@ -261,7 +261,7 @@ def test_rcan_training_grads_vs_oracle(golden_dir, name, monkeypatch):
     between any two precisions) does not decide the comparison -- srcnn.conv3's weight gradient is a sum of such signs
     over the pixels, each flip moving it by about 2 / sqrt(N) of its norm."""
     from oracle import climsr_ref as ref
-    from tests.helpers import RCAN_TRAIN, gemm_conv, rcan_params, rcan_train_batch, update_envelope
+    from tests.helpers import RCAN_TRAIN, SCALAR_CAP, gemm_conv, rcan_params, rcan_train_batch, update_envelope
 
     ng, nb, sf, b, lr_size = RCAN_TRAIN[name]
     want = json.load(open(os.path.join(golden_dir, "rcan_train.json")))[name]
@@ -312,7 +312,7 @@ def test_rcan_training_grads_vs_oracle(golden_dir, name, monkeypatch):
     print(f"  output rel L2 vs fp64 {rel_sr:.2e} (autocast {rel_amp:.2e}); loss rel deviation {rel_loss:.2e} (autocast "
           f"{max(abs(a - want['loss']) for a in amp_losses) / abs(want['loss']):.2e})", flush=True)
     assert rel_sr <= 2.0 * rel_amp, (rel_sr, rel_amp)
-    assert rel_loss <= 1e-3, (loss_n, want["loss"])
+    assert rel_loss <= SCALAR_CAP, (loss_n, want["loss"])
     # every parameter received a gradient that matches the reference module's checksum scale
     for k in keys:
         assert torch.isfinite(grads[k]).all(), k

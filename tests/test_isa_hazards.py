@@ -2,17 +2,11 @@
 around them, so the compiled gfx950 ISA is linted (tests/isa_mfma_lint.py) for any instruction that touches an asm
 MFMA's destination registers before the kernel's hazard pad, on every control-flow path.  Compiles for gfx950 on the
 CPU (no GPU needed)."""
-import os
 import re
-import subprocess
 
 import pytest
 
 from tests.isa_mfma_lint import lint
-
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CSRC = os.path.join(ROOT, "climate-super-resolution_amd", "csrc")
-HIPCC = "/opt/rocm/bin/hipcc"
 
 
 def _kernels(asm_text):
@@ -27,16 +21,8 @@ def _kernels(asm_text):
 
 
 @pytest.mark.parametrize("src", ["rdb_chain.hip", "conv_wr.hip", "srcnn.hip"])
-def test_asm_mfma_results_are_padded(src, tmp_path):
-    if not os.path.exists(HIPCC):
-        pytest.skip("hipcc not available")
-    if not os.path.exists(os.path.join(CSRC, src)):
-        pytest.skip(f"{src} not in this build")
-    subprocess.run([HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", f"-I{ROOT}/include", "--save-temps", "-c",
-                    os.path.join(CSRC, src), "-o", str(tmp_path / "k.o")], cwd=tmp_path, check=True, capture_output=True)
-    asm = [f for f in os.listdir(tmp_path) if f.endswith("gfx950.s")]
-    assert asm, os.listdir(tmp_path)
-    kern = _kernels(open(tmp_path / asm[0]).read())
+def test_asm_mfma_results_are_padded(src, gfx950_isa):
+    kern = _kernels(gfx950_isa[src])
     assert kern, "no kernels found in the ISA"
     bad = {name: lint(lines)[:5] for name, lines in kern.items()}
     bad = {k: v for k, v in bad.items() if v}

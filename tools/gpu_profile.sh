@@ -1,8 +1,8 @@
-# Round-5 profile of the build the driver benches, on one MI355X: the whole -m gpu suite, smoke, then for the GAN step
+# Round profile of the build the driver benches, on one MI355X: the whole -m gpu suite, smoke, then for the GAN step
 # and both config-5 inference models: FETCH_SIZE / WRITE_SIZE PMC passes (separate runs) -> profiles/<tag>_<mode>_pmc_
 # traffic.{json,md} (with the library sha256 bench.py matches), kernel-trace stats -> profiles/<tag>_<mode>_kernel_stats.csv
 # (+ .meta.json), and the bench lines.
-# usage: CLIMSR_GIT_HEAD=$(git rev-parse HEAD) bash tools/gpu_r05_profile.sh <tag: r05_vN> [part: gan | infer]
+# usage: CLIMSR_GIT_HEAD=$(git rev-parse HEAD) bash tools/gpu_profile.sh <tag: rNN_vM> [part: gan | infer]
 #   (gan: the suite, smoke, the GAN step's profiles and bench line; infer: config 5's; one gpurun call each)
 set -o pipefail
 T=${1:-r05_v1}
@@ -27,7 +27,7 @@ for mode in $MODES; do
   M=$mode; [ $mode != gan ] && M=infer_$mode
   timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${T}_${M}_f -o run --output-format csv -- $B > gpurun_out/${T}_${M}_pmcf.log 2>&1 || exit $?
   timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${T}_${M}_w -o run --output-format csv -- $B > gpurun_out/${T}_${M}_pmcw.log 2>&1 || exit $?
-  python3 tools/pmc_traffic.py gpurun_out/${T}_${M}_f gpurun_out/${T}_${M}_w gpurun_out/${T}_${M}_pmc_traffic "round 5 ${T}: $B" > /dev/null || exit $?
+  python3 tools/pmc_traffic.py gpurun_out/${T}_${M}_f gpurun_out/${T}_${M}_w gpurun_out/${T}_${M}_pmc_traffic "${T}: $B" > /dev/null || exit $?
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_${M}_s -o run --output-format csv -- $S > gpurun_out/${T}_${M}_stats.log 2>&1 || exit $?
   python3 tools/prof_record.py gpurun_out/${T}_${M}_s gpurun_out/${T}_${M}_kernel_stats.csv "$S" || exit $?
   rm -rf gpurun_out/${T}_${M}_f gpurun_out/${T}_${M}_w gpurun_out/${T}_${M}_s

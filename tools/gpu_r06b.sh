@@ -1,0 +1,13 @@
+# Round-6 call b: the whole -m gpu suite, smoke, the GAN bench, run-to-run determinism and the stride-2 / chain A/B
+# against ab/libclimsr_hip_old.so (the previous DMA kernel sources).
+set -o pipefail
+T=${1:-r06b}
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/${T}_pytest.log 2>&1 || exit $?
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${T}_smoke.log 2>&1 || exit $?
+timeout -k 10 400 python -u bench.py --no-cpu-baseline > gpurun_out/${T}_gan_bench.json 2> gpurun_out/${T}_gan_bench.err || exit $?
+timeout -k 10 200 python -u tools/det_check.py new > gpurun_out/${T}_det.json 2>&1 || exit $?
+timeout -k 10 200 python -u tools/perf_s2.py new > gpurun_out/${T}_s2.json 2>&1 || exit $?
+CLIMSR_HIP_LIB=$PWD/ab/libclimsr_hip_old.so timeout -k 10 200 python -u tools/perf_s2.py old >> gpurun_out/${T}_s2.json 2>&1 || exit $?
+echo done
