@@ -15,6 +15,7 @@ buffers are averaged over RCCL (DDP semantics, overlapped with the backward); ev
 replica.  Rank 0 prints ONE JSON line.
 """
 import argparse
+import functools
 import json
 import os
 import socket
@@ -142,13 +143,20 @@ def cpu_info():
             "threads": min(aff, quota) if quota else aff}
 
 
+@functools.lru_cache(maxsize=None)
+def _lib_sha256(path):
+    """sha256 of the HIP library (hashed once per process: 9 MB)."""
+    import hashlib
+
+    return hashlib.sha256(open(path, "rb").read()).hexdigest()
+
+
 def pmc_traffic(kernel, mode):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of this workload
     (profiles/r*_<mode>_pmc_traffic.json: separate FETCH_SIZE / WRITE_SIZE passes of this bench,
     FETCH_SIZE x2 gfx950 correction, MI355X_MICROARCH.md).  The summary carries the sha256 of the library it
     profiled; counters of any other build describe other code, so they are refused: (None, reason)."""
     import glob
-    import hashlib
     import re
 
     from climsr_amd import _lib
@@ -160,7 +168,7 @@ def pmc_traffic(kernel, mode):
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{mode}_pmc_traffic.json")), key=build_key)
     if not files:
         return None, "no PMC summary for this workload under profiles/"
-    running = hashlib.sha256(open(_lib.LIB_PATH, "rb").read()).hexdigest()
+    running = _lib_sha256(_lib.LIB_PATH)
     for f in reversed(files):
         try:
             doc = json.load(open(f))
@@ -413,6 +421,7 @@ def run_infer(args, world, rank, dev):
             "config": {"workload": f"config 5: whole-grid inference, LR {W}x{H} -> HR {ww}x{hh}, one grid per GPU per step",
                        "model": desc, "batch": 1, "parallelism": f"replicas{world}", "hip_graph": not args.no_graph,
                        "mode": "infer"},
+            "pmc_summary": (roof or {}).get("traffic_source") or (roof or {}).get("traffic_note"),
             "roofline": roof,
             "step_mfma": ({"algorithmic_tflop_per_step": round(flop_fwd / 1e12, 3),
                            "achieved_tflops": round(flop_fwd / (ms / 1e3) / 1e12, 1),
@@ -784,6 +793,8 @@ def main(argv=None):
                        "parallelism": f"dp{world}", "hip_graph": rec["use_graph"], "ddp_overlap": rec["overlap"],
                        "graph_segments": rec["graph_segments"], "mode": args.mode},
             "median": rec["median"],
+            # the PMC summary roofline.traffic comes from (matched on the library sha256), or why there is none
+            "pmc_summary": (rec.get("roofline") or {}).get("traffic_source") or (rec.get("roofline") or {}).get("traffic_note"),
             "roofline": rec.get("roofline"),
             "step_mfma": rec["step_mfma"],
             "cpu_baseline": cpu,

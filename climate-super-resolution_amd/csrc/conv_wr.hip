@@ -334,7 +334,8 @@ namespace climsr {
 
 // the conv_wr epilogue for (d, ep), or -1 when the conv is not this kernel's: 0 bias / activation, bf16 out; 1 + bf16
 // residual; 2 activation backward from the stored activation (no bias); 3 bias / activation, fp32 out (+ per-tile
-// channel sums); 4 bias / activation, bf16 out + per-tile channel sums (of the fp32 values).
+// channel sums); 4 bias / activation, bf16 out + per-tile channel sums (of the fp32 values).  The bf16 forms store 16 B
+// per lane (8 channels): their output offset and stride must be multiples of 8 channels.
 int conv_wr_ep(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const float* bias) {
   const bool res = ep->res1 != nullptr;
   int epk = -1;
@@ -345,7 +346,7 @@ int conv_wr_ep(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const float* b
   const long opx = (long)d->n * d->out_h * d->out_w;
   if (epk < 0 || (ep->ch_part && epk != 3 && epk != 4) || (ep->pool2 && (epk != 5 || ep->ch_part || (d->out_h | d->out_w) & 1)) || (ep->act == 1 && !(ep->slope >= 0.f && ep->slope <= 1.f)) || d->in_c != 64 || d->out_c != 64 || d->cc != 64 || d->ks != 3 || d->stride != 1 ||
       d->pad != 1 || (d->up != 1 && d->up != 2) || d->out_h != d->in_h * d->up || d->out_w != d->in_w * d->up ||
-      d->in_cstride % 8 || d->in_coff % 8 || (d->out_cstride | d->out_coff) & 3 || ep->down2 || ep->res2 || ep->aux ||
+      d->in_cstride % 8 || d->in_coff % 8 || (d->out_cstride | d->out_coff) & (epk == 3 ? 3 : 7) || ep->down2 || ep->res2 || ep->aux ||
       ep->bn_part || (res && ((ep->res1_cstride | ep->res1_coff) & 3)) ||
       (long)d->n * d->in_h * d->in_w * d->in_cstride * 2 >= (1L << 31) ||
       opx * d->out_cstride * (epk == 3 ? 4 : 2) >= (1L << 31) || (res && opx * ep->res1_cstride * 2 >= (1L << 31)) ||

@@ -72,6 +72,16 @@ def test_generator_forward_routes(routes):
     assert last(routes) == "conv_co1m_kernel<3, 2>"
 
 
+def test_conv_wr_bf16_output_needs_8_channel_alignment(routes):
+    """conv_wr's bf16 epilogues store 16 B (8 channels) per lane: an output at channel offset 4 (mod 8) must take
+    another kernel, an 8-aligned one conv_wr."""
+    pu = plan(NF, NF)
+    pu.fwd(bf(), NF, 0, 2 * H, 2 * H, bf(), NF + 8, 8, N, act=ACT_LRELU)
+    assert last(routes) == "conv_wr_kernel<0, 1>"
+    pu.fwd(bf(), NF, 0, 2 * H, 2 * H, bf(), NF + 8, 4, N, act=ACT_LRELU)
+    assert not last(routes).startswith("conv_wr_kernel"), last(routes)
+
+
 @pytest.mark.parametrize("cin,cout,hw,want", [
     (3, 64, 256, "conv_pw_kernel<8, 2, 4, false, 2, 3, 2>"),     # conv1_1: 4-channel taps
     (64, 64, 256, "conv_wr_kernel<0, 2>"),                         # conv1_2: weights in registers
