@@ -61,19 +61,15 @@ __global__ __launch_bounds__(512, 1) void stem_s2_kernel(StemArgs a) {
     const uint4 v = *(const uint4*)(a.w2 + (long)co * a.kpk2 + (c >> 1) * 288 + t * 32 + (c & 1) * 16 + hf * 8);
     *(uint4*)(smem + c * ST_WCH + ((co * 9 + t) * 2 + hf) * 16) = v;
   }
-  // features.0's A fragments: rows 16 c + col; lane groups 0 / 1: taps 0..7 / tap 8 of w_hi = bf16(w0), groups 2 / 3 the
-  // same taps of w_lo = bf16(w0 - w_hi).  The B fragments repeat the im2col taps in groups 2 / 3, so the one MFMA sums
-  // (w_hi + w_lo) x: the fp32 weight to 2^-16 (the 9-tap K left 23 of its 32 slots idle).  The backward reads the fp32 w0.
+  // features.0's A fragments: rows 16 c + col, lane group g: taps 8 g .. 8 g + 7 (tap 8 alone in group 1), bf16 RNE
   bf16x8 A0[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     bf16x8 v = {};
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const int t = 8 * (g & 1) + e;
-      const float wf = t < 9 ? a.w0[(16 * c + col) * 9 + t] : 0.f;
-      const __bf16 hi = (__bf16)wf;
-      v[e] = g < 2 ? hi : (__bf16)(wf - (float)hi);
+      const int t = 8 * g + e;
+      v[e] = t < 9 ? (__bf16)a.w0[(16 * c + col) * 9 + t] : (__bf16)0.f;
     }
     A0[c] = v;
   }
@@ -111,8 +107,8 @@ __global__ __launch_bounds__(512, 1) void stem_s2_kernel(StemArgs a) {
       }
     }
     lds_barrier();
-    // this wave's im2col fragments j = wave + 8 i of the region (pixel p = 16 j + col): lane groups 0 / 2 = taps 0..7,
-    // groups 1 / 3 = tap 8 and zeros (w_hi against groups 0 / 1, w_lo against 2 / 3)
+    // this wave's im2col fragments j = wave + 8 i of the region (pixel p = 16 j + col): lane group 0 = taps 0..7,
+    // group 1 = tap 8 and zeros, groups 2 / 3 zeros (K = 9 of 32)
     bf16x8 Bs[ST_FPW];
     {
       const char* ic = smem + ST_OFF_X + ST_XB;
@@ -121,7 +117,7 @@ __global__ __launch_bounds__(512, 1) void stem_s2_kernel(StemArgs a) {
         const int p0 = 16 * (wave + 8 * i) + col, pv = p0 < ST_TP * ST_TP, p = pv ? p0 : 0;
         const uint4 t07 = *(const uint4*)(ic + 16 * p);
         const uint16_t t8 = *(const uint16_t*)(ic + ST_T8 + 2 * p);
-        const uint4 v = !pv ? make_uint4(0, 0, 0, 0) : ((g & 1) == 0 ? t07 : make_uint4((uint32_t)t8, 0, 0, 0));
+        const uint4 v = !pv || g >= 2 ? make_uint4(0, 0, 0, 0) : (g == 0 ? t07 : make_uint4((uint32_t)t8, 0, 0, 0));
         Bs[i] = __builtin_bit_cast(bf16x8, v);
       }
     }
