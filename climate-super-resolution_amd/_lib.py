@@ -213,6 +213,7 @@ SIGNATURES = {
                                               c_void_p, c_void_p, c_void_p, c_void_p]),
     "climsr_channel_attention_parts_mean": (c_int, [c_void_p, c_int, c_int, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                                     c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "climsr_vgg_conv1_1": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "climsr_ca_backward_workspace": (c_size_t, [c_int, c_int64, c_int, c_int]),
     "climsr_ca_backward": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int64, c_int, c_void_p,
                                    c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,

@@ -286,6 +286,114 @@ __global__ __launch_bounds__(512, 1) void stem_s2_kernel(StemArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ---------------------------------------------------------------------------------------------------------------------
+// VGG19 conv1_1 of the perceptual loss on its 1 -> 3 channel repeat (perceptual.py:26-31: torch.cat([x, x, x], 1)):
+// conv(cat[x, x, x], W) = conv(x, W0 + W1 + W2), a 1-channel conv (+ bias, ReLU).  One launch reads the two fp32 image
+// batches directly (rounded to bf16 as the packed NHWC input was) and writes the 64-channel bf16 output at its write
+// floor; the 3-channel form ran the generic pointwise kernel on 8-channel pixels (51 TF/s) after two packing passes.
+// The summed weight W' = bf16(W0) + bf16(W1) + bf16(W2) -- the per-channel bf16 weights the 3-channel conv (and torch
+// autocast) multiply, summed exactly in fp32 -- is split w_hi = bf16(W'), w_lo = bf16(W' - w_hi) into the MFMA's idle
+// K slots (9 taps of 32), so the one MFMA per 16 pixels x 16 channels computes the 3-channel conv's products.  (The
+// fp32 W0 + W1 + W2 was more accurate at conv1_1 but moved the perceptual loss further from the fp64 oracle: +0.55 %
+// against +0.19 %, an L1 of bf16-noisy features on a 4-image test; tools/diag_c11.py.)
+// Workgroup: 16 x 64 output pixels; the 18 x 66 input region goes to LDS (bf16), then an im2col image (taps 0..7 as
+// 16 B, tap 8 as 2 B per pixel); wave w computes rows 4w .. 4w + 3, 4 fragments of 16 pixels each, 4 MFMAs per
+// fragment (16 channels each), and stores each pixel's 128 contiguous bytes as two 64-B chunk pairs of 16-B stores
+// (channel groups traded between lane rows g, g ^ 1 by v_permlane16_swap).
+constexpr int C11_TR = 16, C11_TC = 64, C11_IR = C11_TR + 2, C11_IC = C11_TC + 2;
+constexpr int C11_NP = C11_TR * C11_TC;                               // 1024 output pixels per tile
+constexpr int C11_OFF_IC = (C11_IR * C11_IC * 2 + 15) / 16 * 16;     // im2col image after the input region
+constexpr int C11_OFF_T8 = C11_OFF_IC + C11_NP * 16;
+constexpr int C11_LDS = C11_OFF_T8 + C11_NP * 2;                      // 20,832 B
+
+struct C11Args {
+  const float* xa;
+  const float* xb;
+  const float* wt;    // [64][3][3][3] fp32 (OIHW)
+  const float* bias;  // [64]
+  uint16_t* y;        // [2 n_half][h][w][64] bf16
+  int n_half, h, w, tiles_x, tiles_y;
+  uint32_t y_bytes;
+};
+
+__global__ __launch_bounds__(256) void vgg_conv1_1_kernel(C11Args a) {
+  __shared__ __attribute__((aligned(16))) char smem[C11_LDS];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
+  const int tile = blockIdx.x, tx = tile % a.tiles_x, ty = (tile / a.tiles_x) % a.tiles_y, img = tile / (a.tiles_x * a.tiles_y);
+  const int oy0 = C11_TR * ty, ox0 = C11_TC * tx;
+  const float* src = img < a.n_half ? a.xa + (long)img * a.h * a.w : a.xb + (long)(img - a.n_half) * a.h * a.w;
+  // the input region (zeros outside the image: conv1_1's padding), bf16 RNE
+  uint16_t* in = (uint16_t*)smem;
+  for (int u = tid; u < C11_IR * C11_IC; u += 256) {
+    const int r = u / C11_IC, c = u - r * C11_IC, iy = oy0 - 1 + r, ix = ox0 - 1 + c;
+    const float v = iy >= 0 && iy < a.h && ix >= 0 && ix < a.w ? src[(long)iy * a.w + ix] : 0.f;
+    in[u] = f2bf(v);
+  }
+  // A fragments (rows 16 c + col): lane groups 0 / 1 = taps 0..7 / tap 8 of w_hi, 2 / 3 the same of w_lo
+  bf16x8 A[4];
+  float bb[4][4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    bf16x8 v = {};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int t = 8 * (g & 1) + e, co = 16 * c + col;
+      const float wf = t < 9 ? ((float)(__bf16)a.wt[(co * 3 + 0) * 9 + t] + (float)(__bf16)a.wt[(co * 3 + 1) * 9 + t]) +
+                                   (float)(__bf16)a.wt[(co * 3 + 2) * 9 + t]
+                             : 0.f;
+      const __bf16 hi = (__bf16)wf;
+      v[e] = g < 2 ? hi : (__bf16)(wf - (float)hi);
+    }
+    A[c] = v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bb[c][e] = a.bias[16 * c + 4 * g + e];
+  }
+  __syncthreads();
+  // im2col: output pixel p = (r, c) of the tile -> taps 0..7 (16 B at 16 p), tap 8 (2 B)
+  for (int p = tid; p < C11_NP; p += 256) {
+    const int r = p / C11_TC, c = p - r * C11_TC;
+    const uint16_t* q = in + r * C11_IC + c;
+    uint4 v;
+    v.x = (uint32_t)q[0] | ((uint32_t)q[1] << 16);
+    v.y = (uint32_t)q[2] | ((uint32_t)q[C11_IC] << 16);
+    v.z = (uint32_t)q[C11_IC + 1] | ((uint32_t)q[C11_IC + 2] << 16);
+    v.w = (uint32_t)q[2 * C11_IC] | ((uint32_t)q[2 * C11_IC + 1] << 16);
+    *(uint4*)(smem + C11_OFF_IC + 16 * p) = v;
+    *(uint16_t*)(smem + C11_OFF_T8 + 2 * p) = q[2 * C11_IC + 2];
+  }
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t yr = buf_rsrc(a.y, a.y_bytes);
+  typedef uint32_t v4u32_t __attribute__((ext_vector_type(4)));
+#pragma unroll 2
+  for (int fr = 0; fr < 16; ++fr) {  // this wave's fragments: row 4 wave + fr / 4, columns 16 (fr % 4) ..
+    const int r = 4 * wave + (fr >> 2), c = 16 * (fr & 3) + col, p = r * C11_TC + c;
+    const uint4 t07 = *(const uint4*)(smem + C11_OFF_IC + 16 * p);
+    const uint16_t t8 = *(const uint16_t*)(smem + C11_OFF_T8 + 2 * p);
+    const bf16x8 B = __builtin_bit_cast(bf16x8, (g & 1) == 0 ? t07 : make_uint4((uint32_t)t8, 0, 0, 0));
+    f32x4 z[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) z[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[k], B, (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    const int oy = oy0 + r, ox = ox0 + c;
+    const bool ok = oy < a.h && ox < a.w;
+    const uint32_t pix = (uint32_t)(((long)img * a.h + oy) * a.w + ox);
+    uint32_t pk[4][2];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float v0 = fmaxf(z[k][0] + bb[k][0], 0.f), v1 = fmaxf(z[k][1] + bb[k][1], 0.f);
+      const float v2 = fmaxf(z[k][2] + bb[k][2], 0.f), v3 = fmaxf(z[k][3] + bb[k][3], 0.f);
+      const bf16x2 q0 = {(__bf16)v0, (__bf16)v1}, q1 = {(__bf16)v2, (__bf16)v3};
+      pk[k][0] = __builtin_bit_cast(uint32_t, q0);
+      pk[k][1] = __builtin_bit_cast(uint32_t, q1);
+      if (k & 1) {  // lane (col, g): channels 16 (k - 1 + (g & 1)) + 8 (g >> 1) .. + 7 of its pixel
+        const auto sx = __builtin_amdgcn_permlane16_swap(pk[k - 1][0], pk[k][0], false, false);
+        const auto sy = __builtin_amdgcn_permlane16_swap(pk[k - 1][1], pk[k][1], false, false);
+        const v4u32_t o = {sx[0], sy[0], sx[1], sy[1]};
+        __builtin_amdgcn_raw_buffer_store_b128(o, yr, ok ? (pix * 64u + (uint32_t)(16 * (k - 1 + (g & 1)) + 8 * (g >> 1))) * 2u : BUF_OOB, 0, 0);
+      }
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int climsr_d_stem_s2(const ClimsrStemDesc* d, void* stream) {
@@ -317,4 +425,24 @@ extern "C" int climsr_d_stem_s2(const ClimsrStemDesc* d, void* stream) {
 
 extern "C" int64_t climsr_d_stem_s2_bn_parts(int32_t n, int32_t h, int32_t w) {
   return (int64_t)n * ((((h + 1) / 2) + 15) / 16) * ((((w + 1) / 2) + 15) / 16);
+}
+
+extern "C" int climsr_vgg_conv1_1(const float* xa, const float* xb, int n_half, int h, int w, const float* weight, const float* bias,
+                                  uint16_t* y, void* stream) {
+  if (!xa || !xb || !weight || !bias || !y || n_half <= 0 || h <= 0 || w <= 0) {
+    set_error("vgg_conv1_1: bad args");
+    return CLIMSR_EINVAL;
+  }
+  const long ybytes = 2L * n_half * h * w * 64 * 2;
+  if (ybytes >= (1L << 31)) {
+    set_error("vgg_conv1_1: output over 2 GiB (32-bit buffer offsets)");
+    return CLIMSR_EINVAL;
+  }
+  C11Args a{};
+  a.xa = xa; a.xb = xb; a.wt = weight; a.bias = bias; a.y = y;
+  a.n_half = n_half; a.h = h; a.w = w;
+  a.tiles_x = ceil_div(w, C11_TC); a.tiles_y = ceil_div(h, C11_TR);
+  a.y_bytes = (uint32_t)ybytes;
+  hipLaunchKernelGGL(vgg_conv1_1_kernel, dim3(a.tiles_x * a.tiles_y * 2 * n_half), dim3(256), 0, (hipStream_t)stream, a);
+  return check_launch("vgg_conv1_1");
 }

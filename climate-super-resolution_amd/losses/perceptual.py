@@ -4,6 +4,8 @@ VGG19 ``features[:35]`` (conv1_1 .. conv5_4, the last without ReLU) applied to t
 repeat of both images, L1 between the feature maps, all without gradient (F7: the loss adds to
 the value only).  Both images run as ONE batch through native implicit-GEMM convs with fused
 bias+ReLU epilogues and MaxPool2d(2,2) kernels; the L1 is a deterministic bf16 reduction.
+conv1_1 on the repeat is one 1-channel conv with the summed weight (``climsr_vgg_conv1_1``), read
+straight from the two fp32 image batches.
 
 Weights: ``vgg19(pretrained=True)`` (perceptual.py:15) downloads ImageNet weights, impossible
 offline; the module is built with the reference's parameter names (``loss_network.{i}.weight``)
@@ -66,12 +68,16 @@ class PerceptualLoss(nn.Module):
                 plans.append((p, relu, pool))
         self._plans = plans
         self._dev = dev
+        c11 = mods[0]
+        self._c11_w = c11.weight.detach().contiguous().float()
+        self._c11_b = c11.bias.detach().contiguous().float()
         self._version = sum(int(p.weight._version) for p, _r, _q in plans)
 
-    def features(self, x3: torch.Tensor, n: int, h: int, w: int) -> torch.Tensor:
-        """x3: NHWC bf16 [n,h,w,8] with channels 0..2 = the image.  Returns conv5_4 features (bf16)."""
-        a, cs = x3, 8
-        for p, relu, pool in self._plans:
+    def features(self, x3: torch.Tensor, n: int, h: int, w: int, start: int = 0, cs: int = 8) -> torch.Tensor:
+        """x3: NHWC bf16 [n,h,w,cs]: the image in channels 0..2 (start 0), or the output of conv plan start - 1.
+        Returns conv5_4 features (bf16)."""
+        a = x3
+        for p, relu, pool in self._plans[start:]:
             act = ACT_RELU if relu else ACT_NONE
             if pool and p.pool_ok(cs, h, w, n, p.cout, act):  # conv + ReLU + 2x2 max pool in one kernel
                 h, w = h // 2, w // 2
@@ -98,12 +104,13 @@ class PerceptualLoss(nn.Module):
             self.loss_network.to(a.device)
             self._build(a.device)
         n, _c, h, w = a.shape
-        x3 = torch.empty((2 * n, h, w, 8), dtype=torch.bfloat16, device=a.device)
         a32, b32 = a.contiguous().float(), b.contiguous().float()
-        # torch.cat([x, x, x], dim=1) (perceptual.py:26-31) as channels 0..2 of the padded NHWC input, one pass each
-        ops.pack_planes8([(a32, 0)] * 3, n, h, w, x3[:n])
-        ops.pack_planes8([(b32, 0)] * 3, n, h, w, x3[n:])
-        f = self.features(x3, 2 * n, h, w)
+        # conv1_1 + ReLU on torch.cat([x, x, x], dim=1) (perceptual.py:26-31) = one 1-channel conv with the summed
+        # weight, straight from the fp32 images (both batches in one launch)
+        c11 = self.loss_network[0]
+        y1 = torch.empty((2 * n, h, w, 64), dtype=torch.bfloat16, device=a.device)
+        ops.vgg_conv1_1(a32, b32, n, h, w, self._c11_w, self._c11_b, y1)
+        f = self.features(y1, 2 * n, h, w, start=1, cs=c11.out_channels)
         half = f.numel() // 2
         ws = torch.empty(512, dtype=torch.float64, device=a.device)
         out = torch.empty((), dtype=torch.float32, device=a.device)

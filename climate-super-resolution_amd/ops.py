@@ -722,6 +722,18 @@ def d_stem_s2(x, x_cs, w0, plan2, a0, z2, bn_part, n, h, w, slope=0.2):
          n * h * w * 2 + n * oh * ow * 128 + (n * h * w * 128 if a0 is not None else 0))
 
 
+def vgg_conv1_1(xa, xb, n_half, h, w, weight, bias, y):
+    """VGG19 conv1_1 + ReLU on the 1 -> 3 channel repeat of two fp32 image batches (perceptual.py:16,26-31) as one
+    1-channel conv (csrc/stem.hip): y bf16 NHWC [2 n_half, h, w, 64], images of xa first."""
+    assert xa.dtype == torch.float32 and xb.dtype == torch.float32 and xa.is_contiguous() and xb.is_contiguous()
+    assert xa.numel() == n_half * h * w and xb.numel() == n_half * h * w
+    assert tuple(weight.shape) == (64, 3, 3, 3) and weight.dtype == torch.float32 and weight.is_contiguous()
+    assert bias.numel() == 64 and bias.dtype == torch.float32 and y.dtype == torch.bfloat16 and y.numel() == 2 * n_half * h * w * 64
+    _run("vgg_conv1_1_kernel", 2 * 2 * n_half * h * w * 64 * 27,
+         lambda: check(_L().climsr_vgg_conv1_1(ptr(xa), ptr(xb), n_half, h, w, ptr(weight), ptr(bias), ptr(y), _lib.stream_ptr()),
+                       "vgg_conv1_1"), "vgg conv1_1", 2 * n_half * h * w * (4 + 128))
+
+
 def d_stem_s2_bn_parts(n, h, w):
     return int(_L().climsr_d_stem_s2_bn_parts(n, h, w))
 

@@ -366,6 +366,11 @@ typedef struct ClimsrStemDesc {
 } ClimsrStemDesc;
 int climsr_d_stem_s2(const ClimsrStemDesc* d, void* stream);
 int64_t climsr_d_stem_s2_bn_parts(int32_t n, int32_t h, int32_t w);
+/* VGG19 conv1_1 (+ bias + ReLU) of the perceptual loss on torch.cat([x, x, x], 1) (perceptual.py:16,26-31) as ONE
+ * 1-channel conv with the summed weight W0 + W1 + W2: images 0..n_half-1 from xa, n_half..2 n_half-1 from xb (fp32
+ * [n_half][h][w] planes, rounded to bf16), weight fp32 [64][3][3][3], bias [64]; y bf16 NHWC [2 n_half][h][w][64]. */
+int climsr_vgg_conv1_1(const float* xa, const float* xb, int n_half, int h, int w, const float* weight, const float* bias,
+                       uint16_t* y, void* stream);
 
 /* Discriminator head after fc.0 (+LeakyReLU) (h [n][o] fp32): s[n] = sigmoid(h.w2 + b2) (rfb_esrgan.py:59-60),
  * or h.w2 + b2 with sigmoid = 0 (plain discriminator's classification.1, discriminator.py:40). */

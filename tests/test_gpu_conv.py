@@ -927,3 +927,34 @@ def test_conv_relu_maxpool_fused(cin, cout, n, h, w):
     got = from_nhwc(y, cout).double().cpu()
     err = float((got - want).abs().max())
     assert err <= 2 ** -7 * float(want.abs().max()) + 1e-6, f"err {err:.3e} vs {float(want.abs().max()):.3e}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h,w", [(2, 64, 64), (1, 37, 70), (3, 16, 130)])
+def test_vgg_conv1_1_one_channel_matches_fp64(n, h, w):
+    """VGG19 conv1_1 + ReLU on torch.cat([x, x, x], 1) (perceptual.py:16,26-31) as one 1-channel conv with the summed
+    of the per-channel bf16 weights (csrc/stem.hip climsr_vgg_conv1_1), two fp32 batches in one launch, vs float64 on the
+    bf16-rounded images and weights (the 3-channel conv's operands): within one bf16 rounding of the output plus 2^-16 of
+    sum |w x| (the w_hi + w_lo split of the summed weight); ragged tiles; bit-identical reruns."""
+    from climsr_amd import ops
+
+    g = torch.Generator().manual_seed(51)
+    xa = torch.rand((n, 1, h, w), generator=g) * 2 - 1
+    xb = torch.rand((n, 1, h, w), generator=g) * 2 - 1
+    wt = ((torch.rand((64, 3, 3, 3), generator=g) * 2 - 1) / 4).contiguous()
+    b = (torch.rand(64, generator=g) - 0.5) / 4
+    y = torch.full((2 * n, h, w, 64), 9.0, dtype=torch.bfloat16, device=DEV)
+    args = (xa.to(DEV).contiguous(), xb.to(DEV).contiguous(), n, h, w, wt.to(DEV), b.to(DEV), y)
+    ops.vgg_conv1_1(*args)
+    torch.cuda.synchronize()
+    first = y.clone()
+    ops.vgg_conv1_1(*args)
+    torch.cuda.synchronize()
+    assert torch.equal(first, y), "rerun not bit-identical"
+    x = bf(torch.cat([xa, xb], 0)).double()
+    x3 = torch.cat([x, x, x], 1)
+    want = F.relu(F.conv2d(x3, bf(wt).double(), b.double(), padding=1))
+    mag = F.conv2d(x3.abs(), bf(wt).double().abs(), padding=1)
+    got = from_nhwc(y, 64).cpu().double()
+    err = ((got - want).abs() - want.abs() * 2.0 ** -8 - mag * 2.0 ** -16).max().item()
+    assert err <= 1e-6 * want.abs().max().item(), f"conv1_1 err {err:.3e}"
