@@ -532,10 +532,17 @@ __device__ __forceinline__ void wgrad64_body(const WgArgs& a) {
     int tq = qt0;  // this quad's tile
     issue(tq < a.ntiles, 0);
     int cur = 0;
+    // only wave 0 of each quad of a bias-owning workgroup needs the bias sums (quad 1's are added to quad 0's below): the
+    // other waves skip those 4 MFMAs per k-step (-1 to -3 us per launch)
+    const bool bias_wave = do_bias && __builtin_amdgcn_readfirstlane(wave) == 0;
     if constexpr (NB == 3) {
       lag2 = true;
       issue(tq + qstep < a.ntiles, 1);
     }
+    // the tile loop, instantiated twice: with the bias sums (wave 0 of a bias-owning workgroup) and without (a
+    // wave-uniform branch around the bias MFMAs inside it spilled registers to scratch)
+    auto tiles = [&](auto with_bias) {
+    constexpr bool WB = decltype(with_bias)::value;
     for (int it = 0; it < nit; ++it, tq += qstep) {
       // NB 3: this tile's NZI + NXI DMAs (per wave) have landed once at most the next tile's are outstanding; NB 2:
       // once none is.  The barrier makes that true for every wave, and every wave is past its reads of the buffer the
@@ -560,7 +567,7 @@ __device__ __forceinline__ void wgrad64_body(const WgArgs& a) {
         if (gn < NK * 9) bq[gn % (LA + 1)] = ld_bf(xb, gn / 9, gn % 9);
         if (u == 4 && kk + 1 < NK) ld_af(zb, kk + 1, af[(kk + 1) & 1]);
         __builtin_amdgcn_sched_barrier(0);
-        if (u == 0) {
+        if (WB && u == 0) {
 #pragma unroll
           for (int t = 0; t < 4; ++t) accb[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk & 1][t], ones, accb[t], 0, 0, 0);
         }
@@ -570,6 +577,9 @@ __device__ __forceinline__ void wgrad64_body(const WgArgs& a) {
       }
       cur = cur == NB - 1 ? 0 : cur + 1;
     }
+    };
+    if (bias_wave) tiles(std::true_type{});
+    else tiles(std::false_type{});
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMAs past the last tile (zeros) land before the
                                                         // epilogue staging reuses the buffers
   } else {
