@@ -40,6 +40,10 @@ constexpr int WR_LDS = 4 * 2 * WR_BUF;                  // 4 waves x 2 buffers: 
 constexpr int WR_RED = 64 * 17 * 4;                     // per wave: the channel-sum transpose [64 ch][17] (EP 3 / 4)
 constexpr int WR_LDS_ALL = WR_LDS + 4 * WR_RED;         // 156,672 B
 static_assert(WR_LDS_ALL <= 160 * 1024, "conv_wr LDS");
+// the one-image channel sums' arrival counter: wave 3's transpose corner, row 16's pad column (never written by the
+// transposes, clear of the weight pieces staged at the start of the channel-sum region)
+__device__ inline uint32_t* wr_wg_count(char* smem) { return (uint32_t*)(smem + WR_LDS + 3 * WR_RED) + 16 * 17 + 16; }
+static_assert(3 * WR_RED >= 4 * 1024, "conv_wr arrival counter clear of the staged weights");
 
 struct WrArgs {
   const uint16_t* x;
@@ -53,6 +57,7 @@ struct WrArgs {
   float slope, alpha1, beta1;
   int r1_cs, r1_co;
   int tiles_x, tiles_y, ntiles;
+  int wg_sums;  // EP 3 / 4 with one image: ch_part gets one row per workgroup (its tiles' sums) instead of one per tile
   uint32_t x_bytes, y_bytes, r1_bytes;
 };
 typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
@@ -153,6 +158,7 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
   const __amdgpu_buffer_rsrc_t pr = buf_rsrc(a.ch_part, SUMS && a.ch_part ? (uint32_t)a.ntiles * 256u : 0u);
   const __amdgpu_buffer_rsrc_t rr = buf_rsrc(a.res1, (EP == 1 || EP == 2) ? a.r1_bytes : 0u);
   const int lb = col * WR_XP * 2 + g * 16;  // this lane's byte offset in a footprint row: pixel col, channels 8 g ..
+  if (SUMS && a.wg_sums && tid == 0) *wr_wg_count(smem) = 0u;  // (before the barriers every wave passes)
   if (T < a.ntiles) issue(T, 0);
   // the weights: this wave's 18 pieces have landed once only the footprint just requested is younger; after the
   // barrier every wave's have, and every wave copies all 72 fragments to its registers; the second barrier retires
@@ -167,6 +173,8 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
     for (int j = 0; j < 18; ++j) afb[t][j] = *(const bf16x8*)(smem + wr_piece(18 * t + j) + lane * 16);
   lds_barrier();
   if (T >= a.ntiles) return;
+  const int T0 = T;
+  float wsum = 0.f;  // (wg_sums) this lane's channel over the wave's tiles, in tile order
   for (int it = 0;; ++it) {
     const int Tn = T + G4;
     issue(Tn < a.ntiles ? Tn : -1, (it + 1) & 1);
@@ -320,12 +328,29 @@ __global__ __launch_bounds__(256, 1) void conv_wr_kernel(WrArgs a) {
       float cs = 0.f;
 #pragma unroll
       for (int c = 0; c < 16; ++c) cs += red[lane * 17 + c];
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(cs), pr, (uint32_t)((T * 64 + lane) * 4), 0, 0);
+      wsum += cs;
+      // (wg_sums: the store still issues, out of range, so every tile's vector-memory count stays the same)
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(cs), pr, a.wg_sums ? BUF_OOB : (uint32_t)((T * 64 + lane) * 4), 0, 0);
     }
     if (Tn >= a.ntiles) break;
     T = Tn;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the zero-filling DMA past the last tile lands before the wave ends
+  if constexpr (SUMS) {
+    if (a.wg_sums) {  // (uniform) row blockIdx.x = the sums of the workgroup's waves with tiles, added in wave order by
+                      // the last of them to arrive (the LDS counter; no barrier, so the waves without a tile may leave)
+      const float* red0 = (const float*)(smem + WR_LDS);
+      ((float*)red0)[wv * (WR_RED / 4) + lane] = wsum;  // (this wave's own corner: its transpose reads are behind it)
+      const int nact = min(4, a.ntiles - (T0 - wv));
+      uint32_t prev = 0;
+      if (lane == 0) prev = __hip_atomic_fetch_add(wr_wg_count(smem), 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if ((int)__builtin_amdgcn_readfirstlane(prev) == nact - 1) {
+        float t = 0.f;
+        for (int w = 0; w < nact; ++w) t += red0[w * (WR_RED / 4) + lane];
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(t), pr, (uint32_t)((blockIdx.x * 64 + lane) * 4), 0, 0);
+      }
+    }
+  }
 }
 
 }  // namespace
@@ -355,13 +380,19 @@ int conv_wr_ep(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const float* b
   return epk;
 }
 
-// tiles (rows of ch_part) of the conv, and per image; 0 when conv_wr does not take (d, ep)
+// rows of ch_part (tiles, or with one image the workgroups of the launch) of the conv, and per image; 0 when conv_wr
+// does not take (d, ep)
 long conv_wr_ch_parts(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, int* tiles_per_image) {
   ClimsrEpilogue e = *ep;
   e.ch_part = (float*)1;  // (only its presence matters here)
   const int k = conv_wr_ep(d, &e, nullptr);
   if (k != 3 && k != 4) return 0;
   const int tpi = ceil_div(d->out_w, WR_TC) * ceil_div(d->out_h, WR_TR);
+  if (d->n == 1) {  // one row per workgroup (conv_wr_launch's grid)
+    const int rows = std::min(ceil_div(tpi, 4), device_cus());
+    if (tiles_per_image) *tiles_per_image = rows;
+    return rows;
+  }
   if (tiles_per_image) *tiles_per_image = tpi;
   return (long)tpi * d->n;
 }
@@ -384,6 +415,7 @@ int conv_wr_launch(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, const uint
   a.r1_cs = ep->res1_cstride; a.r1_co = ep->res1_coff;
   a.tiles_x = ceil_div(d->out_w, WR_TC); a.tiles_y = ceil_div(d->out_h, WR_TR);
   a.ntiles = a.tiles_x * a.tiles_y * d->n;
+  a.wg_sums = (epk == 3 || epk == 4) && ep->ch_part && d->n == 1;
   a.x_bytes = (uint32_t)((long)d->n * d->in_h * d->in_w * d->in_cstride * 2);
   a.y_bytes = (uint32_t)((epk == 5 ? opx / 4 : opx) * d->out_cstride * (epk == 3 ? 4 : 2));
   a.r1_bytes = res ? (uint32_t)(opx * ep->res1_cstride * 2) : 0u;

@@ -11,6 +11,7 @@ using namespace climsr;
 
 namespace {
 constexpr int POOL_SPLIT = 256;  // pixel slices per image of the pooling pass (>= 1 block per CU for one grid)
+constexpr int TILE_DIRECT = 1024;  // at most this many fp32 rows per image (64 channels): ca_mlp_kernel reads them itself
 constexpr int TILE_SPLIT = 256;  // slices per image of the per-tile sums (channel_attention_parts; 64 measured neutral)
 }
 
@@ -48,7 +49,11 @@ __global__ __launch_bounds__(256) void channel_sum_partial_kernel(const float* _
 // are staged in LDS by every thread at once when they fit; a hidden unit is one wave's strided dot product finished
 // by a fixed xor-shuffle tree (the serial per-thread loops over global W1 / W2 took most of this kernel's 8.9 us).
 constexpr int CA_STAGE_MAX = 8192;  // floats of W1 + W2 staged in LDS
-__global__ __launch_bounds__(1024) void ca_mlp_kernel(const double* __restrict__ part, int nsl, long hw, int c, int cr, const float* __restrict__ w1,
+// P: the slice sums' type -- fp64 slices of the fold kernels, or fp32 rows straight from the conv epilogue (c == 64: a
+// thread's float4 loads are all in flight at once, 16 channel quads x 64 row lanes; a wave's 4 row lanes are combined by
+// a fixed xor-shuffle tree, the 16 waves in order)
+template <typename P>
+__global__ __launch_bounds__(1024) void ca_mlp_kernel(const P* __restrict__ part, int nsl, long hw, int c, int cr, const float* __restrict__ w1,
                               const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2,
                               float* __restrict__ s, float* __restrict__ mean_out) {
   extern __shared__ float sm[];
@@ -68,19 +73,60 @@ __global__ __launch_bounds__(1024) void ca_mlp_kernel(const double* __restrict__
   const float* W2 = staged ? wst + cr * c : w2;
   const int cw = c < NT ? c : NT;  // channels per round
   const int G = NT / cw;           // split groups summed in parallel, then combined in a fixed order
+  if constexpr (sizeof(P) == 4) {
+    const int q = t & 15, rl = t >> 4;  // channel quad, row lane (0..63)
+    const float4* pp = (const float4*)(part + (long)nimg * nsl * 64) + q;
+    double a[8][4] = {};
+    int r = rl;
+    for (; r + 7 * 64 < nsl; r += 8 * 64) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = pp[(long)(r + u * 64) * 16];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        a[u][0] += v[u].x; a[u][1] += v[u].y; a[u][2] += v[u].z; a[u][3] += v[u].w;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 7; ++u)
+      if (r + u * 64 < nsl) {
+        const float4 v = pp[(long)(r + u * 64) * 16];
+        a[u][0] += v.x; a[u][1] += v.y; a[u][2] += v.z; a[u][3] += v.w;
+      }
+    double m4[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      double v = ((a[0][k] + a[1][k]) + (a[2][k] + a[3][k])) + ((a[4][k] + a[5][k]) + (a[6][k] + a[7][k]));
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      m4[k] = v;
+    }
+    const int wave = t >> 6, lane = t & 63;
+    if (lane < 16)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) grp[wave * 64 + q * 4 + k] = m4[k];
+    __syncthreads();
+    if (t < 64) {
+      double m = 0.0;
+      for (int w = 0; w < NT / 64; ++w) m += grp[w * 64 + t];
+      mean[t] = (float)(m / (double)hw);
+      if (mean_out) mean_out[(long)nimg * 64 + t] = mean[t];
+    }
+    __syncthreads();
+  } else
   for (int c0 = 0; c0 < c; c0 += cw) {
     const int i = c0 + t % cw, gi = t / cw;
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
     if (i < c && gi < G) {
-      const double* pp = part + (long)nimg * nsl * c + i;
+      const P* pp = part + (long)nimg * nsl * c + i;
       int sp = gi;
       for (; sp + 3 * G < nsl; sp += 4 * G) {
-        a0 += pp[(long)sp * c];
-        a1 += pp[(long)(sp + G) * c];
-        a2 += pp[(long)(sp + 2 * G) * c];
-        a3 += pp[(long)(sp + 3 * G) * c];
+        a0 += (double)pp[(long)sp * c];
+        a1 += (double)pp[(long)(sp + G) * c];
+        a2 += (double)pp[(long)(sp + 2 * G) * c];
+        a3 += (double)pp[(long)(sp + 3 * G) * c];
       }
-      for (; sp < nsl; sp += G) a0 += pp[(long)sp * c];
+      for (; sp < nsl; sp += G) a0 += (double)pp[(long)sp * c];
     }
     grp[t] = (a0 + a1) + (a2 + a3);
     __syncthreads();
@@ -121,7 +167,7 @@ extern "C" int climsr_channel_attention_mean(const float* u, int n, int64_t hw, 
   }
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(channel_sum_partial_kernel, dim3(POOL_SPLIT, n), dim3(256), 0, st, u, (long)hw, c, u_cstride, workspace);
-  hipLaunchKernelGGL(ca_mlp_kernel, dim3(n), dim3(1024), (size_t)(c + cr) * sizeof(float), st, workspace, POOL_SPLIT, (long)hw, c, cr, w1, b1,
+  hipLaunchKernelGGL(ca_mlp_kernel<double>, dim3(n), dim3(1024), (size_t)(c + cr) * sizeof(float), st, workspace, POOL_SPLIT, (long)hw, c, cr, w1, b1,
                      w2, b2, s, mean_out);
   return check_launch("channel_attention");
 }
@@ -161,8 +207,13 @@ extern "C" int climsr_channel_attention_parts_mean(const float* part, int n, int
     return CLIMSR_EINVAL;
   }
   hipStream_t st = (hipStream_t)stream;
+  if (tiles_per_image <= TILE_DIRECT && c == 64) {  // few rows (one per conv workgroup, or small images): the MLP folds them
+    hipLaunchKernelGGL(ca_mlp_kernel<float>, dim3(n), dim3(1024), (size_t)(c + cr) * sizeof(float), st, part, tiles_per_image, (long)hw, c,
+                       cr, w1, b1, w2, b2, s, mean_out);
+    return check_launch("channel_attention_parts");
+  }
   hipLaunchKernelGGL(tile_parts_fold_kernel, dim3(TILE_SPLIT, n), dim3(256), 0, st, part, tiles_per_image, c, workspace);
-  hipLaunchKernelGGL(ca_mlp_kernel, dim3(n), dim3(1024), (size_t)(c + cr) * sizeof(float), st, workspace, TILE_SPLIT, (long)hw, c, cr, w1, b1,
+  hipLaunchKernelGGL(ca_mlp_kernel<double>, dim3(n), dim3(1024), (size_t)(c + cr) * sizeof(float), st, workspace, TILE_SPLIT, (long)hw, c, cr, w1, b1,
                      w2, b2, s, mean_out);
   return check_launch("channel_attention_parts");
 }

@@ -672,11 +672,13 @@ def test_conv_wr_matches_fp64(n, h, w, up, mode):
     assert err <= 2 ** -7 * float(want.abs().max()) + 1e-6, f"{mode}: err {err:.3e} vs {float(want.abs().max()):.3e}"
 
 
-@pytest.mark.parametrize("n,h,w,f32", [(2, 13, 37, True), (1, 45, 90, True), (2, 13, 37, False), (1, 30, 70, False)])
+@pytest.mark.parametrize("n,h,w,f32", [(2, 13, 37, True), (1, 45, 90, True), (2, 13, 37, False), (1, 30, 70, False),
+                                       (1, 9, 37, True), (1, 180, 360, False)])
 def test_conv_wr_fp32_out_channel_sums(n, h, w, f32):
-    """conv_wr's fp32-output epilogue (RCAN's RCAB conv2, rcan.py:50-69) and the per-tile channel sums it emits for the
-    channel attention's global pool (climsr_conv2d_fwd_ch_parts rows, tiles of an image contiguous): the output vs
-    fp64 torch, the sums of each image's tiles vs the image's channel sums of that output."""
+    """conv_wr's fp32-output epilogue (RCAN's RCAB conv2, rcan.py:50-69) and the channel sums it emits for the channel
+    attention's global pool (climsr_conv2d_fwd_ch_parts rows: per tile, tiles of an image contiguous; with one image
+    one row per workgroup -- 9 tiles leave the last workgroup one wave with a tile, 180 x 360 gives a workgroup several
+    tiles a wave): the output vs fp64 torch, the sums of each image's rows vs the image's channel sums of that output."""
     from climsr_amd import ops
 
     p, wt, b = make_plan(64, 64, 3, seed=21)
@@ -684,7 +686,9 @@ def test_conv_wr_fp32_out_channel_sums(n, h, w, f32):
     x = bf(torch.rand((n, 64, h, w), generator=g) * 2 - 1)
     y = torch.full((n, h, w, 64), 7.0, dtype=torch.float32 if f32 else torch.bfloat16, device=DEV)
     rows, tpi = p.ch_parts(64, h, w, n, 64)
-    assert rows == n * tpi and tpi == ((w + 15) // 16) * ((h + 3) // 4)
+    tiles = ((w + 15) // 16) * ((h + 3) // 4)
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    assert rows == n * tpi and tpi == (min((tiles + 3) // 4, ncu) if n == 1 else tiles)
     part = torch.full((rows, 64), 7.0, dtype=torch.float32, device=DEV)
     names = []
     ops.PROFILER = lambda name, flops, fn, tag="", nbytes=0: (names.append(name), fn())

@@ -114,11 +114,12 @@ def test_channel_attention_and_rcab_residual():
     assert torch.equal(xb2.cpu(), xr2.cpu().to(torch.bfloat16))
 
 
-@pytest.mark.parametrize("n,tpi,c,cr", [(2, 1035, 64, 4), (1, 7, 64, 4), (3, 300, 96, 6), (1, 50, 1024, 16)])
+@pytest.mark.parametrize("n,tpi,c,cr", [(2, 1035, 64, 4), (1, 7, 64, 4), (3, 300, 96, 6), (1, 50, 1024, 16), (1, 256, 64, 4),
+                                        (2, 1024, 64, 4), (1, 513, 64, 4)])
 def test_channel_attention_parts_vs_float64(n, tpi, c, cr):
-    """climsr_channel_attention_parts (tile sums folded into fp64 slices -> mean -> 1x1-ReLU-1x1-sigmoid, CALayer
-    rcan.py:50-69) from per-tile channel sums as the RCAB conv2 epilogue writes them, vs float64; ragged tile counts,
-    wide c."""
+    """climsr_channel_attention_parts (rows folded into fp64 slices, or with at most 1024 rows of 64 channels read by the
+    MLP kernel itself -> mean -> 1x1-ReLU-1x1-sigmoid, CALayer rcan.py:50-69) from channel-sum rows as the RCAB conv2
+    epilogue writes them, vs float64; ragged row counts, wide c."""
     from climsr_amd import _lib
     from climsr_amd._lib import check, ptr
 
