@@ -213,12 +213,13 @@ __global__ __launch_bounds__(256) void bn_finish_stats_kernel(const double* __re
 }
 
 // y = act(z * scale + shift) with scale = gamma*rstd, shift = beta - mean*scale (mode 0: batch statistics
-// mean/rstd; mode 1: running statistics, rstd = rsqrt(var + eps)).
-template <int MODE>
+// mean/rstd; mode 1: running statistics, rstd = rsqrt(var + eps)).  ACT (0 none, 1 leaky relu, 2 relu) a template
+// parameter: as an argument it compiled to a uniform three-way branch per element (165 branches in the loop).
+template <int MODE, int ACT>
 __global__ __launch_bounds__(256) void bn_apply_kernel(int npix, int c, int per_blk, const uint16_t* __restrict__ z,
                                                        const float* __restrict__ mean, const float* __restrict__ var_or_rstd,
                                                        float eps, const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                       int act, float slope, uint16_t* __restrict__ y) {
+                                                       float slope, uint16_t* __restrict__ y) {
   const int G = c >> 3;
   const int R = 256 / G;
   const int cg = threadIdx.x % G;
@@ -239,7 +240,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(int npix, int c, int per_
     const size_t off = (size_t)p * c + cg * 8;
     unpack8(*(const uint4*)(z + off), f);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) f[i] = act_apply(fmaf(f[i], sc[i], sh[i]), act, slope);
+    for (int i = 0; i < 8; ++i) f[i] = act_apply(fmaf(f[i], sc[i], sh[i]), ACT, slope);
     *(uint4*)(y + off) = pack8(f);
   };
   int p = p0 + r;
@@ -327,6 +328,17 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(int npix, int c, int 
   for (; p < p1; p += R) one(p);
 }
 
+template <int MODE>
+static void launch_bn_apply(hipStream_t s, int nb, int npix, int c, int per, const uint16_t* z, const float* mean, const float* v,
+                            float eps, const float* gamma, const float* beta, int act, float slope, uint16_t* y) {
+  if (act == 1)
+    hipLaunchKernelGGL((bn_apply_kernel<MODE, 1>), dim3(nb), dim3(256), 0, s, npix, c, per, z, mean, v, eps, gamma, beta, slope, y);
+  else if (act == 2)
+    hipLaunchKernelGGL((bn_apply_kernel<MODE, 2>), dim3(nb), dim3(256), 0, s, npix, c, per, z, mean, v, eps, gamma, beta, slope, y);
+  else
+    hipLaunchKernelGGL((bn_apply_kernel<MODE, 0>), dim3(nb), dim3(256), 0, s, npix, c, per, z, mean, v, eps, gamma, beta, slope, y);
+}
+
 static inline int bn_apply_grid(long npix, int c, int* per_blk) {
   const int R = 256 / (c / 8);
   *per_blk = R * bn_px_per_thread(npix, c);
@@ -357,8 +369,7 @@ extern "C" int climsr_bn_forward(const uint16_t* z, int64_t npix, int c, const f
                      momentum, mean, rstd, run_mean, run_var, num_batches_tracked);
   int per;
   const int nb = bn_apply_grid(npix, c, &per);
-  hipLaunchKernelGGL(bn_apply_kernel<0>, dim3(nb), dim3(256), 0, s, (int)npix, c, per, z, mean, rstd, 0.f, gamma, beta, act, slope,
-                     y);
+  launch_bn_apply<0>(s, nb, (int)npix, c, per, z, mean, rstd, 0.f, gamma, beta, act, slope, y);
   return check_launch("bn_forward");
 }
 
@@ -374,8 +385,7 @@ extern "C" int climsr_bn_forward_parts(const double* parts, int64_t nparts, cons
                      mean, rstd, run_mean, run_var, num_batches_tracked);
   int per;
   const int nb = bn_apply_grid(npix, c, &per);
-  hipLaunchKernelGGL(bn_apply_kernel<0>, dim3(nb), dim3(256), 0, s, (int)npix, c, per, z, mean, rstd, 0.f, gamma, beta, act, slope,
-                     y);
+  launch_bn_apply<0>(s, nb, (int)npix, c, per, z, mean, rstd, 0.f, gamma, beta, act, slope, y);
   return check_launch("bn_forward_parts");
 }
 
@@ -387,8 +397,7 @@ extern "C" int climsr_bn_inference(const uint16_t* z, int64_t npix, int c, const
   }
   int per;
   const int nb = bn_apply_grid(npix, c, &per);
-  hipLaunchKernelGGL(bn_apply_kernel<1>, dim3(nb), dim3(256), 0, (hipStream_t)stream, (int)npix, c, per, z, run_mean, run_var, eps,
-                     gamma, beta, act, slope, y);
+  launch_bn_apply<1>((hipStream_t)stream, nb, (int)npix, c, per, z, run_mean, run_var, eps, gamma, beta, act, slope, y);
   return check_launch("bn_inference");
 }
 
