@@ -86,9 +86,10 @@ typedef struct ClimsrEpilogue {
   const float* bn_rstd;
   const float* bn_gamma;
   const float* bn_beta;
-  /* optional (the 64 -> 64 3x3 register-resident conv, climsr_conv2d_fwd_ch_parts > 0; fp32 or bf16 output): per-tile
-     channel sums of the output values before any bf16 rounding, ch_part[tile][out_c] fp32, tiles of one image
-     contiguous -- the global average pool of RCAN's channel attention (rcan.py:50-69) without re-reading the output; finish with climsr_channel_attention_parts */
+  /* optional (the 64 -> 64 3x3 register-resident conv, climsr_conv2d_fwd_ch_parts > 0; fp32 or bf16 output): channel
+     sums of the output values before any bf16 rounding, ch_part[row][out_c] fp32: one row per tile, the tiles of one
+     image contiguous; with one image (n = 1) one row per workgroup of the launch instead (its tiles' sums, added in a
+     fixed order) -- the global average pool of RCAN's channel attention (rcan.py:50-69) without re-reading the output; finish with climsr_channel_attention_parts */
   float* ch_part;
   /* 1: a 2x2 / stride-2 max pool of the (biased, activated) output is what gets stored: out[y/2][x/2] of the
      (out_h/2) x (out_w/2) image (even out_h / out_w; bf16 out, no residual / aux / BatchNorm / channel sums) -- VGG19's
@@ -97,8 +98,8 @@ typedef struct ClimsrEpilogue {
   int32_t pool2;
 } ClimsrEpilogue;
 
-/* rows (tiles) of ClimsrEpilogue.ch_part for this conv and epilogue, 0 when its kernel cannot emit them; the tiles of
- * one image are *tiles_per_image consecutive rows */
+/* rows of ClimsrEpilogue.ch_part for this conv and epilogue (tiles; workgroups when n = 1), 0 when its kernel cannot
+ * emit them; the rows of one image are *tiles_per_image consecutive rows */
 int64_t climsr_conv2d_fwd_ch_parts(const ClimsrConvDesc* d, const ClimsrEpilogue* ep, int32_t* tiles_per_image);
 /* 1 when climsr_conv2d_fwd has a kernel for this conv with ep->pool2 = 1 (the 64 -> 64 register-resident conv, or the
  * LDS-DMA 3x3 conv with bias + activation), else 0 (store the full output and pool it with climsr_maxpool2_bf16). */
@@ -482,8 +483,9 @@ int climsr_denormalize_mask(const float* sr, const float* mask, const double* mi
 size_t climsr_channel_attention_workspace(int n, int c);
 int climsr_channel_attention(const float* u, int n, int64_t hw, int c, int u_cstride, const float* w1, const float* b1,
                              const float* w2, const float* b2, int cr, double* workspace, float* s, void* stream);
-/* The same from per-tile channel sums already pooled by the conv that produced u (ClimsrEpilogue.ch_part):
- * part[n][tiles_per_image][c] fp32, summed over the tiles in a fixed order in fp64; hw = pixels per image;
+/* The same from channel-sum rows already pooled by the conv that produced u (ClimsrEpilogue.ch_part):
+ * part[n][tiles_per_image][c] fp32, summed over the rows in a fixed order in fp64 (at most 1024 rows of c = 64: by the
+ * MLP kernel itself, else folded into fp64 slices first); hw = pixels per image;
  * workspace = climsr_channel_attention_workspace(n, c) bytes. */
 int climsr_channel_attention_parts(const float* part, int n, int tiles_per_image, int64_t hw, int c, const float* w1,
                                    const float* b1, const float* w2, const float* b2, int cr, double* workspace, float* s,
