@@ -540,3 +540,34 @@ def test_linear_wgrad2_two_batches_vs_float64(acc):
     torch.cuda.synchronize()
     want = sum(dy_t.double() @ x_t.double().t() for dy_t, x_t in cols)
     close(dw - 0.5 if acc else dw, want, rel=1e-5, what="linear wgrad2")
+
+
+@pytest.mark.parametrize("act", [0, 1, 2])
+@pytest.mark.parametrize("train", [True, False])
+def test_batchnorm_apply_every_activation(act, train):
+    """The BatchNorm apply for each activation it is compiled for (bn_apply_kernel<MODE, ACT>: none, LeakyReLU(0.2),
+    ReLU) in both modes -- batch statistics (climsr_bn_forward) and running statistics (climsr_bn_inference, eval-mode
+    BatchNorm2d) -- vs float64, on a ragged pixel count."""
+    from climsr_amd import ops
+
+    npix, c = 4099, 64
+    g = torch.Generator(device=DEV).manual_seed(11 + act + 3 * train)
+    z = bf(torch.randn((npix, c), generator=g, device=DEV) * 1.3 - 0.2)
+    gamma = torch.rand(c, generator=g, device=DEV) + 0.5
+    beta = torch.rand(c, generator=g, device=DEV) - 0.5
+    y = torch.empty((npix, c), dtype=torch.bfloat16, device=DEV)
+    zd = z.double()
+    if train:
+        mean, rstd = torch.empty(c, device=DEV), torch.empty(c, device=DEV)
+        ops.bn_forward(z.to(torch.bfloat16), npix, c, gamma, beta, mean, rstd, y, ops.bn_workspace(npix, c, {}, z.device), act=act)
+        m64, r64 = zd.mean(0), 1 / torch.sqrt(zd.var(0, unbiased=False) + 1e-5)
+    else:
+        rm = torch.randn(c, generator=g, device=DEV) * 0.1
+        rv = torch.rand(c, generator=g, device=DEV) + 0.5
+        ops.bn_inference(z.to(torch.bfloat16), npix, c, rm, rv, gamma, beta, y, act=act)
+        m64, r64 = rm.double(), 1 / torch.sqrt(rv.double() + 1e-5)
+    torch.cuda.synchronize()
+    x64 = (zd - m64) * r64 * gamma.double() + beta.double()
+    y64 = {0: x64, 1: F.leaky_relu(x64, 0.2), 2: F.relu(x64)}[act]
+    err = float((y.double() - y64).abs().max())
+    assert err <= 2 ** -7 * float(y64.abs().max()), f"act {act}: err {err:.3e}"
